@@ -1,0 +1,135 @@
+/*
+ * covt_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's COVT Id/Geometry stream decode path
+ * (springmeyer/cov-tiles, evaluation/java, package com.covt.decoder) and of the
+ * third-party arithmetic it calls:
+ *   - org.apache.orc:orc-core:1.8.1  RunLengthIntegerReader / RunLengthByteReader
+ *     (+ the matching writers, which DecodingUtils.getRleChunkSize uses to find
+ *     the stream length, DecodingUtils.java:308-314 -> EncodingUtils.java:123-147)
+ *   - me.lemire.integercompression:JavaFastPFOR:0.1.12
+ *     Composition(FastPFOR, VariableByte)  (DecodingUtils.java:332,365,427)
+ * Neither jar is vendored in the reference; their published algorithms are
+ * restated from SURVEY.md Appendix A.3-A.5 and pinned against the reference's
+ * committed fixtures (tests/golden, tests/test_oracle_*.py).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library.  The product (cov-tiles_amd/, libcovt.so) never links it.
+ *
+ * All integer arithmetic follows Java semantics: int32 wraps, `>>>` is a logical
+ * shift, shifts are masked to 5 (int) / 6 (long) bits.
+ */
+#ifndef COVT_ORACLE_H
+#define COVT_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes: identical numbering to include/covt.h */
+#define ORC_OK 0
+#define ORC_ERR_UNSUPPORTED (-1)
+#define ORC_ERR_TRUNCATED (-2)
+#define ORC_ERR_COUNT (-3)
+#define ORC_ERR_HEADER (-4)
+#define ORC_ERR_ARG (-6)
+
+/* ---- DecodingUtils restatement (DecodingUtils.java) ----------------------
+ * `avail` = readable bytes of `src` (Java: array length).  pos is the in/out
+ * cursor (Java IntWrapper).  Returns a status; on error *pos is unspecified. */
+int oracle_decode_varint(const uint8_t* src, size_t avail, int32_t* pos, int32_t n, int32_t* out);                /* :35-44 */
+int oracle_decode_zigzag_varint(const uint8_t* src, size_t avail, int32_t* pos, int32_t n, int32_t* out);         /* :46-53 */
+int oracle_decode_zigzag_delta_varint(const uint8_t* src, size_t avail, int32_t* pos, int32_t n, int32_t* out);   /* :55-66 */
+int oracle_decode_zigzag_delta_varint_coordinates(const uint8_t* src, size_t avail, int32_t* pos, int32_t n,
+                                                  int32_t* out);                                                  /* :95-112 */
+/* decodeRle :257-272.  *pos advances by the length of the ORC writer's re-encoding of
+ * the decoded values (Java behaviour, :268-270); *consumed (optional) receives the bytes
+ * the reader actually consumed. */
+int oracle_decode_rle(const uint8_t* src, size_t avail, int32_t n, int32_t* pos, int is_signed, int64_t* out,
+                      int32_t* consumed);
+/* decodeByteRle(buffer, n, pos, byteLength) :275-288 (advance by byteLength) */
+int oracle_decode_byte_rle(const uint8_t* src, size_t avail, int32_t n, int32_t* pos, int32_t byte_length,
+                           uint8_t* out, int32_t* consumed);
+/* decodeFastPfor128ZigZagDelta :316-347 */
+int oracle_decode_fastpfor_zigzag_delta(const uint8_t* src, size_t avail, int32_t n, int32_t byte_length,
+                                        int32_t* pos, int32_t* out);
+/* decodeFastPfor128DeltaCoordinates :349-392 */
+int oracle_decode_fastpfor_delta_coordinates(const uint8_t* src, size_t avail, int32_t n, int32_t byte_length,
+                                             int32_t* pos, int32_t* out);
+/* decodeDeltaVarintMortonCodes :394-409 (out has 2*n ints) */
+int oracle_decode_delta_varint_morton_codes(const uint8_t* src, size_t avail, int32_t* pos, int32_t n_vertices,
+                                            int32_t num_bits, int32_t* out);
+/* decodeFastPfor128DeltaMortonCodes :411-444 (out has 2*n ints) */
+int oracle_decode_fastpfor_delta_morton_codes(const uint8_t* src, size_t avail, int32_t n_vertices,
+                                              int32_t byte_length, int32_t* pos, int32_t num_bits, int32_t* out);
+/* GeometryUtils.decodeMorton, GeometryUtils.java:34-47 */
+void oracle_decode_morton(int32_t code, int32_t num_bits, int32_t* x, int32_t* y);
+
+/* Raw Composition(FastPFOR, VariableByte).uncompress of byteLength bytes at pos (BE words,
+ * DecodingUtils.java:317-333).  Writes n raw values (zero-filled past the decoded count);
+ * *decoded receives how many values the codec produced. */
+int oracle_fastpfor_uncompress(const uint8_t* src, size_t avail, int32_t pos, int32_t byte_length, int32_t n,
+                               uint32_t* raw, int32_t* decoded);
+
+/* Full 64-bit LEB128 (format truth for Id VARINT streams). */
+int oracle_decode_varint_u64(const uint8_t* src, size_t avail, int32_t* pos, int32_t n, uint64_t* out);
+
+/* ---- encoders (EncodingUtils.java:39-230 + orc/JavaFastPFOR writers) -------
+ * Used to build synthetic streams for round-trip tests.  Return bytes written
+ * (or a negative status if cap is too small). */
+int64_t oracle_encode_varints_u64(const uint64_t* v, int64_t n, uint8_t* dst, int64_t cap);
+int64_t oracle_encode_rle(const int64_t* v, int64_t n, int is_signed, uint8_t* dst, int64_t cap);
+int64_t oracle_encode_byte_rle(const uint8_t* v, int64_t n, uint8_t* dst, int64_t cap);
+/* FastPFOR(256-blocks, 65536-pages) + VariableByte tail, emitted as BE bytes like
+ * EncodingUtils.encodeFastPfor128 (:149-188) without the delta/zigzag pre-pass. */
+int64_t oracle_encode_fastpfor(const uint32_t* v, int64_t n, uint8_t* dst, int64_t cap);
+
+/* ---- container walkers (Gen C: SURVEY Appendix A.1; Gen D: CovtParser.java:574-652) ---- */
+#define ORACLE_FMT_GENC 0
+#define ORACLE_FMT_GEND 1
+
+typedef struct oracle_stream {
+    int32_t layer;        /* layer index within the tile */
+    int32_t column_kind;  /* 0 = id column, 1 = geometry column */
+    int32_t stream_type;  /* StreamType ordinal (DATA=1 for id) */
+    int32_t encoding;     /* StreamEncoding ordinal */
+    int32_t column_type;  /* ColumnType ordinal */
+    int32_t num_values;   /* wire numValues */
+    int32_t byte_length;  /* wire byteLength */
+    int32_t num_bits;     /* 32 - nlz(extent), CovtParser.java:77 */
+    int64_t offset;       /* payload byte offset within the tile */
+    int32_t extent;
+    int32_t num_features;
+} oracle_stream;
+
+/* Walk one tile; returns status, *n_out = number of Id/Geometry streams found
+ * (property columns are skipped by their byte lengths).  max_out may be 0 to count. */
+int oracle_walk_tile(const uint8_t* tile, size_t len, int format, oracle_stream* out, int32_t max_out,
+                     int32_t* n_out);
+
+/* Id column decode modes */
+#define ORACLE_ID_FORMAT 0 /* format truth: VARINT -> 64-bit LEB128, enc 4 -> unsigned RLE */
+#define ORACLE_ID_JAVA 1   /* CovtParser.decodedIds verbatim (4-byte varint cap, enc 4 zigzag-delta) */
+
+/* Output element type/count of a stream's decode (1,4,8 bytes) */
+int oracle_stream_output(const oracle_stream* s, int id_mode, int32_t* elem_bytes, int64_t* n_elems);
+/* Decode one walked stream with CovtParser's dispatch (decodeGeometryColumn :392-511,
+ * decodedIds :552-572).  RLE/varint reads are bounded by the stream's byteLength.
+ * out must hold n_elems * elem_bytes; *consumed receives bytes consumed. */
+int oracle_decode_stream(const uint8_t* tile, size_t len, const oracle_stream* s, int id_mode, void* out,
+                         int32_t* consumed);
+
+/* CPU baseline: walk + decode every Id/Geometry stream of n_tiles tiles (concatenated in
+ * `bytes` at `offsets`) on n_threads host threads; output goes to per-thread scratch.
+ * Returns status; totals (optional) receive stream bytes, output bytes, vertices. */
+int oracle_decode_tiles_mt(const uint8_t* bytes, const uint64_t* offsets, const uint64_t* sizes, int32_t n_tiles,
+                           int format, int id_mode, int32_t n_threads, int64_t* in_bytes, int64_t* out_bytes,
+                           int64_t* vertices);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
