@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Benchmark: GB/s of raw COVT Id+Geometry stream bytes decoded (+ Mvertices/s) on a z2-z14 tile batch.
+
+BASELINE.json config 5: a 10k-tile mixed-zoom batch sampled with numpy.random.default_rng(20250117),
+uniform over the zoom levels that have decodable fixtures, then uniform over that zoom's tiles, from the
+90 OMT + 27 Bing decodable fixtures (tests/golden/tiles, byte-identical copies of the reference's
+test/fixtures).  A "step" is one decode launch over the whole batch: every Id/Geometry stream of every
+tile, inputs (tile bytes + descriptor table) already resident in HBM, outputs written to HBM.
+
+  python bench.py [--gpus N --steps K --warmup W]     (N>1: torchrun, one rank per GPU)
+
+Scaling is weak by default: each rank decodes its own 10k-tile batch (seed 20250117 + rank), no
+collective on the data path (RCCL only for the timing barrier / max).  --scaling strong shards one
+10k-tile batch over the ranks with the greedy byte-balanced split of SURVEY §8(e).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+METRIC = "GB/s raw COVT bytes decoded + Mvertices/s, z2–z14 tile batch, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md (spec)
+SEED = 20250117
+
+
+def load_covt():
+    if "covtiles_amd" in sys.modules:
+        return sys.modules["covtiles_amd"]
+    path = os.path.join(ROOT, "cov-tiles_amd", "__init__.py")
+    spec = importlib.util.spec_from_file_location("covtiles_amd", path,
+                                                  submodule_search_locations=[os.path.dirname(path)])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["covtiles_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def tile_library():
+    """Decodable OMT + Bing fixtures -> {zoom: [(key, bytes)]}."""
+    with open(os.path.join(ROOT, "tests", "golden", "oracle_streams.json")) as f:
+        rec = json.load(f)["tiles"]
+    lib = {}
+    for s in ("omt", "bing"):
+        for p in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "tiles", s, "*.covt"))):
+            key = s + "/" + os.path.basename(p)[:-5]
+            if not rec[key]["decodable"]:
+                continue
+            z = int(os.path.basename(p).replace("-", "_").split("_")[0])
+            lib.setdefault(z, []).append((key, open(p, "rb").read()))
+    return lib
+
+
+def sample_batch(lib, n_tiles, seed):
+    rng = np.random.default_rng(seed)
+    zooms = sorted(lib)
+    zs = rng.choice(zooms, size=n_tiles)
+    picks = []
+    for z in zs:
+        cand = lib[int(z)]
+        picks.append(cand[int(rng.integers(0, len(cand)))])
+    return picks
+
+
+def lpt_shards(weights, n):
+    order = np.argsort(-np.asarray(weights), kind="stable")
+    load = np.zeros(n)
+    shard = [[] for _ in range(n)]
+    for i in order:
+        g = int(np.argmin(load))
+        shard[g].append(int(i))
+        load[g] += weights[i]
+    return [sorted(s) for s in shard]
+
+
+def cpu_baseline(picks, seconds, threads):
+    """The oracle (C restatement of the Java DecodingUtils semantics) on host cores: bounded sample."""
+    sys.path.insert(0, ROOT)
+    import oracle as O
+
+    O.build()
+    covt = load_covt()
+    sample = picks[: min(len(picks), 400)]
+    blob, offs, sizes = covt.pack_tiles([t for _, t in sample])
+    st, ib, ob, vx = O.decode_tiles_mt(blob, offs, sizes, O.FMT_GENC, O.ID_FORMAT, threads)
+    if st != 0:
+        raise RuntimeError("oracle baseline failed: %d" % st)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        O.decode_tiles_mt(blob, offs, sizes, O.FMT_GENC, O.ID_FORMAT, threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(ib * reps / el / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "%d tiles of the same batch (%.1f MB stream bytes) x %d reps in %.1f s; "
+                      "C restatement of DecodingUtils (oracle/covt_oracle.c), %d threads" %
+                      (len(sample), ib / 1e6, reps, el, threads),
+            "mvert_per_s": round(vx * reps / el / 1e6, 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--tiles", type=int, default=10000)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--id-mode", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    covt = load_covt()
+
+    lib = tile_library()
+    if args.scaling == "weak":
+        picks = sample_batch(lib, args.tiles, SEED + rank)
+    else:
+        allp = sample_batch(lib, args.tiles, SEED)
+        shards = lpt_shards([len(t) for _, t in allp], world)
+        picks = [allp[i] for i in shards[rank]]
+
+    plan = covt.Plan.from_tiles([t for _, t in picks], covt.FORMAT_GENC, args.id_mode)
+    if (plan.tile_status != 0).any():
+        raise RuntimeError("tile walk failed")
+    batch = covt.DeviceBatch(plan, dev)
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        batch.decode(stream)
+    torch.cuda.synchronize(dev)
+    _, res = batch.results()
+    if (res[:, 0] != 0).any():
+        raise RuntimeError("decode reported errors on %d streams" % int((res[:, 0] != 0).sum()))
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        batch.decode(stream)
+        e.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    stats = torch.tensor([wall, float(plan.in_bytes), float(plan.vertices), float(plan.out_bytes), kern_ms],
+                         dtype=torch.float64, device=dev)
+    if dist is not None:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        wall, kern_ms = float(mx[0]), float(mx[4])
+        tot_in, tot_vx = float(sm[1]), float(sm[2])
+    else:
+        tot_in, tot_vx = float(plan.in_bytes), float(plan.vertices)
+
+    if rank == 0:
+        ms_per_step = wall * 1e3 / args.steps
+        value = tot_in * args.steps / wall / 1e9
+        alg_bytes = plan.in_bytes + plan.out_bytes  # stream bytes read + decoded bytes written
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                with open(pmc) as f:
+                    pm = json.load(f)
+                if pm.get("tiles") == args.tiles and pm.get("scaling") == args.scaling:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            except Exception:  # noqa: BLE001
+                traffic = None
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "fixture-sampled: seeded sample of the reference's committed OMT+Bing COVT tiles",
+            "config": {"workload": "config5: %d-tile mixed-zoom z2-z14 batch per GPU (%s scaling), "
+                                   "all Id+Geometry streams" % (len(picks), args.scaling),
+                       "tiles_per_gpu": len(picks), "streams_per_gpu": plan.num_streams,
+                       "stream_bytes_per_gpu": plan.in_bytes, "output_bytes_per_gpu": plan.out_bytes,
+                       "vertices_per_gpu": plan.vertices, "id_mode": "format" if args.id_mode == 0 else "java",
+                       "parallelism": "dp%d (tile shards, no collective)" % world},
+            "mvert_per_s": round(tot_vx * args.steps / wall / 1e6, 2),
+            "kernel_ms": round(kern_ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "covt::decode_streams_kernel",
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(picks, args.cpu_seconds, threads)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,482 @@
+"""covtiles_amd -- MI355X-native COVT Id/Geometry stream decoder (host side).
+
+Python mirror of the reference's decoder API (springmeyer/cov-tiles, evaluation/java,
+package ``com.covt.decoder``) over the C-ABI of ``libcovt.so`` (``include/covt.h``):
+
+* ``DecodingUtils`` -- one static method per ``DecodingUtils.java`` method, same names, argument
+  order and ``IntWrapper`` cursor semantics; errors raise the Python analogue of the Java exception.
+* ``CovtParser.decode_covt`` -- the Id + Geometry part of ``CovtParser.decodeCovt`` for one tile.
+* ``Plan`` / ``DeviceBatch`` -- the batch path: host metadata walk -> descriptor table -> one
+  GPU launch over every stream of every tile, with device-resident inputs/outputs (torch tensors
+  are used as device memory and for the HIP stream; they are plumbing, not the decoder).
+
+The directory name contains a dash, so import it through ``load()`` below or
+``importlib`` (``tests/conftest.py`` and ``bench.py`` do).  There is no CPU fallback: if
+``libcovt.so`` is missing or no GPU is visible, the decode entry points raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "libcovt.so")
+
+OK = 0
+ERR_UNSUPPORTED_ENCODING = -1
+ERR_TRUNCATED = -2
+ERR_COUNT_MISMATCH = -3
+ERR_BAD_HEADER = -4
+ERR_DEVICE = -5
+ERR_INVALID_ARG = -6
+INPUT_PADDING = 4096
+FORMAT_GENC, FORMAT_GEND = 0, 1
+ID_FORMAT, ID_JAVA = 0, 1
+
+(OP_NONE, OP_BYTE_RLE_U8, OP_RLE_U64, OP_RLE_I32, OP_RLE_S64, OP_VARINT_I32, OP_VARINT_ZZ_I32,
+ OP_VARINT_ZZ_DELTA_I32, OP_VARINT_ZZ_DELTA_XY, OP_VARINT_DELTA_MORTON, OP_FPF_ZZ_DELTA_I32, OP_FPF_ZZ_DELTA_XY,
+ OP_FPF_DELTA_MORTON, OP_VARINT_U64, OP_VARINT_I32_AS_I64, OP_VARINT_ZZ_DELTA_I64) = range(16)
+
+# StreamType ordinals (converter/StreamType.java)
+GEOMETRY_TYPES, GEOMETRY_OFFSETS, PART_OFFSETS, RING_OFFSETS, VERTEX_OFFSETS, VERTEX_BUFFER = range(4, 10)
+
+
+# ---------------------------------------------------------------------------
+# Java exception analogues (status -> exception), CovtParser.java:426 etc.
+# ---------------------------------------------------------------------------
+class CovtError(Exception):
+    status = 0
+
+
+class IllegalArgumentException(CovtError, ValueError):
+    pass
+
+
+class ArrayIndexOutOfBoundsException(CovtError, IndexError):
+    pass
+
+
+class DeviceError(CovtError, RuntimeError):
+    pass
+
+
+def _raise(status: int, what: str):
+    if status == OK:
+        return
+    cls = {ERR_UNSUPPORTED_ENCODING: IllegalArgumentException, ERR_BAD_HEADER: IllegalArgumentException,
+           ERR_INVALID_ARG: IllegalArgumentException, ERR_TRUNCATED: ArrayIndexOutOfBoundsException,
+           ERR_COUNT_MISMATCH: ArrayIndexOutOfBoundsException}.get(status, DeviceError)
+    e = cls("%s failed with status %d" % (what, status))
+    e.status = status
+    raise e
+
+
+# ---------------------------------------------------------------------------
+# C-ABI binding
+# ---------------------------------------------------------------------------
+class StreamDesc(C.Structure):
+    _fields_ = [("in_off", C.c_uint64), ("out_off", C.c_uint64), ("avail", C.c_int32), ("num_values", C.c_int32),
+                ("op", C.c_uint8), ("num_bits", C.c_uint8), ("flags", C.c_uint16), ("byte_length", C.c_int32)]
+
+
+class StreamResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("consumed", C.c_int32)]
+
+
+class StreamInfo(C.Structure):
+    _fields_ = [("tile", C.c_int32), ("layer", C.c_int32), ("column_kind", C.c_int32), ("stream_type", C.c_int32),
+                ("encoding", C.c_int32), ("column_type", C.c_int32), ("num_values", C.c_int32),
+                ("byte_length", C.c_int32), ("num_bits", C.c_int32), ("op", C.c_int32), ("elem_bytes", C.c_int32),
+                ("desc_index", C.c_int32), ("in_off", C.c_int64), ("out_off", C.c_int64),
+                ("out_elems", C.c_int64)]
+
+
+STREAM_INFO_DTYPE = np.dtype([(n, np.int32 if t is C.c_int32 else np.int64) for n, t in StreamInfo._fields_])
+assert STREAM_INFO_DTYPE.itemsize == C.sizeof(StreamInfo)
+assert C.sizeof(StreamDesc) == 32
+
+EXPORTED_SYMBOLS = (
+    "covt_decode_varint", "covt_decode_zigzag_varint", "covt_decode_zigzag_delta_varint",
+    "covt_decode_zigzag_delta_varint_coordinates", "covt_decode_rle", "covt_decode_byte_rle",
+    "covt_decode_fastpfor_zigzag_delta", "covt_decode_fastpfor_delta_coordinates",
+    "covt_decode_delta_varint_morton_codes", "covt_decode_fastpfor_delta_morton_codes",
+    "covt_plan_create", "covt_plan_destroy", "covt_plan_num_streams", "covt_plan_output_bytes",
+    "covt_plan_totals", "covt_plan_streams", "covt_plan_descs", "covt_plan_tile_status",
+    "covt_decode_streams_device", "covt_plan_decode_host", "covt_plan_decode_host_multi", "covt_version",
+    "covt_device_count",
+)
+
+
+def build(force: bool = False) -> str:
+    """Compile libcovt.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    args = ["make", "-s", "-C", _HERE, "libcovt.so"]
+    if force:
+        subprocess.check_call(["make", "-s", "-C", _HERE, "clean"])
+    subprocess.check_call(args)
+    return _LIB
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libcovt.so.  torch is imported first so libcovt binds to the same HIP runtime."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401  -- shares its libamdhip64 with libcovt (same SONAME)
+    except ImportError:
+        pass
+    if not os.path.exists(_LIB):
+        raise ImportError("libcovt.so is not built (run __graft_entry__.build() or make -C cov-tiles_amd)")
+    L = C.CDLL(_LIB)
+    u8p, i32p, i64p, vp = C.POINTER(C.c_uint8), C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_void_p
+    sz = C.c_size_t
+    for name in ("covt_decode_varint", "covt_decode_zigzag_varint", "covt_decode_zigzag_delta_varint",
+                 "covt_decode_zigzag_delta_varint_coordinates"):
+        getattr(L, name).argtypes = [u8p, sz, i32p, C.c_int32, i32p]
+    L.covt_decode_rle.argtypes = [u8p, sz, C.c_int32, i32p, C.c_int32, i64p]
+    L.covt_decode_byte_rle.argtypes = [u8p, sz, C.c_int32, i32p, C.c_int32, u8p]
+    L.covt_decode_fastpfor_zigzag_delta.argtypes = [u8p, sz, C.c_int32, C.c_int32, i32p, i32p]
+    L.covt_decode_fastpfor_delta_coordinates.argtypes = [u8p, sz, C.c_int32, C.c_int32, i32p, i32p]
+    L.covt_decode_delta_varint_morton_codes.argtypes = [u8p, sz, i32p, C.c_int32, C.c_int32, i32p]
+    L.covt_decode_fastpfor_delta_morton_codes.argtypes = [u8p, sz, C.c_int32, C.c_int32, i32p, C.c_int32, i32p]
+    L.covt_plan_create.argtypes = [u8p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
+                                   C.c_int32, C.POINTER(vp)]
+    L.covt_plan_destroy.argtypes = [vp]
+    L.covt_plan_destroy.restype = None
+    L.covt_plan_num_streams.argtypes = [vp]
+    L.covt_plan_num_streams.restype = C.c_int64
+    L.covt_plan_output_bytes.argtypes = [vp]
+    L.covt_plan_output_bytes.restype = C.c_int64
+    L.covt_plan_totals.argtypes = [vp, i64p, i64p, i64p]
+    L.covt_plan_streams.argtypes = [vp, vp]
+    L.covt_plan_descs.argtypes = [vp, vp]
+    L.covt_plan_tile_status.argtypes = [vp, i32p]
+    L.covt_decode_streams_device.argtypes = [vp, vp, C.c_int64, vp, vp, vp]
+    L.covt_plan_decode_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
+    L.covt_plan_decode_host_multi.argtypes = [vp, u8p, C.c_uint64, C.c_int32, vp, vp]
+    L.covt_version.restype = C.c_char_p
+    L.covt_device_count.argtypes = [i32p]
+    _lib = L
+    return L
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    lib().covt_device_count(C.byref(n))
+    return n.value
+
+
+def _u8(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf, dtype=np.uint8)
+    return np.frombuffer(bytes(buf), dtype=np.uint8)
+
+
+def _ptr(a: np.ndarray, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+# ---------------------------------------------------------------------------
+# DecodingUtils mirror (DecodingUtils.java)
+# ---------------------------------------------------------------------------
+class IntWrapper:
+    """me.lemire.integercompression.IntWrapper: the mutable cursor of the Java API."""
+
+    def __init__(self, v: int = 0):
+        self.value = int(v)
+
+    def get(self) -> int:
+        return self.value
+
+    def set(self, v: int) -> None:
+        self.value = int(v)
+
+    def increment(self) -> None:
+        self.value += 1
+
+    def add(self, v: int) -> None:
+        self.value += int(v)
+
+    def __repr__(self):
+        return "IntWrapper(%d)" % self.value
+
+
+def _cursor(pos):
+    return pos if isinstance(pos, IntWrapper) else IntWrapper(pos)
+
+
+class DecodingUtils:
+    """Static methods mirroring com.covt.decoder.DecodingUtils (names, argument order, semantics).
+    Every call decodes on the GPU through libcovt."""
+
+    @staticmethod
+    def _varint_like(fn, src, pos, n, out_n, what):
+        pos = _cursor(pos)
+        a = _u8(src)
+        out = np.zeros(max(out_n, 1), dtype=np.int32)
+        p = C.c_int32(pos.get())
+        _raise(getattr(lib(), fn)(_ptr(a, C.c_uint8), a.size, C.byref(p), int(n), _ptr(out, C.c_int32)), what)
+        pos.set(p.value)
+        return out[:out_n]
+
+    @staticmethod
+    def decodeVarint(src, pos: IntWrapper, numValues: int) -> np.ndarray:  # DecodingUtils.java:35
+        return DecodingUtils._varint_like("covt_decode_varint", src, pos, numValues, numValues, "decodeVarint")
+
+    @staticmethod
+    def decodeZigZagVarint(src, pos: IntWrapper, numValues: int) -> np.ndarray:  # :46
+        return DecodingUtils._varint_like("covt_decode_zigzag_varint", src, pos, numValues, numValues,
+                                          "decodeZigZagVarint")
+
+    @staticmethod
+    def decodeZigZagDeltaVarint(src, pos: IntWrapper, numValues: int) -> np.ndarray:  # :55
+        return DecodingUtils._varint_like("covt_decode_zigzag_delta_varint", src, pos, numValues, numValues,
+                                          "decodeZigZagDeltaVarint")
+
+    @staticmethod
+    def decodeZigZagDeltaVarintCoordinates(src, pos: IntWrapper, numValues: int) -> np.ndarray:  # :95
+        return DecodingUtils._varint_like("covt_decode_zigzag_delta_varint_coordinates", src, pos, numValues,
+                                          numValues, "decodeZigZagDeltaVarintCoordinates")
+
+    @staticmethod
+    def decodeDeltaVarintMortonCodes(src, pos: IntWrapper, numVertices: int, numBits: int) -> np.ndarray:  # :394
+        pos = _cursor(pos)
+        a = _u8(src)
+        out = np.zeros(max(2 * numVertices, 1), dtype=np.int32)
+        p = C.c_int32(pos.get())
+        _raise(lib().covt_decode_delta_varint_morton_codes(_ptr(a, C.c_uint8), a.size, C.byref(p), numVertices,
+                                                           numBits, _ptr(out, C.c_int32)),
+               "decodeDeltaVarintMortonCodes")
+        pos.set(p.value)
+        return out[:2 * numVertices]
+
+    @staticmethod
+    def decodeRle(buffer, numValues: int, pos: IntWrapper, signed: bool) -> np.ndarray:  # :257
+        pos = _cursor(pos)
+        a = _u8(buffer)
+        out = np.zeros(max(numValues, 1), dtype=np.int64)
+        p = C.c_int32(pos.get())
+        _raise(lib().covt_decode_rle(_ptr(a, C.c_uint8), a.size, numValues, C.byref(p), int(bool(signed)),
+                                     _ptr(out, C.c_int64)), "decodeRle")
+        pos.set(p.value)
+        return out[:numValues]
+
+    @staticmethod
+    def decodeByteRle(buffer, numValues: int, pos: IntWrapper, byteLength: int) -> np.ndarray:  # :275
+        pos = _cursor(pos)
+        a = _u8(buffer)
+        out = np.zeros(max(numValues, 1), dtype=np.uint8)
+        p = C.c_int32(pos.get())
+        _raise(lib().covt_decode_byte_rle(_ptr(a, C.c_uint8), a.size, numValues, C.byref(p), byteLength,
+                                          _ptr(out, C.c_uint8)), "decodeByteRle")
+        pos.set(p.value)
+        return out[:numValues]
+
+    @staticmethod
+    def _fpf(fn, buf, n, byte_length, pos, out_n, extra, what):
+        pos = _cursor(pos)
+        a = _u8(buf)
+        out = np.zeros(max(out_n, 1), dtype=np.int32)
+        p = C.c_int32(pos.get())
+        args = [_ptr(a, C.c_uint8), a.size, n, byte_length, C.byref(p)] + extra + [_ptr(out, C.c_int32)]
+        _raise(getattr(lib(), fn)(*args), what)
+        pos.set(p.value)
+        return out[:out_n]
+
+    @staticmethod
+    def decodeFastPfor128ZigZagDelta(encodedValues, numValues: int, byteLength: int, pos: IntWrapper):  # :316
+        return DecodingUtils._fpf("covt_decode_fastpfor_zigzag_delta", encodedValues, numValues, byteLength, pos,
+                                  numValues, [], "decodeFastPfor128ZigZagDelta")
+
+    @staticmethod
+    def decodeFastPfor128DeltaCoordinates(encodedValues, numValues: int, byteLength: int, pos: IntWrapper):  # :349
+        return DecodingUtils._fpf("covt_decode_fastpfor_delta_coordinates", encodedValues, numValues, byteLength,
+                                  pos, numValues, [], "decodeFastPfor128DeltaCoordinates")
+
+    @staticmethod
+    def decodeFastPfor128DeltaMortonCodes(encodedValues, numVertices: int, byteLength: int, pos: IntWrapper,
+                                          numBits: int):  # :411
+        return DecodingUtils._fpf("covt_decode_fastpfor_delta_morton_codes", encodedValues, numVertices,
+                                  byteLength, pos, 2 * numVertices, [numBits], "decodeFastPfor128DeltaMortonCodes")
+
+
+# ---------------------------------------------------------------------------
+# Batch path
+# ---------------------------------------------------------------------------
+def pack_tiles(tiles: List[bytes], align: int = 16):
+    """Concatenate tiles (16-byte aligned starts) -> (uint8 blob incl. INPUT_PADDING, offsets, sizes)."""
+    sizes = np.array([len(t) for t in tiles], dtype=np.uint64)
+    offs = np.zeros(len(tiles), dtype=np.uint64)
+    pos = 0
+    for i, t in enumerate(tiles):
+        offs[i] = pos
+        pos += (len(t) + align - 1) // align * align
+    blob = np.zeros(pos + INPUT_PADDING, dtype=np.uint8)
+    for i, t in enumerate(tiles):
+        blob[int(offs[i]):int(offs[i]) + len(t)] = np.frombuffer(t, dtype=np.uint8)
+    return blob, offs, sizes
+
+
+class Plan:
+    """Host-side container walk of a tile batch -> per-stream descriptors (covt_plan_create)."""
+
+    def __init__(self, blob: np.ndarray, offsets, sizes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT):
+        L = lib()
+        self.blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+        self.n_tiles = int(self.offsets.size)
+        h = C.c_void_p()
+        _raise(L.covt_plan_create(_ptr(self.blob, C.c_uint8), _ptr(self.offsets, C.c_uint64),
+                                  _ptr(self.sizes, C.c_uint64), self.n_tiles, fmt, id_mode, C.byref(h)),
+               "covt_plan_create")
+        self._h = h
+        self.num_streams = int(L.covt_plan_num_streams(h))
+        self.output_bytes = int(L.covt_plan_output_bytes(h))
+        ib, ob, vx = C.c_int64(), C.c_int64(), C.c_int64()
+        L.covt_plan_totals(h, C.byref(ib), C.byref(ob), C.byref(vx))
+        self.in_bytes, self.out_bytes, self.vertices = ib.value, ob.value, vx.value
+        self.streams = np.zeros(self.num_streams, dtype=STREAM_INFO_DTYPE)
+        if self.num_streams:
+            L.covt_plan_streams(h, self.streams.ctypes.data)
+        self.descs = np.zeros(self.num_streams * 32, dtype=np.uint8)
+        if self.num_streams:
+            L.covt_plan_descs(h, self.descs.ctypes.data)
+        self.tile_status = np.zeros(max(self.n_tiles, 1), dtype=np.int32)[:self.n_tiles]
+        if self.n_tiles:
+            L.covt_plan_tile_status(h, _ptr(self.tile_status, C.c_int32))
+
+    @classmethod
+    def from_tiles(cls, tiles: List[bytes], fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT):
+        blob, offs, sizes = pack_tiles(tiles)
+        return cls(blob, offs, sizes, fmt, id_mode)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().covt_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def decode_host(self, n_gpus: int = 1):
+        """H2D + decode + D2H of the whole plan (covt_plan_decode_host[_multi]).
+        Returns (uint8 output buffer, results[num_streams, 2] = (status, consumed)) in plan order."""
+        out = np.zeros(max(self.output_bytes, 1), dtype=np.uint8)
+        res = np.zeros((max(self.num_streams, 1), 2), dtype=np.int32)
+        if n_gpus > 1:
+            st = lib().covt_plan_decode_host_multi(self._h, _ptr(self.blob, C.c_uint8), self.blob.size, n_gpus,
+                                                   out.ctypes.data, res.ctypes.data)
+        else:
+            st = lib().covt_plan_decode_host(self._h, _ptr(self.blob, C.c_uint8), self.blob.size, out.ctypes.data,
+                                             res.ctypes.data)
+        _raise(st, "covt_plan_decode_host")
+        return out[:self.output_bytes], res[:self.num_streams]
+
+    def stream_array(self, out: np.ndarray, i: int) -> np.ndarray:
+        s = self.streams[i]
+        dt = {1: np.uint8, 4: np.int32, 8: np.int64}[int(s["elem_bytes"])]
+        off, n = int(s["out_off"]), int(s["out_elems"])
+        return out[off:off + n * int(s["elem_bytes"])].view(dt)
+
+
+class DeviceBatch:
+    """A plan whose tile bytes, descriptors and outputs live in HBM (torch uint8 tensors on `device`).
+    ``decode()`` enqueues the single decode launch on the current torch HIP stream."""
+
+    def __init__(self, plan: Plan, device="cuda"):
+        import torch
+
+        self.plan = plan
+        self.device = torch.device(device)
+        self.d_in = torch.from_numpy(plan.blob).to(self.device)
+        if self.d_in.data_ptr() % 16:
+            raise DeviceError("device input buffer is not 16-byte aligned")
+        n = max(plan.num_streams, 1)
+        self.d_desc = torch.from_numpy(plan.descs).to(self.device) if plan.num_streams else \
+            torch.zeros(32, dtype=torch.uint8, device=self.device)
+        self.d_out = torch.zeros(max(plan.output_bytes, 16), dtype=torch.uint8, device=self.device)
+        self.d_res = torch.zeros(n * 2, dtype=torch.int32, device=self.device)
+
+    def decode(self, stream=None):
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        st = lib().covt_decode_streams_device(self.d_in.data_ptr(), self.d_desc.data_ptr(), self.plan.num_streams,
+                                              self.d_out.data_ptr(), self.d_res.data_ptr(), s.cuda_stream)
+        _raise(st, "covt_decode_streams_device")
+
+    def results(self):
+        """(output bytes, results in plan order) copied to the host."""
+        out = self.d_out.cpu().numpy()[:self.plan.output_bytes]
+        res_launch = self.d_res.cpu().numpy().reshape(-1, 2)[:self.plan.num_streams]
+        res = res_launch[self.plan.streams["desc_index"]] if self.plan.num_streams else res_launch
+        return out, res
+
+
+# ---------------------------------------------------------------------------
+# CovtParser mirror (Id + Geometry columns)
+# ---------------------------------------------------------------------------
+@dataclass
+class GeometryColumn:
+    """record GeometryColumn, CovtParser.java:29-36 (absent streams are None)."""
+    geometryTypes: Optional[np.ndarray] = None
+    geometryOffsets: Optional[np.ndarray] = None
+    partOffsets: Optional[np.ndarray] = None
+    ringOffsets: Optional[np.ndarray] = None
+    vertexOffsets: Optional[np.ndarray] = None
+    vertexBuffer: Optional[np.ndarray] = None
+
+
+@dataclass
+class LayerColumns:
+    layer: int
+    ids: Optional[np.ndarray]
+    geometry: GeometryColumn
+    num_bits: int = 0
+    column_type: int = 0
+
+
+_GEOM_FIELD = {GEOMETRY_TYPES: "geometryTypes", GEOMETRY_OFFSETS: "geometryOffsets", PART_OFFSETS: "partOffsets",
+               RING_OFFSETS: "ringOffsets", VERTEX_OFFSETS: "vertexOffsets", VERTEX_BUFFER: "vertexBuffer"}
+
+
+def split_layers(plan: Plan, out: np.ndarray, res: np.ndarray, tile: int = 0) -> List[LayerColumns]:
+    layers = {}
+    for i in np.nonzero(plan.streams["tile"] == tile)[0]:
+        s = plan.streams[i]
+        _raise(int(res[i][0]), "stream %d (layer %d, type %d)" % (i, s["layer"], s["stream_type"]))
+        lc = layers.setdefault(int(s["layer"]), LayerColumns(int(s["layer"]), None, GeometryColumn()))
+        arr = plan.stream_array(out, int(i))
+        if int(s["column_kind"]) == 0:
+            lc.ids = arr
+        else:
+            setattr(lc.geometry, _GEOM_FIELD[int(s["stream_type"])], arr)
+            lc.num_bits = int(s["num_bits"])
+            lc.column_type = int(s["column_type"])
+    return [layers[k] for k in sorted(layers)]
+
+
+class CovtParser:
+    @staticmethod
+    def decode_covt(covt_buffer: bytes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT) -> List[LayerColumns]:
+        """Id + Geometry columns of CovtParser.decodeCovt (CovtParser.java:53-133), decoded on the GPU."""
+        plan = Plan.from_tiles([covt_buffer], fmt, id_mode)
+        _raise(int(plan.tile_status[0]), "decodeLayerMetadata")
+        out, res = plan.decode_host()
+        return split_layers(plan, out, res, 0)
+
+
+def version() -> str:
+    return lib().covt_version().decode()

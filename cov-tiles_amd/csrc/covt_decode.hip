@@ -1,0 +1,811 @@
+// covt_decode.hip -- gfx950 (MI355X) kernels for the COVT Id/Geometry stream codecs.
+//
+// One wave64 decodes one stream (a covt_stream_desc); a 256-thread workgroup runs four
+// independent waves with no workgroup barrier, so a wave retires as soon as its stream is done.
+// All decode state is wave-uniform except the per-lane data; cross-lane work goes through
+// ballot/prefix-scan primitives and a per-wave LDS scratch area.
+//
+// Codecs (reference semantics, evaluation/java/src/main/java/com/covt/decoder/DecodingUtils.java):
+//   * varint family (:35-112, :394-409): 1 KiB windows of the stream are loaded with one
+//     16-byte load per lane (coalesced), a per-byte terminator bitmask is built in registers,
+//     a wave prefix-sum of popcounts turns it into a list of value end positions in LDS, then
+//     each lane assembles one value and zigzag / delta / Morton run as a wave scan with a
+//     carried running sum.  The Java 4-byte cap (:157-186) is exact: a run of 4 continuation
+//     bytes in a window sends that window through a lane-serial parse.
+//   * ORC RLE v1 integer/byte (orc-core RunLengthIntegerReader/RunLengthByteReader, called at
+//     :257-306): the group headers are walked wave-uniformly out of the LDS window; runs are
+//     expanded lane-parallel, literal groups reuse the varint machinery.
+//   * FastPFOR(256-blocks, 65536-pages) + VariableByte (JavaFastPFOR 0.1.12 via :316-444):
+//     per page the exception-array directory is read, the byte container is walked in batches
+//     of 64 blocks, each block's 8*b packed words are staged in LDS and every lane unpacks four
+//     consecutive values, exceptions are patched through LDS, and the VariableByte tail reuses
+//     the varint machinery on the word-reversed byte order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "covt.h"
+#include "covt_internal.h"
+
+namespace covt {
+
+constexpr int kWin = 1024;  // window bytes (64 lanes x 16 B)
+constexpr int kWavesPerBlock = 4;
+constexpr int kFpfBlock = 256;
+constexpr int kFpfPage = 65536;
+constexpr int kFpfBcCap = 3 * kFpfPage / kFpfBlock + kFpfPage;  // JavaFastPFOR byteContainer size
+constexpr int kBlkBatch = 64;
+
+struct __attribute__((aligned(16))) WaveSmem {
+    union {
+        struct {
+            uint32_t win[kWin / 4 + 4];  // window bytes (+16 B slack for 12-byte reads)
+            uint16_t list[kWin];         // terminator positions (window-relative)
+        } v;
+        struct {
+            uint32_t stage[324];  // packed words of one FastPFOR block (<= 1024 + 15 B)
+            uint32_t patch[256];  // exception patches of one block
+        } f;
+    } u;
+    uint32_t blk[4 * kBlkBatch];  // FastPFOR block records: {b|c<<8|idx<<16, bcoff, xcur, pk}
+    uint32_t xstart[33];
+    int32_t xsize[33];
+    uint32_t xcnt[33];
+    int32_t misc[4];
+};
+
+// --------------------------------------------------------------------------------------------
+// wave primitives
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t uniu(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint32_t lane_bcast(uint32_t x, int src) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, src);
+}
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+// inclusive prefix sum over the 64 lanes (wrapping uint32)
+__device__ __forceinline__ uint32_t incl_scan(uint32_t x) {
+    const int l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (l >= o) x += y;
+    }
+    return x;
+}
+
+// --------------------------------------------------------------------------------------------
+// byte helpers
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {  // any alignment (input is padded)
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+__device__ __forceinline__ uint32_t ld_be32(const uint8_t* p) { return __builtin_bswap32(ld_le32(p)); }
+
+// bits 7,15,23,31 of each dword -> 16-bit mask of "high bit set" bytes
+__device__ __forceinline__ uint32_t hibits4(uint32_t x) {
+    x &= 0x80808080u;
+    return ((x >> 7) & 1u) | ((x >> 14) & 2u) | ((x >> 21) & 4u) | ((x >> 28) & 8u);
+}
+__device__ __forceinline__ uint32_t hibits16(uint4 d) {
+    return hibits4(d.x) | (hibits4(d.y) << 4) | (hibits4(d.z) << 8) | (hibits4(d.w) << 12);
+}
+// mask of byte slots [s, e) within 16 (clamped)
+__device__ __forceinline__ uint32_t range16(int32_t s, int32_t e) {
+    s = s < 0 ? 0 : (s > 16 ? 16 : s);
+    e = e < 0 ? 0 : (e > 16 ? 16 : e);
+    if (e <= s) return 0u;
+    return ((1u << e) - 1u) & ~((1u << s) - 1u);
+}
+// 7-bit groups of up to four LEB128 bytes (little-endian in x)
+__device__ __forceinline__ uint32_t pext7(uint32_t x) {
+    return (x & 0x7fu) | ((x >> 1) & 0x3f80u) | ((x >> 2) & 0x1fc000u) | ((x >> 3) & 0xfe00000u);
+}
+__device__ __forceinline__ uint32_t bytemask(int n) {  // low n bytes, clamped to [0,4]
+    return n >= 4 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << (8 * n)) - 1u));
+}
+__device__ __forceinline__ int32_t zz32(uint32_t e) { return (int32_t)((e >> 1) ^ (0u - (e & 1u))); }
+__device__ __forceinline__ int64_t zz64(uint64_t e) { return (int64_t)((e >> 1) ^ (0ull - (e & 1ull))); }
+
+// GeometryUtils.decodeMorton (GeometryUtils.java:34-47) with Java int/long semantics.
+__device__ __forceinline__ int32_t morton_axis(int32_t code, int nb) {
+    uint32_t x = (uint32_t)code & 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0f0f0f0fu;
+    x = (x | (x >> 4)) & 0x00ff00ffu;
+    x = (x | (x >> 8)) & 0x0000ffffu;
+    const uint32_t low = nb >= 16 ? 0xffffu : (nb <= 0 ? 0u : ((1u << nb) - 1u));
+    x &= low;
+    if (nb > 16 && code < 0) {  // bits 2i >= 32 of the sign-extended long are the sign bit
+        const uint32_t top = nb >= 32 ? 0xffffffffu : ((1u << nb) - 1u);
+        x |= top & ~0xffffu;
+    }
+    return (int32_t)x;
+}
+__device__ __forceinline__ int32_t morton_half(int nb) {
+    const int32_t te = (int32_t)(2u << ((uint32_t)(nb - 2) & 31u));
+    return te / 2;
+}
+
+// --------------------------------------------------------------------------------------------
+// sinks: per-op output transforms for K consecutive values per lane (value index base+lane*K+k)
+// --------------------------------------------------------------------------------------------
+struct Carry {
+    uint32_t x, y;
+};
+
+template <int K>
+__device__ __forceinline__ void sink_values(int op, const uint32_t (&v)[K], int64_t base, int32_t count, int nb,
+                                            uint8_t* __restrict__ out, Carry& c) {
+    const int l = lane_id();
+    const int64_t i0 = base + (int64_t)l * K;
+    const int32_t nvalid = count - l * K;  // values of this lane that are valid (may be <=0 or >K)
+    auto valid = [&](int k) { return k < nvalid; };
+    switch (op) {
+    case COVT_OP_VARINT_I32: {
+        int32_t* o = (int32_t*)out;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (valid(k)) o[i0 + k] = (int32_t)v[k];
+        return;
+    }
+    case COVT_OP_VARINT_ZZ_I32: {
+        int32_t* o = (int32_t*)out;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (valid(k)) o[i0 + k] = zz32(v[k]);
+        return;
+    }
+    case COVT_OP_VARINT_I32_AS_I64: {
+        int64_t* o = (int64_t*)out;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (valid(k)) o[i0 + k] = (int64_t)(int32_t)v[k];
+        return;
+    }
+    case COVT_OP_VARINT_ZZ_DELTA_I32:
+    case COVT_OP_FPF_ZZ_DELTA_I32:
+    case COVT_OP_VARINT_ZZ_DELTA_I64: {
+        uint32_t s[K];
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            acc += valid(k) ? (uint32_t)zz32(v[k]) : 0u;
+            s[k] = acc;
+        }
+        const uint32_t inc = incl_scan(acc);
+        const uint32_t pre = c.x + inc - acc;
+        if (op == COVT_OP_VARINT_ZZ_DELTA_I64) {
+            int64_t* o = (int64_t*)out;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (valid(k)) o[i0 + k] = (int64_t)(int32_t)(pre + s[k]);
+        } else {
+            int32_t* o = (int32_t*)out;
+            if (K == 4 && nvalid >= 4) {
+                *(int4*)(o + i0) = make_int4((int32_t)(pre + s[0]), (int32_t)(pre + s[K > 1 ? 1 : 0]),
+                                             (int32_t)(pre + s[K > 2 ? 2 : 0]), (int32_t)(pre + s[K > 3 ? 3 : 0]));
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (valid(k)) o[i0 + k] = (int32_t)(pre + s[k]);
+            }
+        }
+        c.x += lane_bcast(inc, 63);
+        return;
+    }
+    case COVT_OP_VARINT_ZZ_DELTA_XY:
+    case COVT_OP_FPF_ZZ_DELTA_XY: {
+        uint32_t sx[K], sy[K];
+        uint32_t ax = 0, ay = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t z = valid(k) ? (uint32_t)zz32(v[k]) : 0u;
+            if (((i0 + k) & 1) == 0) ax += z; else ay += z;
+            sx[k] = ax;
+            sy[k] = ay;
+        }
+        const uint32_t incx = incl_scan(ax), incy = incl_scan(ay);
+        const uint32_t prex = c.x + incx - ax, prey = c.y + incy - ay;
+        int32_t* o = (int32_t*)out;
+        if (K == 4 && nvalid >= 4 && ((i0 & 1) == 0)) {
+            *(int4*)(o + i0) = make_int4((int32_t)(prex + sx[0]), (int32_t)(prey + sy[K > 1 ? 1 : 0]),
+                                         (int32_t)(prex + sx[K > 2 ? 2 : 0]), (int32_t)(prey + sy[K > 3 ? 3 : 0]));
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (valid(k)) o[i0 + k] = (int32_t)((((i0 + k) & 1) == 0) ? (prex + sx[k]) : (prey + sy[k]));
+        }
+        c.x += lane_bcast(incx, 63);
+        c.y += lane_bcast(incy, 63);
+        return;
+    }
+    case COVT_OP_VARINT_DELTA_MORTON:
+    case COVT_OP_FPF_DELTA_MORTON: {
+        uint32_t s[K];
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            acc += valid(k) ? v[k] : 0u;  // no zigzag (DecodingUtils.java:398-399, :435)
+            s[k] = acc;
+        }
+        const uint32_t inc = incl_scan(acc);
+        const uint32_t pre = c.x + inc - acc;
+        const int32_t half = morton_half(nb);
+        int32_t* o = (int32_t*)out;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t code = (int32_t)(pre + s[k]);
+            const int32_t x = (int32_t)((uint32_t)morton_axis(code, nb) - (uint32_t)half);
+            const int32_t y = (int32_t)((uint32_t)morton_axis(code >> 1, nb) - (uint32_t)half);
+            if (valid(k)) *(int2*)(o + 2 * (i0 + k)) = make_int2(x, y);
+        }
+        c.x += lane_bcast(inc, 63);
+        return;
+    }
+    default: return;
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// the 1 KiB window and the varint machinery
+// --------------------------------------------------------------------------------------------
+enum { MODE_RAW = 0, MODE_WORDREV = 1 };             // byte order of the window
+enum { VAL_J4 = 0, VAL_VB = 1, VAL_U64 = 2, VAL_U64_STRICT = 3 };  // value grammar
+
+// RAW: window byte j = stream byte woff + j, woff = ((sb + p) & ~15) - sb.
+// WORDREV: window byte j = logical byte woff + j of the VariableByte sequence, i.e. the LE bytes of
+// the big-endian words W[i] (DecodingUtils.java:319-327); woff is a multiple of 16.
+template <int MODE>
+__device__ __forceinline__ int32_t win_fill(WaveSmem& sm, const uint8_t* sb, int32_t p, uint4& d) {
+    const int l = lane_id();
+    int32_t woff;
+    if (MODE == MODE_RAW) {
+        const uintptr_t a = ((uintptr_t)(sb + p)) & ~(uintptr_t)15;
+        woff = (int32_t)((intptr_t)a - (intptr_t)sb);
+        d = ((const uint4*)a)[l];
+    } else {
+        woff = p & ~15;
+        const uint8_t* w = sb + woff + 16 * l;
+        d.x = ld_be32(w);
+        d.y = ld_be32(w + 4);
+        d.z = ld_be32(w + 8);
+        d.w = ld_be32(w + 12);
+    }
+    ((uint4*)sm.u.v.win)[l] = d;
+    wave_sync();
+    return uni(woff);
+}
+
+__device__ __forceinline__ uint32_t win_byte(const WaveSmem& sm, int32_t j) {
+    return (sm.u.v.win[j >> 2] >> (8 * (j & 3))) & 0xffu;
+}
+// bytes [j, j+12) of the window as three little-endian dwords
+__device__ __forceinline__ void win_bytes12(const WaveSmem& sm, int32_t j, uint32_t& x0, uint32_t& x1,
+                                            uint32_t& x2) {
+    const int32_t d = j >> 2;
+    const uint32_t sh = (uint32_t)(j & 3);
+    const uint32_t w0 = sm.u.v.win[d], w1 = sm.u.v.win[d + 1], w2 = sm.u.v.win[d + 2], w3 = sm.u.v.win[d + 3];
+    x0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+}
+
+// Decode up to `want` values starting at stream position `pos` (updated) with bytes valid in
+// [pos, end).  emit(lo, hi, base, count) is called per group of <=64 values, one per lane.
+// Returns the number of values decoded.  With `until_end` (VariableByte tail) the region is
+// decoded to its end, a trailing partial value is dropped and more than `want` values is an error.
+template <int MODE, int VAL, class Emit>
+__device__ int32_t varint_run(WaveSmem& sm, const uint8_t* sb, int32_t& pos, int32_t end, int32_t want,
+                              bool until_end, int32_t& err, Emit&& emit) {
+    const int l = lane_id();
+    int32_t got = 0;
+    while (until_end ? (pos < end) : (got < want)) {
+        uint4 d;
+        const int32_t woff = win_fill<MODE>(sm, sb, pos, d);
+        const int32_t q0 = woff + 16 * l;
+        const uint32_t V = range16(pos - q0, end - q0);
+        const uint32_t H = hibits16(d);
+        uint32_t T = (VAL == VAL_VB) ? (V & H) : (V & ~H);
+        int32_t K;
+        bool serial = false;
+        if (VAL == VAL_J4) {
+            // a run of four continuation bytes changes the capped grammar: parse serially
+            const uint32_t N = V & ~T;
+            uint32_t prevN = (uint32_t)__shfl_up((int)N, 1, 64);
+            if (l == 0) prevN = 0;
+            const uint32_t ext = (N << 3) | ((prevN >> 13) & 7u);
+            serial = __any((ext & (ext >> 1) & (ext >> 2) & (ext >> 3)) != 0);
+        }
+        if (!serial) {
+            const uint32_t cnt = __popc(T);
+            const uint32_t inc = incl_scan(cnt);
+            uint32_t idx = inc - cnt;
+            while (T) {
+                const int k = __ffs(T) - 1;
+                T &= T - 1;
+                sm.u.v.list[idx++] = (uint16_t)(16 * l + k);
+            }
+            K = (int32_t)lane_bcast(inc, 63);
+        } else {
+            if (l == 0) {  // DecodingUtils.java:157-186, one value at a time
+                const int32_t lim = (end < woff + kWin ? end : woff + kWin) - woff;
+                int32_t j = pos - woff, k = 0;
+                while (j < lim) {
+                    int32_t len = 0;
+                    bool done = false;
+                    for (int b = 0; b < 4; ++b) {
+                        if (j + b >= lim) break;
+                        ++len;
+                        if (b == 3 || (win_byte(sm, j + b) & 0x80u) == 0) { done = true; break; }
+                    }
+                    if (!done) break;
+                    sm.u.v.list[k++] = (uint16_t)(j + len - 1);
+                    j += len;
+                }
+                sm.misc[0] = k;
+            }
+            wave_sync();
+            K = uni(sm.misc[0]);
+        }
+        wave_sync();
+        if (K == 0) {
+            if (until_end) break;  // VariableByte: trailing partial value is dropped
+            err = (woff + kWin >= end) ? COVT_ERR_TRUNCATED : COVT_ERR_BAD_HEADER;
+            break;
+        }
+        int32_t take = K;
+        if (until_end) {
+            if (got + K > want) { err = COVT_ERR_COUNT_MISMATCH; take = want - got; }
+        } else if (take > want - got) {
+            take = want - got;
+        }
+        if (take <= 0) break;
+        bool lerr = false;
+        for (int32_t g = 0; g < take; g += 64) {
+            const int32_t vi = g + l;
+            uint32_t lo = 0, hi = 0;
+            if (vi < take) {
+                const int32_t ej = sm.u.v.list[vi];
+                const int32_t sj = (vi == 0) ? (pos - woff) : (int32_t)sm.u.v.list[vi - 1] + 1;
+                const int32_t len = ej - sj + 1;
+                uint32_t x0, x1, x2;
+                win_bytes12(sm, sj, x0, x1, x2);
+                if (VAL == VAL_J4) {
+                    lo = pext7(x0 & bytemask(len));
+                } else if (VAL == VAL_VB) {
+                    if (len <= 5) {
+                        lo = pext7(x0 & bytemask(len));
+                        if (len == 5) lo += (x1 & 0x7fu) << 28;
+                    } else {  // VariableByte.uncompress: v += (c & 127) << shift, shift masked to 5 bits
+                        uint32_t vv = 0;
+                        for (int b = 0; b < len; ++b) vv += (win_byte(sm, sj + b) & 0x7fu) << ((7 * b) & 31);
+                        lo = vv;
+                    }
+                } else {
+                    uint64_t r;
+                    if (len <= 10) {
+                        const uint32_t m0 = x0 & bytemask(len), m1 = x1 & bytemask(len - 4),
+                                       m2 = x2 & bytemask(len - 8);
+                        r = (uint64_t)pext7(m0) | ((uint64_t)pext7(m1) << 28) | ((uint64_t)(m2 & 0x7fu) << 56) |
+                            ((uint64_t)((m2 >> 8) & 0x7fu) << 63);
+                    } else {  // orc readVulong: shift masked to 6 bits
+                        r = 0;
+                        for (int b = 0; b < len; ++b) r |= (uint64_t)(win_byte(sm, sj + b) & 0x7fu) << ((7 * b) & 63);
+                        lerr = true;
+                    }
+                    lo = (uint32_t)r;
+                    hi = (uint32_t)(r >> 32);
+                }
+            }
+            emit(lo, hi, got + g, take - g < 64 ? take - g : 64);
+        }
+        if (VAL == VAL_U64_STRICT && __any(lerr) && !err) err = COVT_ERR_BAD_HEADER;
+        pos = woff + (int32_t)uni(sm.u.v.list[take - 1]) + 1;
+        got += take;
+        wave_sync();
+        if (err) break;
+    }
+    return got;
+}
+
+// --------------------------------------------------------------------------------------------
+// per-op drivers
+// --------------------------------------------------------------------------------------------
+struct Ctx {
+    WaveSmem* sm;
+    const uint8_t* sb;  // stream payload
+    uint8_t* out;       // stream output
+    int32_t avail, n, nb, op, byte_length;
+    int32_t err, consumed;
+};
+
+// byte of the stream through the window (refilled on demand); wave-uniform
+__device__ __forceinline__ uint32_t rd_byte(Ctx& c, int32_t& woff, int32_t q) {
+    if (q < woff || q >= woff + kWin) {
+        uint4 d;
+        woff = win_fill<MODE_RAW>(*c.sm, c.sb, q, d);
+    }
+    return uniu(win_byte(*c.sm, q - woff));
+}
+
+__device__ void run_varint_stream(Ctx& c) {
+    int32_t pos = 0;
+    Carry cr{0, 0};
+    auto sink1 = [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
+        uint32_t v[1] = {lo};
+        sink_values<1>(c.op, v, base, count, c.nb, c.out, cr);
+    };
+    if (c.op == COVT_OP_VARINT_U64) {
+        int64_t* o = (int64_t*)c.out;
+        varint_run<MODE_RAW, VAL_U64_STRICT>(*c.sm, c.sb, pos, c.avail, c.n, false, c.err,
+                                             [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
+                                                 if (lane_id() < count)
+                                                     o[base + lane_id()] = (int64_t)(((uint64_t)hi << 32) | lo);
+                                             });
+    } else {
+        if ((c.op == COVT_OP_VARINT_ZZ_DELTA_XY) && (c.n & 1)) {
+            // Java decodes the x,y pair and then overruns values[] (ArrayIndexOutOfBounds)
+            varint_run<MODE_RAW, VAL_J4>(*c.sm, c.sb, pos, c.avail, c.n - 1, false, c.err, sink1);
+            if (!c.err) c.err = COVT_ERR_COUNT_MISMATCH;
+        } else {
+            varint_run<MODE_RAW, VAL_J4>(*c.sm, c.sb, pos, c.avail, c.n, false, c.err, sink1);
+        }
+    }
+    c.consumed = pos;
+}
+
+// ORC RLE v1 integer reader (RunLengthIntegerReader.readValues / next)
+__device__ void run_rle_int(Ctx& c) {
+    const int l = lane_id();
+    const bool is_signed = c.op == COVT_OP_RLE_S64;
+    const bool to_i32 = c.op == COVT_OP_RLE_I32;
+    int32_t woff = INT32_MIN / 2;
+    int32_t pos = 0, done = 0;
+    auto store = [&](int64_t i, uint64_t raw) {
+        const int64_t v = is_signed ? zz64(raw) : (int64_t)raw;
+        if (to_i32) ((int32_t*)c.out)[i] = (int32_t)v;
+        else ((int64_t*)c.out)[i] = v;
+    };
+    while (done < c.n) {
+        if (pos >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
+        const uint32_t ctl = rd_byte(c, woff, pos);
+        if (ctl < 0x80u) {
+            const int32_t cnt = (int32_t)ctl + 3;
+            if (pos + 1 >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
+            const int32_t delta = (int32_t)(int8_t)rd_byte(c, woff, pos + 1);
+            // base varint (readVulong / readVslong)
+            int32_t q = pos + 2;
+            uint64_t base = 0;
+            uint32_t b;
+            int sh = 0;
+            do {
+                if (q >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
+                b = rd_byte(c, woff, q++);
+                base |= (uint64_t)(b & 0x7fu) << (sh & 63);
+                sh += 7;
+            } while (b >= 0x80u);
+            if (c.err) break;
+            pos = q;
+            const int64_t b64 = is_signed ? zz64(base) : (int64_t)base;
+            const int32_t take = cnt < c.n - done ? cnt : c.n - done;
+            for (int32_t i = l; i < take; i += 64) {  // literals[0] + used * delta
+                const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
+                if (to_i32) ((int32_t*)c.out)[done + i] = (int32_t)v;
+                else ((int64_t*)c.out)[done + i] = v;
+            }
+            done += take;
+        } else {
+            const int32_t cnt = 0x100 - (int32_t)ctl;
+            pos += 1;
+            const int32_t lim = c.n - done;
+            const int32_t d0 = done;
+            varint_run<MODE_RAW, VAL_U64>(*c.sm, c.sb, pos, c.avail, cnt, false, c.err,
+                                          [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
+                                              const int32_t k = base + l;
+                                              if (l < count && k < lim) store(d0 + k, ((uint64_t)hi << 32) | lo);
+                                          });
+            woff = INT32_MIN / 2;  // the window moved
+            if (c.err) break;
+            done += cnt < lim ? cnt : lim;
+        }
+    }
+    c.consumed = pos;
+}
+
+// ORC RLE v1 byte reader (RunLengthByteReader); GeometryType.values()[b] range-checked
+__device__ void run_rle_byte(Ctx& c) {
+    const int l = lane_id();
+    int32_t woff = INT32_MIN / 2;
+    int32_t pos = 0, done = 0;
+    bool bad = false;
+    while (done < c.n) {
+        if (pos >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
+        const uint32_t ctl = rd_byte(c, woff, pos);
+        if (ctl < 0x80u) {
+            const int32_t cnt = (int32_t)ctl + 3;
+            if (pos + 1 >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
+            const uint32_t val = rd_byte(c, woff, pos + 1);
+            pos += 2;
+            const int32_t take = cnt < c.n - done ? cnt : c.n - done;
+            for (int32_t i = l; i < take; i += 64) c.out[done + i] = (uint8_t)val;
+            bad |= val > 5u;
+            done += take;
+        } else {
+            const int32_t cnt = 0x100 - (int32_t)ctl;
+            pos += 1;
+            if (pos + cnt > c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
+            if (pos < woff || pos + cnt > woff + kWin) {
+                uint4 d;
+                woff = win_fill<MODE_RAW>(*c.sm, c.sb, pos, d);
+            }
+            const int32_t take = cnt < c.n - done ? cnt : c.n - done;
+            bool lbad = false;
+            for (int32_t i = l; i < take; i += 64) {
+                const uint32_t v = win_byte(*c.sm, pos - woff + i);
+                c.out[done + i] = (uint8_t)v;
+                lbad |= v > 5u;
+            }
+            bad |= __any(lbad);
+            pos += cnt;
+            done += take;
+        }
+    }
+    if (!c.err && bad) c.err = COVT_ERR_BAD_HEADER;
+    c.consumed = pos;
+}
+
+// ---- FastPFOR ------------------------------------------------------------------------------
+struct Words {
+    const uint8_t* sb;
+    int32_t nw;
+    __device__ __forceinline__ uint32_t operator()(int64_t i) const { return ld_be32(sb + 4 * i); }
+};
+
+// exception value X[k][i] (dataTobePacked[k]); words past the stream read as 0
+__device__ __forceinline__ uint32_t xget(const Words& W, uint32_t xs, int k, uint32_t i) {
+    const int64_t bit = (int64_t)(i & 31u) * k;
+    const int64_t wi = (int64_t)xs + (int64_t)(i >> 5) * k + (bit >> 5);
+    const int off = (int)(bit & 31);
+    const uint64_t lo = wi < W.nw ? W(wi) : 0u;
+    const uint64_t hi = (off + k > 32 && wi + 1 < W.nw) ? W(wi + 1) : 0u;
+    const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
+    return (uint32_t)(((lo | (hi << 32)) >> off) & m);
+}
+// byte j of the page's byte container (LE bytes of the BE words starting at word bc)
+__device__ __forceinline__ uint32_t bc_byte(const uint8_t* sb, int64_t bc, int64_t j) {
+    return sb[4 * (bc + (j >> 2)) + 3 - (j & 3)];
+}
+
+__device__ void run_fastpfor(Ctx& c) {
+    WaveSmem& sm = *c.sm;
+    const int l = lane_id();
+    const Words W{c.sb, c.byte_length / 4};
+    const int64_t nw = W.nw;
+    Carry cr{0, 0};
+    int32_t decoded = 0;
+    int32_t L = 0;
+    int64_t p = 1;
+    if (c.byte_length > c.avail) { c.err = COVT_ERR_TRUNCATED; }
+    if (!c.err && nw > 0) {
+        L = (int32_t)uniu(W(0));
+        if (L < 0) c.err = COVT_ERR_BAD_HEADER;
+        L -= L % kFpfBlock;
+        if (!c.err && L > c.n) c.err = COVT_ERR_COUNT_MISMATCH;
+        int32_t done = 0;
+        while (!c.err && done < L) {
+            const int32_t thissize = (L - done) < kFpfPage ? (L - done) : kFpfPage;
+            const int64_t p0 = p;
+            if (p0 >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+            int64_t ie = p0 + (int32_t)uniu(W(p0));
+            if (ie < 0 || ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+            const int32_t bytesize = (int32_t)uniu(W(ie++));
+            if (bytesize < 0 || bytesize > kFpfBcCap) { c.err = COVT_ERR_BAD_HEADER; break; }
+            const int64_t bcw = (bytesize + 3) / 4;
+            const int64_t bc = ie;
+            if (bc + bcw >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+            ie += bcw;
+            const uint32_t bitmap = uniu(W(ie++));
+            for (int k = 2; k <= 32 && !c.err; ++k) {
+                int32_t size = -1;
+                uint32_t xs = 0;
+                if (bitmap & (1u << (k - 1))) {
+                    if (ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+                    size = (int32_t)uniu(W(ie++));
+                    if (size < 0) { c.err = COVT_ERR_BAD_HEADER; break; }
+                    const int64_t groups = ((int64_t)size + 31) / 32;
+                    xs = (uint32_t)ie;
+                    ie += groups * k;
+                    ie -= ((groups * 32 - size) * k) / 32;
+                }
+                if (l == 0) { sm.xstart[k] = xs; sm.xsize[k] = size; sm.xcnt[k] = 0; }
+            }
+            if (c.err) break;
+            wave_sync();
+            const int32_t nblocks = thissize / kFpfBlock;
+            int64_t bcur = 0, pk = p0 + 1;
+            for (int32_t b0 = 0; b0 < nblocks && !c.err; b0 += kBlkBatch) {
+                const int32_t nbat = (nblocks - b0) < kBlkBatch ? (nblocks - b0) : kBlkBatch;
+                // serial byte-container walk (lane 0): block headers -> LDS records
+                if (l == 0) {
+                    int32_t e = 0;
+                    for (int32_t j = 0; j < nbat; ++j) {
+                        if (bcur + 2 > bcw * 4) { e = COVT_ERR_BAD_HEADER; break; }
+                        const int32_t b = (int32_t)(int8_t)bc_byte(c.sb, bc, bcur);
+                        const int32_t ce = (int32_t)bc_byte(c.sb, bc, bcur + 1);
+                        bcur += 2;
+                        if (b < 0 || b > 32) { e = COVT_ERR_BAD_HEADER; break; }
+                        if (pk + 8 * b > nw) { e = COVT_ERR_TRUNCATED; break; }
+                        int32_t idx = 0;
+                        uint32_t xcur = 0;
+                        if (ce > 0) {
+                            if (bcur + 1 + ce > bcw * 4) { e = COVT_ERR_BAD_HEADER; break; }
+                            idx = (int32_t)(int8_t)bc_byte(c.sb, bc, bcur) - b;
+                            bcur += 1;
+                            if (idx != 1) {
+                                if (idx < 2 || idx > 32 || sm.xsize[idx] < 0) { e = COVT_ERR_BAD_HEADER; break; }
+                                xcur = sm.xcnt[idx];
+                                if ((int64_t)xcur + ce > sm.xsize[idx]) { e = COVT_ERR_BAD_HEADER; break; }
+                                sm.xcnt[idx] = xcur + ce;
+                            }
+                        }
+                        sm.blk[4 * j + 0] = (uint32_t)b | ((uint32_t)ce << 8) | ((uint32_t)idx << 16);
+                        sm.blk[4 * j + 1] = (uint32_t)bcur;
+                        sm.blk[4 * j + 2] = xcur;
+                        sm.blk[4 * j + 3] = (uint32_t)pk;
+                        bcur += ce;
+                        pk += 8 * b;
+                    }
+                    sm.misc[1] = e;
+                    sm.misc[2] = (int32_t)bcur;
+                    sm.misc[3] = (int32_t)pk;
+                }
+                wave_sync();
+                c.err = uni(sm.misc[1]);
+                bcur = uni(sm.misc[2]);
+                pk = uni(sm.misc[3]);
+                if (c.err) break;
+                for (int32_t j = 0; j < nbat; ++j) {
+                    const uint32_t h = uniu(sm.blk[4 * j + 0]);
+                    const int32_t b = (int32_t)(h & 0xffu), ce = (int32_t)((h >> 8) & 0xffu), idx = (int32_t)(h >> 16);
+                    const uint32_t bco = uniu(sm.blk[4 * j + 1]), xcur = uniu(sm.blk[4 * j + 2]);
+                    const int64_t bpk = (int64_t)uniu(sm.blk[4 * j + 3]);
+                    // stage the block's 8*b packed words (raw bytes) in LDS
+                    const uintptr_t a = (uintptr_t)(c.sb + 4 * bpk);
+                    const uintptr_t a16 = a & ~(uintptr_t)15;
+                    const int32_t o = (int32_t)(a - a16);
+                    const int32_t nchunks = (32 * b + o + 15) / 16;
+                    for (int32_t q = l; q < nchunks; q += 64) ((uint4*)sm.u.f.stage)[q] = ((const uint4*)a16)[q];
+                    wave_sync();
+                    uint32_t v[4];
+                    const int mb = l >> 3, r0 = (l & 7) * 4;
+                    const uint32_t sh = (uint32_t)(o & 3);
+                    auto sword = [&](int32_t i) -> uint32_t {  // packed word i of this block
+                        const int32_t d = (o + 4 * i) >> 2;
+                        return __builtin_bswap32(__builtin_amdgcn_alignbyte(sm.u.f.stage[d + 1], sm.u.f.stage[d], sh));
+                    };
+                    const uint64_t m = b == 32 ? 0xffffffffull : ((1ull << b) - 1ull);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (b == 0) { v[k] = 0; continue; }
+                        const int32_t bit = (r0 + k) * b;
+                        const int32_t wi = mb * b + (bit >> 5);
+                        const int off = bit & 31;
+                        const uint64_t lo = sword(wi);
+                        const uint64_t hi = (off + b > 32) ? (uint64_t)sword(wi + 1) : 0ull;
+                        v[k] = (uint32_t)(((lo | (hi << 32)) >> off) & m);
+                    }
+                    if (ce > 0) {
+                        ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
+                        wave_sync();
+                        for (int32_t e = l; e < ce; e += 64) {
+                            const uint32_t pos8 = bc_byte(c.sb, bc, (int64_t)bco + e);
+                            const uint32_t ex = (idx == 1) ? 1u : xget(W, sm.xstart[idx], idx, xcur + (uint32_t)e);
+                            atomicOr(&sm.u.f.patch[pos8], ex << (b & 31));  // out[pos] |= ...
+                        }
+                        wave_sync();
+                        const uint4 pt = ((const uint4*)sm.u.f.patch)[l];
+                        v[0] |= pt.x;
+                        v[1] |= pt.y;
+                        v[2] |= pt.z;
+                        v[3] |= pt.w;
+                    }
+                    sink_values<4>(c.op, v, (int64_t)done + (int64_t)(b0 + j) * kFpfBlock, kFpfBlock, c.nb, c.out,
+                                   cr);
+                    wave_sync();
+                }
+            }
+            done += thissize;
+            p = ie;
+        }
+        decoded = L;
+        // VariableByte tail over words [p, nw)
+        if (!c.err && p < nw) {
+            int32_t vpos = (int32_t)(4 * p);
+            const int32_t base = L;
+            const int32_t got = varint_run<MODE_WORDREV, VAL_VB>(
+                sm, c.sb, vpos, (int32_t)(4 * nw), c.n - L, true, c.err,
+                [&](uint32_t lo, uint32_t hi, int32_t vb, int32_t count) {
+                    uint32_t vv[1] = {lo};
+                    sink_values<1>(c.op, vv, (int64_t)base + vb, count, c.nb, c.out, cr);
+                });
+            decoded = L + got;
+        }
+    }
+    // values the codec did not produce stay 0 in Java's decompressedValues[]: transform them too
+    if (!c.err) {
+        for (int32_t b = decoded; b < c.n; b += 64) {
+            uint32_t vv[1] = {0};
+            sink_values<1>(c.op, vv, b, c.n - b < 64 ? c.n - b : 64, c.nb, c.out, cr);
+        }
+        if (c.op == COVT_OP_FPF_ZZ_DELTA_XY && (c.n & 1)) c.err = COVT_ERR_COUNT_MISMATCH;
+    }
+    c.consumed = c.byte_length;
+}
+
+__global__ __launch_bounds__(256) void decode_streams_kernel(const uint8_t* __restrict__ in,
+                                                             const covt_stream_desc* __restrict__ descs,
+                                                             int64_t n_streams, uint8_t* __restrict__ out,
+                                                             covt_stream_result* __restrict__ res) {
+    __shared__ WaveSmem smem[kWavesPerBlock];
+    const int wv = uni((int)(threadIdx.x >> 6));
+    const int64_t sid = (int64_t)blockIdx.x * kWavesPerBlock + wv;
+    if (sid >= n_streams) return;
+    const covt_stream_desc d = descs[sid];
+    Ctx c;
+    c.sm = &smem[wv];
+    c.sb = in + d.in_off;
+    c.out = out + d.out_off;
+    c.avail = d.avail;
+    c.n = d.num_values;
+    c.nb = d.num_bits;
+    c.op = d.op;
+    c.byte_length = d.byte_length;
+    c.err = 0;
+    c.consumed = 0;
+    if (c.n < 0 || c.avail < 0 || c.byte_length < 0) {
+        c.err = COVT_ERR_INVALID_ARG;
+    } else if (c.n > 0 || c.op >= COVT_OP_FPF_ZZ_DELTA_I32) {
+        switch (c.op) {
+        case COVT_OP_BYTE_RLE_U8: run_rle_byte(c); break;
+        case COVT_OP_RLE_U64:
+        case COVT_OP_RLE_I32:
+        case COVT_OP_RLE_S64: run_rle_int(c); break;
+        case COVT_OP_VARINT_I32:
+        case COVT_OP_VARINT_ZZ_I32:
+        case COVT_OP_VARINT_ZZ_DELTA_I32:
+        case COVT_OP_VARINT_ZZ_DELTA_XY:
+        case COVT_OP_VARINT_DELTA_MORTON:
+        case COVT_OP_VARINT_U64:
+        case COVT_OP_VARINT_I32_AS_I64:
+        case COVT_OP_VARINT_ZZ_DELTA_I64: run_varint_stream(c); break;
+        case COVT_OP_FPF_ZZ_DELTA_I32:
+        case COVT_OP_FPF_ZZ_DELTA_XY:
+        case COVT_OP_FPF_DELTA_MORTON: run_fastpfor(c); break;
+        default: c.err = COVT_ERR_UNSUPPORTED_ENCODING; break;
+        }
+    }
+    if (lane_id() == 0) {
+        covt_stream_result r;
+        r.status = c.err;
+        r.consumed = c.consumed;
+        res[sid] = r;
+    }
+}
+
+}  // namespace covt
+
+extern "C" int covt_launch_decode(const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
+                                  uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream) {
+    if (n_streams <= 0) return COVT_OK;
+    const int64_t blocks = (n_streams + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
+    if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
+    hipLaunchKernelGGL(covt::decode_streams_kernel, dim3((unsigned)blocks), dim3(64 * covt::kWavesPerBlock), 0,
+                       stream, d_in, d_desc, n_streams, d_out, d_res);
+    return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
+}

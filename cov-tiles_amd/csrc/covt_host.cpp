@@ -1,0 +1,667 @@
+// covt_host.cpp -- host side of libcovt: container walkers (plan), the C-ABI of include/covt.h,
+// device contexts and the multi-GPU shard driver.
+//
+// The container walk is the host half of CovtParser.decodeCovt (CovtParser.java:53-133): it reads
+// only metadata (tens of bytes per layer) and turns every Id / Geometry stream into a 32-byte
+// covt_stream_desc.  Output sizes are known from numValues before anything is decoded, so one pass
+// assigns every stream its output slice; the GPU then decodes all streams of all tiles in one launch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <thread>
+#include <vector>
+
+#include "covt.h"
+#include "covt_internal.h"
+
+namespace {
+
+// ---- wire enums --------------------------------------------------
+enum StreamType { ST_PRESENT = 0, ST_DATA = 1, ST_LENGTH = 2, ST_DICTIONARY = 3, ST_GEOMETRY_TYPES = 4,
+                  ST_GEOMETRY_OFFSETS = 5, ST_PART_OFFSETS = 6, ST_RING_OFFSETS = 7, ST_VERTEX_OFFSETS = 8,
+                  ST_VERTEX_BUFFER = 9, ST_Z = 10, ST_M = 11 };
+enum Encoding { ENC_PLAIN = 0, ENC_VARINT = 1, ENC_VARINT_DELTA_ZZ = 4, ENC_RLE = 5, ENC_FPF_DELTA_ZZ = 9 };
+enum ColumnType { CT_PLAIN = 0, CT_ICE = 3, CT_ICE_MORTON = 4 };
+
+struct RawStream {
+    int32_t layer, kind, type, enc, ctype, nv, bl, nb;
+    int64_t off;  // tile-relative payload offset
+};
+
+// LEB128 (metadata of Gen C is written with EncodingUtils.encodeVarints, i.e. 64-bit varints)
+bool rd_uv(const uint8_t* t, size_t len, size_t& o, uint64_t& v) {
+    v = 0;
+    for (int i = 0; i < 10; ++i) {
+        if (o >= len) return false;
+        const uint8_t b = t[o++];
+        v |= (uint64_t)(b & 0x7f) << (7 * i);
+        if (!(b & 0x80)) return true;
+    }
+    return false;
+}
+// DecodingUtils.decodeVarint (4-byte cap) as used by the Gen D metadata reader
+bool rd_j4(const uint8_t* t, size_t len, size_t& o, int32_t& v) {
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) {
+        if (o >= len) return false;
+        const uint8_t b = t[o++];
+        r |= (uint32_t)(b & 0x7f) << (7 * i);
+        if (i < 3 && !(b & 0x80)) break;
+    }
+    v = (int32_t)r;
+    return true;
+}
+int nbits_of_extent(uint64_t extent) {  // 32 - Integer.numberOfLeadingZeros(extent), CovtParser.java:77
+    const uint32_t e = (uint32_t)extent;
+    return e ? 32 - __builtin_clz(e) : 0;
+}
+int genc_stream_type(const uint8_t* s, uint64_t n) {
+    static const char* kNames[] = {"present", "data", "length", "dictionary", "geometry_types",
+                                   "geometry_offsets", "part_offsets", "ring_offsets", "vertex_offsets",
+                                   "vertex_buffer"};
+    for (int i = 0; i < 10; ++i)
+        if (std::strlen(kNames[i]) == n && std::memcmp(kNames[i], s, n) == 0) return i;
+    return -1;
+}
+
+// Gen C container (all committed fixtures), SURVEY.md Appendix A.1.  Geometry streams are laid
+// out in StreamType order whatever their metadata order; other columns in metadata order.
+int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
+    size_t o = 0;
+    uint64_t version, nlayers;
+    if (!rd_uv(t, len, o, version) || !rd_uv(t, len, o, nlayers)) return COVT_ERR_TRUNCATED;
+    if (version != 1) return COVT_ERR_BAD_HEADER;
+    struct SM { int type, enc; int64_t nv, bl; };
+    struct CM { int kind, dtype, ctype; std::vector<SM> s; };
+    std::vector<CM> cols;
+    for (uint64_t L = 0; L < nlayers; ++L) {
+        uint64_t nlen, extent, nfeat, ncols;
+        if (!rd_uv(t, len, o, nlen) || o + nlen > len) return COVT_ERR_TRUNCATED;
+        o += nlen;
+        if (!rd_uv(t, len, o, extent) || !rd_uv(t, len, o, nfeat) || !rd_uv(t, len, o, ncols))
+            return COVT_ERR_TRUNCATED;
+        if (ncols > 4096) return COVT_ERR_BAD_HEADER;
+        cols.assign(ncols, CM{});
+        for (auto& c : cols) {
+            uint64_t cn, ns;
+            if (!rd_uv(t, len, o, cn) || o + cn + 2 > len) return COVT_ERR_TRUNCATED;
+            const uint8_t* name = t + o;
+            o += cn;
+            c.dtype = t[o++];
+            c.ctype = t[o++];
+            c.kind = (cn == 2 && !std::memcmp(name, "id", 2)) ? 0
+                     : ((cn == 8 && !std::memcmp(name, "geometry", 8)) || c.dtype == 6) ? 1 : 2;
+            if (!rd_uv(t, len, o, ns)) return COVT_ERR_TRUNCATED;
+            if (ns > 256) return COVT_ERR_BAD_HEADER;
+            c.s.resize(ns);
+            for (auto& s : c.s) {
+                uint64_t sn, nv, bl;
+                if (!rd_uv(t, len, o, sn) || o + sn > len) return COVT_ERR_TRUNCATED;
+                s.type = genc_stream_type(t + o, sn);
+                o += sn;
+                if (!rd_uv(t, len, o, nv) || !rd_uv(t, len, o, bl) || o >= len) return COVT_ERR_TRUNCATED;
+                s.enc = t[o++];
+                if (nv > 0x7fffffff || bl > 0x7fffffff) return COVT_ERR_BAD_HEADER;
+                s.nv = (int64_t)nv;
+                s.bl = (int64_t)bl;
+            }
+        }
+        const int nb = nbits_of_extent(extent);
+        for (auto& c : cols) {
+            if (c.kind == 1) {
+                for (int type = ST_GEOMETRY_TYPES; type <= ST_VERTEX_BUFFER; ++type)
+                    for (auto& s : c.s)
+                        if (s.type == type) {
+                            out.push_back({(int32_t)L, 1, type, s.enc, c.ctype, (int32_t)s.nv, (int32_t)s.bl, nb,
+                                           (int64_t)o});
+                            o += s.bl;
+                        }
+                for (auto& s : c.s)
+                    if (s.type < ST_GEOMETRY_TYPES || s.type > ST_VERTEX_BUFFER) o += s.bl;
+            } else {
+                for (auto& s : c.s) {
+                    if (c.kind == 0 && s.type == ST_DATA)
+                        out.push_back({(int32_t)L, 0, ST_DATA, s.enc, c.ctype, (int32_t)s.nv, (int32_t)s.bl, nb,
+                                       (int64_t)o});
+                    o += s.bl;
+                }
+            }
+            if (o > len) return COVT_ERR_TRUNCATED;
+        }
+    }
+    return o == len ? COVT_OK : COVT_ERR_BAD_HEADER;
+}
+
+// Gen D container: CovtParser.decodeLayerMetadata (CovtParser.java:574-652) + the column loop
+// of decodeCovt (:56-85).  Streams of a column follow TreeMap<StreamType> order.
+int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
+    size_t o = 0;
+    int32_t layer = 0;
+    struct SM { int enc; int32_t nv, bl; bool have; };
+    struct CM { int kind, dtype, ctype; SM s[12]; };
+    std::vector<CM> cols;
+    while (o < len) {
+        const int hdr = t[o++];
+        const bool optimized = hdr & 1;
+        int32_t v, extent, nfeat, ncols;
+        if (!rd_j4(t, len, o, v)) return COVT_ERR_TRUNCATED;
+        if (!optimized) {  // decodeString: varint length + UTF-8 bytes
+            if (v < 0 || o + (size_t)v > len) return COVT_ERR_TRUNCATED;
+            o += (size_t)v;
+        }
+        if (!rd_j4(t, len, o, extent) || !rd_j4(t, len, o, nfeat) || !rd_j4(t, len, o, ncols))
+            return COVT_ERR_TRUNCATED;
+        if (ncols < 0 || ncols > 4096) return COVT_ERR_BAD_HEADER;
+        cols.assign((size_t)ncols, CM{});
+        for (int32_t ci = 0; ci < ncols; ++ci) {
+            CM& c = cols[(size_t)ci];
+            if (optimized || ci == 0) {
+                int32_t cid;
+                if (!rd_j4(t, len, o, cid)) return COVT_ERR_TRUNCATED;
+                c.kind = cid == 0 ? 0 : (cid == 1 ? 1 : 2);
+            } else {
+                int32_t sl;
+                if (!rd_j4(t, len, o, sl) || sl < 0 || o + (size_t)sl > len) return COVT_ERR_TRUNCATED;
+                c.kind = (sl == 2 && !std::memcmp(t + o, "id", 2)) ? 0
+                         : (sl == 8 && !std::memcmp(t + o, "geometry", 8)) ? 1 : 2;
+                o += (size_t)sl;
+            }
+            if (o >= len) return COVT_ERR_TRUNCATED;
+            const int desc = t[o++];
+            c.dtype = (desc >> 3) & 0xF;
+            c.ctype = desc & 0x7;
+            if (c.ctype > 4) return COVT_ERR_BAD_HEADER;
+            for (;;) {
+                if (o >= len) return COVT_ERR_TRUNCATED;
+                const int sd = t[o++];
+                const int type = sd >> 4, enc = sd & 0xF;
+                if (type > ST_M || enc > 9) return COVT_ERR_BAD_HEADER;
+                int32_t nv, bl;
+                if (!rd_j4(t, len, o, nv) || !rd_j4(t, len, o, bl)) return COVT_ERR_TRUNCATED;
+                c.s[type] = SM{enc, nv, bl, true};
+                if (c.dtype == 8 && type == ST_VERTEX_BUFFER) break;
+                if (type == ST_DATA && c.ctype == CT_PLAIN) break;
+                if (type == ST_DICTIONARY) break;
+            }
+        }
+        const int nb = nbits_of_extent((uint32_t)extent);
+        for (auto& c : cols) {
+            for (int type = 0; type < 12; ++type) {
+                const SM& s = c.s[type];
+                if (!s.have) continue;
+                const bool hot = (c.kind == 0 && type == ST_DATA) ||
+                                 (c.kind == 1 && type >= ST_GEOMETRY_TYPES && type <= ST_VERTEX_BUFFER);
+                if (hot) out.push_back({layer, c.kind, type, s.enc, c.ctype, s.nv, s.bl, nb, (int64_t)o});
+                if (s.bl < 0) return COVT_ERR_BAD_HEADER;
+                o += (size_t)s.bl;
+            }
+            if (o > len) return COVT_ERR_TRUNCATED;
+        }
+        ++layer;
+    }
+    return COVT_OK;
+}
+
+// CovtParser dispatch: decodeGeometryColumn (:392-511) and decodedIds (:552-572)
+void choose_op(const RawStream& s, int id_mode, int& op, int64_t& nvals, int& elem, int64_t& out_elems) {
+    op = COVT_OP_NONE;
+    nvals = s.nv;
+    elem = 4;
+    out_elems = s.nv;
+    if (s.kind == 0) {
+        elem = 8;
+        if (s.enc == ENC_RLE) op = COVT_OP_RLE_U64;
+        else if (s.enc == ENC_VARINT) op = id_mode == COVT_ID_JAVA ? COVT_OP_VARINT_I32_AS_I64 : COVT_OP_VARINT_U64;
+        else if (s.enc == ENC_VARINT_DELTA_ZZ)
+            op = id_mode == COVT_ID_JAVA ? COVT_OP_VARINT_ZZ_DELTA_I64 : COVT_OP_RLE_U64;
+        return;
+    }
+    switch (s.type) {
+    case ST_GEOMETRY_TYPES: op = COVT_OP_BYTE_RLE_U8; elem = 1; return;
+    case ST_GEOMETRY_OFFSETS:
+    case ST_PART_OFFSETS:
+    case ST_RING_OFFSETS:
+        if (s.enc == ENC_RLE) op = COVT_OP_RLE_I32;
+        else if (s.enc == ENC_FPF_DELTA_ZZ) op = COVT_OP_FPF_ZZ_DELTA_I32;
+        return;
+    case ST_VERTEX_OFFSETS:
+        if (s.enc == ENC_VARINT_DELTA_ZZ) op = COVT_OP_VARINT_ZZ_DELTA_I32;
+        else if (s.enc == ENC_FPF_DELTA_ZZ) op = COVT_OP_FPF_ZZ_DELTA_I32;
+        return;
+    case ST_VERTEX_BUFFER:
+        if (s.ctype == CT_ICE_MORTON) {
+            out_elems = 2 * (int64_t)s.nv;
+            if (s.enc == ENC_VARINT_DELTA_ZZ) op = COVT_OP_VARINT_DELTA_MORTON;
+            else if (s.enc == ENC_FPF_DELTA_ZZ) op = COVT_OP_FPF_DELTA_MORTON;
+        } else {
+            if (s.ctype == CT_ICE) nvals = out_elems = 2 * (int64_t)s.nv;  // SURVEY Q4 build rule
+            if (s.enc == ENC_VARINT_DELTA_ZZ) op = COVT_OP_VARINT_ZZ_DELTA_XY;
+            else if (s.enc == ENC_FPF_DELTA_ZZ) op = COVT_OP_FPF_ZZ_DELTA_XY;
+        }
+        return;
+    default: return;
+    }
+}
+
+inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
+
+// ---- per-thread device context for the stream-level API -----------------------------------------
+struct DevCtx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint8_t* d_in = nullptr;
+    size_t in_cap = 0;
+    uint8_t* d_out = nullptr;
+    size_t out_cap = 0;
+    covt_stream_desc* d_desc = nullptr;
+    covt_stream_result* d_res = nullptr;
+    ~DevCtx() {
+        if (device < 0) return;
+        (void)hipSetDevice(device);
+        if (d_in) (void)hipFree(d_in);
+        if (d_out) (void)hipFree(d_out);
+        if (d_desc) (void)hipFree(d_desc);
+        if (d_res) (void)hipFree(d_res);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+bool grow(uint8_t*& p, size_t& cap, size_t need) {
+    if (need <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t c = std::max<size_t>(need, 1 << 16);
+    c = (c + 4095) & ~(size_t)4095;
+    if (hipMalloc(&p, c) != hipSuccess) return false;
+    cap = c;
+    return true;
+}
+
+DevCtx* ctx() {
+    thread_local DevCtx c;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (c.device != dev) {
+        c.~DevCtx();
+        new (&c) DevCtx();
+        c.device = dev;
+        if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        if (hipMalloc(&c.d_desc, sizeof(covt_stream_desc)) != hipSuccess) return nullptr;
+        if (hipMalloc(&c.d_res, sizeof(covt_stream_result)) != hipSuccess) return nullptr;
+    }
+    return &c;
+}
+
+// Decode one stream held in host memory: `region` bytes become the device stream payload.
+int run_one(const uint8_t* region, size_t region_len, size_t pad_to, int op, int32_t n, int32_t byte_length, int nb,
+            void* out, size_t out_bytes, covt_stream_result* res) {
+    DevCtx* c = ctx();
+    if (!c) return COVT_ERR_DEVICE;
+    const size_t payload = std::max(region_len, pad_to);
+    if (!grow(c->d_in, c->in_cap, payload + COVT_INPUT_PADDING)) return COVT_ERR_DEVICE;
+    if (!grow(c->d_out, c->out_cap, out_bytes + 16)) return COVT_ERR_DEVICE;
+    if (region_len && hipMemcpyAsync(c->d_in, region, region_len, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    if (payload > region_len &&  // Arrays.copyOfRange zero-pads past the source (DecodingUtils.java:317)
+        hipMemsetAsync(c->d_in + region_len, 0, payload - region_len, c->stream) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    covt_stream_desc d{};
+    d.in_off = 0;
+    d.out_off = 0;
+    d.avail = (int32_t)std::min<size_t>(payload, 0x7fffffff);
+    d.num_values = n;
+    d.op = (uint8_t)op;
+    d.num_bits = (uint8_t)nb;
+    d.byte_length = byte_length;
+    if (hipMemcpyAsync(c->d_desc, &d, sizeof d, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    int st = covt_launch_decode(c->d_in, c->d_desc, 1, c->d_out, c->d_res, c->stream);
+    if (st) return st;
+    if (out_bytes && hipMemcpyAsync(out, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    if (hipMemcpyAsync(res, c->d_res, sizeof *res, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return COVT_ERR_DEVICE;
+    return COVT_OK;
+}
+
+// stream-level wrappers: varint / RLE ops read [pos, buf_len) (Java reads up to the array end)
+int stream_call(const uint8_t* buf, size_t buf_len, int32_t* pos, int op, int32_t n, int nb, void* out,
+                size_t elem_bytes, size_t out_elems) {
+    if (!pos || n < 0 || (!buf && buf_len) || (!out && out_elems)) return COVT_ERR_INVALID_ARG;
+    if (*pos < 0 || (size_t)*pos > buf_len) return COVT_ERR_TRUNCATED;
+    covt_stream_result r{};
+    const size_t rl = buf_len - (size_t)*pos;
+    int st = run_one(buf + *pos, rl, 0, op, n, 0, nb, out, elem_bytes * out_elems, &r);
+    if (st) return st;
+    if (r.status) return r.status;
+    *pos += r.consumed;
+    return COVT_OK;
+}
+int fpf_call(const uint8_t* buf, size_t buf_len, int32_t* pos, int op, int32_t n, int32_t byte_length, int nb,
+             void* out, size_t out_elems) {
+    if (!pos || n < 0 || byte_length < 0 || (!buf && buf_len) || (!out && out_elems)) return COVT_ERR_INVALID_ARG;
+    if (*pos < 0) return COVT_ERR_INVALID_ARG;
+    const size_t start = std::min<size_t>((size_t)*pos, buf_len);
+    const size_t rl = std::min<size_t>(buf_len - start, (size_t)byte_length);
+    covt_stream_result r{};
+    int st = run_one(buf + start, rl, (size_t)byte_length, op, n, byte_length, nb, out, 4 * out_elems, &r);
+    if (st) return st;
+    if (r.status) return r.status;
+    *pos += byte_length;
+    return COVT_OK;
+}
+
+}  // namespace
+
+// ================================================================================================
+// C-ABI
+// ================================================================================================
+struct covt_plan {
+    int32_t n_tiles = 0;
+    std::vector<int32_t> tile_status;
+    std::vector<uint64_t> tile_off, tile_size;
+    std::vector<covt_stream_info> info;   // tile order
+    std::vector<covt_stream_desc> descs;  // launch order (largest first)
+    int64_t out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
+};
+
+extern "C" {
+
+const char* covt_version(void) { return "covt-mi355x 0.1 (gfx950)"; }
+
+int covt_device_count(int32_t* n) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    if (n) *n = c;
+    return COVT_OK;
+}
+
+int covt_decode_varint(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t n, int32_t* out) {
+    return stream_call(buf, buf_len, pos, COVT_OP_VARINT_I32, n, 0, out, 4, (size_t)std::max(n, 0));
+}
+int covt_decode_zigzag_varint(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t n, int32_t* out) {
+    return stream_call(buf, buf_len, pos, COVT_OP_VARINT_ZZ_I32, n, 0, out, 4, (size_t)std::max(n, 0));
+}
+int covt_decode_zigzag_delta_varint(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t n, int32_t* out) {
+    return stream_call(buf, buf_len, pos, COVT_OP_VARINT_ZZ_DELTA_I32, n, 0, out, 4, (size_t)std::max(n, 0));
+}
+int covt_decode_zigzag_delta_varint_coordinates(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t n,
+                                                int32_t* out) {
+    return stream_call(buf, buf_len, pos, COVT_OP_VARINT_ZZ_DELTA_XY, n, 0, out, 4, (size_t)std::max(n, 0));
+}
+int covt_decode_rle(const uint8_t* buf, size_t buf_len, int32_t n, int32_t* pos, int32_t is_signed, int64_t* out) {
+    return stream_call(buf, buf_len, pos, is_signed ? COVT_OP_RLE_S64 : COVT_OP_RLE_U64, n, 0, out, 8,
+                       (size_t)std::max(n, 0));
+}
+int covt_decode_byte_rle(const uint8_t* buf, size_t buf_len, int32_t n, int32_t* pos, int32_t byte_length,
+                         uint8_t* out) {
+    if (!pos) return COVT_ERR_INVALID_ARG;
+    const int32_t p0 = *pos;
+    int st = stream_call(buf, buf_len, pos, COVT_OP_BYTE_RLE_U8, n, 0, out, 1, (size_t)std::max(n, 0));
+    // decodeByteRle(..., byteLength) advances by the metadata byteLength (DecodingUtils.java:286);
+    // the GeometryType range check belongs to decodeGeometryColumn, not to this method
+    if (st == COVT_ERR_BAD_HEADER) st = COVT_OK;
+    if (!st) *pos = p0 + byte_length;
+    return st;
+}
+int covt_decode_fastpfor_zigzag_delta(const uint8_t* buf, size_t buf_len, int32_t n, int32_t byte_length,
+                                      int32_t* pos, int32_t* out) {
+    return fpf_call(buf, buf_len, pos, COVT_OP_FPF_ZZ_DELTA_I32, n, byte_length, 0, out, (size_t)std::max(n, 0));
+}
+int covt_decode_fastpfor_delta_coordinates(const uint8_t* buf, size_t buf_len, int32_t n, int32_t byte_length,
+                                           int32_t* pos, int32_t* out) {
+    return fpf_call(buf, buf_len, pos, COVT_OP_FPF_ZZ_DELTA_XY, n, byte_length, 0, out, (size_t)std::max(n, 0));
+}
+int covt_decode_delta_varint_morton_codes(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t n_vertices,
+                                          int32_t num_bits, int32_t* out) {
+    if (num_bits < 0 || num_bits > 255) return COVT_ERR_INVALID_ARG;
+    return stream_call(buf, buf_len, pos, COVT_OP_VARINT_DELTA_MORTON, n_vertices, num_bits, out, 4,
+                       2 * (size_t)std::max(n_vertices, 0));
+}
+int covt_decode_fastpfor_delta_morton_codes(const uint8_t* buf, size_t buf_len, int32_t n_vertices,
+                                            int32_t byte_length, int32_t* pos, int32_t num_bits, int32_t* out) {
+    if (num_bits < 0 || num_bits > 255) return COVT_ERR_INVALID_ARG;
+    return fpf_call(buf, buf_len, pos, COVT_OP_FPF_DELTA_MORTON, n_vertices, byte_length, num_bits, out,
+                    2 * (size_t)std::max(n_vertices, 0));
+}
+
+int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
+                     int32_t n_tiles, int32_t format, int32_t id_mode, covt_plan** out) {
+    if (!out || n_tiles < 0 || (n_tiles && (!bytes || !tile_offsets || !tile_sizes))) return COVT_ERR_INVALID_ARG;
+    if (format != COVT_FORMAT_GENC && format != COVT_FORMAT_GEND) return COVT_ERR_INVALID_ARG;
+    auto* p = new covt_plan();
+    p->n_tiles = n_tiles;
+    p->tile_status.assign((size_t)n_tiles, 0);
+    p->tile_off.assign(tile_offsets, tile_offsets + n_tiles);
+    p->tile_size.assign(tile_sizes, tile_sizes + n_tiles);
+    std::vector<RawStream> rs;
+    int64_t out_off = 0;
+    for (int32_t t = 0; t < n_tiles; ++t) {
+        rs.clear();
+        const uint8_t* tile = bytes + tile_offsets[t];
+        const int st = format == COVT_FORMAT_GENC ? walk_genc(tile, (size_t)tile_sizes[t], rs)
+                                                  : walk_gend(tile, (size_t)tile_sizes[t], rs);
+        p->tile_status[(size_t)t] = st;
+        if (st) continue;
+        for (const RawStream& s : rs) {
+            int op, elem;
+            int64_t nvals, out_elems;
+            choose_op(s, id_mode, op, nvals, elem, out_elems);
+            covt_stream_info si{};
+            si.tile = t;
+            si.layer = s.layer;
+            si.column_kind = s.kind;
+            si.stream_type = s.type;
+            si.encoding = s.enc;
+            si.column_type = s.ctype;
+            si.num_values = s.nv;
+            si.byte_length = s.bl;
+            si.num_bits = s.nb;
+            si.op = op;
+            si.elem_bytes = elem;
+            si.in_off = (int64_t)tile_offsets[t] + s.off;
+            si.out_elems = op == COVT_OP_NONE ? 0 : out_elems;
+            si.out_off = out_off;
+            out_off = align16(out_off + si.out_elems * elem);
+            p->in_bytes += s.bl;
+            p->out_payload += si.out_elems * elem;
+            if (s.kind == 1 && s.type == ST_VERTEX_BUFFER)
+                p->vertices += (s.ctype == CT_ICE || s.ctype == CT_ICE_MORTON) ? s.nv : s.nv / 2;
+            si.desc_index = (int32_t)nvals;  // temporarily: values to decode
+            p->info.push_back(si);
+        }
+    }
+    p->out_bytes = out_off;
+    // launch order: largest streams first so the long poles start early (static wave->stream map)
+    const size_t ns = p->info.size();
+    std::vector<int64_t> order(ns);
+    std::iota(order.begin(), order.end(), 0);
+    auto cost = [&](int64_t i) {
+        const auto& s = p->info[(size_t)i];
+        return (int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4;
+    };
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return cost(a) > cost(b); });
+    p->descs.resize(ns);
+    for (size_t k = 0; k < ns; ++k) {
+        covt_stream_info& si = p->info[(size_t)order[k]];
+        covt_stream_desc d{};
+        d.in_off = (uint64_t)si.in_off;
+        d.out_off = (uint64_t)si.out_off;
+        d.avail = si.byte_length;
+        d.num_values = si.desc_index;
+        d.op = (uint8_t)si.op;
+        d.num_bits = (uint8_t)si.num_bits;
+        d.byte_length = si.byte_length;
+        p->descs[k] = d;
+        si.desc_index = (int32_t)k;
+    }
+    *out = p;
+    return COVT_OK;
+}
+
+void covt_plan_destroy(covt_plan* plan) { delete plan; }
+int64_t covt_plan_num_streams(const covt_plan* p) { return p ? (int64_t)p->info.size() : 0; }
+int64_t covt_plan_output_bytes(const covt_plan* p) { return p ? p->out_bytes : 0; }
+int covt_plan_totals(const covt_plan* p, int64_t* in_bytes, int64_t* out_bytes, int64_t* vertices) {
+    if (!p) return COVT_ERR_INVALID_ARG;
+    if (in_bytes) *in_bytes = p->in_bytes;
+    if (out_bytes) *out_bytes = p->out_payload;
+    if (vertices) *vertices = p->vertices;
+    return COVT_OK;
+}
+int covt_plan_streams(const covt_plan* p, covt_stream_info* out) {
+    if (!p || (!out && !p->info.empty())) return COVT_ERR_INVALID_ARG;
+    if (!p->info.empty()) std::memcpy(out, p->info.data(), p->info.size() * sizeof(covt_stream_info));
+    return COVT_OK;
+}
+int covt_plan_descs(const covt_plan* p, covt_stream_desc* out) {
+    if (!p || (!out && !p->descs.empty())) return COVT_ERR_INVALID_ARG;
+    if (!p->descs.empty()) std::memcpy(out, p->descs.data(), p->descs.size() * sizeof(covt_stream_desc));
+    return COVT_OK;
+}
+int covt_plan_tile_status(const covt_plan* p, int32_t* out) {
+    if (!p || (!out && p->n_tiles)) return COVT_ERR_INVALID_ARG;
+    if (p->n_tiles) std::memcpy(out, p->tile_status.data(), sizeof(int32_t) * (size_t)p->n_tiles);
+    return COVT_OK;
+}
+
+int covt_decode_streams_device(const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
+                               uint8_t* d_out, covt_stream_result* d_res, void* hip_stream) {
+    if (n_streams < 0 || (n_streams && (!d_in || !d_desc || !d_res))) return COVT_ERR_INVALID_ARG;
+    if ((uintptr_t)d_in & 15) return COVT_ERR_INVALID_ARG;
+    return covt_launch_decode(d_in, d_desc, n_streams, d_out, d_res, (hipStream_t)hip_stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+// Decode a subset of a plan's streams on the current device.  `sel` lists tile-order stream
+// indices; their inputs are the tiles in `tiles` (packed contiguously on the device).
+int decode_subset(const covt_plan* p, const uint8_t* bytes, const std::vector<int32_t>& tiles, uint8_t* host_out,
+                  covt_stream_result* host_res) {
+    // pack the shard's tiles
+    std::vector<int64_t> new_tile_off(p->n_tiles, -1);
+    uint64_t in_total = 0;
+    for (int32_t t : tiles) {
+        new_tile_off[(size_t)t] = (int64_t)in_total;
+        in_total += (p->tile_size[(size_t)t] + 15) & ~(uint64_t)15;
+    }
+    std::vector<int64_t> sel;
+    for (size_t i = 0; i < p->info.size(); ++i)
+        if (new_tile_off[(size_t)p->info[i].tile] >= 0) sel.push_back((int64_t)i);
+    // launch order of the shard = the plan's global launch order restricted to it
+    std::sort(sel.begin(), sel.end(),
+              [&](int64_t a, int64_t b) { return p->info[(size_t)a].desc_index < p->info[(size_t)b].desc_index; });
+    std::vector<covt_stream_desc> descs(sel.size());
+    std::vector<int64_t> new_out(sel.size());
+    int64_t out_total = 0;
+    for (size_t k = 0; k < sel.size(); ++k) {
+        const covt_stream_info& si = p->info[(size_t)sel[k]];
+        covt_stream_desc d = p->descs[(size_t)si.desc_index];
+        d.in_off = (uint64_t)(new_tile_off[(size_t)si.tile] + (si.in_off - (int64_t)p->tile_off[(size_t)si.tile]));
+        new_out[k] = out_total;
+        d.out_off = (uint64_t)out_total;
+        out_total = align16(out_total + si.out_elems * si.elem_bytes);
+        descs[k] = d;
+    }
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return COVT_ERR_DEVICE;
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    covt_stream_desc* d_desc = nullptr;
+    covt_stream_result* d_res = nullptr;
+    int st = COVT_OK;
+    std::vector<covt_stream_result> res(sel.size());
+    std::vector<uint8_t> stage;
+    auto chk = [&](hipError_t e) { if (e != hipSuccess && st == COVT_OK) st = COVT_ERR_DEVICE; };
+    chk(hipMalloc(&d_in, in_total + COVT_INPUT_PADDING));
+    chk(hipMalloc(&d_out, (size_t)std::max<int64_t>(out_total, 16)));
+    chk(hipMalloc(&d_desc, std::max<size_t>(descs.size(), 1) * sizeof(covt_stream_desc)));
+    chk(hipMalloc(&d_res, std::max<size_t>(descs.size(), 1) * sizeof(covt_stream_result)));
+    if (st == COVT_OK) {
+        for (int32_t t : tiles)
+            chk(hipMemcpyAsync(d_in + new_tile_off[(size_t)t], bytes + p->tile_off[(size_t)t],
+                               (size_t)p->tile_size[(size_t)t], hipMemcpyHostToDevice, s));
+        if (!descs.empty())
+            chk(hipMemcpyAsync(d_desc, descs.data(), descs.size() * sizeof(covt_stream_desc), hipMemcpyHostToDevice,
+                               s));
+        if (st == COVT_OK) st = covt_launch_decode(d_in, d_desc, (int64_t)descs.size(), d_out, d_res, s);
+        stage.resize((size_t)out_total);
+        if (st == COVT_OK && out_total)
+            chk(hipMemcpyAsync(stage.data(), d_out, (size_t)out_total, hipMemcpyDeviceToHost, s));
+        if (st == COVT_OK && !res.empty())
+            chk(hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(covt_stream_result), hipMemcpyDeviceToHost, s));
+        chk(hipStreamSynchronize(s));
+    }
+    if (st == COVT_OK) {
+        for (size_t k = 0; k < sel.size(); ++k) {
+            const covt_stream_info& si = p->info[(size_t)sel[k]];
+            std::memcpy(host_out + si.out_off, stage.data() + new_out[k], (size_t)(si.out_elems * si.elem_bytes));
+            host_res[(size_t)sel[k]] = res[k];
+        }
+    }
+    if (d_in) (void)hipFree(d_in);
+    if (d_out) (void)hipFree(d_out);
+    if (d_desc) (void)hipFree(d_desc);
+    if (d_res) (void)hipFree(d_res);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+int covt_plan_decode_host(const covt_plan* p, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_out,
+                          covt_stream_result* host_res) {
+    if (!p || (!host_res && !p->info.empty()) || (!host_out && p->out_bytes)) return COVT_ERR_INVALID_ARG;
+    (void)n_bytes;
+    std::vector<int32_t> tiles;
+    for (int32_t t = 0; t < p->n_tiles; ++t)
+        if (p->tile_status[(size_t)t] == 0) tiles.push_back(t);
+    return decode_subset(p, bytes, tiles, host_out, host_res);
+}
+
+int covt_plan_decode_host_multi(const covt_plan* p, const uint8_t* bytes, uint64_t n_bytes, int32_t n_gpus,
+                                uint8_t* host_out, covt_stream_result* host_res) {
+    if (!p || n_gpus < 1 || (!host_res && !p->info.empty()) || (!host_out && p->out_bytes))
+        return COVT_ERR_INVALID_ARG;
+    (void)n_bytes;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return COVT_ERR_DEVICE;
+    n_gpus = std::min(n_gpus, ndev);
+    // greedy longest-processing-time split on stream bytes + output bytes (no collectives)
+    std::vector<int64_t> w((size_t)p->n_tiles, 0);
+    for (const auto& si : p->info) w[(size_t)si.tile] += si.byte_length + si.out_elems * si.elem_bytes;
+    std::vector<int32_t> order;
+    for (int32_t t = 0; t < p->n_tiles; ++t)
+        if (p->tile_status[(size_t)t] == 0) order.push_back(t);
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return w[(size_t)a] > w[(size_t)b]; });
+    std::vector<std::vector<int32_t>> shard((size_t)n_gpus);
+    std::vector<int64_t> load((size_t)n_gpus, 0);
+    for (int32_t t : order) {
+        const size_t g = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
+        shard[g].push_back(t);
+        load[g] += w[(size_t)t];
+    }
+    std::vector<int> st((size_t)n_gpus, COVT_OK);
+    std::vector<std::thread> th;
+    for (int32_t g = 0; g < n_gpus; ++g) {
+        th.emplace_back([&, g] {
+            if (hipSetDevice(g) != hipSuccess) { st[(size_t)g] = COVT_ERR_DEVICE; return; }
+            std::sort(shard[(size_t)g].begin(), shard[(size_t)g].end());
+            st[(size_t)g] = decode_subset(p, bytes, shard[(size_t)g], host_out, host_res);
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int s : st)
+        if (s) return s;
+    return COVT_OK;
+}
+
+}  // extern "C"

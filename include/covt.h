@@ -1,0 +1,179 @@
+/*
+ * covt.h -- C-ABI of libcovt, the MI355X (gfx950) COVT Id/Geometry stream decoder.
+ *
+ * Drop-in boundary for the reference's Java decoder API (springmeyer/cov-tiles,
+ * evaluation/java, package com.covt.decoder).  Each stream-level entry point
+ * replaces one `public static` method of DecodingUtils.java with the same
+ * argument order and meaning; the Java `IntWrapper pos` becomes an int32_t*
+ * in/out cursor, `byte[]` inputs gain an explicit length, and outputs are
+ * caller-provided arrays (the Java methods allocate theirs).  Decoding runs on
+ * the GPU in every case: there is no CPU fallback.  A JNI shim
+ * (cov-tiles_amd/jni/covt_jni.cc) binds these to
+ * com.covt.decoder.gpu.GpuDecodingUtils; see INTEGRATION.md.
+ *
+ * Status codes map onto the Java exceptions of the reference:
+ *   COVT_ERR_UNSUPPORTED_ENCODING -> IllegalArgumentException (CovtParser.java:426,443,460,475,493,508,571)
+ *   COVT_ERR_TRUNCATED            -> ArrayIndexOutOfBoundsException / EOFException (ORC readers)
+ *   COVT_ERR_COUNT_MISMATCH       -> ArrayIndexOutOfBoundsException (output overrun)
+ *   COVT_ERR_BAD_HEADER           -> IllegalArgumentException (malformed FastPFOR / container)
+ */
+#ifndef COVT_H
+#define COVT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define COVT_OK 0
+#define COVT_ERR_UNSUPPORTED_ENCODING (-1)
+#define COVT_ERR_TRUNCATED (-2)
+#define COVT_ERR_COUNT_MISMATCH (-3)
+#define COVT_ERR_BAD_HEADER (-4)
+#define COVT_ERR_DEVICE (-5)
+#define COVT_ERR_INVALID_ARG (-6)
+
+/* Device input buffers handed to the *_device entry points must start 16-byte aligned
+ * and stay readable for COVT_INPUT_PADDING bytes past the last stream byte. */
+#define COVT_INPUT_PADDING 4096
+
+/* Container generations */
+#define COVT_FORMAT_GENC 0 /* every committed fixture (test/fixtures/NAME/covt) */
+#define COVT_FORMAT_GEND 1 /* what CovtParser.decodeCovt reads, CovtParser.java:574-652 */
+
+/* Id column decode modes */
+#define COVT_ID_FORMAT 0 /* format truth: VARINT = 64-bit LEB128, enc 4 = unsigned RLE */
+#define COVT_ID_JAVA 1   /* CovtParser.decodedIds verbatim: 4-byte varint cap, enc 4 = zigzag-delta */
+
+/* ---------------------------------------------------------------------------
+ * Stream-level API: one function per DecodingUtils method.
+ * `buf`/`buf_len` is the Java byte[]; *pos is the IntWrapper.  Host memory in and out.
+ * ------------------------------------------------------------------------- */
+/* DecodingUtils.decodeVarint(byte[] src, IntWrapper pos, int numValues)          DecodingUtils.java:35 */
+int covt_decode_varint(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t num_values, int32_t* out);
+/* DecodingUtils.decodeZigZagVarint(byte[], IntWrapper, int)                       DecodingUtils.java:46 */
+int covt_decode_zigzag_varint(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t num_values, int32_t* out);
+/* DecodingUtils.decodeZigZagDeltaVarint(byte[], IntWrapper, int)                  DecodingUtils.java:55 */
+int covt_decode_zigzag_delta_varint(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t num_values,
+                                    int32_t* out);
+/* DecodingUtils.decodeZigZagDeltaVarintCoordinates(byte[], IntWrapper, int)       DecodingUtils.java:95 */
+int covt_decode_zigzag_delta_varint_coordinates(const uint8_t* buf, size_t buf_len, int32_t* pos,
+                                                int32_t num_values, int32_t* out);
+/* DecodingUtils.decodeRle(byte[], int numValues, IntWrapper, boolean signed)      DecodingUtils.java:257
+ * *pos advances by the bytes the RLE reader consumed; for ORC-writer-produced streams this equals
+ * the Java advance (the length of the re-encoding, :268-270, :308-310). */
+int covt_decode_rle(const uint8_t* buf, size_t buf_len, int32_t num_values, int32_t* pos, int32_t is_signed,
+                    int64_t* out);
+/* DecodingUtils.decodeByteRle(byte[], int numValues, IntWrapper, int byteLength)  DecodingUtils.java:275 */
+int covt_decode_byte_rle(const uint8_t* buf, size_t buf_len, int32_t num_values, int32_t* pos, int32_t byte_length,
+                         uint8_t* out);
+/* DecodingUtils.decodeFastPfor128ZigZagDelta(byte[], int, int byteLength, IntWrapper) DecodingUtils.java:316 */
+int covt_decode_fastpfor_zigzag_delta(const uint8_t* buf, size_t buf_len, int32_t num_values, int32_t byte_length,
+                                      int32_t* pos, int32_t* out);
+/* DecodingUtils.decodeFastPfor128DeltaCoordinates(byte[], int, int, IntWrapper)   DecodingUtils.java:349 */
+int covt_decode_fastpfor_delta_coordinates(const uint8_t* buf, size_t buf_len, int32_t num_values,
+                                           int32_t byte_length, int32_t* pos, int32_t* out);
+/* DecodingUtils.decodeDeltaVarintMortonCodes(byte[], IntWrapper, int numVertices, int numBits)
+ *                                                                                 DecodingUtils.java:394
+ * out holds 2*num_vertices ints (x,y interleaved). */
+int covt_decode_delta_varint_morton_codes(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t num_vertices,
+                                          int32_t num_bits, int32_t* out);
+/* DecodingUtils.decodeFastPfor128DeltaMortonCodes(byte[], int, int, IntWrapper, int numBits)
+ *                                                                                 DecodingUtils.java:411 */
+int covt_decode_fastpfor_delta_morton_codes(const uint8_t* buf, size_t buf_len, int32_t num_vertices,
+                                            int32_t byte_length, int32_t* pos, int32_t num_bits, int32_t* out);
+
+/* ---------------------------------------------------------------------------
+ * Batch API: the replacement for the per-tile CovtParser.decodeCovt loop
+ * (CovtParser.java:53-133) restricted to the Id and Geometry columns.
+ * ------------------------------------------------------------------------- */
+
+/* Device-side decode operations (one per DecodingUtils codec x output type). */
+enum covt_op {
+    COVT_OP_NONE = 0,
+    COVT_OP_BYTE_RLE_U8 = 1,            /* decodeByteRle -> uint8 (GeometryTypes, values <= 5 checked) */
+    COVT_OP_RLE_U64 = 2,                /* decodeRle(signed=false) -> int64 (Id) */
+    COVT_OP_RLE_I32 = 3,                /* decodeRle(signed=false) then (int) -> int32 (topology counts) */
+    COVT_OP_RLE_S64 = 4,                /* decodeRle(signed=true) -> int64 */
+    COVT_OP_VARINT_I32 = 5,             /* decodeVarint -> int32 */
+    COVT_OP_VARINT_ZZ_I32 = 6,          /* decodeZigZagVarint -> int32 */
+    COVT_OP_VARINT_ZZ_DELTA_I32 = 7,    /* decodeZigZagDeltaVarint -> int32 (VertexOffsets) */
+    COVT_OP_VARINT_ZZ_DELTA_XY = 8,     /* decodeZigZagDeltaVarintCoordinates -> int32 x,y */
+    COVT_OP_VARINT_DELTA_MORTON = 9,    /* decodeDeltaVarintMortonCodes -> int32 x,y per vertex */
+    COVT_OP_FPF_ZZ_DELTA_I32 = 10,      /* decodeFastPfor128ZigZagDelta -> int32 */
+    COVT_OP_FPF_ZZ_DELTA_XY = 11,       /* decodeFastPfor128DeltaCoordinates -> int32 x,y */
+    COVT_OP_FPF_DELTA_MORTON = 12,      /* decodeFastPfor128DeltaMortonCodes -> int32 x,y per vertex */
+    COVT_OP_VARINT_U64 = 13,            /* Id VARINT, format truth: 64-bit LEB128 -> int64 */
+    COVT_OP_VARINT_I32_AS_I64 = 14,     /* Id VARINT, Java: decodeVarint then (long) */
+    COVT_OP_VARINT_ZZ_DELTA_I64 = 15,   /* Id enc 4, Java: decodeZigZagDeltaVarint then (long) */
+    COVT_OP_COUNT = 16
+};
+
+/* One device-resident plan entry (32 bytes). */
+typedef struct covt_stream_desc {
+    uint64_t in_off;     /* payload byte offset in the batch input buffer */
+    uint64_t out_off;    /* output byte offset in the batch output buffer (16-byte aligned) */
+    int32_t avail;       /* readable payload bytes (byteLength for plans; buf_len-pos for stream calls) */
+    int32_t num_values;  /* values (vertices for the Morton ops) to produce */
+    uint8_t op;          /* enum covt_op */
+    uint8_t num_bits;    /* Morton bits, 32 - nlz(extent) (CovtParser.java:77) */
+    uint16_t flags;
+    int32_t byte_length; /* wire byteLength (FastPFOR reads byteLength/4 big-endian words) */
+} covt_stream_desc;
+
+/* Per-stream result written by the kernel. */
+typedef struct covt_stream_result {
+    int32_t status;   /* COVT_OK or a negative COVT_ERR_* */
+    int32_t consumed; /* payload bytes consumed (FastPFOR / byte RLE: byteLength) */
+} covt_stream_result;
+
+/* Host-visible stream record of a plan, in tile order. */
+typedef struct covt_stream_info {
+    int32_t tile, layer, column_kind, stream_type; /* column_kind: 0 id, 1 geometry */
+    int32_t encoding, column_type, num_values, byte_length;
+    int32_t num_bits, op, elem_bytes, desc_index; /* desc_index: row in the launch-ordered descs */
+    int64_t in_off, out_off, out_elems;
+} covt_stream_info;
+
+typedef struct covt_plan covt_plan;
+
+/* Walk the container metadata of n_tiles tiles held back to back in `bytes` (host memory) and
+ * build the descriptor table.  Tiles that fail to walk get a negative tile status and no streams. */
+int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
+                     int32_t n_tiles, int32_t format, int32_t id_mode, covt_plan** out);
+void covt_plan_destroy(covt_plan* plan);
+int64_t covt_plan_num_streams(const covt_plan* plan);
+int64_t covt_plan_output_bytes(const covt_plan* plan);
+/* stream-byte, output-byte and vertex totals over all planned streams */
+int covt_plan_totals(const covt_plan* plan, int64_t* in_bytes, int64_t* out_bytes, int64_t* vertices);
+int covt_plan_streams(const covt_plan* plan, covt_stream_info* out);    /* num_streams records */
+int covt_plan_descs(const covt_plan* plan, covt_stream_desc* out);      /* num_streams, launch order */
+int covt_plan_tile_status(const covt_plan* plan, int32_t* out);         /* n_tiles */
+
+/* Launch the decode of n_streams descriptors on `hip_stream` (a hipStream_t; NULL = default).
+ * d_in: batch bytes on the device (see COVT_INPUT_PADDING); d_desc: descriptors on the device;
+ * d_out: output buffer of covt_plan_output_bytes bytes; d_res: n_streams results.  Asynchronous. */
+int covt_decode_streams_device(const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
+                               uint8_t* d_out, covt_stream_result* d_res, void* hip_stream);
+
+/* Convenience: plan + H2D + decode + D2H for host tiles on the current device.
+ * host_out: covt_plan_output_bytes(plan) bytes; host_res: num_streams results (plan stream order). */
+int covt_plan_decode_host(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_out,
+                          covt_stream_result* host_res);
+
+/* Multi-GPU host entry point: shards the plan's tiles over n_gpus devices by a greedy
+ * byte-balanced split (one host thread per device, no collectives), decodes, and gathers the
+ * outputs into host_out / host_res exactly as covt_plan_decode_host would. */
+int covt_plan_decode_host_multi(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, int32_t n_gpus,
+                                uint8_t* host_out, covt_stream_result* host_res);
+
+/* Library info */
+const char* covt_version(void);
+int covt_device_count(int32_t* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COVT_H */

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Runs GPU steps in sequence on the gpurun box.  Every step has its own time limit; an abort,
+# segfault, time limit or GPU fault ends the session (no further GPU step runs).  Plain test
+# failures (pytest rc 1) do not.
+# usage: tools/gpu_session.sh STEP...   where STEP is one of: tests smoke bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+fatal() { echo "FATAL step=$1 rc=$2"; exit "$2"; }
+step() {  # step NAME LIMIT cmd...
+    local name=$1 lim=$2; shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "   rc=$rc"; tail -n 5 "gpurun_out/$name.log"
+    if grep -q -E "Memory access fault|HSA_STATUS_ERROR|hipErrorIllegalAddress|GPU Hang" "gpurun_out/$name.log"; then fatal "$name" 99; fi
+    case $rc in 0|1|5) ;; *) fatal "$name" "$rc";; esac
+}
+for s in "$@"; do
+    case $s in
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests_all) step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    bench_short) step bench 600 python bench.py --steps 10 --warmup 3 --cpu-seconds 8 ;;
+    prof) step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
+    pmc_fetch) step rocprof_pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    pmc_write) step rocprof_pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo "session done"
