@@ -1,0 +1,130 @@
+"""CPU: the C-ABI library loads, exports every entry point include/covt.h declares, and its host-side
+container walk (the plan) agrees with the oracle's walk on every fixture.  No compute calls: the
+decode entry points need a GPU and must fail loudly (never fall back to the CPU) without one."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, tile_key, tile_paths
+
+
+def declared_symbols():
+    hdr = open(os.path.join(ROOT, "include", "covt.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(covt_[a-z0-9_]+)\s*\(", hdr)))
+
+
+def test_header_symbols_exported(covt):
+    so = os.path.join(ROOT, "cov-tiles_amd", "libcovt.so")
+    assert os.path.exists(so), "run __graft_entry__.build()"
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (covt_\w+)", out))
+    decl = declared_symbols()
+    assert len(decl) >= 23
+    missing = [s for s in decl if s not in exported]
+    assert not missing, missing
+    assert set(decl) == set(covt.EXPORTED_SYMBOLS)
+    L = covt.lib()
+    for s in decl:
+        assert hasattr(L, s)
+
+
+def test_kernel_compiled_for_gfx950():
+    """The fat binary embedded in libcovt.so carries a gfx950 code object (and nothing else)."""
+    blob = open(os.path.join(ROOT, "cov-tiles_amd", "libcovt.so"), "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"gfx942" not in blob and b"gfx90a" not in blob
+
+
+def test_struct_layouts(covt):
+    import ctypes as C
+
+    assert C.sizeof(covt.StreamDesc) == 32
+    assert C.sizeof(covt.StreamResult) == 8
+    assert C.sizeof(covt.StreamInfo) == 72
+
+
+@pytest.mark.parametrize("fmt_mode", [(0, 0), (0, 1)])
+def test_plan_matches_oracle_walk(covt, oracle, fmt_mode):
+    fmt, id_mode = fmt_mode
+    paths = tile_paths()
+    tiles = [open(p, "rb").read() for p in paths]
+    plan = covt.Plan.from_tiles(tiles, fmt, id_mode)
+    st = plan.streams
+    assert plan.num_streams == len(st)
+    # descriptor table is a permutation of the streams, largest first
+    di = np.sort(st["desc_index"])
+    assert np.array_equal(di, np.arange(plan.num_streams))
+    descs = plan.descs.view(np.uint8).reshape(-1, 32)
+    for t, p in enumerate(paths):
+        ost, oss = oracle.walk_tile(tiles[t])
+        assert (plan.tile_status[t] == 0) == (ost == 0), tile_key(p)
+        idx = np.nonzero(st["tile"] == t)[0]
+        assert len(idx) == len(oss)
+        for i, s in zip(idx, oss):
+            row = st[i]
+            assert (row["layer"], row["column_kind"], row["stream_type"], row["encoding"], row["column_type"],
+                    row["num_values"], row["byte_length"], row["num_bits"]) == \
+                   (s.layer, s.column_kind, s.stream_type, s.encoding, s.column_type, s.num_values,
+                    s.byte_length, s.num_bits)
+            assert row["in_off"] == int(plan.offsets[t]) + s.offset
+            eb, ne = oracle.stream_output(s, id_mode)
+            if row["op"] != covt.OP_NONE:
+                assert (row["elem_bytes"], row["out_elems"]) == (eb, ne)
+            assert row["out_off"] % 16 == 0
+            d = descs[row["desc_index"]]
+            assert int.from_bytes(d[0:8].tobytes(), "little") == row["in_off"]
+            assert int.from_bytes(d[8:16].tobytes(), "little") == row["out_off"]
+            assert d[24] == row["op"]
+    # output slices are disjoint and in bounds
+    ends = st["out_off"] + st["out_elems"] * st["elem_bytes"]
+    order = np.argsort(st["out_off"], kind="stable")
+    assert (st["out_off"][order][1:] >= ends[order][:-1]).all()
+    assert ends.max() <= plan.output_bytes
+
+
+def test_plan_op_selection_follows_covtparser_dispatch(covt):
+    """CovtParser.decodeGeometryColumn (:392-511) / decodedIds (:552-572) dispatch table."""
+    t = open(os.path.join(ROOT, "tests", "golden", "tiles", "omt", "5_16_20.covt"), "rb").read()
+    for id_mode, id_ops in ((0, {5: covt.OP_RLE_U64, 1: covt.OP_VARINT_U64, 4: covt.OP_RLE_U64}),
+                            (1, {5: covt.OP_RLE_U64, 1: covt.OP_VARINT_I32_AS_I64, 4: covt.OP_VARINT_ZZ_DELTA_I64})):
+        plan = covt.Plan.from_tiles([t], 0, id_mode)
+        for s in plan.streams:
+            if s["column_kind"] == 0:
+                assert s["op"] == id_ops[int(s["encoding"])]
+            elif s["stream_type"] == 4:
+                assert s["op"] == covt.OP_BYTE_RLE_U8
+            elif s["stream_type"] in (5, 6, 7):
+                assert s["op"] == {5: covt.OP_RLE_I32, 9: covt.OP_FPF_ZZ_DELTA_I32}[int(s["encoding"])]
+            elif s["stream_type"] == 8:
+                assert s["op"] == {4: covt.OP_VARINT_ZZ_DELTA_I32, 9: covt.OP_FPF_ZZ_DELTA_I32}[int(s["encoding"])]
+            elif s["column_type"] == 4:
+                assert s["op"] == {4: covt.OP_VARINT_DELTA_MORTON, 9: covt.OP_FPF_DELTA_MORTON}[int(s["encoding"])]
+            else:
+                assert s["op"] == {4: covt.OP_VARINT_ZZ_DELTA_XY, 9: covt.OP_FPF_ZZ_DELTA_XY}[int(s["encoding"])]
+
+
+def test_plan_rejects_truncated_and_garbage(covt):
+    t = open(os.path.join(ROOT, "tests", "golden", "tiles", "omt", "5_16_20.covt"), "rb").read()
+    rng = np.random.default_rng(5)
+    tiles = [t[:len(t) // 2], t[:100], b"", bytes(rng.integers(0, 256, size=3000).astype(np.uint8)), t]
+    plan = covt.Plan.from_tiles(tiles)
+    assert (plan.tile_status[:4] != 0).all() and plan.tile_status[4] == 0
+    assert set(np.unique(plan.streams["tile"])) == {4}
+
+
+def test_no_cpu_fallback_without_gpu(covt):
+    """The product path raises when no device is usable; it never decodes on the CPU."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(covt.CovtError):
+        covt.DecodingUtils.decodeVarint(b"\x01\x02", covt.IntWrapper(0), 2)
+    plan = covt.Plan.from_tiles([open(os.path.join(ROOT, "tests", "golden", "tiles", "omt", "2_2_2.covt"),
+                                      "rb").read()])
+    with pytest.raises(covt.CovtError):
+        plan.decode_host()
