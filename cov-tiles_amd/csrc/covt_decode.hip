@@ -35,22 +35,28 @@ constexpr int kFpfPage = 65536;
 constexpr int kFpfBcCap = 3 * kFpfPage / kFpfBlock + kFpfPage;  // JavaFastPFOR byteContainer size
 constexpr int kBlkBatch = 64;
 
+constexpr int kMaxGroups = 256;  // RLE groups recorded per window walk
+
 struct __attribute__((aligned(16))) WaveSmem {
     union {
         struct {
-            uint32_t win[kWin / 4 + 4];  // window bytes (+16 B slack for 12-byte reads)
-            uint16_t list[kWin];         // terminator positions (window-relative)
+            uint32_t win[kWin / 4 + 4];    // window bytes (+16 B slack for 12-byte reads)
+            uint16_t list[kWin];           // terminator positions (window-relative)
+            uint16_t next[kWin];           // RLE: start of the next group if a header sat at j
+            uint16_t gstart[kMaxGroups];   // RLE: group starts found by the chain walk
         } v;
         struct {
-            uint32_t stage[324];  // packed words of one FastPFOR block (<= 1024 + 15 B)
-            uint32_t patch[256];  // exception patches of one block
+            uint32_t stage[324];          // packed words of one FastPFOR block (<= 1024 + 15 B)
+            uint32_t patch[256];          // exception patches of one block
+            uint32_t blk[4 * kBlkBatch];  // block records: {b|c<<8|idx<<16, bcoff, xcur, pk}
         } f;
     } u;
-    uint32_t blk[4 * kBlkBatch];  // FastPFOR block records: {b|c<<8|idx<<16, bcoff, xcur, pk}
     uint32_t xstart[33];
     int32_t xsize[33];
     uint32_t xcnt[33];
     int32_t misc[4];
+    uint16_t cpre[64];   // window index: terminators before each 16-byte chunk
+    uint16_t cmask[64];  // window index: terminator mask of each chunk
 };
 
 // --------------------------------------------------------------------------------------------
@@ -66,14 +72,15 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
-// inclusive prefix sum over the 64 lanes (wrapping uint32)
+// inclusive prefix sum over the 64 lanes (wrapping uint32): DPP row shifts within 16-lane rows,
+// then row broadcasts 15 and 31 across rows (the GFX9 wave64 scan sequence, no LDS traffic)
 __device__ __forceinline__ uint32_t incl_scan(uint32_t x) {
-    const int l = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-        if (l >= o) x += y;
-    }
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return x;
 }
 
@@ -253,35 +260,18 @@ __device__ __forceinline__ void sink_values(int op, const uint32_t (&v)[K], int6
 }
 
 // --------------------------------------------------------------------------------------------
-// the 1 KiB window and the varint machinery
+// the 1 KiB indexed window and the varint machinery
 // --------------------------------------------------------------------------------------------
-enum { MODE_RAW = 0, MODE_WORDREV = 1 };             // byte order of the window
+enum { MODE_RAW = 0, MODE_WORDREV = 1 };                           // byte order of the window
 enum { VAL_J4 = 0, VAL_VB = 1, VAL_U64 = 2, VAL_U64_STRICT = 3 };  // value grammar
 
+// A window holds 1 KiB of the stream in LDS (and each lane's 16 bytes in registers) plus an index
+// of its value terminators: list[] = window-relative positions of every terminator byte in the
+// valid range, cpre/cmask = per-16-byte-chunk prefix counts and masks, so rank(q) (terminators
+// before q) is O(1) and a run of values starting at any value boundary is list[rank(q) ...].
 // RAW: window byte j = stream byte woff + j, woff = ((sb + p) & ~15) - sb.
 // WORDREV: window byte j = logical byte woff + j of the VariableByte sequence, i.e. the LE bytes of
 // the big-endian words W[i] (DecodingUtils.java:319-327); woff is a multiple of 16.
-template <int MODE>
-__device__ __forceinline__ int32_t win_fill(WaveSmem& sm, const uint8_t* sb, int32_t p, uint4& d) {
-    const int l = lane_id();
-    int32_t woff;
-    if (MODE == MODE_RAW) {
-        const uintptr_t a = ((uintptr_t)(sb + p)) & ~(uintptr_t)15;
-        woff = (int32_t)((intptr_t)a - (intptr_t)sb);
-        d = ((const uint4*)a)[l];
-    } else {
-        woff = p & ~15;
-        const uint8_t* w = sb + woff + 16 * l;
-        d.x = ld_be32(w);
-        d.y = ld_be32(w + 4);
-        d.z = ld_be32(w + 8);
-        d.w = ld_be32(w + 12);
-    }
-    ((uint4*)sm.u.v.win)[l] = d;
-    wave_sync();
-    return uni(woff);
-}
-
 __device__ __forceinline__ uint32_t win_byte(const WaveSmem& sm, int32_t j) {
     return (sm.u.v.win[j >> 2] >> (8 * (j & 3))) & 0xffu;
 }
@@ -296,72 +286,130 @@ __device__ __forceinline__ void win_bytes12(const WaveSmem& sm, int32_t j, uint3
     x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
 }
 
-// Decode up to `want` values starting at stream position `pos` (updated) with bytes valid in
-// [pos, end).  emit(lo, hi, base, count) is called per group of <=64 values, one per lane.
-// Returns the number of values decoded.  With `until_end` (VariableByte tail) the region is
+struct Win {
+    int32_t woff;  // stream-relative position of window byte 0
+    int32_t K;     // terminators indexed
+    int32_t p0;    // J4 serial windows: list[] starts at value boundary p0 (rank(p0) = 0)
+    bool valid, serial;
+    uint4 d;             // this lane's 16 window bytes
+    uint32_t cpre, cmsk; // this lane's chunk: terminators before it, terminator mask
+};
+
+template <int MODE, int VAL>
+__device__ void win_load(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t p, int32_t end) {
+    const int l = lane_id();
+    uint4 d;
+    int32_t woff;
+    if (MODE == MODE_RAW) {
+        const uintptr_t a = ((uintptr_t)(sb + p)) & ~(uintptr_t)15;
+        woff = uni((int32_t)((intptr_t)a - (intptr_t)sb));
+        d = ((const uint4*)a)[l];
+    } else {
+        woff = p & ~15;
+        const uint8_t* q = sb + woff + 16 * l;
+        d.x = ld_be32(q);
+        d.y = ld_be32(q + 4);
+        d.z = ld_be32(q + 8);
+        d.w = ld_be32(q + 12);
+    }
+    ((uint4*)sm.u.v.win)[l] = d;
+    const int32_t q0 = woff + 16 * l;
+    const uint32_t V = range16((VAL == VAL_J4 ? p : 0) - q0, end - q0);  // J4 indexes from p only
+    const uint32_t H = hibits16(d);
+    uint32_t T = (VAL == VAL_VB) ? (V & H) : (V & ~H);
+    bool serial = false;
+    if (VAL == VAL_J4) {
+        // a run of four continuation bytes changes the capped grammar: parse serially
+        const uint32_t N = V & ~T;
+        uint32_t prevN = (uint32_t)__shfl_up((int)N, 1, 64);
+        if (l == 0) prevN = 0;
+        const uint32_t ext = (N << 3) | ((prevN >> 13) & 7u);
+        serial = __any((ext & (ext >> 1) & (ext >> 2) & (ext >> 3)) != 0);
+    }
+    int32_t K;
+    if (!serial) {
+        const uint32_t cnt = __popc(T);
+        const uint32_t inc = incl_scan(cnt);
+        uint32_t idx = inc - cnt;
+        sm.cpre[l] = (uint16_t)idx;
+        sm.cmask[l] = (uint16_t)T;
+        w.cpre = idx;
+        w.cmsk = T;
+        while (T) {
+            const int k = __ffs(T) - 1;
+            T &= T - 1;
+            sm.u.v.list[idx++] = (uint16_t)(16 * l + k);
+        }
+        K = (int32_t)lane_bcast(inc, 63);
+    } else {
+        wave_sync();
+        if (l == 0) {  // DecodingUtils.java:157-186, one value at a time from p
+            const int32_t lim = (end < woff + kWin ? end : woff + kWin) - woff;
+            int32_t j = p - woff, k = 0;
+            while (j < lim) {
+                int32_t len = 0;
+                bool done = false;
+                for (int b = 0; b < 4; ++b) {
+                    if (j + b >= lim) break;
+                    ++len;
+                    if (b == 3 || (win_byte(sm, j + b) & 0x80u) == 0) { done = true; break; }
+                }
+                if (!done) break;
+                sm.u.v.list[k++] = (uint16_t)(j + len - 1);
+                j += len;
+            }
+            sm.misc[0] = k;
+        }
+        wave_sync();
+        K = uni(sm.misc[0]);
+    }
+    wave_sync();
+    w.d = d;
+    w.woff = woff;
+    w.K = K;
+    w.p0 = p;
+    w.valid = true;
+    w.serial = serial || VAL == VAL_J4;
+}
+
+// terminators of the window before stream position q (q inside the window)
+__device__ __forceinline__ int32_t win_rank(const WaveSmem& sm, const Win& w, int32_t q) {
+    const int32_t j = q - w.woff;
+    if (j <= 0) return 0;
+    if (j >= kWin) return w.K;
+    const int32_t c = j >> 4;
+    return (int32_t)uniu((uint32_t)sm.cpre[c] + __popc((uint32_t)sm.cmask[c] & ((1u << (j & 15)) - 1u)));
+}
+
+// Decode up to `want` values starting at stream position `pos` (a value boundary; updated) with
+// bytes valid in [pos, end).  emit(lo, hi, base, count) is called per group of <=64 values, one per
+// lane.  Returns the number of values decoded.  With `until_end` (VariableByte tail) the region is
 // decoded to its end, a trailing partial value is dropped and more than `want` values is an error.
 template <int MODE, int VAL, class Emit>
-__device__ int32_t varint_run(WaveSmem& sm, const uint8_t* sb, int32_t& pos, int32_t end, int32_t want,
-                              bool until_end, int32_t& err, Emit&& emit) {
+__device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t& pos, int32_t end, int32_t want,
+                               bool until_end, int32_t& err, Emit&& emit) {
     const int l = lane_id();
     int32_t got = 0;
     while (until_end ? (pos < end) : (got < want)) {
-        uint4 d;
-        const int32_t woff = win_fill<MODE>(sm, sb, pos, d);
-        const int32_t q0 = woff + 16 * l;
-        const uint32_t V = range16(pos - q0, end - q0);
-        const uint32_t H = hibits16(d);
-        uint32_t T = (VAL == VAL_VB) ? (V & H) : (V & ~H);
-        int32_t K;
-        bool serial = false;
-        if (VAL == VAL_J4) {
-            // a run of four continuation bytes changes the capped grammar: parse serially
-            const uint32_t N = V & ~T;
-            uint32_t prevN = (uint32_t)__shfl_up((int)N, 1, 64);
-            if (l == 0) prevN = 0;
-            const uint32_t ext = (N << 3) | ((prevN >> 13) & 7u);
-            serial = __any((ext & (ext >> 1) & (ext >> 2) & (ext >> 3)) != 0);
-        }
-        if (!serial) {
-            const uint32_t cnt = __popc(T);
-            const uint32_t inc = incl_scan(cnt);
-            uint32_t idx = inc - cnt;
-            while (T) {
-                const int k = __ffs(T) - 1;
-                T &= T - 1;
-                sm.u.v.list[idx++] = (uint16_t)(16 * l + k);
+        if (!w.valid || pos < w.woff || pos >= w.woff + kWin || (w.serial && pos != w.p0))
+            win_load<MODE, VAL>(sm, sb, w, pos, end);
+        const int32_t r = w.serial ? 0 : win_rank(sm, w, pos);
+        const int32_t have = w.K - r;
+        if (have <= 0) {
+            const int32_t aligned = (MODE == MODE_RAW) ? (int32_t)(((uintptr_t)(sb + pos) & ~(uintptr_t)15) -
+                                                                   (uintptr_t)sb)
+                                                       : (pos & ~15);
+            if (w.woff != aligned) {  // the value straddles the window end: reload at pos
+                win_load<MODE, VAL>(sm, sb, w, pos, end);
+                continue;
             }
-            K = (int32_t)lane_bcast(inc, 63);
-        } else {
-            if (l == 0) {  // DecodingUtils.java:157-186, one value at a time
-                const int32_t lim = (end < woff + kWin ? end : woff + kWin) - woff;
-                int32_t j = pos - woff, k = 0;
-                while (j < lim) {
-                    int32_t len = 0;
-                    bool done = false;
-                    for (int b = 0; b < 4; ++b) {
-                        if (j + b >= lim) break;
-                        ++len;
-                        if (b == 3 || (win_byte(sm, j + b) & 0x80u) == 0) { done = true; break; }
-                    }
-                    if (!done) break;
-                    sm.u.v.list[k++] = (uint16_t)(j + len - 1);
-                    j += len;
-                }
-                sm.misc[0] = k;
-            }
-            wave_sync();
-            K = uni(sm.misc[0]);
-        }
-        wave_sync();
-        if (K == 0) {
             if (until_end) break;  // VariableByte: trailing partial value is dropped
-            err = (woff + kWin >= end) ? COVT_ERR_TRUNCATED : COVT_ERR_BAD_HEADER;
+            err = (w.woff + kWin >= end) ? COVT_ERR_TRUNCATED : COVT_ERR_BAD_HEADER;
             break;
         }
-        int32_t take = K;
+        int32_t take = have;
         if (until_end) {
-            if (got + K > want) { err = COVT_ERR_COUNT_MISMATCH; take = want - got; }
+            if (got + have > want) { err = COVT_ERR_COUNT_MISMATCH; take = want - got; }
         } else if (take > want - got) {
             take = want - got;
         }
@@ -371,8 +419,8 @@ __device__ int32_t varint_run(WaveSmem& sm, const uint8_t* sb, int32_t& pos, int
             const int32_t vi = g + l;
             uint32_t lo = 0, hi = 0;
             if (vi < take) {
-                const int32_t ej = sm.u.v.list[vi];
-                const int32_t sj = (vi == 0) ? (pos - woff) : (int32_t)sm.u.v.list[vi - 1] + 1;
+                const int32_t ej = sm.u.v.list[r + vi];
+                const int32_t sj = (vi == 0) ? (pos - w.woff) : (int32_t)sm.u.v.list[r + vi - 1] + 1;
                 const int32_t len = ej - sj + 1;
                 uint32_t x0, x1, x2;
                 win_bytes12(sm, sj, x0, x1, x2);
@@ -388,27 +436,27 @@ __device__ int32_t varint_run(WaveSmem& sm, const uint8_t* sb, int32_t& pos, int
                         lo = vv;
                     }
                 } else {
-                    uint64_t r;
+                    uint64_t rv;
                     if (len <= 10) {
                         const uint32_t m0 = x0 & bytemask(len), m1 = x1 & bytemask(len - 4),
                                        m2 = x2 & bytemask(len - 8);
-                        r = (uint64_t)pext7(m0) | ((uint64_t)pext7(m1) << 28) | ((uint64_t)(m2 & 0x7fu) << 56) |
-                            ((uint64_t)((m2 >> 8) & 0x7fu) << 63);
+                        rv = (uint64_t)pext7(m0) | ((uint64_t)pext7(m1) << 28) | ((uint64_t)(m2 & 0x7fu) << 56) |
+                             ((uint64_t)((m2 >> 8) & 0x7fu) << 63);
                     } else {  // orc readVulong: shift masked to 6 bits
-                        r = 0;
-                        for (int b = 0; b < len; ++b) r |= (uint64_t)(win_byte(sm, sj + b) & 0x7fu) << ((7 * b) & 63);
+                        rv = 0;
+                        for (int b = 0; b < len; ++b) rv |= (uint64_t)(win_byte(sm, sj + b) & 0x7fu) << ((7 * b) & 63);
                         lerr = true;
                     }
-                    lo = (uint32_t)r;
-                    hi = (uint32_t)(r >> 32);
+                    lo = (uint32_t)rv;
+                    hi = (uint32_t)(rv >> 32);
                 }
             }
             emit(lo, hi, got + g, take - g < 64 ? take - g : 64);
         }
         if (VAL == VAL_U64_STRICT && __any(lerr) && !err) err = COVT_ERR_BAD_HEADER;
-        pos = woff + (int32_t)uni(sm.u.v.list[take - 1]) + 1;
+        pos = w.woff + (int32_t)uniu(sm.u.v.list[r + take - 1]) + 1;
+        if (w.serial) { w.p0 = pos; w.valid = false; }  // serial lists are only valid from p0
         got += take;
-        wave_sync();
         if (err) break;
     }
     return got;
@@ -425,136 +473,291 @@ struct Ctx {
     int32_t err, consumed;
 };
 
-// byte of the stream through the window (refilled on demand); wave-uniform
-__device__ __forceinline__ uint32_t rd_byte(Ctx& c, int32_t& woff, int32_t q) {
-    if (q < woff || q >= woff + kWin) {
-        uint4 d;
-        woff = win_fill<MODE_RAW>(*c.sm, c.sb, q, d);
-    }
-    return uniu(win_byte(*c.sm, q - woff));
+// byte q of the stream through the window (loaded on demand so that [q, q + need) is inside
+// the window unless the stream ends first); wave-uniform
+template <int VAL>
+__device__ __forceinline__ uint32_t rd_byte(Ctx& c, Win& w, int32_t q, int32_t need = 1) {
+    if (!w.valid || q < w.woff || (q + need > w.woff + kWin && w.woff + kWin < c.avail))
+        win_load<MODE_RAW, VAL>(*c.sm, c.sb, w, q, c.avail);
+    return uniu(win_byte(*c.sm, q - w.woff));
 }
 
 __device__ void run_varint_stream(Ctx& c) {
     int32_t pos = 0;
     Carry cr{0, 0};
+    Win w;
+    w.valid = false;
     auto sink1 = [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
         uint32_t v[1] = {lo};
         sink_values<1>(c.op, v, base, count, c.nb, c.out, cr);
     };
     if (c.op == COVT_OP_VARINT_U64) {
         int64_t* o = (int64_t*)c.out;
-        varint_run<MODE_RAW, VAL_U64_STRICT>(*c.sm, c.sb, pos, c.avail, c.n, false, c.err,
-                                             [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
-                                                 if (lane_id() < count)
-                                                     o[base + lane_id()] = (int64_t)(((uint64_t)hi << 32) | lo);
-                                             });
+        varint_take<MODE_RAW, VAL_U64_STRICT>(*c.sm, c.sb, w, pos, c.avail, c.n, false, c.err,
+                                              [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
+                                                  if (lane_id() < count)
+                                                      o[base + lane_id()] = (int64_t)(((uint64_t)hi << 32) | lo);
+                                              });
     } else {
         if ((c.op == COVT_OP_VARINT_ZZ_DELTA_XY) && (c.n & 1)) {
             // Java decodes the x,y pair and then overruns values[] (ArrayIndexOutOfBounds)
-            varint_run<MODE_RAW, VAL_J4>(*c.sm, c.sb, pos, c.avail, c.n - 1, false, c.err, sink1);
+            varint_take<MODE_RAW, VAL_J4>(*c.sm, c.sb, w, pos, c.avail, c.n - 1, false, c.err, sink1);
             if (!c.err) c.err = COVT_ERR_COUNT_MISMATCH;
         } else {
-            varint_run<MODE_RAW, VAL_J4>(*c.sm, c.sb, pos, c.avail, c.n, false, c.err, sink1);
+            varint_take<MODE_RAW, VAL_J4>(*c.sm, c.sb, w, pos, c.avail, c.n, false, c.err, sink1);
         }
     }
     c.consumed = pos;
 }
 
-// ORC RLE v1 integer reader (RunLengthIntegerReader.readValues / next)
+// terminators before window-relative position j (per lane, j in [0, kWin])
+__device__ __forceinline__ int32_t rank_rel(const WaveSmem& sm, int32_t j, int32_t K) {
+    if (j >= kWin) return K;
+    const int32_t c = j >> 4;
+    return (int32_t)sm.cpre[c] + __popc((uint32_t)sm.cmask[c] & ((1u << (j & 15)) - 1u));
+}
+// 64-bit LEB128 value in window bytes [sj, ej] (orc SerializationUtils.readVulong)
+__device__ __forceinline__ uint64_t win_vulong(const WaveSmem& sm, int32_t sj, int32_t ej) {
+    const int32_t len = ej - sj + 1;
+    if (len <= 10) {
+        uint32_t x0, x1, x2;
+        win_bytes12(sm, sj, x0, x1, x2);
+        const uint32_t m0 = x0 & bytemask(len), m1 = x1 & bytemask(len - 4), m2 = x2 & bytemask(len - 8);
+        return (uint64_t)pext7(m0) | ((uint64_t)pext7(m1) << 28) | ((uint64_t)(m2 & 0x7fu) << 56) |
+               ((uint64_t)((m2 >> 8) & 0x7fu) << 63);
+    }
+    uint64_t r = 0;  // shift masked to 6 bits
+    for (int b = 0; b < len; ++b) r |= (uint64_t)(win_byte(sm, sj + b) & 0x7fu) << ((7 * b) & 63);
+    return r;
+}
+
+// ORC RLE v1 integer reader (RunLengthIntegerReader.readValues / next).
+// Per 1 KiB window: (1) every byte position j computes, from the terminator index, where the next
+// group would start if a header sat at j (run: after the base varint at j+2; literal: after the
+// (256-c)-th varint from j+1) -- fully lane-parallel; (2) one wave-uniform walk follows that chain
+// (one LDS read per group) and records the group starts; (3) groups expand lane-parallel: small
+// groups one per lane, groups of more than 8 values with the whole wave.
 __device__ void run_rle_int(Ctx& c) {
+    WaveSmem& sm = *c.sm;
     const int l = lane_id();
     const bool is_signed = c.op == COVT_OP_RLE_S64;
     const bool to_i32 = c.op == COVT_OP_RLE_I32;
-    int32_t woff = INT32_MIN / 2;
+    Win w;
+    w.valid = false;
     int32_t pos = 0, done = 0;
     auto store = [&](int64_t i, uint64_t raw) {
         const int64_t v = is_signed ? zz64(raw) : (int64_t)raw;
         if (to_i32) ((int32_t*)c.out)[i] = (int32_t)v;
         else ((int64_t*)c.out)[i] = v;
     };
-    while (done < c.n) {
+    while (done < c.n && !c.err) {
         if (pos >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
-        const uint32_t ctl = rd_byte(c, woff, pos);
-        if (ctl < 0x80u) {
-            const int32_t cnt = (int32_t)ctl + 3;
-            if (pos + 1 >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
-            const int32_t delta = (int32_t)(int8_t)rd_byte(c, woff, pos + 1);
-            // base varint (readVulong / readVslong)
-            int32_t q = pos + 2;
-            uint64_t base = 0;
-            uint32_t b;
-            int sh = 0;
-            do {
-                if (q >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
-                b = rd_byte(c, woff, q++);
-                base |= (uint64_t)(b & 0x7fu) << (sh & 63);
-                sh += 7;
-            } while (b >= 0x80u);
-            if (c.err) break;
-            pos = q;
-            const int64_t b64 = is_signed ? zz64(base) : (int64_t)base;
-            const int32_t take = cnt < c.n - done ? cnt : c.n - done;
-            for (int32_t i = l; i < take; i += 64) {  // literals[0] + used * delta
-                const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
-                if (to_i32) ((int32_t*)c.out)[done + i] = (int32_t)v;
-                else ((int64_t*)c.out)[done + i] = v;
+        win_load<MODE_RAW, VAL_U64>(sm, c.sb, w, pos, c.avail);
+        const int32_t woff = w.woff, K = w.K;
+        const int32_t jlo = pos - woff;
+        const int32_t vend = (c.avail - woff) < kWin ? (c.avail - woff) : kWin;  // valid window end
+        // (1) next[] for this lane's 16 positions
+        {
+            const uint32_t ncpre = (uint32_t)__shfl_down((int)w.cpre, 1, 64);
+            const uint32_t ncmsk = (uint32_t)__shfl_down((int)w.cmsk, 1, 64);
+            auto rank = [&](int32_t j) -> int32_t {  // j in [16l, 16l + 32)
+                if (j >= kWin) return K;
+                const uint32_t pre = (j >> 4) == l ? w.cpre : ncpre;
+                const uint32_t msk = (j >> 4) == l ? w.cmsk : ncmsk;
+                return (int32_t)pre + __popc(msk & ((1u << (j & 15)) - 1u));
+            };
+            const uint32_t dw[4] = {w.d.x, w.d.y, w.d.z, w.d.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int32_t j = 16 * l + k;
+                uint32_t nx = 0xffffu;
+                if (j >= jlo && j < vend) {
+                    const uint32_t cb = (dw[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                    if (cb < 0x80u) {
+                        if (j + 2 < vend) {
+                            const int32_t r = rank(j + 2);
+                            if (r < K) nx = (uint32_t)sm.u.v.list[r] + 1u;
+                        }
+                    } else {
+                        const int32_t r = rank(j + 1), nn = 0x100 - (int32_t)cb;
+                        if (j + 1 < vend && r + nn <= K) nx = (uint32_t)sm.u.v.list[r + nn - 1] + 1u;
+                    }
+                }
+                sm.u.v.next[j] = (uint16_t)nx;
             }
-            done += take;
-        } else {
-            const int32_t cnt = 0x100 - (int32_t)ctl;
-            pos += 1;
-            const int32_t lim = c.n - done;
-            const int32_t d0 = done;
-            varint_run<MODE_RAW, VAL_U64>(*c.sm, c.sb, pos, c.avail, cnt, false, c.err,
-                                          [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
-                                              const int32_t k = base + l;
-                                              if (l < count && k < lim) store(d0 + k, ((uint64_t)hi << 32) | lo);
-                                          });
-            woff = INT32_MIN / 2;  // the window moved
-            if (c.err) break;
-            done += cnt < lim ? cnt : lim;
         }
+        wave_sync();
+        // (2) chain walk
+        int32_t pj = jlo, G = 0, out = done;
+        while (out < c.n && G < kMaxGroups && pj < vend) {
+            const uint32_t nx = uniu(sm.u.v.next[pj]);
+            if (nx == 0xffffu) break;
+            const uint32_t cb = uniu(win_byte(sm, pj));
+            if (l == 0) sm.u.v.gstart[G] = (uint16_t)pj;
+            ++G;
+            out += cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb;
+            pj = (int32_t)nx;
+        }
+        wave_sync();
+        if (G == 0) {
+            // the group at pos does not complete inside this window
+            const uint32_t cb = uniu(win_byte(sm, jlo));
+            const int32_t aligned = (int32_t)(((uintptr_t)(c.sb + pos) & ~(uintptr_t)15) - (uintptr_t)c.sb);
+            if (cb >= 0x80u && woff == aligned && woff + kWin < c.avail) {
+                // a literal group longer than a window (up to 128 x 10 B): multi-window varint path
+                const int32_t cnt = 0x100 - (int32_t)cb, lim = c.n - done, d0 = done;
+                pos += 1;
+                varint_take<MODE_RAW, VAL_U64>(sm, c.sb, w, pos, c.avail, cnt, false, c.err,
+                                               [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
+                                                   const int32_t k = base + l;
+                                                   if (l < count && k < lim) store(d0 + k, ((uint64_t)hi << 32) | lo);
+                                               });
+                done += cnt < lim ? cnt : lim;
+                continue;
+            }
+            c.err = (woff + kWin >= c.avail) ? COVT_ERR_TRUNCATED : COVT_ERR_BAD_HEADER;
+            break;
+        }
+        // (3) expansion
+        int32_t base_out = done;
+        for (int32_t gb = 0; gb < G; gb += 64) {
+            const int32_t g = gb + l;
+            const bool gv = g < G;
+            const int32_t pg = gv ? (int32_t)sm.u.v.gstart[g] : 0;
+            const uint32_t cb = gv ? win_byte(sm, pg) : 0u;
+            const int32_t cnt = !gv ? 0 : (cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb);
+            const uint32_t inc = incl_scan((uint32_t)cnt);
+            const int32_t goff = base_out + (int32_t)(inc - (uint32_t)cnt);
+            int32_t take = c.n - goff;
+            take = take < 0 ? 0 : (take > cnt ? cnt : take);
+            const bool big = take > 8;
+            if (gv && !big && take > 0) {
+                if (cb < 0x80u) {
+                    const int32_t delta = (int32_t)(int8_t)win_byte(sm, pg + 1);
+                    const int32_t r = rank_rel(sm, pg + 2, K);
+                    const uint64_t raw = win_vulong(sm, pg + 2, sm.u.v.list[r]);
+                    const int64_t b64 = is_signed ? zz64(raw) : (int64_t)raw;
+                    for (int32_t i = 0; i < take; ++i) {
+                        const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
+                        if (to_i32) ((int32_t*)c.out)[goff + i] = (int32_t)v;
+                        else ((int64_t*)c.out)[goff + i] = v;
+                    }
+                } else {
+                    const int32_t r = rank_rel(sm, pg + 1, K);
+                    int32_t sj = pg + 1;
+                    for (int32_t i = 0; i < take; ++i) {
+                        const int32_t ej = sm.u.v.list[r + i];
+                        store(goff + i, win_vulong(sm, sj, ej));
+                        sj = ej + 1;
+                    }
+                }
+            }
+            uint64_t bigm = __ballot(gv && big);
+            while (bigm) {  // wave-uniform loop over the big groups of this chunk
+                const int src = __ffsll((long long)bigm) - 1;
+                bigm &= bigm - 1;
+                const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
+                const uint32_t c2 = lane_bcast(cb, src);
+                const int32_t o2 = (int32_t)lane_bcast((uint32_t)goff, src);
+                const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
+                if (c2 < 0x80u) {
+                    const int32_t delta = (int32_t)(int8_t)win_byte(sm, p2 + 1);
+                    const int32_t r = rank_rel(sm, p2 + 2, K);
+                    const uint64_t raw = win_vulong(sm, p2 + 2, sm.u.v.list[r]);
+                    const int64_t b64 = is_signed ? zz64(raw) : (int64_t)raw;
+                    for (int32_t i = l; i < t2; i += 64) {  // literals[0] + used * delta
+                        const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
+                        if (to_i32) ((int32_t*)c.out)[o2 + i] = (int32_t)v;
+                        else ((int64_t*)c.out)[o2 + i] = v;
+                    }
+                } else {
+                    const int32_t r = rank_rel(sm, p2 + 1, K);
+                    for (int32_t i = l; i < t2; i += 64) {
+                        const int32_t ej = sm.u.v.list[r + i];
+                        const int32_t sj = i == 0 ? p2 + 1 : (int32_t)sm.u.v.list[r + i - 1] + 1;
+                        store(o2 + i, win_vulong(sm, sj, ej));
+                    }
+                }
+            }
+            base_out += (int32_t)lane_bcast(inc, 63);
+        }
+        done = out < c.n ? out : c.n;
+        pos = woff + pj;
+        wave_sync();
     }
     c.consumed = pos;
 }
 
-// ORC RLE v1 byte reader (RunLengthByteReader); GeometryType.values()[b] range-checked
+// ORC RLE v1 byte reader (RunLengthByteReader); GeometryType.values()[b] range-checked.
+// Same window structure as run_rle_int; a byte-RLE group's length follows from its header byte.
 __device__ void run_rle_byte(Ctx& c) {
+    WaveSmem& sm = *c.sm;
     const int l = lane_id();
-    int32_t woff = INT32_MIN / 2;
+    Win w;
+    w.valid = false;
     int32_t pos = 0, done = 0;
     bool bad = false;
-    while (done < c.n) {
+    while (done < c.n && !c.err) {
         if (pos >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
-        const uint32_t ctl = rd_byte(c, woff, pos);
-        if (ctl < 0x80u) {
-            const int32_t cnt = (int32_t)ctl + 3;
-            if (pos + 1 >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
-            const uint32_t val = rd_byte(c, woff, pos + 1);
-            pos += 2;
-            const int32_t take = cnt < c.n - done ? cnt : c.n - done;
-            for (int32_t i = l; i < take; i += 64) c.out[done + i] = (uint8_t)val;
-            bad |= val > 5u;
-            done += take;
-        } else {
-            const int32_t cnt = 0x100 - (int32_t)ctl;
-            pos += 1;
-            if (pos + cnt > c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
-            if (pos < woff || pos + cnt > woff + kWin) {
-                uint4 d;
-                woff = win_fill<MODE_RAW>(*c.sm, c.sb, pos, d);
-            }
-            const int32_t take = cnt < c.n - done ? cnt : c.n - done;
-            bool lbad = false;
-            for (int32_t i = l; i < take; i += 64) {
-                const uint32_t v = win_byte(*c.sm, pos - woff + i);
-                c.out[done + i] = (uint8_t)v;
-                lbad |= v > 5u;
-            }
-            bad |= __any(lbad);
-            pos += cnt;
-            done += take;
+        win_load<MODE_RAW, VAL_U64>(sm, c.sb, w, pos, c.avail);
+        const int32_t woff = w.woff;
+        const int32_t vend = (c.avail - woff) < kWin ? (c.avail - woff) : kWin;
+        int32_t pj = pos - woff, G = 0, out = done;
+        while (out < c.n && G < kMaxGroups) {
+            const uint32_t cb = uniu(win_byte(sm, pj));
+            const int32_t nx = cb < 0x80u ? pj + 2 : pj + 1 + 0x100 - (int32_t)cb;
+            if (nx > vend) break;
+            if (l == 0) sm.u.v.gstart[G] = (uint16_t)pj;
+            ++G;
+            out += cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb;
+            pj = nx;
+            if (pj >= vend) break;
         }
+        wave_sync();
+        if (G == 0) {
+            c.err = (woff + kWin >= c.avail) ? COVT_ERR_TRUNCATED : COVT_ERR_BAD_HEADER;
+            break;
+        }
+        int32_t base_out = done;
+        bool lbad = false;
+        for (int32_t gb = 0; gb < G; gb += 64) {
+            const int32_t g = gb + l;
+            const bool gv = g < G;
+            const int32_t pg = gv ? (int32_t)sm.u.v.gstart[g] : 0;
+            const uint32_t cb = gv ? win_byte(sm, pg) : 0u;
+            const int32_t cnt = !gv ? 0 : (cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb);
+            const uint32_t inc = incl_scan((uint32_t)cnt);
+            const int32_t goff = base_out + (int32_t)(inc - (uint32_t)cnt);
+            int32_t take = c.n - goff;
+            take = take < 0 ? 0 : (take > cnt ? cnt : take);
+            const bool big = take > 8;
+            if (gv && !big) {
+                for (int32_t i = 0; i < take; ++i) {
+                    const uint32_t v = cb < 0x80u ? win_byte(sm, pg + 1) : win_byte(sm, pg + 1 + i);
+                    c.out[goff + i] = (uint8_t)v;
+                    lbad |= v > 5u;
+                }
+            }
+            uint64_t bigm = __ballot(gv && big);
+            while (bigm) {
+                const int src = __ffsll((long long)bigm) - 1;
+                bigm &= bigm - 1;
+                const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
+                const uint32_t c2 = lane_bcast(cb, src);
+                const int32_t o2 = (int32_t)lane_bcast((uint32_t)goff, src);
+                const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
+                for (int32_t i = l; i < t2; i += 64) {
+                    const uint32_t v = c2 < 0x80u ? win_byte(sm, p2 + 1) : win_byte(sm, p2 + 1 + i);
+                    c.out[o2 + i] = (uint8_t)v;
+                    lbad |= v > 5u;
+                }
+            }
+            base_out += (int32_t)lane_bcast(inc, 63);
+        }
+        bad |= __any(lbad);
+        done = out < c.n ? out : c.n;
+        pos = woff + pj;
+        wave_sync();
     }
     if (!c.err && bad) c.err = COVT_ERR_BAD_HEADER;
     c.consumed = pos;
@@ -654,10 +857,10 @@ __device__ void run_fastpfor(Ctx& c) {
                                 sm.xcnt[idx] = xcur + ce;
                             }
                         }
-                        sm.blk[4 * j + 0] = (uint32_t)b | ((uint32_t)ce << 8) | ((uint32_t)idx << 16);
-                        sm.blk[4 * j + 1] = (uint32_t)bcur;
-                        sm.blk[4 * j + 2] = xcur;
-                        sm.blk[4 * j + 3] = (uint32_t)pk;
+                        sm.u.f.blk[4 * j + 0] = (uint32_t)b | ((uint32_t)ce << 8) | ((uint32_t)idx << 16);
+                        sm.u.f.blk[4 * j + 1] = (uint32_t)bcur;
+                        sm.u.f.blk[4 * j + 2] = xcur;
+                        sm.u.f.blk[4 * j + 3] = (uint32_t)pk;
                         bcur += ce;
                         pk += 8 * b;
                     }
@@ -671,10 +874,10 @@ __device__ void run_fastpfor(Ctx& c) {
                 pk = uni(sm.misc[3]);
                 if (c.err) break;
                 for (int32_t j = 0; j < nbat; ++j) {
-                    const uint32_t h = uniu(sm.blk[4 * j + 0]);
+                    const uint32_t h = uniu(sm.u.f.blk[4 * j + 0]);
                     const int32_t b = (int32_t)(h & 0xffu), ce = (int32_t)((h >> 8) & 0xffu), idx = (int32_t)(h >> 16);
-                    const uint32_t bco = uniu(sm.blk[4 * j + 1]), xcur = uniu(sm.blk[4 * j + 2]);
-                    const int64_t bpk = (int64_t)uniu(sm.blk[4 * j + 3]);
+                    const uint32_t bco = uniu(sm.u.f.blk[4 * j + 1]), xcur = uniu(sm.u.f.blk[4 * j + 2]);
+                    const int64_t bpk = (int64_t)uniu(sm.u.f.blk[4 * j + 3]);
                     // stage the block's 8*b packed words (raw bytes) in LDS
                     const uintptr_t a = (uintptr_t)(c.sb + 4 * bpk);
                     const uintptr_t a16 = a & ~(uintptr_t)15;
@@ -728,8 +931,10 @@ __device__ void run_fastpfor(Ctx& c) {
         if (!c.err && p < nw) {
             int32_t vpos = (int32_t)(4 * p);
             const int32_t base = L;
-            const int32_t got = varint_run<MODE_WORDREV, VAL_VB>(
-                sm, c.sb, vpos, (int32_t)(4 * nw), c.n - L, true, c.err,
+            Win w;
+            w.valid = false;
+            const int32_t got = varint_take<MODE_WORDREV, VAL_VB>(
+                sm, c.sb, w, vpos, (int32_t)(4 * nw), c.n - L, true, c.err,
                 [&](uint32_t lo, uint32_t hi, int32_t vb, int32_t count) {
                     uint32_t vv[1] = {lo};
                     sink_values<1>(c.op, vv, (int64_t)base + vb, count, c.nb, c.out, cr);

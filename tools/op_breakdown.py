@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Times the decode kernel on the config-5 batch restricted to one op class at a time (GPU).
+Prints per-op stream bytes, output bytes, kernel time and achieved GB/s (algorithmic bytes)."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+NAMES = {1: "BYTE_RLE", 2: "RLE_U64", 3: "RLE_I32", 7: "VAR_ZZD", 8: "VAR_XY", 9: "VAR_MORTON", 10: "FPF_ZZD",
+         11: "FPF_XY", 12: "FPF_MORTON", 13: "VAR_U64", 14: "VAR_I32_I64", 15: "VAR_ZZD_I64"}
+
+
+def main():
+    import torch
+
+    covt = bench.load_covt()
+    tiles = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+    picks = bench.sample_batch(bench.tile_library(), tiles, bench.SEED)
+    plan = covt.Plan.from_tiles([t for _, t in picks])
+    batch = covt.DeviceBatch(plan, "cuda")
+    descs = plan.descs.reshape(-1, 32)
+    ops = descs[:, 24]
+    s = plan.streams
+    order = np.argsort(s["desc_index"])
+    s_launch = s[order]
+    res = torch.zeros(2 * plan.num_streams, dtype=torch.int32, device="cuda")
+    L = covt.lib()
+    stream = torch.cuda.current_stream()
+
+    def run(d_desc, n, reps=5):
+        for _ in range(2):
+            L.covt_decode_streams_device(batch.d_in.data_ptr(), d_desc.data_ptr(), n, batch.d_out.data_ptr(),
+                                         res.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            L.covt_decode_streams_device(batch.d_in.data_ptr(), d_desc.data_ptr(), n, batch.d_out.data_ptr(),
+                                         res.data_ptr(), stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    t_all = run(batch.d_desc, plan.num_streams)
+    print("all ops: %.3f ms  (%d streams)" % (t_all, plan.num_streams))
+    for op in sorted(set(ops.tolist())):
+        m = ops == op
+        sub = torch.from_numpy(np.ascontiguousarray(descs[m]).reshape(-1)).cuda()
+        t = run(sub, int(m.sum()))
+        ib = int(s_launch["byte_length"][m].sum())
+        ob = int((s_launch["out_elems"][m] * s_launch["elem_bytes"][m]).sum())
+        nv = int(s_launch["num_values"][m].sum())
+        print("%-12s streams=%7d values=%11d in=%6.1fMB out=%7.1fMB  t=%7.3f ms  alg=%7.1f GB/s  %.2f Gval/s"
+              % (NAMES.get(op, op), int(m.sum()), nv, ib / 1e6, ob / 1e6, t, (ib + ob) / t / 1e6, nv / t / 1e6))
+
+
+if __name__ == "__main__":
+    main()
