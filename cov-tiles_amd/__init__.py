@@ -108,7 +108,7 @@ EXPORTED_SYMBOLS = (
     "covt_plan_create", "covt_plan_destroy", "covt_plan_num_streams", "covt_plan_output_bytes",
     "covt_plan_totals", "covt_plan_streams", "covt_plan_descs", "covt_plan_tile_status",
     "covt_decode_streams_device", "covt_plan_decode_host", "covt_plan_decode_host_multi", "covt_version",
-    "covt_device_count",
+    "covt_device_count", "covt_plan_family_counts", "covt_decode_streams_device_grouped",
 )
 
 
@@ -160,6 +160,8 @@ def lib() -> C.CDLL:
     L.covt_plan_descs.argtypes = [vp, vp]
     L.covt_plan_tile_status.argtypes = [vp, i32p]
     L.covt_decode_streams_device.argtypes = [vp, vp, C.c_int64, vp, vp, vp]
+    L.covt_decode_streams_device_grouped.argtypes = [vp, vp, i64p, vp, vp, vp]
+    L.covt_plan_family_counts.argtypes = [vp, i64p]
     L.covt_plan_decode_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
     L.covt_plan_decode_host_multi.argtypes = [vp, u8p, C.c_uint64, C.c_int32, vp, vp]
     L.covt_version.restype = C.c_char_p
@@ -350,6 +352,8 @@ class Plan:
         self.descs = np.zeros(self.num_streams * 32, dtype=np.uint8)
         if self.num_streams:
             L.covt_plan_descs(h, self.descs.ctypes.data)
+        self.family_counts = np.zeros(3, dtype=np.int64)
+        L.covt_plan_family_counts(h, _ptr(self.family_counts, C.c_int64))
         self.tile_status = np.zeros(max(self.n_tiles, 1), dtype=np.int32)[:self.n_tiles]
         if self.n_tiles:
             L.covt_plan_tile_status(h, _ptr(self.tile_status, C.c_int32))
@@ -413,9 +417,10 @@ class DeviceBatch:
         import torch
 
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        st = lib().covt_decode_streams_device(self.d_in.data_ptr(), self.d_desc.data_ptr(), self.plan.num_streams,
-                                              self.d_out.data_ptr(), self.d_res.data_ptr(), s.cuda_stream)
-        _raise(st, "covt_decode_streams_device")
+        st = lib().covt_decode_streams_device_grouped(self.d_in.data_ptr(), self.d_desc.data_ptr(),
+                                                      _ptr(self.plan.family_counts, C.c_int64),
+                                                      self.d_out.data_ptr(), self.d_res.data_ptr(), s.cuda_stream)
+        _raise(st, "covt_decode_streams_device_grouped")
 
     def results(self):
         """(output bytes, results in plan order) copied to the host."""

@@ -33,12 +33,20 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kFpfBlock = 256;
 constexpr int kFpfPage = 65536;
 constexpr int kFpfBcCap = 3 * kFpfPage / kFpfBlock + kFpfPage;  // JavaFastPFOR byteContainer size
-constexpr int kBlkBatch = 64;
 
 constexpr int kMaxGroups = 256;  // RLE groups recorded per window walk
 
+// Per-wave LDS scratch.  The small fields come first so each codec family's kernel allocates only
+// the prefix it uses (kFamSmem below): varint windows, RLE windows + group tables, or FastPFOR
+// staging + byte container.
 struct __attribute__((aligned(16))) WaveSmem {
-    union {
+    int32_t misc[4];
+    uint16_t cpre[64];   // window index: terminators before each 16-byte chunk
+    uint16_t cmask[64];  // window index: terminator mask of each chunk
+    uint32_t xstart[33]; // FastPFOR: first word of dataTobePacked[k] in the page
+    int32_t xsize[33];   // FastPFOR: its size (-1 if absent from the page's bitmap)
+    uint32_t xcnt[33];   // FastPFOR: exceptions consumed so far
+    union alignas(16) {  // 16-byte aligned: uint4 (ds_*_b128) accesses
         struct {
             uint32_t win[kWin / 4 + 4];    // window bytes (+16 B slack for 12-byte reads)
             uint16_t list[kWin];           // terminator positions (window-relative)
@@ -46,18 +54,20 @@ struct __attribute__((aligned(16))) WaveSmem {
             uint16_t gstart[kMaxGroups];   // RLE: group starts found by the chain walk
         } v;
         struct {
-            uint32_t stage[324];          // packed words of one FastPFOR block (<= 1024 + 15 B)
-            uint32_t patch[256];          // exception patches of one block
-            uint32_t blk[4 * kBlkBatch];  // block records: {b|c<<8|idx<<16, bcoff, xcur, pk}
+            uint32_t stage[324];  // packed words of one FastPFOR block (<= 1024 + 15 B)
+            uint32_t patch[256];  // exception patches of one block
+            uint32_t cbuf[260];   // 1 KiB chunk of the page's byte container
         } f;
     } u;
-    uint32_t xstart[33];
-    int32_t xsize[33];
-    uint32_t xcnt[33];
-    int32_t misc[4];
-    uint16_t cpre[64];   // window index: terminators before each 16-byte chunk
-    uint16_t cmask[64];  // window index: terminator mask of each chunk
 };
+constexpr int kSmemHdr = 672;  // offsetof(WaveSmem, u), checked below
+constexpr int kFamSmemRle = kSmemHdr + (kWin / 4 + 4) * 4 + 2 * kWin * 2 + kMaxGroups * 2;
+constexpr int kFamSmemVarint = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2;
+constexpr int kFamSmemFpf = kSmemHdr + (324 + 256 + 260) * 4 > kFamSmemVarint ? kSmemHdr + (324 + 256 + 260) * 4
+                                                                                 : kFamSmemVarint;
+static_assert(__builtin_offsetof(WaveSmem, u) == kSmemHdr, "WaveSmem header size");
+static_assert(kFamSmemRle == (int)sizeof(WaveSmem), "RLE uses the whole scratch");
+static_assert(kFamSmemRle % 16 == 0 && kFamSmemVarint % 16 == 0 && kFamSmemFpf % 16 == 0, "16-B strides");
 
 // --------------------------------------------------------------------------------------------
 // wave primitives
@@ -87,9 +97,22 @@ __device__ __forceinline__ uint32_t incl_scan(uint32_t x) {
 // --------------------------------------------------------------------------------------------
 // byte helpers
 // --------------------------------------------------------------------------------------------
+// Loads go through explicit global (address-space 1) pointers: an integer->pointer cast would
+// otherwise yield flat_load, which counts on both vmcnt and lgkmcnt and forces full drains
+// (vmcnt(0) & lgkmcnt(0)) at every LDS wait, serialising the wave's memory traffic.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+typedef __attribute__((address_space(1))) const u32x4 g_v4;
+__device__ __forceinline__ const g_u32* g32(uintptr_t a) { return (const g_u32*)a; }
+// 16-byte load from a 16-byte aligned global address
+__device__ __forceinline__ uint4 ld128(uintptr_t a16) {
+    const u32x4 v = *(const g_v4*)a16;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {  // any alignment (input is padded)
     const uintptr_t a = (uintptr_t)p;
-    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    const g_u32* q = g32(a & ~(uintptr_t)3);
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 __device__ __forceinline__ uint32_t ld_be32(const uint8_t* p) { return __builtin_bswap32(ld_le32(p)); }
@@ -303,7 +326,7 @@ __device__ void win_load(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t p, int
     if (MODE == MODE_RAW) {
         const uintptr_t a = ((uintptr_t)(sb + p)) & ~(uintptr_t)15;
         woff = uni((int32_t)((intptr_t)a - (intptr_t)sb));
-        d = ((const uint4*)a)[l];
+        d = ld128(a + 16 * (uintptr_t)l);
     } else {
         woff = p & ~15;
         const uint8_t* q = sb + woff + 16 * l;
@@ -780,16 +803,38 @@ __device__ __forceinline__ uint32_t xget(const Words& W, uint32_t xs, int k, uin
     const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
     return (uint32_t)(((lo | (hi << 32)) >> off) & m);
 }
-// byte j of the page's byte container (LE bytes of the BE words starting at word bc)
-__device__ __forceinline__ uint32_t bc_byte(const uint8_t* sb, int64_t bc, int64_t j) {
-    return sb[4 * (bc + (j >> 2)) + 3 - (j & 3)];
-}
+// One FastPFOR block header walked out of the byte container (FastPFOR.decodePage loop body).
+struct FpfHdr {
+    int32_t b, ce, idx;  // bit width, exception count, maxbits - b
+    uint32_t xcur;       // cursor into dataTobePacked[idx] for this block
+    int32_t bcoff;       // container offset of the exception positions
+    int32_t next;        // container offset of the next block header
+};
+// Registers prefetched for one block.
+struct FpfPre {
+    uint4 raw;           // 16 raw bytes of the block's packed words (16-B aligned, lane-major)
+    uint4 raw2;          // b == 32: the 16 bytes past the first KiB (lane 0)
+    uint32_t pos[4];     // exception e = lane + 64 q: its position in the block
+    uint32_t x0, x1, x2; // exception e = lane: 12 bytes (4-B aligned) covering its packed word(s)
+};
 
+// 12 bytes from a 4-byte aligned global address
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef __attribute__((address_space(1))) const u32x3 g_v3;
+
+// FastPFOR (256-value blocks, 65536-value pages) + VariableByte, JavaFastPFOR 0.1.12 as called by
+// DecodingUtils.java:316-444.  Per page the exception-array directory is read and the byte
+// container is staged in LDS 1 KiB at a time; blocks then run software-pipelined: while block j
+// is unpacked (4 consecutive values per lane), patched and scanned, block j+1's header is walked
+// and its packed words, exception positions and exception values are already in flight.  The
+// packed words are staged in LDS already aligned to the stream's word grid and byte-swapped, so a
+// value costs one ds_read2_b32 and one v_alignbit_b32.
 __device__ void run_fastpfor(Ctx& c) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
     const Words W{c.sb, c.byte_length / 4};
     const int64_t nw = W.nw;
+    const uint32_t sbmis = (uint32_t)((uintptr_t)c.sb & 15);  // stream base misalignment (uniform)
     Carry cr{0, 0};
     int32_t decoded = 0;
     int32_t L = 0;
@@ -831,97 +876,169 @@ __device__ void run_fastpfor(Ctx& c) {
             if (c.err) break;
             wave_sync();
             const int32_t nblocks = thissize / kFpfBlock;
-            int64_t bcur = 0, pk = p0 + 1;
-            for (int32_t b0 = 0; b0 < nblocks && !c.err; b0 += kBlkBatch) {
-                const int32_t nbat = (nblocks - b0) < kBlkBatch ? (nblocks - b0) : kBlkBatch;
-                // serial byte-container walk (lane 0): block headers -> LDS records
-                if (l == 0) {
-                    int32_t e = 0;
-                    for (int32_t j = 0; j < nbat; ++j) {
-                        if (bcur + 2 > bcw * 4) { e = COVT_ERR_BAD_HEADER; break; }
-                        const int32_t b = (int32_t)(int8_t)bc_byte(c.sb, bc, bcur);
-                        const int32_t ce = (int32_t)bc_byte(c.sb, bc, bcur + 1);
-                        bcur += 2;
-                        if (b < 0 || b > 32) { e = COVT_ERR_BAD_HEADER; break; }
-                        if (pk + 8 * b > nw) { e = COVT_ERR_TRUNCATED; break; }
-                        int32_t idx = 0;
-                        uint32_t xcur = 0;
-                        if (ce > 0) {
-                            if (bcur + 1 + ce > bcw * 4) { e = COVT_ERR_BAD_HEADER; break; }
-                            idx = (int32_t)(int8_t)bc_byte(c.sb, bc, bcur) - b;
-                            bcur += 1;
-                            if (idx != 1) {
-                                if (idx < 2 || idx > 32 || sm.xsize[idx] < 0) { e = COVT_ERR_BAD_HEADER; break; }
-                                xcur = sm.xcnt[idx];
-                                if ((int64_t)xcur + ce > sm.xsize[idx]) { e = COVT_ERR_BAD_HEADER; break; }
-                                sm.xcnt[idx] = xcur + ce;
-                            }
-                        }
-                        sm.u.f.blk[4 * j + 0] = (uint32_t)b | ((uint32_t)ce << 8) | ((uint32_t)idx << 16);
-                        sm.u.f.blk[4 * j + 1] = (uint32_t)bcur;
-                        sm.u.f.blk[4 * j + 2] = xcur;
-                        sm.u.f.blk[4 * j + 3] = (uint32_t)pk;
-                        bcur += ce;
-                        pk += 8 * b;
-                    }
-                    sm.misc[1] = e;
-                    sm.misc[2] = (int32_t)bcur;
-                    sm.misc[3] = (int32_t)pk;
-                }
+            const int32_t bclen = (int32_t)(bcw * 4);
+            const uint8_t* cb8 = (const uint8_t*)sm.u.f.cbuf;
+            int32_t cbase = INT32_MIN / 2;
+            auto chunk_load = [&](int32_t at) {  // container bytes [at, at + 1024), at % 4 == 0
+                cbase = at;
+                const int64_t w0 = bc + at / 4 + 4 * l;
+                uint4 d;
+                d.x = (w0 + 0 < bc + bcw) ? W(w0 + 0) : 0u;  // LE bytes of the BE words = container bytes
+                d.y = (w0 + 1 < bc + bcw) ? W(w0 + 1) : 0u;
+                d.z = (w0 + 2 < bc + bcw) ? W(w0 + 2) : 0u;
+                d.w = (w0 + 3 < bc + bcw) ? W(w0 + 3) : 0u;
                 wave_sync();
-                c.err = uni(sm.misc[1]);
-                bcur = uni(sm.misc[2]);
-                pk = uni(sm.misc[3]);
-                if (c.err) break;
-                for (int32_t j = 0; j < nbat; ++j) {
-                    const uint32_t h = uniu(sm.u.f.blk[4 * j + 0]);
-                    const int32_t b = (int32_t)(h & 0xffu), ce = (int32_t)((h >> 8) & 0xffu), idx = (int32_t)(h >> 16);
-                    const uint32_t bco = uniu(sm.u.f.blk[4 * j + 1]), xcur = uniu(sm.u.f.blk[4 * j + 2]);
-                    const int64_t bpk = (int64_t)uniu(sm.u.f.blk[4 * j + 3]);
-                    // stage the block's 8*b packed words (raw bytes) in LDS
-                    const uintptr_t a = (uintptr_t)(c.sb + 4 * bpk);
-                    const uintptr_t a16 = a & ~(uintptr_t)15;
-                    const int32_t o = (int32_t)(a - a16);
-                    const int32_t nchunks = (32 * b + o + 15) / 16;
-                    for (int32_t q = l; q < nchunks; q += 64) ((uint4*)sm.u.f.stage)[q] = ((const uint4*)a16)[q];
-                    wave_sync();
-                    uint32_t v[4];
-                    const int mb = l >> 3, r0 = (l & 7) * 4;
-                    const uint32_t sh = (uint32_t)(o & 3);
-                    auto sword = [&](int32_t i) -> uint32_t {  // packed word i of this block
-                        const int32_t d = (o + 4 * i) >> 2;
-                        return __builtin_bswap32(__builtin_amdgcn_alignbyte(sm.u.f.stage[d + 1], sm.u.f.stage[d], sh));
-                    };
-                    const uint64_t m = b == 32 ? 0xffffffffull : ((1ull << b) - 1ull);
+                ((uint4*)sm.u.f.cbuf)[l] = d;
+                wave_sync();
+            };
+            auto walk = [&](int32_t cur, FpfHdr& h) -> int32_t {
+                if (cur + 2 > bclen) return COVT_ERR_BAD_HEADER;
+                if (cur < cbase || cur + 3 > cbase + kWin) chunk_load(cur & ~3);
+                h.b = (int32_t)(int8_t)uniu(cb8[cur - cbase]);
+                h.ce = (int32_t)uniu(cb8[cur + 1 - cbase]);
+                if (h.b < 0 || h.b > 32) return COVT_ERR_BAD_HEADER;
+                h.idx = 0;
+                h.xcur = 0;
+                h.bcoff = cur + 2;
+                if (h.ce > 0) {
+                    if (cur + 3 + h.ce > bclen) return COVT_ERR_BAD_HEADER;
+                    if (cur + 3 + h.ce > cbase + kWin) chunk_load(cur & ~3);
+                    h.idx = (int32_t)(int8_t)uniu(cb8[cur + 2 - cbase]) - h.b;
+                    h.bcoff = cur + 3;
+                    if (h.idx != 1) {
+                        if (h.idx < 2 || h.idx > 32) return COVT_ERR_BAD_HEADER;
+                        const int32_t xsz = uni(sm.xsize[h.idx]);
+                        h.xcur = uniu(sm.xcnt[h.idx]);
+                        if (xsz < 0 || (int64_t)h.xcur + h.ce > xsz) return COVT_ERR_BAD_HEADER;
+                        if (l == 0) sm.xcnt[h.idx] = h.xcur + (uint32_t)h.ce;
+                    }
+                }
+                h.next = h.bcoff + h.ce;
+                return COVT_OK;
+            };
+            // word index of X[k][i] (dataTobePacked[k]) and the bit offset inside it
+            auto xword = [&](int32_t k, uint32_t xs, uint32_t i, uint32_t& xbit) -> int64_t {
+                const uint32_t bit = (i & 31u) * (uint32_t)k;
+                xbit = bit & 31u;
+                return (int64_t)xs + (int64_t)(i >> 5) * k + (bit >> 5);
+            };
+            auto prefetch = [&](const FpfHdr& h, int64_t pk, FpfPre& pr) {
+                // unconditional loads consumed only in the next iteration: the vmcnt wait lands there
+                const uintptr_t a16 = ((uintptr_t)(c.sb + 4 * pk)) & ~(uintptr_t)15;
+                pr.raw = ld128(a16 + 16 * (uintptr_t)l);
+                pr.raw2 = make_uint4(0, 0, 0, 0);
+                if (h.b == 32 && l == 0) pr.raw2 = ld128(a16 + 1024);
+                const int32_t k = h.idx;
+                int64_t wi = 0;
+                if (k >= 2 && l < h.ce) {
+                    uint32_t xb;
+                    wi = xword(k, uniu(sm.xstart[k]), h.xcur + (uint32_t)l, xb);
+                    if (wi >= nw) wi = 0;
+                }
+                const uintptr_t xa4 = ((uintptr_t)(c.sb + 4 * wi)) & ~(uintptr_t)3;
+                const u32x3 xv = *(const g_v3*)xa4;
+                pr.x0 = xv.x;
+                pr.x1 = xv.y;
+                pr.x2 = xv.z;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    pr.pos[q] = 0;
+                    if (h.ce > 64 * q && l + 64 * q < h.ce) pr.pos[q] = cb8[h.bcoff + l + 64 * q - cbase];
+                }
+            };
+            FpfHdr h;
+            FpfPre pre;
+            int64_t pk = p0 + 1;
+            c.err = walk(0, h);
+            if (!c.err && pk + 8 * h.b > nw) c.err = COVT_ERR_TRUNCATED;
+            if (!c.err) prefetch(h, pk, pre);
+            for (int32_t j = 0; j < nblocks && !c.err; ++j) {
+                const FpfHdr hc = h;
+                const FpfPre pc = pre;
+                const int64_t pkc = pk;
+                const int32_t b = hc.b;
+                // stage block j: LDS dword qoff + i = packed word i (aligned, byte-swapped)
+                const uint32_t o = (sbmis + 4u * (uint32_t)pkc) & 15u;
+                const uint32_t sh = o & 3u;
+                const int32_t qoff = (int32_t)(o >> 2);
+                {
+                    uint32_t nxt = (uint32_t)__shfl_down((int)pc.raw.x, 1, 64);
+                    if (l == 63) nxt = lane_bcast(pc.raw2.x, 0);
+                    uint4 wv;
+                    wv.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.y, pc.raw.x, sh));
+                    wv.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.z, pc.raw.y, sh));
+                    wv.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.w, pc.raw.z, sh));
+                    wv.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(nxt, pc.raw.w, sh));
+                    ((uint4*)sm.u.f.stage)[l] = wv;
+                    if (b == 32 && l == 0) {
+                        uint4 w2;
+                        w2.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw2.y, pc.raw2.x, sh));
+                        w2.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw2.z, pc.raw2.y, sh));
+                        w2.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw2.w, pc.raw2.z, sh));
+                        w2.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(0u, pc.raw2.w, sh));
+                        ((uint4*)sm.u.f.stage)[64] = w2;
+                    }
+                }
+                if (hc.ce > 0) ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
+                wave_sync();
+                // walk block j+1 and put its loads in flight
+                if (j + 1 < nblocks) {
+                    c.err = walk(hc.next, h);
+                    pk = pkc + 8 * b;
+                    if (!c.err && pk + 8 * h.b > nw) c.err = COVT_ERR_TRUNCATED;
+                    if (c.err) break;
+                    prefetch(h, pk, pre);
+                }
+                // unpack: lane l -> values 4l..4l+3 of miniblock l/8
+                uint32_t v[4];
+                {
+                    const uint32_t mask = b == 32 ? 0xffffffffu : ((1u << b) - 1u);
+                    uint32_t bit = (uint32_t)((l & 7) * 4 * b);
+                    const int32_t wb = (l >> 3) * b + qoff;
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        if (b == 0) { v[k] = 0; continue; }
-                        const int32_t bit = (r0 + k) * b;
-                        const int32_t wi = mb * b + (bit >> 5);
-                        const int off = bit & 31;
-                        const uint64_t lo = sword(wi);
-                        const uint64_t hi = (off + b > 32) ? (uint64_t)sword(wi + 1) : 0ull;
-                        v[k] = (uint32_t)(((lo | (hi << 32)) >> off) & m);
+                        const int32_t wi = wb + (int32_t)(bit >> 5);
+                        const uint32_t lo = sm.u.f.stage[wi], hi = sm.u.f.stage[wi + 1];
+                        v[k] = __builtin_amdgcn_alignbit(hi, lo, bit & 31u) & mask;
+                        bit += (uint32_t)b;
                     }
-                    if (ce > 0) {
-                        ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
-                        wave_sync();
-                        for (int32_t e = l; e < ce; e += 64) {
-                            const uint32_t pos8 = bc_byte(c.sb, bc, (int64_t)bco + e);
-                            const uint32_t ex = (idx == 1) ? 1u : xget(W, sm.xstart[idx], idx, xcur + (uint32_t)e);
-                            atomicOr(&sm.u.f.patch[pos8], ex << (b & 31));  // out[pos] |= ...
-                        }
-                        wave_sync();
-                        const uint4 pt = ((const uint4*)sm.u.f.patch)[l];
-                        v[0] |= pt.x;
-                        v[1] |= pt.y;
-                        v[2] |= pt.z;
-                        v[3] |= pt.w;
-                    }
-                    sink_values<4>(c.op, v, (int64_t)done + (int64_t)(b0 + j) * kFpfBlock, kFpfBlock, c.nb, c.out,
-                                   cr);
-                    wave_sync();
                 }
+                if (hc.ce > 0) {  // out[pos] |= (index == 1 ? 1 : exceptvalue) << b
+                    const int32_t k = hc.idx;
+                    const uint32_t xs = k >= 2 ? uniu(sm.xstart[k]) : 0u;
+                    if (l < hc.ce) {
+                        uint32_t ex = 1u;
+                        if (k != 1) {
+                            uint32_t xbit;
+                            const int64_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
+                            const uint32_t ob = sbmis & 3u;
+                            uint64_t lo = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.x1, pc.x0, ob));
+                            uint64_t hi = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.x2, pc.x1, ob));
+                            if (wi >= nw) lo = 0;  // words past the stream read as 0
+                            if (wi + 1 >= nw || xbit + (uint32_t)k <= 32u) hi = 0;
+                            const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
+                            ex = (uint32_t)(((lo | (hi << 32)) >> xbit) & m);
+                        }
+                        atomicOr(&sm.u.f.patch[pc.pos[0]], ex << (b & 31));
+                    }
+                    if (hc.ce > 64) {  // rare: more than 64 exceptions in the block
+                        for (int q = 1; q < 4; ++q) {
+                            const int32_t e = l + 64 * q;
+                            if (e < hc.ce) {
+                                const uint32_t ex = k == 1 ? 1u : xget(W, xs, k, hc.xcur + (uint32_t)e);
+                                atomicOr(&sm.u.f.patch[pc.pos[q]], ex << (b & 31));
+                            }
+                        }
+                    }
+                    wave_sync();
+                    const uint4 pt = ((const uint4*)sm.u.f.patch)[l];
+                    v[0] |= pt.x;
+                    v[1] |= pt.y;
+                    v[2] |= pt.z;
+                    v[3] |= pt.w;
+                }
+                sink_values<4>(c.op, v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, c.nb, c.out, cr);
+                wave_sync();
             }
             done += thissize;
             p = ie;
@@ -953,17 +1070,30 @@ __device__ void run_fastpfor(Ctx& c) {
     c.consumed = c.byte_length;
 }
 
-__global__ __launch_bounds__(256) void decode_streams_kernel(const uint8_t* __restrict__ in,
-                                                             const covt_stream_desc* __restrict__ descs,
-                                                             int64_t n_streams, uint8_t* __restrict__ out,
-                                                             covt_stream_result* __restrict__ res) {
-    __shared__ WaveSmem smem[kWavesPerBlock];
+__host__ __device__ constexpr int op_family(int op) {
+    return (op >= COVT_OP_FPF_ZZ_DELTA_I32 && op <= COVT_OP_FPF_DELTA_MORTON) ? COVT_FAMILY_FASTPFOR
+           : ((op >= COVT_OP_VARINT_I32 && op <= COVT_OP_VARINT_DELTA_MORTON) || op >= COVT_OP_VARINT_U64)
+               ? COVT_FAMILY_VARINT
+               : COVT_FAMILY_RLE;  // RLE ops and COVT_OP_NONE (reported as unsupported)
+}
+
+// One wave per descriptor; waves whose descriptor belongs to another family return at once (used
+// when the caller's descriptors are not grouped by family).
+template <int FAM>
+__global__ __launch_bounds__(256) void decode_family_kernel(const uint8_t* __restrict__ in,
+                                                            const covt_stream_desc* __restrict__ descs,
+                                                            int64_t n_streams, uint8_t* __restrict__ out,
+                                                            covt_stream_result* __restrict__ res) {
+    constexpr int kStride = FAM == COVT_FAMILY_RLE ? kFamSmemRle
+                            : FAM == COVT_FAMILY_VARINT ? kFamSmemVarint : kFamSmemFpf;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kStride];
     const int wv = uni((int)(threadIdx.x >> 6));
     const int64_t sid = (int64_t)blockIdx.x * kWavesPerBlock + wv;
     if (sid >= n_streams) return;
     const covt_stream_desc d = descs[sid];
+    if (op_family(d.op) != FAM) return;
     Ctx c;
-    c.sm = &smem[wv];
+    c.sm = (WaveSmem*)(smem + wv * kStride);
     c.sb = in + d.in_off;
     c.out = out + d.out_off;
     c.avail = d.avail;
@@ -975,25 +1105,14 @@ __global__ __launch_bounds__(256) void decode_streams_kernel(const uint8_t* __re
     c.consumed = 0;
     if (c.n < 0 || c.avail < 0 || c.byte_length < 0) {
         c.err = COVT_ERR_INVALID_ARG;
-    } else if (c.n > 0 || c.op >= COVT_OP_FPF_ZZ_DELTA_I32) {
-        switch (c.op) {
-        case COVT_OP_BYTE_RLE_U8: run_rle_byte(c); break;
-        case COVT_OP_RLE_U64:
-        case COVT_OP_RLE_I32:
-        case COVT_OP_RLE_S64: run_rle_int(c); break;
-        case COVT_OP_VARINT_I32:
-        case COVT_OP_VARINT_ZZ_I32:
-        case COVT_OP_VARINT_ZZ_DELTA_I32:
-        case COVT_OP_VARINT_ZZ_DELTA_XY:
-        case COVT_OP_VARINT_DELTA_MORTON:
-        case COVT_OP_VARINT_U64:
-        case COVT_OP_VARINT_I32_AS_I64:
-        case COVT_OP_VARINT_ZZ_DELTA_I64: run_varint_stream(c); break;
-        case COVT_OP_FPF_ZZ_DELTA_I32:
-        case COVT_OP_FPF_ZZ_DELTA_XY:
-        case COVT_OP_FPF_DELTA_MORTON: run_fastpfor(c); break;
-        default: c.err = COVT_ERR_UNSUPPORTED_ENCODING; break;
-        }
+    } else if (FAM == COVT_FAMILY_RLE) {
+        if (c.op == COVT_OP_BYTE_RLE_U8) { if (c.n > 0) run_rle_byte(c); }
+        else if (c.op == COVT_OP_NONE) c.err = COVT_ERR_UNSUPPORTED_ENCODING;
+        else if (c.n > 0) run_rle_int(c);
+    } else if (FAM == COVT_FAMILY_VARINT) {
+        run_varint_stream(c);
+    } else {
+        run_fastpfor(c);
     }
     if (lane_id() == 0) {
         covt_stream_result r;
@@ -1005,12 +1124,28 @@ __global__ __launch_bounds__(256) void decode_streams_kernel(const uint8_t* __re
 
 }  // namespace covt
 
-extern "C" int covt_launch_decode(const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
+extern "C" int covt_launch_family(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
                                   uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream) {
     if (n_streams <= 0) return COVT_OK;
     const int64_t blocks = (n_streams + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
-    hipLaunchKernelGGL(covt::decode_streams_kernel, dim3((unsigned)blocks), dim3(64 * covt::kWavesPerBlock), 0,
-                       stream, d_in, d_desc, n_streams, d_out, d_res);
+    const dim3 grid((unsigned)blocks), block(64 * covt::kWavesPerBlock);
+    switch (fam) {
+    case COVT_FAMILY_RLE:
+        hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_RLE>, grid, block, 0, stream, d_in, d_desc,
+                           n_streams, d_out, d_res);
+        break;
+    case COVT_FAMILY_VARINT:
+        hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_VARINT>, grid, block, 0, stream, d_in, d_desc,
+                           n_streams, d_out, d_res);
+        break;
+    case COVT_FAMILY_FASTPFOR:
+        hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_FASTPFOR>, grid, block, 0, stream, d_in, d_desc,
+                           n_streams, d_out, d_res);
+        break;
+    default: return COVT_ERR_INVALID_ARG;
+    }
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
 }
+
+extern "C" int covt_op_family_of(int op) { return covt::op_family(op); }

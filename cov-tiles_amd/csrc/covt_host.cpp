@@ -319,7 +319,7 @@ int run_one(const uint8_t* region, size_t region_len, size_t pad_to, int op, int
     d.byte_length = byte_length;
     if (hipMemcpyAsync(c->d_desc, &d, sizeof d, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return COVT_ERR_DEVICE;
-    int st = covt_launch_decode(c->d_in, c->d_desc, 1, c->d_out, c->d_res, c->stream);
+    int st = covt_launch_family(covt_op_family_of(op), c->d_in, c->d_desc, 1, c->d_out, c->d_res, c->stream);
     if (st) return st;
     if (out_bytes && hipMemcpyAsync(out, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
         return COVT_ERR_DEVICE;
@@ -356,6 +356,42 @@ int fpf_call(const uint8_t* buf, size_t buf_len, int32_t* pos, int op, int32_t n
     return COVT_OK;
 }
 
+// Fork/join of the three family kernels: RLE on the caller's stream, varint and FastPFOR on two
+// per-thread auxiliary streams ordered by events (capturable into a hipGraph).
+struct ForkCtx {
+    int device = -1;
+    hipStream_t aux[2] = {nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+};
+
+int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const int64_t counts[COVT_NUM_FAMILIES],
+                   uint8_t* d_out, covt_stream_result* d_res, hipStream_t s) {
+    thread_local ForkCtx f;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return COVT_ERR_DEVICE;
+    if (f.device != dev) {
+        f = ForkCtx{};
+        f.device = dev;
+        for (int i = 0; i < 2; ++i) {
+            if (hipStreamCreateWithFlags(&f.aux[i], hipStreamNonBlocking) != hipSuccess) return COVT_ERR_DEVICE;
+            if (hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming) != hipSuccess) return COVT_ERR_DEVICE;
+        }
+        if (hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess) return COVT_ERR_DEVICE;
+    }
+    const int64_t o1 = counts[0], o2 = counts[0] + counts[1];
+    if (hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
+    for (int i = 0; i < 2; ++i)
+        if (hipStreamWaitEvent(f.aux[i], f.fork, 0) != hipSuccess) return COVT_ERR_DEVICE;
+    int st = covt_launch_family(COVT_FAMILY_FASTPFOR, d_in, d_desc + o2, counts[2], d_out, d_res + o2, f.aux[0]);
+    if (!st) st = covt_launch_family(COVT_FAMILY_VARINT, d_in, d_desc + o1, counts[1], d_out, d_res + o1, f.aux[1]);
+    if (!st) st = covt_launch_family(COVT_FAMILY_RLE, d_in, d_desc, counts[0], d_out, d_res, s);
+    for (int i = 0; i < 2; ++i) {
+        if (hipEventRecord(f.join[i], f.aux[i]) != hipSuccess) return COVT_ERR_DEVICE;
+        if (hipStreamWaitEvent(s, f.join[i], 0) != hipSuccess) return COVT_ERR_DEVICE;
+    }
+    return st;
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -366,7 +402,8 @@ struct covt_plan {
     std::vector<int32_t> tile_status;
     std::vector<uint64_t> tile_off, tile_size;
     std::vector<covt_stream_info> info;   // tile order
-    std::vector<covt_stream_desc> descs;  // launch order (largest first)
+    std::vector<covt_stream_desc> descs;  // launch order: grouped by family, largest first
+    int64_t fam_counts[COVT_NUM_FAMILIES] = {0, 0, 0};
     int64_t out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
 };
 
@@ -485,7 +522,11 @@ int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const u
         const auto& s = p->info[(size_t)i];
         return (int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4;
     };
-    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return cost(a) > cost(b); });
+    auto fam = [&](int64_t i) { return covt_op_family_of(p->info[(size_t)i].op); };
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+        return fam(a) != fam(b) ? fam(a) < fam(b) : cost(a) > cost(b);
+    });
+    for (int64_t i : order) p->fam_counts[fam(i)]++;
     p->descs.resize(ns);
     for (size_t k = 0; k < ns; ++k) {
         covt_stream_info& si = p->info[(size_t)order[k]];
@@ -534,7 +575,24 @@ int covt_decode_streams_device(const uint8_t* d_in, const covt_stream_desc* d_de
                                uint8_t* d_out, covt_stream_result* d_res, void* hip_stream) {
     if (n_streams < 0 || (n_streams && (!d_in || !d_desc || !d_res))) return COVT_ERR_INVALID_ARG;
     if ((uintptr_t)d_in & 15) return COVT_ERR_INVALID_ARG;
-    return covt_launch_decode(d_in, d_desc, n_streams, d_out, d_res, (hipStream_t)hip_stream);
+    for (int f = 0; f < COVT_NUM_FAMILIES; ++f) {  // any order: each family kernel skips the others
+        const int st = covt_launch_family(f, d_in, d_desc, n_streams, d_out, d_res, (hipStream_t)hip_stream);
+        if (st) return st;
+    }
+    return COVT_OK;
+}
+
+int covt_plan_family_counts(const covt_plan* p, int64_t counts[COVT_NUM_FAMILIES]) {
+    if (!p || !counts) return COVT_ERR_INVALID_ARG;
+    for (int f = 0; f < COVT_NUM_FAMILIES; ++f) counts[f] = p->fam_counts[f];
+    return COVT_OK;
+}
+
+int covt_decode_streams_device_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc,
+                                       const int64_t family_counts[COVT_NUM_FAMILIES], uint8_t* d_out,
+                                       covt_stream_result* d_res, void* hip_stream) {
+    if (!family_counts || ((uintptr_t)d_in & 15)) return COVT_ERR_INVALID_ARG;
+    return launch_grouped(d_in, d_desc, family_counts, d_out, d_res, (hipStream_t)hip_stream);
 }
 
 }  // extern "C"
@@ -590,7 +648,9 @@ int decode_subset(const covt_plan* p, const uint8_t* bytes, const std::vector<in
         if (!descs.empty())
             chk(hipMemcpyAsync(d_desc, descs.data(), descs.size() * sizeof(covt_stream_desc), hipMemcpyHostToDevice,
                                s));
-        if (st == COVT_OK) st = covt_launch_decode(d_in, d_desc, (int64_t)descs.size(), d_out, d_res, s);
+        int64_t cnt[COVT_NUM_FAMILIES] = {0, 0, 0};
+        for (const auto& d : descs) cnt[covt_op_family_of(d.op)]++;  // sel is in grouped launch order
+        if (st == COVT_OK) st = launch_grouped(d_in, d_desc, cnt, d_out, d_res, s);
         stage.resize((size_t)out_total);
         if (st == COVT_OK && out_total)
             chk(hipMemcpyAsync(stage.data(), d_out, (size_t)out_total, hipMemcpyDeviceToHost, s));

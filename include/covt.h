@@ -111,6 +111,12 @@ enum covt_op {
     COVT_OP_COUNT = 16
 };
 
+/* Codec families: each has its own kernel (register / LDS footprint), launched concurrently. */
+#define COVT_FAMILY_RLE 0      /* byte RLE, integer RLE (and COVT_OP_NONE -> unsupported) */
+#define COVT_FAMILY_VARINT 1   /* varint / zigzag / delta / Morton ops */
+#define COVT_FAMILY_FASTPFOR 2 /* FastPFOR + VariableByte ops */
+#define COVT_NUM_FAMILIES 3
+
 /* One device-resident plan entry (32 bytes). */
 typedef struct covt_stream_desc {
     uint64_t in_off;     /* payload byte offset in the batch input buffer */
@@ -150,6 +156,9 @@ int64_t covt_plan_output_bytes(const covt_plan* plan);
 int covt_plan_totals(const covt_plan* plan, int64_t* in_bytes, int64_t* out_bytes, int64_t* vertices);
 int covt_plan_streams(const covt_plan* plan, covt_stream_info* out);    /* num_streams records */
 int covt_plan_descs(const covt_plan* plan, covt_stream_desc* out);      /* num_streams, launch order */
+/* Launch order groups descriptors by family (RLE, varint, FastPFOR; largest stream first inside a
+ * family): counts[f] = descriptors of family f. */
+int covt_plan_family_counts(const covt_plan* plan, int64_t counts[COVT_NUM_FAMILIES]);
 int covt_plan_tile_status(const covt_plan* plan, int32_t* out);         /* n_tiles */
 
 /* Launch the decode of n_streams descriptors on `hip_stream` (a hipStream_t; NULL = default).
@@ -157,6 +166,12 @@ int covt_plan_tile_status(const covt_plan* plan, int32_t* out);         /* n_til
  * d_out: output buffer of covt_plan_output_bytes bytes; d_res: n_streams results.  Asynchronous. */
 int covt_decode_streams_device(const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
                                uint8_t* d_out, covt_stream_result* d_res, void* hip_stream);
+
+/* Same, for descriptors grouped by family (as covt_plan_descs returns them): the three family
+ * kernels run concurrently on forked streams joined back into `hip_stream`. */
+int covt_decode_streams_device_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc,
+                                       const int64_t family_counts[COVT_NUM_FAMILIES], uint8_t* d_out,
+                                       covt_stream_result* d_res, void* hip_stream);
 
 /* Convenience: plan + H2D + decode + D2H for host tiles on the current device.
  * host_out: covt_plan_output_bytes(plan) bytes; host_res: num_streams results (plan stream order). */

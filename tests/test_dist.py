@@ -55,9 +55,14 @@ def test_two_rank_sharding_gloo():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got, mx, total_in, weak = q.get(timeout=300)
+    try:
+        got, mx, total_in, weak = q.get(timeout=180)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
     for p in procs:
-        p.join(timeout=120)
         assert p.exitcode == 0
     idx = sorted(i for g in got for i in g[0])
     assert idx == list(range(600))  # every tile exactly once, no data exchange needed

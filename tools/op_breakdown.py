@@ -45,7 +45,17 @@ def main():
         return e0.elapsed_time(e1) / reps
 
     t_all = run(batch.d_desc, plan.num_streams)
-    print("all ops: %.3f ms  (%d streams)" % (t_all, plan.num_streams))
+    print("all ops, families back to back: %.3f ms  (%d streams)" % (t_all, plan.num_streams))
+    for _ in range(2):
+        batch.decode()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(5):
+        batch.decode(stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    print("all ops, families concurrent (grouped launch): %.3f ms" % (e0.elapsed_time(e1) / 5))
     for op in sorted(set(ops.tolist())):
         m = ops == op
         sub = torch.from_numpy(np.ascontiguousarray(descs[m]).reshape(-1)).cuda()
@@ -53,8 +63,15 @@ def main():
         ib = int(s_launch["byte_length"][m].sum())
         ob = int((s_launch["out_elems"][m] * s_launch["elem_bytes"][m]).sum())
         nv = int(s_launch["num_values"][m].sum())
+        idx = np.nonzero(m)[0]  # launch order is largest first
+        top = torch.from_numpy(np.ascontiguousarray(descs[idx[:1]]).reshape(-1)).cuda()
+        t1 = run(top, 1)
+        rest = torch.from_numpy(np.ascontiguousarray(descs[idx[64:]]).reshape(-1)).cuda()
+        tr = run(rest, max(len(idx) - 64, 0)) if len(idx) > 64 else 0.0
         print("%-12s streams=%7d values=%11d in=%6.1fMB out=%7.1fMB  t=%7.3f ms  alg=%7.1f GB/s  %.2f Gval/s"
-              % (NAMES.get(op, op), int(m.sum()), nv, ib / 1e6, ob / 1e6, t, (ib + ob) / t / 1e6, nv / t / 1e6))
+              "  | largest stream (%d B, %d vals) %.3f ms | all but top-64 %.3f ms"
+              % (NAMES.get(op, op), int(m.sum()), nv, ib / 1e6, ob / 1e6, t, (ib + ob) / t / 1e6, nv / t / 1e6,
+                 int(s_launch["byte_length"][idx[0]]), int(s_launch["num_values"][idx[0]]), t1, tr))
 
 
 if __name__ == "__main__":
