@@ -57,14 +57,16 @@ struct __attribute__((aligned(16))) WaveSmem {
             uint32_t stage[324];  // packed words of one FastPFOR block (<= 1024 + 15 B)
             uint32_t patch[256];  // exception patches of one block
             uint32_t cbuf[260];   // 1 KiB chunk of the page's byte container
+            uint8_t posx[2][192]; // positions of exceptions 64..255 of the next two blocks
         } f;
     } u;
 };
 constexpr int kSmemHdr = 672;  // offsetof(WaveSmem, u), checked below
 constexpr int kFamSmemRle = kSmemHdr + (kWin / 4 + 4) * 4 + 2 * kWin * 2 + kMaxGroups * 2;
 constexpr int kFamSmemVarint = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2;
-constexpr int kFamSmemFpf = kSmemHdr + (324 + 256 + 260) * 4 > kFamSmemVarint ? kSmemHdr + (324 + 256 + 260) * 4
-                                                                                 : kFamSmemVarint;
+constexpr int kFamSmemFpf = kSmemHdr + (324 + 256 + 260) * 4 + 384 > kFamSmemVarint
+                                ? kSmemHdr + (324 + 256 + 260) * 4 + 384
+                                : kFamSmemVarint;
 static_assert(__builtin_offsetof(WaveSmem, u) == kSmemHdr, "WaveSmem header size");
 static_assert(kFamSmemRle == (int)sizeof(WaveSmem), "RLE uses the whole scratch");
 static_assert(kFamSmemRle % 16 == 0 && kFamSmemVarint % 16 == 0 && kFamSmemFpf % 16 == 0, "16-B strides");
@@ -169,116 +171,124 @@ struct Carry {
     uint32_t x, y;
 };
 
-template <int K>
-__device__ __forceinline__ void sink_values(int op, const uint32_t (&v)[K], int64_t base, int32_t count, int nb,
+// Per-op output transform, specialised at compile time.  `count` (uniform) values are valid; a full
+// group (count >= 64 K) takes the branch-free path with vector stores, a partial one masks lanes.
+template <int OP, int K>
+__device__ __forceinline__ void sink_values(const uint32_t (&vin)[K], int64_t base, int32_t count, int nb,
                                             uint8_t* __restrict__ out, Carry& c) {
     const int l = lane_id();
+    const bool full = count >= 64 * K;
+    const int32_t nvalid = count - l * K;
     const int64_t i0 = base + (int64_t)l * K;
-    const int32_t nvalid = count - l * K;  // values of this lane that are valid (may be <=0 or >K)
-    auto valid = [&](int k) { return k < nvalid; };
-    switch (op) {
-    case COVT_OP_VARINT_I32: {
-        int32_t* o = (int32_t*)out;
+    uint32_t v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = (full || k < nvalid) ? vin[k] : 0u;
+    auto st32 = [&](const int32_t (&r)[K]) {
+        int32_t* o = (int32_t*)out + i0;
+        if (full) {
+            if (K == 4) *(int4*)o = make_int4(r[0], r[K > 1 ? 1 : 0], r[K > 2 ? 2 : 0], r[K > 3 ? 3 : 0]);
+            else
+#pragma unroll
+                for (int k = 0; k < K; ++k) o[k] = r[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (k < nvalid) o[k] = r[k];
+        }
+    };
+    auto st64 = [&](const int64_t (&r)[K]) {
+        int64_t* o = (int64_t*)out + i0;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (valid(k)) o[i0 + k] = (int32_t)v[k];
-        return;
-    }
-    case COVT_OP_VARINT_ZZ_I32: {
-        int32_t* o = (int32_t*)out;
+            if (full || k < nvalid) o[k] = r[k];
+    };
+    if constexpr (OP == COVT_OP_VARINT_I32 || OP == COVT_OP_VARINT_ZZ_I32) {
+        int32_t r[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (valid(k)) o[i0 + k] = zz32(v[k]);
-        return;
-    }
-    case COVT_OP_VARINT_I32_AS_I64: {
-        int64_t* o = (int64_t*)out;
+        for (int k = 0; k < K; ++k) r[k] = OP == COVT_OP_VARINT_I32 ? (int32_t)v[k] : zz32(v[k]);
+        st32(r);
+    } else if constexpr (OP == COVT_OP_VARINT_I32_AS_I64) {
+        int64_t r[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (valid(k)) o[i0 + k] = (int64_t)(int32_t)v[k];
-        return;
-    }
-    case COVT_OP_VARINT_ZZ_DELTA_I32:
-    case COVT_OP_FPF_ZZ_DELTA_I32:
-    case COVT_OP_VARINT_ZZ_DELTA_I64: {
-        uint32_t s[K];
+        for (int k = 0; k < K; ++k) r[k] = (int64_t)(int32_t)v[k];
+        st64(r);
+    } else if constexpr (OP == COVT_OP_VARINT_ZZ_DELTA_I32 || OP == COVT_OP_FPF_ZZ_DELTA_I32 ||
+                         OP == COVT_OP_VARINT_ZZ_DELTA_I64) {
+        uint32_t sacc[K];
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            acc += valid(k) ? (uint32_t)zz32(v[k]) : 0u;
-            s[k] = acc;
+            acc += (uint32_t)zz32(v[k]);  // masked lanes hold 0 -> zz 0
+            sacc[k] = acc;
         }
         const uint32_t inc = incl_scan(acc);
         const uint32_t pre = c.x + inc - acc;
-        if (op == COVT_OP_VARINT_ZZ_DELTA_I64) {
-            int64_t* o = (int64_t*)out;
+        if constexpr (OP == COVT_OP_VARINT_ZZ_DELTA_I64) {
+            int64_t r[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (valid(k)) o[i0 + k] = (int64_t)(int32_t)(pre + s[k]);
+            for (int k = 0; k < K; ++k) r[k] = (int64_t)(int32_t)(pre + sacc[k]);
+            st64(r);
         } else {
-            int32_t* o = (int32_t*)out;
-            if (K == 4 && nvalid >= 4) {
-                *(int4*)(o + i0) = make_int4((int32_t)(pre + s[0]), (int32_t)(pre + s[K > 1 ? 1 : 0]),
-                                             (int32_t)(pre + s[K > 2 ? 2 : 0]), (int32_t)(pre + s[K > 3 ? 3 : 0]));
-            } else {
+            int32_t r[K];
 #pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (valid(k)) o[i0 + k] = (int32_t)(pre + s[k]);
-            }
+            for (int k = 0; k < K; ++k) r[k] = (int32_t)(pre + sacc[k]);
+            st32(r);
         }
         c.x += lane_bcast(inc, 63);
-        return;
-    }
-    case COVT_OP_VARINT_ZZ_DELTA_XY:
-    case COVT_OP_FPF_ZZ_DELTA_XY: {
+    } else if constexpr (OP == COVT_OP_VARINT_ZZ_DELTA_XY || OP == COVT_OP_FPF_ZZ_DELTA_XY) {
         uint32_t sx[K], sy[K];
         uint32_t ax = 0, ay = 0;
+        const uint32_t par0 = (uint32_t)(i0 & 1);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const uint32_t z = valid(k) ? (uint32_t)zz32(v[k]) : 0u;
-            if (((i0 + k) & 1) == 0) ax += z; else ay += z;
+            const uint32_t z = (uint32_t)zz32(v[k]);
+            const bool isx = ((par0 + k) & 1u) == 0;
+            ax += isx ? z : 0u;
+            ay += isx ? 0u : z;
             sx[k] = ax;
             sy[k] = ay;
         }
         const uint32_t incx = incl_scan(ax), incy = incl_scan(ay);
         const uint32_t prex = c.x + incx - ax, prey = c.y + incy - ay;
-        int32_t* o = (int32_t*)out;
-        if (K == 4 && nvalid >= 4 && ((i0 & 1) == 0)) {
-            *(int4*)(o + i0) = make_int4((int32_t)(prex + sx[0]), (int32_t)(prey + sy[K > 1 ? 1 : 0]),
-                                         (int32_t)(prex + sx[K > 2 ? 2 : 0]), (int32_t)(prey + sy[K > 3 ? 3 : 0]));
-        } else {
+        int32_t r[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (valid(k)) o[i0 + k] = (int32_t)((((i0 + k) & 1) == 0) ? (prex + sx[k]) : (prey + sy[k]));
-        }
+        for (int k = 0; k < K; ++k) r[k] = (int32_t)((((par0 + k) & 1u) == 0) ? (prex + sx[k]) : (prey + sy[k]));
+        st32(r);
         c.x += lane_bcast(incx, 63);
         c.y += lane_bcast(incy, 63);
-        return;
-    }
-    case COVT_OP_VARINT_DELTA_MORTON:
-    case COVT_OP_FPF_DELTA_MORTON: {
-        uint32_t s[K];
+    } else if constexpr (OP == COVT_OP_VARINT_DELTA_MORTON || OP == COVT_OP_FPF_DELTA_MORTON) {
+        uint32_t sacc[K];
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            acc += valid(k) ? v[k] : 0u;  // no zigzag (DecodingUtils.java:398-399, :435)
-            s[k] = acc;
+            acc += v[k];  // no zigzag (DecodingUtils.java:398-399, :435)
+            sacc[k] = acc;
         }
         const uint32_t inc = incl_scan(acc);
         const uint32_t pre = c.x + inc - acc;
         const int32_t half = morton_half(nb);
-        int32_t* o = (int32_t*)out;
+        int32_t* o = (int32_t*)out + 2 * i0;
+        int32_t xy[2 * K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int32_t code = (int32_t)(pre + s[k]);
-            const int32_t x = (int32_t)((uint32_t)morton_axis(code, nb) - (uint32_t)half);
-            const int32_t y = (int32_t)((uint32_t)morton_axis(code >> 1, nb) - (uint32_t)half);
-            if (valid(k)) *(int2*)(o + 2 * (i0 + k)) = make_int2(x, y);
+            const int32_t code = (int32_t)(pre + sacc[k]);
+            xy[2 * k] = (int32_t)((uint32_t)morton_axis(code, nb) - (uint32_t)half);
+            xy[2 * k + 1] = (int32_t)((uint32_t)morton_axis(code >> 1, nb) - (uint32_t)half);
+        }
+        if (full) {
+            if (K == 4) {
+                *(int4*)o = make_int4(xy[0], xy[1], xy[K > 1 ? 2 : 0], xy[K > 1 ? 3 : 0]);
+                *(int4*)(o + 4) = make_int4(xy[K > 2 ? 4 : 0], xy[K > 2 ? 5 : 0], xy[K > 3 ? 6 : 0], xy[K > 3 ? 7 : 0]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k) *(int2*)(o + 2 * k) = make_int2(xy[2 * k], xy[2 * k + 1]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (k < nvalid) *(int2*)(o + 2 * k) = make_int2(xy[2 * k], xy[2 * k + 1]);
         }
         c.x += lane_bcast(inc, 63);
-        return;
-    }
-    default: return;
     }
 }
 
@@ -505,6 +515,7 @@ __device__ __forceinline__ uint32_t rd_byte(Ctx& c, Win& w, int32_t q, int32_t n
     return uniu(win_byte(*c.sm, q - w.woff));
 }
 
+template <int OP>
 __device__ void run_varint_stream(Ctx& c) {
     int32_t pos = 0;
     Carry cr{0, 0};
@@ -512,9 +523,9 @@ __device__ void run_varint_stream(Ctx& c) {
     w.valid = false;
     auto sink1 = [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
         uint32_t v[1] = {lo};
-        sink_values<1>(c.op, v, base, count, c.nb, c.out, cr);
+        sink_values<OP, 1>(v, base, count, c.nb, c.out, cr);
     };
-    if (c.op == COVT_OP_VARINT_U64) {
+    if constexpr (OP == COVT_OP_VARINT_U64) {
         int64_t* o = (int64_t*)c.out;
         varint_take<MODE_RAW, VAL_U64_STRICT>(*c.sm, c.sb, w, pos, c.avail, c.n, false, c.err,
                                               [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
@@ -522,7 +533,7 @@ __device__ void run_varint_stream(Ctx& c) {
                                                       o[base + lane_id()] = (int64_t)(((uint64_t)hi << 32) | lo);
                                               });
     } else {
-        if ((c.op == COVT_OP_VARINT_ZZ_DELTA_XY) && (c.n & 1)) {
+        if ((OP == COVT_OP_VARINT_ZZ_DELTA_XY) && (c.n & 1)) {
             // Java decodes the x,y pair and then overruns values[] (ArrayIndexOutOfBounds)
             varint_take<MODE_RAW, VAL_J4>(*c.sm, c.sb, w, pos, c.avail, c.n - 1, false, c.err, sink1);
             if (!c.err) c.err = COVT_ERR_COUNT_MISMATCH;
@@ -813,8 +824,7 @@ struct FpfHdr {
 // Registers prefetched for one block.
 struct FpfPre {
     uint4 raw;           // 16 raw bytes of the block's packed words (16-B aligned, lane-major)
-    uint4 raw2;          // b == 32: the 16 bytes past the first KiB (lane 0)
-    uint32_t pos[4];     // exception e = lane + 64 q: its position in the block
+    uint32_t pos;        // exception e = lane: its position in the block (e >= 64: LDS posx[])
     uint32_t x0, x1, x2; // exception e = lane: 12 bytes (4-B aligned) covering its packed word(s)
 };
 
@@ -829,6 +839,7 @@ typedef __attribute__((address_space(1))) const u32x3 g_v3;
 // and its packed words, exception positions and exception values are already in flight.  The
 // packed words are staged in LDS already aligned to the stream's word grid and byte-swapped, so a
 // value costs one ds_read2_b32 and one v_alignbit_b32.
+template <int OP>
 __device__ void run_fastpfor(Ctx& c) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
@@ -922,28 +933,27 @@ __device__ void run_fastpfor(Ctx& c) {
                 xbit = bit & 31u;
                 return (int64_t)xs + (int64_t)(i >> 5) * k + (bit >> 5);
             };
-            auto prefetch = [&](const FpfHdr& h, int64_t pk, FpfPre& pr) {
-                // unconditional loads consumed only in the next iteration: the vmcnt wait lands there
+            auto prefetch = [&](const FpfHdr& h, int64_t pk, FpfPre& pr, int slot) {
+                // unconditional, branch-free loads consumed only in the next iteration: the vmcnt wait
+                // lands there and no exec-mask bookkeeping is spent on lane conditions
                 const uintptr_t a16 = ((uintptr_t)(c.sb + 4 * pk)) & ~(uintptr_t)15;
                 pr.raw = ld128(a16 + 16 * (uintptr_t)l);
-                pr.raw2 = make_uint4(0, 0, 0, 0);
-                if (h.b == 32 && l == 0) pr.raw2 = ld128(a16 + 1024);
                 const int32_t k = h.idx;
-                int64_t wi = 0;
-                if (k >= 2 && l < h.ce) {
-                    uint32_t xb;
-                    wi = xword(k, uniu(sm.xstart[k]), h.xcur + (uint32_t)l, xb);
-                    if (wi >= nw) wi = 0;
-                }
+                const uint32_t xs = k >= 2 ? uniu(sm.xstart[k]) : 0u;
+                uint32_t xb;
+                int64_t wi = xword(k >= 2 ? k : 2, xs, h.xcur + (uint32_t)l, xb);
+                wi = (k >= 2 && l < h.ce && wi < nw) ? wi : 0;
                 const uintptr_t xa4 = ((uintptr_t)(c.sb + 4 * wi)) & ~(uintptr_t)3;
                 const u32x3 xv = *(const g_v3*)xa4;
                 pr.x0 = xv.x;
                 pr.x1 = xv.y;
                 pr.x2 = xv.z;
+                const int32_t pb = h.bcoff - cbase;  // positions of exception e at cbuf byte pb + e
+                pr.pos = cb8[min(pb + l, 4 * 260 - 1)];
+                if (h.ce > 64) {  // rare: keep positions 64.. in LDS (the chunk may move on)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    pr.pos[q] = 0;
-                    if (h.ce > 64 * q && l + 64 * q < h.ce) pr.pos[q] = cb8[h.bcoff + l + 64 * q - cbase];
+                    for (int q = 1; q < 4; ++q)
+                        sm.u.f.posx[slot][64 * (q - 1) + l] = cb8[min(pb + l + 64 * q, 4 * 260 - 1)];
                 }
             };
             FpfHdr h;
@@ -951,10 +961,11 @@ __device__ void run_fastpfor(Ctx& c) {
             int64_t pk = p0 + 1;
             c.err = walk(0, h);
             if (!c.err && pk + 8 * h.b > nw) c.err = COVT_ERR_TRUNCATED;
-            if (!c.err) prefetch(h, pk, pre);
-            for (int32_t j = 0; j < nblocks && !c.err; ++j) {
+            if (!c.err) prefetch(h, pk, pre, 0);
+            // one block; the loop below alternates two register sets so that no in-flight prefetch
+            // register is ever copied (a copy would force the vmcnt wait at the end of the iteration)
+            auto block = [&](int32_t j, const FpfPre& pc, FpfPre& pn, int slot) {
                 const FpfHdr hc = h;
-                const FpfPre pc = pre;
                 const int64_t pkc = pk;
                 const int32_t b = hc.b;
                 // stage block j: LDS dword qoff + i = packed word i (aligned, byte-swapped)
@@ -962,8 +973,13 @@ __device__ void run_fastpfor(Ctx& c) {
                 const uint32_t sh = o & 3u;
                 const int32_t qoff = (int32_t)(o >> 2);
                 {
-                    uint32_t nxt = (uint32_t)__shfl_down((int)pc.raw.x, 1, 64);
-                    if (l == 63) nxt = lane_bcast(pc.raw2.x, 0);
+                    uint4 raw2 = make_uint4(0, 0, 0, 0);
+                    if (b == 32) {  // rare: the 16 bytes past the first KiB (same for every lane)
+                        const uintptr_t a16 = ((uintptr_t)(c.sb + 4 * pkc)) & ~(uintptr_t)15;
+                        raw2 = ld128(a16 + 1024);
+                    }
+                    const uint32_t nsh = (uint32_t)__shfl_down((int)pc.raw.x, 1, 64);
+                    const uint32_t nxt = l == 63 ? raw2.x : nsh;
                     uint4 wv;
                     wv.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.y, pc.raw.x, sh));
                     wv.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.z, pc.raw.y, sh));
@@ -972,10 +988,10 @@ __device__ void run_fastpfor(Ctx& c) {
                     ((uint4*)sm.u.f.stage)[l] = wv;
                     if (b == 32 && l == 0) {
                         uint4 w2;
-                        w2.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw2.y, pc.raw2.x, sh));
-                        w2.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw2.z, pc.raw2.y, sh));
-                        w2.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw2.w, pc.raw2.z, sh));
-                        w2.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(0u, pc.raw2.w, sh));
+                        w2.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(raw2.y, raw2.x, sh));
+                        w2.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(raw2.z, raw2.y, sh));
+                        w2.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(raw2.w, raw2.z, sh));
+                        w2.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(0u, raw2.w, sh));
                         ((uint4*)sm.u.f.stage)[64] = w2;
                     }
                 }
@@ -986,8 +1002,8 @@ __device__ void run_fastpfor(Ctx& c) {
                     c.err = walk(hc.next, h);
                     pk = pkc + 8 * b;
                     if (!c.err && pk + 8 * h.b > nw) c.err = COVT_ERR_TRUNCATED;
-                    if (c.err) break;
-                    prefetch(h, pk, pre);
+                    if (c.err) return;
+                    prefetch(h, pk, pn, slot ^ 1);
                 }
                 // unpack: lane l -> values 4l..4l+3 of miniblock l/8
                 uint32_t v[4];
@@ -1006,27 +1022,27 @@ __device__ void run_fastpfor(Ctx& c) {
                 if (hc.ce > 0) {  // out[pos] |= (index == 1 ? 1 : exceptvalue) << b
                     const int32_t k = hc.idx;
                     const uint32_t xs = k >= 2 ? uniu(sm.xstart[k]) : 0u;
-                    if (l < hc.ce) {
-                        uint32_t ex = 1u;
-                        if (k != 1) {
-                            uint32_t xbit;
-                            const int64_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
-                            const uint32_t ob = sbmis & 3u;
-                            uint64_t lo = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.x1, pc.x0, ob));
-                            uint64_t hi = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.x2, pc.x1, ob));
-                            if (wi >= nw) lo = 0;  // words past the stream read as 0
-                            if (wi + 1 >= nw || xbit + (uint32_t)k <= 32u) hi = 0;
-                            const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
-                            ex = (uint32_t)(((lo | (hi << 32)) >> xbit) & m);
-                        }
-                        atomicOr(&sm.u.f.patch[pc.pos[0]], ex << (b & 31));
+                    const bool el = l < hc.ce;
+                    uint32_t ex = 1u;
+                    if (k != 1) {  // uniform
+                        uint32_t xbit;
+                        const int64_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
+                        const uint32_t ob = sbmis & 3u;
+                        uint64_t lo = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.x1, pc.x0, ob));
+                        uint64_t hi = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.x2, pc.x1, ob));
+                        lo = wi < nw ? lo : 0ull;  // words past the stream read as 0
+                        hi = (wi + 1 < nw && xbit + (uint32_t)k > 32u) ? hi : 0ull;
+                        const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
+                        ex = (uint32_t)(((lo | (hi << 32)) >> xbit) & m);
                     }
+                    // lanes without an exception OR 0 into their own slot: no branch, no conflict
+                    atomicOr(&sm.u.f.patch[el ? pc.pos : (uint32_t)(4 * l)], el ? ex << (b & 31) : 0u);
                     if (hc.ce > 64) {  // rare: more than 64 exceptions in the block
                         for (int q = 1; q < 4; ++q) {
                             const int32_t e = l + 64 * q;
                             if (e < hc.ce) {
                                 const uint32_t ex = k == 1 ? 1u : xget(W, xs, k, hc.xcur + (uint32_t)e);
-                                atomicOr(&sm.u.f.patch[pc.pos[q]], ex << (b & 31));
+                                atomicOr(&sm.u.f.patch[sm.u.f.posx[slot][64 * (q - 1) + l]], ex << (b & 31));
                             }
                         }
                     }
@@ -1037,8 +1053,13 @@ __device__ void run_fastpfor(Ctx& c) {
                     v[2] |= pt.z;
                     v[3] |= pt.w;
                 }
-                sink_values<4>(c.op, v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, c.nb, c.out, cr);
+                sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, c.nb, c.out, cr);
                 wave_sync();
+            };
+            FpfPre preB;
+            for (int32_t j = 0; j < nblocks && !c.err; j += 2) {
+                block(j, pre, preB, 0);
+                if (j + 1 < nblocks && !c.err) block(j + 1, preB, pre, 1);
             }
             done += thissize;
             p = ie;
@@ -1054,7 +1075,7 @@ __device__ void run_fastpfor(Ctx& c) {
                 sm, c.sb, w, vpos, (int32_t)(4 * nw), c.n - L, true, c.err,
                 [&](uint32_t lo, uint32_t hi, int32_t vb, int32_t count) {
                     uint32_t vv[1] = {lo};
-                    sink_values<1>(c.op, vv, (int64_t)base + vb, count, c.nb, c.out, cr);
+                    sink_values<OP, 1>(vv, (int64_t)base + vb, count, c.nb, c.out, cr);
                 });
             decoded = L + got;
         }
@@ -1063,9 +1084,9 @@ __device__ void run_fastpfor(Ctx& c) {
     if (!c.err) {
         for (int32_t b = decoded; b < c.n; b += 64) {
             uint32_t vv[1] = {0};
-            sink_values<1>(c.op, vv, b, c.n - b < 64 ? c.n - b : 64, c.nb, c.out, cr);
+            sink_values<OP, 1>(vv, b, c.n - b < 64 ? c.n - b : 64, c.nb, c.out, cr);
         }
-        if (c.op == COVT_OP_FPF_ZZ_DELTA_XY && (c.n & 1)) c.err = COVT_ERR_COUNT_MISMATCH;
+        if (OP == COVT_OP_FPF_ZZ_DELTA_XY && (c.n & 1)) c.err = COVT_ERR_COUNT_MISMATCH;
     }
     c.consumed = c.byte_length;
 }
@@ -1110,9 +1131,22 @@ __global__ __launch_bounds__(256) void decode_family_kernel(const uint8_t* __res
         else if (c.op == COVT_OP_NONE) c.err = COVT_ERR_UNSUPPORTED_ENCODING;
         else if (c.n > 0) run_rle_int(c);
     } else if (FAM == COVT_FAMILY_VARINT) {
-        run_varint_stream(c);
+        switch (c.op) {  // one uniform switch per stream; the loops are specialised per op
+        case COVT_OP_VARINT_I32: run_varint_stream<COVT_OP_VARINT_I32>(c); break;
+        case COVT_OP_VARINT_ZZ_I32: run_varint_stream<COVT_OP_VARINT_ZZ_I32>(c); break;
+        case COVT_OP_VARINT_ZZ_DELTA_I32: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I32>(c); break;
+        case COVT_OP_VARINT_ZZ_DELTA_XY: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_XY>(c); break;
+        case COVT_OP_VARINT_DELTA_MORTON: run_varint_stream<COVT_OP_VARINT_DELTA_MORTON>(c); break;
+        case COVT_OP_VARINT_U64: run_varint_stream<COVT_OP_VARINT_U64>(c); break;
+        case COVT_OP_VARINT_I32_AS_I64: run_varint_stream<COVT_OP_VARINT_I32_AS_I64>(c); break;
+        default: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I64>(c); break;
+        }
     } else {
-        run_fastpfor(c);
+        switch (c.op) {
+        case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_I32>(c); break;
+        case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_XY>(c); break;
+        default: run_fastpfor<COVT_OP_FPF_DELTA_MORTON>(c); break;
+        }
     }
     if (lane_id() == 0) {
         covt_stream_result r;

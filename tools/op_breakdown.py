@@ -56,6 +56,28 @@ def main():
     e1.record(stream)
     torch.cuda.synchronize()
     print("all ops, families concurrent (grouped launch): %.3f ms" % (e0.elapsed_time(e1) / 5))
+    import ctypes as C
+    for fam, name in enumerate(("RLE", "VARINT", "FASTPFOR")):
+        cnt = np.zeros(3, dtype=np.int64)
+        off = int(plan.family_counts[:fam].sum())
+        n = int(plan.family_counts[fam])
+        sub = torch.from_numpy(np.ascontiguousarray(descs[off:off + n]).reshape(-1)).cuda()
+        cnt[fam] = n
+        sub_full = torch.zeros(plan.num_streams * 32, dtype=torch.uint8, device="cuda")
+        lo = int(cnt[:fam].sum())
+        sub_full[lo * 32:(lo + n) * 32] = sub
+        def go():
+            L.covt_decode_streams_device_grouped(batch.d_in.data_ptr(), sub_full.data_ptr(),
+                                                 cnt.ctypes.data_as(C.POINTER(C.c_int64)), batch.d_out.data_ptr(),
+                                                 res.data_ptr(), stream.cuda_stream)
+        go(); go()
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(5):
+            go()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        print("family %-8s alone: %.3f ms (%d streams)" % (name, e0.elapsed_time(e1) / 5, n))
     for op in sorted(set(ops.tolist())):
         m = ops == op
         sub = torch.from_numpy(np.ascontiguousarray(descs[m]).reshape(-1)).cuda()
