@@ -25,7 +25,7 @@ from typing import List, Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "libcovt.so")
+_LIB = os.path.join(_HERE, os.environ.get("COVT_LIB_VARIANT", "libcovt.so"))  # tools: libcovt_timing.so
 
 OK = 0
 ERR_UNSUPPORTED_ENCODING = -1
@@ -36,6 +36,8 @@ ERR_DEVICE = -5
 ERR_INVALID_ARG = -6
 INPUT_PADDING = 4096
 FORMAT_GENC, FORMAT_GEND = 0, 1
+FAMILY_RLE, FAMILY_VARINT, FAMILY_FASTPFOR, FAMILY_LANE = 0, 1, 2, 3
+NUM_FAMILIES = 4
 ID_FORMAT, ID_JAVA = 0, 1
 
 (OP_NONE, OP_BYTE_RLE_U8, OP_RLE_U64, OP_RLE_I32, OP_RLE_S64, OP_VARINT_I32, OP_VARINT_ZZ_I32,
@@ -352,7 +354,7 @@ class Plan:
         self.descs = np.zeros(self.num_streams * 32, dtype=np.uint8)
         if self.num_streams:
             L.covt_plan_descs(h, self.descs.ctypes.data)
-        self.family_counts = np.zeros(3, dtype=np.int64)
+        self.family_counts = np.zeros(NUM_FAMILIES, dtype=np.int64)
         L.covt_plan_family_counts(h, _ptr(self.family_counts, C.c_int64))
         self.tile_status = np.zeros(max(self.n_tiles, 1), dtype=np.int32)[:self.n_tiles]
         if self.n_tiles:

@@ -34,7 +34,12 @@ constexpr int kFpfBlock = 256;
 constexpr int kFpfPage = 65536;
 constexpr int kFpfBcCap = 3 * kFpfPage / kFpfBlock + kFpfPage;  // JavaFastPFOR byteContainer size
 
-constexpr int kMaxGroups = 256;  // RLE groups recorded per window walk
+constexpr int kLongStream = 16384;  // bytes or values: raised wave priority
+#ifdef COVT_TIMING
+constexpr int kPhases = 8;            // profiling build: per-stream phase clocks
+__device__ uint32_t* covt_phase_buf;  // [n_streams][kPhases], set by covt_debug_set_phase_buffer
+__device__ const covt_stream_desc* covt_phase_desc0;  // descriptor 0 of the launch (row index base)
+#endif
 
 // Per-wave LDS scratch.  The small fields come first so each codec family's kernel allocates only
 // the prefix it uses (kFamSmem below): varint windows, RLE windows + group tables, or FastPFOR
@@ -43,15 +48,11 @@ struct __attribute__((aligned(16))) WaveSmem {
     int32_t misc[4];
     uint16_t cpre[64];   // window index: terminators before each 16-byte chunk
     uint16_t cmask[64];  // window index: terminator mask of each chunk
-    uint32_t xstart[33]; // FastPFOR: first word of dataTobePacked[k] in the page
-    int32_t xsize[33];   // FastPFOR: its size (-1 if absent from the page's bitmap)
-    uint32_t xcnt[33];   // FastPFOR: exceptions consumed so far
     union alignas(16) {  // 16-byte aligned: uint4 (ds_*_b128) accesses
         struct {
             uint32_t win[kWin / 4 + 4];    // window bytes (+16 B slack for 12-byte reads)
             uint16_t list[kWin];           // terminator positions (window-relative)
-            uint16_t next[kWin];           // RLE: start of the next group if a header sat at j
-            uint16_t gstart[kMaxGroups];   // RLE: group starts found by the chain walk
+            uint16_t next[kWin + 8];       // RLE: start of the next group if a header sat at j (+sentinel)
         } v;
         struct {
             uint32_t stage[324];  // packed words of one FastPFOR block (<= 1024 + 15 B)
@@ -61,8 +62,8 @@ struct __attribute__((aligned(16))) WaveSmem {
         } f;
     } u;
 };
-constexpr int kSmemHdr = 672;  // offsetof(WaveSmem, u), checked below
-constexpr int kFamSmemRle = kSmemHdr + (kWin / 4 + 4) * 4 + 2 * kWin * 2 + kMaxGroups * 2;
+constexpr int kSmemHdr = 272;  // offsetof(WaveSmem, u), checked below
+constexpr int kFamSmemRle = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2 + (kWin + 8) * 2;
 constexpr int kFamSmemVarint = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2;
 constexpr int kFamSmemFpf = kSmemHdr + (324 + 256 + 260) * 4 + 384 > kFamSmemVarint
                                 ? kSmemHdr + (324 + 256 + 260) * 4 + 384
@@ -77,6 +78,10 @@ static_assert(kFamSmemRle % 16 == 0 && kFamSmemVarint % 16 == 0 && kFamSmemFpf %
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 __device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint32_t uniu(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+    const uint32_t lo = uniu((uint32_t)x), hi = uniu((uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ uint32_t lane_bcast(uint32_t x, int src) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, src);
 }
@@ -118,6 +123,24 @@ __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {  // any alignmen
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 __device__ __forceinline__ uint32_t ld_be32(const uint8_t* p) { return __builtin_bswap32(ld_le32(p)); }
+// loads from a wave-uniform address through the scalar data cache (constant address space)
+typedef __attribute__((address_space(4))) const uint32_t c_u32;
+typedef __attribute__((address_space(4))) const u32x4 c_v4;
+__device__ __forceinline__ uint32_t sld_le32(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const c_u32* q = (const c_u32*)(a & ~(uintptr_t)3);
+    const uint64_t v = ((uint64_t)q[1] << 32) | q[0];
+    return (uint32_t)(v >> (8u * (uint32_t)(a & 3u)));
+}
+__device__ __forceinline__ uint32_t sld_be32(const uint8_t* p) { return uniu(__builtin_bswap32(sld_le32(p))); }
+__device__ __forceinline__ uint4 sld128(uintptr_t a16) {
+    const u32x4 v = *(const c_v4*)a16;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+// lane l + 1's value (lane 63: 0): DPP wave_shl:1, no LDS traffic
+__device__ __forceinline__ uint32_t lane_next(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
+}
 
 // bits 7,15,23,31 of each dword -> 16-bit mask of "high bit set" bytes
 __device__ __forceinline__ uint32_t hibits4(uint32_t x) {
@@ -504,7 +527,24 @@ struct Ctx {
     uint8_t* out;       // stream output
     int32_t avail, n, nb, op, byte_length;
     int32_t err, consumed;
+#ifdef COVT_TIMING
+    uint64_t ph_last;
+    uint32_t ph[kPhases];
+#endif
 };
+// profiling build only: shader clocks spent per phase of a stream's decode
+#ifdef COVT_TIMING
+#define COVT_PHASE(c, k)                                          \
+    do {                                                          \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();         \
+        (c).ph[k] += (uint32_t)(t_ - (c).ph_last);                \
+        (c).ph_last = t_;                                         \
+    } while (0)
+#else
+#define COVT_PHASE(c, k) \
+    do {                 \
+    } while (0)
+#endif
 
 // byte q of the stream through the window (loaded on demand so that [q, q + need) is inside
 // the window unless the stream ends first); wave-uniform
@@ -586,134 +626,142 @@ __device__ void run_rle_int(Ctx& c) {
     };
     while (done < c.n && !c.err) {
         if (pos >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
+        COVT_PHASE(c, 7);
         win_load<MODE_RAW, VAL_U64>(sm, c.sb, w, pos, c.avail);
+        COVT_PHASE(c, 0);
         const int32_t woff = w.woff, K = w.K;
-        const int32_t jlo = pos - woff;
-        const int32_t vend = (c.avail - woff) < kWin ? (c.avail - woff) : kWin;  // valid window end
-        // (1) next[] for this lane's 16 positions
+        const int32_t jlo = pos - woff;  // (positions at or past the valid end rank K: no group there)
+        // (1) next[] for this lane's 16 positions, branch-free: the terminator rank of position
+        // 16l + k is R[k] (incremental popcounts of this lane's chunk mask, then the next lane's)
         {
-            const uint32_t ncpre = (uint32_t)__shfl_down((int)w.cpre, 1, 64);
-            const uint32_t ncmsk = (uint32_t)__shfl_down((int)w.cmsk, 1, 64);
-            auto rank = [&](int32_t j) -> int32_t {  // j in [16l, 16l + 32)
-                if (j >= kWin) return K;
-                const uint32_t pre = (j >> 4) == l ? w.cpre : ncpre;
-                const uint32_t msk = (j >> 4) == l ? w.cmsk : ncmsk;
-                return (int32_t)pre + __popc(msk & ((1u << (j & 15)) - 1u));
-            };
+            const uint32_t ncmsk = lane_next(w.cmsk);
+            uint32_t R[18];
+            R[0] = w.cpre;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) R[k + 1] = R[k] + ((w.cmsk >> k) & 1u);
+            R[17] = R[16] + (ncmsk & 1u);
             const uint32_t dw[4] = {w.d.x, w.d.y, w.d.z, w.d.w};
+            uint32_t nx2[8];
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const int32_t j = 16 * l + k;
-                uint32_t nx = 0xffffu;
-                if (j >= jlo && j < vend) {
-                    const uint32_t cb = (dw[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                const uint32_t cb = (dw[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                // run: the base varint ends at terminator R[k+2]; literals: the (256-cb)-th from R[k+1]
+                const uint32_t ridx = cb < 0x80u ? R[k + 2] : R[k + 1] + (0xffu - cb);
+                const uint32_t e = (uint32_t)sm.u.v.list[ridx < (uint32_t)kWin ? ridx : (uint32_t)kWin - 1] + 1u;
+                const uint32_t nx = (j >= jlo && ridx < (uint32_t)K) ? e : 0xffffu;
+                if (k & 1) nx2[k >> 1] |= nx << 16;
+                else nx2[k >> 1] = nx;
+            }
+            ((uint4*)sm.u.v.next)[2 * l] = make_uint4(nx2[0], nx2[1], nx2[2], nx2[3]);
+            ((uint4*)sm.u.v.next)[2 * l + 1] = make_uint4(nx2[4], nx2[5], nx2[6], nx2[7]);
+            if (l == 0) sm.u.v.next[kWin] = 0xffffu;  // sentinel: a group ending at the window end
+        }
+        wave_sync();
+        COVT_PHASE(c, 1);
+        // (2) chain walk, 64 groups at a time (lane g of `gs` = start of group g), (3) each batch
+        // expanded right away: small groups one per lane, groups of more than 8 values by the wave
+        int32_t pj = jlo, out = done;
+        bool first = true;
+        while (true) {
+            int32_t G = 0;
+            uint32_t gs = 0;
+            const int32_t out0 = out;
+            while (G < 64 && out < c.n) {
+                const uint32_t nx = uniu(sm.u.v.next[pj]);
+                const uint32_t cb = uniu(win_byte(sm, pj));
+                if (nx == 0xffffu) break;
+                gs = l == G ? (uint32_t)pj : gs;
+                ++G;
+                out += cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb;
+                pj = (int32_t)nx;
+            }
+            COVT_PHASE(c, 2);
+            if (G == 0) {
+                if (!first) break;
+                // the group at pos does not complete inside this window
+                const uint32_t cb = uniu(win_byte(sm, jlo));
+                const int32_t aligned = (int32_t)(((uintptr_t)(c.sb + pos) & ~(uintptr_t)15) - (uintptr_t)c.sb);
+                if (cb >= 0x80u && woff == aligned && woff + kWin < c.avail) {
+                    // a literal group longer than a window (up to 128 x 10 B): multi-window varint path
+                    const int32_t cnt = 0x100 - (int32_t)cb, lim = c.n - done, d0 = done;
+                    int32_t p1 = pos + 1;
+                    varint_take<MODE_RAW, VAL_U64>(sm, c.sb, w, p1, c.avail, cnt, false, c.err,
+                                                   [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
+                                                       const int32_t k = base + l;
+                                                       if (l < count && k < lim) store(d0 + k, ((uint64_t)hi << 32) | lo);
+                                                   });
+                    out = done + (cnt < lim ? cnt : lim);
+                    pj = p1 - woff;
+                    COVT_PHASE(c, 5);
+                    break;
+                }
+                c.err = (woff + kWin >= c.avail) ? COVT_ERR_TRUNCATED : COVT_ERR_BAD_HEADER;
+                break;
+            }
+            first = false;
+            {
+                const bool gv = l < G;
+                const int32_t pg = gv ? (int32_t)gs : 0;
+                const uint32_t cb = gv ? win_byte(sm, pg) : 0u;
+                const int32_t cnt = !gv ? 0 : (cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb);
+                const uint32_t inc = incl_scan((uint32_t)cnt);
+                const int32_t goff = out0 + (int32_t)(inc - (uint32_t)cnt);
+                int32_t take = c.n - goff;
+                take = take < 0 ? 0 : (take > cnt ? cnt : take);
+                const bool big = take > 8;
+                if (gv && !big && take > 0) {
                     if (cb < 0x80u) {
-                        if (j + 2 < vend) {
-                            const int32_t r = rank(j + 2);
-                            if (r < K) nx = (uint32_t)sm.u.v.list[r] + 1u;
+                        const int32_t delta = (int32_t)(int8_t)win_byte(sm, pg + 1);
+                        const int32_t r = rank_rel(sm, pg + 2, K);
+                        const uint64_t raw = win_vulong(sm, pg + 2, sm.u.v.list[r]);
+                        const int64_t b64 = is_signed ? zz64(raw) : (int64_t)raw;
+                        for (int32_t i = 0; i < take; ++i) {
+                            const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
+                            if (to_i32) ((int32_t*)c.out)[goff + i] = (int32_t)v;
+                            else ((int64_t*)c.out)[goff + i] = v;
                         }
                     } else {
-                        const int32_t r = rank(j + 1), nn = 0x100 - (int32_t)cb;
-                        if (j + 1 < vend && r + nn <= K) nx = (uint32_t)sm.u.v.list[r + nn - 1] + 1u;
+                        const int32_t r = rank_rel(sm, pg + 1, K);
+                        int32_t sj = pg + 1;
+                        for (int32_t i = 0; i < take; ++i) {
+                            const int32_t ej = sm.u.v.list[r + i];
+                            store(goff + i, win_vulong(sm, sj, ej));
+                            sj = ej + 1;
+                        }
                     }
                 }
-                sm.u.v.next[j] = (uint16_t)nx;
-            }
-        }
-        wave_sync();
-        // (2) chain walk
-        int32_t pj = jlo, G = 0, out = done;
-        while (out < c.n && G < kMaxGroups && pj < vend) {
-            const uint32_t nx = uniu(sm.u.v.next[pj]);
-            if (nx == 0xffffu) break;
-            const uint32_t cb = uniu(win_byte(sm, pj));
-            if (l == 0) sm.u.v.gstart[G] = (uint16_t)pj;
-            ++G;
-            out += cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb;
-            pj = (int32_t)nx;
-        }
-        wave_sync();
-        if (G == 0) {
-            // the group at pos does not complete inside this window
-            const uint32_t cb = uniu(win_byte(sm, jlo));
-            const int32_t aligned = (int32_t)(((uintptr_t)(c.sb + pos) & ~(uintptr_t)15) - (uintptr_t)c.sb);
-            if (cb >= 0x80u && woff == aligned && woff + kWin < c.avail) {
-                // a literal group longer than a window (up to 128 x 10 B): multi-window varint path
-                const int32_t cnt = 0x100 - (int32_t)cb, lim = c.n - done, d0 = done;
-                pos += 1;
-                varint_take<MODE_RAW, VAL_U64>(sm, c.sb, w, pos, c.avail, cnt, false, c.err,
-                                               [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
-                                                   const int32_t k = base + l;
-                                                   if (l < count && k < lim) store(d0 + k, ((uint64_t)hi << 32) | lo);
-                                               });
-                done += cnt < lim ? cnt : lim;
-                continue;
-            }
-            c.err = (woff + kWin >= c.avail) ? COVT_ERR_TRUNCATED : COVT_ERR_BAD_HEADER;
-            break;
-        }
-        // (3) expansion
-        int32_t base_out = done;
-        for (int32_t gb = 0; gb < G; gb += 64) {
-            const int32_t g = gb + l;
-            const bool gv = g < G;
-            const int32_t pg = gv ? (int32_t)sm.u.v.gstart[g] : 0;
-            const uint32_t cb = gv ? win_byte(sm, pg) : 0u;
-            const int32_t cnt = !gv ? 0 : (cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb);
-            const uint32_t inc = incl_scan((uint32_t)cnt);
-            const int32_t goff = base_out + (int32_t)(inc - (uint32_t)cnt);
-            int32_t take = c.n - goff;
-            take = take < 0 ? 0 : (take > cnt ? cnt : take);
-            const bool big = take > 8;
-            if (gv && !big && take > 0) {
-                if (cb < 0x80u) {
-                    const int32_t delta = (int32_t)(int8_t)win_byte(sm, pg + 1);
-                    const int32_t r = rank_rel(sm, pg + 2, K);
-                    const uint64_t raw = win_vulong(sm, pg + 2, sm.u.v.list[r]);
-                    const int64_t b64 = is_signed ? zz64(raw) : (int64_t)raw;
-                    for (int32_t i = 0; i < take; ++i) {
-                        const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
-                        if (to_i32) ((int32_t*)c.out)[goff + i] = (int32_t)v;
-                        else ((int64_t*)c.out)[goff + i] = v;
-                    }
-                } else {
-                    const int32_t r = rank_rel(sm, pg + 1, K);
-                    int32_t sj = pg + 1;
-                    for (int32_t i = 0; i < take; ++i) {
-                        const int32_t ej = sm.u.v.list[r + i];
-                        store(goff + i, win_vulong(sm, sj, ej));
-                        sj = ej + 1;
+                COVT_PHASE(c, 3);
+                uint64_t bigm = __ballot(gv && big);
+                while (bigm) {  // wave-uniform loop over the big groups of this batch
+                    const int src = __ffsll((long long)bigm) - 1;
+                    bigm &= bigm - 1;
+                    const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
+                    const uint32_t c2 = lane_bcast(cb, src);
+                    const int32_t o2 = (int32_t)lane_bcast((uint32_t)goff, src);
+                    const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
+                    if (c2 < 0x80u) {
+                        const int32_t delta = (int32_t)(int8_t)win_byte(sm, p2 + 1);
+                        const int32_t r = rank_rel(sm, p2 + 2, K);
+                        const uint64_t raw = win_vulong(sm, p2 + 2, sm.u.v.list[r]);
+                        const int64_t b64 = is_signed ? zz64(raw) : (int64_t)raw;
+                        for (int32_t i = l; i < t2; i += 64) {  // literals[0] + used * delta
+                            const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
+                            if (to_i32) ((int32_t*)c.out)[o2 + i] = (int32_t)v;
+                            else ((int64_t*)c.out)[o2 + i] = v;
+                        }
+                    } else {
+                        const int32_t r = rank_rel(sm, p2 + 1, K);
+                        for (int32_t i = l; i < t2; i += 64) {
+                            const int32_t ej = sm.u.v.list[r + i];
+                            const int32_t sj = i == 0 ? p2 + 1 : (int32_t)sm.u.v.list[r + i - 1] + 1;
+                            store(o2 + i, win_vulong(sm, sj, ej));
+                        }
                     }
                 }
+                COVT_PHASE(c, 4);
             }
-            uint64_t bigm = __ballot(gv && big);
-            while (bigm) {  // wave-uniform loop over the big groups of this chunk
-                const int src = __ffsll((long long)bigm) - 1;
-                bigm &= bigm - 1;
-                const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
-                const uint32_t c2 = lane_bcast(cb, src);
-                const int32_t o2 = (int32_t)lane_bcast((uint32_t)goff, src);
-                const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
-                if (c2 < 0x80u) {
-                    const int32_t delta = (int32_t)(int8_t)win_byte(sm, p2 + 1);
-                    const int32_t r = rank_rel(sm, p2 + 2, K);
-                    const uint64_t raw = win_vulong(sm, p2 + 2, sm.u.v.list[r]);
-                    const int64_t b64 = is_signed ? zz64(raw) : (int64_t)raw;
-                    for (int32_t i = l; i < t2; i += 64) {  // literals[0] + used * delta
-                        const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
-                        if (to_i32) ((int32_t*)c.out)[o2 + i] = (int32_t)v;
-                        else ((int64_t*)c.out)[o2 + i] = v;
-                    }
-                } else {
-                    const int32_t r = rank_rel(sm, p2 + 1, K);
-                    for (int32_t i = l; i < t2; i += 64) {
-                        const int32_t ej = sm.u.v.list[r + i];
-                        const int32_t sj = i == 0 ? p2 + 1 : (int32_t)sm.u.v.list[r + i - 1] + 1;
-                        store(o2 + i, win_vulong(sm, sj, ej));
-                    }
-                }
-            }
-            base_out += (int32_t)lane_bcast(inc, 63);
+            if (G < 64 || out >= c.n) break;
         }
         done = out < c.n ? out : c.n;
         pos = woff + pj;
@@ -733,35 +781,38 @@ __device__ void run_rle_byte(Ctx& c) {
     bool bad = false;
     while (done < c.n && !c.err) {
         if (pos >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
+        COVT_PHASE(c, 7);
         win_load<MODE_RAW, VAL_U64>(sm, c.sb, w, pos, c.avail);
+        COVT_PHASE(c, 0);
         const int32_t woff = w.woff;
         const int32_t vend = (c.avail - woff) < kWin ? (c.avail - woff) : kWin;
-        int32_t pj = pos - woff, G = 0, out = done;
-        while (out < c.n && G < kMaxGroups) {
-            const uint32_t cb = uniu(win_byte(sm, pj));
-            const int32_t nx = cb < 0x80u ? pj + 2 : pj + 1 + 0x100 - (int32_t)cb;
-            if (nx > vend) break;
-            if (l == 0) sm.u.v.gstart[G] = (uint16_t)pj;
-            ++G;
-            out += cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb;
-            pj = nx;
-            if (pj >= vend) break;
-        }
-        wave_sync();
-        if (G == 0) {
-            c.err = (woff + kWin >= c.avail) ? COVT_ERR_TRUNCATED : COVT_ERR_BAD_HEADER;
-            break;
-        }
-        int32_t base_out = done;
-        bool lbad = false;
-        for (int32_t gb = 0; gb < G; gb += 64) {
-            const int32_t g = gb + l;
-            const bool gv = g < G;
-            const int32_t pg = gv ? (int32_t)sm.u.v.gstart[g] : 0;
+        int32_t pj = pos - woff, out = done;
+        bool lbad = false, first = true;
+        while (true) {  // 64 groups at a time (lane g of `gs` = start of group g), each batch expanded
+            int32_t G = 0;
+            uint32_t gs = 0;
+            const int32_t out0 = out;
+            while (G < 64 && out < c.n && pj < vend) {
+                const uint32_t cb = uniu(win_byte(sm, pj));
+                const int32_t nx = cb < 0x80u ? pj + 2 : pj + 1 + 0x100 - (int32_t)cb;
+                if (nx > vend) break;
+                gs = l == G ? (uint32_t)pj : gs;
+                ++G;
+                out += cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb;
+                pj = nx;
+            }
+            COVT_PHASE(c, 2);
+            if (G == 0) {
+                if (first) c.err = (woff + kWin >= c.avail) ? COVT_ERR_TRUNCATED : COVT_ERR_BAD_HEADER;
+                break;
+            }
+            first = false;
+            const bool gv = l < G;
+            const int32_t pg = gv ? (int32_t)gs : 0;
             const uint32_t cb = gv ? win_byte(sm, pg) : 0u;
             const int32_t cnt = !gv ? 0 : (cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb);
             const uint32_t inc = incl_scan((uint32_t)cnt);
-            const int32_t goff = base_out + (int32_t)(inc - (uint32_t)cnt);
+            const int32_t goff = out0 + (int32_t)(inc - (uint32_t)cnt);
             int32_t take = c.n - goff;
             take = take < 0 ? 0 : (take > cnt ? cnt : take);
             const bool big = take > 8;
@@ -772,6 +823,7 @@ __device__ void run_rle_byte(Ctx& c) {
                     lbad |= v > 5u;
                 }
             }
+            COVT_PHASE(c, 3);
             uint64_t bigm = __ballot(gv && big);
             while (bigm) {
                 const int src = __ffsll((long long)bigm) - 1;
@@ -786,7 +838,8 @@ __device__ void run_rle_byte(Ctx& c) {
                     lbad |= v > 5u;
                 }
             }
-            base_out += (int32_t)lane_bcast(inc, 63);
+            COVT_PHASE(c, 4);
+            if (G < 64 || out >= c.n || pj >= vend) break;
         }
         bad |= __any(lbad);
         done = out < c.n ? out : c.n;
@@ -802,6 +855,9 @@ struct Words {
     const uint8_t* sb;
     int32_t nw;
     __device__ __forceinline__ uint32_t operator()(int64_t i) const { return ld_be32(sb + 4 * i); }
+    // word i at a wave-uniform index, through the scalar cache (s_load; no vmcnt wait on the stores
+    // in flight)
+    __device__ __forceinline__ uint32_t uniform(int64_t i) const { return sld_be32(sb + 4 * i); }
 };
 
 // exception value X[k][i] (dataTobePacked[k]); words past the stream read as 0
@@ -850,78 +906,102 @@ __device__ void run_fastpfor(Ctx& c) {
     int32_t decoded = 0;
     int32_t L = 0;
     int64_t p = 1;
+    int xs_v = 0, xz_v = -1, xc_v = 0;  // lane k: dataTobePacked[k] start word, size, values consumed
     if (c.byte_length > c.avail) { c.err = COVT_ERR_TRUNCATED; }
     if (!c.err && nw > 0) {
-        L = (int32_t)uniu(W(0));
+        L = (int32_t)W.uniform(0);
         if (L < 0) c.err = COVT_ERR_BAD_HEADER;
         L -= L % kFpfBlock;
         if (!c.err && L > c.n) c.err = COVT_ERR_COUNT_MISMATCH;
         int32_t done = 0;
+        // 1 KiB of stream words from word w on the 16-byte grid, byte-swapped into dst[]:
+        // dst[m] = W(base + m) for m < 255, base = w - (0..3) returned.  One 16-byte load per lane.
+        auto load_words = [&](uint32_t* dst, int64_t w) -> int64_t {
+            const uintptr_t addr = (uintptr_t)(c.sb + 4 * w);
+            const uintptr_t a16 = addr & ~(uintptr_t)15;
+            const uint32_t o = (uint32_t)(addr & 15u), sh = o & 3u;
+            const uint4 r = ld128(a16 + 16 * (uintptr_t)l);
+            const uint32_t nx = lane_next(r.x);
+            uint4 wv;
+            wv.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(r.y, r.x, sh));
+            wv.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(r.z, r.y, sh));
+            wv.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(r.w, r.z, sh));
+            wv.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(nx, r.w, sh));
+            wave_sync();
+            ((uint4*)dst)[l] = wv;
+            wave_sync();
+            return uni64(w - (int64_t)(o >> 2));
+        };
         while (!c.err && done < L) {
-            const int32_t thissize = (L - done) < kFpfPage ? (L - done) : kFpfPage;
-            const int64_t p0 = p;
+            done = uni(done);
+            const int32_t thissize = uni((L - done) < kFpfPage ? (L - done) : kFpfPage);
+            const int64_t p0 = uni64(p);
             if (p0 >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
-            int64_t ie = p0 + (int32_t)uniu(W(p0));
+            int64_t ie = p0 + (int32_t)W.uniform(p0);
             if (ie < 0 || ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
-            const int32_t bytesize = (int32_t)uniu(W(ie++));
+            const int32_t bytesize = (int32_t)W.uniform(ie++);
             if (bytesize < 0 || bytesize > kFpfBcCap) { c.err = COVT_ERR_BAD_HEADER; break; }
             const int64_t bcw = (bytesize + 3) / 4;
             const int64_t bc = ie;
             if (bc + bcw >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
             ie += bcw;
-            const uint32_t bitmap = uniu(W(ie++));
-            for (int k = 2; k <= 32 && !c.err; ++k) {
-                int32_t size = -1;
-                uint32_t xs = 0;
-                if (bitmap & (1u << (k - 1))) {
-                    if (ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
-                    size = (int32_t)uniu(W(ie++));
-                    if (size < 0) { c.err = COVT_ERR_BAD_HEADER; break; }
-                    const int64_t groups = ((int64_t)size + 31) / 32;
-                    xs = (uint32_t)ie;
-                    ie += groups * k;
-                    ie -= ((groups * 32 - size) * k) / 32;
-                }
-                if (l == 0) { sm.xstart[k] = xs; sm.xsize[k] = size; sm.xcnt[k] = 0; }
+            // exception-array directory (bitmap, then size + packed words per set bit), parsed from a
+            // 1 KiB LDS window of words; the arrays' start/size/cursor live in lanes 2..32 of VGPRs
+            int64_t dbase = load_words(sm.u.f.stage, ie);
+            auto dword = [&](int64_t w) -> uint32_t {
+                if (w < dbase || w >= dbase + 255) dbase = load_words(sm.u.f.stage, w);
+                return uniu(sm.u.f.stage[w - dbase]);
+            };
+            uint32_t bm = dword(ie++) & ~1u;  // bit k-1 set: dataTobePacked[k] present (k >= 2)
+            xs_v = 0;
+            xz_v = -1;
+            xc_v = 0;
+            while (bm) {
+                const int32_t k = __builtin_ctz(bm) + 1;
+                bm &= bm - 1;
+                if (ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+                const int32_t size = (int32_t)dword(ie++);
+                if (size < 0) { c.err = COVT_ERR_BAD_HEADER; break; }
+                const int64_t groups = ((int64_t)size + 31) / 32;
+                xs_v = l == k ? (int)(uint32_t)ie : xs_v;
+                xz_v = l == k ? size : xz_v;
+                ie += groups * k;
+                ie -= ((groups * 32 - size) * k) / 32;
             }
             if (c.err) break;
-            wave_sync();
-            const int32_t nblocks = thissize / kFpfBlock;
-            const int32_t bclen = (int32_t)(bcw * 4);
+            COVT_PHASE(c, 0);
+            const int32_t nblocks = uni(thissize / kFpfBlock);
+            const int32_t bclen = uni((int32_t)(bcw * 4));
             const uint8_t* cb8 = (const uint8_t*)sm.u.f.cbuf;
             int32_t cbase = INT32_MIN / 2;
-            auto chunk_load = [&](int32_t at) {  // container bytes [at, at + 1024), at % 4 == 0
-                cbase = at;
-                const int64_t w0 = bc + at / 4 + 4 * l;
-                uint4 d;
-                d.x = (w0 + 0 < bc + bcw) ? W(w0 + 0) : 0u;  // LE bytes of the BE words = container bytes
-                d.y = (w0 + 1 < bc + bcw) ? W(w0 + 1) : 0u;
-                d.z = (w0 + 2 < bc + bcw) ? W(w0 + 2) : 0u;
-                d.w = (w0 + 3 < bc + bcw) ? W(w0 + 3) : 0u;
-                wave_sync();
-                ((uint4*)sm.u.f.cbuf)[l] = d;
-                wave_sync();
+            auto chunk_load = [&](int32_t at) {  // container bytes [cbase, cbase + 1020), cbase in (at - 16, at]
+                cbase = (int32_t)(4 * (load_words(sm.u.f.cbuf, bc + (at >> 2)) - bc));
             };
             auto walk = [&](int32_t cur, FpfHdr& h) -> int32_t {
+                cur = uni(cur);  // header state is wave-uniform: keep it in SGPRs, branches scalar
+                cbase = uni(cbase);
                 if (cur + 2 > bclen) return COVT_ERR_BAD_HEADER;
-                if (cur < cbase || cur + 3 > cbase + kWin) chunk_load(cur & ~3);
-                h.b = (int32_t)(int8_t)uniu(cb8[cur - cbase]);
-                h.ce = (int32_t)uniu(cb8[cur + 1 - cbase]);
+                if (cur < cbase || cur + 4 > cbase + 1020) chunk_load(cur);
+                const int32_t j = cur - cbase;  // container bytes cur..cur+3 (b, exceptions, maxbits)
+                const uint32_t hw =
+                    uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(j >> 2) + 1], sm.u.f.cbuf[j >> 2], (uint32_t)j & 3u));
+                h.b = (int32_t)(int8_t)(hw & 0xffu);
+                h.ce = (int32_t)((hw >> 8) & 0xffu);
                 if (h.b < 0 || h.b > 32) return COVT_ERR_BAD_HEADER;
                 h.idx = 0;
                 h.xcur = 0;
                 h.bcoff = cur + 2;
                 if (h.ce > 0) {
                     if (cur + 3 + h.ce > bclen) return COVT_ERR_BAD_HEADER;
-                    if (cur + 3 + h.ce > cbase + kWin) chunk_load(cur & ~3);
-                    h.idx = (int32_t)(int8_t)uniu(cb8[cur + 2 - cbase]) - h.b;
+                    if (cur + 3 + h.ce > cbase + 1020) chunk_load(cur);
+                    h.idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - h.b;
                     h.bcoff = cur + 3;
                     if (h.idx != 1) {
                         if (h.idx < 2 || h.idx > 32) return COVT_ERR_BAD_HEADER;
-                        const int32_t xsz = uni(sm.xsize[h.idx]);
-                        h.xcur = uniu(sm.xcnt[h.idx]);
+                        const int32_t xsz = __builtin_amdgcn_readlane(xz_v, h.idx);
+                        h.xcur = (uint32_t)__builtin_amdgcn_readlane(xc_v, h.idx);
                         if (xsz < 0 || (int64_t)h.xcur + h.ce > xsz) return COVT_ERR_BAD_HEADER;
-                        if (l == 0) sm.xcnt[h.idx] = h.xcur + (uint32_t)h.ce;
+                        xc_v = l == h.idx ? (int)(h.xcur + (uint32_t)h.ce) : xc_v;
                     }
                 }
                 h.next = h.bcoff + h.ce;
@@ -933,13 +1013,19 @@ __device__ void run_fastpfor(Ctx& c) {
                 xbit = bit & 31u;
                 return (int64_t)xs + (int64_t)(i >> 5) * k + (bit >> 5);
             };
-            auto prefetch = [&](const FpfHdr& h, int64_t pk, FpfPre& pr, int slot) {
+            auto prefetch = [&](const FpfHdr& hv, int64_t pkv, FpfPre& pr, int slot) {
+                FpfHdr h;
+                h.idx = uni(hv.idx);
+                h.ce = uni(hv.ce);
+                h.xcur = uniu(hv.xcur);
+                h.bcoff = uni(hv.bcoff);
+                const int64_t pk = uni64(pkv);
                 // unconditional, branch-free loads consumed only in the next iteration: the vmcnt wait
                 // lands there and no exec-mask bookkeeping is spent on lane conditions
                 const uintptr_t a16 = ((uintptr_t)(c.sb + 4 * pk)) & ~(uintptr_t)15;
                 pr.raw = ld128(a16 + 16 * (uintptr_t)l);
                 const int32_t k = h.idx;
-                const uint32_t xs = k >= 2 ? uniu(sm.xstart[k]) : 0u;
+                const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
                 uint32_t xb;
                 int64_t wi = xword(k >= 2 ? k : 2, xs, h.xcur + (uint32_t)l, xb);
                 wi = (k >= 2 && l < h.ce && wi < nw) ? wi : 0;
@@ -965,8 +1051,14 @@ __device__ void run_fastpfor(Ctx& c) {
             // one block; the loop below alternates two register sets so that no in-flight prefetch
             // register is ever copied (a copy would force the vmcnt wait at the end of the iteration)
             auto block = [&](int32_t j, const FpfPre& pc, FpfPre& pn, int slot) {
-                const FpfHdr hc = h;
-                const int64_t pkc = pk;
+                FpfHdr hc;
+                hc.b = uni(h.b);
+                hc.ce = uni(h.ce);
+                hc.idx = uni(h.idx);
+                hc.xcur = uniu(h.xcur);
+                hc.bcoff = uni(h.bcoff);
+                hc.next = uni(h.next);
+                const int64_t pkc = uni64(pk);
                 const int32_t b = hc.b;
                 // stage block j: LDS dword qoff + i = packed word i (aligned, byte-swapped)
                 const uint32_t o = (sbmis + 4u * (uint32_t)pkc) & 15u;
@@ -974,11 +1066,11 @@ __device__ void run_fastpfor(Ctx& c) {
                 const int32_t qoff = (int32_t)(o >> 2);
                 {
                     uint4 raw2 = make_uint4(0, 0, 0, 0);
-                    if (b == 32) {  // rare: the 16 bytes past the first KiB (same for every lane)
+                    if (b == 32) {  // rare: the 16 bytes past the first KiB (same for every lane; scalar load)
                         const uintptr_t a16 = ((uintptr_t)(c.sb + 4 * pkc)) & ~(uintptr_t)15;
-                        raw2 = ld128(a16 + 1024);
+                        raw2 = sld128(a16 + 1024);
                     }
-                    const uint32_t nsh = (uint32_t)__shfl_down((int)pc.raw.x, 1, 64);
+                    const uint32_t nsh = lane_next(pc.raw.x);
                     const uint32_t nxt = l == 63 ? raw2.x : nsh;
                     uint4 wv;
                     wv.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.y, pc.raw.x, sh));
@@ -997,14 +1089,18 @@ __device__ void run_fastpfor(Ctx& c) {
                 }
                 if (hc.ce > 0) ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
                 wave_sync();
-                // walk block j+1 and put its loads in flight
+                COVT_PHASE(c, 1);
+                // walk block j+1 and put its loads in flight.  The loads are issued unconditionally (the
+                // last block re-reads its own words) so that every path has the same number of memory
+                // ops in flight and the waits for this block's exception words stay partial.
                 if (j + 1 < nblocks) {
                     c.err = walk(hc.next, h);
                     pk = pkc + 8 * b;
                     if (!c.err && pk + 8 * h.b > nw) c.err = COVT_ERR_TRUNCATED;
                     if (c.err) return;
-                    prefetch(h, pk, pn, slot ^ 1);
                 }
+                prefetch(h, pk, pn, slot ^ 1);
+                COVT_PHASE(c, 2);
                 // unpack: lane l -> values 4l..4l+3 of miniblock l/8
                 uint32_t v[4];
                 {
@@ -1019,9 +1115,10 @@ __device__ void run_fastpfor(Ctx& c) {
                         bit += (uint32_t)b;
                     }
                 }
+                COVT_PHASE(c, 3);
                 if (hc.ce > 0) {  // out[pos] |= (index == 1 ? 1 : exceptvalue) << b
                     const int32_t k = hc.idx;
-                    const uint32_t xs = k >= 2 ? uniu(sm.xstart[k]) : 0u;
+                    const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
                     const bool el = l < hc.ce;
                     uint32_t ex = 1u;
                     if (k != 1) {  // uniform
@@ -1053,8 +1150,10 @@ __device__ void run_fastpfor(Ctx& c) {
                     v[2] |= pt.z;
                     v[3] |= pt.w;
                 }
+                COVT_PHASE(c, 4);
                 sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, c.nb, c.out, cr);
                 wave_sync();
+                COVT_PHASE(c, 5);
             };
             FpfPre preB;
             for (int32_t j = 0; j < nblocks && !c.err; j += 2) {
@@ -1088,6 +1187,7 @@ __device__ void run_fastpfor(Ctx& c) {
         }
         if (OP == COVT_OP_FPF_ZZ_DELTA_XY && (c.n & 1)) c.err = COVT_ERR_COUNT_MISMATCH;
     }
+    COVT_PHASE(c, 6);
     c.consumed = c.byte_length;
 }
 
@@ -1112,7 +1212,12 @@ __global__ __launch_bounds__(256) void decode_family_kernel(const uint8_t* __res
     const int64_t sid = (int64_t)blockIdx.x * kWavesPerBlock + wv;
     if (sid >= n_streams) return;
     const covt_stream_desc d = descs[sid];
-    if (op_family(d.op) != FAM) return;
+    if ((d.flags & COVT_DESC_LANE) || op_family(d.op) != FAM) return;
+    // long streams are the kernel's critical path: let their waves win instruction arbitration
+    if (d.byte_length > kLongStream || d.num_values > kLongStream) __builtin_amdgcn_s_setprio(2);
+#ifdef COVT_TIMING  // profiling build (libcovt_timing.so): result = (duration, start) in 100 MHz ticks
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     Ctx c;
     c.sm = (WaveSmem*)(smem + wv * kStride);
     c.sb = in + d.in_off;
@@ -1124,6 +1229,10 @@ __global__ __launch_bounds__(256) void decode_family_kernel(const uint8_t* __res
     c.byte_length = d.byte_length;
     c.err = 0;
     c.consumed = 0;
+#ifdef COVT_TIMING
+    c.ph_last = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k < kPhases; ++k) c.ph[k] = 0;
+#endif
     if (c.n < 0 || c.avail < 0 || c.byte_length < 0) {
         c.err = COVT_ERR_INVALID_ARG;
     } else if (FAM == COVT_FAMILY_RLE) {
@@ -1152,8 +1261,157 @@ __global__ __launch_bounds__(256) void decode_family_kernel(const uint8_t* __res
         covt_stream_result r;
         r.status = c.err;
         r.consumed = c.consumed;
+#ifdef COVT_TIMING
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        r.status = c.err ? -1 : (int32_t)(t_end - t_start);
+        r.consumed = (int32_t)(uint32_t)t_start;
+        if (covt_phase_buf)
+            for (int k = 0; k < kPhases; ++k) covt_phase_buf[(descs + sid - covt_phase_desc0) * kPhases + k] = c.ph[k];
+#endif
         res[sid] = r;
     }
+}
+
+// --------------------------------------------------------------------------------------------
+// lane-per-stream path: small RLE streams (<= kLaneMaxValues values, flagged by the plan), one
+// stream per lane, decoded serially the way RunLengthIntegerReader / RunLengthByteReader read them.
+// A wave-per-stream decode spends its fixed window/index setup on a handful of values; here 64
+// such streams share one wave's instructions.
+// --------------------------------------------------------------------------------------------
+constexpr int kLaneSlot = 17;  // LDS dwords per lane: a stream of <= kLaneMaxBytes bytes + misalignment
+static_assert(4 * kLaneSlot >= kLaneMaxBytes + 4, "lane slot");
+struct LaneBytes {  // the lane's stream staged in its LDS slot; sequential reads with a one-dword cache
+    const uint32_t* slot;
+    uint32_t mis;  // stream start within slot dword 0
+    int32_t avail;
+    int32_t cq;
+    uint32_t cw;
+    __device__ __forceinline__ uint32_t at(int32_t p) {
+        const int32_t a = p + (int32_t)mis, q = a >> 2;
+        if (q != cq) {
+            cq = q;
+            cw = slot[q * 256];
+        }
+        return (cw >> (8u * (uint32_t)(a & 3))) & 0xffu;
+    }
+};
+// orc SerializationUtils.readVulong (shift masked to 6 bits)
+__device__ __forceinline__ int32_t lane_vulong(LaneBytes& in, int32_t& p, uint64_t& v) {
+    uint64_t r = 0;
+    uint32_t sh = 0, b;
+    do {
+        if (p >= in.avail) return COVT_ERR_TRUNCATED;
+        b = in.at(p++);
+        r |= (uint64_t)(b & 0x7fu) << (sh & 63u);
+        sh += 7;
+    } while (b & 0x80u);
+    v = r;
+    return COVT_OK;
+}
+__device__ void lane_rle_int(LaneBytes& in, int op, int32_t n, uint8_t* out, int32_t& err, int32_t& consumed) {
+    const bool is_signed = op == COVT_OP_RLE_S64, to_i32 = op == COVT_OP_RLE_I32;
+    int32_t o = 0, done = 0;
+    auto put = [&](int64_t v) {
+        if (to_i32) ((int32_t*)out)[done] = (int32_t)v;
+        else ((int64_t*)out)[done] = v;
+        ++done;
+    };
+    while (done < n) {
+        if (o >= in.avail) { err = COVT_ERR_TRUNCATED; return; }
+        const uint32_t control = in.at(o++);
+        if (control < 0x80u) {  // run: control + 3 values base + i * delta
+            const int32_t cnt = (int32_t)control + 3;
+            if (o >= in.avail) { err = COVT_ERR_TRUNCATED; return; }
+            const int32_t delta = (int32_t)(int8_t)in.at(o++);
+            uint64_t raw;
+            if ((err = lane_vulong(in, o, raw))) return;
+            const int64_t b = is_signed ? zz64(raw) : (int64_t)raw;
+            const int32_t k = cnt < n - done ? cnt : n - done;
+            for (int32_t i = 0; i < k; ++i) put((int64_t)((uint64_t)b + (uint64_t)(int64_t)(int32_t)(i * delta)));
+        } else {  // literals: 256 - control varints, all read even past n
+            const int32_t cnt = 0x100 - (int32_t)control;
+            for (int32_t i = 0; i < cnt; ++i) {
+                uint64_t raw;
+                if ((err = lane_vulong(in, o, raw))) return;
+                if (done < n) put(is_signed ? zz64(raw) : (int64_t)raw);
+            }
+        }
+    }
+    consumed = o;
+}
+__device__ void lane_rle_byte(LaneBytes& in, int32_t n, uint8_t* out, int32_t& err, int32_t& consumed) {
+    int32_t o = 0, done = 0;
+    bool bad = false;
+    while (done < n) {
+        if (o >= in.avail) { err = COVT_ERR_TRUNCATED; return; }
+        const uint32_t control = in.at(o++);
+        if (control < 0x80u) {
+            const int32_t cnt = (int32_t)control + 3;
+            if (o >= in.avail) { err = COVT_ERR_TRUNCATED; return; }
+            const uint32_t b = in.at(o++);
+            bad |= b > 5u;
+            const int32_t k = cnt < n - done ? cnt : n - done;
+            for (int32_t i = 0; i < k; ++i) out[done++] = (uint8_t)b;
+        } else {
+            const int32_t cnt = 0x100 - (int32_t)control;
+            if (o + cnt > in.avail) { err = COVT_ERR_TRUNCATED; return; }
+            for (int32_t i = 0; i < cnt; ++i) {
+                const uint32_t b = in.at(o++);
+                if (done < n) {
+                    bad |= b > 5u;
+                    out[done++] = (uint8_t)b;
+                }
+            }
+        }
+    }
+    if (bad) err = COVT_ERR_BAD_HEADER;  // GeometryType.values()[b]
+    consumed = o;
+}
+
+__global__ __launch_bounds__(256) void decode_lane_kernel(const uint8_t* __restrict__ in,
+                                                          const covt_stream_desc* __restrict__ descs,
+                                                          int64_t n_streams, uint8_t* __restrict__ out,
+                                                          covt_stream_result* __restrict__ res) {
+    __shared__ uint32_t slots[256 * kLaneSlot];
+    const int64_t sid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (sid >= n_streams) return;
+    const covt_stream_desc d = descs[sid];
+    if (!(d.flags & COVT_DESC_LANE)) return;
+#ifdef COVT_TIMING
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    int32_t err = 0, consumed = 0;
+    // stage the stream's bytes: 4 x 16 + 4 bytes from its 4-byte aligned start, loads issued together
+    uint32_t* slot = slots + threadIdx.x;  // dword k of lane t at slots[k * 256 + t]: conflict-free
+    const uintptr_t a = (uintptr_t)(in + d.in_off);
+    const uintptr_t a4 = a & ~(uintptr_t)3;
+    uint32_t st[kLaneSlot];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(a4 + 16 * k);
+        st[4 * k] = v.x;
+        st[4 * k + 1] = v.y;
+        st[4 * k + 2] = v.z;
+        st[4 * k + 3] = v.w;
+    }
+    st[16] = *g32(a4 + 64);
+#pragma unroll
+    for (int k = 0; k < kLaneSlot; ++k) slot[k * 256] = st[k];
+    LaneBytes lb{slot, (uint32_t)(a & 3u), d.avail, -1, 0u};
+    if (d.num_values < 0 || d.avail < 0 || d.avail > kLaneMaxBytes) err = COVT_ERR_INVALID_ARG;
+    else if (d.op == COVT_OP_BYTE_RLE_U8) lane_rle_byte(lb, d.num_values, out + d.out_off, err, consumed);
+    else if (d.op == COVT_OP_RLE_U64 || d.op == COVT_OP_RLE_S64 || d.op == COVT_OP_RLE_I32)
+        lane_rle_int(lb, d.op, d.num_values, out + d.out_off, err, consumed);
+    else err = COVT_ERR_UNSUPPORTED_ENCODING;
+    covt_stream_result r;
+    r.status = err;
+    r.consumed = err ? 0 : consumed;
+#ifdef COVT_TIMING
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    r.status = err ? -1 : (int32_t)(t_end - t_start);
+    r.consumed = (int32_t)(uint32_t)t_start;
+#endif
+    res[sid] = r;
 }
 
 }  // namespace covt
@@ -1161,6 +1419,13 @@ __global__ __launch_bounds__(256) void decode_family_kernel(const uint8_t* __res
 extern "C" int covt_launch_family(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
                                   uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream) {
     if (n_streams <= 0) return COVT_OK;
+    if (fam == COVT_FAMILY_LANE) {
+        const int64_t lblocks = (n_streams + 255) / 256;
+        if (lblocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
+        hipLaunchKernelGGL(covt::decode_lane_kernel, dim3((unsigned)lblocks), dim3(256), 0, stream, d_in, d_desc,
+                           n_streams, d_out, d_res);
+        return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
+    }
     const int64_t blocks = (n_streams + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
     const dim3 grid((unsigned)blocks), block(64 * covt::kWavesPerBlock);
@@ -1183,3 +1448,11 @@ extern "C" int covt_launch_family(int fam, const uint8_t* d_in, const covt_strea
 }
 
 extern "C" int covt_op_family_of(int op) { return covt::op_family(op); }
+
+#ifdef COVT_TIMING
+// profiling build only: per-stream phase clocks go to d_buf[n_streams][8] (launch order)
+extern "C" int covt_debug_set_phase_buffer(void* d_buf, const void* d_desc0) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(covt::covt_phase_desc0), &d_desc0, sizeof(d_desc0)) != hipSuccess) return -5;
+    return hipMemcpyToSymbol(HIP_SYMBOL(covt::covt_phase_buf), &d_buf, sizeof(d_buf)) == hipSuccess ? 0 : -5;
+}
+#endif

@@ -360,8 +360,8 @@ int fpf_call(const uint8_t* buf, size_t buf_len, int32_t* pos, int op, int32_t n
 // per-thread auxiliary streams ordered by events (capturable into a hipGraph).
 struct ForkCtx {
     int device = -1;
-    hipStream_t aux[2] = {nullptr, nullptr};
-    hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+    hipStream_t aux[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
 };
 
 int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const int64_t counts[COVT_NUM_FAMILIES],
@@ -372,20 +372,21 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
     if (f.device != dev) {
         f = ForkCtx{};
         f.device = dev;
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 3; ++i) {
             if (hipStreamCreateWithFlags(&f.aux[i], hipStreamNonBlocking) != hipSuccess) return COVT_ERR_DEVICE;
             if (hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming) != hipSuccess) return COVT_ERR_DEVICE;
         }
         if (hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess) return COVT_ERR_DEVICE;
     }
-    const int64_t o1 = counts[0], o2 = counts[0] + counts[1];
+    const int64_t o1 = counts[0], o2 = o1 + counts[1], o3 = o2 + counts[2];
     if (hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 3; ++i)
         if (hipStreamWaitEvent(f.aux[i], f.fork, 0) != hipSuccess) return COVT_ERR_DEVICE;
     int st = covt_launch_family(COVT_FAMILY_FASTPFOR, d_in, d_desc + o2, counts[2], d_out, d_res + o2, f.aux[0]);
     if (!st) st = covt_launch_family(COVT_FAMILY_VARINT, d_in, d_desc + o1, counts[1], d_out, d_res + o1, f.aux[1]);
+    if (!st) st = covt_launch_family(COVT_FAMILY_LANE, d_in, d_desc + o3, counts[3], d_out, d_res + o3, f.aux[2]);
     if (!st) st = covt_launch_family(COVT_FAMILY_RLE, d_in, d_desc, counts[0], d_out, d_res, s);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
         if (hipEventRecord(f.join[i], f.aux[i]) != hipSuccess) return COVT_ERR_DEVICE;
         if (hipStreamWaitEvent(s, f.join[i], 0) != hipSuccess) return COVT_ERR_DEVICE;
     }
@@ -403,7 +404,7 @@ struct covt_plan {
     std::vector<uint64_t> tile_off, tile_size;
     std::vector<covt_stream_info> info;   // tile order
     std::vector<covt_stream_desc> descs;  // launch order: grouped by family, largest first
-    int64_t fam_counts[COVT_NUM_FAMILIES] = {0, 0, 0};
+    int64_t fam_counts[COVT_NUM_FAMILIES] = {0, 0, 0, 0};
     int64_t out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
 };
 
@@ -522,9 +523,16 @@ int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const u
         const auto& s = p->info[(size_t)i];
         return (int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4;
     };
-    auto fam = [&](int64_t i) { return covt_op_family_of(p->info[(size_t)i].op); };
+    auto fam = [&](int64_t i) {
+        const auto& s = p->info[(size_t)i];
+        return lane_stream(s.op, s.desc_index, s.byte_length) ? COVT_FAMILY_LANE : covt_op_family_of(s.op);
+    };
     std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-        return fam(a) != fam(b) ? fam(a) < fam(b) : cost(a) > cost(b);
+        const int fa = fam(a), fb = fam(b);
+        if (fa != fb) return fa < fb;
+        if (fa == COVT_FAMILY_LANE && p->info[(size_t)a].op != p->info[(size_t)b].op)  // op-uniform waves
+            return p->info[(size_t)a].op < p->info[(size_t)b].op;
+        return cost(a) > cost(b);
     });
     for (int64_t i : order) p->fam_counts[fam(i)]++;
     p->descs.resize(ns);
@@ -538,6 +546,7 @@ int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const u
         d.op = (uint8_t)si.op;
         d.num_bits = (uint8_t)si.num_bits;
         d.byte_length = si.byte_length;
+        d.flags = lane_stream(si.op, d.num_values, d.byte_length) ? COVT_DESC_LANE : 0;
         p->descs[k] = d;
         si.desc_index = (int32_t)k;
     }
@@ -648,8 +657,8 @@ int decode_subset(const covt_plan* p, const uint8_t* bytes, const std::vector<in
         if (!descs.empty())
             chk(hipMemcpyAsync(d_desc, descs.data(), descs.size() * sizeof(covt_stream_desc), hipMemcpyHostToDevice,
                                s));
-        int64_t cnt[COVT_NUM_FAMILIES] = {0, 0, 0};
-        for (const auto& d : descs) cnt[covt_op_family_of(d.op)]++;  // sel is in grouped launch order
+        int64_t cnt[COVT_NUM_FAMILIES] = {0, 0, 0, 0};
+        for (const auto& d : descs) cnt[desc_family(d)]++;  // sel is in grouped launch order
         if (st == COVT_OK) st = launch_grouped(d_in, d_desc, cnt, d_out, d_res, s);
         stage.resize((size_t)out_total);
         if (st == COVT_OK && out_total)

@@ -7,17 +7,24 @@
 
 #include "covt.h"
 
-#ifdef __cplusplus
 extern "C" {
-#endif
-
-// Enqueues the one-wave-per-stream decode kernel of one codec family (covt_decode.hip) on `stream`
-// over descriptors [0, n_streams); descriptors of other families are skipped.
+// Enqueues the decode kernel of one family (covt_decode.hip) on `stream` over descriptors
+// [0, n_streams); descriptors of other families are skipped.
 int covt_launch_family(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
                        uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream);
 int covt_op_family_of(int op);
-
-#ifdef __cplusplus
 }
-#endif
+
+// Plan rule for the lane-per-stream kernel: RLE streams of at most kLaneMaxValues values and
+// kLaneMaxBytes bytes (staged whole in the lane's LDS slot).
+constexpr int32_t kLaneMaxValues = 256;
+constexpr int32_t kLaneMaxBytes = 64;
+inline bool lane_stream(int op, int32_t num_values, int32_t byte_length) {
+    return (op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_S64 || op == COVT_OP_RLE_I32) &&
+           num_values >= 0 && num_values <= kLaneMaxValues && byte_length >= 0 && byte_length <= kLaneMaxBytes;
+}
+inline int desc_family(const covt_stream_desc& d) {
+    return (d.flags & COVT_DESC_LANE) ? COVT_FAMILY_LANE : covt_op_family_of(d.op);
+}
+
 #endif

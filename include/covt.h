@@ -115,7 +115,11 @@ enum covt_op {
 #define COVT_FAMILY_RLE 0      /* byte RLE, integer RLE (and COVT_OP_NONE -> unsupported) */
 #define COVT_FAMILY_VARINT 1   /* varint / zigzag / delta / Morton ops */
 #define COVT_FAMILY_FASTPFOR 2 /* FastPFOR + VariableByte ops */
-#define COVT_NUM_FAMILIES 3
+#define COVT_FAMILY_LANE 3     /* small RLE streams (flag COVT_DESC_LANE): one lane per stream */
+#define COVT_NUM_FAMILIES 4
+
+/* covt_stream_desc.flags */
+#define COVT_DESC_LANE 0x1u /* decoded by the lane-per-stream kernel (set by the plan for small streams) */
 
 /* One device-resident plan entry (32 bytes). */
 typedef struct covt_stream_desc {
@@ -125,7 +129,7 @@ typedef struct covt_stream_desc {
     int32_t num_values;  /* values (vertices for the Morton ops) to produce */
     uint8_t op;          /* enum covt_op */
     uint8_t num_bits;    /* Morton bits, 32 - nlz(extent) (CovtParser.java:77) */
-    uint16_t flags;
+    uint16_t flags;      /* COVT_DESC_* */
     int32_t byte_length; /* wire byteLength (FastPFOR reads byteLength/4 big-endian words) */
 } covt_stream_desc;
 
@@ -156,8 +160,8 @@ int64_t covt_plan_output_bytes(const covt_plan* plan);
 int covt_plan_totals(const covt_plan* plan, int64_t* in_bytes, int64_t* out_bytes, int64_t* vertices);
 int covt_plan_streams(const covt_plan* plan, covt_stream_info* out);    /* num_streams records */
 int covt_plan_descs(const covt_plan* plan, covt_stream_desc* out);      /* num_streams, launch order */
-/* Launch order groups descriptors by family (RLE, varint, FastPFOR; largest stream first inside a
- * family): counts[f] = descriptors of family f. */
+/* Launch order groups descriptors by family (RLE, varint, FastPFOR, lane; largest stream first inside
+ * a family, the lane family also by op): counts[f] = descriptors of family f. */
 int covt_plan_family_counts(const covt_plan* plan, int64_t counts[COVT_NUM_FAMILIES]);
 int covt_plan_tile_status(const covt_plan* plan, int32_t* out);         /* n_tiles */
 
@@ -167,8 +171,8 @@ int covt_plan_tile_status(const covt_plan* plan, int32_t* out);         /* n_til
 int covt_decode_streams_device(const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
                                uint8_t* d_out, covt_stream_result* d_res, void* hip_stream);
 
-/* Same, for descriptors grouped by family (as covt_plan_descs returns them): the three family
- * kernels run concurrently on forked streams joined back into `hip_stream`. */
+/* Same, for descriptors grouped by family (as covt_plan_descs returns them): the family kernels run
+ * concurrently on forked streams joined back into `hip_stream`. */
 int covt_decode_streams_device_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc,
                                        const int64_t family_counts[COVT_NUM_FAMILIES], uint8_t* d_out,
                                        covt_stream_result* d_res, void* hip_stream);

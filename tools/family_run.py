@@ -23,8 +23,8 @@ def main():
     batch = covt.DeviceBatch(plan, "cuda")
     counts = plan.family_counts.copy()
     if fam != "all":
-        keep = {"rle": 0, "varint": 1, "fastpfor": 2}[fam]
-        for f in range(3):
+        keep = {"rle": 0, "varint": 1, "fastpfor": 2, "lane": 3}[fam]
+        for f in range(covt.NUM_FAMILIES):
             if f != keep:
                 counts[f] = 0
         # move the kept family's descriptors to the front ranges the grouped launch expects

@@ -57,8 +57,8 @@ def main():
     torch.cuda.synchronize()
     print("all ops, families concurrent (grouped launch): %.3f ms" % (e0.elapsed_time(e1) / 5))
     import ctypes as C
-    for fam, name in enumerate(("RLE", "VARINT", "FASTPFOR")):
-        cnt = np.zeros(3, dtype=np.int64)
+    for fam, name in enumerate(("RLE", "VARINT", "FASTPFOR", "LANE")):
+        cnt = np.zeros(covt.NUM_FAMILIES, dtype=np.int64)
         off = int(plan.family_counts[:fam].sum())
         n = int(plan.family_counts[fam])
         sub = torch.from_numpy(np.ascontiguousarray(descs[off:off + n]).reshape(-1)).cuda()
@@ -98,3 +98,44 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def fpf_scaling():
+    """FastPFOR throughput by stream size class: large streams (steady-state block loop) vs small ones
+    (per-stream and per-page overhead, VariableByte tail)."""
+    import torch
+
+    covt = bench.load_covt()
+    picks = bench.sample_batch(bench.tile_library(), 10000, bench.SEED)
+    plan = covt.Plan.from_tiles([t for _, t in picks])
+    batch = covt.DeviceBatch(plan, "cuda")
+    descs = plan.descs.reshape(-1, 32)
+    ops = descs[:, 24]
+    nv = descs[:, 20:24].copy().view(np.int32).ravel()
+    res = torch.zeros(2 * plan.num_streams, dtype=torch.int32, device="cuda")
+    L = covt.lib()
+    import ctypes as C
+    L.covt_launch_family.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+    stream = torch.cuda.current_stream()
+    for lo, hi in ((0, 256), (256, 1024), (1024, 4096), (4096, 16384), (16384, 1 << 30)):
+        m = (ops >= 10) & (ops <= 12) & (nv >= lo) & (nv < hi)
+        if not m.any():
+            continue
+        sub = torch.from_numpy(np.ascontiguousarray(descs[m]).reshape(-1)).cuda()
+        n = int(m.sum())
+        for _ in range(2):
+            L.covt_launch_family(2, batch.d_in.data_ptr(), sub.data_ptr(), n, batch.d_out.data_ptr(), res.data_ptr(),
+                                 stream.cuda_stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(5):
+            L.covt_launch_family(2, batch.d_in.data_ptr(), sub.data_ptr(), n, batch.d_out.data_ptr(), res.data_ptr(),
+                                 stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 5
+        vals = int(nv[m].sum())
+        print("FPF streams with %6d <= values < %9d: n=%6d values=%10d  t=%.3f ms  %.1f Gval/s  %.2f us/stream-slot"
+              % (lo, hi, n, vals, t, vals / t / 1e6, t * 1e3 * 1024 * 7 / max(n, 1)))
+

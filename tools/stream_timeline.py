@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Per-stream timeline of one grouped decode launch over the bench batch (GPU, profiling build).
+
+Loads libcovt_timing.so (make -C cov-tiles_amd timing), whose kernels write (duration, start) in
+100 MHz s_memrealtime ticks in place of each stream's result, and prints per op: total wave time,
+duration percentiles, the slowest streams and the launch's critical path.  The results are not
+decode results, so this never runs in the product path."""
+import ctypes
+import os
+import sys
+
+os.environ["COVT_LIB_VARIANT"] = "libcovt_timing.so"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+
+NAMES = {101: "L_BYTE_RLE", 102: "L_RLE_U64", 103: "L_RLE_I32", 104: "L_RLE_S64",
+         1: "BYTE_RLE", 2: "RLE_U64", 3: "RLE_I32", 4: "RLE_S64", 7: "VAR_ZZD", 8: "VAR_XY", 9: "VAR_MORTON",
+         10: "FPF_ZZD", 11: "FPF_XY", 12: "FPF_MORTON", 13: "VAR_U64", 14: "VAR_I32_I64", 15: "VAR_ZZD_I64"}
+TICK_US = 0.01  # 100 MHz
+
+
+def main():
+    import torch
+
+    covt = bench.load_covt()
+    tiles = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+    picks = bench.sample_batch(bench.tile_library(), tiles, bench.SEED)
+    plan = covt.Plan.from_tiles([t for _, t in picks])
+    batch = covt.DeviceBatch(plan, "cuda")
+    L = covt.lib()
+    phase = torch.zeros(plan.num_streams * 8, dtype=torch.int32, device="cuda")
+    L.covt_debug_set_phase_buffer(ctypes.c_void_p(phase.data_ptr()), ctypes.c_void_p(batch.d_desc.data_ptr()))
+    for _ in range(3):
+        batch.decode()
+    torch.cuda.synchronize()
+    ph_launch = phase.cpu().numpy().view(np.uint32).reshape(-1, 8).astype(np.int64)
+    _, res = batch.results()
+    dur = res[:, 0].astype(np.int64)
+    start = res[:, 1].astype(np.int64) & 0xffffffff
+    if (dur < 0).any():
+        print("streams with errors:", int((dur < 0).sum()))
+    s = plan.streams
+    di = s["desc_index"]
+    ops = plan.descs.reshape(-1, 32)[:, 24]
+    lane = (plan.descs.reshape(-1, 32)[:, 26] & 1).astype(bool)
+    op_t = np.empty(len(s), dtype=np.int64)
+    op_t[:] = ops[di] + 100 * lane[di]  # lane-kernel streams: op + 100
+    d_t = dur  # results are in tile order
+    st_t = start
+    t0 = st_t.min()
+    end_t = st_t - t0 + d_t
+    print("launch span %.1f us (first start -> last end); %d streams" % (end_t.max() * TICK_US, len(s)))
+    print("last 8 streams to finish (op, bytes, values, start us, duration us):")
+    for i in np.argsort(-end_t)[:8]:
+        print("   %-12s %8d %8d  start %7.1f  dur %7.1f" % (NAMES.get(int(op_t[i]), op_t[i]), s["byte_length"][i],
+                                                          s["num_values"][i], (st_t[i] - t0) * TICK_US,
+                                                          d_t[i] * TICK_US))
+    fam_of = {1: 0, 2: 0, 3: 0, 4: 0}
+    for fam, name in enumerate(("RLE", "VARINT", "FASTPFOR", "LANE")):
+        m = np.array([(3 if o >= 100 else fam_of.get(int(o), 2 if o in (10, 11, 12) else 1)) == fam for o in op_t])
+        if m.any():
+            print("  family %-8s first start %7.1f us  last start %7.1f us  last end %7.1f us  wave-time %9.1f us"
+                  % (name, (st_t[m].min() - t0) * TICK_US, (st_t[m].max() - t0) * TICK_US, end_t[m].max() * TICK_US,
+                     d_t[m].sum() * TICK_US))
+    print("%-12s %7s %9s %9s %8s %8s %8s %8s  %s" % ("op", "streams", "MB", "wave-ms", "p50 us", "p99 us", "max us",
+                                                    "ns/B", "slowest (bytes, values, us)"))
+    for op in sorted(set(op_t.tolist())):
+        m = op_t == op
+        d = d_t[m] * TICK_US
+        b = s["byte_length"][m]
+        nv = s["num_values"][m]
+        top = np.argsort(-d)[:3]
+        print("%-12s %7d %9.1f %9.2f %8.2f %8.2f %8.1f %8.2f  %s" % (
+            NAMES.get(op, op), int(m.sum()), b.sum() / 1e6, d.sum() / 1e3, np.percentile(d, 50),
+            np.percentile(d, 99), d.max(), d.sum() * 1e3 / max(b.sum(), 1),
+            " ".join("(%d,%d,%.1f)" % (b[i], nv[i], d[i]) for i in top)))
+    print("wave time (ms) by op and stream size:")
+    edges = (0, 64, 256, 1024, 4096, 16384, 65536, 1 << 30)
+    print("%-12s" % "op" + "".join("%16s" % ("<%d" % e) for e in edges[1:]))
+    for op in sorted(set(op_t.tolist())):
+        m = op_t == op
+        b = s["byte_length"]
+        cells = []
+        for lo, hi in zip(edges[:-1], edges[1:]):
+            mm = m & (b >= lo) & (b < hi)
+            cells.append("%7.1f/%-8d" % (d_t[mm].sum() * TICK_US / 1e3, int(mm.sum())))
+        print("%-12s" % NAMES.get(op, op) + "".join("%16s" % c for c in cells))
+    ph = ph_launch[di]  # tile order
+    print("shader clocks by phase (G = 1e9 clocks; RLE: 0 window 1 next[] 2 walk 3 small-groups 4 big-groups "
+          "5 long-literal 7 loop; FPF: 0 page-dir 1 stage 2 walk+prefetch 3 unpack 4 exceptions 5 sink 6 tail)")
+    for op in sorted(set(op_t.tolist())):
+        m = op_t == op
+        tot = ph[m].sum(axis=0)
+        if tot.sum() == 0:
+            continue
+        print("%-12s total %7.3f G  " % (NAMES.get(op, op), tot.sum() / 1e9) +
+              " ".join("%d:%4.1f%%" % (k, 100.0 * tot[k] / tot.sum()) for k in range(8) if tot[k]))
+    # duration vs size buckets
+    print("duration by stream size (all ops):")
+    b = s["byte_length"]
+    for lo, hi in ((0, 64), (64, 256), (256, 1024), (1024, 4096), (4096, 16384), (16384, 65536), (65536, 1 << 30)):
+        m = (b >= lo) & (b < hi)
+        if m.any():
+            d = d_t[m] * TICK_US
+            print("  [%6d,%9d) n=%7d  mean %7.2f us  p99 %7.2f us  ns/B %7.2f" % (
+                lo, hi, int(m.sum()), d.mean(), np.percentile(d, 99), d.sum() * 1e3 / b[m].sum()))
+
+
+if __name__ == "__main__":
+    main()
