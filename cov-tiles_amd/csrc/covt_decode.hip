@@ -319,7 +319,7 @@ __device__ __forceinline__ void sink_values(const uint32_t (&vin)[K], int64_t ba
 // the 1 KiB indexed window and the varint machinery
 // --------------------------------------------------------------------------------------------
 enum { MODE_RAW = 0, MODE_WORDREV = 1 };                           // byte order of the window
-enum { VAL_J4 = 0, VAL_VB = 1, VAL_U64 = 2, VAL_U64_STRICT = 3 };  // value grammar
+enum { VAL_J4 = 0, VAL_VB = 1, VAL_U64 = 2, VAL_U64_STRICT = 3, VAL_NONE = 4 };  // value grammar (NONE: bytes only)
 
 // A window holds 1 KiB of the stream in LDS (and each lane's 16 bytes in registers) plus an index
 // of its value terminators: list[] = window-relative positions of every terminator byte in the
@@ -369,6 +369,16 @@ __device__ void win_load(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t p, int
         d.w = ld_be32(q + 12);
     }
     ((uint4*)sm.u.v.win)[l] = d;
+    if (VAL == VAL_NONE) {  // byte-oriented readers: no terminator index
+        wave_sync();
+        w.d = d;
+        w.woff = woff;
+        w.K = 0;
+        w.p0 = p;
+        w.valid = true;
+        w.serial = false;
+        return;
+    }
     const int32_t q0 = woff + 16 * l;
     const uint32_t V = range16((VAL == VAL_J4 ? p : 0) - q0, end - q0);  // J4 indexes from p only
     const uint32_t H = hibits16(d);
@@ -710,22 +720,26 @@ __device__ void run_rle_int(Ctx& c) {
                 int32_t take = c.n - goff;
                 take = take < 0 ? 0 : (take > cnt ? cnt : take);
                 const bool big = take > 8;
+                // per-group parameters, lane-parallel: runs base + i * delta, literals from varint rr
+                const bool isrun = cb < 0x80u;
+                const int32_t rr = gv ? rank_rel(sm, pg + (isrun ? 2 : 1), K) : 0;
+                const int32_t delta = (int32_t)(int8_t)win_byte(sm, pg + 1);
+                int64_t b64 = 0;
+                if (gv && isrun) {
+                    const uint64_t raw = win_vulong(sm, pg + 2, sm.u.v.list[rr]);
+                    b64 = is_signed ? zz64(raw) : (int64_t)raw;
+                }
                 if (gv && !big && take > 0) {
-                    if (cb < 0x80u) {
-                        const int32_t delta = (int32_t)(int8_t)win_byte(sm, pg + 1);
-                        const int32_t r = rank_rel(sm, pg + 2, K);
-                        const uint64_t raw = win_vulong(sm, pg + 2, sm.u.v.list[r]);
-                        const int64_t b64 = is_signed ? zz64(raw) : (int64_t)raw;
+                    if (isrun) {
                         for (int32_t i = 0; i < take; ++i) {
                             const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
                             if (to_i32) ((int32_t*)c.out)[goff + i] = (int32_t)v;
                             else ((int64_t*)c.out)[goff + i] = v;
                         }
                     } else {
-                        const int32_t r = rank_rel(sm, pg + 1, K);
                         int32_t sj = pg + 1;
                         for (int32_t i = 0; i < take; ++i) {
-                            const int32_t ej = sm.u.v.list[r + i];
+                            const int32_t ej = sm.u.v.list[rr + i];
                             store(goff + i, win_vulong(sm, sj, ej));
                             sj = ej + 1;
                         }
@@ -736,22 +750,20 @@ __device__ void run_rle_int(Ctx& c) {
                 while (bigm) {  // wave-uniform loop over the big groups of this batch
                     const int src = __ffsll((long long)bigm) - 1;
                     bigm &= bigm - 1;
-                    const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
-                    const uint32_t c2 = lane_bcast(cb, src);
                     const int32_t o2 = (int32_t)lane_bcast((uint32_t)goff, src);
                     const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
-                    if (c2 < 0x80u) {
-                        const int32_t delta = (int32_t)(int8_t)win_byte(sm, p2 + 1);
-                        const int32_t r = rank_rel(sm, p2 + 2, K);
-                        const uint64_t raw = win_vulong(sm, p2 + 2, sm.u.v.list[r]);
-                        const int64_t b64 = is_signed ? zz64(raw) : (int64_t)raw;
+                    if (lane_bcast(cb, src) < 0x80u) {
+                        const int32_t d2 = (int32_t)lane_bcast((uint32_t)delta, src);
+                        const int64_t bb = (int64_t)(((uint64_t)lane_bcast((uint32_t)((uint64_t)b64 >> 32), src) << 32) |
+                                                     lane_bcast((uint32_t)b64, src));
                         for (int32_t i = l; i < t2; i += 64) {  // literals[0] + used * delta
-                            const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
+                            const int64_t v = (int64_t)((uint64_t)bb + (uint64_t)(int64_t)(int32_t)(i * d2));
                             if (to_i32) ((int32_t*)c.out)[o2 + i] = (int32_t)v;
                             else ((int64_t*)c.out)[o2 + i] = v;
                         }
                     } else {
-                        const int32_t r = rank_rel(sm, p2 + 1, K);
+                        const int32_t r = (int32_t)lane_bcast((uint32_t)rr, src);
+                        const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
                         for (int32_t i = l; i < t2; i += 64) {
                             const int32_t ej = sm.u.v.list[r + i];
                             const int32_t sj = i == 0 ? p2 + 1 : (int32_t)sm.u.v.list[r + i - 1] + 1;
@@ -782,7 +794,7 @@ __device__ void run_rle_byte(Ctx& c) {
     while (done < c.n && !c.err) {
         if (pos >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
         COVT_PHASE(c, 7);
-        win_load<MODE_RAW, VAL_U64>(sm, c.sb, w, pos, c.avail);
+        win_load<MODE_RAW, VAL_NONE>(sm, c.sb, w, pos, c.avail);
         COVT_PHASE(c, 0);
         const int32_t woff = w.woff;
         const int32_t vend = (c.avail - woff) < kWin ? (c.avail - woff) : kWin;
@@ -816,9 +828,12 @@ __device__ void run_rle_byte(Ctx& c) {
             int32_t take = c.n - goff;
             take = take < 0 ? 0 : (take > cnt ? cnt : take);
             const bool big = take > 8;
+            const bool isrun = cb < 0x80u;
+            const uint32_t rv = win_byte(sm, pg + 1);  // a run's value
+            lbad |= gv && isrun && take > 0 && rv > 5u;
             if (gv && !big) {
                 for (int32_t i = 0; i < take; ++i) {
-                    const uint32_t v = cb < 0x80u ? win_byte(sm, pg + 1) : win_byte(sm, pg + 1 + i);
+                    const uint32_t v = isrun ? rv : win_byte(sm, pg + 1 + i);
                     c.out[goff + i] = (uint8_t)v;
                     lbad |= v > 5u;
                 }
@@ -828,14 +843,18 @@ __device__ void run_rle_byte(Ctx& c) {
             while (bigm) {
                 const int src = __ffsll((long long)bigm) - 1;
                 bigm &= bigm - 1;
-                const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
-                const uint32_t c2 = lane_bcast(cb, src);
                 const int32_t o2 = (int32_t)lane_bcast((uint32_t)goff, src);
                 const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
-                for (int32_t i = l; i < t2; i += 64) {
-                    const uint32_t v = c2 < 0x80u ? win_byte(sm, p2 + 1) : win_byte(sm, p2 + 1 + i);
-                    c.out[o2 + i] = (uint8_t)v;
-                    lbad |= v > 5u;
+                if (lane_bcast(cb, src) < 0x80u) {
+                    const uint8_t v = (uint8_t)lane_bcast(rv, src);
+                    for (int32_t i = l; i < t2; i += 64) c.out[o2 + i] = v;
+                } else {
+                    const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
+                    for (int32_t i = l; i < t2; i += 64) {
+                        const uint32_t v = win_byte(sm, p2 + 1 + i);
+                        c.out[o2 + i] = (uint8_t)v;
+                        lbad |= v > 5u;
+                    }
                 }
             }
             COVT_PHASE(c, 4);
