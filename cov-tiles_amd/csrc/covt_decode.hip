@@ -101,6 +101,17 @@ __device__ __forceinline__ uint32_t incl_scan(uint32_t x) {
     return x;
 }
 
+// maximum over the 64 lanes (DPP row shifts, then row broadcasts), returned uniform
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return lane_bcast(x, 63);
+}
+
 // --------------------------------------------------------------------------------------------
 // byte helpers
 // --------------------------------------------------------------------------------------------
@@ -674,16 +685,14 @@ __device__ void run_rle_int(Ctx& c) {
         int32_t pj = jlo, out = done;
         bool first = true;
         while (true) {
+            // the walk only follows next[]: value counts (and the stop at n) come from the batch scan
             int32_t G = 0;
             uint32_t gs = 0;
             const int32_t out0 = out;
-            while (G < 64 && out < c.n) {
+            for (; G < 64; ++G) {
                 const uint32_t nx = uniu(sm.u.v.next[pj]);
-                const uint32_t cb = uniu(win_byte(sm, pj));
                 if (nx == 0xffffu) break;
                 gs = l == G ? (uint32_t)pj : gs;
-                ++G;
-                out += cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb;
                 pj = (int32_t)nx;
             }
             COVT_PHASE(c, 2);
@@ -719,6 +728,13 @@ __device__ void run_rle_int(Ctx& c) {
                 const int32_t goff = out0 + (int32_t)(inc - (uint32_t)cnt);
                 int32_t take = c.n - goff;
                 take = take < 0 ? 0 : (take > cnt ? cnt : take);
+                out = out0 + (int32_t)lane_bcast(inc, 63);
+                if (out >= c.n) {  // the batch reaches n: stop after the group that does (Java reads no further)
+                    const uint64_t fin = __ballot(gv && goff + cnt >= c.n);
+                    const int gl = __ffsll((long long)fin) - 1;
+                    const uint32_t nxt = lane_bcast(gs, gl + 1 < 64 ? gl + 1 : 63);
+                    pj = gl + 1 < G ? (int32_t)nxt : pj;
+                }
                 const bool big = take > 8;
                 // per-group parameters, lane-parallel: runs base + i * delta, literals from varint rr
                 const bool isrun = cb < 0x80u;
@@ -729,19 +745,21 @@ __device__ void run_rle_int(Ctx& c) {
                     const uint64_t raw = win_vulong(sm, pg + 2, sm.u.v.list[rr]);
                     b64 = is_signed ? zz64(raw) : (int64_t)raw;
                 }
-                if (gv && !big && take > 0) {
-                    if (isrun) {
-                        for (int32_t i = 0; i < take; ++i) {
+                // Expansion loops run a wave-uniform trip count; lanes past their group's end repeat its
+                // last value (same address, same data) instead of masking exec each iteration.
+                const bool small = gv && !big && take > 0;
+                const int32_t tmax = (int32_t)wave_max((uint32_t)(small ? take : 0));
+                if (small) {
+                    for (int32_t i0 = 0; i0 < tmax; ++i0) {
+                        const int32_t i = i0 < take ? i0 : take - 1;
+                        if (isrun) {
                             const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
                             if (to_i32) ((int32_t*)c.out)[goff + i] = (int32_t)v;
                             else ((int64_t*)c.out)[goff + i] = v;
-                        }
-                    } else {
-                        int32_t sj = pg + 1;
-                        for (int32_t i = 0; i < take; ++i) {
+                        } else {
                             const int32_t ej = sm.u.v.list[rr + i];
+                            const int32_t sj = i == 0 ? pg + 1 : (int32_t)sm.u.v.list[rr + i - 1] + 1;
                             store(goff + i, win_vulong(sm, sj, ej));
-                            sj = ej + 1;
                         }
                     }
                 }
@@ -756,7 +774,8 @@ __device__ void run_rle_int(Ctx& c) {
                         const int32_t d2 = (int32_t)lane_bcast((uint32_t)delta, src);
                         const int64_t bb = (int64_t)(((uint64_t)lane_bcast((uint32_t)((uint64_t)b64 >> 32), src) << 32) |
                                                      lane_bcast((uint32_t)b64, src));
-                        for (int32_t i = l; i < t2; i += 64) {  // literals[0] + used * delta
+                        for (int32_t i0 = 0; i0 < t2; i0 += 64) {  // literals[0] + used * delta
+                            const int32_t i = i0 + l < t2 ? i0 + l : t2 - 1;
                             const int64_t v = (int64_t)((uint64_t)bb + (uint64_t)(int64_t)(int32_t)(i * d2));
                             if (to_i32) ((int32_t*)c.out)[o2 + i] = (int32_t)v;
                             else ((int64_t*)c.out)[o2 + i] = v;
@@ -764,7 +783,8 @@ __device__ void run_rle_int(Ctx& c) {
                     } else {
                         const int32_t r = (int32_t)lane_bcast((uint32_t)rr, src);
                         const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
-                        for (int32_t i = l; i < t2; i += 64) {
+                        for (int32_t i0 = 0; i0 < t2; i0 += 64) {
+                            const int32_t i = i0 + l < t2 ? i0 + l : t2 - 1;
                             const int32_t ej = sm.u.v.list[r + i];
                             const int32_t sj = i == 0 ? p2 + 1 : (int32_t)sm.u.v.list[r + i - 1] + 1;
                             store(o2 + i, win_vulong(sm, sj, ej));
@@ -804,13 +824,11 @@ __device__ void run_rle_byte(Ctx& c) {
             int32_t G = 0;
             uint32_t gs = 0;
             const int32_t out0 = out;
-            while (G < 64 && out < c.n && pj < vend) {
+            for (; G < 64 && pj < vend; ++G) {
                 const uint32_t cb = uniu(win_byte(sm, pj));
                 const int32_t nx = cb < 0x80u ? pj + 2 : pj + 1 + 0x100 - (int32_t)cb;
                 if (nx > vend) break;
                 gs = l == G ? (uint32_t)pj : gs;
-                ++G;
-                out += cb < 0x80u ? (int32_t)cb + 3 : 0x100 - (int32_t)cb;
                 pj = nx;
             }
             COVT_PHASE(c, 2);
@@ -827,12 +845,22 @@ __device__ void run_rle_byte(Ctx& c) {
             const int32_t goff = out0 + (int32_t)(inc - (uint32_t)cnt);
             int32_t take = c.n - goff;
             take = take < 0 ? 0 : (take > cnt ? cnt : take);
+            out = out0 + (int32_t)lane_bcast(inc, 63);
+            if (out >= c.n) {  // stop after the group that reaches n
+                const uint64_t fin = __ballot(gv && goff + cnt >= c.n);
+                const int gl = __ffsll((long long)fin) - 1;
+                const uint32_t nxt = lane_bcast(gs, gl + 1 < 64 ? gl + 1 : 63);
+                pj = gl + 1 < G ? (int32_t)nxt : pj;
+            }
             const bool big = take > 8;
             const bool isrun = cb < 0x80u;
             const uint32_t rv = win_byte(sm, pg + 1);  // a run's value
             lbad |= gv && isrun && take > 0 && rv > 5u;
-            if (gv && !big) {
-                for (int32_t i = 0; i < take; ++i) {
+            const bool small = gv && !big && take > 0;
+            const int32_t tmax = (int32_t)wave_max((uint32_t)(small ? take : 0));
+            if (small) {  // uniform trip count; lanes past their end repeat the last byte
+                for (int32_t i0 = 0; i0 < tmax; ++i0) {
+                    const int32_t i = i0 < take ? i0 : take - 1;
                     const uint32_t v = isrun ? rv : win_byte(sm, pg + 1 + i);
                     c.out[goff + i] = (uint8_t)v;
                     lbad |= v > 5u;
@@ -847,10 +875,11 @@ __device__ void run_rle_byte(Ctx& c) {
                 const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
                 if (lane_bcast(cb, src) < 0x80u) {
                     const uint8_t v = (uint8_t)lane_bcast(rv, src);
-                    for (int32_t i = l; i < t2; i += 64) c.out[o2 + i] = v;
+                    for (int32_t i0 = 0; i0 < t2; i0 += 64) c.out[o2 + (i0 + l < t2 ? i0 + l : t2 - 1)] = v;
                 } else {
                     const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
-                    for (int32_t i = l; i < t2; i += 64) {
+                    for (int32_t i0 = 0; i0 < t2; i0 += 64) {
+                        const int32_t i = i0 + l < t2 ? i0 + l : t2 - 1;
                         const uint32_t v = win_byte(sm, p2 + 1 + i);
                         c.out[o2 + i] = (uint8_t)v;
                         lbad |= v > 5u;
