@@ -1056,10 +1056,12 @@ __device__ void run_fastpfor(Ctx& c) {
                 return COVT_OK;
             };
             // word index of X[k][i] (dataTobePacked[k]) and the bit offset inside it
-            auto xword = [&](int32_t k, uint32_t xs, uint32_t i, uint32_t& xbit) -> int64_t {
+            // (32-bit: a stream holds < 2^29 words)
+            const int32_t nw32 = (int32_t)nw;
+            auto xword = [&](int32_t k, uint32_t xs, uint32_t i, uint32_t& xbit) -> int32_t {
                 const uint32_t bit = (i & 31u) * (uint32_t)k;
                 xbit = bit & 31u;
-                return (int64_t)xs + (int64_t)(i >> 5) * k + (bit >> 5);
+                return (int32_t)(xs + (i >> 5) * (uint32_t)k + (bit >> 5));
             };
             auto prefetch = [&](const FpfHdr& hv, int64_t pkv, FpfPre& pr, int slot) {
                 FpfHdr h;
@@ -1075,9 +1077,9 @@ __device__ void run_fastpfor(Ctx& c) {
                 const int32_t k = h.idx;
                 const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
                 uint32_t xb;
-                int64_t wi = xword(k >= 2 ? k : 2, xs, h.xcur + (uint32_t)l, xb);
-                wi = (k >= 2 && l < h.ce && wi < nw) ? wi : 0;
-                const uintptr_t xa4 = ((uintptr_t)(c.sb + 4 * wi)) & ~(uintptr_t)3;
+                int32_t wi = xword(k >= 2 ? k : 2, xs, h.xcur + (uint32_t)l, xb);
+                wi = (k >= 2 && l < h.ce && wi < nw32) ? wi : 0;
+                const uintptr_t xa4 = ((uintptr_t)c.sb + 4u * (uint32_t)wi) & ~(uintptr_t)3;
                 const u32x3 xv = *(const g_v3*)xa4;
                 pr.x0 = xv.x;
                 pr.x1 = xv.y;
@@ -1171,12 +1173,12 @@ __device__ void run_fastpfor(Ctx& c) {
                     uint32_t ex = 1u;
                     if (k != 1) {  // uniform
                         uint32_t xbit;
-                        const int64_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
+                        const int32_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
                         const uint32_t ob = sbmis & 3u;
                         uint64_t lo = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.x1, pc.x0, ob));
                         uint64_t hi = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.x2, pc.x1, ob));
-                        lo = wi < nw ? lo : 0ull;  // words past the stream read as 0
-                        hi = (wi + 1 < nw && xbit + (uint32_t)k > 32u) ? hi : 0ull;
+                        lo = wi < nw32 ? lo : 0ull;  // words past the stream read as 0
+                        hi = (wi + 1 < nw32 && xbit + (uint32_t)k > 32u) ? hi : 0ull;
                         const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
                         ex = (uint32_t)(((lo | (hi << 32)) >> xbit) & m);
                     }

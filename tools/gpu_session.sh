@@ -26,6 +26,9 @@ for s in "$@"; do
     bench_short) step bench 600 python bench.py --steps 10 --warmup 3 --cpu-seconds 8 ;;
     ops) step op_breakdown 600 python tools/op_breakdown.py ;;
     timeline) step timeline 300 python tools/stream_timeline.py ;;
+    ab) for v in libcovt_base.so libcovt.so libcovt_base.so libcovt.so; do
+            echo "== ab $v"; COVT_LIB_VARIANT=$v OPB_QUICK=1 timeout -k 10 300 python tools/op_breakdown.py 2>&1 | grep -v amdgpu.ids || fatal ab $?
+        done ;;
     fpfsize) step fpfsize 300 python -c "import sys; sys.path.insert(0, 'tools'); import op_breakdown; op_breakdown.fpf_scaling()" ;;
     prof) step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
     pmc_fetch) step rocprof_pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;

@@ -57,6 +57,7 @@ def main():
     torch.cuda.synchronize()
     print("all ops, families concurrent (grouped launch): %.3f ms" % (e0.elapsed_time(e1) / 5))
     import ctypes as C
+    quick = os.environ.get("OPB_QUICK")
     for fam, name in enumerate(("RLE", "VARINT", "FASTPFOR", "LANE")):
         cnt = np.zeros(covt.NUM_FAMILIES, dtype=np.int64)
         off = int(plan.family_counts[:fam].sum())
@@ -78,6 +79,8 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize()
         print("family %-8s alone: %.3f ms (%d streams)" % (name, e0.elapsed_time(e1) / 5, n))
+    if quick:
+        return
     for op in sorted(set(ops.tolist())):
         m = ops == op
         sub = torch.from_numpy(np.ascontiguousarray(descs[m]).reshape(-1)).cuda()
