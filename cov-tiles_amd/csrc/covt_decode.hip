@@ -205,6 +205,23 @@ struct Carry {
     uint32_t x, y;
 };
 
+// Full 16-byte-per-lane output stores (1 KiB per wave instruction) are nontemporal: decoded columns
+// are written once, and streaming whole lines past L2 keeps thousands of concurrent per-stream
+// write fronts from thrashing it (FastPFOR family 1.12 -> 0.94 ms on the config-5 batch).  Narrower
+// stores stay cached: nontemporal partial lines measured 1.8x slower for RLE, 1.2x for varint.
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_out16(int32_t* p, int4 v) {
+    const i32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (i32x4*)p);
+}
+template <class T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+    *p = v;
+}
+__device__ __forceinline__ int64_t pack_xy(int32_t x, int32_t y) {
+    return (int64_t)(((uint64_t)(uint32_t)y << 32) | (uint32_t)x);
+}
+
 // Per-op output transform, specialised at compile time.  `count` (uniform) values are valid; a full
 // group (count >= 64 K) takes the branch-free path with vector stores, a partial one masks lanes.
 template <int OP, int K>
@@ -220,21 +237,21 @@ __device__ __forceinline__ void sink_values(const uint32_t (&vin)[K], int64_t ba
     auto st32 = [&](const int32_t (&r)[K]) {
         int32_t* o = (int32_t*)out + i0;
         if (full) {
-            if (K == 4) *(int4*)o = make_int4(r[0], r[K > 1 ? 1 : 0], r[K > 2 ? 2 : 0], r[K > 3 ? 3 : 0]);
+            if (K == 4) st_out16(o, make_int4(r[0], r[K > 1 ? 1 : 0], r[K > 2 ? 2 : 0], r[K > 3 ? 3 : 0]));
             else
 #pragma unroll
-                for (int k = 0; k < K; ++k) o[k] = r[k];
+                for (int k = 0; k < K; ++k) st_out(o + k, r[k]);
         } else {
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (k < nvalid) o[k] = r[k];
+                if (k < nvalid) st_out(o + k, r[k]);
         }
     };
     auto st64 = [&](const int64_t (&r)[K]) {
         int64_t* o = (int64_t*)out + i0;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (full || k < nvalid) o[k] = r[k];
+            if (full || k < nvalid) st_out(o + k, r[k]);
     };
     if constexpr (OP == COVT_OP_VARINT_I32 || OP == COVT_OP_VARINT_ZZ_I32) {
         int32_t r[K];
@@ -311,16 +328,16 @@ __device__ __forceinline__ void sink_values(const uint32_t (&vin)[K], int64_t ba
         }
         if (full) {
             if (K == 4) {
-                *(int4*)o = make_int4(xy[0], xy[1], xy[K > 1 ? 2 : 0], xy[K > 1 ? 3 : 0]);
-                *(int4*)(o + 4) = make_int4(xy[K > 2 ? 4 : 0], xy[K > 2 ? 5 : 0], xy[K > 3 ? 6 : 0], xy[K > 3 ? 7 : 0]);
+                st_out16(o, make_int4(xy[0], xy[1], xy[K > 1 ? 2 : 0], xy[K > 1 ? 3 : 0]));
+                st_out16(o + 4, make_int4(xy[K > 2 ? 4 : 0], xy[K > 2 ? 5 : 0], xy[K > 3 ? 6 : 0], xy[K > 3 ? 7 : 0]));
             } else {
 #pragma unroll
-                for (int k = 0; k < K; ++k) *(int2*)(o + 2 * k) = make_int2(xy[2 * k], xy[2 * k + 1]);
+                for (int k = 0; k < K; ++k) st_out((int64_t*)(o + 2 * k), pack_xy(xy[2 * k], xy[2 * k + 1]));
             }
         } else {
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (k < nvalid) *(int2*)(o + 2 * k) = make_int2(xy[2 * k], xy[2 * k + 1]);
+                if (k < nvalid) st_out((int64_t*)(o + 2 * k), pack_xy(xy[2 * k], xy[2 * k + 1]));
         }
         c.x += lane_bcast(inc, 63);
     }
@@ -591,7 +608,7 @@ __device__ void run_varint_stream(Ctx& c) {
         varint_take<MODE_RAW, VAL_U64_STRICT>(*c.sm, c.sb, w, pos, c.avail, c.n, false, c.err,
                                               [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
                                                   if (lane_id() < count)
-                                                      o[base + lane_id()] = (int64_t)(((uint64_t)hi << 32) | lo);
+                                                      st_out(o + base + lane_id(), (int64_t)(((uint64_t)hi << 32) | lo));
                                               });
     } else {
         if ((OP == COVT_OP_VARINT_ZZ_DELTA_XY) && (c.n & 1)) {
@@ -642,8 +659,8 @@ __device__ void run_rle_int(Ctx& c) {
     int32_t pos = 0, done = 0;
     auto store = [&](int64_t i, uint64_t raw) {
         const int64_t v = is_signed ? zz64(raw) : (int64_t)raw;
-        if (to_i32) ((int32_t*)c.out)[i] = (int32_t)v;
-        else ((int64_t*)c.out)[i] = v;
+        if (to_i32) st_out((int32_t*)c.out + i, (int32_t)v);
+        else st_out((int64_t*)c.out + i, v);
     };
     while (done < c.n && !c.err) {
         if (pos >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
@@ -754,8 +771,8 @@ __device__ void run_rle_int(Ctx& c) {
                         const int32_t i = i0 < take ? i0 : take - 1;
                         if (isrun) {
                             const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
-                            if (to_i32) ((int32_t*)c.out)[goff + i] = (int32_t)v;
-                            else ((int64_t*)c.out)[goff + i] = v;
+                            if (to_i32) st_out((int32_t*)c.out + goff + i, (int32_t)v);
+                            else st_out((int64_t*)c.out + goff + i, v);
                         } else {
                             const int32_t ej = sm.u.v.list[rr + i];
                             const int32_t sj = i == 0 ? pg + 1 : (int32_t)sm.u.v.list[rr + i - 1] + 1;
@@ -777,8 +794,8 @@ __device__ void run_rle_int(Ctx& c) {
                         for (int32_t i0 = 0; i0 < t2; i0 += 64) {  // literals[0] + used * delta
                             const int32_t i = i0 + l < t2 ? i0 + l : t2 - 1;
                             const int64_t v = (int64_t)((uint64_t)bb + (uint64_t)(int64_t)(int32_t)(i * d2));
-                            if (to_i32) ((int32_t*)c.out)[o2 + i] = (int32_t)v;
-                            else ((int64_t*)c.out)[o2 + i] = v;
+                            if (to_i32) st_out((int32_t*)c.out + o2 + i, (int32_t)v);
+                            else st_out((int64_t*)c.out + o2 + i, v);
                         }
                     } else {
                         const int32_t r = (int32_t)lane_bcast((uint32_t)rr, src);
@@ -862,7 +879,7 @@ __device__ void run_rle_byte(Ctx& c) {
                 for (int32_t i0 = 0; i0 < tmax; ++i0) {
                     const int32_t i = i0 < take ? i0 : take - 1;
                     const uint32_t v = isrun ? rv : win_byte(sm, pg + 1 + i);
-                    c.out[goff + i] = (uint8_t)v;
+                    st_out(c.out + goff + i, (uint8_t)v);
                     lbad |= v > 5u;
                 }
             }
@@ -875,13 +892,13 @@ __device__ void run_rle_byte(Ctx& c) {
                 const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
                 if (lane_bcast(cb, src) < 0x80u) {
                     const uint8_t v = (uint8_t)lane_bcast(rv, src);
-                    for (int32_t i0 = 0; i0 < t2; i0 += 64) c.out[o2 + (i0 + l < t2 ? i0 + l : t2 - 1)] = v;
+                    for (int32_t i0 = 0; i0 < t2; i0 += 64) st_out(c.out + o2 + (i0 + l < t2 ? i0 + l : t2 - 1), v);
                 } else {
                     const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
                     for (int32_t i0 = 0; i0 < t2; i0 += 64) {
                         const int32_t i = i0 + l < t2 ? i0 + l : t2 - 1;
                         const uint32_t v = win_byte(sm, p2 + 1 + i);
-                        c.out[o2 + i] = (uint8_t)v;
+                        st_out(c.out + o2 + i, (uint8_t)v);
                         lbad |= v > 5u;
                     }
                 }
@@ -1019,60 +1036,58 @@ __device__ void run_fastpfor(Ctx& c) {
             if (c.err) break;
             COVT_PHASE(c, 0);
             const int32_t nblocks = uni(thissize / kFpfBlock);
+            const int32_t nw32 = (int32_t)nw;
             const int32_t bclen = uni((int32_t)(bcw * 4));
             const uint8_t* cb8 = (const uint8_t*)sm.u.f.cbuf;
             int32_t cbase = INT32_MIN / 2;
             auto chunk_load = [&](int32_t at) {  // container bytes [cbase, cbase + 1020), cbase in (at - 16, at]
                 cbase = (int32_t)(4 * (load_words(sm.u.f.cbuf, bc + (at >> 2)) - bc));
             };
+            // One block header (FastPFOR.decodePage loop body): all checks merged into one uniform test.
+            // The chunk is (re)loaded so that the header and up to 255 exception positions are inside.
             auto walk = [&](int32_t cur, FpfHdr& h) -> int32_t {
-                cur = uni(cur);  // header state is wave-uniform: keep it in SGPRs, branches scalar
+                cur = uni(cur);
                 cbase = uni(cbase);
-                if (cur + 2 > bclen) return COVT_ERR_BAD_HEADER;
-                if (cur < cbase || cur + 4 > cbase + 1020) chunk_load(cur);
-                const int32_t j = cur - cbase;  // container bytes cur..cur+3 (b, exceptions, maxbits)
+                if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 260)) chunk_load(cur);
+                const int32_t j = cur - cbase;
                 const uint32_t hw =
                     uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(j >> 2) + 1], sm.u.f.cbuf[j >> 2], (uint32_t)j & 3u));
-                h.b = (int32_t)(int8_t)(hw & 0xffu);
-                h.ce = (int32_t)((hw >> 8) & 0xffu);
-                if (h.b < 0 || h.b > 32) return COVT_ERR_BAD_HEADER;
-                h.idx = 0;
-                h.xcur = 0;
-                h.bcoff = cur + 2;
-                if (h.ce > 0) {
-                    if (cur + 3 + h.ce > bclen) return COVT_ERR_BAD_HEADER;
-                    if (cur + 3 + h.ce > cbase + 1020) chunk_load(cur);
-                    h.idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - h.b;
-                    h.bcoff = cur + 3;
-                    if (h.idx != 1) {
-                        if (h.idx < 2 || h.idx > 32) return COVT_ERR_BAD_HEADER;
-                        const int32_t xsz = __builtin_amdgcn_readlane(xz_v, h.idx);
-                        h.xcur = (uint32_t)__builtin_amdgcn_readlane(xc_v, h.idx);
-                        if (xsz < 0 || (int64_t)h.xcur + h.ce > xsz) return COVT_ERR_BAD_HEADER;
-                        xc_v = l == h.idx ? (int)(h.xcur + (uint32_t)h.ce) : xc_v;
-                    }
-                }
-                h.next = h.bcoff + h.ce;
-                return COVT_OK;
+                const int32_t b = (int32_t)(int8_t)(hw & 0xffu);
+                const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
+                const int32_t idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - b;
+                const bool hasx = ce > 0;
+                const bool arr = hasx && idx >= 2 && idx <= 32;  // exceptions from dataTobePacked[idx]
+                const int32_t k = arr ? idx : 0;
+                const int32_t xsz = __builtin_amdgcn_readlane(xz_v, k);
+                const int32_t xc = __builtin_amdgcn_readlane(xc_v, k);
+                bool bad = (uint32_t)b > 32u || cur + 2 > bclen;
+                bad |= hasx && (cur + 3 + ce > bclen || (idx != 1 && !arr));
+                bad |= arr && (xsz < 0 || xc + ce > xsz);
+                h.b = b;
+                h.ce = ce;
+                h.idx = hasx ? idx : 0;
+                h.xcur = arr ? (uint32_t)xc : 0u;
+                h.bcoff = cur + (hasx ? 3 : 2);
+                h.next = h.bcoff + ce;
+                xc_v += (l == (arr ? idx : 64)) ? ce : 0;
+                return bad ? COVT_ERR_BAD_HEADER : COVT_OK;
             };
-            // word index of X[k][i] (dataTobePacked[k]) and the bit offset inside it
             // (32-bit: a stream holds < 2^29 words)
-            const int32_t nw32 = (int32_t)nw;
             auto xword = [&](int32_t k, uint32_t xs, uint32_t i, uint32_t& xbit) -> int32_t {
                 const uint32_t bit = (i & 31u) * (uint32_t)k;
                 xbit = bit & 31u;
                 return (int32_t)(xs + (i >> 5) * (uint32_t)k + (bit >> 5));
             };
-            auto prefetch = [&](const FpfHdr& hv, int64_t pkv, FpfPre& pr, int slot) {
+            auto prefetch = [&](const FpfHdr& hv, int32_t pkv, FpfPre& pr, int slot) {
                 FpfHdr h;
                 h.idx = uni(hv.idx);
                 h.ce = uni(hv.ce);
                 h.xcur = uniu(hv.xcur);
                 h.bcoff = uni(hv.bcoff);
-                const int64_t pk = uni64(pkv);
+                const int32_t pk = uni(pkv);
                 // unconditional, branch-free loads consumed only in the next iteration: the vmcnt wait
                 // lands there and no exec-mask bookkeeping is spent on lane conditions
-                const uintptr_t a16 = ((uintptr_t)(c.sb + 4 * pk)) & ~(uintptr_t)15;
+                const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pk) & ~(uintptr_t)15;
                 pr.raw = ld128(a16 + 16 * (uintptr_t)l);
                 const int32_t k = h.idx;
                 const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
@@ -1094,9 +1109,9 @@ __device__ void run_fastpfor(Ctx& c) {
             };
             FpfHdr h;
             FpfPre pre;
-            int64_t pk = p0 + 1;
+            int32_t pk = (int32_t)p0 + 1;
             c.err = walk(0, h);
-            if (!c.err && pk + 8 * h.b > nw) c.err = COVT_ERR_TRUNCATED;
+            if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
             if (!c.err) prefetch(h, pk, pre, 0);
             // one block; the loop below alternates two register sets so that no in-flight prefetch
             // register is ever copied (a copy would force the vmcnt wait at the end of the iteration)
@@ -1108,7 +1123,7 @@ __device__ void run_fastpfor(Ctx& c) {
                 hc.xcur = uniu(h.xcur);
                 hc.bcoff = uni(h.bcoff);
                 hc.next = uni(h.next);
-                const int64_t pkc = uni64(pk);
+                const int32_t pkc = uni(pk);
                 const int32_t b = hc.b;
                 // stage block j: LDS dword qoff + i = packed word i (aligned, byte-swapped)
                 const uint32_t o = (sbmis + 4u * (uint32_t)pkc) & 15u;
@@ -1117,7 +1132,7 @@ __device__ void run_fastpfor(Ctx& c) {
                 {
                     uint4 raw2 = make_uint4(0, 0, 0, 0);
                     if (b == 32) {  // rare: the 16 bytes past the first KiB (same for every lane; scalar load)
-                        const uintptr_t a16 = ((uintptr_t)(c.sb + 4 * pkc)) & ~(uintptr_t)15;
+                        const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pkc) & ~(uintptr_t)15;
                         raw2 = sld128(a16 + 1024);
                     }
                     const uint32_t nsh = lane_next(pc.raw.x);
@@ -1146,7 +1161,7 @@ __device__ void run_fastpfor(Ctx& c) {
                 if (j + 1 < nblocks) {
                     c.err = walk(hc.next, h);
                     pk = pkc + 8 * b;
-                    if (!c.err && pk + 8 * h.b > nw) c.err = COVT_ERR_TRUNCATED;
+                    if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
                     if (c.err) return;
                 }
                 prefetch(h, pk, pn, slot ^ 1);
@@ -1166,7 +1181,11 @@ __device__ void run_fastpfor(Ctx& c) {
                     }
                 }
                 COVT_PHASE(c, 3);
+#if defined(COVT_ABL_NOEXC)  // ablation build: exceptions not applied
+                if (false) {
+#else
                 if (hc.ce > 0) {  // out[pos] |= (index == 1 ? 1 : exceptvalue) << b
+#endif
                     const int32_t k = hc.idx;
                     const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
                     const bool el = l < hc.ce;
@@ -1201,7 +1220,11 @@ __device__ void run_fastpfor(Ctx& c) {
                     v[3] |= pt.w;
                 }
                 COVT_PHASE(c, 4);
+#if defined(COVT_ABL_NOSTORE)  // ablation build: every block's output to the same 1 KiB (L2-resident)
+                sink_values<OP, 4>(v, 0, kFpfBlock, c.nb, c.out, cr);
+#else
                 sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, c.nb, c.out, cr);
+#endif
                 wave_sync();
                 COVT_PHASE(c, 5);
             };
