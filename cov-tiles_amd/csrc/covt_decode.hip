@@ -479,7 +479,48 @@ __device__ __forceinline__ int32_t win_rank(const WaveSmem& sm, const Win& w, in
 // bytes valid in [pos, end).  emit(lo, hi, base, count) is called per group of <=64 values, one per
 // lane.  Returns the number of values decoded.  With `until_end` (VariableByte tail) the region is
 // decoded to its end, a trailing partial value is dropped and more than `want` values is an error.
-template <int MODE, int VAL, class Emit>
+// one value whose bytes are window bytes [sj, ej] (ej = its terminator) in grammar VAL
+template <int VAL>
+__device__ __forceinline__ void win_value(const WaveSmem& sm, int32_t sj, int32_t ej, uint32_t& lo, uint32_t& hi,
+                                          bool& lerr) {
+    const int32_t len = ej - sj + 1;
+    uint32_t x0, x1, x2;
+    win_bytes12(sm, sj, x0, x1, x2);
+    lo = 0;
+    hi = 0;
+    if (VAL == VAL_J4) {
+        lo = pext7(x0 & bytemask(len));
+    } else if (VAL == VAL_VB) {
+        if (len <= 5) {
+            lo = pext7(x0 & bytemask(len));
+            if (len == 5) lo += (x1 & 0x7fu) << 28;
+        } else {  // VariableByte.uncompress: v += (c & 127) << shift, shift masked to 5 bits
+            uint32_t vv = 0;
+            for (int b = 0; b < len; ++b) vv += (win_byte(sm, sj + b) & 0x7fu) << ((7 * b) & 31);
+            lo = vv;
+        }
+    } else {
+        uint64_t rv;
+        if (len <= 10) {
+            const uint32_t m0 = x0 & bytemask(len), m1 = x1 & bytemask(len - 4), m2 = x2 & bytemask(len - 8);
+            rv = (uint64_t)pext7(m0) | ((uint64_t)pext7(m1) << 28) | ((uint64_t)(m2 & 0x7fu) << 56) |
+                 ((uint64_t)((m2 >> 8) & 0x7fu) << 63);
+        } else {  // orc readVulong: shift masked to 6 bits
+            rv = 0;
+            for (int b = 0; b < len; ++b) rv |= (uint64_t)(win_byte(sm, sj + b) & 0x7fu) << ((7 * b) & 63);
+            lerr = true;
+        }
+        lo = (uint32_t)rv;
+        hi = (uint32_t)(rv >> 32);
+    }
+}
+
+// Decode up to `want` values starting at stream position `pos` (a value boundary; updated) with
+// bytes valid in [pos, end).  emit(lo[K], hi[K], base, count) is called per group of <= 64 K values,
+// lane l holding values base + K l .. base + K l + K - 1.  Returns the number of values decoded.
+// With `until_end` (VariableByte tail) the region is decoded to its end, a trailing partial value
+// is dropped and more than `want` values is an error.
+template <int MODE, int VAL, int K = 1, class Emit>
 __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t& pos, int32_t end, int32_t want,
                                bool until_end, int32_t& err, Emit&& emit) {
     const int l = lane_id();
@@ -509,43 +550,18 @@ __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t&
         }
         if (take <= 0) break;
         bool lerr = false;
-        for (int32_t g = 0; g < take; g += 64) {
-            const int32_t vi = g + l;
-            uint32_t lo = 0, hi = 0;
-            if (vi < take) {
+        const int32_t s0 = pos - w.woff;
+        for (int32_t g = 0; g < take; g += 64 * K) {
+            uint32_t lo[K], hi[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                int32_t vi = g + K * l + k;
+                vi = vi < take ? vi : take - 1;  // lanes past the end repeat the last value (not emitted)
                 const int32_t ej = sm.u.v.list[r + vi];
-                const int32_t sj = (vi == 0) ? (pos - w.woff) : (int32_t)sm.u.v.list[r + vi - 1] + 1;
-                const int32_t len = ej - sj + 1;
-                uint32_t x0, x1, x2;
-                win_bytes12(sm, sj, x0, x1, x2);
-                if (VAL == VAL_J4) {
-                    lo = pext7(x0 & bytemask(len));
-                } else if (VAL == VAL_VB) {
-                    if (len <= 5) {
-                        lo = pext7(x0 & bytemask(len));
-                        if (len == 5) lo += (x1 & 0x7fu) << 28;
-                    } else {  // VariableByte.uncompress: v += (c & 127) << shift, shift masked to 5 bits
-                        uint32_t vv = 0;
-                        for (int b = 0; b < len; ++b) vv += (win_byte(sm, sj + b) & 0x7fu) << ((7 * b) & 31);
-                        lo = vv;
-                    }
-                } else {
-                    uint64_t rv;
-                    if (len <= 10) {
-                        const uint32_t m0 = x0 & bytemask(len), m1 = x1 & bytemask(len - 4),
-                                       m2 = x2 & bytemask(len - 8);
-                        rv = (uint64_t)pext7(m0) | ((uint64_t)pext7(m1) << 28) | ((uint64_t)(m2 & 0x7fu) << 56) |
-                             ((uint64_t)((m2 >> 8) & 0x7fu) << 63);
-                    } else {  // orc readVulong: shift masked to 6 bits
-                        rv = 0;
-                        for (int b = 0; b < len; ++b) rv |= (uint64_t)(win_byte(sm, sj + b) & 0x7fu) << ((7 * b) & 63);
-                        lerr = true;
-                    }
-                    lo = (uint32_t)rv;
-                    hi = (uint32_t)(rv >> 32);
-                }
+                const int32_t sj = vi == 0 ? s0 : (int32_t)sm.u.v.list[r + vi - 1] + 1;
+                win_value<VAL>(sm, sj, ej, lo[k], hi[k], lerr);
             }
-            emit(lo, hi, got + g, take - g < 64 ? take - g : 64);
+            emit(lo, hi, got + g, take - g < 64 * K ? take - g : 64 * K);
         }
         if (VAL == VAL_U64_STRICT && __any(lerr) && !err) err = COVT_ERR_BAD_HEADER;
         pos = w.woff + (int32_t)uniu(sm.u.v.list[r + take - 1]) + 1;
@@ -599,24 +615,32 @@ __device__ void run_varint_stream(Ctx& c) {
     Carry cr{0, 0};
     Win w;
     w.valid = false;
-    auto sink1 = [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
-        uint32_t v[1] = {lo};
-        sink_values<OP, 1>(v, base, count, c.nb, c.out, cr);
+    auto sink4 = [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t count) {
+        sink_values<OP, 4>(lo, base, count, c.nb, c.out, cr);
     };
     if constexpr (OP == COVT_OP_VARINT_U64) {
         int64_t* o = (int64_t*)c.out;
-        varint_take<MODE_RAW, VAL_U64_STRICT>(*c.sm, c.sb, w, pos, c.avail, c.n, false, c.err,
-                                              [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
-                                                  if (lane_id() < count)
-                                                      st_out(o + base + lane_id(), (int64_t)(((uint64_t)hi << 32) | lo));
-                                              });
+        varint_take<MODE_RAW, VAL_U64_STRICT, 4>(
+            *c.sm, c.sb, w, pos, c.avail, c.n, false, c.err,
+            [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t count) {
+                const int32_t nvalid = count - 4 * lane_id();
+                int64_t* p = o + base + 4 * lane_id();
+                if (count >= 256) {
+                    st_out16((int32_t*)p, make_int4((int)lo[0], (int)hi[0], (int)lo[1], (int)hi[1]));
+                    st_out16((int32_t*)(p + 2), make_int4((int)lo[2], (int)hi[2], (int)lo[3], (int)hi[3]));
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (k < nvalid) st_out(p + k, (int64_t)(((uint64_t)hi[k] << 32) | lo[k]));
+                }
+            });
     } else {
         if ((OP == COVT_OP_VARINT_ZZ_DELTA_XY) && (c.n & 1)) {
             // Java decodes the x,y pair and then overruns values[] (ArrayIndexOutOfBounds)
-            varint_take<MODE_RAW, VAL_J4>(*c.sm, c.sb, w, pos, c.avail, c.n - 1, false, c.err, sink1);
+            varint_take<MODE_RAW, VAL_J4, 4>(*c.sm, c.sb, w, pos, c.avail, c.n - 1, false, c.err, sink4);
             if (!c.err) c.err = COVT_ERR_COUNT_MISMATCH;
         } else {
-            varint_take<MODE_RAW, VAL_J4>(*c.sm, c.sb, w, pos, c.avail, c.n, false, c.err, sink1);
+            varint_take<MODE_RAW, VAL_J4, 4>(*c.sm, c.sb, w, pos, c.avail, c.n, false, c.err, sink4);
         }
     }
     c.consumed = pos;
@@ -722,11 +746,12 @@ __device__ void run_rle_int(Ctx& c) {
                     // a literal group longer than a window (up to 128 x 10 B): multi-window varint path
                     const int32_t cnt = 0x100 - (int32_t)cb, lim = c.n - done, d0 = done;
                     int32_t p1 = pos + 1;
-                    varint_take<MODE_RAW, VAL_U64>(sm, c.sb, w, p1, c.avail, cnt, false, c.err,
-                                                   [&](uint32_t lo, uint32_t hi, int32_t base, int32_t count) {
-                                                       const int32_t k = base + l;
-                                                       if (l < count && k < lim) store(d0 + k, ((uint64_t)hi << 32) | lo);
-                                                   });
+                    varint_take<MODE_RAW, VAL_U64>(
+                        sm, c.sb, w, p1, c.avail, cnt, false, c.err,
+                        [&](const uint32_t (&lo)[1], const uint32_t (&hi)[1], int32_t base, int32_t count) {
+                            const int32_t k = base + l;
+                            if (l < count && k < lim) store(d0 + k, ((uint64_t)hi[0] << 32) | lo[0]);
+                        });
                     out = done + (cnt < lim ? cnt : lim);
                     pj = p1 - woff;
                     COVT_PHASE(c, 5);
@@ -1245,9 +1270,8 @@ __device__ void run_fastpfor(Ctx& c) {
             w.valid = false;
             const int32_t got = varint_take<MODE_WORDREV, VAL_VB>(
                 sm, c.sb, w, vpos, (int32_t)(4 * nw), c.n - L, true, c.err,
-                [&](uint32_t lo, uint32_t hi, int32_t vb, int32_t count) {
-                    uint32_t vv[1] = {lo};
-                    sink_values<OP, 1>(vv, (int64_t)base + vb, count, c.nb, c.out, cr);
+                [&](const uint32_t (&lo)[1], const uint32_t (&hi)[1], int32_t vb, int32_t count) {
+                    sink_values<OP, 1>(lo, (int64_t)base + vb, count, c.nb, c.out, cr);
                 });
             decoded = L + got;
         }
