@@ -1405,12 +1405,47 @@ __device__ __forceinline__ int32_t lane_vulong(LaneBytes& in, int32_t& p, uint64
     v = r;
     return COVT_OK;
 }
+// A lane's output gathered into 16-byte packets: one store per 16 bytes instead of one per value
+// (each lane writes a different stream, so every store instruction touches 64 separate lines).
+// The last packet is written whole: stream outputs start 16-byte aligned and are padded to 16.
+struct Pack16 {
+    uint32_t w0, w1, w2, w3;
+    uint32_t nb;   // bytes in the packet
+    uint8_t* dst;  // the packet's address
+    __device__ __forceinline__ void flush() {
+        *(uint4*)dst = make_uint4(w0, w1, w2, w3);
+        dst += 16;
+    }
+    __device__ __forceinline__ void put32(uint32_t v) {
+        const uint32_t k = (nb >> 2) & 3u;
+        w0 = k == 0 ? v : w0;
+        w1 = k == 1 ? v : w1;
+        w2 = k == 2 ? v : w2;
+        w3 = k == 3 ? v : w3;
+        nb += 4;
+        if ((nb & 15u) == 0) flush();
+    }
+    __device__ __forceinline__ void put8(uint32_t b) {
+        const uint32_t k = (nb >> 2) & 3u, sh = 8u * (nb & 3u);
+        const uint32_t m = ~(0xffu << sh), x = b << sh;
+        w0 = k == 0 ? (w0 & m) | x : w0;
+        w1 = k == 1 ? (w1 & m) | x : w1;
+        w2 = k == 2 ? (w2 & m) | x : w2;
+        w3 = k == 3 ? (w3 & m) | x : w3;
+        nb += 1;
+        if ((nb & 15u) == 0) flush();
+    }
+    __device__ __forceinline__ void finish() {
+        if (nb & 15u) flush();
+    }
+};
 __device__ void lane_rle_int(LaneBytes& in, int op, int32_t n, uint8_t* out, int32_t& err, int32_t& consumed) {
     const bool is_signed = op == COVT_OP_RLE_S64, to_i32 = op == COVT_OP_RLE_I32;
     int32_t o = 0, done = 0;
+    Pack16 pk{0, 0, 0, 0, 0, out};
     auto put = [&](int64_t v) {
-        if (to_i32) ((int32_t*)out)[done] = (int32_t)v;
-        else ((int64_t*)out)[done] = v;
+        pk.put32((uint32_t)v);
+        if (!to_i32) pk.put32((uint32_t)((uint64_t)v >> 32));
         ++done;
     };
     while (done < n) {
@@ -1434,11 +1469,13 @@ __device__ void lane_rle_int(LaneBytes& in, int op, int32_t n, uint8_t* out, int
             }
         }
     }
+    pk.finish();
     consumed = o;
 }
 __device__ void lane_rle_byte(LaneBytes& in, int32_t n, uint8_t* out, int32_t& err, int32_t& consumed) {
     int32_t o = 0, done = 0;
     bool bad = false;
+    Pack16 pk{0, 0, 0, 0, 0, out};
     while (done < n) {
         if (o >= in.avail) { err = COVT_ERR_TRUNCATED; return; }
         const uint32_t control = in.at(o++);
@@ -1448,7 +1485,8 @@ __device__ void lane_rle_byte(LaneBytes& in, int32_t n, uint8_t* out, int32_t& e
             const uint32_t b = in.at(o++);
             bad |= b > 5u;
             const int32_t k = cnt < n - done ? cnt : n - done;
-            for (int32_t i = 0; i < k; ++i) out[done++] = (uint8_t)b;
+            for (int32_t i = 0; i < k; ++i) pk.put8(b);
+            done += k;
         } else {
             const int32_t cnt = 0x100 - (int32_t)control;
             if (o + cnt > in.avail) { err = COVT_ERR_TRUNCATED; return; }
@@ -1456,11 +1494,13 @@ __device__ void lane_rle_byte(LaneBytes& in, int32_t n, uint8_t* out, int32_t& e
                 const uint32_t b = in.at(o++);
                 if (done < n) {
                     bad |= b > 5u;
-                    out[done++] = (uint8_t)b;
+                    pk.put8(b);
+                    ++done;
                 }
             }
         }
     }
+    pk.finish();
     if (bad) err = COVT_ERR_BAD_HEADER;  // GeometryType.values()[b]
     consumed = o;
 }

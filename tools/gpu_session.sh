@@ -27,6 +27,7 @@ for s in "$@"; do
     ops) step op_breakdown 600 python tools/op_breakdown.py ;;
     timeline) step timeline 300 python tools/stream_timeline.py ;;
     hbm) step hbm 300 python tools/hbm_probe.py ;;
+    wpat) step wpat 300 python tools/probe/write_pattern.py ;;
     ab) for v in ${AB_VARIANTS:-libcovt_base.so libcovt.so libcovt_base.so libcovt.so}; do
             echo "== ab $v"; COVT_LIB_VARIANT=$v OPB_QUICK=1 timeout -k 10 300 python tools/op_breakdown.py 2>&1 | grep -v amdgpu.ids || fatal ab $?
         done ;;
