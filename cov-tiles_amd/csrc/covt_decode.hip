@@ -216,42 +216,51 @@ __device__ __forceinline__ void st_out16(int32_t* p, int4 v) {
 }
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v) {
+#if defined(COVT_ABL_NOSTORE)  // ablation build: narrow stores all land on one address
+    *(T*)((uintptr_t)p & ~(uintptr_t)1023) = v;
+#else
     *p = v;
+#endif
 }
 __device__ __forceinline__ int64_t pack_xy(int32_t x, int32_t y) {
     return (int64_t)(((uint64_t)(uint32_t)y << 32) | (uint32_t)x);
 }
 
-// Per-op output transform, specialised at compile time.  `count` (uniform) values are valid; a full
-// group (count >= 64 K) takes the branch-free path with vector stores, a partial one masks lanes.
+// Per-op output transform, specialised at compile time.  Lane l holds slots base + K l .. + K - 1;
+// slots [first, first + count) of the group are values (uniform; `first` < K skips leading slots so
+// that `base` can stay a multiple of K and 16-byte stores stay aligned).  A full group takes the
+// branch-free path; otherwise lanes whose K slots are all values still store 16 bytes at once and
+// only the boundary lanes store element by element.  Invalid slots enter the delta scans as 0.
 template <int OP, int K>
-__device__ __forceinline__ void sink_values(const uint32_t (&vin)[K], int64_t base, int32_t count, int nb,
-                                            uint8_t* __restrict__ out, Carry& c) {
+__device__ __forceinline__ void sink_values(const uint32_t (&vin)[K], int64_t base, int32_t first, int32_t count,
+                                            int nb, uint8_t* __restrict__ out, Carry& c) {
     const int l = lane_id();
-    const bool full = count >= 64 * K;
-    const int32_t nvalid = count - l * K;
+    const bool full = first == 0 && count >= 64 * K;
+    const int32_t s0 = l * K - first;  // value index of this lane's slot 0
+    const bool lfull = full || (s0 >= 0 && s0 + K <= count);
     const int64_t i0 = base + (int64_t)l * K;
+    bool ok[K];
     uint32_t v[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = (full || k < nvalid) ? vin[k] : 0u;
+    for (int k = 0; k < K; ++k) {
+        ok[k] = full || (s0 + k >= 0 && s0 + k < count);
+        v[k] = ok[k] ? vin[k] : 0u;
+    }
     auto st32 = [&](const int32_t (&r)[K]) {
         int32_t* o = (int32_t*)out + i0;
-        if (full) {
-            if (K == 4) st_out16(o, make_int4(r[0], r[K > 1 ? 1 : 0], r[K > 2 ? 2 : 0], r[K > 3 ? 3 : 0]));
-            else
-#pragma unroll
-                for (int k = 0; k < K; ++k) st_out(o + k, r[k]);
+        if (K == 4 && lfull) {
+            st_out16(o, make_int4(r[0], r[K > 1 ? 1 : 0], r[K > 2 ? 2 : 0], r[K > 3 ? 3 : 0]));
         } else {
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (k < nvalid) st_out(o + k, r[k]);
+                if (ok[k]) st_out(o + k, r[k]);
         }
     };
     auto st64 = [&](const int64_t (&r)[K]) {
         int64_t* o = (int64_t*)out + i0;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (full || k < nvalid) st_out(o + k, r[k]);
+            if (ok[k]) st_out(o + k, r[k]);
     };
     if constexpr (OP == COVT_OP_VARINT_I32 || OP == COVT_OP_VARINT_ZZ_I32) {
         int32_t r[K];
@@ -269,7 +278,7 @@ __device__ __forceinline__ void sink_values(const uint32_t (&vin)[K], int64_t ba
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            acc += (uint32_t)zz32(v[k]);  // masked lanes hold 0 -> zz 0
+            acc += (uint32_t)zz32(v[k]);  // invalid slots hold 0 -> zz 0
             sacc[k] = acc;
         }
         const uint32_t inc = incl_scan(acc);
@@ -326,18 +335,13 @@ __device__ __forceinline__ void sink_values(const uint32_t (&vin)[K], int64_t ba
             xy[2 * k] = (int32_t)((uint32_t)morton_axis(code, nb) - (uint32_t)half);
             xy[2 * k + 1] = (int32_t)((uint32_t)morton_axis(code >> 1, nb) - (uint32_t)half);
         }
-        if (full) {
-            if (K == 4) {
-                st_out16(o, make_int4(xy[0], xy[1], xy[K > 1 ? 2 : 0], xy[K > 1 ? 3 : 0]));
-                st_out16(o + 4, make_int4(xy[K > 2 ? 4 : 0], xy[K > 2 ? 5 : 0], xy[K > 3 ? 6 : 0], xy[K > 3 ? 7 : 0]));
-            } else {
-#pragma unroll
-                for (int k = 0; k < K; ++k) st_out((int64_t*)(o + 2 * k), pack_xy(xy[2 * k], xy[2 * k + 1]));
-            }
+        if (K == 4 && lfull) {
+            st_out16(o, make_int4(xy[0], xy[1], xy[K > 1 ? 2 : 0], xy[K > 1 ? 3 : 0]));
+            st_out16(o + 4, make_int4(xy[K > 2 ? 4 : 0], xy[K > 2 ? 5 : 0], xy[K > 3 ? 6 : 0], xy[K > 3 ? 7 : 0]));
         } else {
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (k < nvalid) st_out((int64_t*)(o + 2 * k), pack_xy(xy[2 * k], xy[2 * k + 1]));
+                if (ok[k]) st_out((int64_t*)(o + 2 * k), pack_xy(xy[2 * k], xy[2 * k + 1]));
         }
         c.x += lane_bcast(inc, 63);
     }
@@ -516,13 +520,15 @@ __device__ __forceinline__ void win_value(const WaveSmem& sm, int32_t sj, int32_
 }
 
 // Decode up to `want` values starting at stream position `pos` (a value boundary; updated) with
-// bytes valid in [pos, end).  emit(lo[K], hi[K], base, count) is called per group of <= 64 K values,
-// lane l holding values base + K l .. base + K l + K - 1.  Returns the number of values decoded.
-// With `until_end` (VariableByte tail) the region is decoded to its end, a trailing partial value
-// is dropped and more than `want` values is an error.
+// bytes valid in [pos, end).  emit(lo[K], hi[K], base, first, count) is called per group of 64 K
+// slots, lane l holding slots base + K l .. base + K l + K - 1 (base counted from this call's first
+// value, which is output index out0: groups are aligned so that out0 + base is a multiple of K);
+// slots [first, first + count) are values.  Returns the number of values decoded.  With `until_end`
+// (VariableByte tail) the region is decoded to its end, a trailing partial value is dropped and
+// more than `want` values is an error.
 template <int MODE, int VAL, int K = 1, class Emit>
 __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t& pos, int32_t end, int32_t want,
-                               bool until_end, int32_t& err, Emit&& emit) {
+                               bool until_end, int32_t& err, Emit&& emit, int32_t out0 = 0) {
     const int l = lane_id();
     int32_t got = 0;
     while (until_end ? (pos < end) : (got < want)) {
@@ -551,17 +557,20 @@ __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t&
         if (take <= 0) break;
         bool lerr = false;
         const int32_t s0 = pos - w.woff;
-        for (int32_t g = 0; g < take; g += 64 * K) {
+        const int32_t lead = (K > 1) ? ((out0 + got) & (K - 1)) : 0;  // slots before the first value
+        for (int32_t g = -lead; g < take; g += 64 * K) {
             uint32_t lo[K], hi[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 int32_t vi = g + K * l + k;
-                vi = vi < take ? vi : take - 1;  // lanes past the end repeat the last value (not emitted)
+                vi = vi < 0 ? 0 : (vi < take ? vi : take - 1);  // slots outside repeat an edge value (not emitted)
                 const int32_t ej = sm.u.v.list[r + vi];
                 const int32_t sj = vi == 0 ? s0 : (int32_t)sm.u.v.list[r + vi - 1] + 1;
                 win_value<VAL>(sm, sj, ej, lo[k], hi[k], lerr);
             }
-            emit(lo, hi, got + g, take - g < 64 * K ? take - g : 64 * K);
+            const int32_t first = g < 0 ? -g : 0;
+            const int32_t cnt = (take - g < 64 * K ? take - g : 64 * K) - first;
+            emit(lo, hi, got + g, first, cnt);
         }
         if (VAL == VAL_U64_STRICT && __any(lerr) && !err) err = COVT_ERR_BAD_HEADER;
         pos = w.woff + (int32_t)uniu(sm.u.v.list[r + take - 1]) + 1;
@@ -615,23 +624,23 @@ __device__ void run_varint_stream(Ctx& c) {
     Carry cr{0, 0};
     Win w;
     w.valid = false;
-    auto sink4 = [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t count) {
-        sink_values<OP, 4>(lo, base, count, c.nb, c.out, cr);
+    auto sink4 = [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
+        sink_values<OP, 4>(lo, base, first, count, c.nb, c.out, cr);
     };
     if constexpr (OP == COVT_OP_VARINT_U64) {
         int64_t* o = (int64_t*)c.out;
         varint_take<MODE_RAW, VAL_U64_STRICT, 4>(
             *c.sm, c.sb, w, pos, c.avail, c.n, false, c.err,
-            [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t count) {
-                const int32_t nvalid = count - 4 * lane_id();
+            [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
+                const int32_t s0 = 4 * lane_id() - first;
                 int64_t* p = o + base + 4 * lane_id();
-                if (count >= 256) {
+                if (s0 >= 0 && s0 + 4 <= count) {
                     st_out16((int32_t*)p, make_int4((int)lo[0], (int)hi[0], (int)lo[1], (int)hi[1]));
                     st_out16((int32_t*)(p + 2), make_int4((int)lo[2], (int)hi[2], (int)lo[3], (int)hi[3]));
                 } else {
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        if (k < nvalid) st_out(p + k, (int64_t)(((uint64_t)hi[k] << 32) | lo[k]));
+                        if (s0 + k >= 0 && s0 + k < count) st_out(p + k, (int64_t)(((uint64_t)hi[k] << 32) | lo[k]));
                 }
             });
     } else {
@@ -748,7 +757,7 @@ __device__ void run_rle_int(Ctx& c) {
                     int32_t p1 = pos + 1;
                     varint_take<MODE_RAW, VAL_U64>(
                         sm, c.sb, w, p1, c.avail, cnt, false, c.err,
-                        [&](const uint32_t (&lo)[1], const uint32_t (&hi)[1], int32_t base, int32_t count) {
+                        [&](const uint32_t (&lo)[1], const uint32_t (&hi)[1], int32_t base, int32_t, int32_t count) {
                             const int32_t k = base + l;
                             if (l < count && k < lim) store(d0 + k, ((uint64_t)hi[0] << 32) | lo[0]);
                         });
@@ -1246,9 +1255,9 @@ __device__ void run_fastpfor(Ctx& c) {
                 }
                 COVT_PHASE(c, 4);
 #if defined(COVT_ABL_NOSTORE)  // ablation build: every block's output to the same 1 KiB (L2-resident)
-                sink_values<OP, 4>(v, 0, kFpfBlock, c.nb, c.out, cr);
+                sink_values<OP, 4>(v, 0, 0, kFpfBlock, c.nb, c.out, cr);
 #else
-                sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, c.nb, c.out, cr);
+                sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, 0, kFpfBlock, c.nb, c.out, cr);
 #endif
                 wave_sync();
                 COVT_PHASE(c, 5);
@@ -1270,8 +1279,8 @@ __device__ void run_fastpfor(Ctx& c) {
             w.valid = false;
             const int32_t got = varint_take<MODE_WORDREV, VAL_VB>(
                 sm, c.sb, w, vpos, (int32_t)(4 * nw), c.n - L, true, c.err,
-                [&](const uint32_t (&lo)[1], const uint32_t (&hi)[1], int32_t vb, int32_t count) {
-                    sink_values<OP, 1>(lo, (int64_t)base + vb, count, c.nb, c.out, cr);
+                [&](const uint32_t (&lo)[1], const uint32_t (&hi)[1], int32_t vb, int32_t, int32_t count) {
+                    sink_values<OP, 1>(lo, (int64_t)base + vb, 0, count, c.nb, c.out, cr);
                 });
             decoded = L + got;
         }
@@ -1280,7 +1289,7 @@ __device__ void run_fastpfor(Ctx& c) {
     if (!c.err) {
         for (int32_t b = decoded; b < c.n; b += 64) {
             uint32_t vv[1] = {0};
-            sink_values<OP, 1>(vv, b, c.n - b < 64 ? c.n - b : 64, c.nb, c.out, cr);
+            sink_values<OP, 1>(vv, b, 0, c.n - b < 64 ? c.n - b : 64, c.nb, c.out, cr);
         }
         if (OP == COVT_OP_FPF_ZZ_DELTA_XY && (c.n & 1)) c.err = COVT_ERR_COUNT_MISMATCH;
     }
