@@ -220,9 +220,9 @@ def main():
             "kernel_ms": round(kern_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "covt decode launch = decode_family_kernel<RLE|VARINT|FASTPFOR> run "
-                                   "concurrently between fork/join events; duration = HIP events on the "
-                                   "launch stream",
+                         "kernel": "covt decode launch = decode_family_kernel<RLE|VARINT|FASTPFOR> + "
+                                   "decode_lane_kernel run concurrently between fork/join events; "
+                                   "duration = HIP events on the launch stream",
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": None,
         }

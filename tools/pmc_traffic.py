@@ -3,8 +3,8 @@
 
 Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports
 1/2 of the bytes of wide coalesced streaming reads (16 B/lane loads), so the read side is doubled.
-A grouped launch = one dispatch per codec family; traffic per launch sums the last launch's three
-dispatches.  Writes profiles/pmc_traffic.json for bench.py."""
+A grouped launch = one dispatch per kernel family (RLE, varint, FastPFOR, lane); traffic per launch
+sums the last launch's four dispatches.  Writes profiles/pmc_traffic.json for bench.py."""
 import csv
 import json
 import os
@@ -12,11 +12,13 @@ import sys
 
 
 def last_launch(path, counter):
-    rows = [r for r in csv.DictReader(open(path)) if "decode_family" in r["Kernel_Name"]
+    rows = [r for r in csv.DictReader(open(path)) if ("decode_family" in r["Kernel_Name"] or
+                                                        "decode_lane" in r["Kernel_Name"])
             and r["Counter_Name"] == counter]
     by = {}
     for r in rows:
-        fam = r["Kernel_Name"].split("<")[1].split(">")[0]
+        k = r["Kernel_Name"]
+        fam = k.split("<")[1].split(">")[0] if "decode_family" in k else "lane"
         by.setdefault(fam, []).append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     return {f: sorted(v)[-1][1] for f, v in by.items()}
 

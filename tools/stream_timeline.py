@@ -52,6 +52,20 @@ def main():
     t0 = st_t.min()
     end_t = st_t - t0 + d_t
     print("launch span %.1f us (first start -> last end); %d streams" % (end_t.max() * TICK_US, len(s)))
+    # concurrency profile: streams in flight per 5% of the span, and the output bytes finished per slice
+    span = end_t.max()
+    nb = 20
+    ob = (s["out_elems"] * s["elem_bytes"]).astype(np.float64)
+    line_w, line_b = [], []
+    for q in range(nb):
+        t0q, t1q = span * q / nb, span * (q + 1) / nb
+        st_rel = st_t - t0
+        live = ((st_rel < t1q) & (end_t > t0q)).sum()
+        fin = ob[(end_t > t0q) & (end_t <= t1q)].sum()
+        line_w.append("%5d" % live)
+        line_b.append("%5.0f" % (fin / 1e6))
+    print("streams in flight per 5%% of the launch: " + " ".join(line_w))
+    print("output MB finished per 5%% slice:        " + " ".join(line_b))
     print("last 8 streams to finish (op, bytes, values, start us, duration us):")
     for i in np.argsort(-end_t)[:8]:
         print("   %-12s %8d %8d  start %7.1f  dur %7.1f" % (NAMES.get(int(op_t[i]), op_t[i]), s["byte_length"][i],
