@@ -29,7 +29,10 @@
 namespace covt {
 
 constexpr int kWin = 1024;  // window bytes (64 lanes x 16 B)
-constexpr int kWavesPerBlock = 4;
+#ifndef COVT_WAVES_PER_BLOCK
+#define COVT_WAVES_PER_BLOCK 4
+#endif
+constexpr int kWavesPerBlock = COVT_WAVES_PER_BLOCK;  // independent waves (streams) per workgroup
 constexpr int kFpfBlock = 256;
 constexpr int kFpfPage = 65536;
 constexpr int kFpfBcCap = 3 * kFpfPage / kFpfBlock + kFpfPage;  // JavaFastPFOR byteContainer size
@@ -1307,7 +1310,7 @@ __host__ __device__ constexpr int op_family(int op) {
 // One wave per descriptor; waves whose descriptor belongs to another family return at once (used
 // when the caller's descriptors are not grouped by family).
 template <int FAM>
-__global__ __launch_bounds__(256) void decode_family_kernel(const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(const uint8_t* __restrict__ in,
                                                             const covt_stream_desc* __restrict__ descs,
                                                             int64_t n_streams, uint8_t* __restrict__ out,
                                                             covt_stream_result* __restrict__ res) {

@@ -53,6 +53,33 @@ def main():
             b = int(nbytes[offs[f]:offs[f + 1]].sum())
             t = run(int(offs[f]), int(offs[f + 1]), nt)
             print("  %-8s nt=%d: %.3f ms  %.0f GB/s (%d MB)" % (name, nt, t, b / t / 1e6, b // 1000000))
+    lib.probe_copy_regions.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p,
+                                       C.c_void_p]
+    sink = torch.zeros(4, dtype=torch.int32, device="cuda")
+
+    def runc(lo, hi, reps=5):
+        args = (batch.d_in.data_ptr(), batch.d_desc.data_ptr() + 32 * lo, d_nb.data_ptr() + 8 * lo, hi - lo,
+                batch.d_out.data_ptr(), 1, sink.data_ptr(), stream.cuda_stream)
+        for _ in range(2):
+            lib.probe_copy_regions(*args)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            lib.probe_copy_regions(*args)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    ib = plan.descs.reshape(-1, 32)[:, 28:32].copy().view(np.int32).ravel().astype(np.int64)
+    t = runc(0, plan.num_streams)
+    print("read+write pattern, all streams (nt): %.3f ms  %.0f GB/s (r %d MB + w %d MB)" % (
+        t, (ib.sum() + nbytes.sum()) / t / 1e6, ib.sum() // 1000000, nbytes.sum() // 1000000))
+    for f, name in enumerate(("RLE", "VARINT", "FASTPFOR", "LANE")):
+        lo, hi = int(offs[f]), int(offs[f + 1])
+        t = runc(lo, hi)
+        tb = int(ib[lo:hi].sum() + nbytes[lo:hi].sum())
+        print("  %-8s read+write: %.3f ms  %.0f GB/s" % (name, t, tb / t / 1e6))
     x = torch.empty(int(nbytes.sum()) // 4, dtype=torch.int32, device="cuda")
     t = bench_fill(x)
     print("linear fill of the same bytes: %.3f ms  %.0f GB/s" % (t, 4 * x.numel() / t / 1e6))
