@@ -229,6 +229,44 @@ __device__ __forceinline__ int64_t pack_xy(int32_t x, int32_t y) {
     return (int64_t)(((uint64_t)(uint32_t)y << 32) | (uint32_t)x);
 }
 
+// An arithmetic run v(i) = base + i * delta, i in [0, n), written at element index o of an E-byte
+// array (E = 1, 4 or 8; the array is 16-byte aligned): the 16-byte-aligned body with one 16-byte
+// nontemporal store per lane (lanes past the end repeat the last chunk), the unaligned head and
+// tail element by element.  Wave-uniform arguments.
+template <int E>
+__device__ __forceinline__ void store_run(uint8_t* arr, int32_t o, int32_t n, int64_t base, int32_t delta) {
+    constexpr int K = 16 / E;
+    const int l = lane_id();
+    auto val = [&](int32_t i) -> int64_t { return (int64_t)((uint64_t)base + (uint64_t)(int64_t)(int32_t)(i * delta)); };
+    const int32_t a0 = (o + K - 1) & ~(K - 1);  // first aligned element
+    const int32_t head = min(a0 - o, n);
+    const int32_t nch = (n - head) / K;         // whole 16-byte chunks
+    const int32_t body_end = head + nch * K;
+    // head and tail: at most 2 (K - 1) elements, one lane each
+    const int32_t ti = l < head ? l : body_end + (l - head);
+    if (l < head || (l - head < n - body_end && l >= head)) {
+        const int64_t v = val(ti);
+        if (E == 8) st_out((int64_t*)arr + o + ti, v);
+        else if (E == 4) st_out((int32_t*)arr + o + ti, (int32_t)v);
+        else st_out(arr + o + ti, (uint8_t)v);
+    }
+    for (int32_t c0 = 0; c0 < nch; c0 += 64) {
+        const int32_t ch = c0 + l < nch ? c0 + l : nch - 1;
+        const int32_t i = head + K * ch;  // run index of the chunk's first element
+        int4 w;
+        if (E == 8) {
+            const int64_t v0 = val(i), v1 = val(i + 1);
+            w = make_int4((int)v0, (int)(v0 >> 32), (int)v1, (int)(v1 >> 32));
+        } else if (E == 4) {
+            w = make_int4((int)val(i), (int)val(i + 1), (int)val(i + 2), (int)val(i + 3));
+        } else {  // byte runs: delta 0 (ORC byte runs repeat one value)
+            const uint32_t b = (uint32_t)base & 0xffu, q = b * 0x01010101u;
+            w = make_int4((int)q, (int)q, (int)q, (int)q);
+        }
+        st_out16((int32_t*)(arr + (int64_t)(o + i) * E), w);
+    }
+}
+
 // Per-op output transform, specialised at compile time.  Lane l holds slots base + K l .. + K - 1;
 // slots [first, first + count) of the group are values (uniform; `first` < K skips leading slots so
 // that `base` can stay a multiple of K and 16-byte stores stay aligned).  A full group takes the
@@ -828,12 +866,8 @@ __device__ void run_rle_int(Ctx& c) {
                         const int32_t d2 = (int32_t)lane_bcast((uint32_t)delta, src);
                         const int64_t bb = (int64_t)(((uint64_t)lane_bcast((uint32_t)((uint64_t)b64 >> 32), src) << 32) |
                                                      lane_bcast((uint32_t)b64, src));
-                        for (int32_t i0 = 0; i0 < t2; i0 += 64) {  // literals[0] + used * delta
-                            const int32_t i = i0 + l < t2 ? i0 + l : t2 - 1;
-                            const int64_t v = (int64_t)((uint64_t)bb + (uint64_t)(int64_t)(int32_t)(i * d2));
-                            if (to_i32) st_out((int32_t*)c.out + o2 + i, (int32_t)v);
-                            else st_out((int64_t*)c.out + o2 + i, v);
-                        }
+                        if (to_i32) store_run<4>(c.out, o2, t2, bb, d2);  // literals[0] + used * delta
+                        else store_run<8>(c.out, o2, t2, bb, d2);
                     } else {
                         const int32_t r = (int32_t)lane_bcast((uint32_t)rr, src);
                         const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
@@ -928,8 +962,7 @@ __device__ void run_rle_byte(Ctx& c) {
                 const int32_t o2 = (int32_t)lane_bcast((uint32_t)goff, src);
                 const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
                 if (lane_bcast(cb, src) < 0x80u) {
-                    const uint8_t v = (uint8_t)lane_bcast(rv, src);
-                    for (int32_t i0 = 0; i0 < t2; i0 += 64) st_out(c.out + o2 + (i0 + l < t2 ? i0 + l : t2 - 1), v);
+                    store_run<1>(c.out, o2, t2, (int64_t)lane_bcast(rv, src), 0);
                 } else {
                     const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
                     for (int32_t i0 = 0; i0 < t2; i0 += 64) {
