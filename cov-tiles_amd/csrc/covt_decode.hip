@@ -1420,16 +1420,35 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(cons
 // A wave-per-stream decode spends its fixed window/index setup on a handful of values; here 64
 // such streams share one wave's instructions.
 // --------------------------------------------------------------------------------------------
-constexpr int kLaneSlot = 17;  // LDS dwords per lane: a stream of <= kLaneMaxBytes bytes + misalignment
-static_assert(4 * kLaneSlot >= kLaneMaxBytes + 4, "lane slot");
-struct LaneBytes {  // the lane's stream staged in its LDS slot; sequential reads with a one-dword cache
-    const uint32_t* slot;
-    uint32_t mis;  // stream start within slot dword 0
+constexpr int kLaneSlot = 17;  // LDS dwords per lane: a 68-byte sliding window of the lane's stream
+struct LaneBytes {  // the lane's stream through a window in its LDS slot; one-dword read cache
+    const uint8_t* sb;
+    uint32_t* slot;
     int32_t avail;
+    int32_t w0;  // stream offset of slot byte 0 (4-byte aligned in memory)
     int32_t cq;
     uint32_t cw;
+    // window = stream bytes [w0, w0 + 68) from p's 4-byte aligned address; 4 x 16 B + 4 B loads at once
+    __device__ __forceinline__ void load(int32_t p) {
+        const uintptr_t a = (uintptr_t)(sb + p), a4 = a & ~(uintptr_t)3;
+        w0 = p - (int32_t)(a & 3u);
+        uint32_t st[kLaneSlot];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(a4 + 16 * k);
+            st[4 * k] = v.x;
+            st[4 * k + 1] = v.y;
+            st[4 * k + 2] = v.z;
+            st[4 * k + 3] = v.w;
+        }
+        st[16] = *g32(a4 + 64);
+#pragma unroll
+        for (int k = 0; k < kLaneSlot; ++k) slot[k * 256] = st[k];
+        cq = -1;
+    }
     __device__ __forceinline__ uint32_t at(int32_t p) {
-        const int32_t a = p + (int32_t)mis, q = a >> 2;
+        if (p - w0 >= 4 * kLaneSlot) load(p);  // slides forward (reads are sequential)
+        const int32_t a = p - w0, q = a >> 2;
         if (q != cq) {
             cq = q;
             cw = slot[q * 256];
@@ -1563,24 +1582,10 @@ __global__ __launch_bounds__(256) void decode_lane_kernel(const uint8_t* __restr
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     int32_t err = 0, consumed = 0;
-    // stage the stream's bytes: 4 x 16 + 4 bytes from its 4-byte aligned start, loads issued together
-    uint32_t* slot = slots + threadIdx.x;  // dword k of lane t at slots[k * 256 + t]: conflict-free
-    const uintptr_t a = (uintptr_t)(in + d.in_off);
-    const uintptr_t a4 = a & ~(uintptr_t)3;
-    uint32_t st[kLaneSlot];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(a4 + 16 * k);
-        st[4 * k] = v.x;
-        st[4 * k + 1] = v.y;
-        st[4 * k + 2] = v.z;
-        st[4 * k + 3] = v.w;
-    }
-    st[16] = *g32(a4 + 64);
-#pragma unroll
-    for (int k = 0; k < kLaneSlot; ++k) slot[k * 256] = st[k];
-    LaneBytes lb{slot, (uint32_t)(a & 3u), d.avail, -1, 0u};
-    if (d.num_values < 0 || d.avail < 0 || d.avail > kLaneMaxBytes) err = COVT_ERR_INVALID_ARG;
+    // the stream's first 68 bytes into the lane's slot (dword k of lane t at slots[k * 256 + t])
+    LaneBytes lb{in + d.in_off, slots + threadIdx.x, d.avail, 0, -1, 0u};
+    lb.load(0);
+    if (d.num_values < 0 || d.avail < 0) err = COVT_ERR_INVALID_ARG;
     else if (d.op == COVT_OP_BYTE_RLE_U8) lane_rle_byte(lb, d.num_values, out + d.out_off, err, consumed);
     else if (d.op == COVT_OP_RLE_U64 || d.op == COVT_OP_RLE_S64 || d.op == COVT_OP_RLE_I32)
         lane_rle_int(lb, d.op, d.num_values, out + d.out_off, err, consumed);
