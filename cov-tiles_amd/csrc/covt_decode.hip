@@ -605,9 +605,20 @@ __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t&
             for (int k = 0; k < K; ++k) {
                 int32_t vi = g + K * l + k;
                 vi = vi < 0 ? 0 : (vi < take ? vi : take - 1);  // slots outside repeat an edge value (not emitted)
-                const int32_t ej = sm.u.v.list[r + vi];
-                const int32_t sj = vi == 0 ? s0 : (int32_t)sm.u.v.list[r + vi - 1] + 1;
-                win_value<VAL>(sm, sj, ej, lo[k], hi[k], lerr);
+                const int32_t li = r + vi - 1;
+                const int32_t pv = (int32_t)sm.u.v.list[li < 0 ? 0 : li] + 1;
+                const int32_t sj = vi == 0 ? s0 : pv;  // the value starts after the previous terminator
+                if constexpr (VAL == VAL_J4) {
+                    // Java's 4-byte-capped varint: its bytes end at the first terminator among the 4 at
+                    // sj (or all 4): mask = bits up to that terminator's bit 7, no length needed
+                    const int32_t dq = sj >> 2;
+                    const uint32_t x = __builtin_amdgcn_alignbyte(sm.u.v.win[dq + 1], sm.u.v.win[dq], (uint32_t)sj & 3u);
+                    const uint32_t u = ~x & 0x80808080u;
+                    lo[k] = pext7(x & (u ^ (u - 1u)));
+                    hi[k] = 0;
+                } else {
+                    win_value<VAL>(sm, sj, sm.u.v.list[r + vi], lo[k], hi[k], lerr);
+                }
             }
             const int32_t first = g < 0 ? -g : 0;
             const int32_t cnt = (take - g < 64 * K ? take - g : 64 * K) - first;
