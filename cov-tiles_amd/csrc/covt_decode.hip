@@ -71,6 +71,9 @@ constexpr int kFamSmemVarint = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2;
 constexpr int kFamSmemFpf = kSmemHdr + (324 + 256 + 260) * 4 + 384 > kFamSmemVarint
                                 ? kSmemHdr + (324 + 256 + 260) * 4 + 384
                                 : kFamSmemVarint;
+static_assert(kFamSmemFpf >= kSmemHdr + (int)sizeof(((WaveSmem*)nullptr)->u.f), "FastPFOR scratch stride");
+static_assert(kFamSmemVarint >= kSmemHdr + (int)sizeof(((WaveSmem*)nullptr)->u.v.win) +
+                                    (int)sizeof(((WaveSmem*)nullptr)->u.v.list), "varint scratch stride");
 static_assert(__builtin_offsetof(WaveSmem, u) == kSmemHdr, "WaveSmem header size");
 static_assert(kFamSmemRle == (int)sizeof(WaveSmem), "RLE uses the whole scratch");
 static_assert(kFamSmemRle % 16 == 0 && kFamSmemVarint % 16 == 0 && kFamSmemFpf % 16 == 0, "16-B strides");
@@ -151,9 +154,12 @@ __device__ __forceinline__ uint4 sld128(uintptr_t a16) {
     const u32x4 v = *(const c_v4*)a16;
     return make_uint4(v.x, v.y, v.z, v.w);
 }
-// lane l + 1's value (lane 63: 0): DPP wave_shl:1, no LDS traffic
-__device__ __forceinline__ uint32_t lane_next(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
+// lane l + 1's value (lane 63: `tail`, which must be wave-uniform): DPP wave_shl:1, no LDS traffic.
+// The DPP source lane has no successor for lane 63, which then keeps the `old` operand; keeping the
+// select inside the DPP matters: a separate `l == 63 ? tail : dpp(x)` can be turned into an
+// exec-masked branch, and a DPP move reading from a lane masked off returns the old value instead.
+__device__ __forceinline__ uint32_t lane_next(uint32_t x, uint32_t tail = 0) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)tail, (int)x, 0x130, 0xf, 0xf, false);
 }
 
 // bits 7,15,23,31 of each dword -> 16-bit mask of "high bit set" bytes
@@ -1216,8 +1222,7 @@ __device__ void run_fastpfor(Ctx& c) {
                         const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pkc) & ~(uintptr_t)15;
                         raw2 = sld128(a16 + 1024);
                     }
-                    const uint32_t nsh = lane_next(pc.raw.x);
-                    const uint32_t nxt = l == 63 ? raw2.x : nsh;
+                    const uint32_t nxt = lane_next(pc.raw.x, raw2.x);
                     uint4 wv;
                     wv.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.y, pc.raw.x, sh));
                     wv.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.z, pc.raw.y, sh));
