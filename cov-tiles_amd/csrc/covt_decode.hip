@@ -187,20 +187,21 @@ __device__ __forceinline__ uint32_t bytemask(int n) {  // low n bytes, clamped t
 __device__ __forceinline__ int32_t zz32(uint32_t e) { return (int32_t)((e >> 1) ^ (0u - (e & 1u))); }
 __device__ __forceinline__ int64_t zz64(uint64_t e) { return (int64_t)((e >> 1) ^ (0ull - (e & 1ull))); }
 
-// GeometryUtils.decodeMorton (GeometryUtils.java:34-47) with Java int/long semantics.
-__device__ __forceinline__ int32_t morton_axis(int32_t code, int nb) {
-    uint32_t x = (uint32_t)code & 0x55555555u;
-    x = (x | (x >> 1)) & 0x33333333u;
-    x = (x | (x >> 2)) & 0x0f0f0f0fu;
-    x = (x | (x >> 4)) & 0x00ff00ffu;
-    x = (x | (x >> 8)) & 0x0000ffffu;
+// GeometryUtils.decodeMorton (GeometryUtils.java:34-47) with Java int/long semantics, both axes at
+// once: four delta swaps move the even bits of the code to the low half and the odd bits (the even
+// bits of code >> 1) to the high half.
+__host__ __device__ __forceinline__ void morton_xy(int32_t code, int nb, uint32_t& x, uint32_t& y) {
+    uint32_t v = (uint32_t)code, t;
+    t = (v ^ (v >> 1)) & 0x22222222u; v ^= t ^ (t << 1);
+    t = (v ^ (v >> 2)) & 0x0c0c0c0cu; v ^= t ^ (t << 2);
+    t = (v ^ (v >> 4)) & 0x00f000f0u; v ^= t ^ (t << 4);
+    t = (v ^ (v >> 8)) & 0x0000ff00u; v ^= t ^ (t << 8);
     const uint32_t low = nb >= 16 ? 0xffffu : (nb <= 0 ? 0u : ((1u << nb) - 1u));
-    x &= low;
-    if (nb > 16 && code < 0) {  // bits 2i >= 32 of the sign-extended long are the sign bit
-        const uint32_t top = nb >= 32 ? 0xffffffffu : ((1u << nb) - 1u);
-        x |= top & ~0xffffu;
-    }
-    return (int32_t)x;
+    // bits 2i >= 32 of the sign-extended long are the sign bit (both axes: code >> 1 keeps the sign)
+    const uint32_t top = nb <= 16 ? 0u : ((nb >= 32 ? 0xffffffffu : ((1u << nb) - 1u)) & ~0xffffu);
+    const uint32_t hi = code < 0 ? top : 0u;
+    x = (v & low) | hi;
+    y = ((v >> 16) & low) | hi;
 }
 __device__ __forceinline__ int32_t morton_half(int nb) {
     const int32_t te = (int32_t)(2u << ((uint32_t)(nb - 2) & 31u));
@@ -378,9 +379,10 @@ __device__ __forceinline__ void sink_values(const uint32_t (&vin)[K], int64_t ba
         int32_t xy[2 * K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int32_t code = (int32_t)(pre + sacc[k]);
-            xy[2 * k] = (int32_t)((uint32_t)morton_axis(code, nb) - (uint32_t)half);
-            xy[2 * k + 1] = (int32_t)((uint32_t)morton_axis(code >> 1, nb) - (uint32_t)half);
+            uint32_t mx, my;
+            morton_xy((int32_t)(pre + sacc[k]), nb, mx, my);
+            xy[2 * k] = (int32_t)(mx - (uint32_t)half);
+            xy[2 * k + 1] = (int32_t)(my - (uint32_t)half);
         }
         if (K == 4 && lfull) {
             st_out16(o, make_int4(xy[0], xy[1], xy[K > 1 ? 2 : 0], xy[K > 1 ? 3 : 0]));
@@ -1161,9 +1163,10 @@ __device__ void run_fastpfor(Ctx& c) {
             };
             // (32-bit: a stream holds < 2^29 words)
             auto xword = [&](int32_t k, uint32_t xs, uint32_t i, uint32_t& xbit) -> int32_t {
-                const uint32_t bit = (i & 31u) * (uint32_t)k;
+                // 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate): k <= 32, i < 2^16
+                const uint32_t bit = __umul24(i & 31u, (uint32_t)k);
                 xbit = bit & 31u;
-                return (int32_t)(xs + (i >> 5) * (uint32_t)k + (bit >> 5));
+                return (int32_t)(xs + __umul24(i >> 5, (uint32_t)k) + (bit >> 5));
             };
             auto prefetch = [&](const FpfHdr& hv, int32_t pkv, FpfPre& pr, int slot) {
                 FpfHdr h;
@@ -1256,8 +1259,8 @@ __device__ void run_fastpfor(Ctx& c) {
                 uint32_t v[4];
                 {
                     const uint32_t mask = b == 32 ? 0xffffffffu : ((1u << b) - 1u);
-                    uint32_t bit = (uint32_t)((l & 7) * 4 * b);
-                    const int32_t wb = (l >> 3) * b + qoff;
+                    uint32_t bit = __umul24((uint32_t)(l & 7) * 4u, (uint32_t)b);
+                    const int32_t wb = (int32_t)__umul24((uint32_t)(l >> 3), (uint32_t)b) + qoff;
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
                         const int32_t wi = wb + (int32_t)(bit >> 5);
