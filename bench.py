@@ -106,6 +106,47 @@ def cpu_baseline(picks, seconds, threads):
             "mvert_per_s": round(vx * reps / el / 1e6, 3)}
 
 
+def assembly_leg(batch, plan, stream, args, dist, torch, dev):
+    """GPU geometry assembly (nested offsets + ICE gather) over the decoded batch,
+    timed on its own (decode output resident); not part of `value`."""
+    batch.decode(stream)
+    for _ in range(max(args.warmup, 1)):
+        batch.assemble(stream)
+    torch.cuda.synchronize(dev)
+    _, gres = batch.assembly_results()
+    if (gres["status"] != 0).any():
+        raise RuntimeError("assembly reported errors on %d columns" % int((gres["status"] != 0).sum()))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    for s, e in ev:
+        s.record(stream)
+        batch.assemble(stream)
+        e.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    g = plan.geom
+    n_feat = int(g["n_features"].sum())
+    st = plan.streams
+    cnt_elems = 0  # geometryOffsets/partOffsets/ringOffsets/vertexOffsets elements read
+    for k in range(1, 5):
+        idx = g["stream"][:, k]
+        idx = idx[idx >= 0]
+        cnt_elems += int(st["out_elems"][idx].sum())
+    P, R, V = (int(gres[k].astype(np.int64).sum()) for k in ("num_parts", "num_rings", "num_coords"))
+    ncol = plan.num_geometry_columns
+    # algorithmic bytes: types 1 B + count/offset streams 4 B + one 8-byte x,y read per coordinate;
+    # written: the three offset arrays (4 B, n+1 each) + 8 B per coordinate
+    alg = n_feat + 4 * cnt_elems + 8 * V + 4 * (n_feat + P + R + 3 * ncol) + 8 * V
+    achieved = alg / (ms * 1e-3) / 1e9
+    return {"ms": round(ms, 4), "columns": ncol, "features": n_feat, "parts": P, "rings": R, "coords": V,
+            "mcoords_per_s": round(V / (ms * 1e-3) / 1e6, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": alg,
+                         "kernel": "covt::assemble_kernel (one wave per geometry column)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -117,6 +158,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--id-mode", type=int, default=0)
+    ap.add_argument("--no-assemble", action="store_true", help="skip the geometry-assembly leg")
     args = ap.parse_args()
 
     import torch
@@ -169,6 +211,10 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    asm_line = None
+    if not args.no_assemble and plan.num_geometry_columns:
+        asm_line = assembly_leg(batch, plan, stream, args, dist, torch, dev)
 
     stats = torch.tensor([wall, float(plan.in_bytes), float(plan.vertices), float(plan.out_bytes), kern_ms],
                          dtype=torch.float64, device=dev)
@@ -226,6 +272,8 @@ def main():
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": None,
         }
+        if asm_line is not None:
+            line["assembly"] = asm_line
         if world == 1 and not args.no_cpu:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(picks, args.cpu_seconds, threads)

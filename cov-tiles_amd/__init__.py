@@ -98,6 +98,28 @@ class StreamInfo(C.Structure):
                 ("out_elems", C.c_int64)]
 
 
+class GeomDesc(C.Structure):
+    _fields_ = [("in_off", C.c_int64 * 6), ("in_len", C.c_int32 * 6), ("in_res", C.c_int32 * 6),
+                ("out_off", C.c_int64 * 6), ("part_cap", C.c_int32), ("ring_cap", C.c_int32),
+                ("coord_cap", C.c_int32), ("flags", C.c_int32)]
+
+
+class GeomResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("num_parts", C.c_int32), ("num_rings", C.c_int32),
+                ("num_coords", C.c_int32)]
+
+
+GEOM_INFO_DTYPE = np.dtype([("tile", np.int32), ("layer", np.int32), ("column_type", np.int32),
+                            ("n_features", np.int32), ("stream", np.int32, (6,)), ("part_cap", np.int32),
+                            ("ring_cap", np.int32), ("coord_cap", np.int32), ("flags", np.uint32),
+                            ("desc_index", np.int32), ("reserved", np.int32), ("out_off", np.int64, (6,))])
+GEOM_RESULT_DTYPE = np.dtype([("status", np.int32), ("num_parts", np.int32), ("num_rings", np.int32),
+                              ("num_coords", np.int32)])
+GEOM_CLOSED_IN_STREAM = 0x1
+GEOM_TOO_LARGE = 0x80000000
+GEOM_MAX_CAP = 1 << 25
+assert C.sizeof(GeomDesc) == 160 and GEOM_INFO_DTYPE.itemsize == 112
+
 STREAM_INFO_DTYPE = np.dtype([(n, np.int32 if t is C.c_int32 else np.int64) for n, t in StreamInfo._fields_])
 assert STREAM_INFO_DTYPE.itemsize == C.sizeof(StreamInfo)
 assert C.sizeof(StreamDesc) == 32
@@ -111,6 +133,8 @@ EXPORTED_SYMBOLS = (
     "covt_plan_totals", "covt_plan_streams", "covt_plan_descs", "covt_plan_tile_status",
     "covt_decode_streams_device", "covt_plan_decode_host", "covt_plan_decode_host_multi", "covt_version",
     "covt_device_count", "covt_plan_family_counts", "covt_decode_streams_device_grouped",
+    "covt_plan_num_geometry_columns", "covt_plan_assembly_bytes", "covt_plan_geometry_columns",
+    "covt_plan_geometry_descs", "covt_assemble_geometry_device", "covt_plan_assemble_host",
 )
 
 
@@ -166,6 +190,14 @@ def lib() -> C.CDLL:
     L.covt_plan_family_counts.argtypes = [vp, i64p]
     L.covt_plan_decode_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
     L.covt_plan_decode_host_multi.argtypes = [vp, u8p, C.c_uint64, C.c_int32, vp, vp]
+    L.covt_plan_num_geometry_columns.argtypes = [vp]
+    L.covt_plan_num_geometry_columns.restype = C.c_int64
+    L.covt_plan_assembly_bytes.argtypes = [vp]
+    L.covt_plan_assembly_bytes.restype = C.c_int64
+    L.covt_plan_geometry_columns.argtypes = [vp, vp]
+    L.covt_plan_geometry_descs.argtypes = [vp, vp]
+    L.covt_assemble_geometry_device.argtypes = [vp, vp, vp, C.c_int64, vp, vp, vp]
+    L.covt_plan_assemble_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
     L.covt_version.restype = C.c_char_p
     L.covt_device_count.argtypes = [i32p]
     _lib = L
@@ -359,6 +391,14 @@ class Plan:
         self.tile_status = np.zeros(max(self.n_tiles, 1), dtype=np.int32)[:self.n_tiles]
         if self.n_tiles:
             L.covt_plan_tile_status(h, _ptr(self.tile_status, C.c_int32))
+        # geometry assembly (include/covt.h "Geometry assembly")
+        self.num_geometry_columns = int(L.covt_plan_num_geometry_columns(h))
+        self.assembly_bytes = int(L.covt_plan_assembly_bytes(h))
+        self.geom = np.zeros(self.num_geometry_columns, dtype=GEOM_INFO_DTYPE)
+        self.gdescs = np.zeros(self.num_geometry_columns * C.sizeof(GeomDesc), dtype=np.uint8)
+        if self.num_geometry_columns:
+            L.covt_plan_geometry_columns(h, self.geom.ctypes.data)
+            L.covt_plan_geometry_descs(h, self.gdescs.ctypes.data)
 
     @classmethod
     def from_tiles(cls, tiles: List[bytes], fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT):
@@ -389,6 +429,27 @@ class Plan:
                                              res.ctypes.data)
         _raise(st, "covt_plan_decode_host")
         return out[:self.output_bytes], res[:self.num_streams]
+
+    def assemble_host(self):
+        """H2D + decode + geometry assembly + D2H (covt_plan_assemble_host).
+        Returns (uint8 assembly buffer, results[num_geometry_columns] in tile order)."""
+        asm = np.zeros(max(self.assembly_bytes, 1), dtype=np.uint8)
+        gres = np.zeros(max(self.num_geometry_columns, 1), dtype=GEOM_RESULT_DTYPE)
+        _raise(lib().covt_plan_assemble_host(self._h, _ptr(self.blob, C.c_uint8), self.blob.size, asm.ctypes.data,
+                                             gres.ctypes.data), "covt_plan_assemble_host")
+        return asm[:self.assembly_bytes], gres[:self.num_geometry_columns]
+
+    def geometry_arrays(self, asm: np.ndarray, gres: np.ndarray, c: int):
+        """Column c (tile order) of an assembly buffer -> GeoArrowGeometry (raises on its status)."""
+        g, r = self.geom[c], gres[c]
+        _raise(int(r["status"]), "geometry column %d (tile %d, layer %d)" % (c, g["tile"], g["layer"]))
+
+        def seg(k, n, dt=np.int32, w=4):
+            o = int(g["out_off"][k])
+            return asm[o:o + n * w].view(dt)
+
+        return GeoArrowGeometry(seg(0, int(g["n_features"]) + 1), seg(1, int(r["num_parts"]) + 1),
+                                seg(2, int(r["num_rings"]) + 1), seg(3, 2 * int(r["num_coords"])).reshape(-1, 2))
 
     def stream_array(self, out: np.ndarray, i: int) -> np.ndarray:
         s = self.streams[i]
@@ -424,6 +485,34 @@ class DeviceBatch:
                                                       self.d_out.data_ptr(), self.d_res.data_ptr(), s.cuda_stream)
         _raise(st, "covt_decode_streams_device_grouped")
 
+    def _asm_buffers(self):
+        import torch
+
+        if getattr(self, "d_asm", None) is None:
+            p = self.plan
+            self.d_gdesc = torch.from_numpy(p.gdescs).to(self.device) if p.num_geometry_columns else \
+                torch.zeros(C.sizeof(GeomDesc), dtype=torch.uint8, device=self.device)
+            self.d_asm = torch.empty(max(p.assembly_bytes, 16), dtype=torch.uint8, device=self.device)
+            self.d_gres = torch.zeros(max(p.num_geometry_columns, 1) * 4, dtype=torch.int32, device=self.device)
+
+    def assemble(self, stream=None):
+        """Enqueue the geometry assembly (after decode() on the same stream)."""
+        import torch
+
+        self._asm_buffers()
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _raise(lib().covt_assemble_geometry_device(self.d_out.data_ptr(), self.d_res.data_ptr(),
+                                                   self.d_gdesc.data_ptr(), self.plan.num_geometry_columns,
+                                                   self.d_asm.data_ptr(), self.d_gres.data_ptr(), s.cuda_stream),
+               "covt_assemble_geometry_device")
+
+    def assembly_results(self):
+        """(assembly bytes, geometry results in tile order) copied to the host."""
+        self._asm_buffers()
+        asm = self.d_asm.cpu().numpy()[:self.plan.assembly_bytes]
+        g = self.d_gres.cpu().numpy().view(GEOM_RESULT_DTYPE)[:self.plan.num_geometry_columns]
+        return asm, g[self.plan.geom["desc_index"]] if self.plan.num_geometry_columns else g
+
     def results(self):
         """(output bytes, results in plan order) copied to the host."""
         out = self.d_out.cpu().numpy()[:self.plan.output_bytes]
@@ -444,6 +533,21 @@ class GeometryColumn:
     ringOffsets: Optional[np.ndarray] = None
     vertexOffsets: Optional[np.ndarray] = None
     vertexBuffer: Optional[np.ndarray] = None
+
+
+@dataclass
+class GeoArrowGeometry:
+    """One assembled geometry column (include/covt.h "Geometry assembly"): nested offsets
+    feature -> parts -> rings -> coordinates, coords int32 [k, 2]; polygon rings closed."""
+    geometry_offsets: np.ndarray
+    part_offsets: np.ndarray
+    ring_offsets: np.ndarray
+    coords: np.ndarray
+
+    def feature(self, i: int):
+        """Parts of feature i as lists of rings, each an int32 [m, 2] array."""
+        g, p, r = self.geometry_offsets, self.part_offsets, self.ring_offsets
+        return [[self.coords[r[k]:r[k + 1]] for k in range(p[j], p[j + 1])] for j in range(g[i], g[i + 1])]
 
 
 @dataclass

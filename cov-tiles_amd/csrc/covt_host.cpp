@@ -406,7 +406,89 @@ struct covt_plan {
     std::vector<covt_stream_desc> descs;  // launch order: grouped by family, largest first
     int64_t fam_counts[COVT_NUM_FAMILIES] = {0, 0, 0, 0};
     int64_t out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
+    int32_t format = COVT_FORMAT_GENC;
+    std::vector<covt_geom_info> ginfo;   // geometry columns, tile order
+    std::vector<covt_geom_desc> gdescs;  // launch order: largest first
+    int64_t asm_bytes = 0;
 };
+
+namespace {
+
+// Geometry columns of a plan: one record per (tile, layer) geometry column,
+// its source streams located in the decode output, and an assembly-output slice sized by
+// data-independent bounds (every point part/ring consumes one source vertex, every line part one
+// partOffsets entry, every polygon ring one ringOffsets entry):
+//   parts <= Vs + n_po, rings <= Vs + n_po + n_ro, coordinates <= Vs (+ n_ro closing vertices).
+void plan_geometry(covt_plan* p) {
+    const size_t ns = p->info.size();
+    int64_t off = 0;
+    for (size_t i = 0; i < ns;) {
+        const covt_stream_info& s0 = p->info[i];
+        if (s0.column_kind != 1) { ++i; continue; }
+        covt_geom_info g{};
+        g.tile = s0.tile;
+        g.layer = s0.layer;
+        g.column_type = s0.column_type;
+        for (int k = 0; k < 6; ++k) g.stream[k] = -1;
+        int64_t len[6] = {0, 0, 0, 0, 0, 0};
+        size_t j = i;
+        for (; j < ns && p->info[j].tile == s0.tile && p->info[j].layer == s0.layer && p->info[j].column_kind == 1; ++j) {
+            const covt_stream_info& s = p->info[j];
+            const int k = s.stream_type - ST_GEOMETRY_TYPES;
+            if (k < 0 || k > 5) continue;
+            g.stream[k] = (int32_t)j;
+            len[k] = k == 5 ? s.out_elems / 2 : s.out_elems;  // vertexBuffer: x,y pairs
+            if (k == 5) g.column_type = s.column_type;
+        }
+        i = j;
+        g.n_features = (int32_t)len[0];
+        const int64_t vs = g.stream[4] >= 0 ? len[4] : len[5];
+        const int64_t pcap = vs + len[2], rcap = vs + len[2] + len[3];
+        g.flags = (p->format == COVT_FORMAT_GENC && (g.column_type == CT_ICE || g.column_type == CT_ICE_MORTON))
+                      ? COVT_GEOM_CLOSED_IN_STREAM : 0;
+        const int64_t ccap = vs + ((g.flags & COVT_GEOM_CLOSED_IN_STREAM) ? 0 : len[3]);
+        const bool fits = rcap <= COVT_GEOM_MAX_CAP && ccap <= COVT_GEOM_MAX_CAP && len[0] <= COVT_GEOM_MAX_CAP;
+        g.part_cap = fits ? (int32_t)pcap : 0;
+        g.ring_cap = fits ? (int32_t)rcap : 0;
+        g.coord_cap = fits ? (int32_t)ccap : 0;
+        if (!fits) g.flags |= COVT_GEOM_TOO_LARGE;
+        const int64_t nf = fits ? len[0] : 0;
+        const int64_t bytes[6] = {4 * (nf + 1), 4 * ((int64_t)g.part_cap + 1), 4 * ((int64_t)g.ring_cap + 1),
+                                  8 * (int64_t)g.coord_cap, 4 * (int64_t)g.part_cap, 4 * (int64_t)g.ring_cap};
+        for (int k = 0; k < 6; ++k) {
+            g.out_off[k] = off;
+            off = align16(off + bytes[k]);
+        }
+        p->ginfo.push_back(g);
+    }
+    p->asm_bytes = off;
+    const size_t nc = p->ginfo.size();
+    std::vector<size_t> order(nc);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+        return p->ginfo[a].coord_cap + p->ginfo[a].n_features > p->ginfo[b].coord_cap + p->ginfo[b].n_features;
+    });
+    p->gdescs.resize(nc);
+    for (size_t k = 0; k < nc; ++k) {
+        covt_geom_info& g = p->ginfo[order[k]];
+        covt_geom_desc d{};
+        for (int m = 0; m < 6; ++m) {
+            const int32_t si = g.stream[m];
+            d.in_off[m] = si >= 0 ? p->info[(size_t)si].out_off : -1;
+            d.in_len[m] = si >= 0 ? (int32_t)(m == 5 ? p->info[(size_t)si].out_elems / 2 : p->info[(size_t)si].out_elems) : 0;
+            d.in_res[m] = si >= 0 ? p->info[(size_t)si].desc_index : -1;  // its decode status gates the column
+            d.out_off[m] = g.out_off[m];
+        }
+        d.part_cap = g.part_cap;
+        d.ring_cap = g.ring_cap;
+        d.coord_cap = g.coord_cap;
+        d.flags = (int32_t)g.flags;
+        g.desc_index = (int32_t)k;
+        p->gdescs[k] = d;
+    }
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -474,6 +556,7 @@ int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const u
     if (format != COVT_FORMAT_GENC && format != COVT_FORMAT_GEND) return COVT_ERR_INVALID_ARG;
     auto* p = new covt_plan();
     p->n_tiles = n_tiles;
+    p->format = format;
     p->tile_status.assign((size_t)n_tiles, 0);
     p->tile_off.assign(tile_offsets, tile_offsets + n_tiles);
     p->tile_size.assign(tile_sizes, tile_sizes + n_tiles);
@@ -550,6 +633,7 @@ int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const u
         p->descs[k] = d;
         si.desc_index = (int32_t)k;
     }
+    plan_geometry(p);
     *out = p;
     return COVT_OK;
 }
@@ -731,6 +815,69 @@ int covt_plan_decode_host_multi(const covt_plan* p, const uint8_t* bytes, uint64
     for (int s : st)
         if (s) return s;
     return COVT_OK;
+}
+
+int64_t covt_plan_num_geometry_columns(const covt_plan* p) { return p ? (int64_t)p->ginfo.size() : 0; }
+int64_t covt_plan_assembly_bytes(const covt_plan* p) { return p ? p->asm_bytes : 0; }
+int covt_plan_geometry_columns(const covt_plan* p, covt_geom_info* out) {
+    if (!p || (!out && !p->ginfo.empty())) return COVT_ERR_INVALID_ARG;
+    if (!p->ginfo.empty()) std::memcpy(out, p->ginfo.data(), p->ginfo.size() * sizeof(covt_geom_info));
+    return COVT_OK;
+}
+int covt_plan_geometry_descs(const covt_plan* p, covt_geom_desc* out) {
+    if (!p || (!out && !p->gdescs.empty())) return COVT_ERR_INVALID_ARG;
+    if (!p->gdescs.empty()) std::memcpy(out, p->gdescs.data(), p->gdescs.size() * sizeof(covt_geom_desc));
+    return COVT_OK;
+}
+
+// Whole plan on the current device: the caller's tile bytes [0, n_bytes) go to the device as they
+// lie (the plan's offsets index them), then decode, assembly and the copies back on one stream.
+int covt_plan_assemble_host(const covt_plan* p, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_asm,
+                            covt_geom_result* host_gres) {
+    if (!p || (!bytes && n_bytes) || (!host_asm && p->asm_bytes) || (!host_gres && !p->ginfo.empty()))
+        return COVT_ERR_INVALID_ARG;
+    for (int32_t t = 0; t < p->n_tiles; ++t)
+        if (p->tile_off[(size_t)t] + p->tile_size[(size_t)t] > n_bytes) return COVT_ERR_INVALID_ARG;
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return COVT_ERR_DEVICE;
+    const size_t nd = p->descs.size(), nc = p->gdescs.size();
+    uint8_t *d_in = nullptr, *d_out = nullptr, *d_asm = nullptr;
+    covt_stream_desc* d_desc = nullptr;
+    covt_stream_result* d_res = nullptr;
+    covt_geom_desc* d_gdesc = nullptr;
+    covt_geom_result* d_gres = nullptr;
+    int st = COVT_OK;
+    auto chk = [&](hipError_t e) { if (e != hipSuccess && st == COVT_OK) st = COVT_ERR_DEVICE; };
+    chk(hipMalloc(&d_in, (size_t)n_bytes + COVT_INPUT_PADDING));
+    chk(hipMalloc(&d_out, (size_t)std::max<int64_t>(p->out_bytes, 16)));
+    chk(hipMalloc(&d_asm, (size_t)std::max<int64_t>(p->asm_bytes, 16)));
+    chk(hipMalloc(&d_desc, std::max<size_t>(nd, 1) * sizeof(covt_stream_desc)));
+    chk(hipMalloc(&d_res, std::max<size_t>(nd, 1) * sizeof(covt_stream_result)));
+    chk(hipMalloc(&d_gdesc, std::max<size_t>(nc, 1) * sizeof(covt_geom_desc)));
+    chk(hipMalloc(&d_gres, std::max<size_t>(nc, 1) * sizeof(covt_geom_result)));
+    std::vector<covt_geom_result> gres(nc);
+    if (st == COVT_OK) {
+        if (n_bytes) chk(hipMemcpyAsync(d_in, bytes, (size_t)n_bytes, hipMemcpyHostToDevice, s));
+        chk(hipMemsetAsync(d_in + n_bytes, 0, COVT_INPUT_PADDING, s));
+        if (nd) chk(hipMemcpyAsync(d_desc, p->descs.data(), nd * sizeof(covt_stream_desc), hipMemcpyHostToDevice, s));
+        if (nc)
+            chk(hipMemcpyAsync(d_gdesc, p->gdescs.data(), nc * sizeof(covt_geom_desc), hipMemcpyHostToDevice, s));
+        if (st == COVT_OK && ((uintptr_t)d_in & 15)) st = COVT_ERR_DEVICE;
+        if (st == COVT_OK) st = launch_grouped(d_in, d_desc, p->fam_counts, d_out, d_res, s);
+        if (st == COVT_OK)
+            st = covt_assemble_geometry_device(d_out, d_res, d_gdesc, (int64_t)nc, d_asm, d_gres, s);
+        if (st == COVT_OK && p->asm_bytes)
+            chk(hipMemcpyAsync(host_asm, d_asm, (size_t)p->asm_bytes, hipMemcpyDeviceToHost, s));
+        if (st == COVT_OK && nc)
+            chk(hipMemcpyAsync(gres.data(), d_gres, nc * sizeof(covt_geom_result), hipMemcpyDeviceToHost, s));
+        chk(hipStreamSynchronize(s));
+    }
+    if (st == COVT_OK)
+        for (size_t k = 0; k < nc; ++k) host_gres[k] = gres[(size_t)p->ginfo[k].desc_index];
+    for (void* q : {(void*)d_in, (void*)d_out, (void*)d_asm, (void*)d_desc, (void*)d_res, (void*)d_gdesc, (void*)d_gres})
+        if (q) (void)hipFree(q);
+    (void)hipStreamDestroy(s);
+    return st;
 }
 
 }  // extern "C"

@@ -1,0 +1,76 @@
+// covt_wave.h -- wave64 primitives shared by the gfx950 kernels of libcovt (decode, assembly):
+// wave-uniform reads, lane broadcast, DPP inclusive scan / max without LDS traffic.
+#ifndef COVT_WAVE_H
+#define COVT_WAVE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace covt {
+
+// --------------------------------------------------------------------------------------------
+// wave primitives
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t uniu(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+    const uint32_t lo = uniu((uint32_t)x), hi = uniu((uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t lane_bcast(uint32_t x, int src) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, src);
+}
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+// inclusive prefix sum over the 64 lanes (wrapping uint32): DPP row shifts within 16-lane rows,
+// then row broadcasts 15 and 31 across rows (the GFX9 wave64 scan sequence, no LDS traffic)
+__device__ __forceinline__ uint32_t incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
+// inclusive running maximum over the 64 lanes (same DPP sequence as incl_scan)
+__device__ __forceinline__ uint32_t incl_max_scan(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return x;
+}
+
+// maximum over the 64 lanes (DPP row shifts, then row broadcasts), returned uniform
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return lane_bcast(x, 63);
+}
+
+// lane l + 1's value (lane 63: `tail`, which must be wave-uniform): DPP wave_shl:1, no LDS traffic.
+// The DPP source lane has no successor for lane 63, which then keeps the `old` operand; keeping the
+// select inside the DPP matters: a separate `l == 63 ? tail : dpp(x)` can be turned into an
+// exec-masked branch, and a DPP move reading from a lane masked off returns the old value instead.
+__device__ __forceinline__ uint32_t lane_next(uint32_t x, uint32_t tail = 0) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)tail, (int)x, 0x130, 0xf, 0xf, false);
+}
+// value of lane `src` (any lane index 0..63 per lane): ds_bpermute, no LDS allocation
+__device__ __forceinline__ int32_t lane_get(int32_t x, int32_t src) {
+    return __builtin_amdgcn_ds_bpermute(src << 2, x);
+}
+
+}  // namespace covt
+
+#endif

@@ -188,6 +188,82 @@ int covt_plan_decode_host(const covt_plan* plan, const uint8_t* bytes, uint64_t 
 int covt_plan_decode_host_multi(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, int32_t n_gpus,
                                 uint8_t* host_out, covt_stream_result* host_res);
 
+/* ---------------------------------------------------------------------------
+ * Geometry assembly: the GPU replacement for
+ * CovtParser.convertGeometryColumn (CovtParser.java:135-274, getLineString / getLinearRing /
+ * getICELineString :513-550).  Java builds one JTS Geometry per feature out of the decoded
+ * GeometryColumn; here every geometry column of a plan becomes one GeoArrow-style nested-offset
+ * record, computed on the device from the decoded streams (prefix sums of the count streams,
+ * ICE vertex gather):
+ *
+ *   geometry_offsets[n_features + 1]  feature -> parts    (POINT/LINESTRING/POLYGON: 1 part,
+ *                                                          MULTI*: geometryOffsets count)
+ *   part_offsets[num_parts + 1]       part -> rings       (POLYGON parts: partOffsets count,
+ *                                                          point / line parts: 1 ring)
+ *   ring_offsets[num_rings + 1]       ring -> coordinates (point: 1, line: partOffsets count,
+ *                                                          polygon ring: ringOffsets count, closed)
+ *   coords[2 * num_coords]            int32 x,y (ICE: vertexBuffer[2*vertexOffsets[i]], +0/+1)
+ *
+ * Offsets are absolute within the column and start at 0; types[] of the decoded GeometryTypes
+ * stream says how to read a feature.  Polygon rings are closed as JTS LinearRings are
+ * (getLinearRing appends the first vertex): a ring whose stream omits the closing vertex gets it
+ * appended; Gen C ICE rings already carry it and are copied as they are.
+ * Deviations from the Java method, decided for format truth: the MULTIPOLYGON bugs of SURVEY Q7
+ * (CovtParser.java:237-259) are not reproduced, and MULTIPOINT (which Java rejects with
+ * IllegalArgumentException) reads one geometryOffsets count of points.
+ * ------------------------------------------------------------------------- */
+#define COVT_GEOM_CLOSED_IN_STREAM 0x1u /* polygon rings carry their closing vertex in the stream */
+#define COVT_GEOM_TOO_LARGE 0x80000000u /* over COVT_GEOM_MAX_CAP: not assembled (COVT_ERR_INVALID_ARG) */
+
+/* One device-resident geometry-column entry (160 bytes). */
+typedef struct covt_geom_desc {
+    int64_t in_off[6];   /* decode-output byte offsets of the GeometryTypes, GeometryOffsets, PartOffsets,
+                            RingOffsets, VertexOffsets, VertexBuffer arrays (-1: stream absent) */
+    int32_t in_len[6];   /* their element counts (VertexBuffer: vertices) */
+    int32_t in_res[6];   /* their row in the decode result array (-1: absent) */
+    int64_t out_off[6];  /* assembly-output byte offsets: geometry_offsets, part_offsets, ring_offsets,
+                            coords, part scratch, ring scratch (16-byte aligned) */
+    int32_t part_cap, ring_cap, coord_cap; /* capacities the output slices were sized for */
+    int32_t flags;                         /* COVT_GEOM_* */
+} covt_geom_desc;
+
+/* Per-column assembly result written by the kernel. */
+typedef struct covt_geom_result {
+    int32_t status; /* COVT_OK, a source stream's decode status, or a COVT_ERR_* of the assembly */
+    int32_t num_parts, num_rings, num_coords;
+} covt_geom_result;
+
+/* Host-visible geometry-column record of a plan, in tile order. */
+typedef struct covt_geom_info {
+    int32_t tile, layer, column_type, n_features;
+    int32_t stream[6]; /* tile-order stream index of each source stream (-1: absent) */
+    int32_t part_cap, ring_cap, coord_cap, flags;
+    int32_t desc_index, reserved; /* desc_index: row in the launch-ordered geometry descriptors */
+    int64_t out_off[6];
+} covt_geom_info;
+
+/* Column capacities are bounded so the kernel's 32-bit scans cannot wrap; a larger column
+ * (over 2^25 rings or coordinates) is flagged COVT_GEOM_TOO_LARGE and not assembled. */
+#define COVT_GEOM_MAX_CAP (1 << 25)
+
+int64_t covt_plan_num_geometry_columns(const covt_plan* plan);
+int64_t covt_plan_assembly_bytes(const covt_plan* plan); /* size of the assembly output buffer */
+int covt_plan_geometry_columns(const covt_plan* plan, covt_geom_info* out); /* tile order */
+int covt_plan_geometry_descs(const covt_plan* plan, covt_geom_desc* out);   /* launch order (largest first) */
+
+/* Assemble every geometry column on `hip_stream` after the decode launch of the same plan:
+ * d_decoded / d_res are the decode output and result arrays (launch-order results), d_gdesc the
+ * geometry descriptors, d_asm an output buffer of covt_plan_assembly_bytes bytes, d_gres
+ * n_columns results (in d_gdesc order).  Asynchronous. */
+int covt_assemble_geometry_device(const uint8_t* d_decoded, const covt_stream_result* d_res,
+                                  const covt_geom_desc* d_gdesc, int64_t n_columns, uint8_t* d_asm,
+                                  covt_geom_result* d_gres, void* hip_stream);
+
+/* Convenience: H2D + decode + assembly + D2H of the whole plan on the current device.
+ * host_asm: covt_plan_assembly_bytes bytes; host_gres: one result per column in tile order. */
+int covt_plan_assemble_host(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_asm,
+                            covt_geom_result* host_gres);
+
 /* Library info */
 const char* covt_version(void);
 int covt_device_count(int32_t* n);

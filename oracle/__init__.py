@@ -87,6 +87,9 @@ def lib():
                                                                 i32p]
         L.oracle_decode_morton.argtypes = [C.c_int32, C.c_int32, i32p, i32p]
         L.oracle_decode_morton.restype = None
+        L.oracle_assemble_geometry.argtypes = [u8p, C.c_int32, i32p, C.c_int32, i32p, C.c_int32, i32p, C.c_int32,
+                                               i32p, C.c_int32, i32p, C.c_int32, C.c_int, C.c_int32, C.c_int32,
+                                               C.c_int32, i32p, i32p, i32p, i32p, i32p, i32p, i32p]
         _lib = L
     return _lib
 
@@ -282,3 +285,33 @@ def decode_tiles_mt(blob: np.ndarray, offsets, sizes, fmt=FMT_GENC, id_mode=ID_F
     st = lib().oracle_decode_tiles_mt(_p(blob, C.c_uint8), _p(offs, C.c_uint64), _p(szs, C.c_uint64), offs.size,
                                       fmt, id_mode, threads, C.byref(ib), C.byref(ob), C.byref(vx))
     return st, ib.value, ob.value, vx.value
+
+
+# ---------------------------------------------------------------------------
+# geometry assembly (CovtParser.convertGeometryColumn, CovtParser.java:135-274)
+# ---------------------------------------------------------------------------
+def assemble_geometry(types, go, po, ro, vo, vb, closed_in_stream: bool, caps=None):
+    """Nested-offset assembly of one decoded GeometryColumn (count arrays may be None).
+    vb: int32 x,y interleaved.  Returns (status, geo_off, part_off, ring_off, coords[k,2])."""
+    def arr(a):
+        return None if a is None else np.ascontiguousarray(np.asarray(a, dtype=np.int32))
+
+    types = np.ascontiguousarray(np.asarray(types if types is not None else [], dtype=np.uint8))
+    go, po, ro, vo, vb = arr(go), arr(po), arr(ro), arr(vo), arr(vb if vb is not None else [])
+    n_vb = vb.size // 2
+    n_src = vo.size if vo is not None else n_vb
+    nl = lambda a: 0 if a is None else a.size  # noqa: E731
+    if caps is None:  # the plan's data-independent bounds (cov-tiles_amd/csrc/covt_host.cpp plan_geometry)
+        caps = (n_src + nl(po), n_src + nl(po) + nl(ro), n_src + (0 if closed_in_stream else nl(ro)))
+    pcap, rcap, ccap = caps
+    geo = np.zeros(types.size + 1, dtype=np.int32)
+    part = np.zeros(pcap + 1, dtype=np.int32)
+    ring = np.zeros(rcap + 1, dtype=np.int32)
+    coords = np.zeros(2 * max(ccap, 1), dtype=np.int32)
+    np_, nr, nc = C.c_int32(), C.c_int32(), C.c_int32()
+    ip = lambda a: None if a is None else _p(a, C.c_int32)  # noqa: E731
+    st = lib().oracle_assemble_geometry(_p(types, C.c_uint8), types.size, ip(go), nl(go), ip(po), nl(po), ip(ro),
+                                        nl(ro), ip(vo), nl(vo), ip(vb), n_vb, int(bool(closed_in_stream)), pcap,
+                                        rcap, ccap, _p(geo, C.c_int32), _p(part, C.c_int32), _p(ring, C.c_int32),
+                                        _p(coords, C.c_int32), C.byref(np_), C.byref(nr), C.byref(nc))
+    return (st, geo, part[:np_.value + 1], ring[:nr.value + 1], coords[:2 * nc.value].reshape(-1, 2))

@@ -1210,3 +1210,120 @@ int oracle_decode_tiles_mt(const uint8_t* bytes, const uint64_t* offsets, const 
     if (vertices) *vertices = atomic_load(&j.vertices);
     return atomic_load(&j.status);
 }
+
+/* ------------------------------------------------------------------------ */
+/* Geometry assembly: CovtParser.convertGeometryColumn (CovtParser.java:135-274)               */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const int32_t *go, *po, *ro, *vo, *vb;
+    int32_t n_go, n_po, n_ro, n_vo, n_vb, closed;
+    int32_t gi, pi, ri, vi;              /* geometryOffsetsCounter, partOffsetCounter, ringOffsetsCounter,
+                                            vertexBufferOffset / vertexOffsetsOffset (in vertices) */
+    int32_t np, nr, nc, pcap, rcap, ccap; /* emitted parts / rings / coordinates and capacities */
+    int32_t *part_off, *ring_off, *coords;
+    int st;
+} asm_state;
+
+static int32_t asm_count(asm_state* a, const int32_t* s, int32_t n, int32_t* i) {
+    if (*i >= n || !s) { a->st = ORC_ERR_COUNT; return 0; }
+    const int32_t c = s[(*i)++];
+    if (c < 0) { a->st = ORC_ERR_COUNT; return 0; }
+    return c;
+}
+/* one source vertex: getLineString (:522-534) reads vertexBuffer[vertexBufferOffset + 2i],
+ * getICELineString (:537-550) reads vertexBuffer[vertexOffsets[vertexOffset + i] * 2] */
+static void asm_vertex(asm_state* a, int32_t src) {
+    if (a->st) return;
+    int32_t idx = src;
+    if (a->vo) {
+        if (src >= a->n_vo) { a->st = ORC_ERR_COUNT; return; }
+        idx = a->vo[src];
+    } else if (src >= a->n_vb) {
+        a->st = ORC_ERR_COUNT;
+        return;
+    }
+    if (idx < 0 || idx >= a->n_vb) { a->st = ORC_ERR_TRUNCATED; return; }
+    if (a->nc >= a->ccap) { a->st = ORC_ERR_COUNT; return; }
+    a->coords[2 * a->nc] = a->vb[2 * (int64_t)idx];
+    a->coords[2 * a->nc + 1] = a->vb[2 * (int64_t)idx + 1];
+    a->nc++;
+}
+/* a ring / line of nv source vertices; poly: a LinearRing, closed once (getLinearRing :513-516) */
+static void asm_ring(asm_state* a, int32_t nv, int poly) {
+    if (a->st) return;
+    if (a->nr >= a->rcap) { a->st = ORC_ERR_COUNT; return; }
+    a->ring_off[a->nr++] = a->nc;
+    const int32_t first = a->vi;
+    for (int32_t k = 0; k < nv && !a->st; ++k) asm_vertex(a, a->vi++);
+    if (poly && !a->closed && nv > 0) asm_vertex(a, first);
+}
+static void asm_part_begin(asm_state* a) {
+    if (a->st) return;
+    if (a->np >= a->pcap) { a->st = ORC_ERR_COUNT; return; }
+    a->part_off[a->np++] = a->nr;
+}
+
+int oracle_assemble_geometry(const uint8_t* types, int32_t n, const int32_t* go, int32_t n_go, const int32_t* po,
+                             int32_t n_po, const int32_t* ro, int32_t n_ro, const int32_t* vo, int32_t n_vo,
+                             const int32_t* vb, int32_t n_vb, int closed_in_stream, int32_t part_cap,
+                             int32_t ring_cap, int32_t coord_cap, int32_t* geo_off, int32_t* part_off,
+                             int32_t* ring_off, int32_t* coords, int32_t* n_parts, int32_t* n_rings,
+                             int32_t* n_coords) {
+    asm_state a = {go, po, ro, vo, vb, n_go, n_po, n_ro, n_vo, n_vb, closed_in_stream ? 1 : 0,
+                   0, 0, 0, 0, 0, 0, 0, part_cap, ring_cap, coord_cap, part_off, ring_off, coords, ORC_OK};
+    for (int32_t f = 0; f < n && !a.st; ++f) { /* for(var geometryType : geometryTypes) :152 */
+        geo_off[f] = a.np;
+        switch (types[f]) {
+        case 0: /* POINT :153-167 */
+            asm_part_begin(&a);
+            asm_ring(&a, 1, 0);
+            break;
+        case 1: /* LINESTRING :168-181 */
+            asm_part_begin(&a);
+            asm_ring(&a, asm_count(&a, po, n_po, &a.pi), 0);
+            break;
+        case 2: { /* POLYGON :182-206: numRings from partOffsets, each ring's vertices from ringOffsets */
+            const int32_t nrings = asm_count(&a, po, n_po, &a.pi);
+            asm_part_begin(&a);
+            for (int32_t r = 0; r < nrings && !a.st; ++r) asm_ring(&a, asm_count(&a, ro, n_ro, &a.ri), 1);
+            break;
+        }
+        case 3: { /* MULTIPOINT: rejected by Java (:270); format truth = a count of points */
+            const int32_t k = asm_count(&a, go, n_go, &a.gi);
+            for (int32_t i = 0; i < k && !a.st; ++i) {
+                asm_part_begin(&a);
+                asm_ring(&a, 1, 0);
+            }
+            break;
+        }
+        case 4: { /* MULTILINESTRING :207-230 */
+            const int32_t k = asm_count(&a, go, n_go, &a.gi);
+            for (int32_t i = 0; i < k && !a.st; ++i) {
+                const int32_t nv = asm_count(&a, po, n_po, &a.pi);
+                asm_part_begin(&a);
+                asm_ring(&a, nv, 0);
+            }
+            break;
+        }
+        case 5: { /* MULTIPOLYGON :231-268 (without the Q7 accumulation / rings[i] / offset bugs) */
+            const int32_t k = asm_count(&a, go, n_go, &a.gi);
+            for (int32_t i = 0; i < k && !a.st; ++i) {
+                const int32_t nrings = asm_count(&a, po, n_po, &a.pi);
+                asm_part_begin(&a);
+                for (int32_t r = 0; r < nrings && !a.st; ++r) asm_ring(&a, asm_count(&a, ro, n_ro, &a.ri), 1);
+            }
+            break;
+        }
+        default: a.st = ORC_ERR_HEADER; /* GeometryType.values()[b] / :270-272 */
+        }
+    }
+    if (!a.st) {
+        geo_off[n] = a.np;
+        part_off[a.np] = a.nr;
+        ring_off[a.nr] = a.nc;
+    }
+    *n_parts = a.np;
+    *n_rings = a.nr;
+    *n_coords = a.nc;
+    return a.st;
+}

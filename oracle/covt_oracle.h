@@ -122,6 +122,22 @@ int oracle_stream_output(const oracle_stream* s, int id_mode, int32_t* elem_byte
 int oracle_decode_stream(const uint8_t* tile, size_t len, const oracle_stream* s, int id_mode, void* out,
                          int32_t* consumed);
 
+/* CovtParser.convertGeometryColumn (CovtParser.java:135-274) restated into the nested-offset
+ * layout of include/covt.h ("Geometry assembly"): geo_off[n+1], part_off[parts+1],
+ * ring_off[rings+1], coords[2*coords].  Count streams may be NULL (absent); vo == NULL means a
+ * PLAIN column (vertices read in order), else ICE (vb[2*vo[i]]).  n_vb counts vertices.
+ * Deviations from Java (documented in include/covt.h): MULTIPOLYGON without the SURVEY Q7 bugs,
+ * MULTIPOINT = geometryOffsets count of points, rings closed once (closed_in_stream: the stream
+ * already holds the closing vertex).  Returns 0, ORC_ERR_HEADER (type > 5),
+ * ORC_ERR_COUNT (a count stream over-read, a negative count, a capacity exceeded) or
+ * ORC_ERR_TRUNCATED (a vertex index outside the vertex buffer). */
+int oracle_assemble_geometry(const uint8_t* types, int32_t n, const int32_t* go, int32_t n_go, const int32_t* po,
+                             int32_t n_po, const int32_t* ro, int32_t n_ro, const int32_t* vo, int32_t n_vo,
+                             const int32_t* vb, int32_t n_vb, int closed_in_stream, int32_t part_cap,
+                             int32_t ring_cap, int32_t coord_cap, int32_t* geo_off, int32_t* part_off,
+                             int32_t* ring_off, int32_t* coords, int32_t* n_parts, int32_t* n_rings,
+                             int32_t* n_coords);
+
 /* CPU baseline: walk + decode every Id/Geometry stream of n_tiles tiles (concatenated in
  * `bytes` at `offsets`) on n_threads host threads; output goes to per-thread scratch.
  * Returns status; totals (optional) receive stream bytes, output bytes, vertices. */
