@@ -20,12 +20,16 @@
 //                (the closing coordinate repeats the first); ICE: through vertexOffsets; gather
 //                the x,y pair.
 //
-// The expansion (`Expand`): output items are processed 64 at a time; the 64 segment ends after the
-// carried segment base are loaded one per lane, each segment end marks its position in a 64-slot
-// LDS table (the last of equal ends wins), and an inclusive running max over the table gives each
-// lane the number of segments that end at or before its item -- its segment index, with the
-// segment start fetched by ds_bpermute.  Empty segments cost nothing extra; a step consumes 64
-// items or 64 segments, so every wave reaches its exit.
+// The expansion (`Expand`): output items are processed 256 at a time, four consecutive ones per
+// lane; the 256 segment ends after the carried segment base are loaded (four per lane) into LDS,
+// each end marks its position in a 256-slot LDS table (the last of equal ends wins), and a running
+// max over the table (in-lane over four slots, then a DPP wave scan) gives each item the number of
+// segments that end at or before it -- its segment index; the segment's start and end come from
+// the LDS copy of the ends.  Empty segments cost nothing extra; a step consumes 256 items or 256
+// segments, so every wave reaches its exit.  Four items per lane give each wave four independent
+// gathers in flight per dependent step (the passes are latency-bound chains of gathers).
+// Pass 4 skips the expansion when the column inserts no closing vertex (ICE rings of Gen C, line
+// and point layers): coordinate v is then source vertex v.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -36,16 +40,66 @@
 namespace covt {
 
 constexpr int kAsmWaves = 4;  // independent waves (columns) per workgroup
+constexpr int kW = 256;       // items per step: 4 consecutive items per lane
 
 typedef __attribute__((address_space(1))) const int32_t g_i32;
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
 typedef __attribute__((address_space(1))) const uint64_t g_u64;
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const i32x4 g_i32x4;
 
-struct AsmSmem {
-    int32_t slot[64];
+struct __attribute__((aligned(16))) AsmSmem {
+    int32_t slot[kW];  // expansion: segment-end marks of the current step
+    int32_t ends[kW];  // expansion: the step's 256 segment ends
 };
 
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {  // lane l - 1's value (lane 0: 0), DPP wave_shr:1
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
+}
+
+// exclusive scan of 256 items held 4 per lane (items 4l .. 4l+3); `tot` gets the uniform total
+__device__ __forceinline__ void excl_scan4(const uint32_t x[4], uint32_t ex[4], uint32_t& tot) {
+    const uint32_t s = x[0] + x[1] + x[2] + x[3];
+    const uint32_t inc = incl_scan(s);
+    tot = lane_bcast(inc, 63);
+    uint32_t run = inc - s;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        ex[k] = run;
+        run += x[k];
+    }
+}
+
+// items q + 4l + k (k < 4) of a step of L: one 16-byte store when the lane's four are valid and
+// aligned (arrays are 16-byte aligned; aligned when q % 4 == 0), else element stores
+__device__ __forceinline__ void store4(int32_t* a, int32_t q, int32_t L, const uint32_t v[4]) {
+    const int32_t i0 = 4 * lane_id();
+    if ((q & 3) == 0 && i0 + 4 <= L) {
+        *(i32x4*)(a + q + i0) = i32x4{(int32_t)v[0], (int32_t)v[1], (int32_t)v[2], (int32_t)v[3]};
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i0 + k < L) a[q + i0 + k] = (int32_t)v[k];
+    }
+}
+// coordinates (8 bytes each): two 16-byte nontemporal stores for four aligned valid items
+__device__ __forceinline__ void store4_xy(uint64_t* a, int32_t q, int32_t L, const uint64_t v[4]) {
+    const int32_t i0 = 4 * lane_id();
+    if ((q & 3) == 0 && i0 + 4 <= L) {
+        i32x4* p = (i32x4*)(a + q + i0);
+        __builtin_nontemporal_store(i32x4{(int32_t)v[0], (int32_t)(v[0] >> 32), (int32_t)v[1], (int32_t)(v[1] >> 32)}, p);
+        __builtin_nontemporal_store(i32x4{(int32_t)v[2], (int32_t)(v[2] >> 32), (int32_t)v[3], (int32_t)(v[3] >> 32)},
+                                    p + 1);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i0 + k < L) a[q + i0 + k] = v[k];
+    }
+}
+
 // Segmented expansion cursor over O[0..S] (nondecreasing, O[0] = 0, O[S] = total), wave-uniform.
+// A step covers up to 256 items, lane l the four items q + 4l + k.
 struct Expand {
     const int32_t* O;
     int32_t S, total;
@@ -53,32 +107,52 @@ struct Expand {
     int32_t obase;  // O[base]
     int32_t q;      // first item of the next step
 
-    // one step: L items (uniform) from q; lane l < L gets its segment, rank in it and segment end
-    __device__ __forceinline__ int32_t step(AsmSmem& sm, int32_t& seg, int32_t& rank, int32_t& seg_end) {
+    // one step: L items (uniform); item k of the lane (valid if 4l + k < L) gets its segment, the
+    // segment's start and end
+    __device__ __forceinline__ int32_t step(AsmSmem& sm, int32_t seg[4], int32_t start[4], int32_t end[4]) {
         const int l = lane_id();
-        const int32_t j = base + 1 + l;
-        const int32_t e = j <= S ? ((const g_i32*)O)[j] : 0x7fffffff;
-        const int32_t r0 = max(e - q, 0);  // item offset (in this step) where segment base+l+1 starts
-        const int32_t r1 = (int32_t)lane_next((uint32_t)r0, 0x7fffffffu);
-        sm.slot[l] = 0;
+        int32_t e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // end of segment base + 1 + 4l + k
+            const int32_t j = base + 1 + 4 * l + k;
+            e[k] = j <= S ? ((const g_i32*)O)[j] : 0x7fffffff;
+        }
+        *(i32x4*)&sm.ends[4 * l] = i32x4{e[0], e[1], e[2], e[3]};
+        *(i32x4*)&sm.slot[4 * l] = i32x4{0, 0, 0, 0};
         wave_sync();
-        if (r0 < 64 && r1 != r0) sm.slot[r0] = l + 1;  // the last of equal ends wins
+        int32_t r[5];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = max(e[k] - q, 0);  // item offset where segment base+2+4l+k starts
+        r[4] = (int32_t)lane_next((uint32_t)r[0], 0x7fffffffu);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (r[k] < kW && r[k + 1] != r[k]) sm.slot[r[k]] = 4 * l + k + 1;  // the last of equal ends wins
         wave_sync();
-        const int32_t cnt = (int32_t)incl_max_scan((uint32_t)sm.slot[l]);  // segment ends <= q + l
-        wave_sync();
-        const int32_t e_prev = lane_get(e, max(cnt - 1, 0));
-        seg_end = lane_get(e, min(cnt, 63));
-        const int32_t start = cnt == 0 ? obase : e_prev;
-        seg = base + cnt;
-        rank = q + l - start;
-        // items this step: at most 64, the rest of the column, and what the 64 loaded ends cover
-        int32_t L = min(64, total - q);
-        if (base + 64 < S) L = min(L, (int32_t)lane_bcast((uint32_t)e, 63) - q);
+        const i32x4 sl = *(const i32x4*)&sm.slot[4 * l];
+        uint32_t m[4];
+        m[0] = (uint32_t)sl.x;
+        m[1] = max(m[0], (uint32_t)sl.y);
+        m[2] = max(m[1], (uint32_t)sl.z);
+        m[3] = max(m[2], (uint32_t)sl.w);
+        const uint32_t prev = wave_shr1(incl_max_scan(m[3]));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int32_t cnt = (int32_t)max(prev, m[k]);  // segment ends <= q + 4l + k
+            start[k] = cnt == 0 ? obase : sm.ends[cnt - 1];
+            end[k] = sm.ends[min(cnt, kW - 1)];
+            seg[k] = base + cnt;
+        }
+        // items this step: at most 256, the rest of the column, and what the 256 loaded ends cover
+        int32_t L = min(kW, total - q);
+        if (base + kW < S) L = min(L, (int32_t)lane_bcast((uint32_t)e[3], 63) - q);
         L = max(L, 0);
-        const uint64_t done = __ballot(e <= q + L);
-        const int k = __popcll(done);  // segments ending at or before the next q (a prefix of lanes)
-        if (k > 0) obase = (int32_t)lane_bcast((uint32_t)e, k - 1);
-        base += k;
+        int adv = 0;  // segments ending at or before the next q
+#pragma unroll
+        for (int k = 0; k < 4; ++k) adv += __popcll(__ballot(e[k] <= q + L));
+        const int32_t nob = adv > 0 ? uni(sm.ends[adv - 1]) : obase;
+        wave_sync();
+        obase = nob;
+        base += adv;
         q += L;
         return L;
     }
@@ -87,13 +161,6 @@ struct Expand {
 __device__ __forceinline__ void mem_publish() {  // this wave's global stores visible to its own loads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// exclusive scan of x over the lanes (uint32); `tot` gets the uniform total
-__device__ __forceinline__ uint32_t excl_scan(uint32_t x, uint32_t& tot) {
-    const uint32_t inc = incl_scan(x);
-    tot = lane_bcast(inc, 63);
-    return inc - x;
 }
 
 __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stream_result* __restrict__ dres,
@@ -131,31 +198,40 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     int32_t* part_scr = (int32_t*)(outb + d.out_off[4]);
     int32_t* ring_scr = (int32_t*)(outb + d.out_off[5]);
     const uint32_t pcap = (uint32_t)d.part_cap, rcap = (uint32_t)d.ring_cap, ccap = (uint32_t)d.coord_cap;
-
-    // ---- pass 1: features -> parts ----
-    uint32_t go_base = 0, P = 0;
     bool bad_type = false, bad_cnt = false;
-    for (int32_t f0 = 0; f0 < n; f0 += 64) {
-        const int32_t f = f0 + l;
-        const bool valid = f < n;
-        const uint32_t t = valid ? (uint32_t)((const g_u8*)types)[f] : 0u;
-        bad_type |= t > 5u;
-        const bool multi = valid && t >= 3u && t <= 5u;
-        uint32_t nm;
-        const uint32_t gi = go_base + excl_scan(multi ? 1u : 0u, nm);
-        uint32_t pf = valid ? 1u : 0u;
-        if (multi) {
-            if (gi < (uint32_t)n_go) {
-                const int32_t c = ((const g_i32*)go)[gi];
-                bad_cnt |= c < 0;
-                pf = min((uint32_t)max(c, 0), pcap + 1u);  // clamped: the scan below cannot wrap
-            } else {
-                bad_cnt = true;
+
+    // ---- pass 1: features -> parts (items: features) ----
+    uint32_t go_base = 0, P = 0;
+    for (int32_t f0 = 0; f0 < n; f0 += kW) {
+        const int32_t fl = f0 + 4 * l;  // this lane's first feature; types are 16-byte aligned
+        const uint32_t tw = fl < n ? ((const g_u32*)types)[fl >> 2] : 0u;
+        uint32_t t[4], multi[4], gi[4], pf[4], ex[4], nm, tot;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool valid = fl + k < n;
+            t[k] = valid ? (tw >> (8 * k)) & 0xffu : 0u;
+            bad_type |= t[k] > 5u;
+            multi[k] = (valid && t[k] >= 3u && t[k] <= 5u) ? 1u : 0u;
+            pf[k] = valid ? 1u : 0u;
+        }
+        excl_scan4(multi, gi, nm);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (multi[k]) {
+                const uint32_t i = go_base + gi[k];
+                if (i < (uint32_t)n_go) {
+                    const int32_t c = ((const g_i32*)go)[i];
+                    bad_cnt |= c < 0;
+                    pf[k] = min((uint32_t)max(c, 0), pcap + 1u);  // clamped: the scans cannot wrap
+                } else {
+                    bad_cnt = true;
+                }
             }
         }
-        uint32_t tot;
-        const uint32_t ex = P + excl_scan(pf, tot);
-        if (valid) geo_off[f] = (int32_t)ex;
+        excl_scan4(pf, ex, tot);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ex[k] += P;
+        store4(geo_off, f0, n - f0, ex);
         go_base += nm;
         P += tot;
         if (__ballot(bad_type || bad_cnt) || P > pcap) break;
@@ -165,38 +241,50 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     if (l == 0) geo_off[n] = (int32_t)P;
     mem_publish();
 
-    // ---- pass 2: parts -> rings ----
+#if defined(COVT_ASM_PASSES) && COVT_ASM_PASSES < 2  // ablation build: stop here
+    res.status = COVT_OK;
+    return;
+#endif
+    // ---- pass 2: parts -> rings (items: parts, segments: features) ----
     uint32_t po_base = 0, R = 0;
     {
         Expand x{geo_off, n, (int32_t)P, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t p0 = x.q;
-            int32_t f, rank, fend;
-            const int32_t L = x.step(sm, f, rank, fend);
-            const bool valid = l < L;
-            const uint32_t t = valid ? (uint32_t)((const g_u8*)types)[f] : 0u;
-            const bool uses_po = valid && t != 0u && t != 3u;  // line and polygon parts
-            uint32_t npo;
-            const uint32_t pi = po_base + excl_scan(uses_po ? 1u : 0u, npo);
-            uint32_t c = 0;
-            if (uses_po) {
-                if (pi < (uint32_t)n_po) {
-                    const int32_t v = ((const g_i32*)po)[pi];
-                    bad_cnt |= v < 0;
-                    c = min((uint32_t)max(v, 0), rcap + 1u);
-                } else {
-                    bad_cnt = true;
+            int32_t f[4], fs[4], fe[4];
+            const int32_t L = x.step(sm, f, fs, fe);
+            uint32_t t[4], usep[4], pi[4], rp[4], scr[4], ex[4], npo, tot;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool valid = 4 * l + k < L;
+                t[k] = valid ? (uint32_t)((const g_u8*)types)[f[k]] : 0u;
+                usep[k] = (valid && t[k] != 0u && t[k] != 3u) ? 1u : 0u;  // line and polygon parts
+            }
+            excl_scan4(usep, pi, npo);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool valid = 4 * l + k < L;
+                uint32_t c = 0;
+                if (usep[k]) {
+                    const uint32_t i = po_base + pi[k];
+                    if (i < (uint32_t)n_po) {
+                        const int32_t v = ((const g_i32*)po)[i];
+                        bad_cnt |= v < 0;
+                        c = min((uint32_t)max(v, 0), rcap + 1u);
+                    } else {
+                        bad_cnt = true;
+                    }
                 }
+                const bool poly = t[k] == 2u || t[k] == 5u;
+                rp[k] = valid ? (poly ? c : 1u) : 0u;
+                const uint32_t vcount = (t[k] == 1u || t[k] == 4u) ? c : 1u;  // vertices of a line / point part
+                scr[k] = poly ? 1u : (min(vcount, ccap + 1u) << 1);
             }
-            const bool poly = t == 2u || t == 5u;
-            const uint32_t rp = valid ? (poly ? c : 1u) : 0u;
-            const uint32_t vcount = (t == 1u || t == 4u) ? c : 1u;  // vertices of a line / point part
-            uint32_t tot;
-            const uint32_t ex = R + excl_scan(rp, tot);
-            if (valid) {
-                part_off[p0 + l] = (int32_t)ex;
-                part_scr[p0 + l] = poly ? 1 : (int32_t)(min(vcount, ccap + 1u) << 1);
-            }
+            excl_scan4(rp, ex, tot);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ex[k] += R;
+            store4(part_off, p0, L, ex);
+            store4(part_scr, p0, L, scr);
             po_base += npo;
             R += tot;
             if (__ballot(bad_cnt) || R > rcap) break;
@@ -206,37 +294,52 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     if (l == 0) part_off[P] = (int32_t)R;
     mem_publish();
 
-    // ---- pass 3: rings -> coordinates ----
+#if defined(COVT_ASM_PASSES) && COVT_ASM_PASSES < 3  // ablation build: stop here
+    res.status = COVT_OK;
+    return;
+#endif
+    // ---- pass 3: rings -> coordinates (items: rings, segments: parts) ----
     uint32_t ro_base = 0, V = 0, VS = 0;
     {
         Expand x{part_off, (int32_t)P, (int32_t)R, 0, 0, 0};
         while (x.q < x.total) {
-            const int32_t r0i = x.q;
-            int32_t p, rank, pend;
-            const int32_t L = x.step(sm, p, rank, pend);
-            const bool valid = l < L;
-            const int32_t sp = valid ? ((const g_i32*)part_scr)[p] : 0;
-            const bool poly = valid && (sp & 1);
-            uint32_t nr;
-            const uint32_t ri = ro_base + excl_scan(poly ? 1u : 0u, nr);
-            uint32_t vs = valid ? (uint32_t)sp >> 1 : 0u;
-            if (poly) {
-                if (ri < (uint32_t)n_ro) {
-                    const int32_t v = ((const g_i32*)ro)[ri];
-                    bad_cnt |= v < 0;
-                    vs = min((uint32_t)max(v, 0), ccap + 1u);
-                } else {
-                    bad_cnt = true;
+            const int32_t r0 = x.q;
+            int32_t p[4], ps[4], pe[4];
+            const int32_t L = x.step(sm, p, ps, pe);
+            uint32_t poly[4], ri[4], vs[4], vo_[4], ex[4], src[4], nr, tv, ts;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool valid = 4 * l + k < L;
+                const int32_t sp = valid ? ((const g_i32*)part_scr)[p[k]] : 0;
+                poly[k] = (valid && (sp & 1)) ? 1u : 0u;
+                vs[k] = valid ? (uint32_t)sp >> 1 : 0u;
+            }
+            excl_scan4(poly, ri, nr);
+            uint32_t closing[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (poly[k]) {
+                    const uint32_t i = ro_base + ri[k];
+                    if (i < (uint32_t)n_ro) {
+                        const int32_t v = ((const g_i32*)ro)[i];
+                        bad_cnt |= v < 0;
+                        vs[k] = min((uint32_t)max(v, 0), ccap + 1u);
+                    } else {
+                        bad_cnt = true;
+                    }
                 }
+                closing[k] = (poly[k] && !closed && vs[k] > 0u) ? 1u : 0u;
+                vo_[k] = vs[k] + closing[k];
             }
-            const uint32_t closing = (poly && !closed && vs > 0u) ? 1u : 0u;
-            uint32_t tv, ts;
-            const uint32_t ex = V + excl_scan(vs + closing, tv);
-            const uint32_t src = VS + excl_scan(vs, ts);
-            if (valid) {
-                ring_off[r0i + l] = (int32_t)ex;
-                ring_scr[r0i + l] = (int32_t)(src | (closing << 31));
+            excl_scan4(vo_, ex, tv);
+            excl_scan4(vs, src, ts);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                ex[k] += V;
+                src[k] = (VS + src[k]) | (closing[k] << 31);
             }
+            store4(ring_off, r0, L, ex);
+            store4(ring_scr, r0, L, src);
             ro_base += nr;
             V += tv;
             VS += ts;
@@ -247,27 +350,56 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     if (l == 0) ring_off[R] = (int32_t)V;
     mem_publish();
 
+#if defined(COVT_ASM_PASSES) && COVT_ASM_PASSES < 4  // ablation build: stop here
+    res.status = COVT_OK;
+    return;
+#endif
     // ---- pass 4: coordinates (ICE gather) ----
     bool bad_idx = false;
-    {
+    if (V == VS) {
+        // no closing vertex to insert: coordinate v is source vertex v (a straight copy / gather)
+        for (int32_t v0 = 0; v0 < (int32_t)V; v0 += kW) {
+            const int32_t i0 = v0 + 4 * l;
+            const int32_t L = (int32_t)V - v0;
+            int32_t idx[4];
+            if (ice && i0 + 4 <= (int32_t)V) {  // vertexOffsets are 16-byte aligned, i0 % 4 == 0
+                const i32x4 w = *(const g_i32x4*)(vo + i0);
+                idx[0] = w.x; idx[1] = w.y; idx[2] = w.z; idx[3] = w.w;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    idx[k] = i0 + k < (int32_t)V ? (ice ? ((const g_i32*)vo)[i0 + k] : i0 + k) : 0;
+            }
+            uint64_t xy[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool valid = i0 + k < (int32_t)V;
+                const bool inr = (uint32_t)idx[k] < (uint32_t)n_vb;
+                bad_idx |= valid && !inr;
+                xy[k] = (valid && inr) ? ((const g_u64*)vb)[idx[k]] : 0ull;
+            }
+            store4_xy(coords, v0, L, xy);
+        }
+    } else {
         Expand x{ring_off, (int32_t)R, (int32_t)V, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t v0 = x.q;
-            int32_t r, rank, rend;
-            const int32_t L = x.step(sm, r, rank, rend);
-            if (l < L) {
-                const uint32_t sr = (uint32_t)((const g_i32*)ring_scr)[r];
+            int32_t r[4], rs[4], re[4];
+            const int32_t L = x.step(sm, r, rs, re);
+            uint64_t xy[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int32_t v = v0 + 4 * l + k;
+                const bool valid = 4 * l + k < L;
+                const uint32_t sr = valid ? (uint32_t)((const g_i32*)ring_scr)[r[k]] : 0u;
                 const int32_t first = (int32_t)(sr & 0x7fffffffu);
-                const bool last = (int32_t)(v0 + l) == rend - 1;
-                const int32_t src = (sr >> 31) && last ? first : first + rank;
-                const int32_t idx = ice ? ((const g_i32*)vo)[src] : src;
-                if ((uint32_t)idx < (uint32_t)n_vb) {
-                    coords[v0 + l] = ((const g_u64*)vb)[idx];
-                } else {
-                    bad_idx = true;  // vertexBuffer[offset] out of range (ArrayIndexOutOfBounds)
-                    coords[v0 + l] = 0;
-                }
+                const int32_t src = ((sr >> 31) && v == re[k] - 1) ? first : first + (v - rs[k]);
+                const int32_t idx = valid ? (ice ? ((const g_i32*)vo)[src] : src) : 0;
+                const bool inr = (uint32_t)idx < (uint32_t)n_vb;
+                bad_idx |= valid && !inr;  // vertexBuffer[offset] out of range (ArrayIndexOutOfBounds)
+                xy[k] = (valid && inr) ? ((const g_u64*)vb)[idx] : 0ull;
             }
+            store4_xy(coords, v0, L, xy);
         }
     }
     if (__ballot(bad_idx)) { res.status = COVT_ERR_TRUNCATED; return; }

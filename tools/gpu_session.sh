@@ -20,6 +20,12 @@ step() {  # step NAME LIMIT cmd...
 for s in "$@"; do
     case $s in
     tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests_asm) step pytest_gpu_asm 600 python -m pytest tests/test_gpu_assembly.py -m gpu -q -p no:cacheprovider --durations=5 ;;
+    asm_ab) for v in libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so; do
+            COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/asm_run.py 20 2>&1 | grep -v amdgpu.ids || fatal asm_ab $?
+        done ;;
+    pmc_asm) step pmc_asm_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_asm_fetch -o run --output-format csv -- python tools/asm_run.py 3 && \
+             step pmc_asm_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_asm_write -o run --output-format csv -- python tools/asm_run.py 3 ;;
     tests_all) step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
