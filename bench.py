@@ -80,6 +80,16 @@ def lpt_shards(weights, n):
     return [sorted(s) for s in shard]
 
 
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(picks, seconds, threads):
     """The oracle (C restatement of the Java DecodingUtils semantics) on host cores: bounded sample."""
     sys.path.insert(0, ROOT)
@@ -92,18 +102,58 @@ def cpu_baseline(picks, seconds, threads):
     st, ib, ob, vx = O.decode_tiles_mt(blob, offs, sizes, O.FMT_GENC, O.ID_FORMAT, threads)
     if st != 0:
         raise RuntimeError("oracle baseline failed: %d" % st)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        O.decode_tiles_mt(blob, offs, sizes, O.FMT_GENC, O.ID_FORMAT, threads)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+    def timed(nthr, secs):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            O.decode_tiles_mt(blob, offs, sizes, O.FMT_GENC, O.ID_FORMAT, nthr)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return reps, el
+
+    reps, el = timed(threads, seconds)
+    reps1, el1 = timed(1, max(seconds / 3, 1.0))
     return {"value": round(ib * reps / el / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": "%d tiles of the same batch (%.1f MB stream bytes) x %d reps in %.1f s; "
                       "C restatement of DecodingUtils (oracle/covt_oracle.c), %d threads" %
                       (len(sample), ib / 1e6, reps, el, threads),
-            "mvert_per_s": round(vx * reps / el / 1e6, 3)}
+            "mvert_per_s": round(vx * reps / el / 1e6, 3),
+            "value_1thread": round(ib * reps1 / el1 / 1e9, 4),
+            "host": {"cpu_model": cpu_model(), "nproc": os.cpu_count()}}
+
+
+def end_to_end(plan, batch, stream, torch, dev, reps):
+    """SURVEY §8(d) second timing: pinned host tiles -> H2D -> decode -> D2H of every output (not `value`)."""
+    h_in = torch.from_numpy(plan.blob).pin_memory()
+    h_desc = torch.from_numpy(plan.descs).pin_memory() if plan.num_streams else None
+    h_out = torch.empty(batch.d_out.numel(), dtype=torch.uint8).pin_memory()
+    h_res = torch.empty(batch.d_res.numel(), dtype=torch.int32).pin_memory()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    tot = [0.0, 0.0, 0.0, 0.0]
+    with torch.cuda.stream(stream):
+        for i in range(reps + 1):
+            ev[0].record(stream)
+            batch.d_in.copy_(h_in, non_blocking=True)
+            if h_desc is not None:
+                batch.d_desc.copy_(h_desc, non_blocking=True)
+            ev[1].record(stream)
+            batch.decode(stream)
+            ev[2].record(stream)
+            h_out.copy_(batch.d_out, non_blocking=True)
+            h_res.copy_(batch.d_res, non_blocking=True)
+            ev[3].record(stream)
+            torch.cuda.synchronize(dev)
+            if i:  # first rep warms the pinned buffers
+                tot[0] += ev[0].elapsed_time(ev[3])
+                tot[1] += ev[0].elapsed_time(ev[1])
+                tot[2] += ev[1].elapsed_time(ev[2])
+                tot[3] += ev[2].elapsed_time(ev[3])
+    ms = [t / reps for t in tot]
+    return {"value": round(plan.in_bytes / (ms[0] * 1e-3) / 1e9, 3), "unit": "GB/s", "ms": round(ms[0], 3),
+            "h2d_ms": round(ms[1], 3), "decode_ms": round(ms[2], 3), "d2h_ms": round(ms[3], 3),
+            "h2d_GBps": round(h_in.numel() / (ms[1] * 1e-3) / 1e9, 2),
+            "d2h_GBps": round(h_out.numel() / (ms[3] * 1e-3) / 1e9, 2), "reps": reps,
+            "note": "pinned host tile bytes + descriptors H2D, one decode launch, all outputs + results D2H"}
 
 
 def assembly_leg(batch, plan, stream, args, dist, torch, dev):
@@ -159,6 +209,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--id-mode", type=int, default=0)
     ap.add_argument("--no-assemble", action="store_true", help="skip the geometry-assembly leg")
+    ap.add_argument("--e2e-reps", type=int, default=3, help="end-to-end (PCIe-inclusive) reps; 0 skips")
     args = ap.parse_args()
 
     import torch
@@ -184,7 +235,9 @@ def main():
         shards = lpt_shards([len(t) for _, t in allp], world)
         picks = [allp[i] for i in shards[rank]]
 
+    t_plan = time.perf_counter()
     plan = covt.Plan.from_tiles([t for _, t in picks], covt.FORMAT_GENC, args.id_mode)
+    t_plan = time.perf_counter() - t_plan
     if (plan.tile_status != 0).any():
         raise RuntimeError("tile walk failed")
     batch = covt.DeviceBatch(plan, dev)
@@ -212,6 +265,9 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
 
+    e2e = None
+    if args.e2e_reps > 0:
+        e2e = end_to_end(plan, batch, stream, torch, dev, args.e2e_reps)
     asm_line = None
     if not args.no_assemble and plan.num_geometry_columns:
         asm_line = assembly_leg(batch, plan, stream, args, dist, torch, dev)
@@ -274,6 +330,9 @@ def main():
         }
         if asm_line is not None:
             line["assembly"] = asm_line
+        if e2e is not None:
+            line["end_to_end"] = e2e
+        line["host_plan_ms"] = round(t_plan * 1e3, 1)  # covt_plan_create metadata walk (+ packing), host
         if world == 1 and not args.no_cpu:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(picks, args.cpu_seconds, threads)
