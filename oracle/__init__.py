@@ -40,9 +40,22 @@ class OracleStream(C.Structure):
     ]
 
 
+PROP_BOOLEAN, PROP_INT64, PROP_FLOAT, PROP_STRING = 0, 1, 2, 3
+
+
+class OracleProp(C.Structure):
+    """oracle_prop (covt_oracle.h): one property (sub)column; s_* indexed by role
+    0 present, 1 data, 2 length, 3 dictionary."""
+    _fields_ = [("layer", C.c_int32), ("column", C.c_int32), ("type", C.c_int32), ("column_type", C.c_int32),
+                ("n_features", C.c_int32), ("lang", C.c_int32), ("name_len", C.c_int32), ("lang_len", C.c_int32),
+                ("name_off", C.c_int64), ("lang_off", C.c_int64), ("s_off", C.c_int64 * 4), ("s_nv", C.c_int32 * 4),
+                ("s_bl", C.c_int32 * 4), ("s_enc", C.c_int32 * 4)]
+
+
 def build(force: bool = False) -> str:
+    srcs = ("covt_oracle.c", "covt_oracle_props.c", "covt_oracle.h")
     if force or not os.path.exists(_LIB_PATH) or (
-        os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "covt_oracle.c"))
+        os.path.getmtime(_LIB_PATH) < max(os.path.getmtime(os.path.join(_HERE, f)) for f in srcs)
     ):
         subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle_covt.so"])
     return _LIB_PATH
@@ -90,6 +103,11 @@ def lib():
         L.oracle_assemble_geometry.argtypes = [u8p, C.c_int32, i32p, C.c_int32, i32p, C.c_int32, i32p, C.c_int32,
                                                i32p, C.c_int32, i32p, C.c_int32, C.c_int, C.c_int32, C.c_int32,
                                                C.c_int32, i32p, i32p, i32p, i32p, i32p, i32p, i32p]
+        L.oracle_walk_properties.argtypes = [u8p, sz, C.c_int, C.POINTER(OracleProp), C.c_int32, i32p]
+        L.oracle_property_sizes.argtypes = [C.POINTER(OracleProp), i64p]
+        L.oracle_property_sizes.restype = None
+        L.oracle_decode_property.argtypes = [u8p, sz, C.POINTER(OracleProp), C.c_int, C.c_void_p, C.c_void_p,
+                                             C.c_void_p, C.c_void_p, i32p]
         _lib = L
     return _lib
 
@@ -256,6 +274,65 @@ def walk_tile(tile: bytes, fmt: int = FMT_GENC):
     ss = (OracleStream * max(n.value, 1))()
     st = lib().oracle_walk_tile(p, arr.size, fmt, ss, n.value, C.byref(n))
     return st, list(ss[: n.value])
+
+
+def walk_properties(tile: bytes, fmt: int = FMT_GENC):
+    """(status, [OracleProp]) -- every property (sub)column of a tile (covt_oracle_props.c)."""
+    arr, p = _u8(tile)
+    n = C.c_int32(0)
+    st = lib().oracle_walk_properties(p, arr.size, fmt, None, 0, C.byref(n))
+    if st:
+        return st, []
+    ps = (OracleProp * max(n.value, 1))()
+    st = lib().oracle_walk_properties(p, arr.size, fmt, ps, n.value, C.byref(n))
+    return st, list(ps[: n.value])
+
+
+def prop_name(tile: bytes, p: OracleProp) -> str:
+    """Column name, plus ':<lang>' for a localized sub-column (Gen C)."""
+    name = bytes(tile[p.name_off:p.name_off + p.name_len]).decode("utf-8") if p.name_off >= 0 else ""
+    if p.lang >= 0:
+        name += ":" + bytes(tile[p.lang_off:p.lang_off + p.lang_len]).decode("utf-8")
+    return name
+
+
+def decode_property(tile: bytes, p: OracleProp, mode: int = ID_FORMAT):
+    """(status, validity u8[ceil(n/8)], values, dict_offsets i32[n_dict+1], dict_bytes u8, n_valid) in the
+    Arrow-style layout of include/covt.h ("Property columns")."""
+    arr, tp = _u8(tile)
+    sz = np.zeros(4, dtype=np.int64)
+    lib().oracle_property_sizes(C.byref(p), _p(sz, C.c_int64))
+    bufs = [np.zeros(max(int(x), 1) + 16, dtype=np.uint8) for x in sz]
+    nv = C.c_int32(0)
+    st = lib().oracle_decode_property(tp, arr.size, C.byref(p), mode, bufs[0].ctypes.data, bufs[1].ctypes.data,
+                                      bufs[2].ctypes.data, bufs[3].ctypes.data, C.byref(nv))
+    vdt = {PROP_INT64: np.int64, PROP_FLOAT: np.float32, PROP_STRING: np.int32}.get(p.type)
+    vals = bufs[1][:int(sz[1])]
+    if vdt is not None:
+        vals = vals.view(vdt)
+    return (st, bufs[0][:int(sz[0])], vals, bufs[2][:int(sz[2])].view(np.int32), bufs[3][:int(sz[3])],
+            nv.value)
+
+
+def property_values(tile: bytes, p: OracleProp, mode: int = ID_FORMAT):
+    """Java-level view (List<Optional>): per feature None or the value (bool / int / float / str)."""
+    st, val, vals, doff, dby, _ = decode_property(tile, p, mode)
+    if st:
+        return st, None
+    out = []
+    for i in range(p.n_features):
+        if not (int(val[i >> 3]) >> (i & 7)) & 1:
+            out.append(None)
+        elif p.type == PROP_BOOLEAN:
+            out.append(bool((int(vals[i >> 3]) >> (i & 7)) & 1))
+        elif p.type == PROP_INT64:
+            out.append(int(vals[i]))
+        elif p.type == PROP_FLOAT:
+            out.append(float(vals[i]))
+        else:
+            k = int(vals[i])
+            out.append(bytes(dby[doff[k]:doff[k + 1]]).decode("utf-8"))
+    return st, out
 
 
 def stream_output(s: OracleStream, id_mode: int = ID_FORMAT):

@@ -138,6 +138,32 @@ int oracle_assemble_geometry(const uint8_t* types, int32_t n, const int32_t* go,
                              int32_t* ring_off, int32_t* coords, int32_t* n_parts, int32_t* n_rings,
                              int32_t* n_coords);
 
+/* ---- property columns (covt_oracle_props.c; CovtParser.decodePropertyColumn :276-354) ----
+ * One record per property (sub)column: Gen C LOCALIZED_DICTIONARY columns yield one per language
+ * (lang >= 0, sharing the column's length/dictionary streams).  Streams by role:
+ * 0 present, 1 data, 2 length, 3 dictionary (s_off = tile-relative payload offset, -1 absent). */
+#define ORACLE_PROP_BOOLEAN 0
+#define ORACLE_PROP_INT64 1
+#define ORACLE_PROP_FLOAT 2
+#define ORACLE_PROP_STRING 3
+typedef struct oracle_prop {
+    int32_t layer, column, type, column_type; /* type: ORACLE_PROP_* or -1 (unsupported data type) */
+    int32_t n_features, lang, name_len, lang_len;
+    int64_t name_off, lang_off;               /* UTF-8 names inside the tile (-1: none) */
+    int64_t s_off[4];
+    int32_t s_nv[4], s_bl[4], s_enc[4];
+} oracle_prop;
+int oracle_walk_properties(const uint8_t* tile, size_t len, int format, oracle_prop* out, int32_t max_out,
+                           int32_t* n_out);
+/* Output byte sizes: validity, values, dictionary offsets, dictionary bytes */
+void oracle_property_sizes(const oracle_prop* p, int64_t sizes[4]);
+/* Decode one property (sub)column into the Arrow-style layout of include/covt.h: validity bitmap
+ * (LSB first, bits >= n clear), values at feature positions (BOOLEAN: bitmap; INT64: int64;
+ * FLOAT: float32 bits; STRING: int32 dictionary index; absent slots 0), dictionary offsets
+ * [n_dict + 1] and bytes.  mode: ORACLE_ID_FORMAT (64-bit varints) / ORACLE_ID_JAVA (4-byte cap). */
+int oracle_decode_property(const uint8_t* tile, size_t len, const oracle_prop* p, int mode, uint8_t* validity,
+                           void* values, int32_t* dict_offsets, uint8_t* dict_bytes, int32_t* n_valid);
+
 /* CPU baseline: walk + decode every Id/Geometry stream of n_tiles tiles (concatenated in
  * `bytes` at `offsets`) on n_threads host threads; output goes to per-thread scratch.
  * Returns status; totals (optional) receive stream bytes, output bytes, vertices. */

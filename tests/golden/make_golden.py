@@ -12,6 +12,9 @@ What it writes (all DATA -- inputs and expected outputs, no reference source):
                                    Also the oracle-vs-MVT pass list at generation time.
   kats.json                        known-answer vectors from the reference's TS unit tests
                                    (parser/js/test/unit/decoder/decodingUtils.spec.ts), valid subset.
+  mvt_prop_digests.json            per OMT tile, layer and MVT key: SHA-256 of the per-feature property
+                                   values of the reference's MVT originals (tests/covt_props.py), plus
+                                   the oracle's property-column pass list at generation time.
   oracle_streams.json              per tile and Id/Geometry stream: walk record + SHA-256 of the
                                    oracle's decoded bytes (both Id modes) -- regression pin.
   5_16_20.npz                      full decoded arrays of the config-1/2 tile.
@@ -34,6 +37,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import oracle as O  # noqa: E402
 import covt_geom as G  # noqa: E402
+import covt_props as P  # noqa: E402
 
 REF = "/root/reference/test/fixtures"
 SETS = ("omt", "bing", "amazon")
@@ -146,6 +150,39 @@ def mvt_digests():
     return res
 
 
+def mvt_prop_digests():
+    """{tile: {"mvt": {layer: {key: digest}}, "oracle_pass": [[layer, column name], ...]}} over the
+    OMT tiles that have an MVT original; a decoded (sub)column passes when its value digest equals
+    the MVT digest of one of its candidate keys."""
+    res = {}
+    for f in sorted(glob.glob(os.path.join(HERE, "tiles", "omt", "*.covt"))):
+        name = os.path.basename(f)[:-5]
+        mpath = os.path.join(REF, "omt", "mvt", name + ".mvt")
+        if not os.path.exists(mpath):
+            continue
+        t = open(f, "rb").read()
+        mvt = P.mvt_properties(open(mpath, "rb").read())
+        dig = {}
+        for lname, feats in mvt.items():
+            keys = sorted({k for ft in feats for k in ft})
+            dig[lname] = {k: P.values_digest([ft.get(k) for ft in feats]) for k in keys}
+        names = layer_names(t)
+        st, props = O.walk_properties(t)
+        passed = []
+        for p in props:
+            lname = names[p.layer]
+            st2, vals = O.property_values(t, p)
+            if st2 or lname not in dig:
+                continue
+            col = O.prop_name(t, p)
+            base, lang = (col.split(":", 1) + [None])[:2] if p.lang >= 0 else (col, None)
+            d = P.values_digest(vals)
+            if any(dig[lname].get(k) == d for k in P.candidate_keys(base, lang)):
+                passed.append([p.layer, col])
+        res[name] = {"mvt": dig, "oracle_pass": passed, "n_props": len(props)}
+    return res
+
+
 def kats():
     src = "parser/js/test/unit/decoder/decodingUtils.spec.ts"
     return {
@@ -213,6 +250,10 @@ def tile_arrays(name="omt/5_16_20"):
 
 def main():
     O.build()
+    if "--props" in sys.argv:  # regenerate only the property digests
+        with open(os.path.join(HERE, "mvt_prop_digests.json"), "w") as f:
+            json.dump(mvt_prop_digests(), f, separators=(",", ":"), sort_keys=True)
+        return
     copy_tiles()
     with open(os.path.join(HERE, "kats.json"), "w") as f:
         json.dump(kats(), f, indent=1)
@@ -220,6 +261,8 @@ def main():
         json.dump(mvt_digests(), f, indent=0, sort_keys=True)
     with open(os.path.join(HERE, "oracle_streams.json"), "w") as f:
         json.dump(stream_records(), f, separators=(",", ":"))
+    with open(os.path.join(HERE, "mvt_prop_digests.json"), "w") as f:
+        json.dump(mvt_prop_digests(), f, separators=(",", ":"), sort_keys=True)
     tile_arrays()
     print("golden fixtures written to", HERE)
 
