@@ -42,7 +42,13 @@ ID_FORMAT, ID_JAVA = 0, 1
 
 (OP_NONE, OP_BYTE_RLE_U8, OP_RLE_U64, OP_RLE_I32, OP_RLE_S64, OP_VARINT_I32, OP_VARINT_ZZ_I32,
  OP_VARINT_ZZ_DELTA_I32, OP_VARINT_ZZ_DELTA_XY, OP_VARINT_DELTA_MORTON, OP_FPF_ZZ_DELTA_I32, OP_FPF_ZZ_DELTA_XY,
- OP_FPF_DELTA_MORTON, OP_VARINT_U64, OP_VARINT_I32_AS_I64, OP_VARINT_ZZ_DELTA_I64) = range(16)
+ OP_FPF_DELTA_MORTON, OP_VARINT_U64, OP_VARINT_I32_AS_I64, OP_VARINT_ZZ_DELTA_I64, OP_BYTE_RLE_RAW,
+ OP_VARINT_ZZ_I32_AS_I64, OP_VARINT_ZZ_S64, OP_VARINT_ZZ_DELTA_S64) = range(20)
+
+# property columns (include/covt.h "Property columns")
+PLAN_PROPERTIES = 0x1
+PROP_BOOLEAN, PROP_INT64, PROP_FLOAT, PROP_STRING = 0, 1, 2, 3
+PROP_DICT_OWNER, PROP_DENSE_BOOL, PROP_UNSUPPORTED, PROP_DATA_SHORT, PROP_UNSUPPORTED_LATE = 0x1, 0x2, 0x4, 0x8, 0x10
 
 # StreamType ordinals (converter/StreamType.java)
 GEOMETRY_TYPES, GEOMETRY_OFFSETS, PART_OFFSETS, RING_OFFSETS, VERTEX_OFFSETS, VERTEX_BUFFER = range(4, 10)
@@ -115,6 +121,17 @@ GEOM_INFO_DTYPE = np.dtype([("tile", np.int32), ("layer", np.int32), ("column_ty
                             ("desc_index", np.int32), ("reserved", np.int32), ("out_off", np.int64, (6,))])
 GEOM_RESULT_DTYPE = np.dtype([("status", np.int32), ("num_parts", np.int32), ("num_rings", np.int32),
                               ("num_coords", np.int32)])
+PROP_INFO_DTYPE = np.dtype([("tile", np.int32), ("layer", np.int32), ("column", np.int32), ("type", np.int32),
+                            ("column_type", np.int32), ("n_features", np.int32), ("n_data", np.int32),
+                            ("n_dict", np.int32), ("lang", np.int32), ("name_len", np.int32), ("lang_len", np.int32),
+                            ("dict_bytes", np.int32), ("stream", np.int32, (3,)), ("desc_index", np.int32),
+                            ("name_off", np.int64), ("lang_off", np.int64), ("out_off", np.int64, (4,))])
+PROP_DESC_DTYPE = np.dtype([("present_off", np.int64), ("data_off", np.int64), ("length_off", np.int64),
+                            ("dict_in_off", np.int64), ("out_off", np.int64, (4,)), ("res", np.int32, (3,)),
+                            ("n_features", np.int32), ("n_data", np.int32), ("n_dict", np.int32),
+                            ("dict_bytes", np.int32), ("type", np.int16), ("flags", np.int16)])
+PROP_RESULT_DTYPE = np.dtype([("status", np.int32), ("n_valid", np.int32)])
+assert PROP_INFO_DTYPE.itemsize == 112 and PROP_DESC_DTYPE.itemsize == 96
 GEOM_CLOSED_IN_STREAM = 0x1
 GEOM_TOO_LARGE = 0x80000000
 GEOM_MAX_CAP = 1 << 25
@@ -135,6 +152,9 @@ EXPORTED_SYMBOLS = (
     "covt_device_count", "covt_plan_family_counts", "covt_decode_streams_device_grouped",
     "covt_plan_num_geometry_columns", "covt_plan_assembly_bytes", "covt_plan_geometry_columns",
     "covt_plan_geometry_descs", "covt_assemble_geometry_device", "covt_plan_assemble_host",
+    "covt_plan_create_ex", "covt_plan_num_property_columns", "covt_plan_property_bytes",
+    "covt_plan_property_columns", "covt_plan_property_descs", "covt_materialize_properties_device",
+    "covt_plan_properties_host",
 )
 
 
@@ -198,6 +218,16 @@ def lib() -> C.CDLL:
     L.covt_plan_geometry_descs.argtypes = [vp, vp]
     L.covt_assemble_geometry_device.argtypes = [vp, vp, vp, C.c_int64, vp, vp, vp]
     L.covt_plan_assemble_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
+    L.covt_plan_create_ex.argtypes = [u8p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
+                                      C.c_int32, C.c_uint32, C.POINTER(vp)]
+    L.covt_plan_num_property_columns.argtypes = [vp]
+    L.covt_plan_num_property_columns.restype = C.c_int64
+    L.covt_plan_property_bytes.argtypes = [vp]
+    L.covt_plan_property_bytes.restype = C.c_int64
+    L.covt_plan_property_columns.argtypes = [vp, vp]
+    L.covt_plan_property_descs.argtypes = [vp, vp]
+    L.covt_materialize_properties_device.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp]
+    L.covt_plan_properties_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
     L.covt_version.restype = C.c_char_p
     L.covt_device_count.argtypes = [i32p]
     _lib = L
@@ -364,15 +394,16 @@ def pack_tiles(tiles: List[bytes], align: int = 16):
 class Plan:
     """Host-side container walk of a tile batch -> per-stream descriptors (covt_plan_create)."""
 
-    def __init__(self, blob: np.ndarray, offsets, sizes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT):
+    def __init__(self, blob: np.ndarray, offsets, sizes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT,
+                 flags: int = 0):
         L = lib()
         self.blob = np.ascontiguousarray(blob, dtype=np.uint8)
         self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         self.sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
         self.n_tiles = int(self.offsets.size)
         h = C.c_void_p()
-        _raise(L.covt_plan_create(_ptr(self.blob, C.c_uint8), _ptr(self.offsets, C.c_uint64),
-                                  _ptr(self.sizes, C.c_uint64), self.n_tiles, fmt, id_mode, C.byref(h)),
+        _raise(L.covt_plan_create_ex(_ptr(self.blob, C.c_uint8), _ptr(self.offsets, C.c_uint64),
+                                     _ptr(self.sizes, C.c_uint64), self.n_tiles, fmt, id_mode, flags, C.byref(h)),
                "covt_plan_create")
         self._h = h
         self.num_streams = int(L.covt_plan_num_streams(h))
@@ -399,11 +430,19 @@ class Plan:
         if self.num_geometry_columns:
             L.covt_plan_geometry_columns(h, self.geom.ctypes.data)
             L.covt_plan_geometry_descs(h, self.gdescs.ctypes.data)
+        # property columns (include/covt.h "Property columns"; plans made with PLAN_PROPERTIES)
+        self.num_property_columns = int(L.covt_plan_num_property_columns(h))
+        self.property_bytes = int(L.covt_plan_property_bytes(h))
+        self.props = np.zeros(self.num_property_columns, dtype=PROP_INFO_DTYPE)
+        self.pdescs = np.zeros(self.num_property_columns, dtype=PROP_DESC_DTYPE)
+        if self.num_property_columns:
+            L.covt_plan_property_columns(h, self.props.ctypes.data)
+            L.covt_plan_property_descs(h, self.pdescs.ctypes.data)
 
     @classmethod
-    def from_tiles(cls, tiles: List[bytes], fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT):
+    def from_tiles(cls, tiles: List[bytes], fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT, flags: int = 0):
         blob, offs, sizes = pack_tiles(tiles)
-        return cls(blob, offs, sizes, fmt, id_mode)
+        return cls(blob, offs, sizes, fmt, id_mode, flags)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -438,6 +477,44 @@ class Plan:
         _raise(lib().covt_plan_assemble_host(self._h, _ptr(self.blob, C.c_uint8), self.blob.size, asm.ctypes.data,
                                              gres.ctypes.data), "covt_plan_assemble_host")
         return asm[:self.assembly_bytes], gres[:self.num_geometry_columns]
+
+    def properties_host(self):
+        """H2D + decode + property materialization + D2H (covt_plan_properties_host).
+        Returns (uint8 property buffer, results[num_property_columns] in tile order)."""
+        buf = np.zeros(max(self.property_bytes, 1), dtype=np.uint8)
+        pres = np.zeros(max(self.num_property_columns, 1), dtype=PROP_RESULT_DTYPE)
+        _raise(lib().covt_plan_properties_host(self._h, _ptr(self.blob, C.c_uint8), self.blob.size,
+                                               buf.ctypes.data, pres.ctypes.data), "covt_plan_properties_host")
+        return buf[:self.property_bytes], pres[:self.num_property_columns]
+
+    def property_name(self, c: int) -> str:
+        """Column name of property (sub)column c, plus ':<lang>' for a localized language stream."""
+        p = self.props[c]
+        name = bytes(self.blob[int(p["name_off"]):int(p["name_off"]) + int(p["name_len"])]).decode("utf-8") \
+            if p["name_off"] >= 0 else ""
+        if p["lang"] >= 0:
+            name += ":" + bytes(self.blob[int(p["lang_off"]):int(p["lang_off"]) + int(p["lang_len"])]).decode("utf-8")
+        return name
+
+    def property_column(self, buf: np.ndarray, pres: np.ndarray, c: int) -> "PropertyColumn":
+        """Property (sub)column c (tile order) of a property buffer (raises on its status)."""
+        p, r = self.props[c], pres[c]
+        _raise(int(r["status"]), "property column %d (tile %d, layer %d)" % (c, p["tile"], p["layer"]))
+        n = int(p["n_features"])
+        nb = (n + 7) // 8
+        t = int(p["type"])
+
+        def seg(k, nbytes):
+            o = int(p["out_off"][k])
+            return buf[o:o + nbytes]
+
+        vals = {PROP_BOOLEAN: lambda: seg(1, nb), PROP_INT64: lambda: seg(1, 8 * n).view(np.int64),
+                PROP_FLOAT: lambda: seg(1, 4 * n).view(np.float32), PROP_STRING: lambda: seg(1, 4 * n).view(np.int32)}[t]()
+        doff = dby = None
+        if t == PROP_STRING and p["out_off"][2] >= 0:
+            doff = seg(2, 4 * (int(p["n_dict"]) + 1)).view(np.int32)
+            dby = seg(3, int(p["dict_bytes"]))
+        return PropertyColumn(self.property_name(c), t, n, seg(0, nb), vals, doff, dby, int(r["n_valid"]))
 
     def geometry_arrays(self, asm: np.ndarray, gres: np.ndarray, c: int):
         """Column c (tile order) of an assembly buffer -> GeoArrowGeometry (raises on its status)."""
@@ -506,6 +583,35 @@ class DeviceBatch:
                                                    self.d_asm.data_ptr(), self.d_gres.data_ptr(), s.cuda_stream),
                "covt_assemble_geometry_device")
 
+    def _prop_buffers(self):
+        import torch
+
+        if getattr(self, "d_props", None) is None:
+            p = self.plan
+            self.d_pdesc = torch.from_numpy(p.pdescs.view(np.uint8).reshape(-1)).to(self.device) \
+                if p.num_property_columns else torch.zeros(PROP_DESC_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+            self.d_props = torch.zeros(max(p.property_bytes, 16), dtype=torch.uint8, device=self.device)
+            self.d_pres = torch.zeros(max(p.num_property_columns, 1) * 2, dtype=torch.int32, device=self.device)
+
+    def materialize_properties(self, stream=None):
+        """Enqueue the property-column materialization (after decode() on the same stream)."""
+        import torch
+
+        self._prop_buffers()
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _raise(lib().covt_materialize_properties_device(self.d_in.data_ptr(), self.d_out.data_ptr(),
+                                                        self.d_res.data_ptr(), self.d_pdesc.data_ptr(),
+                                                        self.plan.num_property_columns, self.d_props.data_ptr(),
+                                                        self.d_pres.data_ptr(), s.cuda_stream),
+               "covt_materialize_properties_device")
+
+    def property_results(self):
+        """(property bytes, results in tile order) copied to the host."""
+        self._prop_buffers()
+        buf = self.d_props.cpu().numpy()[:self.plan.property_bytes]
+        r = self.d_pres.cpu().numpy().view(PROP_RESULT_DTYPE)[:self.plan.num_property_columns]
+        return buf, r[self.plan.props["desc_index"]] if self.plan.num_property_columns else r
+
     def assembly_results(self):
         """(assembly bytes, geometry results in tile order) copied to the host."""
         self._asm_buffers()
@@ -551,12 +657,48 @@ class GeoArrowGeometry:
 
 
 @dataclass
+class PropertyColumn:
+    """One materialized property (sub)column (include/covt.h "Property columns"): Arrow-style validity
+    bitmap (LSB first) + values at feature positions (BOOLEAN: bitmap; INT64: int64; FLOAT: float32;
+    STRING: int32 dictionary index) + dictionary offsets / UTF-8 bytes."""
+    name: str
+    type: int
+    n_features: int
+    validity: np.ndarray
+    values: np.ndarray
+    dict_offsets: Optional[np.ndarray]
+    dict_bytes: Optional[np.ndarray]
+    n_valid: int
+
+    def valid(self, i: int) -> bool:
+        return bool((int(self.validity[i >> 3]) >> (i & 7)) & 1)
+
+    def value(self, i: int):
+        """CovtParser's Optional for feature i: None (empty) or the value."""
+        if not self.valid(i):
+            return None
+        if self.type == PROP_BOOLEAN:
+            return bool((int(self.values[i >> 3]) >> (i & 7)) & 1)
+        if self.type == PROP_INT64:
+            return int(self.values[i])
+        if self.type == PROP_FLOAT:
+            return float(self.values[i])
+        k = int(self.values[i])
+        return bytes(self.dict_bytes[self.dict_offsets[k]:self.dict_offsets[k + 1]]).decode("utf-8")
+
+    def to_list(self):
+        """The List<Optional> of decodePropertyColumn (CovtParser.java:276-354)."""
+        return [self.value(i) for i in range(self.n_features)]
+
+
+@dataclass
 class LayerColumns:
     layer: int
     ids: Optional[np.ndarray]
     geometry: GeometryColumn
     num_bits: int = 0
     column_type: int = 0
+    properties: Optional[dict] = None
 
 
 _GEOM_FIELD = {GEOMETRY_TYPES: "geometryTypes", GEOMETRY_OFFSETS: "geometryOffsets", PART_OFFSETS: "partOffsets",
@@ -568,6 +710,8 @@ def split_layers(plan: Plan, out: np.ndarray, res: np.ndarray, tile: int = 0) ->
     for i in np.nonzero(plan.streams["tile"] == tile)[0]:
         s = plan.streams[i]
         _raise(int(res[i][0]), "stream %d (layer %d, type %d)" % (i, s["layer"], s["stream_type"]))
+        if int(s["column_kind"]) == 2:  # property streams: see Plan.property_column
+            continue
         lc = layers.setdefault(int(s["layer"]), LayerColumns(int(s["layer"]), None, GeometryColumn()))
         arr = plan.stream_array(out, int(i))
         if int(s["column_kind"]) == 0:
@@ -581,12 +725,26 @@ def split_layers(plan: Plan, out: np.ndarray, res: np.ndarray, tile: int = 0) ->
 
 class CovtParser:
     @staticmethod
-    def decode_covt(covt_buffer: bytes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT) -> List[LayerColumns]:
-        """Id + Geometry columns of CovtParser.decodeCovt (CovtParser.java:53-133), decoded on the GPU."""
-        plan = Plan.from_tiles([covt_buffer], fmt, id_mode)
+    def decode_covt(covt_buffer: bytes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT,
+                    properties: bool = False) -> List[LayerColumns]:
+        """CovtParser.decodeCovt (CovtParser.java:53-133) decoded on the GPU: Id + Geometry columns, and with
+        ``properties`` every property column as a PropertyColumn (LayerColumns.properties, by name)."""
+        plan = Plan.from_tiles([covt_buffer], fmt, id_mode, PLAN_PROPERTIES if properties else 0)
         _raise(int(plan.tile_status[0]), "decodeLayerMetadata")
         out, res = plan.decode_host()
-        return split_layers(plan, out, res, 0)
+        layers = split_layers(plan, out, res, 0)
+        if properties and plan.num_property_columns:
+            buf, pres = plan.properties_host()
+            by_layer = {lc.layer: lc for lc in layers}
+            for c in range(plan.num_property_columns):
+                L = int(plan.props["layer"][c])
+                lc = by_layer.setdefault(L, LayerColumns(L, None, GeometryColumn()))
+                if lc.properties is None:
+                    lc.properties = {}
+                col = plan.property_column(buf, pres, c)
+                lc.properties[col.name] = col
+            layers = [by_layer[k] for k in sorted(by_layer)]
+        return layers
 
 
 def version() -> str:

@@ -269,10 +269,10 @@ __device__ __forceinline__ void sink_values(const uint32_t (&vin)[K], int64_t ba
 #pragma unroll
         for (int k = 0; k < K; ++k) r[k] = OP == COVT_OP_VARINT_I32 ? (int32_t)v[k] : zz32(v[k]);
         st32(r);
-    } else if constexpr (OP == COVT_OP_VARINT_I32_AS_I64) {
+    } else if constexpr (OP == COVT_OP_VARINT_I32_AS_I64 || OP == COVT_OP_VARINT_ZZ_I32_AS_I64) {
         int64_t r[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) r[k] = (int64_t)(int32_t)v[k];
+        for (int k = 0; k < K; ++k) r[k] = OP == COVT_OP_VARINT_I32_AS_I64 ? (int64_t)(int32_t)v[k] : (int64_t)zz32(v[k]);
         st64(r);
     } else if constexpr (OP == COVT_OP_VARINT_ZZ_DELTA_I32 || OP == COVT_OP_FPF_ZZ_DELTA_I32 ||
                          OP == COVT_OP_VARINT_ZZ_DELTA_I64) {
@@ -641,20 +641,42 @@ __device__ void run_varint_stream(Ctx& c) {
     auto sink4 = [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
         sink_values<OP, 4>(lo, base, first, count, c.nb, c.out, cr);
     };
-    if constexpr (OP == COVT_OP_VARINT_U64) {
+    if constexpr (OP == COVT_OP_VARINT_U64 || OP == COVT_OP_VARINT_ZZ_S64 || OP == COVT_OP_VARINT_ZZ_DELTA_S64) {
+        // 64-bit LEB128 values (ids; INT_64 property columns in format mode: zigzag64, + running sum)
         int64_t* o = (int64_t*)c.out;
+        uint64_t acc = 0;  // running sum carried across groups (uniform)
         varint_take<MODE_RAW, VAL_U64_STRICT, 4>(
             *c.sm, c.sb, w, pos, c.avail, c.n, false, c.err,
             [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
                 const int32_t s0 = 4 * lane_id() - first;
                 int64_t* p = o + base + 4 * lane_id();
+                uint64_t v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const bool ok = s0 + k >= 0 && s0 + k < count;
+                    v[k] = ok ? (((uint64_t)hi[k] << 32) | lo[k]) : 0ull;
+                    if constexpr (OP != COVT_OP_VARINT_U64) v[k] = (uint64_t)zz64(v[k]);  // zz(0) = 0
+                }
+                if constexpr (OP == COVT_OP_VARINT_ZZ_DELTA_S64) {
+                    uint64_t sacc = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        sacc += v[k];
+                        v[k] = sacc;
+                    }
+                    const uint64_t inc = incl_scan64(sacc);
+                    const uint64_t pre = acc + inc - sacc;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) v[k] += pre;
+                    acc += lane_bcast64(inc, 63);
+                }
                 if (s0 >= 0 && s0 + 4 <= count) {
-                    st_out16((int32_t*)p, make_int4((int)lo[0], (int)hi[0], (int)lo[1], (int)hi[1]));
-                    st_out16((int32_t*)(p + 2), make_int4((int)lo[2], (int)hi[2], (int)lo[3], (int)hi[3]));
+                    st_out16((int32_t*)p, make_int4((int)v[0], (int)(v[0] >> 32), (int)v[1], (int)(v[1] >> 32)));
+                    st_out16((int32_t*)(p + 2), make_int4((int)v[2], (int)(v[2] >> 32), (int)v[3], (int)(v[3] >> 32)));
                 } else {
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        if (s0 + k >= 0 && s0 + k < count) st_out(p + k, (int64_t)(((uint64_t)hi[k] << 32) | lo[k]));
+                        if (s0 + k >= 0 && s0 + k < count) st_out(p + k, (int64_t)v[k]);
                 }
             });
     } else {
@@ -863,7 +885,8 @@ __device__ void run_rle_int(Ctx& c) {
     c.consumed = pos;
 }
 
-// ORC RLE v1 byte reader (RunLengthByteReader); GeometryType.values()[b] range-checked.
+// ORC RLE v1 byte reader (RunLengthByteReader); GeometryType.values()[b] range-checked for
+// COVT_OP_BYTE_RLE_U8 (present / boolean bitsets: COVT_OP_BYTE_RLE_RAW, no check).
 // Same window structure as run_rle_int; a byte-RLE group's length follows from its header byte.
 __device__ void run_rle_byte(Ctx& c) {
     WaveSmem& sm = *c.sm;
@@ -954,7 +977,7 @@ __device__ void run_rle_byte(Ctx& c) {
         pos = woff + pj;
         wave_sync();
     }
-    if (!c.err && bad) c.err = COVT_ERR_BAD_HEADER;
+    if (!c.err && bad && c.op == COVT_OP_BYTE_RLE_U8) c.err = COVT_ERR_BAD_HEADER;  // GeometryType.values()[b]
     c.consumed = pos;
 }
 
@@ -1308,9 +1331,11 @@ __device__ void run_fastpfor(Ctx& c) {
 
 __host__ __device__ constexpr int op_family(int op) {
     return (op >= COVT_OP_FPF_ZZ_DELTA_I32 && op <= COVT_OP_FPF_DELTA_MORTON) ? COVT_FAMILY_FASTPFOR
-           : ((op >= COVT_OP_VARINT_I32 && op <= COVT_OP_VARINT_DELTA_MORTON) || op >= COVT_OP_VARINT_U64)
+           : ((op >= COVT_OP_VARINT_I32 && op <= COVT_OP_VARINT_DELTA_MORTON) ||
+              (op >= COVT_OP_VARINT_U64 && op <= COVT_OP_VARINT_ZZ_DELTA_I64) ||
+              (op >= COVT_OP_VARINT_ZZ_I32_AS_I64 && op <= COVT_OP_VARINT_ZZ_DELTA_S64))
                ? COVT_FAMILY_VARINT
-               : COVT_FAMILY_RLE;  // RLE ops and COVT_OP_NONE (reported as unsupported)
+               : COVT_FAMILY_RLE;  // RLE ops and COVT_OP_NONE / unknown ops (reported as unsupported)
 }
 
 // One wave per descriptor; waves whose descriptor belongs to another family return at once (used
@@ -1351,9 +1376,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(cons
     if (c.n < 0 || c.avail < 0 || c.byte_length < 0) {
         c.err = COVT_ERR_INVALID_ARG;
     } else if (FAM == COVT_FAMILY_RLE) {
-        if (c.op == COVT_OP_BYTE_RLE_U8) { if (c.n > 0) run_rle_byte(c); }
-        else if (c.op == COVT_OP_NONE) c.err = COVT_ERR_UNSUPPORTED_ENCODING;
-        else if (c.n > 0) run_rle_int(c);
+        if (c.op == COVT_OP_BYTE_RLE_U8 || c.op == COVT_OP_BYTE_RLE_RAW) { if (c.n > 0) run_rle_byte(c); }
+        else if (c.op == COVT_OP_RLE_U64 || c.op == COVT_OP_RLE_I32 || c.op == COVT_OP_RLE_S64) { if (c.n > 0) run_rle_int(c); }
+        else c.err = COVT_ERR_UNSUPPORTED_ENCODING;
     } else if (FAM == COVT_FAMILY_VARINT) {
         switch (c.op) {  // one uniform switch per stream; the loops are specialised per op
         case COVT_OP_VARINT_I32: run_varint_stream<COVT_OP_VARINT_I32>(c); break;
@@ -1363,6 +1388,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(cons
         case COVT_OP_VARINT_DELTA_MORTON: run_varint_stream<COVT_OP_VARINT_DELTA_MORTON>(c); break;
         case COVT_OP_VARINT_U64: run_varint_stream<COVT_OP_VARINT_U64>(c); break;
         case COVT_OP_VARINT_I32_AS_I64: run_varint_stream<COVT_OP_VARINT_I32_AS_I64>(c); break;
+        case COVT_OP_VARINT_ZZ_I32_AS_I64: run_varint_stream<COVT_OP_VARINT_ZZ_I32_AS_I64>(c); break;
+        case COVT_OP_VARINT_ZZ_S64: run_varint_stream<COVT_OP_VARINT_ZZ_S64>(c); break;
+        case COVT_OP_VARINT_ZZ_DELTA_S64: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_S64>(c); break;
         default: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I64>(c); break;
         }
     } else {
@@ -1509,7 +1537,7 @@ __device__ void lane_rle_int(LaneBytes& in, int op, int32_t n, uint8_t* out, int
     pk.finish();
     consumed = o;
 }
-__device__ void lane_rle_byte(LaneBytes& in, int32_t n, uint8_t* out, int32_t& err, int32_t& consumed) {
+__device__ void lane_rle_byte(LaneBytes& in, int32_t n, uint8_t* out, bool check, int32_t& err, int32_t& consumed) {
     int32_t o = 0, done = 0;
     bool bad = false;
     Pack16 pk{0, 0, 0, 0, 0, out};
@@ -1538,7 +1566,7 @@ __device__ void lane_rle_byte(LaneBytes& in, int32_t n, uint8_t* out, int32_t& e
         }
     }
     pk.finish();
-    if (bad) err = COVT_ERR_BAD_HEADER;  // GeometryType.values()[b]
+    if (bad && check) err = COVT_ERR_BAD_HEADER;  // GeometryType.values()[b]
     consumed = o;
 }
 
@@ -1559,7 +1587,8 @@ __global__ __launch_bounds__(256) void decode_lane_kernel(const uint8_t* __restr
     LaneBytes lb{in + d.in_off, slots + threadIdx.x, d.avail, 0, -1, 0u};
     lb.load(0);
     if (d.num_values < 0 || d.avail < 0) err = COVT_ERR_INVALID_ARG;
-    else if (d.op == COVT_OP_BYTE_RLE_U8) lane_rle_byte(lb, d.num_values, out + d.out_off, err, consumed);
+    else if (d.op == COVT_OP_BYTE_RLE_U8 || d.op == COVT_OP_BYTE_RLE_RAW)
+        lane_rle_byte(lb, d.num_values, out + d.out_off, d.op == COVT_OP_BYTE_RLE_U8, err, consumed);
     else if (d.op == COVT_OP_RLE_U64 || d.op == COVT_OP_RLE_S64 || d.op == COVT_OP_RLE_I32)
         lane_rle_int(lb, d.op, d.num_values, out + d.out_off, err, consumed);
     else err = COVT_ERR_UNSUPPORTED_ENCODING;

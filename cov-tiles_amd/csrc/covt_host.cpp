@@ -31,6 +31,37 @@ struct RawStream {
     int64_t off;  // tile-relative payload offset
 };
 
+// One property (sub)column found by a walker (CovtParser.decodePropertyColumn, CovtParser.java:276-354).
+// Streams by role 0 present, 1 data, 2 length, 3 dictionary; offsets tile-relative (-1: absent).
+struct PropRaw {
+    int32_t layer, column, type, ctype, nf, lang, name_len, lang_len;
+    int64_t name_off, lang_off;  // tile-relative UTF-8 names (-1: none)
+    int64_t s_off[4];
+    int32_t s_nv[4], s_bl[4], s_enc[4];
+};
+PropRaw prop_init(int32_t layer, int32_t column, int32_t nf) {
+    PropRaw p{};
+    p.layer = layer;
+    p.column = column;
+    p.nf = nf;
+    p.lang = -1;
+    p.name_off = p.lang_off = -1;
+    for (int r = 0; r < 4; ++r) p.s_off[r] = -1;
+    return p;
+}
+void prop_stream(PropRaw& p, int role, int64_t off, int32_t nv, int32_t bl, int32_t enc) {
+    p.s_off[role] = off;
+    p.s_nv[role] = nv;
+    p.s_bl[role] = bl;
+    p.s_enc[role] = enc;
+}
+bool name_is(const uint8_t* t, int64_t off, int64_t len, const char* s) {
+    return (size_t)len == std::strlen(s) && std::memcmp(t + off, s, (size_t)len) == 0;
+}
+// Gen C ColumnDataType (evaluation/file/ColumnDataType.java) / Gen D (converter/ColumnDataType.java)
+int genc_prop_type(int dt) { return dt == 0 ? COVT_PROP_STRING : dt == 1 ? COVT_PROP_FLOAT : dt == 3 ? COVT_PROP_INT64 : dt == 5 ? COVT_PROP_BOOLEAN : -1; }
+int gend_prop_type(int dt) { return dt == 0 ? COVT_PROP_BOOLEAN : dt == 3 ? COVT_PROP_INT64 : dt == 5 ? COVT_PROP_FLOAT : dt == 7 ? COVT_PROP_STRING : -1; }
+
 // LEB128 (metadata of Gen C is written with EncodingUtils.encodeVarints, i.e. 64-bit varints)
 bool rd_uv(const uint8_t* t, size_t len, size_t& o, uint64_t& v) {
     v = 0;
@@ -69,13 +100,13 @@ int genc_stream_type(const uint8_t* s, uint64_t n) {
 
 // Gen C container (all committed fixtures), SURVEY.md Appendix A.1.  Geometry streams are laid
 // out in StreamType order whatever their metadata order; other columns in metadata order.
-int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
+int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::vector<PropRaw>* props) {
     size_t o = 0;
     uint64_t version, nlayers;
     if (!rd_uv(t, len, o, version) || !rd_uv(t, len, o, nlayers)) return COVT_ERR_TRUNCATED;
     if (version != 1) return COVT_ERR_BAD_HEADER;
-    struct SM { int type, enc; int64_t nv, bl; };
-    struct CM { int kind, dtype, ctype; std::vector<SM> s; };
+    struct SM { int type, enc; int64_t nv, bl, name_off, name_len, off; };
+    struct CM { int kind, dtype, ctype; int64_t name_off, name_len; std::vector<SM> s; };
     std::vector<CM> cols;
     for (uint64_t L = 0; L < nlayers; ++L) {
         uint64_t nlen, extent, nfeat, ncols;
@@ -89,6 +120,8 @@ int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
             uint64_t cn, ns;
             if (!rd_uv(t, len, o, cn) || o + cn + 2 > len) return COVT_ERR_TRUNCATED;
             const uint8_t* name = t + o;
+            c.name_off = (int64_t)o;
+            c.name_len = (int64_t)cn;
             o += cn;
             c.dtype = t[o++];
             c.ctype = t[o++];
@@ -101,6 +134,8 @@ int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
                 uint64_t sn, nv, bl;
                 if (!rd_uv(t, len, o, sn) || o + sn > len) return COVT_ERR_TRUNCATED;
                 s.type = genc_stream_type(t + o, sn);
+                s.name_off = (int64_t)o;
+                s.name_len = (int64_t)sn;
                 o += sn;
                 if (!rd_uv(t, len, o, nv) || !rd_uv(t, len, o, bl) || o >= len) return COVT_ERR_TRUNCATED;
                 s.enc = t[o++];
@@ -126,10 +161,50 @@ int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
                     if (c.kind == 0 && s.type == ST_DATA)
                         out.push_back({(int32_t)L, 0, ST_DATA, s.enc, c.ctype, (int32_t)s.nv, (int32_t)s.bl, nb,
                                        (int64_t)o});
+                    s.off = (int64_t)o;
                     o += s.bl;
                 }
             }
             if (o > len) return COVT_ERR_TRUNCATED;
+            if (props && c.kind == 2) {  // streams of a property column in metadata order
+                PropRaw p = prop_init((int32_t)L, (int32_t)(&c - cols.data()), (int32_t)nfeat);
+                p.name_off = c.name_off;
+                p.name_len = (int32_t)c.name_len;
+                p.type = genc_prop_type(c.dtype);
+                p.ctype = c.ctype;
+                if (p.type == COVT_PROP_STRING && c.ctype == 2) {
+                    // LOCALIZED_DICTIONARY: (present_<lang>, <lang>)*, then the shared length + dictionary
+                    const SM *ls = nullptr, *ds = nullptr;
+                    for (const SM& s : c.s) {
+                        if (name_is(t, s.name_off, s.name_len, "length")) ls = &s;
+                        else if (name_is(t, s.name_off, s.name_len, "dictionary")) ds = &s;
+                    }
+                    int32_t lang = 0;
+                    for (const SM& s : c.s) {
+                        if (s.name_len <= 8 || std::memcmp(t + s.name_off, "present_", 8)) continue;
+                        const int64_t ll = s.name_len - 8;
+                        const SM* d = nullptr;
+                        for (const SM& k : c.s)
+                            if (k.name_len == ll && !std::memcmp(t + k.name_off, t + s.name_off + 8, (size_t)ll)) d = &k;
+                        PropRaw q = p;
+                        q.lang = lang++;
+                        q.lang_off = s.name_off + 8;
+                        q.lang_len = (int32_t)ll;
+                        prop_stream(q, 0, s.off, (int32_t)s.nv, (int32_t)s.bl, s.enc);
+                        if (d) prop_stream(q, 1, d->off, (int32_t)d->nv, (int32_t)d->bl, d->enc);
+                        if (ls) prop_stream(q, 2, ls->off, (int32_t)ls->nv, (int32_t)ls->bl, ls->enc);
+                        if (ds) prop_stream(q, 3, ds->off, (int32_t)ds->nv, (int32_t)ds->bl, ds->enc);
+                        props->push_back(q);
+                    }
+                } else {
+                    static const char* kRoles[4] = {"present", "data", "length", "dictionary"};
+                    for (const SM& s : c.s)
+                        for (int r = 0; r < 4; ++r)
+                            if (name_is(t, s.name_off, s.name_len, kRoles[r]))
+                                prop_stream(p, r, s.off, (int32_t)s.nv, (int32_t)s.bl, s.enc);
+                    props->push_back(p);
+                }
+            }
         }
     }
     return o == len ? COVT_OK : COVT_ERR_BAD_HEADER;
@@ -137,11 +212,11 @@ int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
 
 // Gen D container: CovtParser.decodeLayerMetadata (CovtParser.java:574-652) + the column loop
 // of decodeCovt (:56-85).  Streams of a column follow TreeMap<StreamType> order.
-int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
+int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::vector<PropRaw>* props) {
     size_t o = 0;
     int32_t layer = 0;
     struct SM { int enc; int32_t nv, bl; bool have; };
-    struct CM { int kind, dtype, ctype; SM s[12]; };
+    struct CM { int kind, dtype, ctype; int64_t name_off; int32_t name_len; SM s[12]; };
     std::vector<CM> cols;
     while (o < len) {
         const int hdr = t[o++];
@@ -158,6 +233,8 @@ int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
         cols.assign((size_t)ncols, CM{});
         for (int32_t ci = 0; ci < ncols; ++ci) {
             CM& c = cols[(size_t)ci];
+            c.name_off = -1;
+            c.name_len = 0;
             if (optimized || ci == 0) {
                 int32_t cid;
                 if (!rd_j4(t, len, o, cid)) return COVT_ERR_TRUNCATED;
@@ -167,6 +244,8 @@ int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
                 if (!rd_j4(t, len, o, sl) || sl < 0 || o + (size_t)sl > len) return COVT_ERR_TRUNCATED;
                 c.kind = (sl == 2 && !std::memcmp(t + o, "id", 2)) ? 0
                          : (sl == 8 && !std::memcmp(t + o, "geometry", 8)) ? 1 : 2;
+                c.name_off = (int64_t)o;
+                c.name_len = sl;
                 o += (size_t)sl;
             }
             if (o >= len) return COVT_ERR_TRUNCATED;
@@ -189,6 +268,7 @@ int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
         }
         const int nb = nbits_of_extent((uint32_t)extent);
         for (auto& c : cols) {
+            PropRaw p = prop_init(layer, (int32_t)(&c - cols.data()), nfeat);
             for (int type = 0; type < 12; ++type) {
                 const SM& s = c.s[type];
                 if (!s.have) continue;
@@ -196,9 +276,18 @@ int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out) {
                                  (c.kind == 1 && type >= ST_GEOMETRY_TYPES && type <= ST_VERTEX_BUFFER);
                 if (hot) out.push_back({layer, c.kind, type, s.enc, c.ctype, s.nv, s.bl, nb, (int64_t)o});
                 if (s.bl < 0) return COVT_ERR_BAD_HEADER;
+                if (type <= ST_DICTIONARY) prop_stream(p, type, (int64_t)o, s.nv, s.bl, s.enc);
                 o += (size_t)s.bl;
             }
             if (o > len) return COVT_ERR_TRUNCATED;
+            if (props && c.kind == 2) {  // TreeMap<StreamType> order: present, data, length, dictionary
+                p.name_off = c.name_off;
+                p.name_len = c.name_len;
+                p.type = gend_prop_type(c.dtype);
+                p.ctype = c.ctype;
+                if (p.type == COVT_PROP_BOOLEAN) p.s_off[0] = -1;  // Java reads only DATA (:280-291)
+                props->push_back(p);
+            }
         }
         ++layer;
     }
@@ -410,6 +499,10 @@ struct covt_plan {
     std::vector<covt_geom_info> ginfo;   // geometry columns, tile order
     std::vector<covt_geom_desc> gdescs;  // launch order: largest first
     int64_t asm_bytes = 0;
+    std::vector<covt_prop_info> pinfo;   // property (sub)columns, tile order
+    std::vector<uint16_t> pflags;        // their COVT_PROP_* flags
+    std::vector<covt_prop_desc> pdescs;  // launch order: largest first
+    int64_t prop_bytes = 0;
 };
 
 namespace {
@@ -488,6 +581,161 @@ void plan_geometry(covt_plan* p) {
     }
 }
 
+// Property (sub)columns (include/covt.h "Property columns"; CovtParser.decodePropertyColumn
+// :276-354): their present / data / length streams join the decode launch as column_kind 2, and a
+// record remembers where the materialization finds them.  Unsupported shapes get a flag instead of
+// streams, in the order Java would throw: before anything (type, missing streams) or after the
+// present stream was decoded (data encodings, non-dictionary strings).
+void plan_property(covt_plan* p, int32_t t, int64_t tile_off, const PropRaw& q, int id_mode, int64_t& out_off) {
+    covt_prop_info pi{};
+    pi.tile = t;
+    pi.layer = q.layer;
+    pi.column = q.column;
+    pi.type = q.type;
+    pi.column_type = q.ctype;
+    pi.n_features = q.nf;
+    pi.n_data = q.s_nv[1];
+    pi.n_dict = q.s_off[3] >= 0 ? std::max(q.s_nv[3], 0) : 0;
+    pi.lang = q.lang;
+    pi.name_len = q.name_len;
+    pi.lang_len = q.lang_len;
+    pi.dict_bytes = q.s_off[3] >= 0 ? std::max(q.s_bl[3], 0) : 0;
+    pi.name_off = q.name_off >= 0 ? tile_off + q.name_off : -1;
+    pi.lang_off = q.lang_off >= 0 ? tile_off + q.lang_off : -1;
+    for (int k = 0; k < 3; ++k) pi.stream[k] = -1;
+    uint16_t fl = 0;
+    const int32_t nf = std::max(q.nf, 0), nb = (int32_t)(((int64_t)nf + 7) / 8);
+    const bool early_unsup = q.type < 0 || q.s_off[1] < 0 || (q.type != COVT_PROP_BOOLEAN && q.s_off[0] < 0) ||
+                             q.nf < 0 || q.s_nv[1] < 0;
+    int data_op = COVT_OP_NONE, data_elem = 0;
+    int64_t data_n = 0;
+    bool late_unsup = false;
+    if (!early_unsup) {
+        switch (q.type) {
+        case COVT_PROP_BOOLEAN:
+            if (q.s_off[0] >= 0) fl |= COVT_PROP_DENSE_BOOL;
+            data_op = COVT_OP_BYTE_RLE_RAW;
+            data_elem = 1;
+            data_n = (q.s_off[0] >= 0) ? ((int64_t)q.s_nv[1] + 7) / 8 : nb;
+            break;
+        case COVT_PROP_INT64:
+            data_elem = 8;
+            data_n = q.s_nv[1];
+            if (q.s_enc[1] == ENC_RLE) data_op = COVT_OP_RLE_S64;
+            else if (q.s_enc[1] == 2) data_op = id_mode == COVT_ID_JAVA ? COVT_OP_VARINT_ZZ_I32_AS_I64 : COVT_OP_VARINT_ZZ_S64;
+            else if (q.s_enc[1] == ENC_VARINT_DELTA_ZZ)
+                data_op = id_mode == COVT_ID_JAVA ? COVT_OP_VARINT_ZZ_DELTA_I64 : COVT_OP_VARINT_ZZ_DELTA_S64;
+            else late_unsup = true;
+            break;
+        case COVT_PROP_FLOAT:  // no decode: the kernel reads the little-endian words from the input
+            if ((int64_t)q.s_nv[1] * 4 > q.s_bl[1]) fl |= COVT_PROP_DATA_SHORT;
+            break;
+        default:  // STRING
+            if ((q.ctype != 1 && q.ctype != 2) || q.s_off[2] < 0 || q.s_off[3] < 0 || q.s_enc[1] != ENC_RLE ||
+                q.s_nv[3] < 0) {
+                late_unsup = true;
+            } else {
+                data_op = COVT_OP_RLE_I32;  // (int) data[dataCounter++]
+                data_elem = 4;
+                data_n = q.s_nv[1];
+                if (q.lang <= 0) fl |= COVT_PROP_DICT_OWNER;
+            }
+            break;
+        }
+    }
+    if (early_unsup) fl |= COVT_PROP_UNSUPPORTED;
+    if (late_unsup) fl |= COVT_PROP_UNSUPPORTED_LATE;
+    auto add = [&](int role, int op, int64_t n, int elem) {
+        covt_stream_info si{};
+        si.tile = t;
+        si.layer = q.layer;
+        si.column_kind = 2;
+        si.stream_type = role;
+        si.encoding = q.s_enc[role];
+        si.column_type = q.ctype;
+        si.num_values = q.s_nv[role];
+        si.byte_length = q.s_bl[role];
+        si.op = op;
+        si.elem_bytes = elem;
+        si.in_off = tile_off + q.s_off[role];
+        si.out_elems = n;
+        si.out_off = out_off;
+        out_off = align16(out_off + n * elem);
+        p->out_payload += n * elem;
+        si.desc_index = (int32_t)n;  // temporarily: values to decode
+        pi.stream[role] = (int32_t)p->info.size();
+        p->info.push_back(si);
+    };
+    if (!early_unsup) {
+        if (q.s_off[0] >= 0) add(0, COVT_OP_BYTE_RLE_RAW, nb, 1);  // decodeByteRle(numBytes), :296
+        if (!late_unsup && data_op != COVT_OP_NONE) add(1, data_op, data_n, data_elem);
+        if (!late_unsup && q.type == COVT_PROP_STRING) add(2, COVT_OP_RLE_I32, q.s_nv[3], 4);  // lengths: n_dict
+    }
+    if (q.type == COVT_PROP_FLOAT && q.s_off[1] >= 0) pi.out_off[1] = tile_off + q.s_off[1];  // temporarily
+    if (q.type == COVT_PROP_STRING && q.s_off[3] >= 0) pi.out_off[3] = tile_off + q.s_off[3];  // temporarily
+    p->pinfo.push_back(pi);
+    p->pflags.push_back(fl);
+}
+
+// Output slices of the property columns and the launch-ordered descriptors (after the decode
+// streams got their launch rows).  A localized column's sub-columns share the owner's dictionary.
+void plan_property_layout(covt_plan* p) {
+    int64_t off = 0;
+    const size_t np = p->pinfo.size();
+    std::vector<int64_t> in_float(np), in_dict(np);
+    size_t owner = 0;
+    for (size_t k = 0; k < np; ++k) {
+        covt_prop_info& pi = p->pinfo[k];
+        in_float[k] = pi.out_off[1];
+        in_dict[k] = pi.out_off[3];
+        const int64_t n = pi.n_features > 0 ? pi.n_features : 0, nb = (n + 7) / 8;
+        const int64_t vbytes = pi.type == COVT_PROP_BOOLEAN ? nb : pi.type == COVT_PROP_INT64 ? 8 * n : 4 * n;
+        pi.out_off[0] = off;
+        off = align16(off + nb);
+        pi.out_off[1] = off;
+        off = align16(off + vbytes);
+        if (pi.type == COVT_PROP_STRING && (p->pflags[k] & COVT_PROP_DICT_OWNER)) {
+            owner = k;
+            pi.out_off[2] = off;
+            off = align16(off + 4 * ((int64_t)pi.n_dict + 1));
+            pi.out_off[3] = off;
+            off = align16(off + pi.dict_bytes);
+        } else if (pi.type == COVT_PROP_STRING && pi.lang > 0 && owner < k && p->pinfo[owner].tile == pi.tile &&
+                   p->pinfo[owner].layer == pi.layer && p->pinfo[owner].column == pi.column) {
+            pi.out_off[2] = p->pinfo[owner].out_off[2];
+            pi.out_off[3] = p->pinfo[owner].out_off[3];
+        } else {
+            pi.out_off[2] = pi.out_off[3] = -1;
+        }
+    }
+    p->prop_bytes = off;
+    std::vector<size_t> order(np);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+        return (int64_t)p->pinfo[a].n_features + p->pinfo[a].n_dict > (int64_t)p->pinfo[b].n_features + p->pinfo[b].n_dict;
+    });
+    p->pdescs.resize(np);
+    for (size_t k = 0; k < np; ++k) {
+        covt_prop_info& pi = p->pinfo[order[k]];
+        covt_prop_desc d{};
+        auto s_out = [&](int role) { return pi.stream[role] >= 0 ? p->info[(size_t)pi.stream[role]].out_off : -1; };
+        d.present_off = s_out(0);
+        d.data_off = pi.type == COVT_PROP_FLOAT ? in_float[order[k]] : s_out(1);
+        d.length_off = s_out(2);
+        d.dict_in_off = pi.type == COVT_PROP_STRING ? in_dict[order[k]] : -1;
+        for (int m = 0; m < 4; ++m) d.out_off[m] = pi.out_off[m];
+        for (int m = 0; m < 3; ++m) d.res[m] = pi.stream[m] >= 0 ? p->info[(size_t)pi.stream[m]].desc_index : -1;
+        d.n_features = pi.n_features;
+        d.n_data = pi.n_data;
+        d.n_dict = pi.n_dict;
+        d.dict_bytes = pi.dict_bytes;
+        d.type = (int16_t)pi.type;
+        d.flags = (int16_t)p->pflags[order[k]];
+        pi.desc_index = (int32_t)k;
+        p->pdescs[k] = d;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -522,10 +770,9 @@ int covt_decode_byte_rle(const uint8_t* buf, size_t buf_len, int32_t n, int32_t*
                          uint8_t* out) {
     if (!pos) return COVT_ERR_INVALID_ARG;
     const int32_t p0 = *pos;
-    int st = stream_call(buf, buf_len, pos, COVT_OP_BYTE_RLE_U8, n, 0, out, 1, (size_t)std::max(n, 0));
-    // decodeByteRle(..., byteLength) advances by the metadata byteLength (DecodingUtils.java:286);
-    // the GeometryType range check belongs to decodeGeometryColumn, not to this method
-    if (st == COVT_ERR_BAD_HEADER) st = COVT_OK;
+    // the GeometryType range check belongs to decodeGeometryColumn, not to this method: raw bytes
+    int st = stream_call(buf, buf_len, pos, COVT_OP_BYTE_RLE_RAW, n, 0, out, 1, (size_t)std::max(n, 0));
+    // decodeByteRle(..., byteLength) advances by the metadata byteLength (DecodingUtils.java:286)
     if (!st) *pos = p0 + byte_length;
     return st;
 }
@@ -552,7 +799,13 @@ int covt_decode_fastpfor_delta_morton_codes(const uint8_t* buf, size_t buf_len, 
 
 int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
                      int32_t n_tiles, int32_t format, int32_t id_mode, covt_plan** out) {
+    return covt_plan_create_ex(bytes, tile_offsets, tile_sizes, n_tiles, format, id_mode, 0u, out);
+}
+
+int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
+                        int32_t n_tiles, int32_t format, int32_t id_mode, uint32_t flags, covt_plan** out) {
     if (!out || n_tiles < 0 || (n_tiles && (!bytes || !tile_offsets || !tile_sizes))) return COVT_ERR_INVALID_ARG;
+    if (flags & ~COVT_PLAN_PROPERTIES) return COVT_ERR_INVALID_ARG;
     if (format != COVT_FORMAT_GENC && format != COVT_FORMAT_GEND) return COVT_ERR_INVALID_ARG;
     auto* p = new covt_plan();
     p->n_tiles = n_tiles;
@@ -561,12 +814,15 @@ int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const u
     p->tile_off.assign(tile_offsets, tile_offsets + n_tiles);
     p->tile_size.assign(tile_sizes, tile_sizes + n_tiles);
     std::vector<RawStream> rs;
+    std::vector<PropRaw> props;
     int64_t out_off = 0;
     for (int32_t t = 0; t < n_tiles; ++t) {
         rs.clear();
         const uint8_t* tile = bytes + tile_offsets[t];
-        const int st = format == COVT_FORMAT_GENC ? walk_genc(tile, (size_t)tile_sizes[t], rs)
-                                                  : walk_gend(tile, (size_t)tile_sizes[t], rs);
+        props.clear();
+        std::vector<PropRaw>* pp = (flags & COVT_PLAN_PROPERTIES) ? &props : nullptr;
+        const int st = format == COVT_FORMAT_GENC ? walk_genc(tile, (size_t)tile_sizes[t], rs, pp)
+                                                  : walk_gend(tile, (size_t)tile_sizes[t], rs, pp);
         p->tile_status[(size_t)t] = st;
         if (st) continue;
         for (const RawStream& s : rs) {
@@ -596,6 +852,7 @@ int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const u
             si.desc_index = (int32_t)nvals;  // temporarily: values to decode
             p->info.push_back(si);
         }
+        for (const PropRaw& q : props) plan_property(p, t, (int64_t)tile_offsets[t], q, id_mode, out_off);
     }
     p->out_bytes = out_off;
     // launch order: largest streams first so the long poles start early (static wave->stream map)
@@ -634,6 +891,7 @@ int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const u
         si.desc_index = (int32_t)k;
     }
     plan_geometry(p);
+    plan_property_layout(p);
     *out = p;
     return COVT_OK;
 }
@@ -875,6 +1133,70 @@ int covt_plan_assemble_host(const covt_plan* p, const uint8_t* bytes, uint64_t n
     if (st == COVT_OK)
         for (size_t k = 0; k < nc; ++k) host_gres[k] = gres[(size_t)p->ginfo[k].desc_index];
     for (void* q : {(void*)d_in, (void*)d_out, (void*)d_asm, (void*)d_desc, (void*)d_res, (void*)d_gdesc, (void*)d_gres})
+        if (q) (void)hipFree(q);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+int64_t covt_plan_num_property_columns(const covt_plan* p) { return p ? (int64_t)p->pinfo.size() : 0; }
+int64_t covt_plan_property_bytes(const covt_plan* p) { return p ? p->prop_bytes : 0; }
+int covt_plan_property_columns(const covt_plan* p, covt_prop_info* out) {
+    if (!p || (!out && !p->pinfo.empty())) return COVT_ERR_INVALID_ARG;
+    if (!p->pinfo.empty()) std::memcpy(out, p->pinfo.data(), p->pinfo.size() * sizeof(covt_prop_info));
+    return COVT_OK;
+}
+int covt_plan_property_descs(const covt_plan* p, covt_prop_desc* out) {
+    if (!p || (!out && !p->pdescs.empty())) return COVT_ERR_INVALID_ARG;
+    if (!p->pdescs.empty()) std::memcpy(out, p->pdescs.data(), p->pdescs.size() * sizeof(covt_prop_desc));
+    return COVT_OK;
+}
+
+// Whole plan on the current device: tile bytes H2D as they lie, decode, property materialization,
+// copies back on one stream.
+int covt_plan_properties_host(const covt_plan* p, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_props,
+                              covt_prop_result* host_pres) {
+    if (!p || (!bytes && n_bytes) || (!host_props && p->prop_bytes) || (!host_pres && !p->pinfo.empty()))
+        return COVT_ERR_INVALID_ARG;
+    for (int32_t t = 0; t < p->n_tiles; ++t)
+        if (p->tile_off[(size_t)t] + p->tile_size[(size_t)t] > n_bytes) return COVT_ERR_INVALID_ARG;
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return COVT_ERR_DEVICE;
+    const size_t nd = p->descs.size(), nc = p->pdescs.size();
+    uint8_t *d_in = nullptr, *d_out = nullptr, *d_props = nullptr;
+    covt_stream_desc* d_desc = nullptr;
+    covt_stream_result* d_res = nullptr;
+    covt_prop_desc* d_pdesc = nullptr;
+    covt_prop_result* d_pres = nullptr;
+    int st = COVT_OK;
+    auto chk = [&](hipError_t e) { if (e != hipSuccess && st == COVT_OK) st = COVT_ERR_DEVICE; };
+    chk(hipMalloc(&d_in, (size_t)n_bytes + COVT_INPUT_PADDING));
+    chk(hipMalloc(&d_out, (size_t)std::max<int64_t>(p->out_bytes, 16)));
+    chk(hipMalloc(&d_props, (size_t)std::max<int64_t>(p->prop_bytes, 16)));
+    chk(hipMalloc(&d_desc, std::max<size_t>(nd, 1) * sizeof(covt_stream_desc)));
+    chk(hipMalloc(&d_res, std::max<size_t>(nd, 1) * sizeof(covt_stream_result)));
+    chk(hipMalloc(&d_pdesc, std::max<size_t>(nc, 1) * sizeof(covt_prop_desc)));
+    chk(hipMalloc(&d_pres, std::max<size_t>(nc, 1) * sizeof(covt_prop_result)));
+    std::vector<covt_prop_result> pres(nc);
+    if (st == COVT_OK) {
+        if (n_bytes) chk(hipMemcpyAsync(d_in, bytes, (size_t)n_bytes, hipMemcpyHostToDevice, s));
+        chk(hipMemsetAsync(d_in + n_bytes, 0, COVT_INPUT_PADDING, s));
+        if (nd) chk(hipMemcpyAsync(d_desc, p->descs.data(), nd * sizeof(covt_stream_desc), hipMemcpyHostToDevice, s));
+        if (nc)
+            chk(hipMemcpyAsync(d_pdesc, p->pdescs.data(), nc * sizeof(covt_prop_desc), hipMemcpyHostToDevice, s));
+        if (st == COVT_OK && ((uintptr_t)d_in & 15)) st = COVT_ERR_DEVICE;
+        if (st == COVT_OK) st = launch_grouped(d_in, d_desc, p->fam_counts, d_out, d_res, s);
+        if (st == COVT_OK)
+            st = covt_materialize_properties_device(d_in, d_out, d_res, d_pdesc, (int64_t)nc, d_props, d_pres, s);
+        if (st == COVT_OK && p->prop_bytes)
+            chk(hipMemcpyAsync(host_props, d_props, (size_t)p->prop_bytes, hipMemcpyDeviceToHost, s));
+        if (st == COVT_OK && nc)
+            chk(hipMemcpyAsync(pres.data(), d_pres, nc * sizeof(covt_prop_result), hipMemcpyDeviceToHost, s));
+        chk(hipStreamSynchronize(s));
+    }
+    if (st == COVT_OK)
+        for (size_t k = 0; k < nc; ++k) host_pres[k] = pres[(size_t)p->pinfo[k].desc_index];
+    for (void* q : {(void*)d_in, (void*)d_out, (void*)d_props, (void*)d_desc, (void*)d_res, (void*)d_pdesc,
+                    (void*)d_pres})
         if (q) (void)hipFree(q);
     (void)hipStreamDestroy(s);
     return st;

@@ -20,7 +20,8 @@ int covt_op_family_of(int op);
 constexpr int32_t kLaneMaxValues = 256;
 constexpr int32_t kLaneMaxBytes = 256;
 inline bool lane_stream(int op, int32_t num_values, int32_t byte_length) {
-    return (op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_S64 || op == COVT_OP_RLE_I32) &&
+    return (op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_BYTE_RLE_RAW || op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_S64 ||
+            op == COVT_OP_RLE_I32) &&
            num_values >= 0 && num_values <= kLaneMaxValues && byte_length >= 0 && byte_length <= kLaneMaxBytes;
 }
 inline int desc_family(const covt_stream_desc& d) {

@@ -1,0 +1,248 @@
+// covt_props.hip -- gfx950 property-column materialization (include/covt.h "Property columns";
+// SURVEY.md §8(f) row 3): the decoded present / data / length streams of a property column become
+// an Arrow-style column (validity bitmap, values at feature positions, dictionary offsets + bytes).
+//
+// Reference: CovtParser.decodePropertyColumn (CovtParser.java:276-354) walks the features of a layer
+// once and takes the next decoded data value (j++) for every feature whose present bit is set;
+// string columns look the value up in the dictionary built by getStringDictionary (:367-377).  Here
+// one wave64 materializes one (sub)column, 256 features per step, four consecutive features per
+// lane: the lane's four validity bits give it a count, a DPP wave prefix sum (plus the carried total
+// of the earlier steps) gives every present feature its rank j in the dense data stream, and the
+// value is gathered from there.  A dictionary owner first turns the decoded length stream into Arrow
+// offsets (exclusive scan, 256 per step) and copies the dictionary bytes (16 bytes per lane).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "covt.h"
+#include "covt_internal.h"
+#include "covt_wave.h"
+
+namespace covt {
+
+constexpr int kPropWaves = 4;  // independent waves (columns) per workgroup
+
+typedef __attribute__((address_space(1))) const uint8_t gp_u8;
+typedef __attribute__((address_space(1))) const uint32_t gp_u32;
+typedef __attribute__((address_space(1))) const int32_t gp_i32;
+typedef __attribute__((address_space(1))) const int64_t gp_i64;
+typedef int32_t pi32x4 __attribute__((ext_vector_type(4)));
+
+// 4 bytes at any address of the input (the batch input is padded past its last byte)
+__device__ __forceinline__ uint32_t pld_le32(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const gp_u32* q = (const gp_u32*)(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+
+// bits f .. f+3 (f % 4 == 0) of an LSB-first bitmap, clipped to n
+__device__ __forceinline__ uint32_t nibble(const uint8_t* bm, int32_t f, int32_t n) {
+    if (f >= n) return 0u;
+    const uint32_t v = (((const gp_u8*)bm)[f >> 3] >> (f & 4)) & 0xfu;
+    return n - f >= 4 ? v : (v & ((1u << (n - f)) - 1u));
+}
+__device__ __forceinline__ uint32_t all_valid(int32_t f, int32_t n) {
+    return f >= n ? 0u : (n - f >= 4 ? 0xfu : ((1u << (n - f)) - 1u));
+}
+
+// Arrow offsets of the dictionary (exclusive scan of the int32 lengths) and its bytes.  Returns a status.
+__device__ int32_t dictionary(const uint8_t* in, const uint8_t* dec, const covt_prop_desc& d, uint8_t* outb,
+                              bool write) {
+    const int l = lane_id();
+    const int32_t nd = d.n_dict;
+    const gp_i32* lens = (const gp_i32*)(dec + d.length_off);
+    int32_t* offs = (int32_t*)(outb + d.out_off[2]);
+    bool neg = false;
+    for (int32_t q = 0; q < nd; q += 256) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int32_t j = q + 4 * l + k;
+            neg |= j < nd && lens[j] < 0;
+        }
+    }
+    if (__ballot(neg)) return COVT_ERR_COUNT_MISMATCH;  // decodeString with a negative length
+    uint64_t run = 0;                                    // uniform: bytes before this step
+    if (!write) {
+        for (int32_t q = 0; q < nd; q += 256) {
+            uint64_t s = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int32_t j = q + 4 * l + k;
+                s += j < nd ? (uint64_t)lens[j] : 0ull;
+            }
+            run += lane_bcast64(incl_scan64(s), 63);
+        }
+        return run > (uint64_t)d.dict_bytes ? COVT_ERR_TRUNCATED : COVT_OK;
+    }
+    for (int32_t q = 0; q < nd; q += 256) {
+        uint64_t x[4], s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int32_t j = q + 4 * l + k;
+            x[k] = j < nd ? (uint64_t)lens[j] : 0ull;
+            s += x[k];
+        }
+        const uint64_t inc = incl_scan64(s);
+        uint64_t e = run + inc - s;
+        int32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            o[k] = (int32_t)e;
+            e += x[k];
+        }
+        const int32_t i0 = q + 4 * l;
+        if (i0 + 4 <= nd) {
+            *(pi32x4*)(offs + i0) = pi32x4{o[0], o[1], o[2], o[3]};
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (i0 + k < nd) offs[i0 + k] = o[k];
+        }
+        run += lane_bcast64(inc, 63);
+    }
+    if (run > (uint64_t)d.dict_bytes) return COVT_ERR_TRUNCATED;  // strings past the dictionary stream
+    if (l == 0) offs[nd] = (int32_t)run;
+    const uint8_t* src = in + d.dict_in_off;
+    uint8_t* dst = outb + d.out_off[3];
+    for (int32_t b = 16 * l; b < d.dict_bytes; b += 1024) {
+        if (b + 16 <= d.dict_bytes) {
+            *(pi32x4*)(dst + b) = pi32x4{(int32_t)pld_le32(src + b), (int32_t)pld_le32(src + b + 4),
+                                         (int32_t)pld_le32(src + b + 8), (int32_t)pld_le32(src + b + 12)};
+        } else {
+            for (int32_t i = b; i < d.dict_bytes; ++i) dst[i] = ((const gp_u8*)src)[i];
+        }
+    }
+    return COVT_OK;
+}
+
+__device__ void materialize(const uint8_t* in, const uint8_t* dec, const covt_stream_result* dres,
+                            const covt_prop_desc& d, uint8_t* outb, covt_prop_result& res) {
+    const int l = lane_id();
+    res.status = COVT_OK;
+    res.n_valid = 0;
+    // Java's order: unsupported shapes, the present stream, encodings rejected after it, the data and
+    // length streams, a short float stream, the dictionary, then the feature loop
+    if (d.flags & COVT_PROP_UNSUPPORTED) { res.status = COVT_ERR_UNSUPPORTED_ENCODING; return; }
+    int32_t st[3];
+    for (int k = 0; k < 3; ++k) st[k] = d.res[k] >= 0 ? uni(((const gp_i32*)dres)[2 * d.res[k]]) : COVT_OK;
+    // every sub-column checks its dictionary lengths; the owner also writes the dictionary, whatever
+    // its own present / data streams hold (the other languages of a localized column share it)
+    int32_t dst = COVT_OK;
+    if (d.type == COVT_PROP_STRING && d.res[2] >= 0 && st[2] == COVT_OK)
+        dst = dictionary(in, dec, d, outb, (d.flags & COVT_PROP_DICT_OWNER) != 0);
+    for (int k = 0; k < 3; ++k) {
+        if (st[k]) { res.status = st[k]; return; }
+        if (k == 0 && (d.flags & COVT_PROP_UNSUPPORTED_LATE)) { res.status = COVT_ERR_UNSUPPORTED_ENCODING; return; }
+    }
+    if (d.flags & COVT_PROP_DATA_SHORT) { res.status = COVT_ERR_TRUNCATED; return; }
+    if (dst) { res.status = dst; return; }
+    const int32_t n = d.n_features, dn = d.n_data;
+    const uint8_t* pres = d.present_off >= 0 ? dec + d.present_off : nullptr;
+    uint8_t* vout = outb + d.out_off[0];
+    uint8_t* xout = outb + d.out_off[1];
+    const bool dense_bool = (d.flags & COVT_PROP_DENSE_BOOL) != 0;
+    uint32_t carry = 0;  // present features before this step (uniform)
+    bool bad = false;
+    for (int32_t f0 = 0; f0 < n; f0 += 256) {
+        const int32_t f = f0 + 4 * l;
+        const uint32_t vb = pres ? nibble(pres, f, n) : all_valid(f, n);
+        const uint32_t cnt = (uint32_t)__popc(vb);
+        const uint32_t inc = incl_scan(cnt);
+        uint32_t j = carry + inc - cnt;  // rank of this lane's first present feature
+        carry += lane_bcast(inc, 63);
+        // lanes 2m and 2m+1 hold the two nibbles of byte m of the step
+        const uint32_t vhi = lane_next(vb);
+        if (!(l & 1) && f < n) vout[f >> 3] = (uint8_t)(vb | (vhi << 4));
+        if (d.type == COVT_PROP_BOOLEAN) {
+            uint32_t xb;
+            if (dense_bool) {  // Gen C: the bitset holds the present values only
+                xb = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const bool p = (vb >> k) & 1u;
+                    const bool ok = p && j < (uint32_t)dn;
+                    bad |= p && !ok;
+                    if (ok) xb |= ((((const gp_u8*)(dec + d.data_off))[j >> 3] >> (j & 7u)) & 1u) << k;
+                    j += p ? 1u : 0u;
+                }
+            } else {  // one bit per feature (CovtParser.java:280-291)
+                xb = nibble(dec + d.data_off, f, n) & vb;
+            }
+            const uint32_t xhi = lane_next(xb);
+            if (!(l & 1) && f < n) xout[f >> 3] = (uint8_t)(xb | (xhi << 4));
+        } else if (d.type == COVT_PROP_INT64) {
+            int64_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool p = (vb >> k) & 1u;
+                const bool ok = p && j < (uint32_t)dn;
+                bad |= p && !ok;
+                v[k] = ok ? ((const gp_i64*)(dec + d.data_off))[j] : 0;
+                j += p ? 1u : 0u;
+            }
+            int64_t* o = (int64_t*)xout + f;
+            if (f + 4 <= n) {
+                *(pi32x4*)o = pi32x4{(int32_t)v[0], (int32_t)(v[0] >> 32), (int32_t)v[1], (int32_t)(v[1] >> 32)};
+                *(pi32x4*)(o + 2) = pi32x4{(int32_t)v[2], (int32_t)(v[2] >> 32), (int32_t)v[3], (int32_t)(v[3] >> 32)};
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (f + k < n) o[k] = v[k];
+            }
+        } else {  // FLOAT (little-endian words of the input) or STRING (int32 dictionary indices)
+            const bool flt = d.type == COVT_PROP_FLOAT;
+            int32_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool p = (vb >> k) & 1u;
+                const bool ok = p && j < (uint32_t)dn;
+                bad |= p && !ok;
+                int32_t x = 0;
+                if (ok) x = flt ? (int32_t)pld_le32(in + d.data_off + 4 * (int64_t)j) : ((const gp_i32*)(dec + d.data_off))[j];
+                bad |= ok && !flt && (uint32_t)x >= (uint32_t)d.n_dict;  // dictionaryData[index]
+                v[k] = x;
+                j += p ? 1u : 0u;
+            }
+            int32_t* o = (int32_t*)xout + f;
+            if (f + 4 <= n) {
+                *(pi32x4*)o = pi32x4{v[0], v[1], v[2], v[3]};
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (f + k < n) o[k] = v[k];
+            }
+        }
+    }
+    if (__ballot(bad)) { res.status = COVT_ERR_COUNT_MISMATCH; return; }
+    res.n_valid = (int32_t)carry;
+}
+
+__global__ __launch_bounds__(64 * kPropWaves) void props_kernel(const uint8_t* __restrict__ in,
+                                                                const uint8_t* __restrict__ dec,
+                                                                const covt_stream_result* __restrict__ dres,
+                                                                const covt_prop_desc* __restrict__ descs,
+                                                                int64_t n_cols, uint8_t* __restrict__ outb,
+                                                                covt_prop_result* __restrict__ pres) {
+    const int w = threadIdx.x >> 6;
+    const int64_t c = uni64((int64_t)blockIdx.x * kPropWaves + w);
+    if (c >= n_cols) return;
+    const covt_prop_desc d = descs[c];
+    covt_prop_result r;
+    materialize(in, dec, dres, d, outb, r);
+    if (lane_id() == 0) pres[c] = r;
+}
+
+}  // namespace covt
+
+extern "C" int covt_materialize_properties_device(const uint8_t* d_in, const uint8_t* d_decoded,
+                                                  const covt_stream_result* d_res, const covt_prop_desc* d_pdesc,
+                                                  int64_t n_columns, uint8_t* d_props, covt_prop_result* d_pres,
+                                                  void* hip_stream) {
+    if (n_columns < 0 || (n_columns && (!d_in || !d_decoded || !d_res || !d_pdesc || !d_props || !d_pres)))
+        return COVT_ERR_INVALID_ARG;
+    if (n_columns == 0) return COVT_OK;
+    const int64_t blocks = (n_columns + covt::kPropWaves - 1) / covt::kPropWaves;
+    if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
+    hipLaunchKernelGGL(covt::props_kernel, dim3((unsigned)blocks), dim3(64 * covt::kPropWaves), 0,
+                       (hipStream_t)hip_stream, d_in, d_decoded, d_res, d_pdesc, n_columns, d_props, d_pres);
+    return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
+}

@@ -37,6 +37,30 @@ __device__ __forceinline__ uint32_t incl_scan(uint32_t x) {
     return x;
 }
 
+// inclusive prefix sum of 64-bit values over the 64 lanes (same DPP sequence, carry by hand)
+__device__ __forceinline__ uint64_t incl_scan64(uint64_t x) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+#define COVT_SCAN64_STEP(ctrl, rmask)                                                             \
+    {                                                                                             \
+        const uint32_t l2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, ctrl, rmask, 0xf, false); \
+        const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, ctrl, rmask, 0xf, false); \
+        const uint32_t s = lo + l2;                                                               \
+        hi = hi + h2 + (s < lo ? 1u : 0u);                                                        \
+        lo = s;                                                                                   \
+    }
+    COVT_SCAN64_STEP(0x111, 0xf)  // row_shr:1
+    COVT_SCAN64_STEP(0x112, 0xf)  // row_shr:2
+    COVT_SCAN64_STEP(0x114, 0xf)  // row_shr:4
+    COVT_SCAN64_STEP(0x118, 0xf)  // row_shr:8
+    COVT_SCAN64_STEP(0x142, 0xa)  // row_bcast:15
+    COVT_SCAN64_STEP(0x143, 0xc)  // row_bcast:31
+#undef COVT_SCAN64_STEP
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t lane_bcast64(uint64_t x, int src) {
+    return ((uint64_t)lane_bcast((uint32_t)(x >> 32), src) << 32) | lane_bcast((uint32_t)x, src);
+}
+
 // inclusive running maximum over the 64 lanes (same DPP sequence as incl_scan)
 __device__ __forceinline__ uint32_t incl_max_scan(uint32_t x) {
     x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1

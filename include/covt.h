@@ -108,7 +108,12 @@ enum covt_op {
     COVT_OP_VARINT_U64 = 13,            /* Id VARINT, format truth: 64-bit LEB128 -> int64 */
     COVT_OP_VARINT_I32_AS_I64 = 14,     /* Id VARINT, Java: decodeVarint then (long) */
     COVT_OP_VARINT_ZZ_DELTA_I64 = 15,   /* Id enc 4, Java: decodeZigZagDeltaVarint then (long) */
-    COVT_OP_COUNT = 16
+    COVT_OP_BYTE_RLE_RAW = 16,          /* decodeByteRle -> uint8, no value check (present / boolean bitsets) */
+    COVT_OP_VARINT_ZZ_I32_AS_I64 = 17,  /* INT_64 VARINT_ZIG_ZAG, Java: decodeZigZagVarint then (long)
+                                           (CovtParser.java:304-307) */
+    COVT_OP_VARINT_ZZ_S64 = 18,         /* INT_64 VARINT_ZIG_ZAG, format truth: 64-bit LEB128, zigzag64 */
+    COVT_OP_VARINT_ZZ_DELTA_S64 = 19,   /* INT_64 VARINT_DELTA_ZIG_ZAG, format truth: 64-bit, int64 running sum */
+    COVT_OP_COUNT = 20
 };
 
 /* Codec families: each has its own kernel (register / LDS footprint), launched concurrently. */
@@ -263,6 +268,93 @@ int covt_assemble_geometry_device(const uint8_t* d_decoded, const covt_stream_re
  * host_asm: covt_plan_assembly_bytes bytes; host_gres: one result per column in tile order. */
 int covt_plan_assemble_host(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_asm,
                             covt_geom_result* host_gres);
+
+/* ---------------------------------------------------------------------------
+ * Property columns: the GPU replacement for
+ * CovtParser.decodePropertyColumn (CovtParser.java:276-354) and getStringDictionary (:367-377).
+ * A plan created with COVT_PLAN_PROPERTIES also plans every property column: its present / data /
+ * length streams join the decode launch (column_kind 2 in covt_stream_info, stream_type = the
+ * StreamType PRESENT 0 / DATA 1 / LENGTH 2), and covt_materialize_properties_device turns them into
+ * Arrow-style columns, one per (sub)column:
+ *
+ *   validity[ceil(n/8)]   present bits, LSB first (BitSet.valueOf); all set without a present stream
+ *   values                BOOLEAN: bitmap[ceil(n/8)];  INT64: int64[n];  FLOAT: float32[n];
+ *                         STRING: int32 dictionary index [n]  (absent slots hold 0)
+ *   dict_offsets[n_dict+1], dict_bytes   STRING: Arrow string offsets + UTF-8 bytes of the dictionary
+ *
+ * Java's List<Optional> per feature is validity bit i ? value i : empty.  Localized dictionary
+ * columns (Gen C LOCALIZED_DICTIONARY, which Java rejects with IllegalArgumentException) are
+ * decoded as format truth: one STRING sub-column per language stream, sharing the column's
+ * dictionary (written once, by the sub-column flagged COVT_PROP_DICT_OWNER).  Gen C boolean columns
+ * with a present stream store only the present values' bits (data numValues = present count).
+ * INT_64 varint columns follow id_mode: COVT_ID_JAVA = the 4-byte-capped int decode widened to long
+ * (CovtParser.java:304-312), COVT_ID_FORMAT = 64-bit zigzag varints (what the writer emits).
+ * Statuses follow Java's order: a failed source stream first, then the dictionary (negative length
+ * -> COUNT_MISMATCH, strings past the dictionary stream -> TRUNCATED), then the feature loop
+ * (a present bit without a data value or a dictionary index out of range -> COUNT_MISMATCH).
+ * ------------------------------------------------------------------------- */
+#define COVT_PLAN_PROPERTIES 0x1u /* covt_plan_create_ex flag */
+
+#define COVT_PROP_BOOLEAN 0
+#define COVT_PROP_INT64 1
+#define COVT_PROP_FLOAT 2
+#define COVT_PROP_STRING 3
+
+#define COVT_PROP_DICT_OWNER 0x1  /* this sub-column writes the dictionary offsets and bytes */
+#define COVT_PROP_DENSE_BOOL 0x2  /* BOOLEAN data holds the present values' bits only (Gen C) */
+#define COVT_PROP_UNSUPPORTED 0x4 /* data type / missing stream Java rejects: UNSUPPORTED_ENCODING */
+#define COVT_PROP_DATA_SHORT 0x8  /* FLOAT data stream shorter than numValues * 4: TRUNCATED */
+#define COVT_PROP_UNSUPPORTED_LATE 0x10 /* encoding Java rejects after decoding the present stream */
+
+/* One device-resident property (sub)column entry (96 bytes). */
+typedef struct covt_prop_desc {
+    int64_t present_off; /* decode-output byte offset of the present bitset (-1: none, all valid) */
+    int64_t data_off;    /* decode-output offset of the dense data (BOOLEAN bits, INT64 int64, STRING int32
+                            indices); FLOAT: INPUT offset of the little-endian floats */
+    int64_t length_off;  /* STRING: decode-output offset of the int32 dictionary lengths */
+    int64_t dict_in_off; /* STRING: input offset of the dictionary bytes */
+    int64_t out_off[4];  /* validity, values, dictionary offsets, dictionary bytes (16-byte aligned) */
+    int32_t res[3];      /* decode-result rows of the present, data, length streams (-1: none) */
+    int32_t n_features, n_data, n_dict, dict_bytes;
+    int16_t type, flags; /* COVT_PROP_*, COVT_PROP_* flags */
+} covt_prop_desc;
+
+typedef struct covt_prop_result {
+    int32_t status;  /* COVT_OK, a source stream's status, or a COVT_ERR_* of the materialization */
+    int32_t n_valid; /* features with a value */
+} covt_prop_result;
+
+/* Host-visible property (sub)column record of a plan, in tile order (112 bytes). */
+typedef struct covt_prop_info {
+    int32_t tile, layer, column, type;          /* type: COVT_PROP_* or -1 (unsupported data type) */
+    int32_t column_type, n_features, n_data, n_dict;
+    int32_t lang, name_len, lang_len, dict_bytes; /* lang: language index of a localized sub-column, -1 */
+    int32_t stream[3];                          /* tile-order stream index of present, data, length (-1) */
+    int32_t desc_index;                         /* row in the launch-ordered property descriptors */
+    int64_t name_off, lang_off;                 /* UTF-8 column / language names in the batch input (-1) */
+    int64_t out_off[4];
+} covt_prop_info;
+
+/* covt_plan_create plus flags (COVT_PLAN_PROPERTIES). */
+int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
+                        int32_t n_tiles, int32_t format, int32_t id_mode, uint32_t flags, covt_plan** out);
+int64_t covt_plan_num_property_columns(const covt_plan* plan);
+int64_t covt_plan_property_bytes(const covt_plan* plan); /* size of the property output buffer */
+int covt_plan_property_columns(const covt_plan* plan, covt_prop_info* out); /* tile order */
+int covt_plan_property_descs(const covt_plan* plan, covt_prop_desc* out);   /* launch order (largest first) */
+
+/* Materialize every property column on `hip_stream` after the decode launch of the same plan:
+ * d_in the batch input (dictionary bytes and floats are read from it), d_decoded / d_res the decode
+ * output and launch-order results, d_pdesc the property descriptors, d_props an output buffer of
+ * covt_plan_property_bytes bytes, d_pres n_columns results (in d_pdesc order).  Asynchronous. */
+int covt_materialize_properties_device(const uint8_t* d_in, const uint8_t* d_decoded, const covt_stream_result* d_res,
+                                       const covt_prop_desc* d_pdesc, int64_t n_columns, uint8_t* d_props,
+                                       covt_prop_result* d_pres, void* hip_stream);
+
+/* Convenience: H2D + decode + property materialization + D2H of the whole plan on the current device.
+ * host_props: covt_plan_property_bytes bytes; host_pres: one result per (sub)column in tile order. */
+int covt_plan_properties_host(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_props,
+                              covt_prop_result* host_pres);
 
 /* Library info */
 const char* covt_version(void);

@@ -86,6 +86,56 @@ def test_plan_matches_oracle_walk(covt, oracle, fmt_mode):
     assert ends.max() <= plan.output_bytes
 
 
+@pytest.mark.parametrize("id_mode", [0, 1])
+def test_plan_properties_match_oracle_walk(covt, oracle, id_mode):
+    """COVT_PLAN_PROPERTIES: one record per property (sub)column in the oracle's walk order, its decode
+    streams (column_kind 2) on the right payload bytes with CovtParser.decodePropertyColumn's ops, and
+    disjoint 16-byte aligned output slices; Id/Geometry streams unchanged."""
+    paths = tile_paths()
+    tiles = [open(p, "rb").read() for p in paths]
+    plan = covt.Plan.from_tiles(tiles, 0, id_mode, covt.PLAN_PROPERTIES)
+    plain = covt.Plan.from_tiles(tiles, 0, id_mode)
+    st = plan.streams
+    assert np.array_equal(st[st["column_kind"] != 2][["tile", "layer", "stream_type", "op", "in_off"]],
+                          plain.streams[["tile", "layer", "stream_type", "op", "in_off"]])
+    P = plan.props
+    k = 0
+    for t, p in enumerate(paths):
+        ost, props = oracle.walk_properties(tiles[t])
+        assert ost == 0
+        for q in props:
+            r = P[k]
+            assert (r["tile"], r["layer"], r["column"], r["lang"], r["n_features"]) == \
+                   (t, q.layer, q.column, q.lang, q.n_features)
+            assert plan.property_name(k) == oracle.prop_name(tiles[t], q)
+            for role in range(3):
+                si = int(r["stream"][role])
+                if si < 0:
+                    continue
+                s = st[si]
+                assert s["column_kind"] == 2 and s["stream_type"] == role
+                assert s["in_off"] == int(plan.offsets[t]) + q.s_off[role]
+                if role == 0:
+                    assert s["op"] == covt.OP_BYTE_RLE_RAW and s["out_elems"] == (q.n_features + 7) // 8
+                elif q.type == covt.PROP_INT64:
+                    assert s["op"] == {5: covt.OP_RLE_S64,
+                                       2: (covt.OP_VARINT_ZZ_S64, covt.OP_VARINT_ZZ_I32_AS_I64)[id_mode],
+                                       4: (covt.OP_VARINT_ZZ_DELTA_S64, covt.OP_VARINT_ZZ_DELTA_I64)[id_mode]}[q.s_enc[1]]
+                elif q.type == covt.PROP_STRING:
+                    assert s["op"] == covt.OP_RLE_I32
+            k += 1
+    assert k == plan.num_property_columns
+    owners = plan.pdescs["flags"] & covt.PROP_DICT_OWNER != 0
+    assert owners.sum() >= 2500
+    ends = []
+    for r, d in zip(P, plan.pdescs[P["desc_index"]]):
+        assert (d["out_off"] == r["out_off"]).all()
+        for m in range(4):
+            if r["out_off"][m] >= 0:
+                assert r["out_off"][m] % 16 == 0 and r["out_off"][m] <= plan.property_bytes
+    assert plan.property_bytes > 0
+
+
 def test_plan_op_selection_follows_covtparser_dispatch(covt):
     """CovtParser.decodeGeometryColumn (:392-511) / decodedIds (:552-572) dispatch table."""
     t = open(os.path.join(ROOT, "tests", "golden", "tiles", "omt", "5_16_20.covt"), "rb").read()
