@@ -347,10 +347,10 @@ int oracle_decode_property(const uint8_t* tile, size_t len, const oracle_prop* p
             return ORC_OK;
         }
         /* Gen C with a present stream: the data bitset holds the present values only (numValues bits) */
-        if (nv > dn) return ORC_ERR_COUNT;
         const int32_t db = (int32_t)(((int64_t)dn + 7) / 8);
         uint8_t* dense = (uint8_t*)calloc((size_t)db + 1, 1);
         st = byte_rle_bits(tile, len, doff, dbl, db, dense);
+        if (!st && nv > dn) st = ORC_ERR_COUNT;
         memset(v, 0, (size_t)nbytes);
         for (int32_t i = 0, j = 0; !st && i < n; i++)
             if (bit(validity, i)) {
@@ -360,7 +360,8 @@ int oracle_decode_property(const uint8_t* tile, size_t len, const oracle_prop* p
         free(dense);
         return st;
     }
-    if (nv > dn) return ORC_ERR_COUNT; /* decodedDataColumn[j++] past its end */
+    /* Java decodes the data stream first; a present bit without a data value then fails in the
+       feature loop (decodedDataColumn[j++] past its end): statuses in that order */
     if (p->type == ORACLE_PROP_INT64) {
         int64_t* dense = (int64_t*)malloc(sizeof(int64_t) * (size_t)(dn > 0 ? dn : 1));
         int32_t pos = 0, cons = 0;
@@ -387,6 +388,7 @@ int oracle_decode_property(const uint8_t* tile, size_t len, const oracle_prop* p
         } else {
             st = ORC_ERR_UNSUPPORTED; /* "The specified encoding for the long data stream is not supported." */
         }
+        if (!st && nv > dn) st = ORC_ERR_COUNT;
         int64_t* v = (int64_t*)values;
         for (int32_t i = 0, j = 0; !st && i < n; i++) v[i] = bit(validity, i) ? dense[j++] : 0;
         free(dense);
@@ -394,6 +396,7 @@ int oracle_decode_property(const uint8_t* tile, size_t len, const oracle_prop* p
     }
     if (p->type == ORACLE_PROP_FLOAT) { /* decodeFloatsLE (:446-453) */
         if ((int64_t)dn * 4 > dbl) return ORC_ERR_TRUNCATED;
+        if (nv > dn) return ORC_ERR_COUNT;
         uint32_t* v = (uint32_t*)values;
         for (int32_t i = 0, j = 0; i < n; i++) {
             uint32_t w = 0;
@@ -421,22 +424,24 @@ int oracle_decode_property(const uint8_t* tile, size_t len, const oracle_prop* p
             st = oracle_decode_rle(tile + lo, (size_t)lbl, nd, &pos, 0, lens, &cons);
         }
     }
-    if (!st) { /* getStringDictionary: (int) lengths, decodeString back to back */
+    if (!st) { /* getStringDictionary: (int) lengths, decodeString back to back; a negative length
+                  fails (COUNT), then strings running past the dictionary stream (TRUNCATED) */
         int64_t acc = 0;
         dict_offsets[0] = 0;
+        for (int32_t i = 0; i < nd && !st; i++)
+            if ((int32_t)lens[i] < 0) st = ORC_ERR_COUNT;
         for (int32_t i = 0; i < nd && !st; i++) {
-            const int32_t l = (int32_t)lens[i];
-            if (l < 0) st = ORC_ERR_COUNT;
-            acc += l;
-            if (acc > p->s_bl[P_ST_DICTIONARY]) st = ORC_ERR_TRUNCATED;
+            acc += (int32_t)lens[i];
             dict_offsets[i + 1] = (int32_t)acc;
         }
+        if (!st && acc > p->s_bl[P_ST_DICTIONARY]) st = ORC_ERR_TRUNCATED;
         if (!st) {
             const int64_t so = p->s_off[P_ST_DICTIONARY];
             if ((uint64_t)so + (uint64_t)p->s_bl[P_ST_DICTIONARY] > len) st = ORC_ERR_TRUNCATED;
             else memcpy(dict_bytes, tile + so, (size_t)p->s_bl[P_ST_DICTIONARY]);
         }
     }
+    if (!st && nv > dn) st = ORC_ERR_COUNT;
     int32_t* v = (int32_t*)values;
     for (int32_t i = 0, j = 0; !st && i < n; i++) {
         if (bit(validity, i)) {
