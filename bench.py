@@ -197,6 +197,64 @@ def assembly_leg(batch, plan, stream, args, dist, torch, dev):
                          "kernel": "covt::assemble_kernel (one wave per geometry column)"}}
 
 
+def properties_leg(picks, args, dist, torch, dev, covt, stream):
+    """property columns of the same batch (a second plan with COVT_PLAN_PROPERTIES).
+    Times the decode launch over every stream (Id + Geometry + property streams) and the property
+    materialization kernel on its own; not part of `value`."""
+    plan = covt.Plan.from_tiles([t for _, t in picks], covt.FORMAT_GENC, args.id_mode, covt.PLAN_PROPERTIES)
+    batch = covt.DeviceBatch(plan, dev)
+
+    def timed(fn):
+        for _ in range(max(args.warmup, 1)):
+            fn()
+        torch.cuda.synchronize(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        for s, e in ev:
+            s.record(stream)
+            fn()
+            e.record(stream)
+        torch.cuda.synchronize(dev)
+        return float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    with torch.cuda.stream(stream):
+        ms_dec = timed(lambda: batch.decode(stream))
+        ms_mat = timed(lambda: batch.materialize_properties(stream))
+    _, pres = batch.property_results()
+    if (pres["status"] != 0).any():
+        raise RuntimeError("property materialization failed on %d columns" % int((pres["status"] != 0).sum()))
+    st = plan.streams
+    pst = st[st["column_kind"] == 2]
+    P = plan.props
+    n = P["n_features"].astype(np.int64)
+    nb = (n + 7) // 8
+    typ = P["type"]
+    vbytes = np.where(typ == covt.PROP_BOOLEAN, nb, np.where(typ == covt.PROP_INT64, 8 * n, 4 * n))
+    owner = (plan.pdescs["flags"][P["desc_index"]] & covt.PROP_DICT_OWNER) != 0
+    nd = P["n_dict"].astype(np.int64)
+    db = P["dict_bytes"].astype(np.int64)
+    nv = pres["n_valid"].astype(np.int64)
+    dense_elem = np.where(typ == covt.PROP_INT64, 8, np.where(typ == covt.PROP_BOOLEAN, 0, 4))
+    # algorithmic bytes of the materialization: present bitmap + dense values read (+ lengths and
+    # dictionary bytes read per string sub-column), validity + values written (+ offsets and dictionary
+    # bytes by the owner)
+    rd = nb.sum() + (nv * dense_elem).sum() + (4 * nd + np.where(owner, db, 0)).sum() * 1
+    wr = nb.sum() + vbytes.sum() + np.where(owner, 4 * (nd + 1) + db, 0).sum()
+    alg = int(rd + wr)
+    achieved = alg / (ms_mat * 1e-3) / 1e9
+    return {"ms_decode_all_streams": round(ms_dec, 4), "ms_materialize": round(ms_mat, 4),
+            "columns": plan.num_property_columns, "streams_all": plan.num_streams,
+            "stream_bytes_all": int(plan.in_bytes),
+            "note": "stream_bytes_all = Id + Geometry + property stream bytes (present/data/length decoded, "
+                    "float data and dictionary bytes read in place)",
+            "gbps_raw_all_streams": round(plan.in_bytes / (ms_dec * 1e-3) / 1e9, 2),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": alg,
+                         "kernel": "covt::props_kernel (one wave per property (sub)column)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -210,6 +268,7 @@ def main():
     ap.add_argument("--id-mode", type=int, default=0)
     ap.add_argument("--no-assemble", action="store_true", help="skip the geometry-assembly leg")
     ap.add_argument("--e2e-reps", type=int, default=3, help="end-to-end (PCIe-inclusive) reps; 0 skips")
+    ap.add_argument("--no-props", action="store_true", help="skip the property-column leg")
     args = ap.parse_args()
 
     import torch
@@ -271,6 +330,9 @@ def main():
     asm_line = None
     if not args.no_assemble and plan.num_geometry_columns:
         asm_line = assembly_leg(batch, plan, stream, args, dist, torch, dev)
+    props_line = None
+    if not args.no_props:
+        props_line = properties_leg(picks, args, dist, torch, dev, covt, stream)
 
     stats = torch.tensor([wall, float(plan.in_bytes), float(plan.vertices), float(plan.out_bytes), kern_ms],
                          dtype=torch.float64, device=dev)
@@ -330,6 +392,8 @@ def main():
         }
         if asm_line is not None:
             line["assembly"] = asm_line
+        if props_line is not None:
+            line["properties"] = props_line
         if e2e is not None:
             line["end_to_end"] = e2e
         line["host_plan_ms"] = round(t_plan * 1e3, 1)  # covt_plan_create metadata walk (+ packing), host

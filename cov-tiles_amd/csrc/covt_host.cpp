@@ -661,6 +661,7 @@ void plan_property(covt_plan* p, int32_t t, int64_t tile_off, const PropRaw& q, 
         si.out_elems = n;
         si.out_off = out_off;
         out_off = align16(out_off + n * elem);
+        p->in_bytes += q.s_bl[role];
         p->out_payload += n * elem;
         si.desc_index = (int32_t)n;  // temporarily: values to decode
         pi.stream[role] = (int32_t)p->info.size();
@@ -671,6 +672,8 @@ void plan_property(covt_plan* p, int32_t t, int64_t tile_off, const PropRaw& q, 
         if (!late_unsup && data_op != COVT_OP_NONE) add(1, data_op, data_n, data_elem);
         if (!late_unsup && q.type == COVT_PROP_STRING) add(2, COVT_OP_RLE_I32, q.s_nv[3], 4);  // lengths: n_dict
     }
+    if (!early_unsup && q.type == COVT_PROP_FLOAT) p->in_bytes += q.s_bl[1];  // read in place
+    if (!early_unsup && (fl & COVT_PROP_DICT_OWNER)) p->in_bytes += q.s_bl[3];
     if (q.type == COVT_PROP_FLOAT && q.s_off[1] >= 0) pi.out_off[1] = tile_off + q.s_off[1];  // temporarily
     if (q.type == COVT_PROP_STRING && q.s_off[3] >= 0) pi.out_off[3] = tile_off + q.s_off[3];  // temporarily
     p->pinfo.push_back(pi);
