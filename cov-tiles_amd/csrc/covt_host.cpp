@@ -210,6 +210,21 @@ int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::ve
     return o == len ? COVT_OK : COVT_ERR_BAD_HEADER;
 }
 
+// Bytes an ORC byte-RLE stream of n values starting at tile offset o occupies (control bytes walked,
+// values skipped); -1 if it runs past the tile.
+int32_t byte_rle_length(const uint8_t* t, size_t len, size_t o, int32_t n) {
+    size_t q = o;
+    int64_t done = 0;
+    while (done < n) {
+        if (q >= len) return -1;
+        const uint32_t c = t[q++];
+        if (c < 0x80u) { done += c + 3; q += 1; }
+        else { done += 0x100 - c; q += 0x100 - c; }
+        if (q > len) return -1;
+    }
+    return (int32_t)(q - o);
+}
+
 // Gen D container: CovtParser.decodeLayerMetadata (CovtParser.java:574-652) + the column loop
 // of decodeCovt (:56-85).  Streams of a column follow TreeMap<StreamType> order.
 int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::vector<PropRaw>* props) {
@@ -269,14 +284,23 @@ int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::ve
         const int nb = nbits_of_extent((uint32_t)extent);
         for (auto& c : cols) {
             PropRaw p = prop_init(layer, (int32_t)(&c - cols.data()), nfeat);
+            if (c.kind == 2 && c.dtype != 0) {
+                // implicit present stream: its bytes lead the column without metadata
+                // (CovtConverter.addNamedColumnMetadata skips PRESENT, :452-458; CovtParser.java:296 reads
+                // ceil(numFeatures/8) bytes with the 3-argument decodeByteRle); BOOLEAN (0) has none
+                const int32_t pl = byte_rle_length(t, len, o, nfeat < 0 ? 0 : (int32_t)(((int64_t)nfeat + 7) / 8));
+                if (pl < 0) return COVT_ERR_TRUNCATED;
+                prop_stream(p, 0, (int64_t)o, nfeat, pl, 7);
+                o += (size_t)pl;
+            }
             for (int type = 0; type < 12; ++type) {
                 const SM& s = c.s[type];
-                if (!s.have) continue;
+                if (!s.have || (c.kind == 2 && type == ST_PRESENT)) continue;
                 const bool hot = (c.kind == 0 && type == ST_DATA) ||
                                  (c.kind == 1 && type >= ST_GEOMETRY_TYPES && type <= ST_VERTEX_BUFFER);
                 if (hot) out.push_back({layer, c.kind, type, s.enc, c.ctype, s.nv, s.bl, nb, (int64_t)o});
                 if (s.bl < 0) return COVT_ERR_BAD_HEADER;
-                if (type <= ST_DICTIONARY) prop_stream(p, type, (int64_t)o, s.nv, s.bl, s.enc);
+                if (type > ST_PRESENT && type <= ST_DICTIONARY) prop_stream(p, type, (int64_t)o, s.nv, s.bl, s.enc);
                 o += (size_t)s.bl;
             }
             if (o > len) return COVT_ERR_TRUNCATED;
@@ -285,7 +309,6 @@ int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::ve
                 p.name_len = c.name_len;
                 p.type = gend_prop_type(c.dtype);
                 p.ctype = c.ctype;
-                if (p.type == COVT_PROP_BOOLEAN) p.s_off[0] = -1;  // Java reads only DATA (:280-291)
                 props->push_back(p);
             }
         }

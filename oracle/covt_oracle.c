@@ -901,6 +901,22 @@ static int walk_genc(const uint8_t* t, size_t len, oracle_stream* out, int32_t m
     return ORC_OK;
 }
 
+/* Gen D property columns carry an implicit present stream: the writer puts its bytes first in the column
+ * but no metadata for it (CovtConverter.addNamedColumnMetadata skips StreamType.PRESENT, :452-458), and
+ * decodePropertyColumn reads it with the 3-argument decodeByteRle (CovtParser.java:296): ceil(numFeatures/8)
+ * bytes, advancing by the length of their re-encoding (DecodingUtils.java:290-306).  BOOLEAN columns have
+ * none (:280-291).  Gen D ColumnDataType: BOOLEAN = 0 (converter/ColumnDataType.java). */
+int oracle_gend_present_length(const uint8_t* t, size_t len, int64_t off, int32_t n_features, int32_t* length) {
+    const int32_t nb = (int32_t)(((int64_t)(n_features > 0 ? n_features : 0) + 7) / 8);
+    if (off < 0 || (uint64_t)off > len) return ORC_ERR_TRUNCATED;
+    uint8_t* v = (uint8_t*)malloc((size_t)nb + 1);
+    int32_t pos = 0, cons = 0;
+    int st = oracle_decode_byte_rle(t + off, len - (size_t)off, nb, &pos, 0, v, &cons);
+    if (!st) *length = (int32_t)oracle_encode_byte_rle(v, nb, NULL, 0); /* getByteRleChunkSize */
+    free(v);
+    return st;
+}
+
 /* Gen D: CovtParser.decodeLayerMetadata :574-652 + the column loop of decodeCovt :56-85 */
 static int walk_gend(const uint8_t* t, size_t len, oracle_stream* out, int32_t max_out, int32_t* n_out) {
     int64_t o = 0;
@@ -958,8 +974,13 @@ static int walk_gend(const uint8_t* t, size_t len, oracle_stream* out, int32_t m
         }
         for (int32_t c = 0; c < ncols; c++) {
             dmeta* cm = &cols[c];
+            if (cm->kind == 2 && cm->dtype != 0) { /* implicit present stream (oracle_gend_present_length) */
+                int32_t pl = 0;
+                if ((st = oracle_gend_present_length(t, len, o, nfeat, &pl))) goto fail;
+                o += pl;
+            }
             for (int type = 0; type < 12; type++) { /* TreeMap<StreamType> order */
-                if (!cm->have[type]) continue;
+                if (!cm->have[type] || (cm->kind == 2 && type == ST_PRESENT)) continue;
                 int is_hot = (cm->kind == 0 && type == ST_DATA) ||
                              (cm->kind == 1 && type >= ST_GEOMETRY_TYPES && type <= ST_VERTEX_BUFFER);
                 if (is_hot) {

@@ -114,6 +114,10 @@ int oracle_walk_tile(const uint8_t* tile, size_t len, int format, oracle_stream*
 #define ORACLE_ID_FORMAT 0 /* format truth: VARINT -> 64-bit LEB128, enc 4 -> unsigned RLE */
 #define ORACLE_ID_JAVA 1   /* CovtParser.decodedIds verbatim (4-byte varint cap, enc 4 zigzag-delta) */
 
+/* Byte length of the implicit present stream of a Gen D property column starting at tile offset off
+ * (Java: re-encoding length of its ceil(n/8) decoded bytes). */
+int oracle_gend_present_length(const uint8_t* tile, size_t len, int64_t off, int32_t n_features, int32_t* length);
+
 /* Output element type/count of a stream's decode (1,4,8 bytes) */
 int oracle_stream_output(const oracle_stream* s, int id_mode, int32_t* elem_bytes, int64_t* n_elems);
 /* Decode one walked stream with CovtParser's dispatch (decodeGeometryColumn :392-511,

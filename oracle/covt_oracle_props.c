@@ -268,15 +268,20 @@ static int walk_props_gend(const uint8_t* t, size_t len, oracle_prop* out, int32
             p.name_len = cm->name_len;
             p.type = gend_prop_type(cm->dtype);
             p.column_type = cm->ctype;
+            if (cm->kind == 2 && cm->dtype != 0) { /* implicit present stream: no metadata (see covt_oracle.h) */
+                int32_t pl = 0;
+                if ((st = oracle_gend_present_length(t, len, o, nfeat, &pl))) goto fail;
+                set_stream(&p, P_ST_PRESENT, o, nfeat, pl, 7);
+                o += pl;
+            }
             for (int type = 0; type < 12; type++) { /* TreeMap<StreamType> order */
-                if (!cm->have[type]) continue;
+                if (!cm->have[type] || (cm->kind == 2 && type == P_ST_PRESENT)) continue;
                 if (cm->bl[type] < 0) { st = ORC_ERR_HEADER; goto fail; }
                 if (type <= P_ST_DICTIONARY) set_stream(&p, type, o, cm->nv[type], cm->bl[type], cm->enc[type]);
                 o += cm->bl[type];
             }
             if ((uint64_t)o > len) { st = ORC_ERR_TRUNCATED; goto fail; }
             if (cm->kind != 2) continue;
-            if (p.type == ORACLE_PROP_BOOLEAN) p.s_off[P_ST_PRESENT] = -1; /* Java reads only DATA (:280-291) */
             put(out, max_out, &cnt, &p);
         }
         free(cols);
