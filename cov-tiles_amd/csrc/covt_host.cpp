@@ -133,7 +133,8 @@ int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::ve
             for (auto& s : c.s) {
                 uint64_t sn, nv, bl;
                 if (!rd_uv(t, len, o, sn) || o + sn > len) return COVT_ERR_TRUNCATED;
-                s.type = genc_stream_type(t + o, sn);
+                // stream names matter for Id / Geometry columns; property streams only when planned
+                s.type = (c.kind != 2 || props) ? genc_stream_type(t + o, sn) : -1;
                 s.name_off = (int64_t)o;
                 s.name_len = (int64_t)sn;
                 o += sn;
@@ -839,19 +840,53 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
     p->tile_status.assign((size_t)n_tiles, 0);
     p->tile_off.assign(tile_offsets, tile_offsets + n_tiles);
     p->tile_size.assign(tile_sizes, tile_sizes + n_tiles);
-    std::vector<RawStream> rs;
-    std::vector<PropRaw> props;
+    // 1. container walks, tiles split over host threads (metadata only, independent per tile)
+    struct Chunk {
+        int32_t t0 = 0, t1 = 0;
+        std::vector<RawStream> rs;
+        std::vector<PropRaw> props;
+        std::vector<int32_t> rs_end, props_end;  // per tile of the chunk: end index in rs / props
+    };
+    const int32_t n_thr = (int32_t)std::max<int64_t>(
+        1, std::min<int64_t>({(int64_t)std::thread::hardware_concurrency(), 16, ((int64_t)n_tiles + 63) / 64}));
+    std::vector<Chunk> chunks((size_t)n_thr);
+    auto walk_chunk = [&](Chunk* c) {
+        for (int32_t t = c->t0; t < c->t1; ++t) {
+            const uint8_t* tile = bytes + tile_offsets[t];
+            const size_t r0 = c->rs.size(), q0 = c->props.size();
+            std::vector<PropRaw>* pp = (flags & COVT_PLAN_PROPERTIES) ? &c->props : nullptr;
+            const int st = format == COVT_FORMAT_GENC ? walk_genc(tile, (size_t)tile_sizes[t], c->rs, pp)
+                                                      : walk_gend(tile, (size_t)tile_sizes[t], c->rs, pp);
+            p->tile_status[(size_t)t] = st;
+            if (st) {  // a failed tile contributes nothing
+                c->rs.resize(r0);
+                c->props.resize(q0);
+            }
+            c->rs_end.push_back((int32_t)c->rs.size());
+            c->props_end.push_back((int32_t)c->props.size());
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int32_t k = 0; k < n_thr; ++k) {
+            chunks[(size_t)k].t0 = (int32_t)((int64_t)n_tiles * k / n_thr);
+            chunks[(size_t)k].t1 = (int32_t)((int64_t)n_tiles * (k + 1) / n_thr);
+            if (k + 1 < n_thr) th.emplace_back(walk_chunk, &chunks[(size_t)k]);
+        }
+        walk_chunk(&chunks[(size_t)n_thr - 1]);
+        for (auto& x : th) x.join();
+    }
+    // 2. stream records and output slices in tile order
     int64_t out_off = 0;
-    for (int32_t t = 0; t < n_tiles; ++t) {
-        rs.clear();
-        const uint8_t* tile = bytes + tile_offsets[t];
-        props.clear();
-        std::vector<PropRaw>* pp = (flags & COVT_PLAN_PROPERTIES) ? &props : nullptr;
-        const int st = format == COVT_FORMAT_GENC ? walk_genc(tile, (size_t)tile_sizes[t], rs, pp)
-                                                  : walk_gend(tile, (size_t)tile_sizes[t], rs, pp);
-        p->tile_status[(size_t)t] = st;
-        if (st) continue;
-        for (const RawStream& s : rs) {
+    size_t total = 0;
+    for (const Chunk& c : chunks) total += c.rs.size();
+    p->info.reserve(total);
+    for (const Chunk& c : chunks) {
+      int32_t r = 0, q = 0;
+      for (int32_t t = c.t0; t < c.t1; ++t) {
+        const int32_t re = c.rs_end[(size_t)(t - c.t0)], qe = c.props_end[(size_t)(t - c.t0)];
+        for (; r < re; ++r) {
+            const RawStream& s = c.rs[(size_t)r];
             int op, elem;
             int64_t nvals, out_elems;
             choose_op(s, id_mode, op, nvals, elem, out_elems);
@@ -878,29 +913,33 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
             si.desc_index = (int32_t)nvals;  // temporarily: values to decode
             p->info.push_back(si);
         }
-        for (const PropRaw& q : props) plan_property(p, t, (int64_t)tile_offsets[t], q, id_mode, out_off);
+        for (; q < qe; ++q) plan_property(p, t, (int64_t)tile_offsets[t], c.props[(size_t)q], id_mode, out_off);
+      }
     }
     p->out_bytes = out_off;
-    // launch order: largest streams first so the long poles start early (static wave->stream map)
+    // 3. launch order: grouped by family (the lane family also by op, for op-uniform waves), largest
+    // streams first inside a family so the long poles start early (static wave->stream map); one
+    // precomputed key per stream, ties in tile order
     const size_t ns = p->info.size();
+    struct Key {
+        uint64_t k;
+        uint32_t i;
+    };
+    std::vector<Key> keys(ns);
+    for (size_t i = 0; i < ns; ++i) {
+        const auto& s = p->info[i];
+        const bool lane = lane_stream(s.op, s.desc_index, s.byte_length);
+        const uint64_t fam = lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);
+        const uint64_t cost = std::min<uint64_t>((uint64_t)((int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4),
+                                                 (1ull << 48) - 1);
+        keys[i] = Key{(fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost), (uint32_t)i};
+    }
+    std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) { return a.k != b.k ? a.k < b.k : a.i < b.i; });
     std::vector<int64_t> order(ns);
-    std::iota(order.begin(), order.end(), 0);
-    auto cost = [&](int64_t i) {
-        const auto& s = p->info[(size_t)i];
-        return (int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4;
-    };
-    auto fam = [&](int64_t i) {
-        const auto& s = p->info[(size_t)i];
-        return lane_stream(s.op, s.desc_index, s.byte_length) ? COVT_FAMILY_LANE : covt_op_family_of(s.op);
-    };
-    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-        const int fa = fam(a), fb = fam(b);
-        if (fa != fb) return fa < fb;
-        if (fa == COVT_FAMILY_LANE && p->info[(size_t)a].op != p->info[(size_t)b].op)  // op-uniform waves
-            return p->info[(size_t)a].op < p->info[(size_t)b].op;
-        return cost(a) > cost(b);
-    });
-    for (int64_t i : order) p->fam_counts[fam(i)]++;
+    for (size_t k = 0; k < ns; ++k) {
+        order[k] = keys[k].i;
+        p->fam_counts[keys[k].k >> 60]++;
+    }
     p->descs.resize(ns);
     for (size_t k = 0; k < ns; ++k) {
         covt_stream_info& si = p->info[(size_t)order[k]];

@@ -25,9 +25,11 @@ def main():
     import torch
 
     covt = bench.load_covt()
-    tiles = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    tiles = int(args[0]) if args else 10000
     picks = bench.sample_batch(bench.tile_library(), tiles, bench.SEED)
-    plan = covt.Plan.from_tiles([t for _, t in picks])
+    # --props: the plan also decodes every property column's streams (COVT_PLAN_PROPERTIES)
+    plan = covt.Plan.from_tiles([t for _, t in picks], flags=covt.PLAN_PROPERTIES if "--props" in sys.argv else 0)
     batch = covt.DeviceBatch(plan, "cuda")
     L = covt.lib()
     phase = torch.zeros(plan.num_streams * 8, dtype=torch.int32, device="cuda")
