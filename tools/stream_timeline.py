@@ -17,7 +17,8 @@ import bench  # noqa: E402
 
 NAMES = {101: "L_BYTE_RLE", 102: "L_RLE_U64", 103: "L_RLE_I32", 104: "L_RLE_S64",
          1: "BYTE_RLE", 2: "RLE_U64", 3: "RLE_I32", 4: "RLE_S64", 7: "VAR_ZZD", 8: "VAR_XY", 9: "VAR_MORTON",
-         10: "FPF_ZZD", 11: "FPF_XY", 12: "FPF_MORTON", 13: "VAR_U64", 14: "VAR_I32_I64", 15: "VAR_ZZD_I64"}
+         10: "FPF_ZZD", 11: "FPF_XY", 12: "FPF_MORTON", 13: "VAR_U64", 14: "VAR_I32_I64", 15: "VAR_ZZD_I64",
+         16: "BYTE_RLE_RAW", 116: "L_BYTE_RAW", 17: "VAR_ZZ_I64J", 18: "VAR_ZZ_S64", 19: "VAR_ZZD_S64"}
 TICK_US = 0.01  # 100 MHz
 
 
@@ -73,7 +74,7 @@ def main():
         print("   %-12s %8d %8d  start %7.1f  dur %7.1f" % (NAMES.get(int(op_t[i]), op_t[i]), s["byte_length"][i],
                                                           s["num_values"][i], (st_t[i] - t0) * TICK_US,
                                                           d_t[i] * TICK_US))
-    fam_of = {1: 0, 2: 0, 3: 0, 4: 0}
+    fam_of = {1: 0, 2: 0, 3: 0, 4: 0, 16: 0}
     for fam, name in enumerate(("RLE", "VARINT", "FASTPFOR", "LANE")):
         m = np.array([(3 if o >= 100 else fam_of.get(int(o), 2 if o in (10, 11, 12) else 1)) == fam for o in op_t])
         if m.any():
