@@ -711,6 +711,17 @@ __device__ __forceinline__ uint64_t win_vulong(const WaveSmem& sm, int32_t sj, i
     for (int b = 0; b < len; ++b) r |= (uint64_t)(win_byte(sm, sj + b) & 0x7fu) << ((7 * b) & 63);
     return r;
 }
+// its low 32 bits (the (int) of RLE_I32): bytes 5..9 only reach bits >= 35, so up to 10 bytes the
+// first five decide; longer (malformed) varints wrap their shifts and take the full path
+__device__ __forceinline__ uint32_t win_vulong_lo32(const WaveSmem& sm, int32_t sj, int32_t ej) {
+    const int32_t len = ej - sj + 1;
+    if (len > 10) return (uint32_t)win_vulong(sm, sj, ej);
+    const int32_t d = sj >> 2;
+    const uint32_t sh = (uint32_t)(sj & 3);
+    const uint32_t w0 = sm.u.v.win[d], w1 = sm.u.v.win[d + 1], w2 = sm.u.v.win[d + 2];
+    const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    return pext7(x0 & bytemask(len)) | (len >= 5 ? (x1 & 0x7fu) << 28 : 0u);
+}
 
 // ORC RLE v1 integer reader (RunLengthIntegerReader.readValues / next).
 // Per 1 KiB window: (1) every byte position j computes, from the terminator index, where the next
@@ -822,55 +833,75 @@ __device__ void run_rle_int(Ctx& c) {
                     const uint32_t nxt = lane_bcast(gs, gl + 1 < 64 ? gl + 1 : 63);
                     pj = gl + 1 < G ? (int32_t)nxt : pj;
                 }
-                const bool big = take > 8;
-                // per-group parameters, lane-parallel: runs base + i * delta, literals from varint rr
+                // runs, base + i * delta: one lane per run of at most 8 values (a wave-uniform trip
+                // count; lanes past their run's end repeat its last value, same address and data),
+                // the whole wave per longer run
                 const bool isrun = cb < 0x80u;
                 const int32_t rr = gv ? rank_rel(sm, pg + (isrun ? 2 : 1), K) : 0;
-                const int32_t delta = (int32_t)(int8_t)win_byte(sm, pg + 1);
+                const bool rv = gv && isrun && take > 0;
                 int64_t b64 = 0;
-                if (gv && isrun) {
+                int32_t delta = 0;
+                if (rv) {
+                    delta = (int32_t)(int8_t)win_byte(sm, pg + 1);
                     const uint64_t raw = win_vulong(sm, pg + 2, sm.u.v.list[rr]);
                     b64 = is_signed ? zz64(raw) : (int64_t)raw;
                 }
-                // Expansion loops run a wave-uniform trip count; lanes past their group's end repeat its
-                // last value (same address, same data) instead of masking exec each iteration.
-                const bool small = gv && !big && take > 0;
+                const bool small = rv && take <= 8;
                 const int32_t tmax = (int32_t)wave_max((uint32_t)(small ? take : 0));
                 if (small) {
                     for (int32_t i0 = 0; i0 < tmax; ++i0) {
                         const int32_t i = i0 < take ? i0 : take - 1;
-                        if (isrun) {
-                            const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
-                            if (to_i32) st_out((int32_t*)c.out + goff + i, (int32_t)v);
-                            else st_out((int64_t*)c.out + goff + i, v);
-                        } else {
-                            const int32_t ej = sm.u.v.list[rr + i];
-                            const int32_t sj = i == 0 ? pg + 1 : (int32_t)sm.u.v.list[rr + i - 1] + 1;
-                            store(goff + i, win_vulong(sm, sj, ej));
-                        }
+                        const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
+                        if (to_i32) st_out((int32_t*)c.out + goff + i, (int32_t)v);
+                        else st_out((int64_t*)c.out + goff + i, v);
                     }
                 }
-                COVT_PHASE(c, 3);
-                uint64_t bigm = __ballot(gv && big);
-                while (bigm) {  // wave-uniform loop over the big groups of this batch
+                uint64_t bigm = __ballot(rv && take > 8);
+                while (bigm) {  // wave-uniform loop over the long runs of this batch
                     const int src = __ffsll((long long)bigm) - 1;
                     bigm &= bigm - 1;
                     const int32_t o2 = (int32_t)lane_bcast((uint32_t)goff, src);
                     const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
-                    if (lane_bcast(cb, src) < 0x80u) {
-                        const int32_t d2 = (int32_t)lane_bcast((uint32_t)delta, src);
-                        const int64_t bb = (int64_t)(((uint64_t)lane_bcast((uint32_t)((uint64_t)b64 >> 32), src) << 32) |
-                                                     lane_bcast((uint32_t)b64, src));
-                        if (to_i32) store_run<4>(c.out, o2, t2, bb, d2);  // literals[0] + used * delta
-                        else store_run<8>(c.out, o2, t2, bb, d2);
-                    } else {
-                        const int32_t r = (int32_t)lane_bcast((uint32_t)rr, src);
-                        const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
-                        for (int32_t i0 = 0; i0 < t2; i0 += 64) {
-                            const int32_t i = i0 + l < t2 ? i0 + l : t2 - 1;
-                            const int32_t ej = sm.u.v.list[r + i];
-                            const int32_t sj = i == 0 ? p2 + 1 : (int32_t)sm.u.v.list[r + i - 1] + 1;
-                            store(o2 + i, win_vulong(sm, sj, ej));
+                    const int32_t d2 = (int32_t)lane_bcast((uint32_t)delta, src);
+                    const int64_t bb = (int64_t)lane_bcast64((uint64_t)b64, src);
+                    if (to_i32) store_run<4>(c.out, o2, t2, bb, d2);  // literals[0] + used * delta
+                    else store_run<8>(c.out, o2, t2, bb, d2);
+                }
+                COVT_PHASE(c, 3);
+                // literals: every literal value of the batch, 64 per step whatever the group sizes.
+                // Literal groups are compacted to lanes 0..nl-1 (ds_permute); value u's group is the
+                // number of group starts at or before u (ballot over the starts <= u0, then a 64-bit
+                // mask of the starts inside the step), and its varint is terminator rank rr + (u - ust).
+                const bool lv = gv && !isrun && take > 0;
+                const uint32_t lc = lv ? (uint32_t)take : 0u;
+                const uint32_t linc = incl_scan(lc);
+                const int32_t U = (int32_t)lane_bcast(linc, 63);
+                if (U > 0) {
+                    const uint64_t lm = __ballot(lv), below = (1ull << l) - 1ull;
+                    const int32_t nl = __popcll(lm);
+                    const int32_t dst = lv ? __popcll(lm & below) : nl + __popcll(~lm & below);
+                    const int32_t ust = (int32_t)(linc - lc);
+                    // rank and output offsets relative to u, 15 + 17 bits (rr <= 1024, ust and goff - out0 < 2^14)
+                    const uint32_t pk = (uint32_t)(rr - ust + 16384) | ((uint32_t)(goff - out0 - ust) << 15);
+                    const int32_t cust = __builtin_amdgcn_ds_permute(dst << 2, lv ? ust : 0x3fffffff);
+                    const uint32_t cpk = (uint32_t)__builtin_amdgcn_ds_permute(dst << 2, (int32_t)pk);
+                    for (int32_t u0 = 0; u0 < U; u0 += 64) {
+                        const int32_t s = cust - u0;
+                        const uint64_t mask = wave_or64(s >= 0 && s < 64 ? 1ull << s : 0ull);
+                        const int32_t gb = __popcll(__ballot(cust <= u0)) - 1;  // group holding value u0
+                        const int32_t gk = gb + __popcll(mask & ((2ull << l) - 1ull) & ~1ull);
+                        const uint32_t info = (uint32_t)lane_get((int32_t)cpk, gk);
+                        const int32_t u = u0 + l;
+                        if (u < U) {
+                            const int32_t rank = u + (int32_t)(info & 0x7fffu) - 16384;
+                            const int32_t o = out0 + u + (int32_t)(info >> 15);
+                            const int32_t ej = sm.u.v.list[rank];
+                            const int32_t pv = rank > 0 ? (int32_t)sm.u.v.list[rank - 1] : -2;
+                            // a group's first varint starts after its header (the byte after the previous
+                            // group's last terminator; at the window's first group, after jlo)
+                            const int32_t sj = ((mask >> l) & 1ull) ? max(pv + 2, jlo + 1) : pv + 1;
+                            if (to_i32) st_out((int32_t*)c.out + o, (int32_t)win_vulong_lo32(sm, sj, ej));
+                            else store(o, win_vulong(sm, sj, ej));
                         }
                     }
                 }
@@ -936,35 +967,51 @@ __device__ void run_rle_byte(Ctx& c) {
                 const uint32_t nxt = lane_bcast(gs, gl + 1 < 64 ? gl + 1 : 63);
                 pj = gl + 1 < G ? (int32_t)nxt : pj;
             }
-            const bool big = take > 8;
+            // runs as in run_rle_int: one lane per run of at most 8 bytes, the wave per longer run
             const bool isrun = cb < 0x80u;
             const uint32_t rv = win_byte(sm, pg + 1);  // a run's value
-            lbad |= gv && isrun && take > 0 && rv > 5u;
-            const bool small = gv && !big && take > 0;
+            const bool runv = gv && isrun && take > 0;
+            lbad |= runv && rv > 5u;
+            const bool small = runv && take <= 8;
             const int32_t tmax = (int32_t)wave_max((uint32_t)(small ? take : 0));
             if (small) {  // uniform trip count; lanes past their end repeat the last byte
                 for (int32_t i0 = 0; i0 < tmax; ++i0) {
                     const int32_t i = i0 < take ? i0 : take - 1;
-                    const uint32_t v = isrun ? rv : win_byte(sm, pg + 1 + i);
-                    st_out(c.out + goff + i, (uint8_t)v);
-                    lbad |= v > 5u;
+                    st_out(c.out + goff + i, (uint8_t)rv);
                 }
             }
-            COVT_PHASE(c, 3);
-            uint64_t bigm = __ballot(gv && big);
+            uint64_t bigm = __ballot(runv && take > 8);
             while (bigm) {
                 const int src = __ffsll((long long)bigm) - 1;
                 bigm &= bigm - 1;
-                const int32_t o2 = (int32_t)lane_bcast((uint32_t)goff, src);
-                const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
-                if (lane_bcast(cb, src) < 0x80u) {
-                    store_run<1>(c.out, o2, t2, (int64_t)lane_bcast(rv, src), 0);
-                } else {
-                    const int32_t p2 = (int32_t)lane_bcast((uint32_t)pg, src);
-                    for (int32_t i0 = 0; i0 < t2; i0 += 64) {
-                        const int32_t i = i0 + l < t2 ? i0 + l : t2 - 1;
-                        const uint32_t v = win_byte(sm, p2 + 1 + i);
-                        st_out(c.out + o2 + i, (uint8_t)v);
+                store_run<1>(c.out, (int32_t)lane_bcast((uint32_t)goff, src), (int32_t)lane_bcast((uint32_t)take, src),
+                             (int64_t)lane_bcast(rv, src), 0);
+            }
+            COVT_PHASE(c, 3);
+            // literal bytes of the batch, 64 per step across groups (the run_rle_int scheme: value u
+            // of the batch's literals is window byte u + (pg + 1 - ust) of its group)
+            const bool lv = gv && !isrun && take > 0;
+            const uint32_t lc = lv ? (uint32_t)take : 0u;
+            const uint32_t linc = incl_scan(lc);
+            const int32_t U = (int32_t)lane_bcast(linc, 63);
+            if (U > 0) {
+                const uint64_t lm = __ballot(lv), below = (1ull << l) - 1ull;
+                const int32_t nl = __popcll(lm);
+                const int32_t dst = lv ? __popcll(lm & below) : nl + __popcll(~lm & below);
+                const int32_t ust = (int32_t)(linc - lc);
+                const uint32_t pk = (uint32_t)(pg + 1 - ust + 16384) | ((uint32_t)(goff - out0 - ust) << 15);
+                const int32_t cust = __builtin_amdgcn_ds_permute(dst << 2, lv ? ust : 0x3fffffff);
+                const uint32_t cpk = (uint32_t)__builtin_amdgcn_ds_permute(dst << 2, (int32_t)pk);
+                for (int32_t u0 = 0; u0 < U; u0 += 64) {
+                    const int32_t s = cust - u0;
+                    const uint64_t mask = wave_or64(s >= 0 && s < 64 ? 1ull << s : 0ull);
+                    const int32_t gb = __popcll(__ballot(cust <= u0)) - 1;
+                    const int32_t gk = gb + __popcll(mask & ((2ull << l) - 1ull) & ~1ull);
+                    const uint32_t info = (uint32_t)lane_get((int32_t)cpk, gk);
+                    const int32_t u = u0 + l;
+                    if (u < U) {
+                        const uint32_t v = win_byte(sm, u + (int32_t)(info & 0x7fffu) - 16384);
+                        st_out(c.out + out0 + u + (int32_t)(info >> 15), (uint8_t)v);
                         lbad |= v > 5u;
                     }
                 }

@@ -83,6 +83,22 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
     return lane_bcast(x, 63);
 }
 
+// bitwise OR over the 64 lanes of a 64-bit value (DPP on both halves), returned uniform
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#define COVT_OR64_STEP(ctrl, rmask)                                                    \
+    lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, ctrl, rmask, 0xf, false); \
+    hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, ctrl, rmask, 0xf, false);
+    COVT_OR64_STEP(0x111, 0xf)  // row_shr:1
+    COVT_OR64_STEP(0x112, 0xf)  // row_shr:2
+    COVT_OR64_STEP(0x114, 0xf)  // row_shr:4
+    COVT_OR64_STEP(0x118, 0xf)  // row_shr:8
+    COVT_OR64_STEP(0x142, 0xa)  // row_bcast:15
+    COVT_OR64_STEP(0x143, 0xc)  // row_bcast:31
+#undef COVT_OR64_STEP
+    return ((uint64_t)lane_bcast(hi, 63) << 32) | lane_bcast(lo, 63);
+}
+
 // lane l + 1's value (lane 63: `tail`, which must be wave-uniform): DPP wave_shl:1, no LDS traffic.
 // The DPP source lane has no successor for lane 63, which then keeps the `old` operand; keeping the
 // select inside the DPP matters: a separate `l == 63 ? tail : dpp(x)` can be turned into an

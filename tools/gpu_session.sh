@@ -34,7 +34,8 @@ for s in "$@"; do
     timeline) step timeline 300 python tools/stream_timeline.py ;;
     hbm) step hbm 300 python tools/hbm_probe.py ;;
     wpat) step wpat 300 python tools/probe/write_pattern.py ;;
-    ab) for v in ${AB_VARIANTS:-libcovt_base.so libcovt.so libcovt_base.so libcovt.so}; do
+    ab|ab_props) [ "$s" = ab_props ] && export OPB_PROPS=1
+        for v in ${AB_VARIANTS:-libcovt_base.so libcovt.so libcovt_base.so libcovt.so}; do
             echo "== ab $v"; COVT_LIB_VARIANT=$v OPB_QUICK=1 timeout -k 10 300 python tools/op_breakdown.py 2>&1 | grep -v amdgpu.ids || fatal ab $?
         done ;;
     fpfsize) step fpfsize 300 python -c "import sys; sys.path.insert(0, 'tools'); import op_breakdown; op_breakdown.fpf_scaling()" ;;

@@ -19,7 +19,9 @@ def main():
     covt = bench.load_covt()
     tiles = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
     picks = bench.sample_batch(bench.tile_library(), tiles, bench.SEED)
-    plan = covt.Plan.from_tiles([t for _, t in picks])
+    # OPB_PROPS=1: the plan also decodes every property column's streams (COVT_PLAN_PROPERTIES)
+    flags = covt.PLAN_PROPERTIES if os.environ.get("OPB_PROPS") else 0
+    plan = covt.Plan.from_tiles([t for _, t in picks], flags=flags)
     batch = covt.DeviceBatch(plan, "cuda")
     descs = plan.descs.reshape(-1, 32)
     ops = descs[:, 24]
