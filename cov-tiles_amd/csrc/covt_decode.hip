@@ -786,11 +786,25 @@ __device__ void run_rle_int(Ctx& c) {
             int32_t G = 0;
             uint32_t gs = 0;
             const int32_t out0 = out;
-            for (; G < 64; ++G) {
-                const uint32_t nx = uniu(sm.u.v.next[pj]);
-                if (nx == 0xffffu) break;
-                gs = l == G ? (uint32_t)pj : gs;
-                pj = (int32_t)nx;
+            {
+                // Eight steps per scalar test, branch-free: the chain's critical path is LDS read ->
+                // address of the next read, all in VGPRs.  Steps past the end are no-ops (next[kWin] is
+                // the 0xffff sentinel, so a stopped chain stays stopped); lanes left at ~0 hold no group.
+                gs = ~0u;
+                uint32_t cur = (uint32_t)pj, nx = sm.u.v.next[pj];
+                for (int32_t g0 = 0; g0 < 64; g0 += 8) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const uint32_t nn = sm.u.v.next[min(nx, (uint32_t)kWin)];
+                        const bool ok = nx != 0xffffu;
+                        gs = (ok && l == g0 + k) ? cur : gs;
+                        cur = ok ? nx : cur;
+                        nx = nn;
+                    }
+                    if (uniu(nx) == 0xffffu) break;
+                }
+                G = __popcll(__ballot(gs != ~0u));
+                pj = (int32_t)uniu(cur);
             }
             COVT_PHASE(c, 2);
             if (G == 0) {
@@ -939,12 +953,23 @@ __device__ void run_rle_byte(Ctx& c) {
             int32_t G = 0;
             uint32_t gs = 0;
             const int32_t out0 = out;
-            for (; G < 64 && pj < vend; ++G) {
-                const uint32_t cb = uniu(win_byte(sm, pj));
-                const int32_t nx = cb < 0x80u ? pj + 2 : pj + 1 + 0x100 - (int32_t)cb;
-                if (nx > vend) break;
-                gs = l == G ? (uint32_t)pj : gs;
-                pj = nx;
+            {  // branch-free steps, eight per scalar test (as in run_rle_int)
+                int32_t cur = pj;
+                bool live = pj < vend;
+                gs = ~0u;
+                for (int32_t g0 = 0; g0 < 64 && uni(live ? 1 : 0); g0 += 8) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int32_t cb = (int32_t)win_byte(sm, min(cur, kWin - 1));
+                        const int32_t nx = cb < 0x80 ? cur + 2 : cur + 0x101 - cb;
+                        live = live && nx <= vend;
+                        gs = (live && l == g0 + k) ? (uint32_t)cur : gs;
+                        cur = live ? nx : cur;
+                        live = live && cur < vend;
+                    }
+                }
+                G = __popcll(__ballot(gs != ~0u));
+                pj = uni(cur);
             }
             COVT_PHASE(c, 2);
             if (G == 0) {

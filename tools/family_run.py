@@ -19,7 +19,8 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     covt = bench.load_covt()
     picks = bench.sample_batch(bench.tile_library(), 10000, bench.SEED)
-    plan = covt.Plan.from_tiles([t for _, t in picks])
+    # OPB_PROPS=1: the plan also decodes every property column's streams (COVT_PLAN_PROPERTIES)
+    plan = covt.Plan.from_tiles([t for _, t in picks], flags=covt.PLAN_PROPERTIES if os.environ.get("OPB_PROPS") else 0)
     batch = covt.DeviceBatch(plan, "cuda")
     counts = plan.family_counts.copy()
     if fam != "all":
