@@ -51,54 +51,72 @@ __device__ int32_t dictionary(const uint8_t* in, const uint8_t* dec, const covt_
     const int32_t nd = d.n_dict;
     const gp_i32* lens = (const gp_i32*)(dec + d.length_off);
     int32_t* offs = (int32_t*)(outb + d.out_off[2]);
-    bool neg = false;
-    for (int32_t q = 0; q < nd; q += 256) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int32_t j = q + 4 * l + k;
-            neg |= j < nd && lens[j] < 0;
-        }
-    }
-    if (__ballot(neg)) return COVT_ERR_COUNT_MISMATCH;  // decodeString with a negative length
-    uint64_t run = 0;                                    // uniform: bytes before this step
     if (!write) {
-        for (int32_t q = 0; q < nd; q += 256) {
-            uint64_t s = 0;
+        // sub-columns that share the owner's dictionary only check it: the lengths are summed and
+        // tested for negatives in one strided pass, 16 independent loads per lane per iteration
+        bool neg = false;
+        uint64_t s = 0;
+        for (int32_t q = 0; q < nd; q += 1024) {
+            int32_t x[16];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int32_t j = q + 4 * l + k;
-                s += j < nd ? (uint64_t)lens[j] : 0ull;
+            for (int k = 0; k < 16; ++k) {
+                const int32_t j = q + 256 * (k >> 2) + 4 * l + (k & 3);
+                x[k] = j < nd ? lens[j] : 0;
             }
-            run += lane_bcast64(incl_scan64(s), 63);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                neg |= x[k] < 0;
+                s += (uint64_t)(uint32_t)x[k];
+            }
         }
+        if (__ballot(neg)) return COVT_ERR_COUNT_MISMATCH;  // decodeString with a negative length
+        const uint64_t run = lane_bcast64(incl_scan64(s), 63);
         return run > (uint64_t)d.dict_bytes ? COVT_ERR_TRUNCATED : COVT_OK;
     }
-    for (int32_t q = 0; q < nd; q += 256) {
-        uint64_t x[4], s = 0;
+    // the owner: offsets (exclusive scan, 256 per step, four steps' loads in flight) and the bytes; a
+    // negative length anywhere fails the column (decodeString) whatever was written
+    bool neg = false;
+    uint64_t run = 0;  // uniform: bytes before this step
+    for (int32_t q0 = 0; q0 < nd; q0 += 1024) {
+        int32_t xs[4][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int32_t j = q + 4 * l + k;
-            x[k] = j < nd ? (uint64_t)lens[j] : 0ull;
-            s += x[k];
-        }
-        const uint64_t inc = incl_scan64(s);
-        uint64_t e = run + inc - s;
-        int32_t o[4];
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            o[k] = (int32_t)e;
-            e += x[k];
-        }
-        const int32_t i0 = q + 4 * l;
-        if (i0 + 4 <= nd) {
-            *(pi32x4*)(offs + i0) = pi32x4{o[0], o[1], o[2], o[3]};
-        } else {
+            for (int k = 0; k < 4; ++k) {
+                const int32_t j = q0 + 256 * t + 4 * l + k;
+                xs[t][k] = j < nd ? lens[j] : 0;
+            }
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (i0 + k < nd) offs[i0 + k] = o[k];
+        for (int t = 0; t < 4; ++t) {
+            const int32_t q = q0 + 256 * t;
+            if (q >= nd) break;
+            uint64_t x[4], s = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                neg |= xs[t][k] < 0;
+                x[k] = (uint64_t)(uint32_t)xs[t][k];
+                s += x[k];
+            }
+            const uint64_t inc = incl_scan64(s);
+            uint64_t e = run + inc - s;
+            int32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                o[k] = (int32_t)e;
+                e += x[k];
+            }
+            const int32_t i0 = q + 4 * l;
+            if (i0 + 4 <= nd) {
+                *(pi32x4*)(offs + i0) = pi32x4{o[0], o[1], o[2], o[3]};
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (i0 + k < nd) offs[i0 + k] = o[k];
+            }
+            run += lane_bcast64(inc, 63);
         }
-        run += lane_bcast64(inc, 63);
     }
+    if (__ballot(neg)) return COVT_ERR_COUNT_MISMATCH;
     if (run > (uint64_t)d.dict_bytes) return COVT_ERR_TRUNCATED;  // strings past the dictionary stream
     if (l == 0) offs[nd] = (int32_t)run;
     const uint8_t* src = in + d.dict_in_off;
