@@ -45,6 +45,8 @@ __device__ uint32_t* covt_phase_buf;  // [n_streams][kPhases], set by covt_debug
 __device__ const covt_stream_desc* covt_phase_desc0;  // descriptor 0 of the launch (row index base)
 #endif
 
+typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+
 // Per-wave LDS scratch.  The small fields come first so each codec family's kernel allocates only
 // the prefix it uses (kFamSmem below): varint windows, RLE windows + group tables, or FastPFOR
 // staging + byte container.
@@ -750,7 +752,11 @@ __device__ void run_rle_int(Ctx& c) {
         const int32_t woff = w.woff, K = w.K;
         const int32_t jlo = pos - woff;  // (positions at or past the valid end rank K: no group there)
         // (1) next[] for this lane's 16 positions, branch-free: the terminator rank of position
-        // 16l + k is R[k] (incremental popcounts of this lane's chunk mask, then the next lane's)
+        // 16l + k is R[k] (incremental popcounts of this lane's chunk mask, then the next lane's).
+        // Entries hold the LDS byte address of next[target] (the walk's read -> read chain then needs
+        // no arithmetic); "no group completes here" is the sentinel next[kWin], which points at itself.
+        const uint32_t nb = (uint32_t)(uintptr_t)(lds_cu16*)&sm.u.v.next[0];
+        const uint32_t sent = nb + 2u * (uint32_t)kWin;
         {
             const uint32_t ncmsk = lane_next(w.cmsk);
             uint32_t R[18];
@@ -767,13 +773,13 @@ __device__ void run_rle_int(Ctx& c) {
                 // run: the base varint ends at terminator R[k+2]; literals: the (256-cb)-th from R[k+1]
                 const uint32_t ridx = cb < 0x80u ? R[k + 2] : R[k + 1] + (0xffu - cb);
                 const uint32_t e = (uint32_t)sm.u.v.list[ridx < (uint32_t)kWin ? ridx : (uint32_t)kWin - 1] + 1u;
-                const uint32_t nx = (j >= jlo && ridx < (uint32_t)K) ? e : 0xffffu;
+                const uint32_t nx = (j >= jlo && ridx < (uint32_t)K) ? nb + 2u * e : sent;
                 if (k & 1) nx2[k >> 1] |= nx << 16;
                 else nx2[k >> 1] = nx;
             }
             ((uint4*)sm.u.v.next)[2 * l] = make_uint4(nx2[0], nx2[1], nx2[2], nx2[3]);
             ((uint4*)sm.u.v.next)[2 * l + 1] = make_uint4(nx2[4], nx2[5], nx2[6], nx2[7]);
-            if (l == 0) sm.u.v.next[kWin] = 0xffffu;  // sentinel: a group ending at the window end
+            if (l == 0) sm.u.v.next[kWin] = (uint16_t)sent;  // a group ending at the window end
         }
         wave_sync();
         COVT_PHASE(c, 1);
@@ -787,24 +793,26 @@ __device__ void run_rle_int(Ctx& c) {
             uint32_t gs = 0;
             const int32_t out0 = out;
             {
-                // Eight steps per scalar test, branch-free: the chain's critical path is LDS read ->
-                // address of the next read, all in VGPRs.  Steps past the end are no-ops (next[kWin] is
-                // the 0xffff sentinel, so a stopped chain stays stopped); lanes left at ~0 hold no group.
+                // Eight steps per scalar test, branch-free: the chain's critical path is one LDS read
+                // whose result is the next read's address.  Steps past the end are no-ops (the sentinel
+                // points at itself); lanes left at ~0 hold no group.
                 gs = ~0u;
-                uint32_t cur = (uint32_t)pj, nx = sm.u.v.next[pj];
+                auto rd = [](uint32_t a) -> uint32_t { return *(lds_cu16*)(uintptr_t)a; };
+                uint32_t cur = nb + 2u * (uint32_t)pj, nx = rd(cur);
                 for (int32_t g0 = 0; g0 < 64; g0 += 8) {
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
-                        const uint32_t nn = sm.u.v.next[min(nx, (uint32_t)kWin)];
-                        const bool ok = nx != 0xffffu;
+                        const uint32_t nn = rd(nx);
+                        const bool ok = nx != sent;
                         gs = (ok && l == g0 + k) ? cur : gs;
                         cur = ok ? nx : cur;
                         nx = nn;
                     }
-                    if (uniu(nx) == 0xffffu) break;
+                    if (uniu(nx) == sent) break;
                 }
                 G = __popcll(__ballot(gs != ~0u));
-                pj = (int32_t)uniu(cur);
+                gs = gs != ~0u ? (gs - nb) >> 1 : gs;  // positions
+                pj = (int32_t)((uniu(cur) - nb) >> 1);
             }
             COVT_PHASE(c, 2);
             if (G == 0) {
