@@ -178,6 +178,9 @@ struct Carry {
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_out16(int32_t* p, int4 v) {
     const i32x4 w = {v.x, v.y, v.z, v.w};
+#if defined(COVT_ABL_NOSTORE)  // ablation build: wide stores land on the first KiB of their 64 KiB
+    p = (int32_t*)(((uintptr_t)p & ~(uintptr_t)65535) | ((uintptr_t)p & 1023));
+#endif
     __builtin_nontemporal_store(w, (i32x4*)p);
 }
 template <class T>
