@@ -53,7 +53,7 @@ class OracleProp(C.Structure):
 
 
 def build(force: bool = False) -> str:
-    srcs = ("covt_oracle.c", "covt_oracle_props.c", "covt_oracle.h")
+    srcs = ("covt_oracle.c", "covt_oracle_props.c", "mvt_decode.c", "covt_oracle.h")
     if force or not os.path.exists(_LIB_PATH) or (
         os.path.getmtime(_LIB_PATH) < max(os.path.getmtime(os.path.join(_HERE, f)) for f in srcs)
     ):
@@ -73,6 +73,7 @@ def lib():
         u8p, i32p, i64p = C.POINTER(C.c_uint8), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
         sz = C.c_size_t
         L.oracle_walk_tile.argtypes = [u8p, sz, C.c_int, C.POINTER(OracleStream), C.c_int32, i32p]
+        L.mvt_decode_tile.argtypes = [u8p, C.c_int64, C.c_int, i32p, C.c_int64, i64p, C.POINTER(C.c_uint64)]
         L.oracle_decode_stream.argtypes = [u8p, sz, C.POINTER(OracleStream), C.c_int, C.c_void_p, i32p]
         L.oracle_stream_output.argtypes = [C.POINTER(OracleStream), C.c_int, i32p, i64p]
         L.oracle_decode_tiles_mt.argtypes = [u8p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int32,
@@ -392,3 +393,18 @@ def assemble_geometry(types, go, po, ro, vo, vb, closed_in_stream: bool, caps=No
                                         rcap, ccap, _p(geo, C.c_int32), _p(part, C.c_int32), _p(ring, C.c_int32),
                                         _p(coords, C.c_int32), C.byref(np_), C.byref(nr), C.byref(nc))
     return (st, geo, part[:np_.value + 1], ring[:nr.value + 1], coords[:2 * nc.value].reshape(-1, 2))
+
+
+# ---------------------------------------------------------------------------
+# MVT decoder (benchmark infrastructure for the MVT-vs-COVT comparison, oracle/mvt_decode.c)
+# ---------------------------------------------------------------------------
+def mvt_decode(tile: bytes, with_props: bool = False, cap: int = 1 << 20):
+    """Decodes one MVT tile (geometry commands to vertices, ids, types; tags + values with
+    with_props).  Returns (status, features, vertices, parts, values, checksum)."""
+    arr, p = _u8(tile)
+    xy = np.empty(2 * cap, dtype=np.int32)
+    o4 = np.zeros(4, dtype=np.int64)
+    ck = C.c_uint64(0)
+    st = lib().mvt_decode_tile(p, arr.size, int(with_props), xy.ctypes.data_as(C.POINTER(C.c_int32)), cap,
+                               o4.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(ck))
+    return st, int(o4[0]), int(o4[1]), int(o4[2]), int(o4[3]), ck.value
