@@ -7,6 +7,7 @@
 // (make -C cov-tiles_amd jni JAVA_HOME=...); this image has no JDK.
 #include <jni.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "covt.h"
@@ -151,6 +152,98 @@ JNIEXPORT jintArray JNICALL JFN(decodeFastPfor128DeltaMortonCodes)(JNIEnv* env, 
     });
     if (r) set_pos(env, pos, p);
     return r;
+}
+
+// ---- com.covt.decoder.gpu.GpuCovtBatch: whole-tile batches through the plan API -------------------
+#define BFN(name) Java_com_covt_decoder_gpu_GpuCovtBatch_##name
+
+static covt_plan* plan_of(jlong h) { return reinterpret_cast<covt_plan*>(h); }
+static const uint8_t* direct(JNIEnv* env, jobject buf) {
+    return static_cast<const uint8_t*>(env->GetDirectBufferAddress(buf));
+}
+
+JNIEXPORT jlong JNICALL BFN(create)(JNIEnv* env, jclass, jobject tiles, jlongArray offsets, jlongArray sizes,
+                                    jint format, jint id_mode, jint flags) {
+    const jsize n = env->GetArrayLength(offsets);
+    std::vector<uint64_t> off((size_t)n), sz((size_t)n);
+    env->GetLongArrayRegion(offsets, 0, n, reinterpret_cast<jlong*>(off.data()));
+    env->GetLongArrayRegion(sizes, 0, n, reinterpret_cast<jlong*>(sz.data()));
+    covt_plan* p = nullptr;
+    if (!check(env, covt_plan_create_ex(direct(env, tiles), off.data(), sz.data(), n, format, id_mode,
+                                        (uint32_t)flags, &p)))
+        return 0;
+    return reinterpret_cast<jlong>(p);
+}
+JNIEXPORT void JNICALL BFN(destroy)(JNIEnv*, jclass, jlong h) { covt_plan_destroy(plan_of(h)); }
+JNIEXPORT jlong JNICALL BFN(numStreams)(JNIEnv*, jclass, jlong h) { return covt_plan_num_streams(plan_of(h)); }
+JNIEXPORT jlong JNICALL BFN(outputBytes)(JNIEnv*, jclass, jlong h) { return covt_plan_output_bytes(plan_of(h)); }
+JNIEXPORT jlong JNICALL BFN(numPropertyColumns)(JNIEnv*, jclass, jlong h) {
+    return covt_plan_num_property_columns(plan_of(h));
+}
+JNIEXPORT jlong JNICALL BFN(propertyBytes)(JNIEnv*, jclass, jlong h) { return covt_plan_property_bytes(plan_of(h)); }
+
+JNIEXPORT jintArray JNICALL BFN(tileStatus)(JNIEnv* env, jclass, jlong h, jint n_tiles) {
+    std::vector<int32_t> st((size_t)(n_tiles > 0 ? n_tiles : 0));
+    if (!check(env, covt_plan_tile_status(plan_of(h), st.data()))) return nullptr;
+    jintArray a = env->NewIntArray(n_tiles);
+    env->SetIntArrayRegion(a, 0, n_tiles, st.data());
+    return a;
+}
+JNIEXPORT jlongArray JNICALL BFN(streams)(JNIEnv* env, jclass, jlong h) {
+    const int64_t n = covt_plan_num_streams(plan_of(h));
+    std::vector<covt_stream_info> info((size_t)n);
+    if (!check(env, covt_plan_streams(plan_of(h), info.data()))) return nullptr;
+    std::vector<jlong> rows((size_t)n * 15);
+    for (int64_t i = 0; i < n; ++i) {
+        const covt_stream_info& s = info[(size_t)i];
+        const jlong r[15] = {s.tile, s.layer, s.column_kind, s.stream_type, s.encoding, s.column_type, s.num_values,
+                             s.byte_length, s.num_bits, s.op, s.elem_bytes, s.desc_index, s.in_off, s.out_off,
+                             s.out_elems};
+        std::copy(r, r + 15, rows.begin() + 15 * i);
+    }
+    jlongArray a = env->NewLongArray((jsize)rows.size());
+    env->SetLongArrayRegion(a, 0, (jsize)rows.size(), rows.data());
+    return a;
+}
+JNIEXPORT jlongArray JNICALL BFN(propertyColumns)(JNIEnv* env, jclass, jlong h) {
+    const int64_t n = covt_plan_num_property_columns(plan_of(h));
+    std::vector<covt_prop_info> info((size_t)n);
+    if (!check(env, covt_plan_property_columns(plan_of(h), info.data()))) return nullptr;
+    std::vector<jlong> rows((size_t)n * 22);
+    for (int64_t i = 0; i < n; ++i) {
+        const covt_prop_info& q = info[(size_t)i];
+        const jlong r[22] = {q.tile, q.layer, q.column, q.type, q.column_type, q.n_features, q.n_data, q.n_dict,
+                             q.lang, q.name_len, q.lang_len, q.dict_bytes, q.stream[0], q.stream[1], q.stream[2],
+                             q.desc_index, q.name_off, q.lang_off, q.out_off[0], q.out_off[1], q.out_off[2],
+                             q.out_off[3]};
+        std::copy(r, r + 22, rows.begin() + 22 * i);
+    }
+    jlongArray a = env->NewLongArray((jsize)rows.size());
+    env->SetLongArrayRegion(a, 0, (jsize)rows.size(), rows.data());
+    return a;
+}
+JNIEXPORT jintArray JNICALL BFN(decode)(JNIEnv* env, jclass, jlong h, jobject tiles, jobject out) {
+    const int64_t n = covt_plan_num_streams(plan_of(h));
+    std::vector<covt_stream_result> res((size_t)n);
+    if (!check(env, covt_plan_decode_host(plan_of(h), direct(env, tiles), (uint64_t)env->GetDirectBufferCapacity(tiles),
+                                          static_cast<uint8_t*>(env->GetDirectBufferAddress(out)), res.data())))
+        return nullptr;
+    std::vector<jint> st((size_t)n);
+    for (int64_t i = 0; i < n; ++i) st[(size_t)i] = res[(size_t)i].status;
+    jintArray a = env->NewIntArray((jsize)n);
+    env->SetIntArrayRegion(a, 0, (jsize)n, st.data());
+    return a;
+}
+JNIEXPORT jintArray JNICALL BFN(properties)(JNIEnv* env, jclass, jlong h, jobject tiles, jobject out) {
+    const int64_t n = covt_plan_num_property_columns(plan_of(h));
+    std::vector<covt_prop_result> res((size_t)n);
+    if (!check(env, covt_plan_properties_host(plan_of(h), direct(env, tiles),
+                                              (uint64_t)env->GetDirectBufferCapacity(tiles),
+                                              static_cast<uint8_t*>(env->GetDirectBufferAddress(out)), res.data())))
+        return nullptr;
+    jintArray a = env->NewIntArray((jsize)(2 * n));
+    env->SetIntArrayRegion(a, 0, (jsize)(2 * n), reinterpret_cast<const jint*>(res.data()));
+    return a;
 }
 
 }  // extern "C"
