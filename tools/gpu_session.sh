@@ -42,6 +42,8 @@ for s in "$@"; do
     props_ab) for v in ${AB_VARIANTS:-libcovt_base.so libcovt.so libcovt_base.so libcovt.so}; do
             COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/props_run.py 2>&1 | grep -v amdgpu.ids || fatal props_ab $?
         done ;;
+    timeline_omt) step timeline_omt 300 python tools/stream_timeline.py 9000 --omt ;;
+    mvt_gpu) step mvt_gpu 300 python tools/mvt_vs_covt.py --gpu 9000 ;;
     fpfsize) step fpfsize 300 python -c "import sys; sys.path.insert(0, 'tools'); import op_breakdown; op_breakdown.fpf_scaling()" ;;
     prof) step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
     pmc_fetch) step rocprof_pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;

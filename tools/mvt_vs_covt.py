@@ -100,13 +100,15 @@ def gpu(n_tiles):
     torch.cuda.synchronize()
     _, res = batch.results()
     assert (res[:, 0] == 0).all()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ev[0].record(stream)
-    for _ in range(10):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+    for s, e in ev:
+        s.record(stream)
         batch.decode(stream)
-    ev[1].record(stream)
+        e.record(stream)
     torch.cuda.synchronize()
-    ms = ev[0].elapsed_time(ev[1]) / 10
+    per = [s.elapsed_time(e) for s, e in ev]
+    print("per-launch ms:", " ".join("%.3f" % t for t in per))
+    ms = float(np.median(per))
     print("GPU COVT decode (ids + geometry), %d OMT tiles (%d distinct, %.1f MB): %.3f ms per launch, %.0f tiles/s, %.1f GB/s"
           % (n_tiles, len(lib), plan.in_bytes / 1e6, ms, n_tiles / ms * 1e3, plan.in_bytes / ms / 1e6))
 

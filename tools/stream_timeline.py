@@ -28,9 +28,16 @@ def main():
     covt = bench.load_covt()
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     tiles = int(args[0]) if args else 10000
-    picks = bench.sample_batch(bench.tile_library(), tiles, bench.SEED)
+    if "--omt" in sys.argv:  # the MVT-vs-COVT GPU set: decodable OMT fixtures replicated to `tiles`
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import mvt_vs_covt
+
+        lib = [open(os.path.join(mvt_vs_covt.COVT_DIR, n + ".covt"), "rb").read() for n in mvt_vs_covt._decodable()]
+        tile_bytes = [lib[i % len(lib)] for i in range(tiles)]
+    else:
+        tile_bytes = [t for _, t in bench.sample_batch(bench.tile_library(), tiles, bench.SEED)]
     # --props: the plan also decodes every property column's streams (COVT_PLAN_PROPERTIES)
-    plan = covt.Plan.from_tiles([t for _, t in picks], flags=covt.PLAN_PROPERTIES if "--props" in sys.argv else 0)
+    plan = covt.Plan.from_tiles(tile_bytes, flags=covt.PLAN_PROPERTIES if "--props" in sys.argv else 0)
     batch = covt.DeviceBatch(plan, "cuda")
     L = covt.lib()
     phase = torch.zeros(plan.num_streams * 8, dtype=torch.int32, device="cuda")
