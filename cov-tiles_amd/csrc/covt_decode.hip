@@ -31,7 +31,7 @@ namespace covt {
 
 constexpr int kWin = 1024;  // window bytes (64 lanes x 16 B)
 #ifndef COVT_WAVES_PER_BLOCK
-#define COVT_WAVES_PER_BLOCK 4
+#define COVT_WAVES_PER_BLOCK 2  // A/B: 1 -> +8 %, 4 -> +1 % on the bench launch
 #endif
 constexpr int kWavesPerBlock = COVT_WAVES_PER_BLOCK;  // independent waves (streams) per workgroup
 constexpr int kFpfBlock = 256;
