@@ -39,7 +39,10 @@
 
 namespace covt {
 
-constexpr int kAsmWaves = 4;  // independent waves (columns) per workgroup
+#ifndef COVT_ASM_WAVES
+#define COVT_ASM_WAVES 4
+#endif
+constexpr int kAsmWaves = COVT_ASM_WAVES;  // independent waves (columns) per workgroup
 constexpr int kW = 256;       // items per step: 4 consecutive items per lane
 
 typedef __attribute__((address_space(1))) const int32_t g_i32;

@@ -19,7 +19,10 @@
 
 namespace covt {
 
-constexpr int kPropWaves = 4;  // independent waves (columns) per workgroup
+#ifndef COVT_PROP_WAVES
+#define COVT_PROP_WAVES 2  // A/B: 4 -> +2 %
+#endif
+constexpr int kPropWaves = COVT_PROP_WAVES;  // independent waves (columns) per workgroup
 
 typedef __attribute__((address_space(1))) const uint8_t gp_u8;
 typedef __attribute__((address_space(1))) const uint32_t gp_u32;

@@ -43,6 +43,10 @@ for s in "$@"; do
             COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/props_run.py 2>&1 | grep -v amdgpu.ids || fatal props_ab $?
         done ;;
     timeline_omt) step timeline_omt 300 python tools/stream_timeline.py 9000 --omt ;;
+    asm_props_ab) for v in ${AB_VARIANTS:-libcovt_base.so libcovt.so libcovt_base.so libcovt.so}; do
+            echo "== $v"; COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/asm_run.py 20 2>&1 | grep -v amdgpu.ids || fatal asm_props_ab $?
+            COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/props_run.py 2>&1 | grep -v amdgpu.ids || fatal asm_props_ab $?
+        done ;;
     mvt_gpu) step mvt_gpu 300 python tools/mvt_vs_covt.py --gpu 9000 ;;
     fpfsize) step fpfsize 300 python -c "import sys; sys.path.insert(0, 'tools'); import op_breakdown; op_breakdown.fpf_scaling()" ;;
     prof) step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
