@@ -1462,6 +1462,13 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(cons
         if (c.op == COVT_OP_BYTE_RLE_U8 || c.op == COVT_OP_BYTE_RLE_RAW) { if (c.n > 0) run_rle_byte(c); }
         else if (c.op == COVT_OP_RLE_U64 || c.op == COVT_OP_RLE_I32 || c.op == COVT_OP_RLE_S64) { if (c.n > 0) run_rle_int(c); }
         else c.err = COVT_ERR_UNSUPPORTED_ENCODING;
+#if defined(COVT_ABL_ONEOP)  // ablation build (instruction-cache footprint): one code path per family
+    } else if (FAM == COVT_FAMILY_VARINT) {
+        if (c.op == COVT_OP_VARINT_U64) run_varint_stream<COVT_OP_VARINT_U64>(c);
+        else run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I32>(c);
+    } else if (true) {
+        run_fastpfor<COVT_OP_FPF_ZZ_DELTA_I32>(c);
+#endif
     } else if (FAM == COVT_FAMILY_VARINT) {
         switch (c.op) {  // one uniform switch per stream; the loops are specialised per op
         case COVT_OP_VARINT_I32: run_varint_stream<COVT_OP_VARINT_I32>(c); break;
