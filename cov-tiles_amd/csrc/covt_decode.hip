@@ -1235,10 +1235,15 @@ __device__ void run_fastpfor(Ctx& c) {
                 h.xcur = uniu(hv.xcur);
                 h.bcoff = uni(hv.bcoff);
                 const int32_t pk = uni(pkv);
-                // unconditional, branch-free loads consumed only in the next iteration: the vmcnt wait
-                // lands there and no exec-mask bookkeeping is spent on lane conditions
+                // loads consumed only in the next iteration (the vmcnt wait lands there).  The packed
+                // words are requested only by the lanes whose 16 bytes the unpack reads (8b words from
+                // word qoff <= 3, plus the next lane's first word): 2b + 2 lanes, not all 64.
                 const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pk) & ~(uintptr_t)15;
+#if defined(COVT_FPF_FULL_RAW)  // experiment: every lane loads
                 pr.raw = ld128(a16 + 16 * (uintptr_t)l);
+#else
+                pr.raw = l <= 2 * uni(hv.b) + 1 ? ld128(a16 + 16 * (uintptr_t)l) : make_uint4(0, 0, 0, 0);
+#endif
                 const int32_t k = h.idx;
                 const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
                 uint32_t xb;
