@@ -553,6 +553,25 @@ class DeviceBatch:
         self.d_out = torch.zeros(max(plan.output_bytes, 16), dtype=torch.uint8, device=self.device)
         self.d_res = torch.zeros(n * 2, dtype=torch.int32, device=self.device)
 
+    def decode_graph(self):
+        """The same launch replayed from a captured HIP graph on the current torch stream: the fork,
+        the four family kernels on their forked streams and the join become one graph launch, so
+        back-to-back decodes pay one submission instead of eleven stream operations."""
+        import torch
+
+        g = getattr(self, "_graph", None)
+        if g is None:
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):  # the fork streams and events exist before the capture
+                self.decode(side)
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.decode(torch.cuda.current_stream(self.device))
+            self._graph = g
+        g.replay()
+
     def decode(self, stream=None):
         import torch
 

@@ -88,6 +88,24 @@ def test_device_batch_equals_host_path(covt, gpu_available, decodable_tiles):
         assert np.array_equal(a, b), i
 
 
+def test_graph_replay_equals_launch(covt, gpu_available, decodable_tiles):
+    """DeviceBatch.decode_graph (the fork/join launch captured once as a HIP graph, then replayed)
+    writes exactly what the stream launch writes, replay after replay."""
+    import torch
+
+    plan = covt.Plan.from_tiles([t for _, t in decodable_tiles])
+    db = covt.DeviceBatch(plan, "cuda")
+    db.decode()
+    torch.cuda.synchronize()
+    ref_out, ref_res = db.d_out.clone(), db.d_res.clone()
+    for _ in range(3):
+        db.d_out.zero_()
+        db.d_res.fill_(-99)
+        db.decode_graph()
+        torch.cuda.synchronize()
+        assert torch.equal(db.d_out, ref_out) and torch.equal(db.d_res, ref_res)
+
+
 def test_multi_gpu_host_api_equals_single(covt, gpu_available, decodable_tiles):
     plan = covt.Plan.from_tiles([t for _, t in decodable_tiles[:40]])
     o1, r1 = plan.decode_host(1)
