@@ -156,6 +156,32 @@ def end_to_end(plan, batch, stream, torch, dev, reps):
             "note": "pinned host tile bytes + descriptors H2D, one decode launch, all outputs + results D2H"}
 
 
+def abi_host_leg(plan, t_plan, reps):
+    """The C-ABI host entry a JNI/ctypes caller would use (include/covt.h covt_plan_decode_host): pageable
+    tile bytes in, device buffers allocated per call, H2D, one decode launch, D2H into pageable host memory
+    (fresh buffers each call, so first-touch page faults are included).  Not `value`."""
+    plan.decode_host()  # warm: HIP context, allocator
+    t = time.perf_counter()
+    for _ in range(reps):
+        out, res = plan.decode_host()
+        if (res[:, 0] != 0).any():
+            raise RuntimeError("covt_plan_decode_host reported stream errors")
+        del out, res
+    ms = (time.perf_counter() - t) * 1e3 / reps
+    # the same call into caller-owned host buffers reused across calls (already touched: no page faults)
+    out, res = plan.decode_host()
+    t = time.perf_counter()
+    for _ in range(reps):
+        plan.decode_host(out=out, res=res)
+    ms_reuse = (time.perf_counter() - t) * 1e3 / reps
+    return {"ms": round(ms, 3), "value": round(plan.in_bytes / (ms * 1e-3) / 1e9, 3), "unit": "GB/s",
+            "ms_reused_buffers": round(ms_reuse, 3),
+            "raw_tiles_to_host_ms": round(ms + t_plan * 1e3, 1), "reps": reps,
+            "note": "covt_plan_decode_host wall clock (pageable bytes, per-call device alloc, H2D + decode + "
+                    "D2H) into fresh host buffers; ms_reused_buffers: into caller buffers reused across calls; "
+                    "raw_tiles_to_host_ms adds the host metadata walk (covt_plan_create)"}
+
+
 def assembly_leg(batch, plan, stream, args, dist, torch, dev):
     """GPU geometry assembly (nested offsets + ICE gather) over the decoded batch,
     timed on its own (decode output resident); not part of `value`."""
@@ -269,6 +295,8 @@ def main():
     ap.add_argument("--no-assemble", action="store_true", help="skip the geometry-assembly leg")
     ap.add_argument("--e2e-reps", type=int, default=3, help="end-to-end (PCIe-inclusive) reps; 0 skips")
     ap.add_argument("--no-props", action="store_true", help="skip the property-column leg")
+    ap.add_argument("--abi-host-reps", type=int, default=2,
+                    help="reps of the C-ABI host entry covt_plan_decode_host (pageable in/out); 0 skips")
     args = ap.parse_args()
 
     import torch
@@ -327,6 +355,9 @@ def main():
     e2e = None
     if args.e2e_reps > 0:
         e2e = end_to_end(plan, batch, stream, torch, dev, args.e2e_reps)
+    abi = None
+    if args.abi_host_reps > 0 and rank == 0:
+        abi = abi_host_leg(plan, t_plan, args.abi_host_reps)
     asm_line = None
     if not args.no_assemble and plan.num_geometry_columns:
         asm_line = assembly_leg(batch, plan, stream, args, dist, torch, dev)
@@ -396,6 +427,8 @@ def main():
             line["properties"] = props_line
         if e2e is not None:
             line["end_to_end"] = e2e
+        if abi is not None:
+            line["c_abi_host"] = abi
         line["host_plan_ms"] = round(t_plan * 1e3, 1)  # covt_plan_create metadata walk (+ packing), host
         if world == 1 and not args.no_cpu:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)

@@ -455,11 +455,19 @@ class Plan:
         except Exception:  # noqa: BLE001
             pass
 
-    def decode_host(self, n_gpus: int = 1):
+    def decode_host(self, n_gpus: int = 1, out=None, res=None):
         """H2D + decode + D2H of the whole plan (covt_plan_decode_host[_multi]).
-        Returns (uint8 output buffer, results[num_streams, 2] = (status, consumed)) in plan order."""
-        out = np.zeros(max(self.output_bytes, 1), dtype=np.uint8)
-        res = np.zeros((max(self.num_streams, 1), 2), dtype=np.int32)
+        Returns (uint8 output buffer, results[num_streams, 2] = (status, consumed)) in plan order.
+        `out` / `res` may be caller-owned buffers reused across calls (C-contiguous uint8 of at least
+        output_bytes, int32 of shape (>= num_streams, 2)); fresh zeroed ones are allocated otherwise."""
+        if out is None:
+            out = np.zeros(max(self.output_bytes, 1), dtype=np.uint8)
+        if res is None:
+            res = np.zeros((max(self.num_streams, 1), 2), dtype=np.int32)
+        if (out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < self.output_bytes
+                or res.dtype != np.int32 or not res.flags.c_contiguous or res.ndim != 2 or res.shape[1] != 2
+                or res.shape[0] < self.num_streams):
+            raise ValueError("decode_host: out/res buffers have the wrong dtype, layout or size")
         if n_gpus > 1:
             st = lib().covt_plan_decode_host_multi(self._h, _ptr(self.blob, C.c_uint8), self.blob.size, n_gpus,
                                                    out.ctypes.data, res.ctypes.data)

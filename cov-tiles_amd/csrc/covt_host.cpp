@@ -8,7 +8,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <sys/mman.h>
 #include <mutex>
 #include <numeric>
 #include <thread>
@@ -1017,8 +1019,43 @@ namespace {
 
 // Decode a subset of a plan's streams on the current device.  `sel` lists tile-order stream
 // indices; their inputs are the tiles in `tiles` (packed contiguously on the device).
+int decode_all(const covt_plan* p, const uint8_t* bytes, uint8_t* host_out, covt_stream_result* host_res);
+
+// Pageable caller memory for the D2H: fault its pages in on host threads (MADV_POPULATE_WRITE) while
+// the device runs H2D + decode, so the copy itself meets resident pages.  Into a fresh 4.5 GB buffer
+// the single-threaded first touch inside the copy otherwise costs ~3x the copy.
+// COVT_HOST_PREFAULT=0 turns it off.  Kernels without MADV_POPULATE_WRITE (< 5.14) touch each page.
+void prefault(uint8_t* p, size_t n) {
+    const char* e = std::getenv("COVT_HOST_PREFAULT");
+    if ((e && e[0] == '0') || n < (64u << 20)) return;
+#ifdef MADV_POPULATE_WRITE
+    const uintptr_t pg = 4096, lo = ((uintptr_t)p + pg - 1) & ~(pg - 1), hi = ((uintptr_t)p + n) & ~(pg - 1);
+    if (hi <= lo) return;
+    const size_t len = hi - lo;
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t nthr = std::max<size_t>(1, std::min<size_t>(8, hw ? hw : 1));
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < nthr; ++k) {
+        const uintptr_t a = lo + ((len * k / nthr) & ~(pg - 1));
+        const uintptr_t b = k + 1 == nthr ? hi : lo + ((len * (k + 1) / nthr) & ~(pg - 1));
+        th.emplace_back([=] {
+            if (madvise((void*)a, b - a, MADV_POPULATE_WRITE) == 0) return;
+            // older kernels: write each page's first byte back to itself (the copy overwrites it anyway)
+            for (uintptr_t q = a; q < b; q += pg) {
+                volatile uint8_t* v = (volatile uint8_t*)q;
+                *v = *v;
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+#else
+    (void)p;
+#endif
+}
+
 int decode_subset(const covt_plan* p, const uint8_t* bytes, const std::vector<int32_t>& tiles, uint8_t* host_out,
                   covt_stream_result* host_res) {
+    if (tiles.size() == (size_t)p->n_tiles) return decode_all(p, bytes, host_out, host_res);
     // pack the shard's tiles
     std::vector<int64_t> new_tile_off(p->n_tiles, -1);
     uint64_t in_total = 0;
@@ -1081,6 +1118,50 @@ int decode_subset(const covt_plan* p, const uint8_t* bytes, const std::vector<in
             host_res[(size_t)sel[k]] = res[k];
         }
     }
+    if (d_in) (void)hipFree(d_in);
+    if (d_out) (void)hipFree(d_out);
+    if (d_desc) (void)hipFree(d_desc);
+    if (d_res) (void)hipFree(d_res);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+// Every tile of the plan on one device: the caller's buffer already has the plan's layout, so the
+// plan's own descriptor table runs unchanged — one H2D of the tile bytes, one launch, one D2H straight
+// into host_out (no per-tile copies, no staging buffer, no per-stream scatter).  Padding between
+// output slices is zeroed on the device so host_out matches the subset path byte for byte.
+int decode_all(const covt_plan* p, const uint8_t* bytes, uint8_t* host_out, covt_stream_result* host_res) {
+    uint64_t extent = 0;
+    for (int32_t t = 0; t < p->n_tiles; ++t)
+        extent = std::max<uint64_t>(extent, p->tile_off[(size_t)t] + p->tile_size[(size_t)t]);
+    const size_t ns = p->descs.size();
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return COVT_ERR_DEVICE;
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    covt_stream_desc* d_desc = nullptr;
+    covt_stream_result* d_res = nullptr;
+    int st = COVT_OK;
+    std::vector<covt_stream_result> res(ns);
+    auto chk = [&](hipError_t e) { if (e != hipSuccess && st == COVT_OK) st = COVT_ERR_DEVICE; };
+    chk(hipMalloc(&d_in, extent + COVT_INPUT_PADDING));
+    chk(hipMalloc(&d_out, (size_t)std::max<int64_t>(p->out_bytes, 16)));
+    chk(hipMalloc(&d_desc, std::max<size_t>(ns, 1) * sizeof(covt_stream_desc)));
+    chk(hipMalloc(&d_res, std::max<size_t>(ns, 1) * sizeof(covt_stream_result)));
+    if (st == COVT_OK) {
+        if (extent) chk(hipMemcpyAsync(d_in, bytes, extent, hipMemcpyHostToDevice, s));
+        if (ns) chk(hipMemcpyAsync(d_desc, p->descs.data(), ns * sizeof(covt_stream_desc), hipMemcpyHostToDevice, s));
+        if (p->out_bytes) chk(hipMemsetAsync(d_out, 0, (size_t)p->out_bytes, s));
+        if (st == COVT_OK) st = launch_grouped(d_in, d_desc, p->fam_counts, d_out, d_res, s);
+        if (st == COVT_OK && ns)
+            chk(hipMemcpyAsync(res.data(), d_res, ns * sizeof(covt_stream_result), hipMemcpyDeviceToHost, s));
+        if (st == COVT_OK && p->out_bytes) {
+            prefault(host_out, (size_t)p->out_bytes);  // overlaps the device work queued above
+            chk(hipMemcpyAsync(host_out, d_out, (size_t)p->out_bytes, hipMemcpyDeviceToHost, s));
+        }
+        chk(hipStreamSynchronize(s));
+    }
+    if (st == COVT_OK)
+        for (size_t i = 0; i < p->info.size(); ++i) host_res[i] = res[(size_t)p->info[i].desc_index];
     if (d_in) (void)hipFree(d_in);
     if (d_out) (void)hipFree(d_out);
     if (d_desc) (void)hipFree(d_desc);

@@ -114,6 +114,34 @@ def test_multi_gpu_host_api_equals_single(covt, gpu_available, decodable_tiles):
     assert np.array_equal(o1, o2)
 
 
+def test_host_api_whole_plan_equals_subset_path(covt, gpu_available, decodable_tiles):
+    """covt_plan_decode_host: the whole-plan path (plan's own descriptor table, one D2H into host_out)
+    gives the same bytes as the per-tile subset path, which a plan with a failed tile takes; reused
+    caller buffers (dirty on entry) give the same bytes as fresh ones."""
+    good = [t for _, t in decodable_tiles[:60]]
+    whole = covt.Plan.from_tiles(good)
+    subset = covt.Plan.from_tiles(good + [b"\x01\x05garbage"])  # failed last tile: no streams, same layout
+    assert subset.tile_status[-1] != 0 and subset.output_bytes == whole.output_bytes
+    o1, r1 = whole.decode_host()
+    o2, r2 = subset.decode_host()
+    assert np.array_equal(r1, r2)
+    # every stream's output slice matches; the align-16 padding between slices is unspecified (the
+    # whole-plan path copies the device buffer as the kernels left it, the subset path only slices)
+    s = whole.streams
+    mask = np.zeros(whole.output_bytes, dtype=bool)
+    for off, n in zip(s["out_off"], s["out_elems"].astype(np.int64) * s["elem_bytes"]):
+        mask[off:off + n] = True
+    assert np.array_equal(o1[mask], o2[mask])
+    out = np.full(whole.output_bytes + 64, 0xAB, dtype=np.uint8)
+    res = np.full((whole.num_streams, 2), -7, dtype=np.int32)
+    for _ in range(2):
+        o3, r3 = whole.decode_host(out=out, res=res)
+        assert o3.ctypes.data == out.ctypes.data
+        assert np.array_equal(o3, o1) and np.array_equal(r3, r1)
+    with pytest.raises(ValueError):
+        whole.decode_host(out=np.zeros(1, dtype=np.uint8))
+
+
 def test_decode_covt_layers(covt, gpu_available, oracle):
     """CovtParser mirror returns the GeometryColumn record of CovtParser.java:29-36."""
     t = open(tile_paths(("omt",))[0].replace("10_530_682", "5_16_20"), "rb").read()
