@@ -7,11 +7,16 @@ uniform over the zoom levels that have decodable fixtures, then uniform over tha
 test/fixtures).  A "step" is one decode launch over the whole batch: every Id/Geometry stream of every
 tile, inputs (tile bytes + descriptor table) already resident in HBM, outputs written to HBM.
 
-  python bench.py [--gpus N --steps K --warmup W]     (N>1: torchrun, one rank per GPU)
+  python bench.py [--gpus N --steps K --warmup W]
 
-Scaling is weak by default: each rank decodes its own 10k-tile batch (seed 20250117 + rank), no
-collective on the data path (RCCL only for the timing barrier / max).  --scaling strong shards one
-10k-tile batch over the ranks with the greedy byte-balanced split of SURVEY §8(e).
+N>1: one process per GPU -- either started by torch.distributed.run (WORLD_SIZE/RANK/LOCAL_RANK in the
+environment) or, without a launcher, spawned here (one child per GPU, started before anything touches
+the GPU; fails if fewer than N GPUs are visible).  Scaling is weak by default: each rank decodes its own
+10k-tile batch (seed 20250117 + rank).  Tiles are independent, so there is no collective on the data
+path and no RCCL: a gloo group carries the timing barriers and gathers the per-rank numbers.
+--scaling strong shards one 10k-tile batch over the ranks with the greedy byte-balanced split of
+SURVEY §8(e).  Besides `value` (config 5) the line carries BASELINE configs 2-4 (`configs`), the
+PCIe-inclusive and C-ABI host timings, assembly and property legs, and the CPU baseline.
 """
 from __future__ import annotations
 
@@ -20,6 +25,8 @@ import glob
 import importlib.util
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -90,36 +97,64 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(picks, seconds, threads):
-    """The oracle (C restatement of the Java DecodingUtils semantics) on host cores: bounded sample."""
+def host_cpus():
+    """CPUs this process may actually run on: the affinity mask, capped by a cgroup-v2 CPU quota."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    n = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return n, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota}
+
+
+def cpu_baseline(plan, args):
+    """SURVEY §8(d) "CPU timing": the oracle (C restatement of the Java DecodingUtils semantics; the Java
+    decoder cannot run, §8(c)) built -O3 -march=native on this host, over the SAME batch as the GPU run
+    (every tile walked + every Id/Geometry stream decoded, one tile per task), all usable host cores:
+    median of >= 20 timed iterations after 3 warm-ups; plus a 1-thread figure on the same batch."""
+    import tempfile
+
     sys.path.insert(0, ROOT)
     import oracle as O
 
-    O.build()
-    covt = load_covt()
-    sample = picks[: min(len(picks), 400)]
-    blob, offs, sizes = covt.pack_tiles([t for _, t in sample])
-    st, ib, ob, vx = O.decode_tiles_mt(blob, offs, sizes, O.FMT_GENC, O.ID_FORMAT, threads)
-    if st != 0:
-        raise RuntimeError("oracle baseline failed: %d" % st)
-    def timed(nthr, secs):
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            O.decode_tiles_mt(blob, offs, sizes, O.FMT_GENC, O.ID_FORMAT, nthr)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el >= secs:
-                return reps, el
+    bdir = tempfile.mkdtemp(prefix="covt_oracle_native_")
+    try:
+        L = O.load_native(O.build_native(bdir))
+        march = "native"
+    except (OSError, subprocess.CalledProcessError):  # no compiler on this host: the portable in-tree build
+        L, march = O.lib(), "x86-64-v3"
+    threads, cpus = host_cpus()
+    threads = args.cpu_threads or threads
 
-    reps, el = timed(threads, seconds)
-    reps1, el1 = timed(1, max(seconds / 3, 1.0))
-    return {"value": round(ib * reps / el / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": "%d tiles of the same batch (%.1f MB stream bytes) x %d reps in %.1f s; "
-                      "C restatement of DecodingUtils (oracle/covt_oracle.c), %d threads" %
-                      (len(sample), ib / 1e6, reps, el, threads),
-            "mvert_per_s": round(vx * reps / el / 1e6, 3),
-            "value_1thread": round(ib * reps1 / el1 / 1e9, 4),
-            "host": {"cpu_model": cpu_model(), "nproc": os.cpu_count()}}
+    def run(nthr):
+        t = time.perf_counter()
+        st, ib, ob, vx = O.decode_tiles_mt(plan.blob, plan.offsets, plan.sizes, O.FMT_GENC, args.id_mode, nthr, L)
+        el = time.perf_counter() - t
+        if st != 0:
+            raise RuntimeError("oracle baseline failed: %d" % st)
+        return el, ib, vx
+
+    for _ in range(3):
+        run(threads)
+    times = [run(threads)[0] for _ in range(max(args.cpu_iters, 1))]
+    _, ib, vx = run(threads)
+    med = float(np.median(times))
+    el1, _, _ = run(1)  # 1 thread: one warm-up-free pass is already seconds long; take the median of 3
+    times1 = [el1] + [run(1)[0] for _ in range(2 if el1 < 10 else 0)]
+    med1 = float(np.median(times1))
+    return {"value": round(ib / med / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "the full bench batch (%d tiles, %.1f MB stream bytes), median of %d iterations after 3 "
+                      "warm-ups (%.1f ms); oracle/covt_oracle.c (C restatement of DecodingUtils + ORC + "
+                      "FastPFOR) built -O3 -march=%s here, %d threads, one tile per task" %
+                      (plan.n_tiles, ib / 1e6, len(times), med * 1e3, march, threads),
+            "mvert_per_s": round(vx / med / 1e6, 3),
+            "value_1thread": round(ib / med1 / 1e9, 4), "ms_1thread": round(med1 * 1e3, 1),
+            "iters_1thread": len(times1),
+            "host": dict(cpus, cpu_model=cpu_model())}
 
 
 def end_to_end(plan, batch, stream, torch, dev, reps):
@@ -281,6 +316,116 @@ def properties_leg(picks, args, dist, torch, dev, covt, stream):
                          "kernel": "covt::props_kernel (one wave per property (sub)column)"}}
 
 
+CONFIG_LEGS = {
+    # BASELINE.json configs[1..3]: stream selections of the reference's OMT fixtures
+    "config2": ("VertexBuffer Int32 ZigZag-delta-varint decode, one z5 tile (omt/5_16_20): its VERTEX_BUFFER "
+                "streams with encoding VARINT_DELTA_ZIG_ZAG (5 ICE_MORTON + 1 PLAIN)"),
+    "config3": "Full geometry column (RLE offsets + VertexBuffer), OMT z2-z8 batch: every geometry stream",
+    "config4": ("FastPFOR128 topology streams + Id column, OMT z9-z14 batch: FastPFOR non-VertexBuffer geometry "
+                "streams + every Id stream"),
+}
+
+
+def config_tiles(lib, name):
+    omt = {z: [(k, t) for k, t in tl if k.startswith("omt/")] for z, tl in lib.items()}
+    if name == "config2":
+        return [(k, t) for k, t in omt[5] if k == "omt/5_16_20"]
+    zs = range(2, 9) if name == "config3" else range(9, 15)
+    return [kt for z in zs for kt in omt.get(z, [])]
+
+
+def config_mask(plan, name):
+    st = plan.streams
+    geom = st["column_kind"] == 1
+    if name == "config2":
+        return geom & (st["stream_type"] == 9) & (st["encoding"] == 4)
+    if name == "config3":
+        return geom
+    return (geom & (st["encoding"] == 9) & (st["stream_type"] != 9)) | (st["column_kind"] == 0)
+
+
+def config_legs(lib, args, torch, dev, covt, stream):
+    """BASELINE configs 2-4 on one GPU: kernel-only time of one decode launch over exactly the config's
+    streams (inputs + descriptors resident, HIP events on the launch stream, mean of --steps after
+    --warmup), bit-exactness of those streams' statuses, and their own roofline.  Not `value`."""
+    out = {}
+    for name, desc in CONFIG_LEGS.items():
+        picks = config_tiles(lib, name)
+        plan = covt.Plan.from_tiles([t for _, t in picks], covt.FORMAT_GENC, args.id_mode)
+        mask = config_mask(plan, name)
+        batch = covt.DeviceBatch(plan, dev)
+        sub = batch.subset(mask)
+        with torch.cuda.stream(stream):
+            for _ in range(max(args.warmup, 1)):
+                sub.decode(stream)
+            torch.cuda.synchronize(dev)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(args.steps)]
+            for s, e in ev:
+                s.record(stream)
+                sub.decode(stream)
+                e.record(stream)
+            torch.cuda.synchronize(dev)
+        ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+        _, res, _ = sub.results()
+        if (res[:, 0] != 0).any():
+            raise RuntimeError("%s: decode reported errors on %d streams" % (name, int((res[:, 0] != 0).sum())))
+        st = plan.streams[mask]
+        ib = int(st["byte_length"].sum())
+        ob = int((st["out_elems"] * st["elem_bytes"]).sum())
+        vb = st[st["stream_type"] == 9]
+        vx = int(np.where((vb["column_type"] == 3) | (vb["column_type"] == 4), vb["num_values"],
+                          vb["num_values"] // 2).sum())
+        ach = (ib + ob) / (ms * 1e-3) / 1e9
+        out[name] = {"workload": desc, "tiles": len(picks), "streams": int(mask.sum()), "stream_bytes": ib,
+                     "output_bytes": ob, "vertices": vx, "kernel_ms": round(ms, 5),
+                     "gbps_raw": round(ib / (ms * 1e-3) / 1e9, 3),
+                     "mvert_per_s": round(vx / (ms * 1e-3) / 1e6, 3),
+                     "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(ach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": ib + ob}}
+        del sub, batch, plan
+    return out
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: one child process per GPU (RANK/LOCAL_RANK/WORLD_SIZE set
+    before the child touches the GPU), rank 0 prints the line.  This parent never initialises HIP."""
+    n = args.gpus
+    if not args.dry_run:
+        import torch
+
+        have = torch.cuda.device_count()  # does not initialise the GPU on this image
+        if have < n:
+            print("bench.py: --gpus %d but only %d GPU(s) visible" % (n, have), file=sys.stderr, flush=True)
+            sys.exit(2)
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            c = p.poll()
+            if c is None:
+                continue
+            alive.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in alive:  # a failed rank would leave the others waiting in a barrier
+                    q.kill()
+        time.sleep(0.05)
+    sys.exit(rc if rc >= 0 else 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -288,37 +433,52 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--tiles", type=int, default=10000)
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-iters", type=int, default=20, help="timed CPU-baseline iterations (after 3 warm-ups)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (default: all usable CPUs)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--id-mode", type=int, default=0)
     ap.add_argument("--no-assemble", action="store_true", help="skip the geometry-assembly leg")
     ap.add_argument("--e2e-reps", type=int, default=3, help="end-to-end (PCIe-inclusive) reps; 0 skips")
     ap.add_argument("--no-props", action="store_true", help="skip the property-column leg")
+    ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE config 2-4 legs")
     ap.add_argument("--abi-host-reps", type=int, default=2,
                     help="reps of the C-ABI host entry covt_plan_decode_host (pageable in/out); 0 skips")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: sample + plan per rank, time an empty step, print the aggregated line "
+                         "(tests the rank launch and aggregation on CPU)")
     args = ap.parse_args()
 
-    import torch
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        launch_ranks(args)  # exits
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr, flush=True)
+        sys.exit(2)
+
+    import torch
+
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
+        # tiles are independent: no collective on the data path, so no RCCL either --
+        # gloo carries the timing barriers and the max/sum of per-rank numbers on the host
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    if not args.dry_run:
+        if torch.cuda.device_count() < world:
+            raise SystemExit("bench.py: %d ranks but only %d GPU(s) visible" % (world, torch.cuda.device_count()))
+        dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev)
     covt = load_covt()
 
     lib = tile_library()
+    seed = SEED + rank if args.scaling == "weak" else SEED
     if args.scaling == "weak":
-        picks = sample_batch(lib, args.tiles, SEED + rank)
+        picks = sample_batch(lib, args.tiles, seed)
     else:
-        allp = sample_batch(lib, args.tiles, SEED)
+        allp = sample_batch(lib, args.tiles, seed)
         shards = lpt_shards([len(t) for _, t in allp], world)
         picks = [allp[i] for i in shards[rank]]
 
@@ -327,55 +487,69 @@ def main():
     t_plan = time.perf_counter() - t_plan
     if (plan.tile_status != 0).any():
         raise RuntimeError("tile walk failed")
-    batch = covt.DeviceBatch(plan, dev)
-    stream = torch.cuda.current_stream(dev)
 
-    for _ in range(args.warmup):
-        batch.decode(stream)
-    torch.cuda.synchronize(dev)
-    _, res = batch.results()
-    if (res[:, 0] != 0).any():
-        raise RuntimeError("decode reported errors on %d streams" % int((res[:, 0] != 0).sum()))
+    def barrier():
+        if dist is not None:
+            dist.barrier()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
-        batch.decode(stream)
-        e.record(stream)
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-
-    e2e = None
-    if args.e2e_reps > 0:
-        e2e = end_to_end(plan, batch, stream, torch, dev, args.e2e_reps)
-    abi = None
-    if args.abi_host_reps > 0 and rank == 0:
-        abi = abi_host_leg(plan, t_plan, args.abi_host_reps)
-    asm_line = None
-    if not args.no_assemble and plan.num_geometry_columns:
-        asm_line = assembly_leg(batch, plan, stream, args, dist, torch, dev)
-    props_line = None
-    if not args.no_props:
-        props_line = properties_leg(picks, args, dist, torch, dev, covt, stream)
-
-    stats = torch.tensor([wall, float(plan.in_bytes), float(plan.vertices), float(plan.out_bytes), kern_ms],
-                         dtype=torch.float64, device=dev)
-    if dist is not None:
-        mx = stats.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = stats.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        wall, kern_ms = float(mx[0]), float(mx[4])
-        tot_in, tot_vx = float(sm[1]), float(sm[2])
+    if args.dry_run:
+        barrier()
+        t0 = time.perf_counter()
+        barrier()
+        wall = time.perf_counter() - t0
+        kern_ms = wall * 1e3 / max(args.steps, 1)
+        dev_name = "cpu (dry run)"
     else:
-        tot_in, tot_vx = float(plan.in_bytes), float(plan.vertices)
+        batch = covt.DeviceBatch(plan, dev)
+        stream = torch.cuda.current_stream(dev)
+        dev_name = torch.cuda.get_device_name(dev)
+        for _ in range(args.warmup):
+            batch.decode(stream)
+        torch.cuda.synchronize(dev)
+        _, res = batch.results()
+        if (res[:, 0] != 0).any():
+            raise RuntimeError("decode reported errors on %d streams" % int((res[:, 0] != 0).sum()))
+
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for s, e in ev:
+            s.record(stream)
+            batch.decode(stream)
+            e.record(stream)
+        torch.cuda.synchronize(dev)
+        barrier()
+        wall = time.perf_counter() - t0
+        kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    legs = {}
+    if not args.dry_run:
+        if args.e2e_reps > 0:
+            legs["end_to_end"] = end_to_end(plan, batch, stream, torch, dev, args.e2e_reps)
+        if args.abi_host_reps > 0 and rank == 0:
+            legs["c_abi_host"] = abi_host_leg(plan, t_plan, args.abi_host_reps)
+        if not args.no_assemble and plan.num_geometry_columns:
+            legs["assembly"] = assembly_leg(batch, plan, stream, args, dist, torch, dev)
+        if not args.no_props:
+            legs["properties"] = properties_leg(picks, args, dist, torch, dev, covt, stream)
+        if not args.no_configs and rank == 0 and world == 1:
+            legs["configs"] = config_legs(lib, args, torch, dev, covt, stream)
+
+    mine = {"rank": rank, "device": dev_name, "local_rank": local_rank, "seed": seed, "tiles": len(picks),
+            "stream_bytes": int(plan.in_bytes), "vertices": int(plan.vertices), "wall_s": wall,
+            "kernel_ms": kern_ms}
+    if dist is not None:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    else:
+        ranks = [mine]
+    wall = max(r["wall_s"] for r in ranks)
+    kern_ms = max(r["kernel_ms"] for r in ranks)
+    tot_in = float(sum(r["stream_bytes"] for r in ranks))
+    tot_vx = float(sum(r["vertices"] for r in ranks))
 
     if rank == 0:
         ms_per_step = wall * 1e3 / args.steps
@@ -396,7 +570,7 @@ def main():
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "GB/s",
-            "n_gpus": world,
+            "n_gpus": len(ranks),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
@@ -410,31 +584,30 @@ def main():
                        "tiles_per_gpu": len(picks), "streams_per_gpu": plan.num_streams,
                        "stream_bytes_per_gpu": plan.in_bytes, "output_bytes_per_gpu": plan.out_bytes,
                        "vertices_per_gpu": plan.vertices, "id_mode": "format" if args.id_mode == 0 else "java",
-                       "parallelism": "dp%d (tile shards, no collective)" % world},
+                       "parallelism": "dp%d (tile shards, no collective)" % len(ranks)},
             "mvert_per_s": round(tot_vx * args.steps / wall / 1e6, 2),
             "kernel_ms": round(kern_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "covt decode launch = decode_family_kernel<RLE|VARINT|FASTPFOR> + "
                                    "decode_lane_kernel run concurrently between fork/join events; "
-                                   "duration = HIP events on the launch stream",
+                                   "duration = HIP events on the launch stream (max over ranks)",
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": None,
+            "per_rank": [{"rank": r["rank"], "device": r["device"], "seed": r["seed"], "tiles": r["tiles"],
+                          "kernel_ms": round(r["kernel_ms"], 4),
+                          "gbps": round(r["stream_bytes"] * args.steps / r["wall_s"] / 1e9, 3)
+                          if r["wall_s"] > 0 else None} for r in ranks],
         }
-        if asm_line is not None:
-            line["assembly"] = asm_line
-        if props_line is not None:
-            line["properties"] = props_line
-        if e2e is not None:
-            line["end_to_end"] = e2e
-        if abi is not None:
-            line["c_abi_host"] = abi
+        line.update(legs)
         line["host_plan_ms"] = round(t_plan * 1e3, 1)  # covt_plan_create metadata walk (+ packing), host
-        if world == 1 and not args.no_cpu:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(picks, args.cpu_seconds, threads)
+        if len(ranks) == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(plan, args)
+        if args.dry_run:
+            line["dry_run"] = True
         print(json.dumps(line), flush=True)
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
 
 

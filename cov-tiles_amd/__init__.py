@@ -154,7 +154,8 @@ EXPORTED_SYMBOLS = (
     "covt_plan_geometry_descs", "covt_assemble_geometry_device", "covt_plan_assemble_host",
     "covt_plan_create_ex", "covt_plan_num_property_columns", "covt_plan_property_bytes",
     "covt_plan_property_columns", "covt_plan_property_descs", "covt_materialize_properties_device",
-    "covt_plan_properties_host",
+    "covt_plan_properties_host", "covt_decode_byte_rle_reencode", "covt_decode_floats_le", "covt_decode_string",
+    "covt_plan_decode_host_shards", "covt_plan_release_device",
 )
 
 
@@ -210,6 +211,11 @@ def lib() -> C.CDLL:
     L.covt_plan_family_counts.argtypes = [vp, i64p]
     L.covt_plan_decode_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
     L.covt_plan_decode_host_multi.argtypes = [vp, u8p, C.c_uint64, C.c_int32, vp, vp]
+    L.covt_plan_decode_host_shards.argtypes = [vp, u8p, C.c_uint64, C.c_int32, i32p, vp, vp]
+    L.covt_plan_release_device.argtypes = [vp]
+    L.covt_decode_byte_rle_reencode.argtypes = [u8p, sz, C.c_int32, i32p, u8p]
+    L.covt_decode_floats_le.argtypes = [u8p, sz, i32p, C.c_int32, C.POINTER(C.c_float)]
+    L.covt_decode_string.argtypes = [u8p, sz, i32p, i32p, i32p]
     L.covt_plan_num_geometry_columns.argtypes = [vp]
     L.covt_plan_num_geometry_columns.restype = C.c_int64
     L.covt_plan_assembly_bytes.argtypes = [vp]
@@ -336,15 +342,49 @@ class DecodingUtils:
         return out[:numValues]
 
     @staticmethod
-    def decodeByteRle(buffer, numValues: int, pos: IntWrapper, byteLength: int) -> np.ndarray:  # :275
+    def decodeByteRle(buffer, numValues: int, pos: IntWrapper, byteLength: Optional[int] = None) -> np.ndarray:
+        """:275 (with byteLength: advance by it) and the :290 overload (without: advance by the length
+        of the values' ORC re-encoding, as CovtParser.java:295 relies on for Gen D present streams)."""
         pos = _cursor(pos)
         a = _u8(buffer)
         out = np.zeros(max(numValues, 1), dtype=np.uint8)
         p = C.c_int32(pos.get())
-        _raise(lib().covt_decode_byte_rle(_ptr(a, C.c_uint8), a.size, numValues, C.byref(p), byteLength,
-                                          _ptr(out, C.c_uint8)), "decodeByteRle")
+        if byteLength is None:
+            st = lib().covt_decode_byte_rle_reencode(_ptr(a, C.c_uint8), a.size, numValues, C.byref(p),
+                                                     _ptr(out, C.c_uint8))
+        else:
+            st = lib().covt_decode_byte_rle(_ptr(a, C.c_uint8), a.size, numValues, C.byref(p), byteLength,
+                                            _ptr(out, C.c_uint8))
+        _raise(st, "decodeByteRle")
         pos.set(p.value)
         return out[:numValues]
+
+    @staticmethod
+    def decodeFloatsLE(encodedValues, pos: IntWrapper, numValues: int) -> np.ndarray:  # :446
+        pos = _cursor(pos)
+        a = _u8(encodedValues)
+        out = np.zeros(max(numValues, 1), dtype=np.float32)
+        p = C.c_int32(pos.get())
+        _raise(lib().covt_decode_floats_le(_ptr(a, C.c_uint8), a.size, C.byref(p), numValues,
+                                           out.ctypes.data_as(C.POINTER(C.c_float))), "decodeFloatsLE")
+        pos.set(p.value)
+        return out[:numValues]
+
+    @staticmethod
+    def decodeString(content, pos: IntWrapper, numChars: Optional[int] = None) -> str:  # :21 / :28
+        pos = _cursor(pos)
+        a = _u8(content)
+        if numChars is not None:  # :28 -- the caller knows the length
+            if pos.get() < 0 or pos.get() + numChars > a.size or numChars < 0:
+                _raise(ERR_TRUNCATED, "decodeString")
+            s = bytes(a[pos.get():pos.get() + numChars]).decode("utf-8", errors="replace")
+            pos.set(pos.get() + numChars)
+            return s
+        p, off, ln = C.c_int32(pos.get()), C.c_int32(), C.c_int32()
+        _raise(lib().covt_decode_string(_ptr(a, C.c_uint8), a.size, C.byref(p), C.byref(off), C.byref(ln)),
+               "decodeString")
+        pos.set(p.value)
+        return bytes(a[off.value:off.value + ln.value]).decode("utf-8", errors="replace")
 
     @staticmethod
     def _fpf(fn, buf, n, byte_length, pos, out_n, extra, what):
@@ -455,7 +495,11 @@ class Plan:
         except Exception:  # noqa: BLE001
             pass
 
-    def decode_host(self, n_gpus: int = 1, out=None, res=None):
+    def release_device(self):
+        """Free the device buffers decode_host cached on this plan (covt_plan_release_device)."""
+        _raise(lib().covt_plan_release_device(self._h), "covt_plan_release_device")
+
+    def decode_host(self, n_gpus: int = 1, out=None, res=None, shard_devices=None):
         """H2D + decode + D2H of the whole plan (covt_plan_decode_host[_multi]).
         Returns (uint8 output buffer, results[num_streams, 2] = (status, consumed)) in plan order.
         `out` / `res` may be caller-owned buffers reused across calls (C-contiguous uint8 of at least
@@ -468,7 +512,11 @@ class Plan:
                 or res.dtype != np.int32 or not res.flags.c_contiguous or res.ndim != 2 or res.shape[1] != 2
                 or res.shape[0] < self.num_streams):
             raise ValueError("decode_host: out/res buffers have the wrong dtype, layout or size")
-        if n_gpus > 1:
+        if shard_devices is not None:
+            devs = np.ascontiguousarray(shard_devices, dtype=np.int32)
+            st = lib().covt_plan_decode_host_shards(self._h, _ptr(self.blob, C.c_uint8), self.blob.size, devs.size,
+                                                    _ptr(devs, C.c_int32), out.ctypes.data, res.ctypes.data)
+        elif n_gpus > 1:
             st = lib().covt_plan_decode_host_multi(self._h, _ptr(self.blob, C.c_uint8), self.blob.size, n_gpus,
                                                    out.ctypes.data, res.ctypes.data)
         else:
@@ -536,6 +584,23 @@ class Plan:
         return GeoArrowGeometry(seg(0, int(g["n_features"]) + 1), seg(1, int(r["num_parts"]) + 1),
                                 seg(2, int(r["num_rings"]) + 1), seg(3, 2 * int(r["num_coords"])).reshape(-1, 2))
 
+    def subset_descs(self, mask):
+        """Descriptor table of the streams selected by `mask` (bool per stream, plan order), in launch
+        order (still grouped by family, largest first inside a family) -> (uint8 descs, family counts,
+        plan-order stream index per selected descriptor).  Outputs keep their slices in the full output
+        buffer; results land at the subset position."""
+        mask = np.asarray(mask, dtype=bool)
+        if mask.shape != (self.num_streams,):
+            raise ValueError("subset mask must have one entry per stream")
+        keep = np.zeros(self.num_streams, dtype=bool)
+        keep[self.streams["desc_index"][mask]] = True
+        fam = np.repeat(np.arange(NUM_FAMILIES), self.family_counts)
+        inv = np.empty(self.num_streams, dtype=np.int64)
+        inv[self.streams["desc_index"]] = np.arange(self.num_streams)
+        descs = np.ascontiguousarray(self.descs.reshape(-1, 32)[keep]).reshape(-1)
+        counts = np.bincount(fam[keep], minlength=NUM_FAMILIES).astype(np.int64)
+        return descs, counts, inv[keep]
+
     def stream_array(self, out: np.ndarray, i: int) -> np.ndarray:
         s = self.streams[i]
         dt = {1: np.uint8, 4: np.int32, 8: np.int64}[int(s["elem_bytes"])]
@@ -588,6 +653,41 @@ class DeviceBatch:
                                                       _ptr(self.plan.family_counts, C.c_int64),
                                                       self.d_out.data_ptr(), self.d_res.data_ptr(), s.cuda_stream)
         _raise(st, "covt_decode_streams_device_grouped")
+
+    def subset(self, mask) -> "DeviceSubset":
+        """A launch over only the streams selected by `mask` (Plan.subset_descs), sharing this batch's
+        device input and output buffers."""
+        return DeviceSubset(self, mask)
+
+
+class DeviceSubset:
+    """One decode launch over a subset of a DeviceBatch's streams (e.g. BASELINE configs 2-4, which are
+    stream selections of fixture tiles); its own descriptor table and result array on the device."""
+
+    def __init__(self, batch: DeviceBatch, mask):
+        import torch
+
+        self.batch = batch
+        descs, self.family_counts, self.stream_index = batch.plan.subset_descs(mask)
+        self.num_streams = int(self.stream_index.size)
+        self.d_desc = torch.from_numpy(descs).to(batch.device) if self.num_streams else \
+            torch.zeros(32, dtype=torch.uint8, device=batch.device)
+        self.d_res = torch.zeros(max(self.num_streams, 1) * 2, dtype=torch.int32, device=batch.device)
+
+    def decode(self, stream=None):
+        import torch
+
+        b = self.batch
+        s = stream if stream is not None else torch.cuda.current_stream(b.device)
+        _raise(lib().covt_decode_streams_device_grouped(b.d_in.data_ptr(), self.d_desc.data_ptr(),
+                                                        _ptr(self.family_counts, C.c_int64), b.d_out.data_ptr(),
+                                                        self.d_res.data_ptr(), s.cuda_stream),
+               "covt_decode_streams_device_grouped")
+
+    def results(self):
+        """(full output bytes, results[num_streams, 2] of the subset in launch order, plan-order index)."""
+        out = self.batch.d_out.cpu().numpy()[:self.batch.plan.output_bytes]
+        return out, self.d_res.cpu().numpy().reshape(-1, 2)[:self.num_streams], self.stream_index
 
     def _asm_buffers(self):
         import torch

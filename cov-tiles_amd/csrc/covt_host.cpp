@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <sys/mman.h>
+#include <memory>
 #include <mutex>
 #include <numeric>
 #include <thread>
@@ -445,12 +446,76 @@ int run_one(const uint8_t* region, size_t region_len, size_t pad_to, int op, int
 }
 
 // stream-level wrappers: varint / RLE ops read [pos, buf_len) (Java reads up to the array end)
+// Most bytes decoding n values of `op` can read from *pos on: Java's capped varints take <= 4 bytes
+// each (DecodingUtils.java:157-186); an ORC RLE reader reads whole groups, so past n values it may
+// still read the rest of the last group (<= 128 literal varints of <= 10 bytes, RunLengthIntegerReader;
+// <= 128 literal bytes, RunLengthByteReader).  The stream-level calls copy only that much of the
+// caller's array to the device instead of everything up to its end.
+size_t max_stream_bytes(int op, int32_t n) {
+    const size_t v = (size_t)std::max(n, 0);
+    switch (op) {
+        case COVT_OP_RLE_U64: case COVT_OP_RLE_S64: case COVT_OP_RLE_I32: return 11 * v + 2 + 128 * 10;
+        case COVT_OP_BYTE_RLE_RAW: case COVT_OP_BYTE_RLE_U8: return 2 * v + 1 + 128;
+        case COVT_OP_VARINT_U64: return 10 * v;
+        default: return 4 * v;  // 4-byte-capped int32 varints (x,y coordinates: num_values varints)
+    }
+}
+
+// Length of ORC RunLengthByteWriter's encoding of v[0..n) (orc-core 1.8.1; EncodingUtils.encodeByteRle,
+// EncodingUtils.java:123-135): runs of 3..130 equal bytes -> 2 bytes, literal groups of <= 128 -> 1 + k.
+int64_t orc_byte_rle_length(const uint8_t* v, int32_t n) {
+    constexpr int kMinRepeat = 3, kMaxLiteral = 128, kMaxRepeat = 127 + kMinRepeat;
+    int64_t len = 0;
+    int num = 0, tail = 0;
+    bool repeat = false;
+    uint8_t first = 0, last = 0;
+    auto flush = [&] {
+        if (num) len += repeat ? 2 : 1 + num;
+        repeat = false;
+        tail = num = 0;
+    };
+    for (int32_t i = 0; i < n; ++i) {
+        const uint8_t x = v[i];
+        if (num == 0) {
+            first = last = x;
+            num = tail = 1;
+        } else if (repeat) {
+            if (x == first) {
+                if (++num == kMaxRepeat) flush();
+            } else {
+                flush();
+                first = last = x;
+                num = tail = 1;
+            }
+        } else {
+            tail = x == last ? tail + 1 : 1;
+            if (tail == kMinRepeat) {
+                if (num + 1 == kMinRepeat) {
+                    repeat = true;
+                    ++num;
+                } else {
+                    num -= kMinRepeat - 1;  // the literal prefix before the run is written first
+                    flush();
+                    first = x;
+                    repeat = true;
+                    num = kMinRepeat;
+                }
+            } else {
+                last = x;
+                if (++num == kMaxLiteral) flush();
+            }
+        }
+    }
+    flush();
+    return len;
+}
+
 int stream_call(const uint8_t* buf, size_t buf_len, int32_t* pos, int op, int32_t n, int nb, void* out,
                 size_t elem_bytes, size_t out_elems) {
     if (!pos || n < 0 || (!buf && buf_len) || (!out && out_elems)) return COVT_ERR_INVALID_ARG;
     if (*pos < 0 || (size_t)*pos > buf_len) return COVT_ERR_TRUNCATED;
     covt_stream_result r{};
-    const size_t rl = buf_len - (size_t)*pos;
+    const size_t rl = std::min(buf_len - (size_t)*pos, max_stream_bytes(op, n));
     int st = run_one(buf + *pos, rl, 0, op, n, 0, nb, out, elem_bytes * out_elems, &r);
     if (st) return st;
     if (r.status) return r.status;
@@ -471,28 +536,63 @@ int fpf_call(const uint8_t* buf, size_t buf_len, int32_t* pos, int op, int32_t n
     return COVT_OK;
 }
 
-// Fork/join of the three family kernels: RLE on the caller's stream, varint and FastPFOR on two
-// per-thread auxiliary streams ordered by events (capturable into a hipGraph).
+// Fork/join of the family kernels: RLE on the caller's stream, the other three on auxiliary
+// streams ordered by events (capturable into a hipGraph).  The auxiliary streams and events come
+// from a process-wide per-device pool: a launch takes a set, enqueues, and hands it back, so
+// concurrent callers (one host thread per device, JNI threads) never share one and nothing leaks
+// when threads come and go; the pool holds as many sets as launches ever overlapped.
 struct ForkCtx {
     int device = -1;
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};
     hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
 };
+std::mutex g_fork_mu;
+std::vector<ForkCtx*> g_fork_free;
+
+void fork_destroy(ForkCtx* f) {
+    for (int i = 0; i < 3; ++i) {
+        if (f->aux[i]) (void)hipStreamDestroy(f->aux[i]);
+        if (f->join[i]) (void)hipEventDestroy(f->join[i]);
+    }
+    if (f->fork) (void)hipEventDestroy(f->fork);
+    delete f;
+}
+ForkCtx* fork_acquire(int dev) {
+    {
+        std::lock_guard<std::mutex> g(g_fork_mu);
+        for (size_t i = 0; i < g_fork_free.size(); ++i)
+            if (g_fork_free[i]->device == dev) {
+                ForkCtx* f = g_fork_free[i];
+                g_fork_free.erase(g_fork_free.begin() + (std::ptrdiff_t)i);
+                return f;
+            }
+    }
+    auto* f = new ForkCtx();
+    f->device = dev;
+    bool ok = true;
+    for (int i = 0; i < 3 && ok; ++i)
+        ok = hipStreamCreateWithFlags(&f->aux[i], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&f->join[i], hipEventDisableTiming) == hipSuccess;
+    if (ok) ok = hipEventCreateWithFlags(&f->fork, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        fork_destroy(f);
+        return nullptr;
+    }
+    return f;
+}
+void fork_release(ForkCtx* f) {
+    std::lock_guard<std::mutex> g(g_fork_mu);
+    g_fork_free.push_back(f);
+}
 
 int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const int64_t counts[COVT_NUM_FAMILIES],
                    uint8_t* d_out, covt_stream_result* d_res, hipStream_t s) {
-    thread_local ForkCtx f;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return COVT_ERR_DEVICE;
-    if (f.device != dev) {
-        f = ForkCtx{};
-        f.device = dev;
-        for (int i = 0; i < 3; ++i) {
-            if (hipStreamCreateWithFlags(&f.aux[i], hipStreamNonBlocking) != hipSuccess) return COVT_ERR_DEVICE;
-            if (hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming) != hipSuccess) return COVT_ERR_DEVICE;
-        }
-        if (hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess) return COVT_ERR_DEVICE;
-    }
+    ForkCtx* fp = fork_acquire(dev);
+    if (!fp) return COVT_ERR_DEVICE;
+    struct Back { ForkCtx* f; ~Back() { fork_release(f); } } back{fp};
+    ForkCtx& f = *fp;
     const int64_t o1 = counts[0], o2 = o1 + counts[1], o3 = o2 + counts[2];
     if (hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
     for (int i = 0; i < 3; ++i)
@@ -513,6 +613,116 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
 // ================================================================================================
 // C-ABI
 // ================================================================================================
+namespace {
+
+// Pageable caller memory for the D2H: fault its pages in on host threads (MADV_POPULATE_WRITE) while
+// the device runs H2D + decode, so the copy itself meets resident pages.  Started
+// before the H2D is queued and joined just before the output D2H.  COVT_HOST_PREFAULT=0 turns it
+// off.  Kernels without MADV_POPULATE_WRITE (< 5.14) touch each page.
+struct Prefault {
+    std::vector<std::thread> th;
+    Prefault(uint8_t* p, size_t n) {
+        const char* e = std::getenv("COVT_HOST_PREFAULT");
+        if ((e && e[0] == '0') || n < (64u << 20)) return;
+#ifdef MADV_POPULATE_WRITE
+        const uintptr_t pg = 4096, lo = ((uintptr_t)p + pg - 1) & ~(pg - 1), hi = ((uintptr_t)p + n) & ~(pg - 1);
+        if (hi <= lo) return;
+        const size_t len = hi - lo;
+        const unsigned hw = std::thread::hardware_concurrency();
+        const size_t nthr = std::max<size_t>(1, std::min<size_t>(8, hw ? hw : 1));
+        for (size_t k = 0; k < nthr; ++k) {
+            const uintptr_t a = lo + ((len * k / nthr) & ~(pg - 1));
+            const uintptr_t b = k + 1 == nthr ? hi : lo + ((len * (k + 1) / nthr) & ~(pg - 1));
+            th.emplace_back([=] {
+                if (madvise((void*)a, b - a, MADV_POPULATE_WRITE) == 0) return;
+                // older kernels: write each page's first byte back to itself (the copy overwrites it)
+                for (uintptr_t q = a; q < b; q += pg) {
+                    volatile uint8_t* v = (volatile uint8_t*)q;
+                    *v = *v;
+                }
+            });
+        }
+#else
+        (void)p;
+#endif
+    }
+    void join() {
+        for (auto& t : th) t.join();
+        th.clear();
+    }
+    ~Prefault() { join(); }
+};
+
+}  // namespace
+
+// One shard of a plan for the host entry points: a contiguous tile range, its descriptor table
+// rebased to that range (built once), and the device buffers, kept on the plan across calls.
+struct HostShard {
+    int device = -1;
+    uint64_t in_lo = 0, in_len = 0;  // caller bytes [in_lo, in_lo + in_len) -> d_in
+    int64_t out_lo = 0, out_len = 0; // plan output bytes [out_lo, out_lo + out_len) <- d_out
+    std::vector<covt_stream_desc> descs;  // launch order, offsets rebased
+    std::vector<int64_t> stream;          // plan-order stream index of each descriptor
+    int64_t fam[COVT_NUM_FAMILIES] = {0, 0, 0, 0};
+    std::vector<covt_stream_result> res;
+    hipStream_t s = nullptr;
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    covt_stream_desc* d_desc = nullptr;
+    covt_stream_result* d_res = nullptr;
+
+    ~HostShard() {
+        if (device < 0) return;
+        int cur = 0;
+        const bool have = hipGetDevice(&cur) == hipSuccess;
+        (void)hipSetDevice(device);
+        if (s) (void)hipStreamSynchronize(s);
+        for (void* q : {(void*)d_in, (void*)d_out, (void*)d_desc, (void*)d_res})
+            if (q) (void)hipFree(q);
+        if (s) (void)hipStreamDestroy(s);
+        if (have) (void)hipSetDevice(cur);
+    }
+
+    // device buffers + the descriptor upload, once per shard (on the calling thread's device)
+    int open() {
+        if (s) return COVT_OK;
+        if (hipSetDevice(device) != hipSuccess) return COVT_ERR_DEVICE;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return COVT_ERR_DEVICE;
+        const size_t nd = descs.size();
+        if (hipMalloc(&d_in, in_len + COVT_INPUT_PADDING) != hipSuccess ||
+            hipMalloc(&d_out, (size_t)std::max<int64_t>(out_len, 16)) != hipSuccess ||
+            hipMalloc(&d_desc, std::max<size_t>(nd, 1) * sizeof(covt_stream_desc)) != hipSuccess ||
+            hipMalloc(&d_res, std::max<size_t>(nd, 1) * sizeof(covt_stream_result)) != hipSuccess)
+            return COVT_ERR_DEVICE;
+        if ((uintptr_t)d_in & 15) return COVT_ERR_DEVICE;
+        // the read-ahead tail past the last tile byte is defined (zero); the H2D never overwrites it
+        if (hipMemsetAsync(d_in + in_len, 0, COVT_INPUT_PADDING, s) != hipSuccess) return COVT_ERR_DEVICE;
+        if (nd && hipMemcpyAsync(d_desc, descs.data(), nd * sizeof(covt_stream_desc), hipMemcpyHostToDevice, s) !=
+                      hipSuccess)
+            return COVT_ERR_DEVICE;
+        return hipStreamSynchronize(s) == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
+    }
+
+    // one H2D of the shard's tile bytes, one grouped launch, one D2H straight into the caller's buffer
+    int run(const uint8_t* bytes, uint8_t* host_out, covt_stream_result* host_res) {
+        int st = open();
+        if (st) return st;
+        if (descs.empty()) return COVT_OK;
+        auto chk = [&](hipError_t e) { if (e != hipSuccess && st == COVT_OK) st = COVT_ERR_DEVICE; };
+        Prefault pf(host_out + out_lo, (size_t)out_len);
+        if (in_len) chk(hipMemcpyAsync(d_in, bytes + in_lo, in_len, hipMemcpyHostToDevice, s));
+        if (st == COVT_OK) st = launch_grouped(d_in, d_desc, fam, d_out, d_res, s);
+        if (st == COVT_OK) chk(hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(covt_stream_result),
+                                              hipMemcpyDeviceToHost, s));
+        pf.join();
+        if (st == COVT_OK && out_len)
+            chk(hipMemcpyAsync(host_out + out_lo, d_out, (size_t)out_len, hipMemcpyDeviceToHost, s));
+        chk(hipStreamSynchronize(s));
+        if (st == COVT_OK)
+            for (size_t k = 0; k < stream.size(); ++k) host_res[(size_t)stream[k]] = res[k];
+        return st;
+    }
+};
+
 struct covt_plan {
     int32_t n_tiles = 0;
     std::vector<int32_t> tile_status;
@@ -529,6 +739,10 @@ struct covt_plan {
     std::vector<uint16_t> pflags;        // their COVT_PROP_* flags
     std::vector<covt_prop_desc> pdescs;  // launch order: largest first
     int64_t prop_bytes = 0;
+    // host entry points (covt_plan_decode_host*): shards with device buffers kept across calls
+    mutable std::mutex host_mu;
+    mutable std::vector<int32_t> host_devs;
+    mutable std::vector<std::unique_ptr<HostShard>> host_shards;
 };
 
 namespace {
@@ -805,6 +1019,47 @@ int covt_decode_byte_rle(const uint8_t* buf, size_t buf_len, int32_t n, int32_t*
     if (!st) *pos = p0 + byte_length;
     return st;
 }
+// decodeByteRle(byte[], int, IntWrapper) (DecodingUtils.java:290-306) advances by the length of the
+// values' re-encoding (getByteRleChunkSize :312-314 -> EncodingUtils.encodeByteRle, i.e. ORC
+// RunLengthByteWriter): decoded on the GPU like :275, then the writer's output length is computed
+// here from the decoded bytes (the Java code re-encodes them on the host as well).
+int covt_decode_byte_rle_reencode(const uint8_t* buf, size_t buf_len, int32_t n, int32_t* pos, uint8_t* out) {
+    if (!pos) return COVT_ERR_INVALID_ARG;
+    const int32_t p0 = *pos;
+    int st = stream_call(buf, buf_len, pos, COVT_OP_BYTE_RLE_RAW, n, 0, out, 1, (size_t)std::max(n, 0));
+    if (st) return st;
+    *pos = p0 + (int32_t)orc_byte_rle_length(out, n);
+    return COVT_OK;
+}
+// decodeFloatsLE(byte[], IntWrapper, int) (DecodingUtils.java:446-453): a little-endian view of
+// numValues*4 bytes (no decode arithmetic; the batch path reads float columns in place on the GPU).
+int covt_decode_floats_le(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t n, float* out) {
+    if (!pos || n < 0 || (!buf && buf_len) || (!out && n)) return COVT_ERR_INVALID_ARG;
+    if (*pos < 0 || (size_t)*pos + 4 * (size_t)n > buf_len) return COVT_ERR_TRUNCATED;  // ByteBuffer.wrap bounds
+    if (n) std::memcpy(out, buf + *pos, 4 * (size_t)n);
+    *pos += 4 * n;
+    return COVT_OK;
+}
+// decodeString(byte[], IntWrapper) (DecodingUtils.java:21-26): a 4-byte-capped varint length
+// (decodeVarint(src, pos) :189-194), then that many UTF-8 bytes; returns where they are.
+int covt_decode_string(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t* str_off, int32_t* str_len) {
+    if (!pos || !str_off || !str_len || (!buf && buf_len)) return COVT_ERR_INVALID_ARG;
+    if (*pos < 0) return COVT_ERR_TRUNCATED;
+    size_t q = (size_t)*pos;
+    uint32_t v = 0;
+    for (int k = 0; k < 4; ++k) {  // Java's cap: the 4th byte is always the last
+        if (q >= buf_len) return COVT_ERR_TRUNCATED;
+        const uint8_t b = buf[q++];
+        v |= (uint32_t)(b & 0x7f) << (7 * k);
+        if (!(b & 0x80)) break;
+    }
+    const int32_t len = (int32_t)v;
+    if (len < 0 || q + (size_t)len > buf_len) return COVT_ERR_TRUNCATED;  // new String(...) bounds
+    *str_off = (int32_t)q;
+    *str_len = len;
+    *pos = (int32_t)q + len;
+    return COVT_OK;
+}
 int covt_decode_fastpfor_zigzag_delta(const uint8_t* buf, size_t buf_len, int32_t n, int32_t byte_length,
                                       int32_t* pos, int32_t* out) {
     return fpf_call(buf, buf_len, pos, COVT_OP_FPF_ZZ_DELTA_I32, n, byte_length, 0, out, (size_t)std::max(n, 0));
@@ -1017,157 +1272,89 @@ int covt_decode_streams_device_grouped(const uint8_t* d_in, const covt_stream_de
 
 namespace {
 
-// Decode a subset of a plan's streams on the current device.  `sel` lists tile-order stream
-// indices; their inputs are the tiles in `tiles` (packed contiguously on the device).
-int decode_all(const covt_plan* p, const uint8_t* bytes, uint8_t* host_out, covt_stream_result* host_res);
-
-// Pageable caller memory for the D2H: fault its pages in on host threads (MADV_POPULATE_WRITE) while
-// the device runs H2D + decode, so the copy itself meets resident pages.  Into a fresh 4.5 GB buffer
-// the single-threaded first touch inside the copy otherwise costs ~3x the copy.
-// COVT_HOST_PREFAULT=0 turns it off.  Kernels without MADV_POPULATE_WRITE (< 5.14) touch each page.
-void prefault(uint8_t* p, size_t n) {
-    const char* e = std::getenv("COVT_HOST_PREFAULT");
-    if ((e && e[0] == '0') || n < (64u << 20)) return;
-#ifdef MADV_POPULATE_WRITE
-    const uintptr_t pg = 4096, lo = ((uintptr_t)p + pg - 1) & ~(pg - 1), hi = ((uintptr_t)p + n) & ~(pg - 1);
-    if (hi <= lo) return;
-    const size_t len = hi - lo;
-    const unsigned hw = std::thread::hardware_concurrency();
-    const size_t nthr = std::max<size_t>(1, std::min<size_t>(8, hw ? hw : 1));
-    std::vector<std::thread> th;
-    for (size_t k = 0; k < nthr; ++k) {
-        const uintptr_t a = lo + ((len * k / nthr) & ~(pg - 1));
-        const uintptr_t b = k + 1 == nthr ? hi : lo + ((len * (k + 1) / nthr) & ~(pg - 1));
-        th.emplace_back([=] {
-            if (madvise((void*)a, b - a, MADV_POPULATE_WRITE) == 0) return;
-            // older kernels: write each page's first byte back to itself (the copy overwrites it anyway)
-            for (uintptr_t q = a; q < b; q += pg) {
-                volatile uint8_t* v = (volatile uint8_t*)q;
-                *v = *v;
-            }
-        });
+// Tile ranges of the shards: contiguous in tile order (so each shard's inputs and, the plan's output
+// layout being in tile order, its outputs are single byte ranges), cut where the running weight
+// (stream bytes + output bytes) crosses k/n of the total.  For 10k tiles the imbalance is at most
+// one tile (~0.01 %).
+std::vector<std::pair<int32_t, int32_t>> shard_ranges(const covt_plan* p, int32_t n) {
+    std::vector<double> w((size_t)p->n_tiles + 1, 0.0);
+    for (const auto& si : p->info) w[(size_t)si.tile + 1] += (double)si.byte_length + (double)(si.out_elems * si.elem_bytes);
+    for (int32_t t = 0; t < p->n_tiles; ++t) w[(size_t)t + 1] += w[(size_t)t];
+    const double tot = w[(size_t)p->n_tiles];
+    std::vector<std::pair<int32_t, int32_t>> r;
+    int32_t t0 = 0;
+    for (int32_t k = 0; k < n; ++k) {
+        int32_t t1 = p->n_tiles;
+        if (k + 1 < n) {
+            const double cut = tot * (k + 1) / n;
+            t1 = (int32_t)(std::lower_bound(w.begin() + t0, w.end(), cut) - w.begin());
+            t1 = std::max(t0, std::min(t1, p->n_tiles));
+        }
+        r.emplace_back(t0, t1);
+        t0 = t1;
     }
-    for (auto& t : th) t.join();
-#else
-    (void)p;
-#endif
+    return r;
 }
 
-int decode_subset(const covt_plan* p, const uint8_t* bytes, const std::vector<int32_t>& tiles, uint8_t* host_out,
-                  covt_stream_result* host_res) {
-    if (tiles.size() == (size_t)p->n_tiles) return decode_all(p, bytes, host_out, host_res);
-    // pack the shard's tiles
-    std::vector<int64_t> new_tile_off(p->n_tiles, -1);
-    uint64_t in_total = 0;
-    for (int32_t t : tiles) {
-        new_tile_off[(size_t)t] = (int64_t)in_total;
-        in_total += (p->tile_size[(size_t)t] + 15) & ~(uint64_t)15;
-    }
-    std::vector<int64_t> sel;
-    for (size_t i = 0; i < p->info.size(); ++i)
-        if (new_tile_off[(size_t)p->info[i].tile] >= 0) sel.push_back((int64_t)i);
-    // launch order of the shard = the plan's global launch order restricted to it
-    std::sort(sel.begin(), sel.end(),
-              [&](int64_t a, int64_t b) { return p->info[(size_t)a].desc_index < p->info[(size_t)b].desc_index; });
-    std::vector<covt_stream_desc> descs(sel.size());
-    std::vector<int64_t> new_out(sel.size());
-    int64_t out_total = 0;
-    for (size_t k = 0; k < sel.size(); ++k) {
-        const covt_stream_info& si = p->info[(size_t)sel[k]];
-        covt_stream_desc d = p->descs[(size_t)si.desc_index];
-        d.in_off = (uint64_t)(new_tile_off[(size_t)si.tile] + (si.in_off - (int64_t)p->tile_off[(size_t)si.tile]));
-        new_out[k] = out_total;
-        d.out_off = (uint64_t)out_total;
-        out_total = align16(out_total + si.out_elems * si.elem_bytes);
-        descs[k] = d;
-    }
-    hipStream_t s;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return COVT_ERR_DEVICE;
-    uint8_t *d_in = nullptr, *d_out = nullptr;
-    covt_stream_desc* d_desc = nullptr;
-    covt_stream_result* d_res = nullptr;
-    int st = COVT_OK;
-    std::vector<covt_stream_result> res(sel.size());
-    std::vector<uint8_t> stage;
-    auto chk = [&](hipError_t e) { if (e != hipSuccess && st == COVT_OK) st = COVT_ERR_DEVICE; };
-    chk(hipMalloc(&d_in, in_total + COVT_INPUT_PADDING));
-    chk(hipMalloc(&d_out, (size_t)std::max<int64_t>(out_total, 16)));
-    chk(hipMalloc(&d_desc, std::max<size_t>(descs.size(), 1) * sizeof(covt_stream_desc)));
-    chk(hipMalloc(&d_res, std::max<size_t>(descs.size(), 1) * sizeof(covt_stream_result)));
-    if (st == COVT_OK) {
-        for (int32_t t : tiles)
-            chk(hipMemcpyAsync(d_in + new_tile_off[(size_t)t], bytes + p->tile_off[(size_t)t],
-                               (size_t)p->tile_size[(size_t)t], hipMemcpyHostToDevice, s));
-        if (!descs.empty())
-            chk(hipMemcpyAsync(d_desc, descs.data(), descs.size() * sizeof(covt_stream_desc), hipMemcpyHostToDevice,
-                               s));
-        int64_t cnt[COVT_NUM_FAMILIES] = {0, 0, 0, 0};
-        for (const auto& d : descs) cnt[desc_family(d)]++;  // sel is in grouped launch order
-        if (st == COVT_OK) st = launch_grouped(d_in, d_desc, cnt, d_out, d_res, s);
-        stage.resize((size_t)out_total);
-        if (st == COVT_OK && out_total)
-            chk(hipMemcpyAsync(stage.data(), d_out, (size_t)out_total, hipMemcpyDeviceToHost, s));
-        if (st == COVT_OK && !res.empty())
-            chk(hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(covt_stream_result), hipMemcpyDeviceToHost, s));
-        chk(hipStreamSynchronize(s));
-    }
-    if (st == COVT_OK) {
-        for (size_t k = 0; k < sel.size(); ++k) {
-            const covt_stream_info& si = p->info[(size_t)sel[k]];
-            std::memcpy(host_out + si.out_off, stage.data() + new_out[k], (size_t)(si.out_elems * si.elem_bytes));
-            host_res[(size_t)sel[k]] = res[k];
+}  // namespace
+
+namespace {
+
+void build_shards(const covt_plan* p, const std::vector<int32_t>& devs, std::vector<std::unique_ptr<HostShard>>& out) {
+    out.clear();
+    const auto rng = shard_ranges(p, (int32_t)devs.size());
+    std::vector<int32_t> shard_of_tile((size_t)p->n_tiles, 0);
+    for (size_t g = 0; g < rng.size(); ++g) {
+        auto h = std::make_unique<HostShard>();
+        h->device = devs[g];
+        const int32_t t0 = rng[g].first, t1 = rng[g].second;
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (int32_t t = t0; t < t1; ++t) {
+            shard_of_tile[(size_t)t] = (int32_t)g;
+            lo = std::min<uint64_t>(lo, p->tile_off[(size_t)t]);
+            hi = std::max<uint64_t>(hi, p->tile_off[(size_t)t] + p->tile_size[(size_t)t]);
         }
+        if (t1 > t0) {
+            h->in_lo = lo & ~(uint64_t)15;  // keeps every stream's 16-byte window alignment
+            h->in_len = hi - h->in_lo;
+        }
+        h->out_lo = INT64_MAX;
+        out.push_back(std::move(h));
     }
-    if (d_in) (void)hipFree(d_in);
-    if (d_out) (void)hipFree(d_out);
-    if (d_desc) (void)hipFree(d_desc);
-    if (d_res) (void)hipFree(d_res);
-    (void)hipStreamDestroy(s);
-    return st;
+    for (const auto& si : p->info) {  // output range of each shard (tile order = output order)
+        HostShard& h = *out[(size_t)shard_of_tile[(size_t)si.tile]];
+        h.out_lo = std::min<int64_t>(h.out_lo, si.out_off);
+        h.out_len = std::max<int64_t>(h.out_len, si.out_off + si.out_elems * si.elem_bytes);
+    }
+    for (auto& h : out) {
+        if (h->out_lo == INT64_MAX) h->out_lo = h->out_len = 0;
+        else h->out_len -= h->out_lo;
+    }
+    std::vector<int64_t> stream_of_desc(p->descs.size());
+    for (size_t i = 0; i < p->info.size(); ++i) stream_of_desc[(size_t)p->info[i].desc_index] = (int64_t)i;
+    for (size_t k = 0; k < p->descs.size(); ++k) {  // launch order restricted to each shard stays grouped
+        const int64_t i = stream_of_desc[k];
+        HostShard& h = *out[(size_t)shard_of_tile[(size_t)p->info[(size_t)i].tile]];
+        covt_stream_desc d = p->descs[k];
+        d.in_off -= h.in_lo;
+        d.out_off -= (uint64_t)h.out_lo;
+        h.fam[desc_family(d)]++;
+        h.descs.push_back(d);
+        h.stream.push_back(i);
+    }
+    for (auto& h : out) h->res.resize(h->descs.size());
 }
 
-// Every tile of the plan on one device: the caller's buffer already has the plan's layout, so the
-// plan's own descriptor table runs unchanged — one H2D of the tile bytes, one launch, one D2H straight
-// into host_out (no per-tile copies, no staging buffer, no per-stream scatter).  Padding between
-// output slices is zeroed on the device so host_out matches the subset path byte for byte.
-int decode_all(const covt_plan* p, const uint8_t* bytes, uint8_t* host_out, covt_stream_result* host_res) {
-    uint64_t extent = 0;
-    for (int32_t t = 0; t < p->n_tiles; ++t)
-        extent = std::max<uint64_t>(extent, p->tile_off[(size_t)t] + p->tile_size[(size_t)t]);
-    const size_t ns = p->descs.size();
-    hipStream_t s;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return COVT_ERR_DEVICE;
-    uint8_t *d_in = nullptr, *d_out = nullptr;
-    covt_stream_desc* d_desc = nullptr;
-    covt_stream_result* d_res = nullptr;
-    int st = COVT_OK;
-    std::vector<covt_stream_result> res(ns);
-    auto chk = [&](hipError_t e) { if (e != hipSuccess && st == COVT_OK) st = COVT_ERR_DEVICE; };
-    chk(hipMalloc(&d_in, extent + COVT_INPUT_PADDING));
-    chk(hipMalloc(&d_out, (size_t)std::max<int64_t>(p->out_bytes, 16)));
-    chk(hipMalloc(&d_desc, std::max<size_t>(ns, 1) * sizeof(covt_stream_desc)));
-    chk(hipMalloc(&d_res, std::max<size_t>(ns, 1) * sizeof(covt_stream_result)));
-    if (st == COVT_OK) {
-        if (extent) chk(hipMemcpyAsync(d_in, bytes, extent, hipMemcpyHostToDevice, s));
-        if (ns) chk(hipMemcpyAsync(d_desc, p->descs.data(), ns * sizeof(covt_stream_desc), hipMemcpyHostToDevice, s));
-        if (p->out_bytes) chk(hipMemsetAsync(d_out, 0, (size_t)p->out_bytes, s));
-        if (st == COVT_OK) st = launch_grouped(d_in, d_desc, p->fam_counts, d_out, d_res, s);
-        if (st == COVT_OK && ns)
-            chk(hipMemcpyAsync(res.data(), d_res, ns * sizeof(covt_stream_result), hipMemcpyDeviceToHost, s));
-        if (st == COVT_OK && p->out_bytes) {
-            prefault(host_out, (size_t)p->out_bytes);  // overlaps the device work queued above
-            chk(hipMemcpyAsync(host_out, d_out, (size_t)p->out_bytes, hipMemcpyDeviceToHost, s));
-        }
-        chk(hipStreamSynchronize(s));
-    }
-    if (st == COVT_OK)
-        for (size_t i = 0; i < p->info.size(); ++i) host_res[i] = res[(size_t)p->info[i].desc_index];
-    if (d_in) (void)hipFree(d_in);
-    if (d_out) (void)hipFree(d_out);
-    if (d_desc) (void)hipFree(d_desc);
-    if (d_res) (void)hipFree(d_res);
-    (void)hipStreamDestroy(s);
-    return st;
+int decode_host_shards(const covt_plan* p, const uint8_t* bytes, uint64_t n_bytes, const std::vector<int32_t>& devs,
+                       uint8_t* host_out, covt_stream_result* host_res);
+
+// argument checks of the host entry points, before anything touches the device
+bool host_args_ok(const covt_plan* p, const uint8_t* bytes, uint64_t n_bytes, const uint8_t* host_out,
+                  const covt_stream_result* host_res) {
+    if (!p || (!host_res && !p->info.empty()) || (!host_out && p->out_bytes) || (!bytes && n_bytes)) return false;
+    for (int32_t t = 0; t < p->n_tiles; ++t)  // the caller's buffer must hold every tile the plan names
+        if (p->tile_off[(size_t)t] + p->tile_size[(size_t)t] > n_bytes) return false;
+    return true;
 }
 
 }  // namespace
@@ -1176,50 +1363,75 @@ extern "C" {
 
 int covt_plan_decode_host(const covt_plan* p, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_out,
                           covt_stream_result* host_res) {
-    if (!p || (!host_res && !p->info.empty()) || (!host_out && p->out_bytes)) return COVT_ERR_INVALID_ARG;
-    (void)n_bytes;
-    std::vector<int32_t> tiles;
-    for (int32_t t = 0; t < p->n_tiles; ++t)
-        if (p->tile_status[(size_t)t] == 0) tiles.push_back(t);
-    return decode_subset(p, bytes, tiles, host_out, host_res);
+    if (!host_args_ok(p, bytes, n_bytes, host_out, host_res)) return COVT_ERR_INVALID_ARG;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return COVT_ERR_DEVICE;
+    return decode_host_shards(p, bytes, n_bytes, std::vector<int32_t>{dev}, host_out, host_res);
 }
 
 int covt_plan_decode_host_multi(const covt_plan* p, const uint8_t* bytes, uint64_t n_bytes, int32_t n_gpus,
                                 uint8_t* host_out, covt_stream_result* host_res) {
-    if (!p || n_gpus < 1 || (!host_res && !p->info.empty()) || (!host_out && p->out_bytes))
-        return COVT_ERR_INVALID_ARG;
-    (void)n_bytes;
+    if (n_gpus < 1 || !host_args_ok(p, bytes, n_bytes, host_out, host_res)) return COVT_ERR_INVALID_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return COVT_ERR_DEVICE;
-    n_gpus = std::min(n_gpus, ndev);
-    // greedy longest-processing-time split on stream bytes + output bytes (no collectives)
-    std::vector<int64_t> w((size_t)p->n_tiles, 0);
-    for (const auto& si : p->info) w[(size_t)si.tile] += si.byte_length + si.out_elems * si.elem_bytes;
-    std::vector<int32_t> order;
-    for (int32_t t = 0; t < p->n_tiles; ++t)
-        if (p->tile_status[(size_t)t] == 0) order.push_back(t);
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return w[(size_t)a] > w[(size_t)b]; });
-    std::vector<std::vector<int32_t>> shard((size_t)n_gpus);
-    std::vector<int64_t> load((size_t)n_gpus, 0);
-    for (int32_t t : order) {
-        const size_t g = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
-        shard[g].push_back(t);
-        load[g] += w[(size_t)t];
-    }
-    std::vector<int> st((size_t)n_gpus, COVT_OK);
-    std::vector<std::thread> th;
-    for (int32_t g = 0; g < n_gpus; ++g) {
-        th.emplace_back([&, g] {
-            if (hipSetDevice(g) != hipSuccess) { st[(size_t)g] = COVT_ERR_DEVICE; return; }
-            std::sort(shard[(size_t)g].begin(), shard[(size_t)g].end());
-            st[(size_t)g] = decode_subset(p, bytes, shard[(size_t)g], host_out, host_res);
-        });
-    }
-    for (auto& t : th) t.join();
-    for (int s : st)
-        if (s) return s;
+    std::vector<int32_t> devs((size_t)std::min(n_gpus, ndev));
+    std::iota(devs.begin(), devs.end(), 0);
+    return decode_host_shards(p, bytes, n_bytes, devs, host_out, host_res);
+}
+
+int covt_plan_decode_host_shards(const covt_plan* p, const uint8_t* bytes, uint64_t n_bytes, int32_t n_shards,
+                                 const int32_t* shard_devices, uint8_t* host_out, covt_stream_result* host_res) {
+    if (n_shards < 1 || !shard_devices || !host_args_ok(p, bytes, n_bytes, host_out, host_res))
+        return COVT_ERR_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return COVT_ERR_DEVICE;
+    for (int32_t g = 0; g < n_shards; ++g)
+        if (shard_devices[g] < 0 || shard_devices[g] >= ndev) return COVT_ERR_INVALID_ARG;
+    return decode_host_shards(p, bytes, n_bytes, std::vector<int32_t>(shard_devices, shard_devices + n_shards),
+                              host_out, host_res);
+}
+
+int covt_plan_release_device(const covt_plan* p) {
+    if (!p) return COVT_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(p->host_mu);
+    p->host_shards.clear();
+    p->host_devs.clear();
     return COVT_OK;
 }
+
+}  // extern "C"
+
+namespace {
+
+int decode_host_shards(const covt_plan* p, const uint8_t* bytes, uint64_t n_bytes, const std::vector<int32_t>& devs,
+                       uint8_t* host_out, covt_stream_result* host_res) {
+    std::lock_guard<std::mutex> g(p->host_mu);  // one call per plan at a time; plans are independent
+    int cur = 0;
+    const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+    if (p->host_devs != devs) {
+        p->host_shards.clear();
+        build_shards(p, devs, p->host_shards);
+        p->host_devs = devs;
+    }
+    const size_t n = p->host_shards.size();
+    std::vector<int> st(n, COVT_OK);
+    if (n == 1) {
+        st[0] = p->host_shards[0]->run(bytes, host_out, host_res);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t k = 0; k < n; ++k)
+            th.emplace_back([&, k] { st[k] = p->host_shards[k]->run(bytes, host_out, host_res); });
+        for (auto& t : th) t.join();
+    }
+    if (have_cur) (void)hipSetDevice(cur);
+    for (int x : st)
+        if (x) return x;
+    return COVT_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 int64_t covt_plan_num_geometry_columns(const covt_plan* p) { return p ? (int64_t)p->ginfo.size() : 0; }
 int64_t covt_plan_assembly_bytes(const covt_plan* p) { return p ? p->asm_bytes : 0; }

@@ -111,6 +111,18 @@ JNIEXPORT jbyteArray JNICALL JFN(decodeByteRle)(JNIEnv* env, jclass, jbyteArray 
     set_pos(env, pos, p);
     return r;
 }
+// decodeByteRle(byte[], int, IntWrapper) (DecodingUtils.java:290): GpuDecodingUtils' 3-argument
+// overload forwards here (a distinct name keeps the 4-argument native's short JNI symbol unambiguous).
+JNIEXPORT jbyteArray JNICALL JFN(decodeByteRleReencode)(JNIEnv* env, jclass, jbyteArray buf, jint n, jobject pos) {
+    Bytes b(env, buf);
+    int32_t p = get_pos(env, pos);
+    std::vector<uint8_t> out((size_t)(n > 0 ? n : 0));
+    if (!check(env, covt_decode_byte_rle_reencode(b.u8(), (size_t)b.n, n, &p, out.data()))) return nullptr;
+    jbyteArray r = env->NewByteArray(n);
+    env->SetByteArrayRegion(r, 0, n, reinterpret_cast<const jbyte*>(out.data()));
+    set_pos(env, pos, p);
+    return r;
+}
 JNIEXPORT jintArray JNICALL JFN(decodeFastPfor128ZigZagDelta)(JNIEnv* env, jclass, jbyteArray buf, jint n,
                                                               jint byte_length, jobject pos) {
     Bytes b(env, buf);

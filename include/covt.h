@@ -69,6 +69,18 @@ int covt_decode_rle(const uint8_t* buf, size_t buf_len, int32_t num_values, int3
 /* DecodingUtils.decodeByteRle(byte[], int numValues, IntWrapper, int byteLength)  DecodingUtils.java:275 */
 int covt_decode_byte_rle(const uint8_t* buf, size_t buf_len, int32_t num_values, int32_t* pos, int32_t byte_length,
                          uint8_t* out);
+/* DecodingUtils.decodeByteRle(byte[], int numValues, IntWrapper)                  DecodingUtils.java:290
+ * (the form CovtParser.java:295 uses for Gen D present streams): *pos advances by the length of the
+ * ORC RunLengthByteWriter re-encoding of the decoded values (getByteRleChunkSize :312-314). */
+int covt_decode_byte_rle_reencode(const uint8_t* buf, size_t buf_len, int32_t num_values, int32_t* pos,
+                                  uint8_t* out);
+/* DecodingUtils.decodeFloatsLE(byte[], IntWrapper, int numValues)                 DecodingUtils.java:446
+ * numValues little-endian floats copied out (host memory; no decode arithmetic). */
+int covt_decode_floats_le(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t num_values, float* out);
+/* DecodingUtils.decodeString(byte[], IntWrapper)                                  DecodingUtils.java:21
+ * Reads the 4-byte-capped varint length and returns where the UTF-8 bytes lie (*str_off, *str_len);
+ * *pos advances past them.  The JNI shim builds the java.lang.String from them. */
+int covt_decode_string(const uint8_t* buf, size_t buf_len, int32_t* pos, int32_t* str_off, int32_t* str_len);
 /* DecodingUtils.decodeFastPfor128ZigZagDelta(byte[], int, int byteLength, IntWrapper) DecodingUtils.java:316 */
 int covt_decode_fastpfor_zigzag_delta(const uint8_t* buf, size_t buf_len, int32_t num_values, int32_t byte_length,
                                       int32_t* pos, int32_t* out);
@@ -182,16 +194,30 @@ int covt_decode_streams_device_grouped(const uint8_t* d_in, const covt_stream_de
                                        const int64_t family_counts[COVT_NUM_FAMILIES], uint8_t* d_out,
                                        covt_stream_result* d_res, void* hip_stream);
 
-/* Convenience: plan + H2D + decode + D2H for host tiles on the current device.
- * host_out: covt_plan_output_bytes(plan) bytes; host_res: num_streams results (plan stream order). */
+/* Host entry point: H2D + decode + D2H for host tiles on the current device.
+ * bytes/n_bytes: the caller's buffer the plan's tile offsets index (every tile must lie inside
+ * [0, n_bytes), else COVT_ERR_INVALID_ARG); host_out: covt_plan_output_bytes(plan) bytes, stream i's
+ * values at covt_stream_info.out_off; host_res: num_streams results (plan stream order).  Bytes of
+ * host_out outside the stream slices (16-byte alignment padding) are unspecified.
+ * Device buffers and the descriptor table stay cached on the plan across calls (released by
+ * covt_plan_release_device or covt_plan_destroy); calls on one plan are serialised. */
 int covt_plan_decode_host(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_out,
                           covt_stream_result* host_res);
 
-/* Multi-GPU host entry point: shards the plan's tiles over n_gpus devices by a greedy
- * byte-balanced split (one host thread per device, no collectives), decodes, and gathers the
- * outputs into host_out / host_res exactly as covt_plan_decode_host would. */
+/* Multi-GPU host entry point: shards the plan's tiles over min(n_gpus, devices) devices (contiguous
+ * tile ranges balanced on stream + output bytes, one host thread per device, no collectives); each
+ * shard is one H2D, one launch and one D2H into its part of host_out.  Same results as
+ * covt_plan_decode_host. */
 int covt_plan_decode_host_multi(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, int32_t n_gpus,
                                 uint8_t* host_out, covt_stream_result* host_res);
+
+/* The same with an explicit shard -> device map: n_shards shards, shard k on device shard_devices[k]
+ * (devices may repeat: several shards of one device run concurrently on their own streams). */
+int covt_plan_decode_host_shards(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, int32_t n_shards,
+                                 const int32_t* shard_devices, uint8_t* host_out, covt_stream_result* host_res);
+
+/* Free the device buffers the host entry points cached on this plan. */
+int covt_plan_release_device(const covt_plan* plan);
 
 /* ---------------------------------------------------------------------------
  * Geometry assembly: the GPU replacement for

@@ -64,53 +64,72 @@ def build(force: bool = False) -> str:
 _lib = None
 
 
+def build_native(out_dir: str) -> str:
+    """The same restatement built with -march=native into `out_dir` (bench.py's cpu_baseline leg builds it on
+    the GPU box's own host, SURVEY §8(d) "CPU timing"); returns the library path."""
+    out = os.path.join(out_dir, "liboracle_covt_native.so")
+    srcs = [os.path.join(_HERE, f) for f in ("covt_oracle.c", "covt_oracle_props.c", "mvt_decode.c")]
+    subprocess.check_call([os.environ.get("CC", "gcc"), "-O3", "-march=native", "-fPIC", "-std=c11", "-shared",
+                           "-o", out] + srcs + ["-lpthread"])
+    return out
+
+
+def load_native(path: str):
+    """A separately built copy of the restatement (build_native), bound like lib()."""
+    return _bind(C.CDLL(path))
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(_LIB_PATH):
             build()
-        L = C.CDLL(_LIB_PATH)
-        u8p, i32p, i64p = C.POINTER(C.c_uint8), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
-        sz = C.c_size_t
-        L.oracle_walk_tile.argtypes = [u8p, sz, C.c_int, C.POINTER(OracleStream), C.c_int32, i32p]
-        L.mvt_decode_tile.argtypes = [u8p, C.c_int64, C.c_int, i32p, C.c_int64, i64p, C.POINTER(C.c_uint64)]
-        L.oracle_decode_stream.argtypes = [u8p, sz, C.POINTER(OracleStream), C.c_int, C.c_void_p, i32p]
-        L.oracle_stream_output.argtypes = [C.POINTER(OracleStream), C.c_int, i32p, i64p]
-        L.oracle_decode_tiles_mt.argtypes = [u8p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int32,
-                                             C.c_int, C.c_int, C.c_int32, i64p, i64p, i64p]
-        L.oracle_encode_varints_u64.restype = C.c_int64
-        L.oracle_encode_varints_u64.argtypes = [C.POINTER(C.c_uint64), C.c_int64, u8p, C.c_int64]
-        L.oracle_encode_rle.restype = C.c_int64
-        L.oracle_encode_rle.argtypes = [i64p, C.c_int64, C.c_int, u8p, C.c_int64]
-        L.oracle_encode_byte_rle.restype = C.c_int64
-        L.oracle_encode_byte_rle.argtypes = [u8p, C.c_int64, u8p, C.c_int64]
-        L.oracle_encode_fastpfor.restype = C.c_int64
-        L.oracle_encode_fastpfor.argtypes = [C.POINTER(C.c_uint32), C.c_int64, u8p, C.c_int64]
-        L.oracle_fastpfor_uncompress.argtypes = [u8p, sz, C.c_int32, C.c_int32, C.c_int32,
-                                                 C.POINTER(C.c_uint32), i32p]
-        for name in ("oracle_decode_varint", "oracle_decode_zigzag_varint", "oracle_decode_zigzag_delta_varint",
-                     "oracle_decode_zigzag_delta_varint_coordinates"):
-            getattr(L, name).argtypes = [u8p, sz, i32p, C.c_int32, i32p]
-        L.oracle_decode_varint_u64.argtypes = [u8p, sz, i32p, C.c_int32, C.POINTER(C.c_uint64)]
-        L.oracle_decode_rle.argtypes = [u8p, sz, C.c_int32, i32p, C.c_int, i64p, i32p]
-        L.oracle_decode_byte_rle.argtypes = [u8p, sz, C.c_int32, i32p, C.c_int32, u8p, i32p]
-        L.oracle_decode_fastpfor_zigzag_delta.argtypes = [u8p, sz, C.c_int32, C.c_int32, i32p, i32p]
-        L.oracle_decode_fastpfor_delta_coordinates.argtypes = [u8p, sz, C.c_int32, C.c_int32, i32p, i32p]
-        L.oracle_decode_delta_varint_morton_codes.argtypes = [u8p, sz, i32p, C.c_int32, C.c_int32, i32p]
-        L.oracle_decode_fastpfor_delta_morton_codes.argtypes = [u8p, sz, C.c_int32, C.c_int32, i32p, C.c_int32,
-                                                                i32p]
-        L.oracle_decode_morton.argtypes = [C.c_int32, C.c_int32, i32p, i32p]
-        L.oracle_decode_morton.restype = None
-        L.oracle_assemble_geometry.argtypes = [u8p, C.c_int32, i32p, C.c_int32, i32p, C.c_int32, i32p, C.c_int32,
-                                               i32p, C.c_int32, i32p, C.c_int32, C.c_int, C.c_int32, C.c_int32,
-                                               C.c_int32, i32p, i32p, i32p, i32p, i32p, i32p, i32p]
-        L.oracle_walk_properties.argtypes = [u8p, sz, C.c_int, C.POINTER(OracleProp), C.c_int32, i32p]
-        L.oracle_property_sizes.argtypes = [C.POINTER(OracleProp), i64p]
-        L.oracle_property_sizes.restype = None
-        L.oracle_decode_property.argtypes = [u8p, sz, C.POINTER(OracleProp), C.c_int, C.c_void_p, C.c_void_p,
-                                             C.c_void_p, C.c_void_p, i32p]
-        _lib = L
+        _lib = _bind(C.CDLL(_LIB_PATH))
     return _lib
+
+
+def _bind(L):
+    """Set the ctypes signatures of a liboracle_covt CDLL."""
+    u8p, i32p, i64p = C.POINTER(C.c_uint8), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
+    sz = C.c_size_t
+    L.oracle_walk_tile.argtypes = [u8p, sz, C.c_int, C.POINTER(OracleStream), C.c_int32, i32p]
+    L.mvt_decode_tile.argtypes = [u8p, C.c_int64, C.c_int, i32p, C.c_int64, i64p, C.POINTER(C.c_uint64)]
+    L.oracle_decode_stream.argtypes = [u8p, sz, C.POINTER(OracleStream), C.c_int, C.c_void_p, i32p]
+    L.oracle_stream_output.argtypes = [C.POINTER(OracleStream), C.c_int, i32p, i64p]
+    L.oracle_decode_tiles_mt.argtypes = [u8p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int32,
+                                         C.c_int, C.c_int, C.c_int32, i64p, i64p, i64p]
+    L.oracle_encode_varints_u64.restype = C.c_int64
+    L.oracle_encode_varints_u64.argtypes = [C.POINTER(C.c_uint64), C.c_int64, u8p, C.c_int64]
+    L.oracle_encode_rle.restype = C.c_int64
+    L.oracle_encode_rle.argtypes = [i64p, C.c_int64, C.c_int, u8p, C.c_int64]
+    L.oracle_encode_byte_rle.restype = C.c_int64
+    L.oracle_encode_byte_rle.argtypes = [u8p, C.c_int64, u8p, C.c_int64]
+    L.oracle_encode_fastpfor.restype = C.c_int64
+    L.oracle_encode_fastpfor.argtypes = [C.POINTER(C.c_uint32), C.c_int64, u8p, C.c_int64]
+    L.oracle_fastpfor_uncompress.argtypes = [u8p, sz, C.c_int32, C.c_int32, C.c_int32,
+                                             C.POINTER(C.c_uint32), i32p]
+    for name in ("oracle_decode_varint", "oracle_decode_zigzag_varint", "oracle_decode_zigzag_delta_varint",
+                 "oracle_decode_zigzag_delta_varint_coordinates"):
+        getattr(L, name).argtypes = [u8p, sz, i32p, C.c_int32, i32p]
+    L.oracle_decode_varint_u64.argtypes = [u8p, sz, i32p, C.c_int32, C.POINTER(C.c_uint64)]
+    L.oracle_decode_rle.argtypes = [u8p, sz, C.c_int32, i32p, C.c_int, i64p, i32p]
+    L.oracle_decode_byte_rle.argtypes = [u8p, sz, C.c_int32, i32p, C.c_int32, u8p, i32p]
+    L.oracle_decode_fastpfor_zigzag_delta.argtypes = [u8p, sz, C.c_int32, C.c_int32, i32p, i32p]
+    L.oracle_decode_fastpfor_delta_coordinates.argtypes = [u8p, sz, C.c_int32, C.c_int32, i32p, i32p]
+    L.oracle_decode_delta_varint_morton_codes.argtypes = [u8p, sz, i32p, C.c_int32, C.c_int32, i32p]
+    L.oracle_decode_fastpfor_delta_morton_codes.argtypes = [u8p, sz, C.c_int32, C.c_int32, i32p, C.c_int32,
+                                                            i32p]
+    L.oracle_decode_morton.argtypes = [C.c_int32, C.c_int32, i32p, i32p]
+    L.oracle_decode_morton.restype = None
+    L.oracle_assemble_geometry.argtypes = [u8p, C.c_int32, i32p, C.c_int32, i32p, C.c_int32, i32p, C.c_int32,
+                                           i32p, C.c_int32, i32p, C.c_int32, C.c_int, C.c_int32, C.c_int32,
+                                           C.c_int32, i32p, i32p, i32p, i32p, i32p, i32p, i32p]
+    L.oracle_walk_properties.argtypes = [u8p, sz, C.c_int, C.POINTER(OracleProp), C.c_int32, i32p]
+    L.oracle_property_sizes.argtypes = [C.POINTER(OracleProp), i64p]
+    L.oracle_property_sizes.restype = None
+    L.oracle_decode_property.argtypes = [u8p, sz, C.POINTER(OracleProp), C.c_int, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, i32p]
+    return L
 
 
 def _u8(buf) -> tuple:
@@ -355,12 +374,15 @@ def decode_stream(tile: bytes, s: OracleStream, id_mode: int = ID_FORMAT):
     return st, out[:ne], cons.value
 
 
-def decode_tiles_mt(blob: np.ndarray, offsets, sizes, fmt=FMT_GENC, id_mode=ID_FORMAT, threads=1):
+def decode_tiles_mt(blob: np.ndarray, offsets, sizes, fmt=FMT_GENC, id_mode=ID_FORMAT, threads=1, L=None):
+    """Walk + decode every Id/Geometry stream of every tile on `threads` host threads (the CPU baseline);
+    `L` = a library from load_native() (default: lib())."""
+    L = L or lib()
     blob = np.ascontiguousarray(blob, dtype=np.uint8)
     offs = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
     szs = np.ascontiguousarray(np.asarray(sizes, dtype=np.uint64))
     ib, ob, vx = C.c_int64(), C.c_int64(), C.c_int64()
-    st = lib().oracle_decode_tiles_mt(_p(blob, C.c_uint8), _p(offs, C.c_uint64), _p(szs, C.c_uint64), offs.size,
+    st = L.oracle_decode_tiles_mt(_p(blob, C.c_uint8), _p(offs, C.c_uint64), _p(szs, C.c_uint64), offs.size,
                                       fmt, id_mode, threads, C.byref(ib), C.byref(ob), C.byref(vx))
     return st, ib.value, ob.value, vx.value
 

@@ -1,0 +1,88 @@
+"""bench.py contract on CPU: the N-rank launch (--gpus N spawns N processes, gloo aggregation), the
+GPU-count check, the BASELINE config 2-4 stream selections and the CPU-baseline leg."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _run(args, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p, lines
+
+
+def test_gpus2_dry_run_spawns_two_ranks():
+    p, lines = _run(["--gpus", "2", "--dry-run", "--tiles", "40", "--steps", "2", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["dry_run"]
+    pr = line["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1]
+    assert len({r["seed"] for r in pr}) == 2  # weak scaling: distinct per-rank batches
+    assert all(r["tiles"] == 40 for r in pr)
+    assert line["config"]["parallelism"].startswith("dp2")
+    assert line["cpu_baseline"] is None  # CPU baseline on rank 0 at N=1 only
+
+
+def test_gpus2_strong_dry_run_shards_one_batch():
+    p, lines = _run(["--gpus", "2", "--dry-run", "--tiles", "41", "--steps", "1", "--warmup", "0",
+                     "--scaling", "strong"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    pr = json.loads(lines[0])["per_rank"]
+    assert sum(r["tiles"] for r in pr) == 41 and len({r["seed"] for r in pr}) == 1
+
+
+@pytest.mark.skipif(__import__("torch").cuda.device_count() >= 2, reason="host has >= 2 GPUs")
+def test_gpus2_fails_loudly_without_two_gpus():
+    p, lines = _run(["--gpus", "2", "--tiles", "10", "--steps", "1"], timeout=120)
+    assert p.returncode != 0 and not lines
+    assert "GPU" in p.stderr
+
+
+def test_world_size_must_match_gpus():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+def test_config_selections_match_survey():
+    """config 2 = 6 streams / 23,992 B / 137,864 B out; config 3 = 29 tiles, 1,104
+    streams, 2,983,091 B; config 4 = 61 tiles, 787 streams, 722,977 B in, 5,167,832 B out."""
+    import bench
+
+    covt = bench.load_covt()
+    lib = bench.tile_library()
+    want = {"config2": (1, 6, 23992, 137864), "config3": (29, 1104, 2983091, 14096776),
+            "config4": (61, 787, 722977, 5167832)}
+    for name, (nt, ns, ib, ob) in want.items():
+        picks = bench.config_tiles(lib, name)
+        plan = covt.Plan.from_tiles([t for _, t in picks])
+        m = bench.config_mask(plan, name)
+        st = plan.streams[m]
+        assert (len(picks), int(m.sum()), int(st["byte_length"].sum()),
+                int((st["out_elems"] * st["elem_bytes"]).sum())) == (nt, ns, ib, ob), name
+        descs, counts, idx = plan.subset_descs(m)
+        assert counts.sum() == ns and descs.size == 32 * ns
+        assert sorted(idx.tolist()) == sorted(map(int, m.nonzero()[0]))
+
+
+def test_cpu_baseline_leg_uses_host_cpus():
+    import bench
+
+    p, lines = _run(["--dry-run", "--tiles", "30", "--steps", "1", "--warmup", "0", "--cpu-iters", "3"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    cb = json.loads(lines[0])["cpu_baseline"]
+    n, info = bench.host_cpus()
+    assert cb["cores"] == n and cb["host"]["nproc"] == os.cpu_count()
+    assert cb["kind"] == "port" and "full bench batch (30 tiles" in cb["sample"]
+    assert cb["value"] > 0 and cb["value_1thread"] > 0

@@ -178,3 +178,48 @@ def test_no_cpu_fallback_without_gpu(covt):
                                       "rb").read()])
     with pytest.raises(covt.CovtError):
         plan.decode_host()
+
+
+def test_host_entry_rejects_short_buffer(covt):
+    """covt_plan_decode_host[_multi|_shards] check n_bytes against the plan's tiles before any device
+    call (a short caller buffer would otherwise be read past its end)."""
+    import ctypes as C
+
+    t = open(os.path.join(ROOT, "tests", "golden", "tiles", "omt", "5_16_20.covt"), "rb").read()
+    plan = covt.Plan.from_tiles([t, t])
+    L = covt.lib()
+    out = np.zeros(plan.output_bytes, dtype=np.uint8)
+    res = np.zeros((plan.num_streams, 2), dtype=np.int32)
+    blob = plan.blob
+    short = int(plan.offsets[1] + plan.sizes[1]) - 1
+    u8 = blob.ctypes.data_as(C.POINTER(C.c_uint8))
+    assert L.covt_plan_decode_host(plan._h, u8, short, out.ctypes.data, res.ctypes.data) == covt.ERR_INVALID_ARG
+    assert L.covt_plan_decode_host_multi(plan._h, u8, short, 2, out.ctypes.data, res.ctypes.data) == \
+        covt.ERR_INVALID_ARG
+    devs = np.zeros(2, dtype=np.int32)
+    assert L.covt_plan_decode_host_shards(plan._h, u8, short, 2, devs.ctypes.data_as(C.POINTER(C.c_int32)),
+                                          out.ctypes.data, res.ctypes.data) == covt.ERR_INVALID_ARG
+    assert L.covt_plan_decode_host(plan._h, None, 0, out.ctypes.data, res.ctypes.data) == covt.ERR_INVALID_ARG
+    assert L.covt_plan_release_device(plan._h) == covt.OK
+
+
+def test_floats_le_and_string_entries(covt):
+    """decodeFloatsLE (DecodingUtils.java:446) and decodeString (:21, :28): host-side views, Java bounds."""
+    D = covt.DecodingUtils
+    vals = np.array([1.5, -2.25, 3e38, np.inf], dtype="<f4")
+    buf = b"\x07" + vals.tobytes() + b"\x00"
+    p = covt.IntWrapper(1)
+    assert np.array_equal(D.decodeFloatsLE(buf, p, 4), vals) and p.get() == 17
+    with pytest.raises(covt.ArrayIndexOutOfBoundsException):
+        D.decodeFloatsLE(buf, covt.IntWrapper(3), 4)
+    s = "Zürich 東京".encode("utf-8")
+    buf = b"\xff" + bytes([len(s)]) + s + b"tail"
+    p = covt.IntWrapper(1)
+    assert D.decodeString(buf, p) == "Zürich 東京" and p.get() == 2 + len(s)
+    assert D.decodeString(buf, p, 4) == "tail" and p.get() == len(buf)
+    long = b"x" * 300
+    buf = bytes([0x80 | (300 & 0x7f), 300 >> 7]) + long
+    p = covt.IntWrapper(0)
+    assert D.decodeString(buf, p) == long.decode() and p.get() == len(buf)
+    with pytest.raises(covt.ArrayIndexOutOfBoundsException):
+        D.decodeString(buf[:-1], covt.IntWrapper(0))

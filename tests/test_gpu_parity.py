@@ -106,40 +106,119 @@ def test_graph_replay_equals_launch(covt, gpu_available, decodable_tiles):
         assert torch.equal(db.d_out, ref_out) and torch.equal(db.d_res, ref_res)
 
 
-def test_multi_gpu_host_api_equals_single(covt, gpu_available, decodable_tiles):
-    plan = covt.Plan.from_tiles([t for _, t in decodable_tiles[:40]])
-    o1, r1 = plan.decode_host(1)
-    o2, r2 = plan.decode_host(2)  # clamps to the visible devices; same shard/gather path
-    assert np.array_equal(r1, r2)
-    assert np.array_equal(o1, o2)
-
-
-def test_host_api_whole_plan_equals_subset_path(covt, gpu_available, decodable_tiles):
-    """covt_plan_decode_host: the whole-plan path (plan's own descriptor table, one D2H into host_out)
-    gives the same bytes as the per-tile subset path, which a plan with a failed tile takes; reused
-    caller buffers (dirty on entry) give the same bytes as fresh ones."""
-    good = [t for _, t in decodable_tiles[:60]]
-    whole = covt.Plan.from_tiles(good)
-    subset = covt.Plan.from_tiles(good + [b"\x01\x05garbage"])  # failed last tile: no streams, same layout
-    assert subset.tile_status[-1] != 0 and subset.output_bytes == whole.output_bytes
-    o1, r1 = whole.decode_host()
-    o2, r2 = subset.decode_host()
-    assert np.array_equal(r1, r2)
-    # every stream's output slice matches; the align-16 padding between slices is unspecified (the
-    # whole-plan path copies the device buffer as the kernels left it, the subset path only slices)
-    s = whole.streams
-    mask = np.zeros(whole.output_bytes, dtype=bool)
+def _slice_mask(plan):
+    s = plan.streams
+    mask = np.zeros(plan.output_bytes, dtype=bool)
     for off, n in zip(s["out_off"], s["out_elems"].astype(np.int64) * s["elem_bytes"]):
         mask[off:off + n] = True
+    return mask
+
+
+def test_forced_shards_equal_single(covt, gpu_available, decodable_tiles):
+    """covt_plan_decode_host_shards with K shards on device 0 runs the multi-GPU shard path (contiguous
+    tile ranges, per-shard descriptor tables, one H2D / launch / D2H each, concurrent host threads) on a
+    one-GPU box: stream slices and results byte-identical to the single-shard call; covt_plan_decode_host_multi
+    (clamped to the visible devices) too."""
+    plan = covt.Plan.from_tiles([t for _, t in decodable_tiles])
+    o1, r1 = plan.decode_host()
+    o1 = o1.copy()
+    mask = _slice_mask(plan)
+    for k in (2, 3, 7, len(decodable_tiles) + 5):  # more shards than tiles: empty shards are fine
+        ok, rk = plan.decode_host(shard_devices=[0] * k)
+        assert np.array_equal(rk, r1), k
+        assert np.array_equal(ok[mask], o1[mask]), k
+    o2, r2 = plan.decode_host(2)
+    assert np.array_equal(r2, r1) and np.array_equal(o2[mask], o1[mask])
+    plan.release_device()
+    o3, r3 = plan.decode_host(shard_devices=[0, 0])  # rebuilt after release
+    assert np.array_equal(r3, r1) and np.array_equal(o3[mask], o1[mask])
+
+
+def test_host_api_failed_tile_and_reused_buffers(covt, gpu_available, decodable_tiles):
+    """A plan with a failed tile (no streams, same layout) decodes the rest identically; reused caller
+    buffers (dirty on entry) get the same stream slices as fresh ones, call after call."""
+    good = [t for _, t in decodable_tiles[:60]]
+    whole = covt.Plan.from_tiles(good)
+    bad = covt.Plan.from_tiles(good + [b"\x01\x05garbage"])  # failed last tile
+    assert bad.tile_status[-1] != 0 and bad.output_bytes == whole.output_bytes
+    o1, r1 = whole.decode_host()
+    o1 = o1.copy()
+    o2, r2 = bad.decode_host()
+    assert np.array_equal(r1, r2)
+    mask = _slice_mask(whole)  # bytes outside the stream slices are unspecified (include/covt.h)
     assert np.array_equal(o1[mask], o2[mask])
     out = np.full(whole.output_bytes + 64, 0xAB, dtype=np.uint8)
     res = np.full((whole.num_streams, 2), -7, dtype=np.int32)
-    for _ in range(2):
+    for _ in range(3):
         o3, r3 = whole.decode_host(out=out, res=res)
         assert o3.ctypes.data == out.ctypes.data
-        assert np.array_equal(o3, o1) and np.array_equal(r3, r1)
+        assert np.array_equal(o3[mask], o1[mask]) and np.array_equal(r3, r1)
+        out[:] = 0xCD
     with pytest.raises(ValueError):
         whole.decode_host(out=np.zeros(1, dtype=np.uint8))
+
+
+@pytest.mark.parametrize("id_mode", [0, 1], ids=["id_format", "id_java"])
+def test_full_batch_digests(covt, gpu_available, golden_streams, id_mode):
+    """BASELINE config 5 at full size (the bench's 10k-tile batch, 4.5 GB of output, slices past 4 GiB
+    included): every stream's SHA-256 and status equal the oracle's for its source tile
+    (tests/golden/oracle_streams.json), decoded by the bench's device-resident launch."""
+    import torch
+
+    import bench
+
+    picks = bench.sample_batch(bench.tile_library(), 10000, bench.SEED)
+    plan = covt.Plan.from_tiles([t for _, t in picks], covt.FORMAT_GENC, id_mode)
+    assert plan.output_bytes > (1 << 32)
+    db = covt.DeviceBatch(plan, "cuda")
+    db.decode()
+    torch.cuda.synchronize()
+    out, res = db.results()
+    del db
+    col = golden_streams["columns"]
+    pre = "fmt_" if id_mode == 0 else "java_"
+    ish, ist, ico = col.index(pre + "sha256"), col.index(pre + "status"), col.index(pre + "consumed")
+    st = plan.streams
+    bounds = np.searchsorted(st["tile"], np.arange(plan.n_tiles + 1))
+    n_past_4g = 0
+    for t, (key, _) in enumerate(picks):
+        rows = golden_streams["tiles"][key]["streams"]
+        i0, i1 = int(bounds[t]), int(bounds[t + 1])
+        assert i1 - i0 == len(rows), key
+        for i, row in zip(range(i0, i1), rows):
+            assert int(res[i][0]) == row[ist], (key, i)
+            if row[ist] != 0:
+                continue
+            assert int(res[i][1]) == row[ico], (key, i)
+            assert hashlib.sha256(plan.stream_array(out, i).tobytes()).hexdigest() == row[ish], (key, i)
+            n_past_4g += int(st["out_off"][i] >= (1 << 32))
+    assert n_past_4g > 10000
+
+
+def test_byte_rle_reencode_advance(covt, oracle, gpu_available):
+    """decodeByteRle(byte[], int, IntWrapper) (DecodingUtils.java:290): values as the :275 form, the
+    cursor advanced by the ORC writer's re-encoded length (oracle_encode_byte_rle), including streams
+    whose own encoding is not the writer's (non-canonical groups) and a partially read last group."""
+    D = covt.DecodingUtils
+    rng = np.random.default_rng(290)
+    for trial in range(60):
+        n = int(rng.integers(1, 700))
+        kind = trial % 3
+        if kind == 0:
+            v = rng.integers(0, 3, size=n).astype(np.uint8)
+        elif kind == 1:
+            v = np.repeat(rng.integers(0, 256, size=n // 7 + 1), 7)[:n].astype(np.uint8)
+        else:
+            v = rng.integers(0, 256, size=n).astype(np.uint8)
+        enc = oracle.encode_byte_rle(v)
+        if trial % 5 == 4:  # non-canonical: every value as a 1-literal group (0xff = -1, value)
+            enc = bytes(b for x in v for b in (0xFF, int(x)))
+        m = n if trial % 4 else max(1, n - int(rng.integers(0, min(n, 50))))  # read fewer than encoded
+        buf = b"\x11\x22" + enc + b"\x00" * 8
+        p = covt.IntWrapper(2)
+        got = D.decodeByteRle(buf, m, p)
+        assert np.array_equal(got, v[:m]), trial
+        assert p.get() == 2 + len(oracle.encode_byte_rle(v[:m])), trial
 
 
 def test_decode_covt_layers(covt, gpu_available, oracle):

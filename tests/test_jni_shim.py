@@ -1,0 +1,137 @@
+"""The JNI shim (cov-tiles_amd/jni/covt_jni.cc) driven through a hand-built JNIEnv function table
+(tests/jni/jni.h + jni_shim_test.cc, a fake VM; no JDK in this image).  CPU: the status -> Java
+exception mapping and IntWrapper handling.  GPU: every GpuDecodingUtils native on every Id/Geometry
+stream of fixture tiles against the Java-semantics oracle, and GpuCovtBatch create + decode."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, tile_paths
+
+EXE = os.path.join(ROOT, "tests", "jni", "jni_shim_test")
+
+
+@pytest.fixture(scope="module")
+def shim(covt):
+    covt.lib()
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "jni")])
+    return EXE
+
+
+def run(exe, cases):
+    p = subprocess.run([exe], input="\n".join(cases) + "\n", capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = p.stdout.splitlines()
+    assert len(out) == len(cases)
+    return out
+
+
+def test_status_to_exception_mapping(shim):
+    import torch
+
+    cases = ["varint 0 -1 | 0102",  # COVT_ERR_INVALID_ARG -> IllegalArgumentException
+             "varint 5 1 | 0102",  # pos past the array: COVT_ERR_TRUNCATED -> ArrayIndexOutOfBoundsException
+             "fpf 4 -8 0 | 00000000",  # negative byteLength: IllegalArgumentException
+             "morton 0 1 300 | 01",  # numBits out of range: IllegalArgumentException
+             "byterle3 2 9 | fe0102"]  # pos past the array
+    want = ["IllegalArgumentException", "ArrayIndexOutOfBoundsException", "IllegalArgumentException",
+            "IllegalArgumentException", "ArrayIndexOutOfBoundsException"]
+    pos0 = [0, 5, 0, 0, 9]
+    for got, w, p0 in zip(run(shim, cases), want, pos0):
+        kind, cls, pos = got.split()
+        assert kind == "exc" and cls == "java/lang/" + w and int(pos) == p0  # the cursor is left alone
+    if not torch.cuda.is_available():  # a well-formed call with no device: IllegalStateException, no CPU path
+        (got,) = run(shim, ["varint 0 2 | 0102"])
+        assert got.split()[:2] == ["exc", "java/lang/IllegalStateException"]
+
+
+def _stream_cases(oracle, t):
+    """One shim case per Id/Geometry stream of tile t (the CovtParser.decodeGeometryColumn / decodedIds
+    dispatch, CovtParser.java:392-572) with the oracle's expected (status, array, pos after)."""
+    st, ss = oracle.walk_tile(t)
+    assert st == 0
+    hx = t.hex()
+    cases, want = [], []
+    for s in ss:
+        off, n, bl, nb = s.offset, s.num_values, s.byte_length, s.num_bits
+        if s.column_kind == 1 and s.stream_type == 4:
+            cases.append("byterle %d %d %d | %s" % (n, off, bl, hx))
+            want.append(oracle.decode_byte_rle(t, n, off, bl))
+        elif s.encoding == 5:
+            cases.append("rle %d %d 0 | %s" % (n, off, hx))
+            want.append(oracle.decode_rle(t, n, off, False))
+        elif s.encoding == 9:
+            if s.stream_type == 9 and s.column_type == 4:
+                cases.append("fpfmorton %d %d %d %d | %s" % (n, bl, off, nb, hx))
+                want.append(oracle.decode_fastpfor_delta_morton_codes(t, n, bl, off, nb))
+            elif s.stream_type == 9:
+                m = n * (2 if s.column_type == 3 else 1)
+                cases.append("fpfcoords %d %d %d | %s" % (m, bl, off, hx))
+                want.append(oracle.decode_fastpfor_delta_coordinates(t, m, bl, off))
+            else:
+                cases.append("fpf %d %d %d | %s" % (n, bl, off, hx))
+                want.append(oracle.decode_fastpfor_zigzag_delta(t, n, bl, off))
+        elif s.encoding == 4:
+            if s.stream_type == 9 and s.column_type == 4:
+                cases.append("morton %d %d %d | %s" % (off, n, nb, hx))
+                want.append(oracle.decode_delta_varint_morton_codes(t, off, n, nb))
+            elif s.stream_type == 9:
+                m = n * (2 if s.column_type == 3 else 1)
+                cases.append("coords %d %d | %s" % (off, m, hx))
+                want.append(oracle.decode_zigzag_delta_varint_coordinates(t, off, m))
+            else:
+                cases.append("zzdelta %d %d | %s" % (off, n, hx))
+                want.append(oracle.decode_zigzag_delta_varint(t, off, n))
+        elif s.encoding == 1:
+            cases.append("varint %d %d | %s" % (off, n, hx))
+            want.append(oracle.decode_varint(t, off, n))
+    return cases, want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ["omt/5_16_20", "omt/14_8298_10748", "bing/4-8-5"])
+def test_gpu_decoding_utils_through_jni(shim, oracle, gpu_available, key):
+    t = open(os.path.join(ROOT, "tests", "golden", "tiles", key + ".covt"), "rb").read()
+    cases, want = _stream_cases(oracle, t)
+    assert len(cases) >= 10
+    for c, got, (ost, arr, pend) in zip(cases, run(shim, cases), want):
+        assert ost == 0
+        kind, pos, hx = got.split()
+        assert kind == "ok", (c[:40], got)
+        assert int(pos) == pend, c[:40]
+        assert bytes.fromhex(hx) == np.ascontiguousarray(arr).tobytes(), c[:40]
+
+
+@pytest.mark.gpu
+def test_gpu_byte_rle_reencode_and_kats_through_jni(shim, oracle, gpu_available):
+    rng = np.random.default_rng(7)
+    v = np.repeat(rng.integers(0, 6, size=40), rng.integers(1, 9, size=40)).astype(np.uint8)
+    enc = oracle.encode_byte_rle(v)
+    (got,) = run(shim, ["byterle3 %d 1 | 00%s00" % (v.size, enc.hex())])
+    kind, pos, hx = got.split()
+    assert kind == "ok" and int(pos) == 1 + len(enc) and bytes.fromhex(hx) == v.tobytes()
+    # TS known-answer vectors (parser/js/test/unit/decoder/decodingUtils.spec.ts) through the shim
+    out = run(shim, ["varint 0 1 | 80808004", "rle 10 0 0 | 020101020101", "rle 100 0 1 | 61000e"])
+    assert out[0] == "ok 4 " + np.array([8388608], "<i4").tobytes().hex()
+    assert out[1] == "ok 6 " + np.array([1, 2, 3, 4, 5, 1, 2, 3, 4, 5], "<i8").tobytes().hex()
+    assert out[2] == "ok 3 " + np.full(100, 7, "<i8").tobytes().hex()
+
+
+@pytest.mark.gpu
+def test_gpu_covt_batch_through_jni(shim, covt, gpu_available):
+    """GpuCovtBatch.create + decode over a direct ByteBuffer: statuses and output bytes equal the
+    ctypes host path's."""
+    t = open(os.path.join(ROOT, "tests", "golden", "tiles", "omt", "5_16_20.covt"), "rb").read()
+    (got,) = run(shim, ["batch | " + t.hex()])
+    kind, ns, st_hex, out_hex = got.split()
+    plan = covt.Plan.from_tiles([t])
+    out, res = plan.decode_host()
+    assert kind == "ok" and int(ns) == plan.num_streams
+    assert np.array_equal(np.frombuffer(bytes.fromhex(st_hex), "<i4"), res[:, 0])
+    jout = np.frombuffer(bytes.fromhex(out_hex), np.uint8)
+    for i in range(plan.num_streams):
+        s = plan.streams[i]
+        o, n = int(s["out_off"]), int(s["out_elems"]) * int(s["elem_bytes"])
+        assert np.array_equal(jout[o:o + n], out[o:o + n]), i
