@@ -660,35 +660,6 @@ class DeviceBatch:
         return DeviceSubset(self, mask)
 
 
-class DeviceSubset:
-    """One decode launch over a subset of a DeviceBatch's streams (e.g. BASELINE configs 2-4, which are
-    stream selections of fixture tiles); its own descriptor table and result array on the device."""
-
-    def __init__(self, batch: DeviceBatch, mask):
-        import torch
-
-        self.batch = batch
-        descs, self.family_counts, self.stream_index = batch.plan.subset_descs(mask)
-        self.num_streams = int(self.stream_index.size)
-        self.d_desc = torch.from_numpy(descs).to(batch.device) if self.num_streams else \
-            torch.zeros(32, dtype=torch.uint8, device=batch.device)
-        self.d_res = torch.zeros(max(self.num_streams, 1) * 2, dtype=torch.int32, device=batch.device)
-
-    def decode(self, stream=None):
-        import torch
-
-        b = self.batch
-        s = stream if stream is not None else torch.cuda.current_stream(b.device)
-        _raise(lib().covt_decode_streams_device_grouped(b.d_in.data_ptr(), self.d_desc.data_ptr(),
-                                                        _ptr(self.family_counts, C.c_int64), b.d_out.data_ptr(),
-                                                        self.d_res.data_ptr(), s.cuda_stream),
-               "covt_decode_streams_device_grouped")
-
-    def results(self):
-        """(full output bytes, results[num_streams, 2] of the subset in launch order, plan-order index)."""
-        out = self.batch.d_out.cpu().numpy()[:self.batch.plan.output_bytes]
-        return out, self.d_res.cpu().numpy().reshape(-1, 2)[:self.num_streams], self.stream_index
-
     def _asm_buffers(self):
         import torch
 
@@ -752,6 +723,36 @@ class DeviceSubset:
         res_launch = self.d_res.cpu().numpy().reshape(-1, 2)[:self.plan.num_streams]
         res = res_launch[self.plan.streams["desc_index"]] if self.plan.num_streams else res_launch
         return out, res
+
+
+class DeviceSubset:
+    """One decode launch over a subset of a DeviceBatch's streams (e.g. BASELINE configs 2-4, which are
+    stream selections of fixture tiles); its own descriptor table and result array on the device."""
+
+    def __init__(self, batch: DeviceBatch, mask):
+        import torch
+
+        self.batch = batch
+        descs, self.family_counts, self.stream_index = batch.plan.subset_descs(mask)
+        self.num_streams = int(self.stream_index.size)
+        self.d_desc = torch.from_numpy(descs).to(batch.device) if self.num_streams else \
+            torch.zeros(32, dtype=torch.uint8, device=batch.device)
+        self.d_res = torch.zeros(max(self.num_streams, 1) * 2, dtype=torch.int32, device=batch.device)
+
+    def decode(self, stream=None):
+        import torch
+
+        b = self.batch
+        s = stream if stream is not None else torch.cuda.current_stream(b.device)
+        _raise(lib().covt_decode_streams_device_grouped(b.d_in.data_ptr(), self.d_desc.data_ptr(),
+                                                        _ptr(self.family_counts, C.c_int64), b.d_out.data_ptr(),
+                                                        self.d_res.data_ptr(), s.cuda_stream),
+               "covt_decode_streams_device_grouped")
+
+    def results(self):
+        """(full output bytes, results[num_streams, 2] of the subset in launch order, plan-order index)."""
+        out = self.batch.d_out.cpu().numpy()[:self.batch.plan.output_bytes]
+        return out, self.d_res.cpu().numpy().reshape(-1, 2)[:self.num_streams], self.stream_index
 
 
 # ---------------------------------------------------------------------------

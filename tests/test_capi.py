@@ -223,3 +223,12 @@ def test_floats_le_and_string_entries(covt):
     assert D.decodeString(buf, p) == long.decode() and p.get() == len(buf)
     with pytest.raises(covt.ArrayIndexOutOfBoundsException):
         D.decodeString(buf[:-1], covt.IntWrapper(0))
+
+
+def test_device_batch_api_surface(covt):
+    """The device-resident batch classes keep their whole method set (checked on CPU)."""
+    for m in ("decode", "decode_graph", "subset", "assemble", "materialize_properties", "results",
+              "assembly_results", "property_results"):
+        assert callable(getattr(covt.DeviceBatch, m, None)), m
+    for m in ("decode", "results"):
+        assert callable(getattr(covt.DeviceSubset, m, None)), m

@@ -96,9 +96,10 @@ def test_gpu_decoding_utils_through_jni(shim, oracle, gpu_available, key):
     t = open(os.path.join(ROOT, "tests", "golden", "tiles", key + ".covt"), "rb").read()
     cases, want = _stream_cases(oracle, t)
     assert len(cases) >= 10
-    for c, got, (ost, arr, pend) in zip(cases, run(shim, cases), want):
+    for c, got, o in zip(cases, run(shim, cases), want):
+        ost, arr, pend = o[0], o[1], o[2]
         assert ost == 0
-        kind, pos, hx = got.split()
+        kind, pos, hx = (got.split() + [""])[:3]  # an empty result array prints no hex
         assert kind == "ok", (c[:40], got)
         assert int(pos) == pend, c[:40]
         assert bytes.fromhex(hx) == np.ascontiguousarray(arr).tobytes(), c[:40]
