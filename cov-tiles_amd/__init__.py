@@ -36,8 +36,10 @@ ERR_DEVICE = -5
 ERR_INVALID_ARG = -6
 INPUT_PADDING = 4096
 FORMAT_GENC, FORMAT_GEND = 0, 1
-FAMILY_RLE, FAMILY_VARINT, FAMILY_FASTPFOR, FAMILY_LANE = 0, 1, 2, 3
-NUM_FAMILIES = 4
+FAMILY_RLE, FAMILY_VARINT, FAMILY_FASTPFOR, FAMILY_LANE, FAMILY_SPLIT = 0, 1, 2, 3, 4
+NUM_FAMILIES = 5
+DESC_LANE, DESC_SPLIT, DESC_SPLIT_PAD = 0x1, 0x2, 0x4
+SPLIT_SLOTS = 6
 ID_FORMAT, ID_JAVA = 0, 1
 
 (OP_NONE, OP_BYTE_RLE_U8, OP_RLE_U64, OP_RLE_I32, OP_RLE_S64, OP_VARINT_I32, OP_VARINT_ZZ_I32,
@@ -155,7 +157,7 @@ EXPORTED_SYMBOLS = (
     "covt_plan_create_ex", "covt_plan_num_property_columns", "covt_plan_property_bytes",
     "covt_plan_property_columns", "covt_plan_property_descs", "covt_materialize_properties_device",
     "covt_plan_properties_host", "covt_decode_byte_rle_reencode", "covt_decode_floats_le", "covt_decode_string",
-    "covt_plan_decode_host_shards", "covt_plan_release_device",
+    "covt_plan_decode_host_shards", "covt_plan_release_device", "covt_plan_num_descs", "covt_plan_desc_streams",
 )
 
 
@@ -205,6 +207,9 @@ def lib() -> C.CDLL:
     L.covt_plan_totals.argtypes = [vp, i64p, i64p, i64p]
     L.covt_plan_streams.argtypes = [vp, vp]
     L.covt_plan_descs.argtypes = [vp, vp]
+    L.covt_plan_num_descs.argtypes = [vp]
+    L.covt_plan_num_descs.restype = C.c_int64
+    L.covt_plan_desc_streams.argtypes = [vp, i64p]
     L.covt_plan_tile_status.argtypes = [vp, i32p]
     L.covt_decode_streams_device.argtypes = [vp, vp, C.c_int64, vp, vp, vp]
     L.covt_decode_streams_device_grouped.argtypes = [vp, vp, i64p, vp, vp, vp]
@@ -454,9 +459,12 @@ class Plan:
         self.streams = np.zeros(self.num_streams, dtype=STREAM_INFO_DTYPE)
         if self.num_streams:
             L.covt_plan_streams(h, self.streams.ctypes.data)
-        self.descs = np.zeros(self.num_streams * 32, dtype=np.uint8)
-        if self.num_streams:
+        self.num_descs = int(L.covt_plan_num_descs(h))  # >= num_streams: split chunks and their pads
+        self.descs = np.zeros(self.num_descs * 32, dtype=np.uint8)
+        self.desc_streams = np.zeros(self.num_descs, dtype=np.int64)
+        if self.num_descs:
             L.covt_plan_descs(h, self.descs.ctypes.data)
+            L.covt_plan_desc_streams(h, _ptr(self.desc_streams, C.c_int64))
         self.family_counts = np.zeros(NUM_FAMILIES, dtype=np.int64)
         L.covt_plan_family_counts(h, _ptr(self.family_counts, C.c_int64))
         self.tile_status = np.zeros(max(self.n_tiles, 1), dtype=np.int32)[:self.n_tiles]
@@ -587,19 +595,19 @@ class Plan:
     def subset_descs(self, mask):
         """Descriptor table of the streams selected by `mask` (bool per stream, plan order), in launch
         order (still grouped by family, largest first inside a family) -> (uint8 descs, family counts,
-        plan-order stream index per selected descriptor).  Outputs keep their slices in the full output
+        plan-order stream index of each selected descriptor that holds a stream's result, else -1).
+        Outputs keep their slices in the full output
         buffer; results land at the subset position."""
         mask = np.asarray(mask, dtype=bool)
         if mask.shape != (self.num_streams,):
             raise ValueError("subset mask must have one entry per stream")
-        keep = np.zeros(self.num_streams, dtype=bool)
-        keep[self.streams["desc_index"][mask]] = True
+        keep = mask[self.desc_streams]  # every descriptor of a selected stream (split chunks + pads)
         fam = np.repeat(np.arange(NUM_FAMILIES), self.family_counts)
-        inv = np.empty(self.num_streams, dtype=np.int64)
-        inv[self.streams["desc_index"]] = np.arange(self.num_streams)
+        primary = np.full(self.num_descs, -1, dtype=np.int64)  # the descriptor holding the stream's result
+        primary[self.streams["desc_index"]] = np.arange(self.num_streams)
         descs = np.ascontiguousarray(self.descs.reshape(-1, 32)[keep]).reshape(-1)
         counts = np.bincount(fam[keep], minlength=NUM_FAMILIES).astype(np.int64)
-        return descs, counts, inv[keep]
+        return descs, counts, primary[keep]
 
     def stream_array(self, out: np.ndarray, i: int) -> np.ndarray:
         s = self.streams[i]
@@ -620,8 +628,8 @@ class DeviceBatch:
         self.d_in = torch.from_numpy(plan.blob).to(self.device)
         if self.d_in.data_ptr() % 16:
             raise DeviceError("device input buffer is not 16-byte aligned")
-        n = max(plan.num_streams, 1)
-        self.d_desc = torch.from_numpy(plan.descs).to(self.device) if plan.num_streams else \
+        n = max(plan.num_descs, 1)  # one result entry per descriptor (split pads hold look-back records)
+        self.d_desc = torch.from_numpy(plan.descs).to(self.device) if plan.num_descs else \
             torch.zeros(32, dtype=torch.uint8, device=self.device)
         self.d_out = torch.zeros(max(plan.output_bytes, 16), dtype=torch.uint8, device=self.device)
         self.d_res = torch.zeros(n * 2, dtype=torch.int32, device=self.device)
@@ -720,7 +728,7 @@ class DeviceBatch:
     def results(self):
         """(output bytes, results in plan order) copied to the host."""
         out = self.d_out.cpu().numpy()[:self.plan.output_bytes]
-        res_launch = self.d_res.cpu().numpy().reshape(-1, 2)[:self.plan.num_streams]
+        res_launch = self.d_res.cpu().numpy().reshape(-1, 2)[:self.plan.num_descs]
         res = res_launch[self.plan.streams["desc_index"]] if self.plan.num_streams else res_launch
         return out, res
 
@@ -734,10 +742,11 @@ class DeviceSubset:
 
         self.batch = batch
         descs, self.family_counts, self.stream_index = batch.plan.subset_descs(mask)
-        self.num_streams = int(self.stream_index.size)
-        self.d_desc = torch.from_numpy(descs).to(batch.device) if self.num_streams else \
+        self.num_descs = int(self.stream_index.size)
+        self.num_streams = int((self.stream_index >= 0).sum())
+        self.d_desc = torch.from_numpy(descs).to(batch.device) if self.num_descs else \
             torch.zeros(32, dtype=torch.uint8, device=batch.device)
-        self.d_res = torch.zeros(max(self.num_streams, 1) * 2, dtype=torch.int32, device=batch.device)
+        self.d_res = torch.zeros(max(self.num_descs, 1) * 2, dtype=torch.int32, device=batch.device)
 
     def decode(self, stream=None):
         import torch
@@ -750,9 +759,11 @@ class DeviceSubset:
                "covt_decode_streams_device_grouped")
 
     def results(self):
-        """(full output bytes, results[num_streams, 2] of the subset in launch order, plan-order index)."""
+        """(full output bytes, results[k, 2] of the subset's k streams, their plan-order indices)."""
         out = self.batch.d_out.cpu().numpy()[:self.batch.plan.output_bytes]
-        return out, self.d_res.cpu().numpy().reshape(-1, 2)[:self.num_streams], self.stream_index
+        res = self.d_res.cpu().numpy().reshape(-1, 2)[:self.num_descs]
+        prim = self.stream_index >= 0
+        return out, res[prim], self.stream_index[prim]
 
 
 # ---------------------------------------------------------------------------

@@ -1440,7 +1440,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(cons
     const int64_t sid = (int64_t)blockIdx.x * kWavesPerBlock + wv;
     if (sid >= n_streams) return;
     const covt_stream_desc d = descs[sid];
-    if ((d.flags & COVT_DESC_LANE) || op_family(d.op) != FAM) return;
+    if ((d.flags & (COVT_DESC_LANE | COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD)) || op_family(d.op) != FAM) return;
     // long streams are the kernel's critical path: let their waves win instruction arbitration
     if (d.byte_length > kLongStream || d.num_values > kLongStream) __builtin_amdgcn_s_setprio(2);
 #ifdef COVT_TIMING  // profiling build (libcovt_timing.so): result = (duration, start) in 100 MHz ticks
@@ -1507,6 +1507,205 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(cons
             for (int k = 0; k < kPhases; ++k) covt_phase_buf[(descs + sid - covt_phase_desc0) * kPhases + k] = c.ph[k];
 #endif
         res[sid] = r;
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// long streams split into chunks (COVT_FAMILY_SPLIT; plan rule and layout in include/covt.h)
+// --------------------------------------------------------------------------------------------
+// A long varint stream is a serial chain only through two things: where each value starts and the
+// running sum of the delta ops.  Both are local once a chunk knows its first value and its
+// predecessors' totals: every byte with bit 7 clear ends a Java-capped varint (a value's bytes are
+// continuation bytes then one terminator, or four bytes), so the value after the last such byte
+// before the chunk starts a value; values are owned by the chunk their last byte falls in.  Each
+// chunk wave (1) finds its first owned value, (2) decodes its values once to count and sum them
+// (no stores), (3) publishes that aggregate, (4) looks back over its predecessors' records (their
+// inclusive prefix if published, else their aggregate and one step further back) for the values
+// and sums before it, publishes its inclusive prefix, and (5) decodes again with that carry,
+// storing its values at their global indices.  Chunks take tickets from a counter in launch order,
+// so a chunk only ever waits on chunks whose waves were started before it.
+constexpr int kSplitSlots = COVT_SPLIT_SLOTS;
+struct Agg {
+    int32_t cnt;
+    uint32_t sx, sy;  // wrapping sums of the transformed values (x,y ops: of local-even / local-odd values)
+};
+// a's values followed by b's: b's parity flips when a holds an odd number of values
+__device__ __forceinline__ Agg agg_cat(const Agg& a, const Agg& b, bool xy) {
+    const bool sw = xy && (a.cnt & 1);
+    return Agg{a.cnt + b.cnt, a.sx + (sw ? b.sy : b.sx), a.sy + (sw ? b.sx : b.sy)};
+}
+// record = 4 dwords {flag, cnt, sx, sy}: values first, then the flag with release semantics
+__device__ __forceinline__ void rec_publish(uint32_t* r, const Agg& a, uint32_t flag) {
+    if (lane_id() == 0) {
+        __hip_atomic_store(r + 1, (uint32_t)a.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(r + 2, a.sx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(r + 3, a.sy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(r, flag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+__device__ __forceinline__ Agg rec_read(uint32_t* r) {
+    Agg a;
+    a.cnt = (int32_t)uniu(__hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    a.sx = uniu(__hip_atomic_load(r + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    a.sy = uniu(__hip_atomic_load(r + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return a;
+}
+constexpr int kRecAgg = 2, kRecIncl = 6;  // dword offsets of the records in a chunk's result entries
+constexpr uint32_t kSpinLimit = 1u << 22;  // ~0.5 s of polling: a predecessor that never publishes
+// values and sums before chunk `chunk` (ticket t) of a stream: its predecessors are tickets t-chunk..t-1
+__device__ Agg lookback(covt_stream_result* res, int64_t t, int32_t chunk, bool xy, int32_t& err) {
+    Agg acc{0, 0u, 0u};
+    int64_t k = t - 1;
+    uint32_t spins = 0;
+    for (int32_t left = chunk; left > 0;) {
+        uint32_t* r = (uint32_t*)(res + kSplitSlots * k);
+        if (uniu(__hip_atomic_load(r + kRecIncl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 2u) {
+            acc = agg_cat(rec_read(r + kRecIncl), acc, xy);
+            break;
+        }
+        if (uniu(__hip_atomic_load(r + kRecAgg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 1u) {
+            acc = agg_cat(rec_read(r + kRecAgg), acc, xy);
+            --k;
+            --left;
+            continue;
+        }
+        if (++spins > kSpinLimit) { err = COVT_ERR_DEVICE; break; }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return acc;
+}
+
+// One chunk [s, e) of a split Java-capped varint stream (ops of split_op, include/covt_internal.h).
+template <int OP>
+__device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, covt_stream_result* res, int64_t t) {
+    constexpr bool kXY = OP == COVT_OP_VARINT_ZZ_DELTA_XY;
+    constexpr bool kZZ = OP == COVT_OP_VARINT_ZZ_I32 || OP == COVT_OP_VARINT_ZZ_DELTA_I32 || kXY ||
+                         OP == COVT_OP_VARINT_ZZ_I32_AS_I64 || OP == COVT_OP_VARINT_ZZ_DELTA_I64;
+    constexpr bool kSum = OP == COVT_OP_VARINT_ZZ_DELTA_I32 || kXY || OP == COVT_OP_VARINT_DELTA_MORTON ||
+                          OP == COVT_OP_VARINT_ZZ_DELTA_I64;
+    const int l = lane_id();
+    // (1) the last byte before s with bit 7 clear ends a value; search back 1 KiB at a time
+    int32_t p = 0;
+    if (chunk > 0) {
+        const uintptr_t lo = (uintptr_t)c.sb & ~(uintptr_t)15;
+        int32_t hi = s, last = -1;
+        while (hi > 0) {
+            uintptr_t w0 = ((uintptr_t)(c.sb + hi) & ~(uintptr_t)15);
+            w0 = w0 >= lo + 1008 ? w0 - 1008 : lo;
+            const uint4 d = ld128(w0 + 16 * (uintptr_t)l);
+            const int32_t q0 = (int32_t)((intptr_t)(w0 + 16 * (uintptr_t)l) - (intptr_t)c.sb);
+            const uint32_t T = ~hibits16(d) & 0xffffu & range16(-q0, hi - q0);
+            const uint32_t best = T ? (uint32_t)(q0 + 31 - __builtin_clz(T)) + 1u : 0u;
+            const uint32_t m = wave_max(best);
+            if (m) { last = (int32_t)m - 1; break; }
+            hi = (int32_t)((intptr_t)w0 - (intptr_t)c.sb);
+        }
+        p = last + 1;
+        // values of 4 continuation bytes may still end before s: skip them
+        while (p < s) {
+            const uint32_t x = uniu(ld_le32(c.sb + p));
+            const uint32_t u = ~x & 0x80808080u;
+            const int32_t len = u ? (__builtin_ctz(u) >> 3) + 1 : 4;
+            if (p + len - 1 >= s) break;
+            p += len;
+        }
+    }
+    // (2) count and sum the values ending in [s, e)
+    Win w;
+    w.valid = false;
+    int32_t pa = p, err = 0;
+    uint32_t ax = 0, ay = 0;
+    const int32_t cnt = varint_take<MODE_RAW, VAL_J4, 4>(
+        *c.sm, c.sb, w, pa, e, INT32_MAX, true, err,
+        [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
+            if constexpr (kSum) {
+                const int32_t s0 = 4 * l - first;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const bool ok = s0 + k >= 0 && s0 + k < count;
+                    const uint32_t z = ok ? (kZZ ? (uint32_t)zz32(lo[k]) : lo[k]) : 0u;
+                    const bool odd = kXY && (((uint32_t)(base + 4 * l + k)) & 1u);
+                    ax += odd ? 0u : z;
+                    ay += odd ? z : 0u;
+                }
+            }
+        });
+    Agg mine{cnt, 0u, 0u};
+    if constexpr (kSum) {
+        mine.sx = lane_bcast(incl_scan(ax), 63);
+        mine.sy = kXY ? lane_bcast(incl_scan(ay), 63) : 0u;
+    }
+    // (3) + (4) publish, look back, publish the inclusive prefix
+    uint32_t* rec = (uint32_t*)(res + kSplitSlots * t);
+    Agg excl{0, 0u, 0u};
+    if (chunk == 0) {
+        rec_publish(rec + kRecIncl, mine, 2u);
+    } else {
+        rec_publish(rec + kRecAgg, mine, 1u);
+        excl = lookback(res, t, chunk, kXY, err);
+        rec_publish(rec + kRecIncl, agg_cat(excl, mine, kXY), 2u);
+    }
+    // (5) decode again with the carry; values past num_values are not stored
+    const int32_t take = min(cnt, c.n - excl.cnt);
+    int32_t pos = p;
+    if (take > 0 && !err) {
+        w.valid = false;
+        Carry cr{excl.sx, excl.sy};
+        const int32_t g0 = excl.cnt;
+        varint_take<MODE_RAW, VAL_J4, 4>(
+            *c.sm, c.sb, w, pos, e, take, false, err,
+            [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
+                sink_values<OP, 4>(lo, (int64_t)g0 + base, first, count, c.nb, c.out, cr);
+            },
+            g0);
+    }
+    // the stream's result, from the chunk holding its last value (or the last chunk if it is short)
+    covt_stream_result* r0 = res + kSplitSlots * (t - chunk);
+    const bool has_last = excl.cnt < c.n && excl.cnt + cnt >= c.n;
+    const bool short_end = e >= c.byte_length && excl.cnt + cnt < c.n;
+    if (l == 0 && (has_last || short_end || err)) {
+        covt_stream_result r;
+        r.status = err ? err : (has_last ? COVT_OK : COVT_ERR_TRUNCATED);
+        r.consumed = pos;
+        *r0 = r;
+    }
+}
+
+// One wave per chunk, chunks in ticket order (tickets from a counter in the family's result entries).
+__global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const uint8_t* __restrict__ in,
+                                                                           const covt_stream_desc* __restrict__ descs,
+                                                                           int64_t n_chunks, uint8_t* __restrict__ out,
+                                                                           covt_stream_result* __restrict__ res) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kFamSmemVarint];
+    const int wv = uni((int)(threadIdx.x >> 6));
+    uint32_t* ctr = (uint32_t*)(res + 5);  // chunk 0's sixth entry
+    uint32_t tk = 0;
+    if (lane_id() == 0) tk = atomicAdd(ctr, 1u);
+    const int64_t t = (int64_t)lane_bcast(tk, 0);
+    if (t >= n_chunks) return;
+    const covt_stream_desc d = descs[kSplitSlots * t];
+    const covt_stream_desc rg = descs[kSplitSlots * t + 1];  // the chunk's byte range
+    Ctx c;
+    c.sm = (WaveSmem*)(smem + wv * kFamSmemVarint);
+    c.sb = in + d.in_off;
+    c.out = out + d.out_off;
+    c.avail = d.byte_length;
+    c.n = d.num_values;
+    c.nb = d.num_bits;
+    c.op = d.op;
+    c.byte_length = d.byte_length;
+    c.err = 0;
+    c.consumed = 0;
+    const int32_t chunk = d.avail, s = (int32_t)rg.in_off, e = (int32_t)rg.out_off;
+    switch (d.op) {
+    case COVT_OP_VARINT_I32: run_varint_chunk<COVT_OP_VARINT_I32>(c, s, e, chunk, res, t); break;
+    case COVT_OP_VARINT_ZZ_I32: run_varint_chunk<COVT_OP_VARINT_ZZ_I32>(c, s, e, chunk, res, t); break;
+    case COVT_OP_VARINT_ZZ_DELTA_I32: run_varint_chunk<COVT_OP_VARINT_ZZ_DELTA_I32>(c, s, e, chunk, res, t); break;
+    case COVT_OP_VARINT_ZZ_DELTA_XY: run_varint_chunk<COVT_OP_VARINT_ZZ_DELTA_XY>(c, s, e, chunk, res, t); break;
+    case COVT_OP_VARINT_DELTA_MORTON: run_varint_chunk<COVT_OP_VARINT_DELTA_MORTON>(c, s, e, chunk, res, t); break;
+    case COVT_OP_VARINT_I32_AS_I64: run_varint_chunk<COVT_OP_VARINT_I32_AS_I64>(c, s, e, chunk, res, t); break;
+    case COVT_OP_VARINT_ZZ_I32_AS_I64: run_varint_chunk<COVT_OP_VARINT_ZZ_I32_AS_I64>(c, s, e, chunk, res, t); break;
+    default: run_varint_chunk<COVT_OP_VARINT_ZZ_DELTA_I64>(c, s, e, chunk, res, t); break;
     }
 }
 
@@ -1726,6 +1925,13 @@ extern "C" int covt_launch_family(int fam, const uint8_t* d_in, const covt_strea
         hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_FASTPFOR>, grid, block, 0, stream, d_in, d_desc,
                            n_streams, d_out, d_res);
         break;
+    case COVT_FAMILY_SPLIT: {
+        const int64_t n_chunks = n_streams / covt::kSplitSlots;
+        if (n_chunks * covt::kSplitSlots != n_streams) return COVT_ERR_INVALID_ARG;
+        const dim3 sgrid((unsigned)((n_chunks + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock));
+        hipLaunchKernelGGL(covt::decode_split_kernel, sgrid, block, 0, stream, d_in, d_desc, n_chunks, d_out, d_res);
+        break;
+    }
     default: return COVT_ERR_INVALID_ARG;
     }
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;

@@ -446,6 +446,11 @@ int run_one(const uint8_t* region, size_t region_len, size_t pad_to, int op, int
 }
 
 // stream-level wrappers: varint / RLE ops read [pos, buf_len) (Java reads up to the array end)
+int64_t env_i64(const char* name, int64_t dflt) {
+    const char* e = std::getenv(name);
+    return (e && *e) ? std::strtoll(e, nullptr, 10) : dflt;
+}
+
 // Most bytes decoding n values of `op` can read from *pos on: Java's capped varints take <= 4 bytes
 // each (DecodingUtils.java:157-186); an ORC RLE reader reads whole groups, so past n values it may
 // still read the rest of the last group (<= 128 literal varints of <= 10 bytes, RunLengthIntegerReader;
@@ -536,21 +541,22 @@ int fpf_call(const uint8_t* buf, size_t buf_len, int32_t* pos, int op, int32_t n
     return COVT_OK;
 }
 
-// Fork/join of the family kernels: RLE on the caller's stream, the other three on auxiliary
+// Fork/join of the family kernels: RLE on the caller's stream, the other four on auxiliary
 // streams ordered by events (capturable into a hipGraph).  The auxiliary streams and events come
 // from a process-wide per-device pool: a launch takes a set, enqueues, and hands it back, so
 // concurrent callers (one host thread per device, JNI threads) never share one and nothing leaks
 // when threads come and go; the pool holds as many sets as launches ever overlapped.
+constexpr int kForkAux = 4;
 struct ForkCtx {
     int device = -1;
-    hipStream_t aux[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+    hipStream_t aux[kForkAux] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[kForkAux] = {nullptr, nullptr, nullptr, nullptr};
 };
 std::mutex g_fork_mu;
 std::vector<ForkCtx*> g_fork_free;
 
 void fork_destroy(ForkCtx* f) {
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < kForkAux; ++i) {
         if (f->aux[i]) (void)hipStreamDestroy(f->aux[i]);
         if (f->join[i]) (void)hipEventDestroy(f->join[i]);
     }
@@ -570,7 +576,7 @@ ForkCtx* fork_acquire(int dev) {
     auto* f = new ForkCtx();
     f->device = dev;
     bool ok = true;
-    for (int i = 0; i < 3 && ok; ++i)
+    for (int i = 0; i < kForkAux && ok; ++i)
         ok = hipStreamCreateWithFlags(&f->aux[i], hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&f->join[i], hipEventDisableTiming) == hipSuccess;
     if (ok) ok = hipEventCreateWithFlags(&f->fork, hipEventDisableTiming) == hipSuccess;
@@ -593,15 +599,32 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
     if (!fp) return COVT_ERR_DEVICE;
     struct Back { ForkCtx* f; ~Back() { fork_release(f); } } back{fp};
     ForkCtx& f = *fp;
-    const int64_t o1 = counts[0], o2 = o1 + counts[1], o3 = o2 + counts[2];
-    if (hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
-    for (int i = 0; i < 3; ++i)
+    int64_t off[COVT_NUM_FAMILIES];
+    off[0] = 0;
+    for (int k = 1; k < COVT_NUM_FAMILIES; ++k) off[k] = off[k - 1] + counts[k - 1];
+    // the families other than RLE go to the auxiliary streams (longest-running first); empty ones
+    // are not forked at all
+    const int aux_fam[kForkAux] = {COVT_FAMILY_SPLIT, COVT_FAMILY_FASTPFOR, COVT_FAMILY_VARINT, COVT_FAMILY_LANE};
+    bool any = false;
+    for (int i = 0; i < kForkAux; ++i) any |= counts[aux_fam[i]] > 0;
+    if (any && hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
+    int st = COVT_OK;
+    bool forked[kForkAux] = {false, false, false, false};
+    for (int i = 0; i < kForkAux && !st; ++i) {
+        const int fam = aux_fam[i];
+        if (counts[fam] <= 0) continue;
         if (hipStreamWaitEvent(f.aux[i], f.fork, 0) != hipSuccess) return COVT_ERR_DEVICE;
-    int st = covt_launch_family(COVT_FAMILY_FASTPFOR, d_in, d_desc + o2, counts[2], d_out, d_res + o2, f.aux[0]);
-    if (!st) st = covt_launch_family(COVT_FAMILY_VARINT, d_in, d_desc + o1, counts[1], d_out, d_res + o1, f.aux[1]);
-    if (!st) st = covt_launch_family(COVT_FAMILY_LANE, d_in, d_desc + o3, counts[3], d_out, d_res + o3, f.aux[2]);
+        forked[i] = true;
+        // split chunks: look-back records and the ticket counter live in the family's result entries
+        if (fam == COVT_FAMILY_SPLIT &&
+            hipMemsetAsync(d_res + off[fam], 0, (size_t)counts[fam] * sizeof(covt_stream_result), f.aux[i]) !=
+                hipSuccess)
+            st = COVT_ERR_DEVICE;
+        if (!st) st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], f.aux[i]);
+    }
     if (!st) st = covt_launch_family(COVT_FAMILY_RLE, d_in, d_desc, counts[0], d_out, d_res, s);
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < kForkAux; ++i) {
+        if (!forked[i]) continue;
         if (hipEventRecord(f.join[i], f.aux[i]) != hipSuccess) return COVT_ERR_DEVICE;
         if (hipStreamWaitEvent(s, f.join[i], 0) != hipSuccess) return COVT_ERR_DEVICE;
     }
@@ -663,7 +686,7 @@ struct HostShard {
     int64_t out_lo = 0, out_len = 0; // plan output bytes [out_lo, out_lo + out_len) <- d_out
     std::vector<covt_stream_desc> descs;  // launch order, offsets rebased
     std::vector<int64_t> stream;          // plan-order stream index of each descriptor
-    int64_t fam[COVT_NUM_FAMILIES] = {0, 0, 0, 0};
+    int64_t fam[COVT_NUM_FAMILIES] = {0, 0, 0, 0, 0};
     std::vector<covt_stream_result> res;
     hipStream_t s = nullptr;
     uint8_t *d_in = nullptr, *d_out = nullptr;
@@ -718,7 +741,8 @@ struct HostShard {
             chk(hipMemcpyAsync(host_out + out_lo, d_out, (size_t)out_len, hipMemcpyDeviceToHost, s));
         chk(hipStreamSynchronize(s));
         if (st == COVT_OK)
-            for (size_t k = 0; k < stream.size(); ++k) host_res[(size_t)stream[k]] = res[k];
+            for (size_t k = 0; k < stream.size(); ++k)
+                if (stream[k] >= 0) host_res[(size_t)stream[k]] = res[k];
         return st;
     }
 };
@@ -729,7 +753,8 @@ struct covt_plan {
     std::vector<uint64_t> tile_off, tile_size;
     std::vector<covt_stream_info> info;   // tile order
     std::vector<covt_stream_desc> descs;  // launch order: grouped by family, largest first
-    int64_t fam_counts[COVT_NUM_FAMILIES] = {0, 0, 0, 0};
+    std::vector<int64_t> desc_stream;     // plan-order stream of each descriptor
+    int64_t fam_counts[COVT_NUM_FAMILIES] = {0, 0, 0, 0, 0};
     int64_t out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
     int32_t format = COVT_FORMAT_GENC;
     std::vector<covt_geom_info> ginfo;   // geometry columns, tile order
@@ -1183,23 +1208,25 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         uint32_t i;
     };
     std::vector<Key> keys(ns);
+    const int64_t split_min = env_i64("COVT_SPLIT_MIN", COVT_SPLIT_MIN);
+    const int64_t split_chunk = std::max<int64_t>(64, env_i64("COVT_SPLIT_CHUNK", COVT_SPLIT_CHUNK));
     for (size_t i = 0; i < ns; ++i) {
         const auto& s = p->info[i];
         const bool lane = lane_stream(s.op, s.desc_index, s.byte_length);
-        const uint64_t fam = lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);
+        const bool split = split_stream(s.op, s.desc_index, s.byte_length, split_min);
+        const uint64_t fam = split ? (uint64_t)COVT_FAMILY_SPLIT
+                             : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);
         const uint64_t cost = std::min<uint64_t>((uint64_t)((int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4),
                                                  (1ull << 48) - 1);
         keys[i] = Key{(fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost), (uint32_t)i};
     }
     std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) { return a.k != b.k ? a.k < b.k : a.i < b.i; });
-    std::vector<int64_t> order(ns);
+    p->descs.reserve(ns);
+    p->desc_stream.reserve(ns);
     for (size_t k = 0; k < ns; ++k) {
-        order[k] = keys[k].i;
-        p->fam_counts[keys[k].k >> 60]++;
-    }
-    p->descs.resize(ns);
-    for (size_t k = 0; k < ns; ++k) {
-        covt_stream_info& si = p->info[(size_t)order[k]];
+        const size_t i = keys[k].i;
+        covt_stream_info& si = p->info[i];
+        const int fam = (int)(keys[k].k >> 60);
         covt_stream_desc d{};
         d.in_off = (uint64_t)si.in_off;
         d.out_off = (uint64_t)si.out_off;
@@ -1208,9 +1235,33 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         d.op = (uint8_t)si.op;
         d.num_bits = (uint8_t)si.num_bits;
         d.byte_length = si.byte_length;
-        d.flags = lane_stream(si.op, d.num_values, d.byte_length) ? COVT_DESC_LANE : 0;
-        p->descs[k] = d;
-        si.desc_index = (int32_t)k;
+        d.flags = fam == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
+        si.desc_index = (int32_t)p->descs.size();
+        if (fam != COVT_FAMILY_SPLIT) {
+            p->descs.push_back(d);
+            p->desc_stream.push_back((int64_t)i);
+            p->fam_counts[fam]++;
+            continue;
+        }
+        // chunk c: [c * split_chunk, min((c + 1) * split_chunk, byte_length)); COVT_SPLIT_SLOTS descriptors
+        const int64_t nch = ((int64_t)d.byte_length + split_chunk - 1) / split_chunk;
+        for (int64_t c = 0; c < nch; ++c) {
+            covt_stream_desc cd = d;
+            cd.flags = COVT_DESC_SPLIT;
+            cd.avail = (int32_t)c;
+            p->descs.push_back(cd);
+            for (int q = 1; q < COVT_SPLIT_SLOTS; ++q) {
+                covt_stream_desc pd{};
+                pd.flags = COVT_DESC_SPLIT_PAD;
+                if (q == 1) {
+                    pd.in_off = (uint64_t)(c * split_chunk);
+                    pd.out_off = (uint64_t)std::min<int64_t>((c + 1) * split_chunk, d.byte_length);
+                }
+                p->descs.push_back(pd);
+            }
+            for (int q = 0; q < COVT_SPLIT_SLOTS; ++q) p->desc_stream.push_back((int64_t)i);
+        }
+        p->fam_counts[COVT_FAMILY_SPLIT] += nch * COVT_SPLIT_SLOTS;
     }
     plan_geometry(p);
     plan_property_layout(p);
@@ -1233,6 +1284,12 @@ int covt_plan_streams(const covt_plan* p, covt_stream_info* out) {
     if (!p->info.empty()) std::memcpy(out, p->info.data(), p->info.size() * sizeof(covt_stream_info));
     return COVT_OK;
 }
+int64_t covt_plan_num_descs(const covt_plan* p) { return p ? (int64_t)p->descs.size() : 0; }
+int covt_plan_desc_streams(const covt_plan* p, int64_t* out) {
+    if (!p || (!out && !p->desc_stream.empty())) return COVT_ERR_INVALID_ARG;
+    if (!p->desc_stream.empty()) std::memcpy(out, p->desc_stream.data(), p->desc_stream.size() * sizeof(int64_t));
+    return COVT_OK;
+}
 int covt_plan_descs(const covt_plan* p, covt_stream_desc* out) {
     if (!p || (!out && !p->descs.empty())) return COVT_ERR_INVALID_ARG;
     if (!p->descs.empty()) std::memcpy(out, p->descs.data(), p->descs.size() * sizeof(covt_stream_desc));
@@ -1249,6 +1306,7 @@ int covt_decode_streams_device(const uint8_t* d_in, const covt_stream_desc* d_de
     if (n_streams < 0 || (n_streams && (!d_in || !d_desc || !d_res))) return COVT_ERR_INVALID_ARG;
     if ((uintptr_t)d_in & 15) return COVT_ERR_INVALID_ARG;
     for (int f = 0; f < COVT_NUM_FAMILIES; ++f) {  // any order: each family kernel skips the others
+        if (f == COVT_FAMILY_SPLIT) continue;       // split chunks need the grouped launch
         const int st = covt_launch_family(f, d_in, d_desc, n_streams, d_out, d_res, (hipStream_t)hip_stream);
         if (st) return st;
     }
@@ -1330,17 +1388,18 @@ void build_shards(const covt_plan* p, const std::vector<int32_t>& devs, std::vec
         if (h->out_lo == INT64_MAX) h->out_lo = h->out_len = 0;
         else h->out_len -= h->out_lo;
     }
-    std::vector<int64_t> stream_of_desc(p->descs.size());
-    for (size_t i = 0; i < p->info.size(); ++i) stream_of_desc[(size_t)p->info[i].desc_index] = (int64_t)i;
     for (size_t k = 0; k < p->descs.size(); ++k) {  // launch order restricted to each shard stays grouped
-        const int64_t i = stream_of_desc[k];
-        HostShard& h = *out[(size_t)shard_of_tile[(size_t)p->info[(size_t)i].tile]];
+        const int64_t i = p->desc_stream[k];
+        const covt_stream_info& si = p->info[(size_t)i];
+        HostShard& h = *out[(size_t)shard_of_tile[(size_t)si.tile]];
         covt_stream_desc d = p->descs[k];
-        d.in_off -= h.in_lo;
-        d.out_off -= (uint64_t)h.out_lo;
+        if (!(d.flags & COVT_DESC_SPLIT_PAD)) {  // pads carry stream-relative chunk ranges
+            d.in_off -= h.in_lo;
+            d.out_off -= (uint64_t)h.out_lo;
+        }
         h.fam[desc_family(d)]++;
+        h.stream.push_back(si.desc_index == (int32_t)k ? i : -1);  // only a stream's own entry is its result
         h.descs.push_back(d);
-        h.stream.push_back(i);
     }
     for (auto& h : out) h->res.resize(h->descs.size());
 }

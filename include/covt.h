@@ -133,10 +133,23 @@ enum covt_op {
 #define COVT_FAMILY_VARINT 1   /* varint / zigzag / delta / Morton ops */
 #define COVT_FAMILY_FASTPFOR 2 /* FastPFOR + VariableByte ops */
 #define COVT_FAMILY_LANE 3     /* small RLE streams (flag COVT_DESC_LANE): one lane per stream */
-#define COVT_NUM_FAMILIES 4
+#define COVT_FAMILY_SPLIT 4    /* long streams cut into chunks decoded by separate waves (COVT_DESC_SPLIT) */
+#define COVT_NUM_FAMILIES 5
 
 /* covt_stream_desc.flags */
 #define COVT_DESC_LANE 0x1u /* decoded by the lane-per-stream kernel (set by the plan for small streams) */
+/* Long streams (plan rule: Java-capped varint ops over more than COVT_SPLIT_MIN bytes) are cut into
+ * chunks of COVT_SPLIT_CHUNK bytes, each decoded by its own wave; a chunk's value index and running
+ * sums come from its predecessors by a decoupled look-back.  A chunk is COVT_SPLIT_SLOTS consecutive
+ * descriptors: the chunk descriptor (flags COVT_DESC_SPLIT, avail = chunk index, the other fields those
+ * of the stream) and pads (COVT_DESC_SPLIT_PAD; the first carries the chunk's stream-relative byte
+ * range [in_off, out_off)), whose result entries hold the look-back records.  The stream's result is
+ * written to its chunk 0's entry.  Split descriptors need the grouped launch. */
+#define COVT_DESC_SPLIT 0x2u
+#define COVT_DESC_SPLIT_PAD 0x4u
+#define COVT_SPLIT_SLOTS 6
+#define COVT_SPLIT_CHUNK 4096 /* default chunk bytes (env COVT_SPLIT_CHUNK at plan creation) */
+#define COVT_SPLIT_MIN 8192   /* default: streams longer than this are split (env COVT_SPLIT_MIN; -1: never) */
 
 /* One device-resident plan entry (32 bytes). */
 typedef struct covt_stream_desc {
@@ -176,7 +189,11 @@ int64_t covt_plan_output_bytes(const covt_plan* plan);
 /* stream-byte, output-byte and vertex totals over all planned streams */
 int covt_plan_totals(const covt_plan* plan, int64_t* in_bytes, int64_t* out_bytes, int64_t* vertices);
 int covt_plan_streams(const covt_plan* plan, covt_stream_info* out);    /* num_streams records */
-int covt_plan_descs(const covt_plan* plan, covt_stream_desc* out);      /* num_streams, launch order */
+int64_t covt_plan_num_descs(const covt_plan* plan);  /* descriptors (>= streams: split chunks and pads) */
+int covt_plan_descs(const covt_plan* plan, covt_stream_desc* out);      /* num_descs, launch order */
+/* plan-order stream index of every descriptor (launch order); a stream's result is at its
+ * covt_stream_info.desc_index */
+int covt_plan_desc_streams(const covt_plan* plan, int64_t* out);
 /* Launch order groups descriptors by family (RLE, varint, FastPFOR, lane; largest stream first inside
  * a family, the lane family also by op): counts[f] = descriptors of family f. */
 int covt_plan_family_counts(const covt_plan* plan, int64_t counts[COVT_NUM_FAMILIES]);
@@ -184,12 +201,14 @@ int covt_plan_tile_status(const covt_plan* plan, int32_t* out);         /* n_til
 
 /* Launch the decode of n_streams descriptors on `hip_stream` (a hipStream_t; NULL = default).
  * d_in: batch bytes on the device (see COVT_INPUT_PADDING); d_desc: descriptors on the device;
- * d_out: output buffer of covt_plan_output_bytes bytes; d_res: n_streams results.  Asynchronous. */
+ * d_out: output buffer of covt_plan_output_bytes bytes; d_res: n_streams results.  Asynchronous.
+ * Split descriptors (COVT_DESC_SPLIT / _PAD) are skipped here: they need the grouped launch. */
 int covt_decode_streams_device(const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
                                uint8_t* d_out, covt_stream_result* d_res, void* hip_stream);
 
 /* Same, for descriptors grouped by family (as covt_plan_descs returns them): the family kernels run
- * concurrently on forked streams joined back into `hip_stream`. */
+ * concurrently on forked streams joined back into `hip_stream`.  d_res holds one entry per
+ * descriptor (covt_plan_num_descs); results are at the streams' desc_index entries. */
 int covt_decode_streams_device_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc,
                                        const int64_t family_counts[COVT_NUM_FAMILIES], uint8_t* d_out,
                                        covt_stream_result* d_res, void* hip_stream);

@@ -72,8 +72,8 @@ def test_config_selections_match_survey():
         assert (len(picks), int(m.sum()), int(st["byte_length"].sum()),
                 int((st["out_elems"] * st["elem_bytes"]).sum())) == (nt, ns, ib, ob), name
         descs, counts, idx = plan.subset_descs(m)
-        assert counts.sum() == ns and descs.size == 32 * ns
-        assert sorted(idx.tolist()) == sorted(map(int, m.nonzero()[0]))
+        assert counts.sum() == descs.size // 32 == idx.size  # split chunks + pads included
+        assert sorted(idx[idx >= 0].tolist()) == sorted(map(int, m.nonzero()[0]))
 
 
 def test_cpu_baseline_leg_uses_host_cpus():

@@ -55,9 +55,10 @@ def test_plan_matches_oracle_walk(covt, oracle, fmt_mode):
     plan = covt.Plan.from_tiles(tiles, fmt, id_mode)
     st = plan.streams
     assert plan.num_streams == len(st)
-    # descriptor table is a permutation of the streams, largest first
+    # every stream owns one descriptor (its result entry); split streams add chunks + pads
     di = np.sort(st["desc_index"])
-    assert np.array_equal(di, np.arange(plan.num_streams))
+    assert np.unique(di).size == plan.num_streams and di.max() < plan.num_descs
+    assert np.array_equal(plan.desc_streams[st["desc_index"]], np.arange(plan.num_streams))
     descs = plan.descs.view(np.uint8).reshape(-1, 32)
     for t, p in enumerate(paths):
         ost, oss = oracle.walk_tile(tiles[t])

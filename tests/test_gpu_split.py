@@ -1,0 +1,167 @@
+"""GPU parity of the split-stream path (COVT_FAMILY_SPLIT, include/covt.h): long Java-capped varint
+streams decoded by one wave per chunk with a decoupled look-back must equal the one-wave decode and
+the oracle (DecodingUtils.java:35-112, :394-409) bit for bit -- values, running sums across chunk
+edges, x/y parity, the consumed position, and the errors of short streams.
+
+* every stream of every fixture tile with splitting forced at small chunk sizes, both Id modes;
+* adversarial byte strings (long runs of continuation bytes, so values capped at 4 bytes end on a
+  byte with bit 7 set, also right at chunk edges), exact / short (trailing bytes) / over-long
+  (truncated) value counts, every split op, chunk sizes from 16 bytes to 4 KiB.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import tile_key, tile_paths
+
+pytestmark = pytest.mark.gpu
+
+DESC = np.dtype([("in_off", np.uint64), ("out_off", np.uint64), ("avail", np.int32), ("num_values", np.int32),
+                 ("op", np.uint8), ("num_bits", np.uint8), ("flags", np.uint16), ("byte_length", np.int32)])
+
+
+@pytest.mark.parametrize("chunk", [100, 1024])
+@pytest.mark.parametrize("id_mode", [0, 1], ids=["id_format", "id_java"])
+def test_fixtures_forced_split(covt, gpu_available, golden_streams, monkeypatch, chunk, id_mode):
+    import torch
+
+    monkeypatch.setenv("COVT_SPLIT_MIN", "200")
+    monkeypatch.setenv("COVT_SPLIT_CHUNK", str(chunk))
+    paths = tile_paths()
+    keys = [tile_key(p) for p in paths]
+    tiles = [open(p, "rb").read() for p in paths]
+    plan = covt.Plan.from_tiles(tiles, covt.FORMAT_GENC, id_mode)
+    assert plan.family_counts[covt.FAMILY_SPLIT] > 1000
+    db = covt.DeviceBatch(plan, "cuda")
+    for _ in range(2):  # the look-back records are reset per launch
+        db.decode()
+    torch.cuda.synchronize()
+    out, res = db.results()
+    col = golden_streams["columns"]
+    pre = "fmt_" if id_mode == 0 else "java_"
+    ish, ist, ico = col.index(pre + "sha256"), col.index(pre + "status"), col.index(pre + "consumed")
+    st = plan.streams
+    fam0 = int(plan.family_counts[:covt.FAMILY_SPLIT].sum())
+    n_split = 0
+    for t, key in enumerate(keys):
+        rec = golden_streams["tiles"][key]
+        if rec["walk_status"] != 0:
+            continue
+        idx = np.nonzero(st["tile"] == t)[0]
+        for i, row in zip(idx, rec["streams"]):
+            n_split += int(st["desc_index"][i] >= fam0)
+            assert (int(res[i][0]) == 0) == (row[ist] == 0), (key, int(i))
+            if row[ist] != 0:
+                continue
+            assert int(res[i][1]) == row[ico], (key, int(i))
+            assert hashlib.sha256(plan.stream_array(out, int(i)).tobytes()).hexdigest() == row[ish], (key, int(i))
+    assert n_split > 300
+
+
+def _j4_count(b: bytes) -> int:
+    """Values Java's 4-byte-capped decodeVarint reads from the whole buffer (DecodingUtils.java:157-186)."""
+    p = n = 0
+    while p < len(b):
+        k = 0
+        while k < 3 and p + k < len(b) and b[p + k] & 0x80:
+            k += 1
+        if p + k >= len(b):
+            break  # a value cut off by the end
+        p += k + 1
+        n += 1
+    return n
+
+
+def _split_launch(covt, buf: bytes, op: int, n: int, nb: int, chunk: int, out_bytes: int):
+    import ctypes as C
+
+    import torch
+
+    bl = len(buf)
+    nch = (bl + chunk - 1) // chunk
+    d = np.zeros(nch * covt.SPLIT_SLOTS, dtype=DESC)
+    for c in range(nch):
+        k = c * covt.SPLIT_SLOTS
+        d[k] = (0, 0, c, n, op, nb, covt.DESC_SPLIT, bl)
+        d[k + 1 : k + covt.SPLIT_SLOTS]["flags"] = covt.DESC_SPLIT_PAD
+        d[k + 1]["in_off"], d[k + 1]["out_off"] = c * chunk, min((c + 1) * chunk, bl)
+    counts = np.zeros(covt.NUM_FAMILIES, dtype=np.int64)
+    counts[covt.FAMILY_SPLIT] = d.size
+    dev = torch.device("cuda")
+    d_in = torch.zeros(bl + covt.INPUT_PADDING + 16, dtype=torch.uint8, device=dev)
+    d_in[:bl] = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(dev) if bl else d_in[:0]
+    d_desc = torch.from_numpy(d.view(np.uint8)).to(dev)
+    d_out = torch.full((out_bytes + 16,), 0x5A, dtype=torch.uint8, device=dev)
+    d_res = torch.full((d.size * 2,), 0x33, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream()
+    st = covt.lib().covt_decode_streams_device_grouped(d_in.data_ptr(), d_desc.data_ptr(),
+                                                       counts.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                       d_out.data_ptr(), d_res.data_ptr(), s.cuda_stream)
+    assert st == 0
+    torch.cuda.synchronize()
+    return d_out.cpu().numpy()[:out_bytes], d_res.cpu().numpy().reshape(-1, 2)[0]
+
+
+def _oracle(oracle, covt, op, buf, n, nb):
+    O = oracle
+    if op in (covt.OP_VARINT_I32, covt.OP_VARINT_I32_AS_I64):
+        st, arr, pos = O.decode_varint(buf, 0, n)[:3]
+    elif op in (covt.OP_VARINT_ZZ_I32, covt.OP_VARINT_ZZ_I32_AS_I64):
+        st, arr, pos = O.decode_zigzag_varint(buf, 0, n)[:3]
+    elif op in (covt.OP_VARINT_ZZ_DELTA_I32, covt.OP_VARINT_ZZ_DELTA_I64):
+        st, arr, pos = O.decode_zigzag_delta_varint(buf, 0, n)[:3]
+    elif op == covt.OP_VARINT_ZZ_DELTA_XY:
+        st, arr, pos = O.decode_zigzag_delta_varint_coordinates(buf, 0, n)[:3]
+    else:
+        st, arr, pos = O.decode_delta_varint_morton_codes(buf, 0, n, nb)[:3]
+    if op in (covt.OP_VARINT_I32_AS_I64, covt.OP_VARINT_ZZ_I32_AS_I64, covt.OP_VARINT_ZZ_DELTA_I64):
+        arr = np.asarray(arr, dtype=np.int32).astype(np.int64)
+    return st, np.asarray(arr), pos
+
+
+def _streams(rng, oracle):
+    """(name, bytes) adversarial and plain varint byte strings."""
+    out = []
+    vals = rng.integers(0, 1 << 28, size=9000, dtype=np.uint64) >> rng.integers(0, 28, size=9000).astype(np.uint64)
+    out.append(("plain", oracle.encode_varints(vals)))
+    for p_cont in (0.5, 0.8, 0.97):  # runs of continuation bytes: values capped at 4 bytes
+        b = rng.random(20000) < p_cont
+        raw = rng.integers(0, 128, size=b.size).astype(np.uint8) | (b.astype(np.uint8) << 7)
+        out.append(("rand%.2f" % p_cont, raw.tobytes()))
+    out.append(("all_cont", b"\x80" * 9001))  # every value is four continuation bytes
+    z = bytearray(oracle.encode_varints(rng.integers(0, 200, size=3000, dtype=np.uint64)))
+    for k in range(0, len(z) - 8, 97):  # capped values sprinkled in
+        z[k:k + 4] = b"\xff\x81\x80\x80"
+    out.append(("sprinkled", bytes(z)))
+    return out
+
+
+@pytest.mark.parametrize("chunk", [16, 64, 100, 1000, 4096])
+def test_adversarial_streams_split(covt, oracle, gpu_available, chunk):
+    rng = np.random.default_rng(chunk)
+    ops = [covt.OP_VARINT_I32, covt.OP_VARINT_ZZ_I32, covt.OP_VARINT_ZZ_DELTA_I32, covt.OP_VARINT_ZZ_DELTA_XY,
+           covt.OP_VARINT_DELTA_MORTON, covt.OP_VARINT_I32_AS_I64, covt.OP_VARINT_ZZ_I32_AS_I64,
+           covt.OP_VARINT_ZZ_DELTA_I64]
+    n_checked = 0
+    for name, buf in _streams(rng, oracle):
+        total = _j4_count(buf)
+        for op in ops:
+            nb = 14 if op == covt.OP_VARINT_DELTA_MORTON else 0
+            for n in (total, total - 37, total + 1, 1):
+                if n <= 0:
+                    continue
+                if op == covt.OP_VARINT_ZZ_DELTA_XY and n & 1:
+                    n -= 1  # the plan never splits odd x,y streams
+                nvals = n  # varints to read (Morton: one per vertex)
+                ebytes = (8 if op in (covt.OP_VARINT_I32_AS_I64, covt.OP_VARINT_ZZ_I32_AS_I64,
+                                      covt.OP_VARINT_ZZ_DELTA_I64) else 4) * (2 * nvals if nb else nvals)
+                o_st, o_arr, o_pos = _oracle(oracle, covt, op, buf, nvals, nb)
+                out, r = _split_launch(covt, buf, op, nvals, nb, chunk, ebytes)
+                assert (int(r[0]) == 0) == (o_st == 0), (name, op, n, int(r[0]), o_st)
+                if o_st == 0:
+                    assert int(r[1]) == o_pos, (name, op, n)
+                    got = out.view(np.int64 if ebytes == 8 * (2 * nvals if nb else nvals) else np.int32)
+                    assert np.array_equal(got, o_arr.astype(got.dtype)), (name, op, n)
+                n_checked += 1
+    assert n_checked > 150

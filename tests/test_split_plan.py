@@ -1,0 +1,65 @@
+"""Split-stream plan layout (CPU): long Java-capped varint streams become chunks of COVT_SPLIT_SLOTS
+descriptors (include/covt.h), contiguous byte ranges covering the stream, family counts and the
+descriptor -> stream map consistent; the env knobs COVT_SPLIT_MIN / COVT_SPLIT_CHUNK are read at plan
+creation."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+DESC = np.dtype([("in_off", np.uint64), ("out_off", np.uint64), ("avail", np.int32), ("num_values", np.int32),
+                 ("op", np.uint8), ("num_bits", np.uint8), ("flags", np.uint16), ("byte_length", np.int32)])
+
+
+def _tile(name="5_16_20"):
+    return open(os.path.join(ROOT, "tests", "golden", "tiles", "omt", name + ".covt"), "rb").read()
+
+
+@pytest.mark.parametrize("chunk", [64, 1000, 4096])
+def test_split_layout(covt, monkeypatch, chunk):
+    monkeypatch.setenv("COVT_SPLIT_MIN", "256")
+    monkeypatch.setenv("COVT_SPLIT_CHUNK", str(chunk))
+    plan = covt.Plan.from_tiles([_tile(), _tile("14_8298_10748")])
+    d = plan.descs.view(DESC)
+    assert d.size == plan.num_descs == plan.family_counts.sum()
+    fam0 = int(plan.family_counts[:covt.FAMILY_SPLIT].sum())
+    sp = d[fam0:]
+    assert sp.size % covt.SPLIT_SLOTS == 0 and sp.size > 0
+    st = plan.streams
+    split_streams = set()
+    for k in range(0, sp.size, covt.SPLIT_SLOTS):
+        cd, rg = sp[k], sp[k + 1]
+        assert cd["flags"] == covt.DESC_SPLIT
+        assert all(sp[k + q]["flags"] == covt.DESC_SPLIT_PAD for q in range(1, covt.SPLIT_SLOTS))
+        i = int(plan.desc_streams[fam0 + k])
+        assert all(plan.desc_streams[fam0 + k + q] == i for q in range(covt.SPLIT_SLOTS))
+        c = int(cd["avail"])
+        assert (int(rg["in_off"]), int(rg["out_off"])) == (c * chunk, min((c + 1) * chunk, int(st["byte_length"][i])))
+        if c == 0:
+            assert st["desc_index"][i] == fam0 + k  # the stream's result entry = its chunk 0
+            split_streams.add(i)
+        else:
+            assert int(sp[k - covt.SPLIT_SLOTS]["avail"]) == c - 1 and plan.desc_streams[fam0 + k - 1] == i
+    for i in split_streams:
+        assert st["byte_length"][i] > 256 and st["op"][i] in (covt.OP_VARINT_ZZ_DELTA_I32, covt.OP_VARINT_ZZ_DELTA_XY,
+                                                              covt.OP_VARINT_DELTA_MORTON, covt.OP_VARINT_I32)
+    # every stream has exactly one result entry, and non-split descriptors map 1:1
+    assert len(set(st["desc_index"].tolist())) == plan.num_streams
+    assert np.array_equal(plan.desc_streams[st["desc_index"]], np.arange(plan.num_streams))
+
+
+def test_split_disabled_and_subset(covt, monkeypatch):
+    monkeypatch.setenv("COVT_SPLIT_MIN", "-1")
+    plan = covt.Plan.from_tiles([_tile()])
+    assert plan.family_counts[covt.FAMILY_SPLIT] == 0 and plan.num_descs == plan.num_streams
+    monkeypatch.setenv("COVT_SPLIT_MIN", "256")
+    monkeypatch.setenv("COVT_SPLIT_CHUNK", "512")
+    plan = covt.Plan.from_tiles([_tile()])
+    assert plan.family_counts[covt.FAMILY_SPLIT] > 0
+    mask = plan.streams["stream_type"] == covt.VERTEX_BUFFER
+    descs, counts, prim = plan.subset_descs(mask)
+    assert counts.sum() == descs.size // 32 == prim.size
+    assert (prim >= 0).sum() == mask.sum() and set(prim[prim >= 0].tolist()) == set(np.nonzero(mask)[0].tolist())
+    assert counts[covt.FAMILY_SPLIT] % covt.SPLIT_SLOTS == 0
