@@ -39,7 +39,7 @@ FORMAT_GENC, FORMAT_GEND = 0, 1
 FAMILY_RLE, FAMILY_VARINT, FAMILY_FASTPFOR, FAMILY_LANE, FAMILY_SPLIT = 0, 1, 2, 3, 4
 NUM_FAMILIES = 5
 DESC_LANE, DESC_SPLIT, DESC_SPLIT_PAD = 0x1, 0x2, 0x4
-SPLIT_SLOTS = 6
+SPLIT_SLOTS = 8
 ID_FORMAT, ID_JAVA = 0, 1
 
 (OP_NONE, OP_BYTE_RLE_U8, OP_RLE_U64, OP_RLE_I32, OP_RLE_S64, OP_VARINT_I32, OP_VARINT_ZZ_I32,

@@ -1534,23 +1534,36 @@ __device__ __forceinline__ Agg agg_cat(const Agg& a, const Agg& b, bool xy) {
     const bool sw = xy && (a.cnt & 1);
     return Agg{a.cnt + b.cnt, a.sx + (sw ? b.sy : b.sx), a.sy + (sw ? b.sx : b.sy)};
 }
-// record = 4 dwords {flag, cnt, sx, sy}: values first, then the flag with release semantics
-__device__ __forceinline__ void rec_publish(uint32_t* r, const Agg& a, uint32_t flag) {
+// A record is three 8-byte granules {tag, value} (cnt, sx, sy), each written by one relaxed
+// agent-scope store (a write-through `sc1` store): the data is its own flag, so neither a release
+// fence (an XCD L2 write-back) nor an acquire (an L1/L2 invalidation, which would cost every wave on
+// the CU its cached windows) is needed -- a reader polls the granules with relaxed agent-scope
+// (`sc1`) loads until all three carry the tag (cdna_hip_programming.md, publish/consume recipe R2).
+// The launch zeroes every record beforehand (hipMemsetAsync in launch_grouped).
+typedef __attribute__((address_space(1))) uint64_t g_u64;
+__device__ __forceinline__ void rec_publish(covt_stream_result* rec, const Agg& a, uint32_t tag) {
     if (lane_id() == 0) {
-        __hip_atomic_store(r + 1, (uint32_t)a.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(r + 2, a.sx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(r + 3, a.sy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(r, flag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        g_u64* g = (g_u64*)rec;
+        const uint64_t t = (uint64_t)tag << 32;
+        __hip_atomic_store(g, t | (uint32_t)a.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g + 1, t | a.sx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g + 2, t | a.sy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-__device__ __forceinline__ Agg rec_read(uint32_t* r) {
-    Agg a;
-    a.cnt = (int32_t)uniu(__hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    a.sx = uniu(__hip_atomic_load(r + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    a.sy = uniu(__hip_atomic_load(r + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    return a;
+// the record if all three granules carry the tag
+__device__ __forceinline__ bool rec_try(covt_stream_result* rec, uint32_t tag, Agg& a) {
+    g_u64* g = (g_u64*)rec;
+    const uint64_t x0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t x1 = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t x2 = __hip_atomic_load(g + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool ok = (uint32_t)(x0 >> 32) == tag && (uint32_t)(x1 >> 32) == tag && (uint32_t)(x2 >> 32) == tag;
+    a = Agg{(int32_t)(uint32_t)x0, (uint32_t)x1, (uint32_t)x2};
+    return uniu(ok ? 1u : 0u) != 0u;
 }
-constexpr int kRecAgg = 2, kRecIncl = 6;  // dword offsets of the records in a chunk's result entries
+// result entries of a chunk: 0 = the stream's result (chunk 0), 1-3 aggregate, 4-6 inclusive prefix,
+// 7 = the family's ticket counter (first chunk of the launch)
+constexpr int kRecAgg = 1, kRecIncl = 4, kRecTicket = 7;
+static_assert(kSplitSlots == 8, "split record layout");
 constexpr uint32_t kSpinLimit = 1u << 22;  // ~0.5 s of polling: a predecessor that never publishes
 // values and sums before chunk `chunk` (ticket t) of a stream: its predecessors are tickets t-chunk..t-1
 __device__ Agg lookback(covt_stream_result* res, int64_t t, int32_t chunk, bool xy, int32_t& err) {
@@ -1558,13 +1571,14 @@ __device__ Agg lookback(covt_stream_result* res, int64_t t, int32_t chunk, bool 
     int64_t k = t - 1;
     uint32_t spins = 0;
     for (int32_t left = chunk; left > 0;) {
-        uint32_t* r = (uint32_t*)(res + kSplitSlots * k);
-        if (uniu(__hip_atomic_load(r + kRecIncl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 2u) {
-            acc = agg_cat(rec_read(r + kRecIncl), acc, xy);
+        covt_stream_result* r = res + kSplitSlots * k;
+        Agg a;
+        if (rec_try(r + kRecIncl, 2u, a)) {
+            acc = agg_cat(a, acc, xy);
             break;
         }
-        if (uniu(__hip_atomic_load(r + kRecAgg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 1u) {
-            acc = agg_cat(rec_read(r + kRecAgg), acc, xy);
+        if (rec_try(r + kRecAgg, 1u, a)) {
+            acc = agg_cat(a, acc, xy);
             --k;
             --left;
             continue;
@@ -1636,7 +1650,7 @@ __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, co
         mine.sy = kXY ? lane_bcast(incl_scan(ay), 63) : 0u;
     }
     // (3) + (4) publish, look back, publish the inclusive prefix
-    uint32_t* rec = (uint32_t*)(res + kSplitSlots * t);
+    covt_stream_result* rec = res + kSplitSlots * t;
     Agg excl{0, 0u, 0u};
     if (chunk == 0) {
         rec_publish(rec + kRecIncl, mine, 2u);
@@ -1678,7 +1692,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const
                                                                            covt_stream_result* __restrict__ res) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kFamSmemVarint];
     const int wv = uni((int)(threadIdx.x >> 6));
-    uint32_t* ctr = (uint32_t*)(res + 5);  // chunk 0's sixth entry
+    uint32_t* ctr = (uint32_t*)(res + kRecTicket);  // the first chunk's ticket entry
     uint32_t tk = 0;
     if (lane_id() == 0) tk = atomicAdd(ctr, 1u);
     const int64_t t = (int64_t)lane_bcast(tk, 0);

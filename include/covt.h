@@ -147,7 +147,7 @@ enum covt_op {
  * written to its chunk 0's entry.  Split descriptors need the grouped launch. */
 #define COVT_DESC_SPLIT 0x2u
 #define COVT_DESC_SPLIT_PAD 0x4u
-#define COVT_SPLIT_SLOTS 6
+#define COVT_SPLIT_SLOTS 8
 #define COVT_SPLIT_CHUNK 4096 /* default chunk bytes (env COVT_SPLIT_CHUNK at plan creation) */
 #define COVT_SPLIT_MIN 8192   /* default: streams longer than this are split (env COVT_SPLIT_MIN; -1: never) */
 

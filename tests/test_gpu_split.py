@@ -149,10 +149,10 @@ def test_adversarial_streams_split(covt, oracle, gpu_available, chunk):
         for op in ops:
             nb = 14 if op == covt.OP_VARINT_DELTA_MORTON else 0
             for n in (total, total - 37, total + 1, 1):
-                if n <= 0:
-                    continue
                 if op == covt.OP_VARINT_ZZ_DELTA_XY and n & 1:
                     n -= 1  # the plan never splits odd x,y streams
+                if n <= 0:
+                    continue  # nor empty ones
                 nvals = n  # varints to read (Morton: one per vertex)
                 ebytes = (8 if op in (covt.OP_VARINT_I32_AS_I64, covt.OP_VARINT_ZZ_I32_AS_I64,
                                       covt.OP_VARINT_ZZ_DELTA_I64) else 4) * (2 * nvals if nb else nvals)
