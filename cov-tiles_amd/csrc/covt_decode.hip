@@ -1417,99 +1417,6 @@ __device__ void run_fastpfor(Ctx& c) {
     c.consumed = c.byte_length;
 }
 
-__host__ __device__ constexpr int op_family(int op) {
-    return (op >= COVT_OP_FPF_ZZ_DELTA_I32 && op <= COVT_OP_FPF_DELTA_MORTON) ? COVT_FAMILY_FASTPFOR
-           : ((op >= COVT_OP_VARINT_I32 && op <= COVT_OP_VARINT_DELTA_MORTON) ||
-              (op >= COVT_OP_VARINT_U64 && op <= COVT_OP_VARINT_ZZ_DELTA_I64) ||
-              (op >= COVT_OP_VARINT_ZZ_I32_AS_I64 && op <= COVT_OP_VARINT_ZZ_DELTA_S64))
-               ? COVT_FAMILY_VARINT
-               : COVT_FAMILY_RLE;  // RLE ops and COVT_OP_NONE / unknown ops (reported as unsupported)
-}
-
-// One wave per descriptor; waves whose descriptor belongs to another family return at once (used
-// when the caller's descriptors are not grouped by family).
-template <int FAM>
-__global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(const uint8_t* __restrict__ in,
-                                                            const covt_stream_desc* __restrict__ descs,
-                                                            int64_t n_streams, uint8_t* __restrict__ out,
-                                                            covt_stream_result* __restrict__ res) {
-    constexpr int kStride = FAM == COVT_FAMILY_RLE ? kFamSmemRle
-                            : FAM == COVT_FAMILY_VARINT ? kFamSmemVarint : kFamSmemFpf;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kStride];
-    const int wv = uni((int)(threadIdx.x >> 6));
-    const int64_t sid = (int64_t)blockIdx.x * kWavesPerBlock + wv;
-    if (sid >= n_streams) return;
-    const covt_stream_desc d = descs[sid];
-    if ((d.flags & (COVT_DESC_LANE | COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD)) || op_family(d.op) != FAM) return;
-    // long streams are the kernel's critical path: let their waves win instruction arbitration
-    if (d.byte_length > kLongStream || d.num_values > kLongStream) __builtin_amdgcn_s_setprio(2);
-#ifdef COVT_TIMING  // profiling build (libcovt_timing.so): result = (duration, start) in 100 MHz ticks
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
-    Ctx c;
-    c.sm = (WaveSmem*)(smem + wv * kStride);
-    c.sb = in + d.in_off;
-    c.out = out + d.out_off;
-    c.avail = d.avail;
-    c.n = d.num_values;
-    c.nb = d.num_bits;
-    c.op = d.op;
-    c.byte_length = d.byte_length;
-    c.err = 0;
-    c.consumed = 0;
-#ifdef COVT_TIMING
-    c.ph_last = __builtin_amdgcn_s_memtime();
-    for (int k = 0; k < kPhases; ++k) c.ph[k] = 0;
-#endif
-    if (c.n < 0 || c.avail < 0 || c.byte_length < 0) {
-        c.err = COVT_ERR_INVALID_ARG;
-    } else if (FAM == COVT_FAMILY_RLE) {
-        if (c.op == COVT_OP_BYTE_RLE_U8 || c.op == COVT_OP_BYTE_RLE_RAW) { if (c.n > 0) run_rle_byte(c); }
-        else if (c.op == COVT_OP_RLE_U64 || c.op == COVT_OP_RLE_I32 || c.op == COVT_OP_RLE_S64) { if (c.n > 0) run_rle_int(c); }
-        else c.err = COVT_ERR_UNSUPPORTED_ENCODING;
-#if defined(COVT_ABL_ONEOP)  // ablation build (instruction-cache footprint): one code path per family
-    } else if (FAM == COVT_FAMILY_VARINT) {
-        if (c.op == COVT_OP_VARINT_U64) run_varint_stream<COVT_OP_VARINT_U64>(c);
-        else run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I32>(c);
-    } else if (true) {
-        run_fastpfor<COVT_OP_FPF_ZZ_DELTA_I32>(c);
-#endif
-    } else if (FAM == COVT_FAMILY_VARINT) {
-        switch (c.op) {  // one uniform switch per stream; the loops are specialised per op
-        case COVT_OP_VARINT_I32: run_varint_stream<COVT_OP_VARINT_I32>(c); break;
-        case COVT_OP_VARINT_ZZ_I32: run_varint_stream<COVT_OP_VARINT_ZZ_I32>(c); break;
-        case COVT_OP_VARINT_ZZ_DELTA_I32: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I32>(c); break;
-        case COVT_OP_VARINT_ZZ_DELTA_XY: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_XY>(c); break;
-        case COVT_OP_VARINT_DELTA_MORTON: run_varint_stream<COVT_OP_VARINT_DELTA_MORTON>(c); break;
-        case COVT_OP_VARINT_U64: run_varint_stream<COVT_OP_VARINT_U64>(c); break;
-        case COVT_OP_VARINT_I32_AS_I64: run_varint_stream<COVT_OP_VARINT_I32_AS_I64>(c); break;
-        case COVT_OP_VARINT_ZZ_I32_AS_I64: run_varint_stream<COVT_OP_VARINT_ZZ_I32_AS_I64>(c); break;
-        case COVT_OP_VARINT_ZZ_S64: run_varint_stream<COVT_OP_VARINT_ZZ_S64>(c); break;
-        case COVT_OP_VARINT_ZZ_DELTA_S64: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_S64>(c); break;
-        default: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I64>(c); break;
-        }
-    } else {
-        switch (c.op) {
-        case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_I32>(c); break;
-        case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_XY>(c); break;
-        default: run_fastpfor<COVT_OP_FPF_DELTA_MORTON>(c); break;
-        }
-    }
-    if (lane_id() == 0) {
-        covt_stream_result r;
-        r.status = c.err;
-        r.consumed = c.consumed;
-#ifdef COVT_TIMING
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        r.status = c.err ? -1 : (int32_t)(t_end - t_start);
-        r.consumed = (int32_t)(uint32_t)t_start;
-        if (covt_phase_buf)
-            for (int k = 0; k < kPhases; ++k) covt_phase_buf[(descs + sid - covt_phase_desc0) * kPhases + k] = c.ph[k];
-#endif
-        res[sid] = r;
-    }
-}
-
 // --------------------------------------------------------------------------------------------
 // long streams split into chunks (COVT_FAMILY_SPLIT; plan rule and layout in include/covt.h)
 // --------------------------------------------------------------------------------------------
@@ -1685,13 +1592,11 @@ __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, co
     }
 }
 
-// One wave per chunk, chunks in ticket order (tickets from a counter in the family's result entries).
-__global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const uint8_t* __restrict__ in,
-                                                                           const covt_stream_desc* __restrict__ descs,
-                                                                           int64_t n_chunks, uint8_t* __restrict__ out,
-                                                                           covt_stream_result* __restrict__ res) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kFamSmemVarint];
-    const int wv = uni((int)(threadIdx.x >> 6));
+// One split chunk per wave, chunks in ticket order (tickets from a counter in the split region's
+// result entries); runs inside the varint family kernel (its first workgroups), so the split chunks
+// share that kernel's launch and hardware queue.
+__device__ void decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in, const covt_stream_desc* __restrict__ descs,
+                                   int64_t n_chunks, uint8_t* __restrict__ out, covt_stream_result* __restrict__ res) {
     uint32_t* ctr = (uint32_t*)(res + kRecTicket);  // the first chunk's ticket entry
     uint32_t tk = 0;
     if (lane_id() == 0) tk = atomicAdd(ctr, 1u);
@@ -1700,7 +1605,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const
     const covt_stream_desc d = descs[kSplitSlots * t];
     const covt_stream_desc rg = descs[kSplitSlots * t + 1];  // the chunk's byte range
     Ctx c;
-    c.sm = (WaveSmem*)(smem + wv * kFamSmemVarint);
+    c.sm = sm;
     c.sb = in + d.in_off;
     c.out = out + d.out_off;
     c.avail = d.byte_length;
@@ -1720,6 +1625,112 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const
     case COVT_OP_VARINT_I32_AS_I64: run_varint_chunk<COVT_OP_VARINT_I32_AS_I64>(c, s, e, chunk, res, t); break;
     case COVT_OP_VARINT_ZZ_I32_AS_I64: run_varint_chunk<COVT_OP_VARINT_ZZ_I32_AS_I64>(c, s, e, chunk, res, t); break;
     default: run_varint_chunk<COVT_OP_VARINT_ZZ_DELTA_I64>(c, s, e, chunk, res, t); break;
+    }
+}
+
+__host__ __device__ constexpr int op_family(int op) {
+    return (op >= COVT_OP_FPF_ZZ_DELTA_I32 && op <= COVT_OP_FPF_DELTA_MORTON) ? COVT_FAMILY_FASTPFOR
+           : ((op >= COVT_OP_VARINT_I32 && op <= COVT_OP_VARINT_DELTA_MORTON) ||
+              (op >= COVT_OP_VARINT_U64 && op <= COVT_OP_VARINT_ZZ_DELTA_I64) ||
+              (op >= COVT_OP_VARINT_ZZ_I32_AS_I64 && op <= COVT_OP_VARINT_ZZ_DELTA_S64))
+               ? COVT_FAMILY_VARINT
+               : COVT_FAMILY_RLE;  // RLE ops and COVT_OP_NONE / unknown ops (reported as unsupported)
+}
+
+// One wave per descriptor; waves whose descriptor belongs to another family return at once (used
+// when the caller's descriptors are not grouped by family).
+// The varint family's launch also carries the split chunks (COVT_FAMILY_SPLIT): its first
+// split_blocks workgroups decode chunks, the rest decode whole varint streams.
+template <int FAM>
+__global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(const uint8_t* __restrict__ in,
+                                                            const covt_stream_desc* __restrict__ descs,
+                                                            int64_t n_streams, uint8_t* __restrict__ out,
+                                                            covt_stream_result* __restrict__ res,
+                                                            const covt_stream_desc* __restrict__ split_descs,
+                                                            int64_t n_chunks, covt_stream_result* __restrict__ split_res) {
+    constexpr int kStride = FAM == COVT_FAMILY_RLE ? kFamSmemRle
+                            : FAM == COVT_FAMILY_VARINT ? kFamSmemVarint : kFamSmemFpf;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kStride];
+    const int wv = uni((int)(threadIdx.x >> 6));
+    int64_t blk = blockIdx.x;
+    if (FAM == COVT_FAMILY_VARINT) {
+        const int64_t split_blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
+        if (blk < split_blocks) {
+            decode_split_chunk((WaveSmem*)(smem + wv * kStride), in, split_descs, n_chunks, out, split_res);
+            return;
+        }
+        blk -= split_blocks;
+    }
+    const int64_t sid = blk * kWavesPerBlock + wv;
+    if (sid >= n_streams) return;
+    const covt_stream_desc d = descs[sid];
+    if ((d.flags & (COVT_DESC_LANE | COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD)) || op_family(d.op) != FAM) return;
+    // long streams are the kernel's critical path: let their waves win instruction arbitration
+    if (d.byte_length > kLongStream || d.num_values > kLongStream) __builtin_amdgcn_s_setprio(2);
+#ifdef COVT_TIMING  // profiling build (libcovt_timing.so): result = (duration, start) in 100 MHz ticks
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    Ctx c;
+    c.sm = (WaveSmem*)(smem + wv * kStride);
+    c.sb = in + d.in_off;
+    c.out = out + d.out_off;
+    c.avail = d.avail;
+    c.n = d.num_values;
+    c.nb = d.num_bits;
+    c.op = d.op;
+    c.byte_length = d.byte_length;
+    c.err = 0;
+    c.consumed = 0;
+#ifdef COVT_TIMING
+    c.ph_last = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k < kPhases; ++k) c.ph[k] = 0;
+#endif
+    if (c.n < 0 || c.avail < 0 || c.byte_length < 0) {
+        c.err = COVT_ERR_INVALID_ARG;
+    } else if (FAM == COVT_FAMILY_RLE) {
+        if (c.op == COVT_OP_BYTE_RLE_U8 || c.op == COVT_OP_BYTE_RLE_RAW) { if (c.n > 0) run_rle_byte(c); }
+        else if (c.op == COVT_OP_RLE_U64 || c.op == COVT_OP_RLE_I32 || c.op == COVT_OP_RLE_S64) { if (c.n > 0) run_rle_int(c); }
+        else c.err = COVT_ERR_UNSUPPORTED_ENCODING;
+#if defined(COVT_ABL_ONEOP)  // ablation build (instruction-cache footprint): one code path per family
+    } else if (FAM == COVT_FAMILY_VARINT) {
+        if (c.op == COVT_OP_VARINT_U64) run_varint_stream<COVT_OP_VARINT_U64>(c);
+        else run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I32>(c);
+    } else if (true) {
+        run_fastpfor<COVT_OP_FPF_ZZ_DELTA_I32>(c);
+#endif
+    } else if (FAM == COVT_FAMILY_VARINT) {
+        switch (c.op) {  // one uniform switch per stream; the loops are specialised per op
+        case COVT_OP_VARINT_I32: run_varint_stream<COVT_OP_VARINT_I32>(c); break;
+        case COVT_OP_VARINT_ZZ_I32: run_varint_stream<COVT_OP_VARINT_ZZ_I32>(c); break;
+        case COVT_OP_VARINT_ZZ_DELTA_I32: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I32>(c); break;
+        case COVT_OP_VARINT_ZZ_DELTA_XY: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_XY>(c); break;
+        case COVT_OP_VARINT_DELTA_MORTON: run_varint_stream<COVT_OP_VARINT_DELTA_MORTON>(c); break;
+        case COVT_OP_VARINT_U64: run_varint_stream<COVT_OP_VARINT_U64>(c); break;
+        case COVT_OP_VARINT_I32_AS_I64: run_varint_stream<COVT_OP_VARINT_I32_AS_I64>(c); break;
+        case COVT_OP_VARINT_ZZ_I32_AS_I64: run_varint_stream<COVT_OP_VARINT_ZZ_I32_AS_I64>(c); break;
+        case COVT_OP_VARINT_ZZ_S64: run_varint_stream<COVT_OP_VARINT_ZZ_S64>(c); break;
+        case COVT_OP_VARINT_ZZ_DELTA_S64: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_S64>(c); break;
+        default: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I64>(c); break;
+        }
+    } else {
+        switch (c.op) {
+        case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_I32>(c); break;
+        case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_XY>(c); break;
+        default: run_fastpfor<COVT_OP_FPF_DELTA_MORTON>(c); break;
+        }
+    }
+    if (lane_id() == 0) {
+        covt_stream_result r;
+        r.status = c.err;
+        r.consumed = c.consumed;
+#ifdef COVT_TIMING
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        r.status = c.err ? -1 : (int32_t)(t_end - t_start);
+        r.consumed = (int32_t)(uint32_t)t_start;
+        if (covt_phase_buf)
+            for (int k = 0; k < kPhases; ++k) covt_phase_buf[(descs + sid - covt_phase_desc0) * kPhases + k] = c.ph[k];
+#endif
+        res[sid] = r;
     }
 }
 
@@ -1808,6 +1819,62 @@ struct Pack16 {
         nb += 1;
         if ((nb & 15u) == 0) flush();
     }
+    // a run of k elements base + i * delta (E = 4: int32, E = 8: int64), whole packet slots per step:
+    // a run costs k / (16 / E) steps instead of k (the other lanes of the wave wait on the longest)
+    template <int E>
+    __device__ __forceinline__ void put_run(int64_t base, int32_t delta, int32_t k) {
+        constexpr int PER = 16 / E;  // elements per packet
+        while (k > 0) {
+            const int32_t slot = (int32_t)((nb / E) & (PER - 1));
+            const int32_t m = min(PER - slot, k);
+            uint32_t w[4] = {w0, w1, w2, w3};
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const int32_t i = j - slot;
+                if (i >= 0 && i < m) {
+                    const uint64_t v = (uint64_t)base + (uint64_t)(int64_t)(int32_t)(i * delta);
+                    if (E == 4) {
+                        w[j] = (uint32_t)v;
+                    } else {
+                        w[2 * j] = (uint32_t)v;
+                        w[2 * j + 1] = (uint32_t)(v >> 32);
+                    }
+                }
+            }
+            w0 = w[0];
+            w1 = w[1];
+            w2 = w[2];
+            w3 = w[3];
+            base = (int64_t)((uint64_t)base + (uint64_t)(int64_t)(int32_t)(m * delta));
+            k -= m;
+            nb += (uint32_t)(m * E);
+            if ((nb & 15u) == 0) flush();
+        }
+    }
+    // k copies of byte b, up to 16 per step
+    __device__ __forceinline__ void put_bytes(uint32_t b, int32_t k) {
+        const uint32_t rep = (b & 0xffu) * 0x01010101u;
+        while (k > 0) {
+            const int32_t slot = (int32_t)(nb & 15u);
+            const int32_t m = min(16 - slot, k);
+            uint32_t w[4] = {w0, w1, w2, w3};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int32_t lo = max(slot - 4 * j, 0), hi = min(slot + m - 4 * j, 4);  // bytes [lo, hi) of dword j
+                if (hi > lo) {
+                    const uint32_t mask = (hi >= 4 ? 0xffffffffu : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
+                    w[j] = (w[j] & ~mask) | (rep & mask);
+                }
+            }
+            w0 = w[0];
+            w1 = w[1];
+            w2 = w[2];
+            w3 = w[3];
+            k -= m;
+            nb += (uint32_t)m;
+            if ((nb & 15u) == 0) flush();
+        }
+    }
     __device__ __forceinline__ void finish() {
         if (nb & 15u) flush();
     }
@@ -1832,7 +1899,9 @@ __device__ void lane_rle_int(LaneBytes& in, int op, int32_t n, uint8_t* out, int
             if ((err = lane_vulong(in, o, raw))) return;
             const int64_t b = is_signed ? zz64(raw) : (int64_t)raw;
             const int32_t k = cnt < n - done ? cnt : n - done;
-            for (int32_t i = 0; i < k; ++i) put((int64_t)((uint64_t)b + (uint64_t)(int64_t)(int32_t)(i * delta)));
+            if (to_i32) pk.put_run<4>(b, delta, k);
+            else pk.put_run<8>(b, delta, k);
+            done += k;
         } else {  // literals: 256 - control varints, all read even past n
             const int32_t cnt = 0x100 - (int32_t)control;
             for (int32_t i = 0; i < cnt; ++i) {
@@ -1858,7 +1927,7 @@ __device__ void lane_rle_byte(LaneBytes& in, int32_t n, uint8_t* out, bool check
             const uint32_t b = in.at(o++);
             bad |= b > 5u;
             const int32_t k = cnt < n - done ? cnt : n - done;
-            for (int32_t i = 0; i < k; ++i) pk.put8(b);
+            pk.put_bytes(b, k);
             done += k;
         } else {
             const int32_t cnt = 0x100 - (int32_t)control;
@@ -1913,9 +1982,14 @@ __global__ __launch_bounds__(256) void decode_lane_kernel(const uint8_t* __restr
 
 }  // namespace covt
 
-extern "C" int covt_launch_family(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
-                                  uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream) {
-    if (n_streams <= 0) return COVT_OK;
+extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc,
+                                        int64_t n_streams, uint8_t* d_out, covt_stream_result* d_res,
+                                        const covt_stream_desc* d_split, int64_t n_split, covt_stream_result* d_split_res,
+                                        hipStream_t stream) {
+    if (n_split < 0 || n_split % covt::kSplitSlots) return COVT_ERR_INVALID_ARG;
+    if (n_split && fam != COVT_FAMILY_VARINT) return COVT_ERR_INVALID_ARG;
+    if (n_streams <= 0 && n_split == 0) return COVT_OK;
+    if (n_streams < 0) n_streams = 0;
     if (fam == COVT_FAMILY_LANE) {
         const int64_t lblocks = (n_streams + 255) / 256;
         if (lblocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
@@ -1923,32 +1997,32 @@ extern "C" int covt_launch_family(int fam, const uint8_t* d_in, const covt_strea
                            n_streams, d_out, d_res);
         return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
     }
-    const int64_t blocks = (n_streams + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
+    const int64_t n_chunks = n_split / covt::kSplitSlots;
+    const int64_t blocks = (n_streams + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock +
+                           (n_chunks + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
     const dim3 grid((unsigned)blocks), block(64 * covt::kWavesPerBlock);
     switch (fam) {
     case COVT_FAMILY_RLE:
         hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_RLE>, grid, block, 0, stream, d_in, d_desc,
-                           n_streams, d_out, d_res);
+                           n_streams, d_out, d_res, nullptr, (int64_t)0, nullptr);
         break;
     case COVT_FAMILY_VARINT:
         hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_VARINT>, grid, block, 0, stream, d_in, d_desc,
-                           n_streams, d_out, d_res);
+                           n_streams, d_out, d_res, d_split, n_chunks, d_split_res);
         break;
     case COVT_FAMILY_FASTPFOR:
         hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_FASTPFOR>, grid, block, 0, stream, d_in, d_desc,
-                           n_streams, d_out, d_res);
+                           n_streams, d_out, d_res, nullptr, (int64_t)0, nullptr);
         break;
-    case COVT_FAMILY_SPLIT: {
-        const int64_t n_chunks = n_streams / covt::kSplitSlots;
-        if (n_chunks * covt::kSplitSlots != n_streams) return COVT_ERR_INVALID_ARG;
-        const dim3 sgrid((unsigned)((n_chunks + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock));
-        hipLaunchKernelGGL(covt::decode_split_kernel, sgrid, block, 0, stream, d_in, d_desc, n_chunks, d_out, d_res);
-        break;
-    }
     default: return COVT_ERR_INVALID_ARG;
     }
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
+}
+
+extern "C" int covt_launch_family(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
+                                  uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream) {
+    return covt_launch_family_split(fam, d_in, d_desc, n_streams, d_out, d_res, nullptr, 0, nullptr, stream);
 }
 
 extern "C" int covt_op_family_of(int op) { return covt::op_family(op); }

@@ -541,16 +541,16 @@ int fpf_call(const uint8_t* buf, size_t buf_len, int32_t* pos, int op, int32_t n
     return COVT_OK;
 }
 
-// Fork/join of the family kernels: RLE on the caller's stream, the other four on auxiliary
+// Fork/join of the family kernels: RLE on the caller's stream, the other three on auxiliary
 // streams ordered by events (capturable into a hipGraph).  The auxiliary streams and events come
 // from a process-wide per-device pool: a launch takes a set, enqueues, and hands it back, so
 // concurrent callers (one host thread per device, JNI threads) never share one and nothing leaks
 // when threads come and go; the pool holds as many sets as launches ever overlapped.
-constexpr int kForkAux = 4;
+constexpr int kForkAux = 3;
 struct ForkCtx {
     int device = -1;
-    hipStream_t aux[kForkAux] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t fork = nullptr, join[kForkAux] = {nullptr, nullptr, nullptr, nullptr};
+    hipStream_t aux[kForkAux] = {nullptr, nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[kForkAux] = {nullptr, nullptr, nullptr};
 };
 std::mutex g_fork_mu;
 std::vector<ForkCtx*> g_fork_free;
@@ -602,25 +602,33 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
     int64_t off[COVT_NUM_FAMILIES];
     off[0] = 0;
     for (int k = 1; k < COVT_NUM_FAMILIES; ++k) off[k] = off[k - 1] + counts[k - 1];
-    // the families other than RLE go to the auxiliary streams (longest-running first); empty ones
-    // are not forked at all
-    const int aux_fam[kForkAux] = {COVT_FAMILY_SPLIT, COVT_FAMILY_FASTPFOR, COVT_FAMILY_VARINT, COVT_FAMILY_LANE};
+    // RLE on the caller's stream, the other families on three auxiliary streams (the varint launch
+    // also carries the split chunks): with the caller's stream that is four hardware queues, HIP's
+    // default per process -- a fifth stream would share a queue and serialise behind another family
+    const int aux_fam[kForkAux] = {COVT_FAMILY_FASTPFOR, COVT_FAMILY_VARINT, COVT_FAMILY_LANE};
+    const int64_t n_split = counts[COVT_FAMILY_SPLIT];
+    auto cnt = [&](int fam) { return counts[fam] + (fam == COVT_FAMILY_VARINT ? n_split : 0); };
     bool any = false;
-    for (int i = 0; i < kForkAux; ++i) any |= counts[aux_fam[i]] > 0;
+    for (int i = 0; i < kForkAux; ++i) any |= cnt(aux_fam[i]) > 0;
     if (any && hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
     int st = COVT_OK;
-    bool forked[kForkAux] = {false, false, false, false};
+    bool forked[kForkAux] = {false, false, false};
     for (int i = 0; i < kForkAux && !st; ++i) {
         const int fam = aux_fam[i];
-        if (counts[fam] <= 0) continue;
+        if (cnt(fam) <= 0) continue;
         if (hipStreamWaitEvent(f.aux[i], f.fork, 0) != hipSuccess) return COVT_ERR_DEVICE;
         forked[i] = true;
-        // split chunks: look-back records and the ticket counter live in the family's result entries
-        if (fam == COVT_FAMILY_SPLIT &&
-            hipMemsetAsync(d_res + off[fam], 0, (size_t)counts[fam] * sizeof(covt_stream_result), f.aux[i]) !=
-                hipSuccess)
-            st = COVT_ERR_DEVICE;
-        if (!st) st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], f.aux[i]);
+        if (fam == COVT_FAMILY_VARINT && n_split > 0) {
+            // split chunks: look-back records and the ticket counter live in their result entries
+            covt_stream_result* sres = d_res + off[COVT_FAMILY_SPLIT];
+            if (hipMemsetAsync(sres, 0, (size_t)n_split * sizeof(covt_stream_result), f.aux[i]) != hipSuccess)
+                st = COVT_ERR_DEVICE;
+            if (!st)
+                st = covt_launch_family_split(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam],
+                                              d_desc + off[COVT_FAMILY_SPLIT], n_split, sres, f.aux[i]);
+        } else if (!st) {
+            st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], f.aux[i]);
+        }
     }
     if (!st) st = covt_launch_family(COVT_FAMILY_RLE, d_in, d_desc, counts[0], d_out, d_res, s);
     for (int i = 0; i < kForkAux; ++i) {

@@ -12,6 +12,11 @@ extern "C" {
 // [0, n_streams); descriptors of other families are skipped.
 int covt_launch_family(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
                        uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream);
+// The varint family's launch with the split chunks (COVT_FAMILY_SPLIT descriptors d_split[0, n_split),
+// their results / look-back records at d_split_res) carried in the same kernel.
+int covt_launch_family_split(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
+                             uint8_t* d_out, covt_stream_result* d_res, const covt_stream_desc* d_split,
+                             int64_t n_split, covt_stream_result* d_split_res, hipStream_t stream);
 int covt_op_family_of(int op);
 }
 

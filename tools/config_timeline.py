@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Per-stream timeline of the BASELINE config 2-4 launches (GPU, profiling build libcovt_timing.so).
+
+For each config: HIP-event time of the launch, the in-kernel span (first stream start -> last stream
+end, s_memrealtime at 100 MHz), and the slowest streams -- to tell launch overhead from long poles.
+Run with COVT_SPLIT_MIN=-1 (the timing build writes timestamps into the result entries, which the
+split path uses for its look-back records)."""
+import os
+import sys
+
+os.environ["COVT_LIB_VARIANT"] = "libcovt_timing.so"
+os.environ.setdefault("COVT_SPLIT_MIN", "-1")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+from stream_timeline import NAMES, TICK_US  # noqa: E402
+
+
+def main():
+    import torch
+
+    covt = bench.load_covt()
+    lib = bench.tile_library()
+    for name in bench.CONFIG_LEGS:
+        picks = bench.config_tiles(lib, name)
+        plan = covt.Plan.from_tiles([t for _, t in picks])
+        mask = bench.config_mask(plan, name)
+        batch = covt.DeviceBatch(plan, "cuda")
+        sub = batch.subset(mask)
+        s = torch.cuda.current_stream()
+        for _ in range(3):
+            sub.decode(s)
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(s)
+        sub.decode(s)
+        ev[1].record(s)
+        torch.cuda.synchronize()
+        _, res, idx = sub.results()
+        dur = res[:, 0].astype(np.int64)
+        start = res[:, 1].astype(np.int64) & 0xffffffff
+        end = start + dur
+        t0 = start.min()
+        st = plan.streams
+        ops = st["op"][idx]
+        print("%s: %d streams, event %.1f us, in-kernel span %.1f us, last start %.1f us" % (
+            name, len(idx), ev[0].elapsed_time(ev[1]) * 1e3, (end.max() - t0) * TICK_US, (start.max() - t0) * TICK_US))
+        for i in np.argsort(-end)[:6]:
+            j = idx[i]
+            print("   %-12s bytes %7d values %7d  start %7.1f us  dur %7.1f us" % (
+                NAMES.get(int(ops[i]), ops[i]), st["byte_length"][j], st["num_values"][j], (start[i] - t0) * TICK_US,
+                dur[i] * TICK_US))
+        fl = plan.descs.reshape(-1, 32)[st["desc_index"][idx], 26]
+        fam = np.where(fl & 1, 3, np.where(np.isin(ops, (10, 11, 12)), 2,
+                                           np.where(np.isin(ops, (1, 2, 3, 4, 16)), 0, 1)))
+        for f, fname in enumerate(("RLE", "VARINT", "FASTPFOR", "LANE")):
+            m = fam == f
+            if not m.any():
+                continue
+            k = np.nonzero(m)[0][np.argmax(dur[m])]
+            print("   family %-8s n=%4d first start %6.1f last start %6.1f last end %6.1f us; longest %s %d B %d vals "
+                  "%.1f us (start %.1f)" % (fname, int(m.sum()), (start[m].min() - t0) * TICK_US,
+                                            (start[m].max() - t0) * TICK_US, (end[m].max() - t0) * TICK_US,
+                                            NAMES.get(int(ops[k]), ops[k]), st["byte_length"][idx[k]],
+                                            st["num_values"][idx[k]], dur[k] * TICK_US, (start[k] - t0) * TICK_US))
+        del sub, batch, plan
+
+
+if __name__ == "__main__":
+    main()
