@@ -541,7 +541,7 @@ int fpf_call(const uint8_t* buf, size_t buf_len, int32_t* pos, int op, int32_t n
     return COVT_OK;
 }
 
-// Fork/join of the family kernels: RLE on the caller's stream, the other three on auxiliary
+// Fork/join of the family kernels: the first on the caller's stream, the others on auxiliary
 // streams ordered by events (capturable into a hipGraph).  The auxiliary streams and events come
 // from a process-wide per-device pool: a launch takes a set, enqueues, and hands it back, so
 // concurrent callers (one host thread per device, JNI threads) never share one and nothing leaks
@@ -602,37 +602,41 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
     int64_t off[COVT_NUM_FAMILIES];
     off[0] = 0;
     for (int k = 1; k < COVT_NUM_FAMILIES; ++k) off[k] = off[k - 1] + counts[k - 1];
-    // RLE on the caller's stream, the other families on three auxiliary streams (the varint launch
-    // also carries the split chunks): with the caller's stream that is four hardware queues, HIP's
-    // default per process -- a fifth stream would share a queue and serialise behind another family
-    const int aux_fam[kForkAux] = {COVT_FAMILY_FASTPFOR, COVT_FAMILY_VARINT, COVT_FAMILY_LANE};
+    // Four launches (the varint one also carries the split chunks), longest-running first: the first
+    // with work goes on the caller's stream, the others on up to three auxiliary streams forked from
+    // and joined back into it -- four hardware queues with the caller's, HIP's default per process (a
+    // fifth stream would share a queue and serialise behind another family).  A launch with a single
+    // family forks nothing.  (Measured: where the lane family runs -- own stream, before or after RLE,
+    // behind varint -- does not change the bench launch.)
     const int64_t n_split = counts[COVT_FAMILY_SPLIT];
-    auto cnt = [&](int fam) { return counts[fam] + (fam == COVT_FAMILY_VARINT ? n_split : 0); };
-    bool any = false;
-    for (int i = 0; i < kForkAux; ++i) any |= cnt(aux_fam[i]) > 0;
-    if (any && hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
+    const int order[4] = {COVT_FAMILY_FASTPFOR, COVT_FAMILY_VARINT, COVT_FAMILY_RLE, COVT_FAMILY_LANE};
+    int fams[4], nf = 0;
+    for (int fam : order)
+        if (counts[fam] + (fam == COVT_FAMILY_VARINT ? n_split : 0) > 0) fams[nf++] = fam;
+    if (nf > 1 && hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
     int st = COVT_OK;
-    bool forked[kForkAux] = {false, false, false};
-    for (int i = 0; i < kForkAux && !st; ++i) {
-        const int fam = aux_fam[i];
-        if (cnt(fam) <= 0) continue;
-        if (hipStreamWaitEvent(f.aux[i], f.fork, 0) != hipSuccess) return COVT_ERR_DEVICE;
-        forked[i] = true;
+    int nforked = 0;
+    for (int i = 0; i < nf && !st; ++i) {
+        const int fam = fams[i];
+        hipStream_t q = s;
+        if (i > 0) {
+            q = f.aux[i - 1];
+            if (hipStreamWaitEvent(q, f.fork, 0) != hipSuccess) return COVT_ERR_DEVICE;
+            nforked = i;
+        }
         if (fam == COVT_FAMILY_VARINT && n_split > 0) {
             // split chunks: look-back records and the ticket counter live in their result entries
             covt_stream_result* sres = d_res + off[COVT_FAMILY_SPLIT];
-            if (hipMemsetAsync(sres, 0, (size_t)n_split * sizeof(covt_stream_result), f.aux[i]) != hipSuccess)
+            if (hipMemsetAsync(sres, 0, (size_t)n_split * sizeof(covt_stream_result), q) != hipSuccess)
                 st = COVT_ERR_DEVICE;
             if (!st)
                 st = covt_launch_family_split(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam],
-                                              d_desc + off[COVT_FAMILY_SPLIT], n_split, sres, f.aux[i]);
-        } else if (!st) {
-            st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], f.aux[i]);
+                                              d_desc + off[COVT_FAMILY_SPLIT], n_split, sres, q);
+        } else {
+            st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], q);
         }
     }
-    if (!st) st = covt_launch_family(COVT_FAMILY_RLE, d_in, d_desc, counts[0], d_out, d_res, s);
-    for (int i = 0; i < kForkAux; ++i) {
-        if (!forked[i]) continue;
+    for (int i = 0; i < nforked; ++i) {
         if (hipEventRecord(f.join[i], f.aux[i]) != hipSuccess) return COVT_ERR_DEVICE;
         if (hipStreamWaitEvent(s, f.join[i], 0) != hipSuccess) return COVT_ERR_DEVICE;
     }
@@ -1216,11 +1220,18 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         uint32_t i;
     };
     std::vector<Key> keys(ns);
-    const int64_t split_min = env_i64("COVT_SPLIT_MIN", COVT_SPLIT_MIN);
+    // split a stream only where one wave decoding it would outlast the launch: above COVT_SPLIT_MIN
+    // bytes and above the batch's stream bytes / COVT_SPLIT_RATIO (a wave decodes ~0.35 GB/s, the
+    // launch moves ~500 GB/s: a stream over ~1/1400 of the batch is a long pole).  Big batches are
+    // throughput-bound and split nothing; single tiles and small batches split their long streams.
+    int64_t split_min = env_i64("COVT_SPLIT_MIN", COVT_SPLIT_MIN);
+    const int64_t split_ratio = env_i64("COVT_SPLIT_RATIO", COVT_SPLIT_RATIO);
+    if (split_min >= 0 && split_ratio > 0) split_min = std::max<int64_t>(split_min, p->in_bytes / split_ratio);
+    const int32_t lane_max = (int32_t)env_i64("COVT_LANE_MAX_BYTES", kLaneMaxBytes);  // A/B knob
     const int64_t split_chunk = std::max<int64_t>(64, env_i64("COVT_SPLIT_CHUNK", COVT_SPLIT_CHUNK));
     for (size_t i = 0; i < ns; ++i) {
         const auto& s = p->info[i];
-        const bool lane = lane_stream(s.op, s.desc_index, s.byte_length);
+        const bool lane = lane_stream(s.op, s.desc_index, s.byte_length, lane_max);
         const bool split = split_stream(s.op, s.desc_index, s.byte_length, split_min);
         const uint64_t fam = split ? (uint64_t)COVT_FAMILY_SPLIT
                              : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);

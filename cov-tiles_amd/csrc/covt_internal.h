@@ -23,11 +23,11 @@ int covt_op_family_of(int op);
 // Plan rule for the lane-per-stream kernel: RLE streams of at most kLaneMaxValues values and
 // kLaneMaxBytes bytes (a lane decodes serially; larger streams amortise a wave's window setup).
 constexpr int32_t kLaneMaxValues = 256;
-constexpr int32_t kLaneMaxBytes = 256;
-inline bool lane_stream(int op, int32_t num_values, int32_t byte_length) {
+constexpr int32_t kLaneMaxBytes = 64;  // the lane's first 68-byte window: no reloads (A/B: COVT_LANE_MAX_BYTES)
+inline bool lane_stream(int op, int32_t num_values, int32_t byte_length, int32_t max_bytes = kLaneMaxBytes) {
     return (op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_BYTE_RLE_RAW || op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_S64 ||
             op == COVT_OP_RLE_I32) &&
-           num_values >= 0 && num_values <= kLaneMaxValues && byte_length >= 0 && byte_length <= kLaneMaxBytes;
+           num_values >= 0 && num_values <= kLaneMaxValues && byte_length >= 0 && byte_length <= max_bytes;
 }
 inline int desc_family(const covt_stream_desc& d) {
     if (d.flags & (COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD)) return COVT_FAMILY_SPLIT;

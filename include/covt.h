@@ -150,6 +150,7 @@ enum covt_op {
 #define COVT_SPLIT_SLOTS 8
 #define COVT_SPLIT_CHUNK 4096 /* default chunk bytes (env COVT_SPLIT_CHUNK at plan creation) */
 #define COVT_SPLIT_MIN 8192   /* default: streams longer than this are split (env COVT_SPLIT_MIN; -1: never) */
+#define COVT_SPLIT_RATIO 3000 /* ... and longer than the plan's stream bytes / this (env COVT_SPLIT_RATIO; 0: off) */
 
 /* One device-resident plan entry (32 bytes). */
 typedef struct covt_stream_desc {

@@ -27,6 +27,7 @@ def test_fixtures_forced_split(covt, gpu_available, golden_streams, monkeypatch,
     import torch
 
     monkeypatch.setenv("COVT_SPLIT_MIN", "200")
+    monkeypatch.setenv("COVT_SPLIT_RATIO", "0")
     monkeypatch.setenv("COVT_SPLIT_CHUNK", str(chunk))
     paths = tile_paths()
     keys = [tile_key(p) for p in paths]

@@ -20,6 +20,7 @@ def _tile(name="5_16_20"):
 @pytest.mark.parametrize("chunk", [64, 1000, 4096])
 def test_split_layout(covt, monkeypatch, chunk):
     monkeypatch.setenv("COVT_SPLIT_MIN", "256")
+    monkeypatch.setenv("COVT_SPLIT_RATIO", "0")
     monkeypatch.setenv("COVT_SPLIT_CHUNK", str(chunk))
     plan = covt.Plan.from_tiles([_tile(), _tile("14_8298_10748")])
     d = plan.descs.view(DESC)
@@ -55,6 +56,7 @@ def test_split_disabled_and_subset(covt, monkeypatch):
     plan = covt.Plan.from_tiles([_tile()])
     assert plan.family_counts[covt.FAMILY_SPLIT] == 0 and plan.num_descs == plan.num_streams
     monkeypatch.setenv("COVT_SPLIT_MIN", "256")
+    monkeypatch.setenv("COVT_SPLIT_RATIO", "0")
     monkeypatch.setenv("COVT_SPLIT_CHUNK", "512")
     plan = covt.Plan.from_tiles([_tile()])
     assert plan.family_counts[covt.FAMILY_SPLIT] > 0
@@ -63,3 +65,14 @@ def test_split_disabled_and_subset(covt, monkeypatch):
     assert counts.sum() == descs.size // 32 == prim.size
     assert (prim >= 0).sum() == mask.sum() and set(prim[prim >= 0].tolist()) == set(np.nonzero(mask)[0].tolist())
     assert counts[covt.FAMILY_SPLIT] % covt.SPLIT_SLOTS == 0
+
+
+def test_split_threshold_relative_to_batch(covt, monkeypatch):
+    """Default policy: a stream is split only above COVT_SPLIT_MIN and above the batch's stream bytes /
+    COVT_SPLIT_RATIO -- one tile splits its long streams, a big batch of the same tiles splits none."""
+    monkeypatch.delenv("COVT_SPLIT_MIN", raising=False)
+    monkeypatch.delenv("COVT_SPLIT_RATIO", raising=False)
+    one = covt.Plan.from_tiles([_tile()])
+    assert one.family_counts[covt.FAMILY_SPLIT] > 0
+    many = covt.Plan.from_tiles([_tile()] * 1000)
+    assert many.family_counts[covt.FAMILY_SPLIT] == 0
