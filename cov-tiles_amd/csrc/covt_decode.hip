@@ -96,6 +96,12 @@ __device__ __forceinline__ uint4 ld128(uintptr_t a16) {
     const u32x4 v = *(const g_v4*)a16;
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+// the same from a uniform base and a 32-bit per-lane offset (global_load ... v_off, s[base])
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+__device__ __forceinline__ uint4 ld128_off(const g_u8* base, uint32_t off) {
+    const u32x4 v = *(const g_v4*)(base + off);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {  // any alignment (input is padded)
     const uintptr_t a = (uintptr_t)p;
@@ -1238,19 +1244,21 @@ __device__ void run_fastpfor(Ctx& c) {
                 // loads consumed only in the next iteration (the vmcnt wait lands there).  The packed
                 // words are requested only by the lanes whose 16 bytes the unpack reads (8b words from
                 // word qoff <= 3, plus the next lane's first word): 2b + 2 lanes, not all 64.
+                // Both loads are issued by every lane with no exec mask and from a uniform base plus a
+                // 32-bit lane offset (the `saddr` form, no 64-bit address math per lane): lanes past the
+                // 2b + 2 whose 16 bytes the unpack reads repeat the last one's address, lanes without an
+                // exception read word 0.  A masked load or a select of its address under a branch made
+                // the compiler drain every outstanding load (vmcnt(0)) right after issuing the prefetch.
                 const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pk) & ~(uintptr_t)15;
-#if defined(COVT_FPF_FULL_RAW)  // experiment: every lane loads
-                pr.raw = ld128(a16 + 16 * (uintptr_t)l);
-#else
-                pr.raw = l <= 2 * uni(hv.b) + 1 ? ld128(a16 + 16 * (uintptr_t)l) : make_uint4(0, 0, 0, 0);
-#endif
+                const uint32_t lraw = min((uint32_t)l, 2u * (uint32_t)uni(hv.b) + 1u);
+                pr.raw = ld128_off((const g_u8*)a16, 16u * lraw);
                 const int32_t k = h.idx;
                 const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
                 uint32_t xb;
-                int32_t wi = xword(k >= 2 ? k : 2, xs, h.xcur + (uint32_t)l, xb);
-                wi = (k >= 2 && l < h.ce && wi < nw32) ? wi : 0;
-                const uintptr_t xa4 = ((uintptr_t)c.sb + 4u * (uint32_t)wi) & ~(uintptr_t)3;
-                const u32x3 xv = *(const g_v3*)xa4;
+                const int32_t wx = xword(k >= 2 ? k : 2, xs, h.xcur + (uint32_t)l, xb);
+                const uint32_t xon = (uint32_t)(k >= 2) & (uint32_t)(l < h.ce) & (uint32_t)(wx < nw32);
+                const uint32_t wi = (uint32_t)wx & (0u - xon);
+                const u32x3 xv = *(const g_v3*)((const g_u8*)(((uintptr_t)c.sb) & ~(uintptr_t)3) + 4u * wi);
                 pr.x0 = xv.x;
                 pr.x1 = xv.y;
                 pr.x2 = xv.z;
@@ -1593,8 +1601,7 @@ __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, co
 }
 
 // One split chunk per wave, chunks in ticket order (tickets from a counter in the split region's
-// result entries); runs inside the varint family kernel (its first workgroups), so the split chunks
-// share that kernel's launch and hardware queue.
+// result entries).
 __device__ void decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in, const covt_stream_desc* __restrict__ descs,
                                    int64_t n_chunks, uint8_t* __restrict__ out, covt_stream_result* __restrict__ res) {
     uint32_t* ctr = (uint32_t*)(res + kRecTicket);  // the first chunk's ticket entry
@@ -1639,29 +1646,27 @@ __host__ __device__ constexpr int op_family(int op) {
 
 // One wave per descriptor; waves whose descriptor belongs to another family return at once (used
 // when the caller's descriptors are not grouped by family).
-// The varint family's launch also carries the split chunks (COVT_FAMILY_SPLIT): its first
-// split_blocks workgroups decode chunks, the rest decode whole varint streams.
+// Split chunks (COVT_FAMILY_SPLIT) have a kernel of their own: inside the varint family kernel their
+// code raised it from 31 to 72 VGPRs with a scratch spill (varint family alone 0.63 -> 0.88 ms).
+__global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const uint8_t* __restrict__ in,
+                                                                           const covt_stream_desc* __restrict__ descs,
+                                                                           int64_t n_chunks, uint8_t* __restrict__ out,
+                                                                           covt_stream_result* __restrict__ res) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kFamSmemVarint];
+    const int wv = uni((int)(threadIdx.x >> 6));
+    decode_split_chunk((WaveSmem*)(smem + wv * kFamSmemVarint), in, descs, n_chunks, out, res);
+}
+
 template <int FAM>
 __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(const uint8_t* __restrict__ in,
                                                             const covt_stream_desc* __restrict__ descs,
                                                             int64_t n_streams, uint8_t* __restrict__ out,
-                                                            covt_stream_result* __restrict__ res,
-                                                            const covt_stream_desc* __restrict__ split_descs,
-                                                            int64_t n_chunks, covt_stream_result* __restrict__ split_res) {
+                                                            covt_stream_result* __restrict__ res) {
     constexpr int kStride = FAM == COVT_FAMILY_RLE ? kFamSmemRle
                             : FAM == COVT_FAMILY_VARINT ? kFamSmemVarint : kFamSmemFpf;
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kStride];
     const int wv = uni((int)(threadIdx.x >> 6));
-    int64_t blk = blockIdx.x;
-    if (FAM == COVT_FAMILY_VARINT) {
-        const int64_t split_blocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
-        if (blk < split_blocks) {
-            decode_split_chunk((WaveSmem*)(smem + wv * kStride), in, split_descs, n_chunks, out, split_res);
-            return;
-        }
-        blk -= split_blocks;
-    }
-    const int64_t sid = blk * kWavesPerBlock + wv;
+    const int64_t sid = (int64_t)blockIdx.x * kWavesPerBlock + wv;
     if (sid >= n_streams) return;
     const covt_stream_desc d = descs[sid];
     if ((d.flags & (COVT_DESC_LANE | COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD)) || op_family(d.op) != FAM) return;
@@ -1998,22 +2003,30 @@ extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt
         return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
     }
     const int64_t n_chunks = n_split / covt::kSplitSlots;
-    const int64_t blocks = (n_streams + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock +
-                           (n_chunks + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
+    const dim3 block(64 * covt::kWavesPerBlock);
+    if (n_chunks > 0) {  // the chunks first, on the same stream (the same hardware queue) as the family
+        const int64_t sblocks = (n_chunks + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
+        if (sblocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
+        hipLaunchKernelGGL(covt::decode_split_kernel, dim3((unsigned)sblocks), block, 0, stream, d_in, d_split,
+                           n_chunks, d_out, d_split_res);
+        if (hipGetLastError() != hipSuccess) return COVT_ERR_DEVICE;
+    }
+    if (n_streams <= 0) return COVT_OK;
+    const int64_t blocks = (n_streams + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
-    const dim3 grid((unsigned)blocks), block(64 * covt::kWavesPerBlock);
+    const dim3 grid((unsigned)blocks);
     switch (fam) {
     case COVT_FAMILY_RLE:
         hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_RLE>, grid, block, 0, stream, d_in, d_desc,
-                           n_streams, d_out, d_res, nullptr, (int64_t)0, nullptr);
+                           n_streams, d_out, d_res);
         break;
     case COVT_FAMILY_VARINT:
         hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_VARINT>, grid, block, 0, stream, d_in, d_desc,
-                           n_streams, d_out, d_res, d_split, n_chunks, d_split_res);
+                           n_streams, d_out, d_res);
         break;
     case COVT_FAMILY_FASTPFOR:
         hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_FASTPFOR>, grid, block, 0, stream, d_in, d_desc,
-                           n_streams, d_out, d_res, nullptr, (int64_t)0, nullptr);
+                           n_streams, d_out, d_res);
         break;
     default: return COVT_ERR_INVALID_ARG;
     }
