@@ -1115,14 +1115,36 @@ typedef __attribute__((address_space(1))) const u32x3 g_v3;
 // and its packed words, exception positions and exception values are already in flight.  The
 // packed words are staged in LDS already aligned to the stream's word grid and byte-swapped, so a
 // value costs one ds_read2_b32 and one v_alignbit_b32.
+// Output values [v0, v1) only (a split chunk; the whole stream by default): pages before v0 are
+// skipped after their directory, blocks before v0 in its page are walked (headers, exception cursors)
+// but not decoded, the VariableByte tail and the zero fill belong to the range holding value n - 1.
+// sum_only: no stores -- the transformed values (zigzag, or the raw Morton deltas) are summed into
+// *sums (x,y ops: .x over even, .y over odd value indices).  `cr0`: the running sums before v0.
+template <int OP, int K>
+__device__ __forceinline__ void sum_values(const uint32_t (&v)[K], int64_t base, int32_t count, uint32_t& ax,
+                                           uint32_t& ay) {
+    const int l = lane_id();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const bool ok = l * K + k < count;
+        const uint32_t z = ok ? (OP == COVT_OP_FPF_DELTA_MORTON ? v[k] : (uint32_t)zz32(v[k])) : 0u;
+        const bool odd = OP == COVT_OP_FPF_ZZ_DELTA_XY && ((base + l * K + k) & 1);
+        ax += odd ? 0u : z;
+        ay += odd ? z : 0u;
+    }
+}
+// (sum_only is a run-time flag: two template copies inlined into one chunk kernel made it 248 VGPRs)
 template <int OP>
-__device__ void run_fastpfor(Ctx& c) {
+__device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Carry cr0 = Carry{0, 0},
+                             bool sum_only = false, Carry* sums = nullptr) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
     const Words W{c.sb, c.byte_length / 4};
     const int64_t nw = W.nw;
     const uint32_t sbmis = (uint32_t)((uintptr_t)c.sb & 15);  // stream base misalignment (uniform)
-    Carry cr{0, 0};
+    Carry cr = cr0;
+    uint32_t ax = 0, ay = 0;                  // sum_only: per-lane sums
+    const bool has_end = v1 >= c.n;           // this range holds the stream's last value
     int32_t decoded = 0;
     int32_t L = 0;
     int64_t p = 1;
@@ -1190,7 +1212,10 @@ __device__ void run_fastpfor(Ctx& c) {
             }
             if (c.err) break;
             COVT_PHASE(c, 0);
-            const int32_t nblocks = uni(thissize / kFpfBlock);
+            const int32_t nblocks_page = uni(thissize / kFpfBlock);
+            // blocks of this page holding values of [v0, v1)
+            const int32_t jb0 = v0 > done ? min((v0 - done) / kFpfBlock, nblocks_page) : 0;
+            const int32_t nblocks = v1 <= done ? 0 : uni(min(nblocks_page, (int32_t)(((int64_t)v1 - done + kFpfBlock - 1) / kFpfBlock)));
             const int32_t nw32 = (int32_t)nw;
             const int32_t bclen = uni((int32_t)(bcw * 4));
             const uint8_t* cb8 = (const uint8_t*)sm.u.f.cbuf;
@@ -1273,9 +1298,18 @@ __device__ void run_fastpfor(Ctx& c) {
             FpfHdr h;
             FpfPre pre;
             int32_t pk = (int32_t)p0 + 1;
-            c.err = walk(0, h);
-            if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
-            if (!c.err) prefetch(h, pk, pre, 0);
+            int32_t cur0 = 0;
+            // headers of the page's blocks before the range: walked (offsets, exception cursors) only
+            for (int32_t j = 0; j < jb0 && jb0 < nblocks && !c.err; ++j) {
+                c.err = walk(cur0, h);
+                pk = uni(pk + 8 * h.b);
+                cur0 = uni(h.next);
+            }
+            if (jb0 < nblocks && !c.err) {
+                c.err = walk(cur0, h);
+                if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
+                if (!c.err) prefetch(h, pk, pre, 0);
+            }
             // one block; the loop below alternates two register sets so that no in-flight prefetch
             // register is ever copied (a copy would force the vmcnt wait at the end of the iteration)
             auto block = [&](int32_t j, const FpfPre& pc, FpfPre& pn, int slot) {
@@ -1385,22 +1419,26 @@ __device__ void run_fastpfor(Ctx& c) {
 #if defined(COVT_ABL_NOSTORE)  // ablation build: every block's output to the same 1 KiB (L2-resident)
                 sink_values<OP, 4>(v, 0, 0, kFpfBlock, c.nb, c.out, cr);
 #else
-                sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, 0, kFpfBlock, c.nb, c.out, cr);
+                if (sum_only)
+                    sum_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, ax, ay);
+                else
+                    sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, 0, kFpfBlock, c.nb, c.out, cr);
 #endif
                 wave_sync();
                 COVT_PHASE(c, 5);
             };
             FpfPre preB;
-            for (int32_t j = 0; j < nblocks && !c.err; j += 2) {
+            for (int32_t j = jb0; j < nblocks && !c.err; j += 2) {
                 block(j, pre, preB, 0);
                 if (j + 1 < nblocks && !c.err) block(j + 1, preB, pre, 1);
             }
             done += thissize;
             p = ie;
+            if (done >= v1) break;  // the range ends in this page
         }
         decoded = L;
         // VariableByte tail over words [p, nw)
-        if (!c.err && p < nw) {
+        if (!c.err && has_end && p < nw) {
             int32_t vpos = (int32_t)(4 * p);
             const int32_t base = L;
             Win w;
@@ -1408,14 +1446,15 @@ __device__ void run_fastpfor(Ctx& c) {
             const int32_t got = varint_take<MODE_WORDREV, VAL_VB>(
                 sm, c.sb, w, vpos, (int32_t)(4 * nw), c.n - L, true, c.err,
                 [&](const uint32_t (&lo)[1], const uint32_t (&hi)[1], int32_t vb, int32_t, int32_t count) {
-                    sink_values<OP, 1>(lo, (int64_t)base + vb, 0, count, c.nb, c.out, cr);
+                    if (sum_only) sum_values<OP, 1>(lo, (int64_t)base + vb, count, ax, ay);
+                    else sink_values<OP, 1>(lo, (int64_t)base + vb, 0, count, c.nb, c.out, cr);
                 });
             decoded = L + got;
         }
     }
     // values the codec did not produce stay 0 in Java's decompressedValues[]: transform them too
-    if (!c.err) {
-        for (int32_t b = decoded; b < c.n; b += 64) {
+    if (!c.err && has_end) {
+        for (int32_t b = decoded; !sum_only && b < c.n; b += 64) {
             uint32_t vv[1] = {0};
             sink_values<OP, 1>(vv, b, 0, c.n - b < 64 ? c.n - b : 64, c.nb, c.out, cr);
         }
@@ -1423,6 +1462,10 @@ __device__ void run_fastpfor(Ctx& c) {
     }
     COVT_PHASE(c, 6);
     c.consumed = c.byte_length;
+    if (sum_only) {
+        sums->x = lane_bcast(incl_scan(ax), 63);
+        sums->y = lane_bcast(incl_scan(ay), 63);
+    }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1444,8 +1487,11 @@ struct Agg {
     int32_t cnt;
     uint32_t sx, sy;  // wrapping sums of the transformed values (x,y ops: of local-even / local-odd values)
 };
-// a's values followed by b's: b's parity flips when a holds an odd number of values
+// a's values followed by b's: b's parity flips when a holds an odd number of values.  A record
+// with cnt < 0 is a chunk that found an error (its status in sx): the earlier one wins.
 __device__ __forceinline__ Agg agg_cat(const Agg& a, const Agg& b, bool xy) {
+    if (a.cnt < 0) return a;
+    if (b.cnt < 0) return b;
     const bool sw = xy && (a.cnt & 1);
     return Agg{a.cnt + b.cnt, a.sx + (sw ? b.sy : b.sx), a.sy + (sw ? b.sx : b.sy)};
 }
@@ -1539,54 +1585,55 @@ __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, co
             p += len;
         }
     }
-    // (2) count and sum the values ending in [s, e)
+    // (2) count and sum the values ending in [s, e); (3) + (4) publish, look back, publish the
+    // inclusive prefix; (5) decode again with the carry, values past num_values not stored.  One
+    // varint_take call site for both passes (two inlined copies doubled the kernel's registers).
     Win w;
-    w.valid = false;
-    int32_t pa = p, err = 0;
-    uint32_t ax = 0, ay = 0;
-    const int32_t cnt = varint_take<MODE_RAW, VAL_J4, 4>(
-        *c.sm, c.sb, w, pa, e, INT32_MAX, true, err,
-        [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
-            if constexpr (kSum) {
-                const int32_t s0 = 4 * l - first;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const bool ok = s0 + k >= 0 && s0 + k < count;
-                    const uint32_t z = ok ? (kZZ ? (uint32_t)zz32(lo[k]) : lo[k]) : 0u;
-                    const bool odd = kXY && (((uint32_t)(base + 4 * l + k)) & 1u);
-                    ax += odd ? 0u : z;
-                    ay += odd ? z : 0u;
-                }
-            }
-        });
-    Agg mine{cnt, 0u, 0u};
-    if constexpr (kSum) {
-        mine.sx = lane_bcast(incl_scan(ax), 63);
-        mine.sy = kXY ? lane_bcast(incl_scan(ay), 63) : 0u;
-    }
-    // (3) + (4) publish, look back, publish the inclusive prefix
-    covt_stream_result* rec = res + kSplitSlots * t;
+    int32_t err = 0, cnt = 0, take = 0, pos = p;
     Agg excl{0, 0u, 0u};
-    if (chunk == 0) {
-        rec_publish(rec + kRecIncl, mine, 2u);
-    } else {
-        rec_publish(rec + kRecAgg, mine, 1u);
-        excl = lookback(res, t, chunk, kXY, err);
-        rec_publish(rec + kRecIncl, agg_cat(excl, mine, kXY), 2u);
-    }
-    // (5) decode again with the carry; values past num_values are not stored
-    const int32_t take = min(cnt, c.n - excl.cnt);
-    int32_t pos = p;
-    if (take > 0 && !err) {
-        w.valid = false;
+#pragma nounroll
+    for (int pass = 0; pass < 2; ++pass) {
+        uint32_t ax = 0, ay = 0;
         Carry cr{excl.sx, excl.sy};
         const int32_t g0 = excl.cnt;
-        varint_take<MODE_RAW, VAL_J4, 4>(
-            *c.sm, c.sb, w, pos, e, take, false, err,
+        w.valid = false;
+        pos = p;
+        const int32_t got = varint_take<MODE_RAW, VAL_J4, 4>(
+            *c.sm, c.sb, w, pos, e, pass == 0 ? INT32_MAX : take, pass == 0, err,
             [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
-                sink_values<OP, 4>(lo, (int64_t)g0 + base, first, count, c.nb, c.out, cr);
+                if (pass == 1) {
+                    sink_values<OP, 4>(lo, (int64_t)g0 + base, first, count, c.nb, c.out, cr);
+                } else if (kSum) {
+                    const int32_t s0 = 4 * l - first;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const bool ok = s0 + k >= 0 && s0 + k < count;
+                        const uint32_t z = ok ? (kZZ ? (uint32_t)zz32(lo[k]) : lo[k]) : 0u;
+                        const bool odd = kXY && (((uint32_t)(base + 4 * l + k)) & 1u);
+                        ax += odd ? 0u : z;
+                        ay += odd ? z : 0u;
+                    }
+                }
             },
-            g0);
+            pass == 0 ? 0 : g0);
+        if (pass == 1) break;
+        cnt = got;
+        Agg mine{cnt, 0u, 0u};
+        if (kSum) {
+            mine.sx = lane_bcast(incl_scan(ax), 63);
+            mine.sy = kXY ? lane_bcast(incl_scan(ay), 63) : 0u;
+        }
+        covt_stream_result* rec = res + kSplitSlots * t;
+        if (chunk == 0) {
+            rec_publish(rec + kRecIncl, mine, 2u);
+        } else {
+            rec_publish(rec + kRecAgg, mine, 1u);
+            excl = lookback(res, t, chunk, kXY, err);
+            rec_publish(rec + kRecIncl, agg_cat(excl, mine, kXY), 2u);
+        }
+        take = min(cnt, c.n - excl.cnt);
+        pos = p;
+        if (take <= 0 || err) break;
     }
     // the stream's result, from the chunk holding its last value (or the last chunk if it is short)
     covt_stream_result* r0 = res + kSplitSlots * (t - chunk);
@@ -1600,8 +1647,52 @@ __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, co
     }
 }
 
+// One chunk [v0, v1) (values, whole 256-value blocks; the last chunk ends at num_values) of a split
+// FastPFOR stream: the same two passes as run_varint_chunk over run_fastpfor's value range (pass one
+// sums without storing, pass two stores with the carry).  Each chunk walks the page directories and
+// the block headers before its range itself, so chunks depend on each other only through the sums.
+template <int OP>
+__device__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v1, int32_t chunk, covt_stream_result* res,
+                                   int64_t t) {
+    constexpr bool kXY = OP == COVT_OP_FPF_ZZ_DELTA_XY;
+    Carry carry{0u, 0u};
+    int32_t err = 0;
+#pragma nounroll
+    for (int pass = 0; pass < 2; ++pass) {  // one inlined copy of the decoder for both passes
+        Carry sums{0u, 0u};
+        c.err = 0;
+        run_fastpfor<OP>(c, v0, v1, carry, pass == 0, &sums);
+        if (pass == 1) {
+            err = c.err;
+            break;
+        }
+        const int32_t own_err = c.err;
+        const Agg mine = own_err ? Agg{INT32_MIN, (uint32_t)own_err, 0u} : Agg{v1 - v0, sums.x, sums.y};
+        covt_stream_result* rec = res + kSplitSlots * t;
+        Agg excl{0, 0u, 0u};
+        if (chunk == 0) {
+            rec_publish(rec + kRecIncl, mine, 2u);
+        } else {
+            rec_publish(rec + kRecAgg, mine, 1u);
+            excl = lookback(res, t, chunk, kXY, err);
+            rec_publish(rec + kRecIncl, err ? Agg{INT32_MIN, (uint32_t)err, 0u} : agg_cat(excl, mine, kXY), 2u);
+        }
+        if (!err && excl.cnt < 0) err = (int32_t)excl.sx;  // an earlier chunk's error
+        if (!err) err = own_err;
+        if (err) break;
+        carry = Carry{excl.sx, excl.sy};
+    }
+    if (lane_id() == 0 && (v1 >= c.n || err)) {  // the last chunk (or an error) sets the stream's result
+        covt_stream_result r;
+        r.status = err;
+        r.consumed = c.byte_length;
+        res[kSplitSlots * (t - chunk)] = r;
+    }
+}
+
 // One split chunk per wave, chunks in ticket order (tickets from a counter in the split region's
 // result entries).
+template <bool FPF>
 __device__ void decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in, const covt_stream_desc* __restrict__ descs,
                                    int64_t n_chunks, uint8_t* __restrict__ out, covt_stream_result* __restrict__ res) {
     uint32_t* ctr = (uint32_t*)(res + kRecTicket);  // the first chunk's ticket entry
@@ -1623,6 +1714,14 @@ __device__ void decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in,
     c.err = 0;
     c.consumed = 0;
     const int32_t chunk = d.avail, s = (int32_t)rg.in_off, e = (int32_t)rg.out_off;
+    if constexpr (FPF) {
+        switch (d.op) {
+        case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor_chunk<COVT_OP_FPF_ZZ_DELTA_I32>(c, s, e, chunk, res, t); break;
+        case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor_chunk<COVT_OP_FPF_ZZ_DELTA_XY>(c, s, e, chunk, res, t); break;
+        default: run_fastpfor_chunk<COVT_OP_FPF_DELTA_MORTON>(c, s, e, chunk, res, t); break;
+        }
+        return;
+    }
     switch (d.op) {
     case COVT_OP_VARINT_I32: run_varint_chunk<COVT_OP_VARINT_I32>(c, s, e, chunk, res, t); break;
     case COVT_OP_VARINT_ZZ_I32: run_varint_chunk<COVT_OP_VARINT_ZZ_I32>(c, s, e, chunk, res, t); break;
@@ -1648,13 +1747,16 @@ __host__ __device__ constexpr int op_family(int op) {
 // when the caller's descriptors are not grouped by family).
 // Split chunks (COVT_FAMILY_SPLIT) have a kernel of their own: inside the varint family kernel their
 // code raised it from 31 to 72 VGPRs with a scratch spill (varint family alone 0.63 -> 0.88 ms).
+// (FPF: the FastPFOR chunks, COVT_FAMILY_SPLIT_FPF, their own kernel and ticket sequence for the same reason)
+template <bool FPF>
 __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const uint8_t* __restrict__ in,
                                                                            const covt_stream_desc* __restrict__ descs,
                                                                            int64_t n_chunks, uint8_t* __restrict__ out,
                                                                            covt_stream_result* __restrict__ res) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kFamSmemVarint];
+    constexpr int kStride = FPF ? kFamSmemFpf : kFamSmemVarint;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kStride];
     const int wv = uni((int)(threadIdx.x >> 6));
-    decode_split_chunk((WaveSmem*)(smem + wv * kFamSmemVarint), in, descs, n_chunks, out, res);
+    decode_split_chunk<FPF>((WaveSmem*)(smem + wv * kStride), in, descs, n_chunks, out, res);
 }
 
 template <int FAM>
@@ -1992,7 +2094,7 @@ extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt
                                         const covt_stream_desc* d_split, int64_t n_split, covt_stream_result* d_split_res,
                                         hipStream_t stream) {
     if (n_split < 0 || n_split % covt::kSplitSlots) return COVT_ERR_INVALID_ARG;
-    if (n_split && fam != COVT_FAMILY_VARINT) return COVT_ERR_INVALID_ARG;
+    if (n_split && fam != COVT_FAMILY_VARINT && fam != COVT_FAMILY_FASTPFOR) return COVT_ERR_INVALID_ARG;
     if (n_streams <= 0 && n_split == 0) return COVT_OK;
     if (n_streams < 0) n_streams = 0;
     if (fam == COVT_FAMILY_LANE) {
@@ -2007,8 +2109,12 @@ extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt
     if (n_chunks > 0) {  // the chunks first, on the same stream (the same hardware queue) as the family
         const int64_t sblocks = (n_chunks + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
         if (sblocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
-        hipLaunchKernelGGL(covt::decode_split_kernel, dim3((unsigned)sblocks), block, 0, stream, d_in, d_split,
-                           n_chunks, d_out, d_split_res);
+        if (fam == COVT_FAMILY_FASTPFOR)
+            hipLaunchKernelGGL(covt::decode_split_kernel<true>, dim3((unsigned)sblocks), block, 0, stream, d_in,
+                               d_split, n_chunks, d_out, d_split_res);
+        else
+            hipLaunchKernelGGL(covt::decode_split_kernel<false>, dim3((unsigned)sblocks), block, 0, stream, d_in,
+                               d_split, n_chunks, d_out, d_split_res);
         if (hipGetLastError() != hipSuccess) return COVT_ERR_DEVICE;
     }
     if (n_streams <= 0) return COVT_OK;

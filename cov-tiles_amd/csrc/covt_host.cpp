@@ -608,11 +608,16 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
     // fifth stream would share a queue and serialise behind another family).  A launch with a single
     // family forks nothing.  (Measured: where the lane family runs -- own stream, before or after RLE,
     // behind varint -- does not change the bench launch.)
-    const int64_t n_split = counts[COVT_FAMILY_SPLIT];
+    // split chunks run ahead of their family on its stream: varint chunks before the varint family,
+    // FastPFOR chunks before the FastPFOR family
+    auto split_of = [](int fam) {
+        return fam == COVT_FAMILY_VARINT ? COVT_FAMILY_SPLIT : fam == COVT_FAMILY_FASTPFOR ? COVT_FAMILY_SPLIT_FPF : -1;
+    };
+    auto n_split_of = [&](int fam) { return split_of(fam) < 0 ? (int64_t)0 : counts[split_of(fam)]; };
     const int order[4] = {COVT_FAMILY_FASTPFOR, COVT_FAMILY_VARINT, COVT_FAMILY_RLE, COVT_FAMILY_LANE};
     int fams[4], nf = 0;
     for (int fam : order)
-        if (counts[fam] + (fam == COVT_FAMILY_VARINT ? n_split : 0) > 0) fams[nf++] = fam;
+        if (counts[fam] + n_split_of(fam) > 0) fams[nf++] = fam;
     if (nf > 1 && hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
     int st = COVT_OK;
     int nforked = 0;
@@ -624,14 +629,16 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
             if (hipStreamWaitEvent(q, f.fork, 0) != hipSuccess) return COVT_ERR_DEVICE;
             nforked = i;
         }
-        if (fam == COVT_FAMILY_VARINT && n_split > 0) {
+        const int64_t n_split = n_split_of(fam);
+        if (n_split > 0) {
             // split chunks: look-back records and the ticket counter live in their result entries
-            covt_stream_result* sres = d_res + off[COVT_FAMILY_SPLIT];
+            const int sf = split_of(fam);
+            covt_stream_result* sres = d_res + off[sf];
             if (hipMemsetAsync(sres, 0, (size_t)n_split * sizeof(covt_stream_result), q) != hipSuccess)
                 st = COVT_ERR_DEVICE;
             if (!st)
                 st = covt_launch_family_split(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam],
-                                              d_desc + off[COVT_FAMILY_SPLIT], n_split, sres, q);
+                                              d_desc + off[sf], n_split, sres, q);
         } else {
             st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], q);
         }
@@ -698,7 +705,7 @@ struct HostShard {
     int64_t out_lo = 0, out_len = 0; // plan output bytes [out_lo, out_lo + out_len) <- d_out
     std::vector<covt_stream_desc> descs;  // launch order, offsets rebased
     std::vector<int64_t> stream;          // plan-order stream index of each descriptor
-    int64_t fam[COVT_NUM_FAMILIES] = {0, 0, 0, 0, 0};
+    int64_t fam[COVT_NUM_FAMILIES] = {0, 0, 0, 0, 0, 0};
     std::vector<covt_stream_result> res;
     hipStream_t s = nullptr;
     uint8_t *d_in = nullptr, *d_out = nullptr;
@@ -766,7 +773,7 @@ struct covt_plan {
     std::vector<covt_stream_info> info;   // tile order
     std::vector<covt_stream_desc> descs;  // launch order: grouped by family, largest first
     std::vector<int64_t> desc_stream;     // plan-order stream of each descriptor
-    int64_t fam_counts[COVT_NUM_FAMILIES] = {0, 0, 0, 0, 0};
+    int64_t fam_counts[COVT_NUM_FAMILIES] = {0, 0, 0, 0, 0, 0};
     int64_t out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
     int32_t format = COVT_FORMAT_GENC;
     std::vector<covt_geom_info> ginfo;   // geometry columns, tile order
@@ -1229,11 +1236,13 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
     if (split_min >= 0 && split_ratio > 0) split_min = std::max<int64_t>(split_min, p->in_bytes / split_ratio);
     const int32_t lane_max = (int32_t)env_i64("COVT_LANE_MAX_BYTES", kLaneMaxBytes);  // A/B knob
     const int64_t split_chunk = std::max<int64_t>(64, env_i64("COVT_SPLIT_CHUNK", COVT_SPLIT_CHUNK));
+    const int64_t split_values =
+        std::max<int64_t>(256, env_i64("COVT_SPLIT_VALUES", COVT_SPLIT_VALUES) / 256 * 256);  // FastPFOR
     for (size_t i = 0; i < ns; ++i) {
         const auto& s = p->info[i];
         const bool lane = lane_stream(s.op, s.desc_index, s.byte_length, lane_max);
-        const bool split = split_stream(s.op, s.desc_index, s.byte_length, split_min);
-        const uint64_t fam = split ? (uint64_t)COVT_FAMILY_SPLIT
+        const bool split = split_stream(s.op, s.desc_index, s.byte_length, split_min, split_values);
+        const uint64_t fam = split ? (uint64_t)(split_fpf_op(s.op) ? COVT_FAMILY_SPLIT_FPF : COVT_FAMILY_SPLIT)
                              : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);
         const uint64_t cost = std::min<uint64_t>((uint64_t)((int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4),
                                                  (1ull << 48) - 1);
@@ -1256,31 +1265,35 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         d.byte_length = si.byte_length;
         d.flags = fam == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
         si.desc_index = (int32_t)p->descs.size();
-        if (fam != COVT_FAMILY_SPLIT) {
+        if (fam != COVT_FAMILY_SPLIT && fam != COVT_FAMILY_SPLIT_FPF) {
             p->descs.push_back(d);
             p->desc_stream.push_back((int64_t)i);
             p->fam_counts[fam]++;
             continue;
         }
-        // chunk c: [c * split_chunk, min((c + 1) * split_chunk, byte_length)); COVT_SPLIT_SLOTS descriptors
-        const int64_t nch = ((int64_t)d.byte_length + split_chunk - 1) / split_chunk;
+        // chunk c: bytes [c * split_chunk, min((c + 1) * split_chunk, byte_length)) of a varint stream,
+        // values [c * split_values, min((c + 1) * split_values, num_values)) of a FastPFOR stream
+        const bool fpf = fam == COVT_FAMILY_SPLIT_FPF;
+        const uint16_t fflag = fpf ? COVT_DESC_SPLIT_FPF : 0;
+        const int64_t unit = fpf ? split_values : split_chunk, total = fpf ? d.num_values : d.byte_length;
+        const int64_t nch = (total + unit - 1) / unit;
         for (int64_t c = 0; c < nch; ++c) {
             covt_stream_desc cd = d;
-            cd.flags = COVT_DESC_SPLIT;
+            cd.flags = COVT_DESC_SPLIT | fflag;
             cd.avail = (int32_t)c;
             p->descs.push_back(cd);
             for (int q = 1; q < COVT_SPLIT_SLOTS; ++q) {
                 covt_stream_desc pd{};
-                pd.flags = COVT_DESC_SPLIT_PAD;
+                pd.flags = COVT_DESC_SPLIT_PAD | fflag;
                 if (q == 1) {
-                    pd.in_off = (uint64_t)(c * split_chunk);
-                    pd.out_off = (uint64_t)std::min<int64_t>((c + 1) * split_chunk, d.byte_length);
+                    pd.in_off = (uint64_t)(c * unit);
+                    pd.out_off = (uint64_t)std::min<int64_t>((c + 1) * unit, total);
                 }
                 p->descs.push_back(pd);
             }
             for (int q = 0; q < COVT_SPLIT_SLOTS; ++q) p->desc_stream.push_back((int64_t)i);
         }
-        p->fam_counts[COVT_FAMILY_SPLIT] += nch * COVT_SPLIT_SLOTS;
+        p->fam_counts[fam] += nch * COVT_SPLIT_SLOTS;
     }
     plan_geometry(p);
     plan_property_layout(p);
@@ -1325,7 +1338,7 @@ int covt_decode_streams_device(const uint8_t* d_in, const covt_stream_desc* d_de
     if (n_streams < 0 || (n_streams && (!d_in || !d_desc || !d_res))) return COVT_ERR_INVALID_ARG;
     if ((uintptr_t)d_in & 15) return COVT_ERR_INVALID_ARG;
     for (int f = 0; f < COVT_NUM_FAMILIES; ++f) {  // any order: each family kernel skips the others
-        if (f == COVT_FAMILY_SPLIT) continue;       // split chunks need the grouped launch
+        if (f == COVT_FAMILY_SPLIT || f == COVT_FAMILY_SPLIT_FPF) continue;  // split chunks need the grouped launch
         const int st = covt_launch_family(f, d_in, d_desc, n_streams, d_out, d_res, (hipStream_t)hip_stream);
         if (st) return st;
     }

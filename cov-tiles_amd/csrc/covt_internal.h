@@ -30,7 +30,8 @@ inline bool lane_stream(int op, int32_t num_values, int32_t byte_length, int32_t
            num_values >= 0 && num_values <= kLaneMaxValues && byte_length >= 0 && byte_length <= max_bytes;
 }
 inline int desc_family(const covt_stream_desc& d) {
-    if (d.flags & (COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD)) return COVT_FAMILY_SPLIT;
+    if (d.flags & (COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD))
+        return (d.flags & COVT_DESC_SPLIT_FPF) ? COVT_FAMILY_SPLIT_FPF : COVT_FAMILY_SPLIT;
     return (d.flags & COVT_DESC_LANE) ? COVT_FAMILY_LANE : covt_op_family_of(d.op);
 }
 // Plan rule for split streams: the Java-capped int32 varint ops (value ends are local: every byte
@@ -40,9 +41,15 @@ inline bool split_op(int op) {
            op == COVT_OP_VARINT_ZZ_DELTA_XY || op == COVT_OP_VARINT_DELTA_MORTON || op == COVT_OP_VARINT_I32_AS_I64 ||
            op == COVT_OP_VARINT_ZZ_I32_AS_I64 || op == COVT_OP_VARINT_ZZ_DELTA_I64;
 }
-inline bool split_stream(int op, int32_t num_values, int32_t byte_length, int64_t split_min) {
-    return split_min >= 0 && split_op(op) && num_values > 0 && byte_length > split_min &&
-           !(op == COVT_OP_VARINT_ZZ_DELTA_XY && (num_values & 1));
+inline bool split_fpf_op(int op) {
+    return op == COVT_OP_FPF_ZZ_DELTA_I32 || op == COVT_OP_FPF_ZZ_DELTA_XY || op == COVT_OP_FPF_DELTA_MORTON;
+}
+// FastPFOR streams split by values into chunks of whole blocks (their own headers and page directories
+// locate every block), at least two chunks
+inline bool split_stream(int op, int32_t num_values, int32_t byte_length, int64_t split_min, int64_t split_values) {
+    if (split_min < 0 || num_values <= 0 || byte_length <= split_min) return false;
+    if (split_fpf_op(op)) return num_values > split_values && !(op == COVT_OP_FPF_ZZ_DELTA_XY && (num_values & 1));
+    return split_op(op) && !(op == COVT_OP_VARINT_ZZ_DELTA_XY && (num_values & 1));
 }
 
 #endif

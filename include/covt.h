@@ -133,22 +133,26 @@ enum covt_op {
 #define COVT_FAMILY_VARINT 1   /* varint / zigzag / delta / Morton ops */
 #define COVT_FAMILY_FASTPFOR 2 /* FastPFOR + VariableByte ops */
 #define COVT_FAMILY_LANE 3     /* small RLE streams (flag COVT_DESC_LANE): one lane per stream */
-#define COVT_FAMILY_SPLIT 4    /* long streams cut into chunks decoded by separate waves (COVT_DESC_SPLIT) */
-#define COVT_NUM_FAMILIES 5
+#define COVT_FAMILY_SPLIT 4    /* long varint streams cut into chunks decoded by separate waves (COVT_DESC_SPLIT) */
+#define COVT_FAMILY_SPLIT_FPF 5 /* long FastPFOR streams cut into chunks (COVT_DESC_SPLIT | COVT_DESC_SPLIT_FPF) */
+#define COVT_NUM_FAMILIES 6
 
 /* covt_stream_desc.flags */
 #define COVT_DESC_LANE 0x1u /* decoded by the lane-per-stream kernel (set by the plan for small streams) */
-/* Long streams (plan rule: Java-capped varint ops over more than COVT_SPLIT_MIN bytes) are cut into
- * chunks of COVT_SPLIT_CHUNK bytes, each decoded by its own wave; a chunk's value index and running
+/* Long streams (plan rule: Java-capped varint and FastPFOR ops over more than COVT_SPLIT_MIN bytes) are
+ * cut into chunks of COVT_SPLIT_CHUNK bytes (varint) or COVT_SPLIT_VALUES values (FastPFOR, whole
+ * blocks), each decoded by its own wave; a chunk's value index and running
  * sums come from its predecessors by a decoupled look-back.  A chunk is COVT_SPLIT_SLOTS consecutive
  * descriptors: the chunk descriptor (flags COVT_DESC_SPLIT, avail = chunk index, the other fields those
- * of the stream) and pads (COVT_DESC_SPLIT_PAD; the first carries the chunk's stream-relative byte
- * range [in_off, out_off)), whose result entries hold the look-back records.  The stream's result is
+ * of the stream) and pads (COVT_DESC_SPLIT_PAD; the first carries the chunk's range [in_off, out_off):
+ * stream-relative bytes, or values for FastPFOR), whose result entries hold the look-back records.  The stream's result is
  * written to its chunk 0's entry.  Split descriptors need the grouped launch. */
 #define COVT_DESC_SPLIT 0x2u
 #define COVT_DESC_SPLIT_PAD 0x4u
+#define COVT_DESC_SPLIT_FPF 0x8u /* with SPLIT / SPLIT_PAD: a FastPFOR stream's chunk */
 #define COVT_SPLIT_SLOTS 8
-#define COVT_SPLIT_CHUNK 4096 /* default chunk bytes (env COVT_SPLIT_CHUNK at plan creation) */
+#define COVT_SPLIT_CHUNK 4096 /* default varint chunk bytes (env COVT_SPLIT_CHUNK at plan creation) */
+#define COVT_SPLIT_VALUES 2048 /* default FastPFOR chunk values, whole blocks (env COVT_SPLIT_VALUES) */
 #define COVT_SPLIT_MIN 8192   /* default: streams longer than this are split (env COVT_SPLIT_MIN; -1: never) */
 #define COVT_SPLIT_RATIO 3000 /* ... and longer than the plan's stream bytes / this (env COVT_SPLIT_RATIO; 0: off) */
 

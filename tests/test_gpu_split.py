@@ -21,19 +21,20 @@ DESC = np.dtype([("in_off", np.uint64), ("out_off", np.uint64), ("avail", np.int
                  ("op", np.uint8), ("num_bits", np.uint8), ("flags", np.uint16), ("byte_length", np.int32)])
 
 
-@pytest.mark.parametrize("chunk", [100, 1024])
+@pytest.mark.parametrize("chunk,values", [(100, 256), (1024, 2048)])
 @pytest.mark.parametrize("id_mode", [0, 1], ids=["id_format", "id_java"])
-def test_fixtures_forced_split(covt, gpu_available, golden_streams, monkeypatch, chunk, id_mode):
+def test_fixtures_forced_split(covt, gpu_available, golden_streams, monkeypatch, chunk, values, id_mode):
     import torch
 
     monkeypatch.setenv("COVT_SPLIT_MIN", "200")
     monkeypatch.setenv("COVT_SPLIT_RATIO", "0")
     monkeypatch.setenv("COVT_SPLIT_CHUNK", str(chunk))
+    monkeypatch.setenv("COVT_SPLIT_VALUES", str(values))
     paths = tile_paths()
     keys = [tile_key(p) for p in paths]
     tiles = [open(p, "rb").read() for p in paths]
     plan = covt.Plan.from_tiles(tiles, covt.FORMAT_GENC, id_mode)
-    assert plan.family_counts[covt.FAMILY_SPLIT] > 1000
+    assert plan.family_counts[covt.FAMILY_SPLIT] > 1000 and plan.family_counts[covt.FAMILY_SPLIT_FPF] > 100
     db = covt.DeviceBatch(plan, "cuda")
     for _ in range(2):  # the look-back records are reset per launch
         db.decode()
@@ -74,21 +75,24 @@ def _j4_count(b: bytes) -> int:
     return n
 
 
-def _split_launch(covt, buf: bytes, op: int, n: int, nb: int, chunk: int, out_bytes: int):
+def _split_launch(covt, buf: bytes, op: int, n: int, nb: int, chunk: int, out_bytes: int, fpf=False):
+    """One split stream through the grouped launch: byte chunks (varint) or value chunks (FastPFOR)."""
     import ctypes as C
 
     import torch
 
     bl = len(buf)
-    nch = (bl + chunk - 1) // chunk
+    total = n if fpf else bl
+    nch = (total + chunk - 1) // chunk
+    fl = covt.DESC_SPLIT_FPF if fpf else 0
     d = np.zeros(nch * covt.SPLIT_SLOTS, dtype=DESC)
     for c in range(nch):
         k = c * covt.SPLIT_SLOTS
-        d[k] = (0, 0, c, n, op, nb, covt.DESC_SPLIT, bl)
-        d[k + 1 : k + covt.SPLIT_SLOTS]["flags"] = covt.DESC_SPLIT_PAD
-        d[k + 1]["in_off"], d[k + 1]["out_off"] = c * chunk, min((c + 1) * chunk, bl)
+        d[k] = (0, 0, c, n, op, nb, covt.DESC_SPLIT | fl, bl)
+        d[k + 1 : k + covt.SPLIT_SLOTS]["flags"] = covt.DESC_SPLIT_PAD | fl
+        d[k + 1]["in_off"], d[k + 1]["out_off"] = c * chunk, min((c + 1) * chunk, total)
     counts = np.zeros(covt.NUM_FAMILIES, dtype=np.int64)
-    counts[covt.FAMILY_SPLIT] = d.size
+    counts[covt.FAMILY_SPLIT_FPF if fpf else covt.FAMILY_SPLIT] = d.size
     dev = torch.device("cuda")
     d_in = torch.zeros(bl + covt.INPUT_PADDING + 16, dtype=torch.uint8, device=dev)
     d_in[:bl] = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(dev) if bl else d_in[:0]
@@ -166,3 +170,52 @@ def test_adversarial_streams_split(covt, oracle, gpu_available, chunk):
                     assert np.array_equal(got, o_arr.astype(got.dtype)), (name, op, n)
                 n_checked += 1
     assert n_checked > 150
+
+
+@pytest.mark.parametrize("values", [256, 512, 4096])
+def test_fastpfor_streams_split(covt, oracle, gpu_available, values):
+    """FastPFOR streams split into chunks of whole blocks: every chunk walks the page directories and the
+    block headers before its range, sums its values in a first pass and stores them with its
+    predecessors' carry in a second (exceptions of index 1 and > 1, all bit widths, multi-page, VByte
+    tails, zero-filled and over-long value counts, corrupted payloads)."""
+    from test_gpu_synthetic import _fpf_values
+
+    rng = np.random.default_rng(values)
+    n_checked = 0
+    for n in (300, 1000, 4096 + 77, 65536, 65536 + 256 + 13, 140000):
+        raw = _fpf_values(rng, n)
+        enc = oracle.encode_fastpfor(raw)
+        buf = b"\x01\x02\x03" + enc + b"\x09" * 5
+        bl = len(enc)
+        body = buf[3:]
+        for op, nb in ((covt.OP_FPF_ZZ_DELTA_I32, 0), (covt.OP_FPF_ZZ_DELTA_XY, 0), (covt.OP_FPF_DELTA_MORTON, 14)):
+            for nv in (n, n + 10):  # numValues past the coded values: Java's zero-filled tail
+                if op == covt.OP_FPF_ZZ_DELTA_XY and nv & 1:
+                    continue
+                if op == covt.OP_FPF_ZZ_DELTA_I32:
+                    o = oracle.decode_fastpfor_zigzag_delta(body, nv, bl, 0)
+                elif op == covt.OP_FPF_ZZ_DELTA_XY:
+                    o = oracle.decode_fastpfor_delta_coordinates(body, nv, bl, 0)
+                else:
+                    o = oracle.decode_fastpfor_delta_morton_codes(body, nv, bl, 0, nb)
+                ne = 2 * nv if nb else nv
+                out, r = _split_launch(covt, body, op, nv, nb, values, 4 * ne, fpf=True)
+                assert (int(r[0]) == 0) == (o[0] == 0), (n, op, nv, int(r[0]), o[0])
+                if o[0] == 0:
+                    assert int(r[1]) == bl
+                    assert np.array_equal(out.view(np.int32), np.asarray(o[1], dtype=np.int32)), (n, op, nv)
+                n_checked += 1
+    # corrupted payloads: a status (never a fault), equal arrays whenever the oracle decodes
+    raw = _fpf_values(rng, 5000)
+    enc = oracle.encode_fastpfor(raw)
+    for _ in range(12):
+        e = bytearray(enc)
+        for _ in range(int(rng.integers(1, 4))):
+            e[int(rng.integers(0, len(e)))] ^= 1 << int(rng.integers(0, 8))
+        e = bytes(e)
+        o = oracle.decode_fastpfor_zigzag_delta(e, 5000, len(e), 0)
+        out, r = _split_launch(covt, e, covt.OP_FPF_ZZ_DELTA_I32, 5000, 0, values, 4 * 5000, fpf=True)
+        if o[0] == 0:
+            assert int(r[0]) == 0 and np.array_equal(out.view(np.int32), np.asarray(o[1], dtype=np.int32))
+        n_checked += 1
+    assert n_checked > 40

@@ -22,30 +22,40 @@ def test_split_layout(covt, monkeypatch, chunk):
     monkeypatch.setenv("COVT_SPLIT_MIN", "256")
     monkeypatch.setenv("COVT_SPLIT_RATIO", "0")
     monkeypatch.setenv("COVT_SPLIT_CHUNK", str(chunk))
+    monkeypatch.setenv("COVT_SPLIT_VALUES", "512")
     plan = covt.Plan.from_tiles([_tile(), _tile("14_8298_10748")])
     d = plan.descs.view(DESC)
     assert d.size == plan.num_descs == plan.family_counts.sum()
     fam0 = int(plan.family_counts[:covt.FAMILY_SPLIT].sum())
     sp = d[fam0:]
+    assert plan.family_counts[covt.FAMILY_SPLIT_FPF] > 0
     assert sp.size % covt.SPLIT_SLOTS == 0 and sp.size > 0
     st = plan.streams
     split_streams = set()
     for k in range(0, sp.size, covt.SPLIT_SLOTS):
         cd, rg = sp[k], sp[k + 1]
-        assert cd["flags"] == covt.DESC_SPLIT
-        assert all(sp[k + q]["flags"] == covt.DESC_SPLIT_PAD for q in range(1, covt.SPLIT_SLOTS))
+        fpf = bool(cd["flags"] & covt.DESC_SPLIT_FPF)
+        assert cd["flags"] == covt.DESC_SPLIT | (covt.DESC_SPLIT_FPF if fpf else 0)
+        assert fpf == (k >= int(plan.family_counts[covt.FAMILY_SPLIT]))  # varint chunks, then FastPFOR chunks
+        assert all(sp[k + q]["flags"] == covt.DESC_SPLIT_PAD | (cd["flags"] & covt.DESC_SPLIT_FPF)
+                   for q in range(1, covt.SPLIT_SLOTS))
         i = int(plan.desc_streams[fam0 + k])
         assert all(plan.desc_streams[fam0 + k + q] == i for q in range(covt.SPLIT_SLOTS))
         c = int(cd["avail"])
-        assert (int(rg["in_off"]), int(rg["out_off"])) == (c * chunk, min((c + 1) * chunk, int(st["byte_length"][i])))
+        if fpf:  # FastPFOR: value ranges of COVT_SPLIT_VALUES
+            assert (int(rg["in_off"]), int(rg["out_off"])) == (c * 512, min((c + 1) * 512, int(st["num_values"][i])))
+        else:
+            assert (int(rg["in_off"]), int(rg["out_off"])) == (c * chunk, min((c + 1) * chunk,
+                                                                               int(st["byte_length"][i])))
         if c == 0:
             assert st["desc_index"][i] == fam0 + k  # the stream's result entry = its chunk 0
             split_streams.add(i)
         else:
             assert int(sp[k - covt.SPLIT_SLOTS]["avail"]) == c - 1 and plan.desc_streams[fam0 + k - 1] == i
     for i in split_streams:
-        assert st["byte_length"][i] > 256 and st["op"][i] in (covt.OP_VARINT_ZZ_DELTA_I32, covt.OP_VARINT_ZZ_DELTA_XY,
-                                                              covt.OP_VARINT_DELTA_MORTON, covt.OP_VARINT_I32)
+        assert st["byte_length"][i] > 256 and st["op"][i] in (
+            covt.OP_VARINT_ZZ_DELTA_I32, covt.OP_VARINT_ZZ_DELTA_XY, covt.OP_VARINT_DELTA_MORTON, covt.OP_VARINT_I32,
+            covt.OP_FPF_ZZ_DELTA_I32, covt.OP_FPF_ZZ_DELTA_XY, covt.OP_FPF_DELTA_MORTON)
     # every stream has exactly one result entry, and non-split descriptors map 1:1
     assert len(set(st["desc_index"].tolist())) == plan.num_streams
     assert np.array_equal(plan.desc_streams[st["desc_index"]], np.arange(plan.num_streams))
