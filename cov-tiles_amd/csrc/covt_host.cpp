@@ -608,39 +608,58 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
     // fifth stream would share a queue and serialise behind another family).  A launch with a single
     // family forks nothing.  (Measured: where the lane family runs -- own stream, before or after RLE,
     // behind varint -- does not change the bench launch.)
-    // split chunks run ahead of their family on its stream: varint chunks before the varint family,
-    // FastPFOR chunks before the FastPFOR family
-    auto split_of = [](int fam) {
-        return fam == COVT_FAMILY_VARINT ? COVT_FAMILY_SPLIT : fam == COVT_FAMILY_FASTPFOR ? COVT_FAMILY_SPLIT_FPF : -1;
+    // Up to four queues (the caller's stream and three auxiliary ones), longest-running first:
+    // FastPFOR, varint, RLE, lane.  When the plan split long streams, their chunk kernels (varint,
+    // then FastPFOR) take the last queue and the lane family runs behind RLE on its queue: the chunks
+    // start at once beside the families instead of in front of one.
+    const int64_t n_sv = counts[COVT_FAMILY_SPLIT], n_sf = counts[COVT_FAMILY_SPLIT_FPF];
+    const bool splits = n_sv + n_sf > 0;
+    struct Q {
+        int fam[2];
     };
-    auto n_split_of = [&](int fam) { return split_of(fam) < 0 ? (int64_t)0 : counts[split_of(fam)]; };
-    const int order[4] = {COVT_FAMILY_FASTPFOR, COVT_FAMILY_VARINT, COVT_FAMILY_RLE, COVT_FAMILY_LANE};
-    int fams[4], nf = 0;
-    for (int fam : order)
-        if (counts[fam] + n_split_of(fam) > 0) fams[nf++] = fam;
-    if (nf > 1 && hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
+    Q qs[4];
+    int nq = 0;
+    auto add = [&](int a, int b2) {
+        const int64_t na = a < 0 ? 0 : (a == COVT_FAMILY_SPLIT ? n_sv + n_sf : counts[a]);
+        const int64_t nb = b2 < 0 ? 0 : counts[b2];
+        if (na + nb > 0) qs[nq++] = Q{{na > 0 ? a : b2, na > 0 && nb > 0 ? b2 : -1}};
+    };
+    add(COVT_FAMILY_FASTPFOR, -1);
+    add(COVT_FAMILY_VARINT, -1);
+    if (splits) {
+        add(COVT_FAMILY_RLE, COVT_FAMILY_LANE);
+        add(COVT_FAMILY_SPLIT, -1);
+    } else {
+        add(COVT_FAMILY_RLE, -1);
+        add(COVT_FAMILY_LANE, -1);
+    }
+    if (nq > 1 && hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
     int st = COVT_OK;
     int nforked = 0;
-    for (int i = 0; i < nf && !st; ++i) {
-        const int fam = fams[i];
+    for (int i = 0; i < nq && !st; ++i) {
         hipStream_t q = s;
         if (i > 0) {
             q = f.aux[i - 1];
             if (hipStreamWaitEvent(q, f.fork, 0) != hipSuccess) return COVT_ERR_DEVICE;
             nforked = i;
         }
-        const int64_t n_split = n_split_of(fam);
-        if (n_split > 0) {
-            // split chunks: look-back records and the ticket counter live in their result entries
-            const int sf = split_of(fam);
-            covt_stream_result* sres = d_res + off[sf];
-            if (hipMemsetAsync(sres, 0, (size_t)n_split * sizeof(covt_stream_result), q) != hipSuccess)
-                st = COVT_ERR_DEVICE;
-            if (!st)
-                st = covt_launch_family_split(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam],
-                                              d_desc + off[sf], n_split, sres, q);
-        } else {
-            st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], q);
+        for (int k = 0; k < 2 && !st; ++k) {
+            const int fam = qs[i].fam[k];
+            if (fam < 0) continue;
+            if (fam != COVT_FAMILY_SPLIT) {
+                st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], q);
+                continue;
+            }
+            // split chunks: look-back records and the ticket counters live in their result entries
+            for (int sf : {COVT_FAMILY_SPLIT, COVT_FAMILY_SPLIT_FPF}) {
+                if (counts[sf] <= 0 || st) continue;
+                covt_stream_result* sres = d_res + off[sf];
+                if (hipMemsetAsync(sres, 0, (size_t)counts[sf] * sizeof(covt_stream_result), q) != hipSuccess)
+                    st = COVT_ERR_DEVICE;
+                if (!st)
+                    st = covt_launch_family_split(sf == COVT_FAMILY_SPLIT ? COVT_FAMILY_VARINT : COVT_FAMILY_FASTPFOR,
+                                                  d_in, nullptr, 0, d_out, nullptr, d_desc + off[sf], counts[sf], sres, q);
+            }
         }
     }
     for (int i = 0; i < nforked; ++i) {
@@ -1227,13 +1246,22 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         uint32_t i;
     };
     std::vector<Key> keys(ns);
-    // split a stream only where one wave decoding it would outlast the launch: above COVT_SPLIT_MIN
-    // bytes and above the batch's stream bytes / COVT_SPLIT_RATIO (a wave decodes ~0.35 GB/s, the
-    // launch moves ~500 GB/s: a stream over ~1/1400 of the batch is a long pole).  Big batches are
-    // throughput-bound and split nothing; single tiles and small batches split their long streams.
+    // split a stream only where one wave decoding it would outlast the launch.  A stream's cost is its
+    // bytes + output bytes / 4 (the launch-order key below; FastPFOR and RLE time follows the values as
+    // much as the bytes): split above COVT_SPLIT_MIN and above the batch's total cost /
+    // COVT_SPLIT_RATIO (a wave decodes ~0.35 GB/s, the launch ~500 GB/s: a stream over ~1/1400 of the
+    // batch is a long pole).  Big batches are throughput-bound and split nothing; single tiles and
+    // small batches split their long streams.
+    auto stream_cost = [](const covt_stream_info& s) {
+        return (int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4;
+    };
     int64_t split_min = env_i64("COVT_SPLIT_MIN", COVT_SPLIT_MIN);
     const int64_t split_ratio = env_i64("COVT_SPLIT_RATIO", COVT_SPLIT_RATIO);
-    if (split_min >= 0 && split_ratio > 0) split_min = std::max<int64_t>(split_min, p->in_bytes / split_ratio);
+    if (split_min >= 0 && split_ratio > 0) {
+        int64_t total = 0;
+        for (const auto& si : p->info) total += stream_cost(si);
+        split_min = std::max<int64_t>(split_min, total / split_ratio);
+    }
     const int32_t lane_max = (int32_t)env_i64("COVT_LANE_MAX_BYTES", kLaneMaxBytes);  // A/B knob
     const int64_t split_chunk = std::max<int64_t>(64, env_i64("COVT_SPLIT_CHUNK", COVT_SPLIT_CHUNK));
     const int64_t split_values =
@@ -1241,11 +1269,10 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
     for (size_t i = 0; i < ns; ++i) {
         const auto& s = p->info[i];
         const bool lane = lane_stream(s.op, s.desc_index, s.byte_length, lane_max);
-        const bool split = split_stream(s.op, s.desc_index, s.byte_length, split_min, split_values);
+        const bool split = split_stream(s.op, s.desc_index, stream_cost(s), split_min, split_values);
         const uint64_t fam = split ? (uint64_t)(split_fpf_op(s.op) ? COVT_FAMILY_SPLIT_FPF : COVT_FAMILY_SPLIT)
                              : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);
-        const uint64_t cost = std::min<uint64_t>((uint64_t)((int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4),
-                                                 (1ull << 48) - 1);
+        const uint64_t cost = std::min<uint64_t>((uint64_t)stream_cost(s), (1ull << 48) - 1);
         keys[i] = Key{(fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost), (uint32_t)i};
     }
     std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) { return a.k != b.k ? a.k < b.k : a.i < b.i; });

@@ -46,8 +46,9 @@ inline bool split_fpf_op(int op) {
 }
 // FastPFOR streams split by values into chunks of whole blocks (their own headers and page directories
 // locate every block), at least two chunks
-inline bool split_stream(int op, int32_t num_values, int32_t byte_length, int64_t split_min, int64_t split_values) {
-    if (split_min < 0 || num_values <= 0 || byte_length <= split_min) return false;
+// cost: the stream's bytes + output bytes / 4 (covt_plan_create's launch-order key)
+inline bool split_stream(int op, int32_t num_values, int64_t cost, int64_t split_min, int64_t split_values) {
+    if (split_min < 0 || num_values <= 0 || cost <= split_min) return false;
     if (split_fpf_op(op)) return num_values > split_values && !(op == COVT_OP_FPF_ZZ_DELTA_XY && (num_values & 1));
     return split_op(op) && !(op == COVT_OP_VARINT_ZZ_DELTA_XY && (num_values & 1));
 }

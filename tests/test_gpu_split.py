@@ -199,7 +199,7 @@ def test_fastpfor_streams_split(covt, oracle, gpu_available, values):
                 else:
                     o = oracle.decode_fastpfor_delta_morton_codes(body, nv, bl, 0, nb)
                 ne = 2 * nv if nb else nv
-                out, r = _split_launch(covt, body, op, nv, nb, values, 4 * ne, fpf=True)
+                out, r = _split_launch(covt, body[:bl], op, nv, nb, values, 4 * ne, fpf=True)
                 assert (int(r[0]) == 0) == (o[0] == 0), (n, op, nv, int(r[0]), o[0])
                 if o[0] == 0:
                     assert int(r[1]) == bl

@@ -3,13 +3,12 @@
 
 For each config: HIP-event time of the launch, the in-kernel span (first stream start -> last stream
 end, s_memrealtime at 100 MHz), and the slowest streams -- to tell launch overhead from long poles.
-Run with COVT_SPLIT_MIN=-1 (the timing build writes timestamps into the result entries, which the
-split path uses for its look-back records)."""
+Split streams (their chunks run in the split kernels, which keep real results) are listed apart:
+only the whole-stream kernels write timestamps."""
 import os
 import sys
 
 os.environ["COVT_LIB_VARIANT"] = "libcovt_timing.so"
-os.environ.setdefault("COVT_SPLIT_MIN", "-1")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 
@@ -38,6 +37,12 @@ def main():
         ev[1].record(s)
         torch.cuda.synchronize()
         _, res, idx = sub.results()
+        st = plan.streams
+        fam0 = int(plan.family_counts[:covt.FAMILY_SPLIT].sum())
+        split = st["desc_index"][idx] >= fam0
+        print("%s: %d split streams (%s)" % (name, int(split.sum()), ", ".join(
+            "%s %d B" % (NAMES.get(int(st["op"][j]), st["op"][j]), st["byte_length"][j]) for j in idx[split][:8])))
+        res, idx = res[~split], idx[~split]
         dur = res[:, 0].astype(np.int64)
         start = res[:, 1].astype(np.int64) & 0xffffffff
         end = start + dur
