@@ -539,10 +539,12 @@ __device__ __forceinline__ void win_value(const WaveSmem& sm, int32_t sj, int32_
 // value, which is output index out0: groups are aligned so that out0 + base is a multiple of K);
 // slots [first, first + count) are values.  Returns the number of values decoded.  With `until_end`
 // (VariableByte tail) the region is decoded to its end, a trailing partial value is dropped and
-// more than `want` values is an error.
+// more than `want` values is an error.  VAL_U64_STRICT with `first_bad`: the index (from this call's
+// first value) of the first over-long value is stored there when one stops the call.
 template <int MODE, int VAL, int K = 1, class Emit>
 __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t& pos, int32_t end, int32_t want,
-                               bool until_end, int32_t& err, Emit&& emit, int32_t out0 = 0) {
+                               bool until_end, int32_t& err, Emit&& emit, int32_t out0 = 0,
+                               int32_t* first_bad = nullptr) {
     const int l = lane_id();
     int32_t got = 0;
     while (until_end ? (pos < end) : (got < want)) {
@@ -570,6 +572,7 @@ __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t&
         }
         if (take <= 0) break;
         bool lerr = false;
+        int32_t fb = INT32_MAX;  // first over-long value (VAL_U64_STRICT, first_bad)
         const int32_t s0 = pos - w.woff;
         const int32_t lead = (K > 1) ? ((out0 + got) & (K - 1)) : 0;  // slots before the first value
         for (int32_t g = -lead; g < take; g += 64 * K) {
@@ -590,14 +593,20 @@ __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t&
                     lo[k] = pext7(x & (u ^ (u - 1u)));
                     hi[k] = 0;
                 } else {
-                    win_value<VAL>(sm, sj, sm.u.v.list[r + vi], lo[k], hi[k], lerr);
+                    bool lk = false;
+                    win_value<VAL>(sm, sj, sm.u.v.list[r + vi], lo[k], hi[k], lk);
+                    if (VAL == VAL_U64_STRICT && first_bad && lk) fb = min(fb, got + vi);
+                    lerr = lerr || lk;
                 }
             }
             const int32_t first = g < 0 ? -g : 0;
             const int32_t cnt = (take - g < 64 * K ? take - g : 64 * K) - first;
             emit(lo, hi, got + g, first, cnt);
         }
-        if (VAL == VAL_U64_STRICT && __any(lerr) && !err) err = COVT_ERR_BAD_HEADER;
+        if (VAL == VAL_U64_STRICT && __any(lerr) && !err) {
+            err = COVT_ERR_BAD_HEADER;
+            if (first_bad) *first_bad = (int32_t)~wave_max(~(uint32_t)fb);
+        }
         pos = w.woff + (int32_t)uniu(sm.u.v.list[r + take - 1]) + 1;
         if (w.serial) { w.p0 = pos; w.valid = false; }  // serial lists are only valid from p0
         got += take;
@@ -643,6 +652,43 @@ __device__ __forceinline__ uint32_t rd_byte(Ctx& c, Win& w, int32_t q, int32_t n
     return uniu(win_byte(*c.sm, q - w.woff));
 }
 
+// 64-bit LEB128 values (ids; INT_64 property columns in format mode: zigzag64, + running sum `acc`,
+// carried across groups, uniform) for slots base + 4 lane .. + 3 of the group, values [first, first + count)
+template <int OP>
+__device__ __forceinline__ void sink_u64(const uint32_t (&lo)[4], const uint32_t (&hi)[4], int64_t base, int32_t first,
+                                         int32_t count, int64_t* o, uint64_t& acc) {
+    const int32_t s0 = 4 * lane_id() - first;
+    int64_t* p = o + base + 4 * lane_id();
+    uint64_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool ok = s0 + k >= 0 && s0 + k < count;
+        v[k] = ok ? (((uint64_t)hi[k] << 32) | lo[k]) : 0ull;
+        if constexpr (OP != COVT_OP_VARINT_U64) v[k] = (uint64_t)zz64(v[k]);  // zz(0) = 0
+    }
+    if constexpr (OP == COVT_OP_VARINT_ZZ_DELTA_S64) {
+        uint64_t sacc = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            sacc += v[k];
+            v[k] = sacc;
+        }
+        const uint64_t inc = incl_scan64(sacc);
+        const uint64_t pre = acc + inc - sacc;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] += pre;
+        acc += lane_bcast64(inc, 63);
+    }
+    if (s0 >= 0 && s0 + 4 <= count) {
+        st_out16((int32_t*)p, make_int4((int)v[0], (int)(v[0] >> 32), (int)v[1], (int)(v[1] >> 32)));
+        st_out16((int32_t*)(p + 2), make_int4((int)v[2], (int)(v[2] >> 32), (int)v[3], (int)(v[3] >> 32)));
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (s0 + k >= 0 && s0 + k < count) st_out(p + k, (int64_t)v[k]);
+    }
+}
+
 template <int OP>
 __device__ void run_varint_stream(Ctx& c) {
     int32_t pos = 0;
@@ -653,42 +699,11 @@ __device__ void run_varint_stream(Ctx& c) {
         sink_values<OP, 4>(lo, base, first, count, c.nb, c.out, cr);
     };
     if constexpr (OP == COVT_OP_VARINT_U64 || OP == COVT_OP_VARINT_ZZ_S64 || OP == COVT_OP_VARINT_ZZ_DELTA_S64) {
-        // 64-bit LEB128 values (ids; INT_64 property columns in format mode: zigzag64, + running sum)
-        int64_t* o = (int64_t*)c.out;
-        uint64_t acc = 0;  // running sum carried across groups (uniform)
+        uint64_t acc = 0;
         varint_take<MODE_RAW, VAL_U64_STRICT, 4>(
             *c.sm, c.sb, w, pos, c.avail, c.n, false, c.err,
             [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
-                const int32_t s0 = 4 * lane_id() - first;
-                int64_t* p = o + base + 4 * lane_id();
-                uint64_t v[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const bool ok = s0 + k >= 0 && s0 + k < count;
-                    v[k] = ok ? (((uint64_t)hi[k] << 32) | lo[k]) : 0ull;
-                    if constexpr (OP != COVT_OP_VARINT_U64) v[k] = (uint64_t)zz64(v[k]);  // zz(0) = 0
-                }
-                if constexpr (OP == COVT_OP_VARINT_ZZ_DELTA_S64) {
-                    uint64_t sacc = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        sacc += v[k];
-                        v[k] = sacc;
-                    }
-                    const uint64_t inc = incl_scan64(sacc);
-                    const uint64_t pre = acc + inc - sacc;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) v[k] += pre;
-                    acc += lane_bcast64(inc, 63);
-                }
-                if (s0 >= 0 && s0 + 4 <= count) {
-                    st_out16((int32_t*)p, make_int4((int)v[0], (int)(v[0] >> 32), (int)v[1], (int)(v[1] >> 32)));
-                    st_out16((int32_t*)(p + 2), make_int4((int)v[2], (int)(v[2] >> 32), (int)v[3], (int)(v[3] >> 32)));
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (s0 + k >= 0 && s0 + k < count) st_out(p + k, (int64_t)v[k]);
-                }
+                sink_u64<OP>(lo, hi, base, first, count, (int64_t*)c.out, acc);
             });
     } else {
         if ((OP == COVT_OP_VARINT_ZZ_DELTA_XY) && (c.n & 1)) {
@@ -1488,10 +1503,11 @@ struct Agg {
     uint32_t sx, sy;  // wrapping sums of the transformed values (x,y ops: of local-even / local-odd values)
 };
 // a's values followed by b's: b's parity flips when a holds an odd number of values.  A record
-// with cnt < 0 is a chunk that found an error (its status in sx): the earlier one wins.
+// with cnt < 0 is a chunk that found an error (its status in sx, the index of the failing value
+// relative to the record's first value in sy): the earlier one wins.
 __device__ __forceinline__ Agg agg_cat(const Agg& a, const Agg& b, bool xy) {
     if (a.cnt < 0) return a;
-    if (b.cnt < 0) return b;
+    if (b.cnt < 0) return Agg{b.cnt, b.sx, (uint32_t)a.cnt + b.sy};
     const bool sw = xy && (a.cnt & 1);
     return Agg{a.cnt + b.cnt, a.sx + (sw ? b.sy : b.sx), a.sy + (sw ? b.sx : b.sy)};
 }
@@ -1550,9 +1566,17 @@ __device__ Agg lookback(covt_stream_result* res, int64_t t, int32_t chunk, bool 
     return acc;
 }
 
-// One chunk [s, e) of a split Java-capped varint stream (ops of split_op, include/covt_internal.h).
+// One chunk [s, e) of a split varint stream (ops of split_op, include/covt_internal.h): Java's
+// 4-byte-capped int varints, or 64-bit LEB128 (ids; INT_64 zigzag columns in format mode), where a value of
+// more than 10 bytes is an error only if it is one of the first num_values (the one-wave decode reads
+// no further): a chunk that meets one counts the values before it and publishes an error record
+// carrying its index, and whichever chunk finds that index below num_values reports the status.
 template <int OP>
 __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, covt_stream_result* res, int64_t t) {
+    // (COVT_OP_VARINT_ZZ_DELTA_S64 is not split: its 64-bit running sums took this kernel from 65 to 113
+    // VGPRs with a scratch spill)
+    constexpr bool kU64 = OP == COVT_OP_VARINT_U64 || OP == COVT_OP_VARINT_ZZ_S64;
+    constexpr int kVal = kU64 ? VAL_U64_STRICT : VAL_J4;
     constexpr bool kXY = OP == COVT_OP_VARINT_ZZ_DELTA_XY;
     constexpr bool kZZ = OP == COVT_OP_VARINT_ZZ_I32 || OP == COVT_OP_VARINT_ZZ_DELTA_I32 || kXY ||
                          OP == COVT_OP_VARINT_ZZ_I32_AS_I64 || OP == COVT_OP_VARINT_ZZ_DELTA_I64;
@@ -1576,8 +1600,8 @@ __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, co
             hi = (int32_t)((intptr_t)w0 - (intptr_t)c.sb);
         }
         p = last + 1;
-        // values of 4 continuation bytes may still end before s: skip them
-        while (p < s) {
+        // Java-capped: values of 4 continuation bytes may still end before s: skip them
+        while (!kU64 && p < s) {
             const uint32_t x = uniu(ld_le32(c.sb + p));
             const uint32_t u = ~x & 0x80808080u;
             const int32_t len = u ? (__builtin_ctz(u) >> 3) + 1 : 4;
@@ -1589,20 +1613,22 @@ __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, co
     // inclusive prefix; (5) decode again with the carry, values past num_values not stored.  One
     // varint_take call site for both passes (two inlined copies doubled the kernel's registers).
     Win w;
-    int32_t err = 0, cnt = 0, take = 0, pos = p;
+    int32_t err = 0, ferr = 0, cnt = 0, take = 0, pos = p, bad = -1;
     Agg excl{0, 0u, 0u};
 #pragma nounroll
     for (int pass = 0; pass < 2; ++pass) {
         uint32_t ax = 0, ay = 0;
         Carry cr{excl.sx, excl.sy};
+        uint64_t acc = 0;  // (the split 64-bit ops carry no running sum)
         const int32_t g0 = excl.cnt;
         w.valid = false;
         pos = p;
-        const int32_t got = varint_take<MODE_RAW, VAL_J4, 4>(
+        const int32_t got = varint_take<MODE_RAW, kVal, 4>(
             *c.sm, c.sb, w, pos, e, pass == 0 ? INT32_MAX : take, pass == 0, err,
             [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
                 if (pass == 1) {
-                    sink_values<OP, 4>(lo, (int64_t)g0 + base, first, count, c.nb, c.out, cr);
+                    if constexpr (kU64) sink_u64<OP>(lo, hi, (int64_t)g0 + base, first, count, (int64_t*)c.out, acc);
+                    else sink_values<OP, 4>(lo, (int64_t)g0 + base, first, count, c.nb, c.out, cr);
                 } else if (kSum) {
                     const int32_t s0 = 4 * l - first;
 #pragma unroll
@@ -1615,30 +1641,55 @@ __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, co
                     }
                 }
             },
-            pass == 0 ? 0 : g0);
+            pass == 0 ? 0 : g0, &bad);
         if (pass == 1) break;
         cnt = got;
+        if (kU64 && err) {
+            cnt = bad;  // the values before the over-long one
+        } else if (kU64 && pos < e) {
+            // the chunk's tail without a terminator: fine if the window reached the chunk end (the value
+            // ends in a later chunk), over-long otherwise (the one-wave decode's BAD_HEADER)
+            const int32_t aligned = (int32_t)(((uintptr_t)(c.sb + pos) & ~(uintptr_t)15) - (uintptr_t)c.sb);
+            if (aligned + kWin < e) {
+                err = COVT_ERR_BAD_HEADER;
+                bad = cnt;
+            }
+        }
         Agg mine{cnt, 0u, 0u};
-        if (kSum) {
+        if (err) {
+            mine = Agg{INT32_MIN, (uint32_t)err, (uint32_t)cnt};
+        } else if (kSum) {
             mine.sx = lane_bcast(incl_scan(ax), 63);
             mine.sy = kXY ? lane_bcast(incl_scan(ay), 63) : 0u;
         }
         covt_stream_result* rec = res + kSplitSlots * t;
+        int32_t lerr = 0;
         if (chunk == 0) {
             rec_publish(rec + kRecIncl, mine, 2u);
         } else {
             rec_publish(rec + kRecAgg, mine, 1u);
-            excl = lookback(res, t, chunk, kXY, err);
-            rec_publish(rec + kRecIncl, agg_cat(excl, mine, kXY), 2u);
+            excl = lookback(res, t, chunk, kXY, lerr);
+            rec_publish(rec + kRecIncl, lerr ? Agg{INT32_MIN, (uint32_t)lerr, 0u} : agg_cat(excl, mine, kXY), 2u);
         }
+        if (lerr) {  // a predecessor never published
+            err = lerr;
+            bad = 0;
+            excl = Agg{0, 0u, 0u};
+            break;
+        }
+        if (excl.cnt < 0) return;  // an earlier chunk failed: it reports the stream if it must
+        if (err && excl.cnt + bad < c.n) ferr = err;  // else past num_values: never read
+        err = 0;
         take = min(cnt, c.n - excl.cnt);
         pos = p;
-        if (take <= 0 || err) break;
+        if (take <= 0) break;
     }
-    // the stream's result, from the chunk holding its last value (or the last chunk if it is short)
+    if (ferr) err = ferr;
+    // the stream's result, from the chunk holding its last value (or the last chunk if it is short, or
+    // the chunk that failed within the first num_values)
     covt_stream_result* r0 = res + kSplitSlots * (t - chunk);
-    const bool has_last = excl.cnt < c.n && excl.cnt + cnt >= c.n;
-    const bool short_end = e >= c.byte_length && excl.cnt + cnt < c.n;
+    const bool has_last = !err && excl.cnt < c.n && excl.cnt + cnt >= c.n;
+    const bool short_end = !err && e >= c.byte_length && excl.cnt + cnt < c.n;
     if (l == 0 && (has_last || short_end || err)) {
         covt_stream_result r;
         r.status = err ? err : (has_last ? COVT_OK : COVT_ERR_TRUNCATED);
@@ -1730,7 +1781,9 @@ __device__ void decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in,
     case COVT_OP_VARINT_DELTA_MORTON: run_varint_chunk<COVT_OP_VARINT_DELTA_MORTON>(c, s, e, chunk, res, t); break;
     case COVT_OP_VARINT_I32_AS_I64: run_varint_chunk<COVT_OP_VARINT_I32_AS_I64>(c, s, e, chunk, res, t); break;
     case COVT_OP_VARINT_ZZ_I32_AS_I64: run_varint_chunk<COVT_OP_VARINT_ZZ_I32_AS_I64>(c, s, e, chunk, res, t); break;
-    default: run_varint_chunk<COVT_OP_VARINT_ZZ_DELTA_I64>(c, s, e, chunk, res, t); break;
+    case COVT_OP_VARINT_ZZ_DELTA_I64: run_varint_chunk<COVT_OP_VARINT_ZZ_DELTA_I64>(c, s, e, chunk, res, t); break;
+    case COVT_OP_VARINT_U64: run_varint_chunk<COVT_OP_VARINT_U64>(c, s, e, chunk, res, t); break;
+    default: run_varint_chunk<COVT_OP_VARINT_ZZ_S64>(c, s, e, chunk, res, t); break;
     }
 }
 

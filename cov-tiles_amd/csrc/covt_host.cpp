@@ -1262,7 +1262,15 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         for (const auto& si : p->info) total += stream_cost(si);
         split_min = std::max<int64_t>(split_min, total / split_ratio);
     }
-    const int32_t lane_max = (int32_t)env_i64("COVT_LANE_MAX_BYTES", kLaneMaxBytes);  // A/B knob
+    int32_t lane_max = (int32_t)env_i64("COVT_LANE_MAX_BYTES", kLaneMaxBytes);  // A/B knob
+    // The lane kernel pays off only where tiny RLE streams outnumber the wave slots (it decodes 64
+    // streams per wave, each serially: a wave of 100-250-value streams takes ~80-110 us); in smaller
+    // batches every RLE stream gets a wave of its own.
+    {
+        int64_t n_lane = 0;
+        for (const auto& si : p->info) n_lane += lane_stream(si.op, si.desc_index, si.byte_length, lane_max);
+        if (n_lane < env_i64("COVT_LANE_MIN_STREAMS", kLaneMinStreams)) lane_max = -1;
+    }
     const int64_t split_chunk = std::max<int64_t>(64, env_i64("COVT_SPLIT_CHUNK", COVT_SPLIT_CHUNK));
     const int64_t split_values =
         std::max<int64_t>(256, env_i64("COVT_SPLIT_VALUES", COVT_SPLIT_VALUES) / 256 * 256);  // FastPFOR

@@ -23,6 +23,7 @@ int covt_op_family_of(int op);
 // Plan rule for the lane-per-stream kernel: RLE streams of at most kLaneMaxValues values and
 // kLaneMaxBytes bytes (a lane decodes serially; larger streams amortise a wave's window setup).
 constexpr int32_t kLaneMaxValues = 256;
+constexpr int64_t kLaneMinStreams = 16384;  // plans with fewer lane-eligible streams use no lane kernel
 constexpr int32_t kLaneMaxBytes = 64;  // the lane's first 68-byte window: no reloads (A/B: COVT_LANE_MAX_BYTES)
 inline bool lane_stream(int op, int32_t num_values, int32_t byte_length, int32_t max_bytes = kLaneMaxBytes) {
     return (op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_BYTE_RLE_RAW || op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_S64 ||
@@ -39,7 +40,8 @@ inline int desc_family(const covt_stream_desc& d) {
 inline bool split_op(int op) {
     return op == COVT_OP_VARINT_I32 || op == COVT_OP_VARINT_ZZ_I32 || op == COVT_OP_VARINT_ZZ_DELTA_I32 ||
            op == COVT_OP_VARINT_ZZ_DELTA_XY || op == COVT_OP_VARINT_DELTA_MORTON || op == COVT_OP_VARINT_I32_AS_I64 ||
-           op == COVT_OP_VARINT_ZZ_I32_AS_I64 || op == COVT_OP_VARINT_ZZ_DELTA_I64;
+           op == COVT_OP_VARINT_ZZ_I32_AS_I64 || op == COVT_OP_VARINT_ZZ_DELTA_I64 || op == COVT_OP_VARINT_U64 ||
+           op == COVT_OP_VARINT_ZZ_S64;
 }
 inline bool split_fpf_op(int op) {
     return op == COVT_OP_FPF_ZZ_DELTA_I32 || op == COVT_OP_FPF_ZZ_DELTA_XY || op == COVT_OP_FPF_DELTA_MORTON;

@@ -139,7 +139,8 @@ enum covt_op {
 
 /* covt_stream_desc.flags */
 #define COVT_DESC_LANE 0x1u /* decoded by the lane-per-stream kernel (set by the plan for small streams) */
-/* Long streams (plan rule: Java-capped varint and FastPFOR ops over more than COVT_SPLIT_MIN bytes) are
+/* Long streams (plan rule: varint ops -- Java-capped and 64-bit LEB128 -- and FastPFOR ops whose cost, bytes
+ * + output bytes / 4, exceeds COVT_SPLIT_MIN and the plan's total / COVT_SPLIT_RATIO) are
  * cut into chunks of COVT_SPLIT_CHUNK bytes (varint) or COVT_SPLIT_VALUES values (FastPFOR, whole
  * blocks), each decoded by its own wave; a chunk's value index and running
  * sums come from its predecessors by a decoupled look-back.  A chunk is COVT_SPLIT_SLOTS consecutive
@@ -151,7 +152,7 @@ enum covt_op {
 #define COVT_DESC_SPLIT_PAD 0x4u
 #define COVT_DESC_SPLIT_FPF 0x8u /* with SPLIT / SPLIT_PAD: a FastPFOR stream's chunk */
 #define COVT_SPLIT_SLOTS 8
-#define COVT_SPLIT_CHUNK 4096 /* default varint chunk bytes (env COVT_SPLIT_CHUNK at plan creation) */
+#define COVT_SPLIT_CHUNK 2048 /* default varint chunk bytes (env COVT_SPLIT_CHUNK at plan creation) */
 #define COVT_SPLIT_VALUES 2048 /* default FastPFOR chunk values, whole blocks (env COVT_SPLIT_VALUES) */
 #define COVT_SPLIT_MIN 8192   /* default: streams longer than this are split (env COVT_SPLIT_MIN; -1: never) */
 #define COVT_SPLIT_RATIO 3000 /* ... and longer than the plan's stream bytes / this (env COVT_SPLIT_RATIO; 0: off) */

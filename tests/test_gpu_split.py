@@ -6,7 +6,9 @@ edges, x/y parity, the consumed position, and the errors of short streams.
 * every stream of every fixture tile with splitting forced at small chunk sizes, both Id modes;
 * adversarial byte strings (long runs of continuation bytes, so values capped at 4 bytes end on a
   byte with bit 7 set, also right at chunk edges), exact / short (trailing bytes) / over-long
-  (truncated) value counts, every split op, chunk sizes from 16 bytes to 4 KiB.
+  (truncated) value counts, every split op, chunk sizes from 16 bytes to 4 KiB;
+* 64-bit LEB128 id streams (VARINT_U64, ZZ_S64): values up to 10 bytes, over-long (11 byte to 2 KiB)
+  values before, at and after num_values -- an error only when one of the first num_values is.
 """
 import hashlib
 
@@ -219,3 +221,44 @@ def test_fastpfor_streams_split(covt, oracle, gpu_available, values):
             assert int(r[0]) == 0 and np.array_equal(out.view(np.int32), np.asarray(o[1], dtype=np.int32))
         n_checked += 1
     assert n_checked > 40
+
+
+def _u64_count(b: bytes) -> int:
+    """Terminators (bytes with bit 7 clear) = 64-bit LEB128 values in the buffer."""
+    return int(np.count_nonzero(np.frombuffer(b, dtype=np.uint8) < 0x80))
+
+
+def _u64_streams(rng, oracle):
+    big = rng.integers(0, 1 << 63, size=6000, dtype=np.uint64) >> rng.integers(0, 63, size=6000).astype(np.uint64)
+    plain = oracle.encode_varints(big)
+    out = [("plain", plain)]
+    for bad_len in (11, 40, 1500, 2100):  # one over-long value, at three places
+        for frac in (0.02, 0.5, 0.97):
+            k = _u64_count(plain[: int(len(plain) * frac)])
+            cut = [i for i, x in enumerate(plain) if x < 0x80][k] + 1  # after value k
+            out.append(("bad%d@%.2f" % (bad_len, frac), plain[:cut] + b"\x81" * (bad_len - 1) + b"\x01" + plain[cut:]))
+    out.append(("tail_cont", plain + b"\x80" * 3000))  # trailing bytes without a terminator
+    return out
+
+
+@pytest.mark.parametrize("chunk", [16, 100, 1024, 2048])
+def test_u64_streams_split(covt, oracle, gpu_available, chunk):
+    rng = np.random.default_rng(1000 + chunk)
+    n_checked = n_err = 0
+    for name, buf in _u64_streams(rng, oracle):
+        total = _u64_count(buf)
+        for op in (covt.OP_VARINT_U64, covt.OP_VARINT_ZZ_S64):
+            for n in (total, total - 37, total // 2, total + 1, 1):
+                o_st, o_arr, o_pos = oracle.decode_varint_u64(buf, 0, n)
+                if op == covt.OP_VARINT_ZZ_S64:
+                    u = o_arr.astype(np.uint64)
+                    o_arr = ((u >> np.uint64(1)) ^ (np.uint64(0) - (u & np.uint64(1)))).view(np.int64)
+                out, r = _split_launch(covt, buf, op, n, 0, chunk, 8 * n)
+                assert (int(r[0]) == 0) == (o_st == 0), (name, op, n, int(r[0]), o_st)
+                if o_st == 0:
+                    assert int(r[1]) == o_pos, (name, op, n)
+                    assert np.array_equal(out.view(np.int64), o_arr.view(np.int64)), (name, op, n)
+                else:
+                    n_err += 1
+                n_checked += 1
+    assert n_checked > 100 and n_err > 10

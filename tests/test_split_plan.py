@@ -53,9 +53,10 @@ def test_split_layout(covt, monkeypatch, chunk):
         else:
             assert int(sp[k - covt.SPLIT_SLOTS]["avail"]) == c - 1 and plan.desc_streams[fam0 + k - 1] == i
     for i in split_streams:
-        assert st["byte_length"][i] > 256 and st["op"][i] in (
+        cost = int(st["byte_length"][i]) + int(st["out_elems"][i]) * int(st["elem_bytes"][i]) // 4
+        assert cost > 256 and st["op"][i] in (
             covt.OP_VARINT_ZZ_DELTA_I32, covt.OP_VARINT_ZZ_DELTA_XY, covt.OP_VARINT_DELTA_MORTON, covt.OP_VARINT_I32,
-            covt.OP_FPF_ZZ_DELTA_I32, covt.OP_FPF_ZZ_DELTA_XY, covt.OP_FPF_DELTA_MORTON)
+            covt.OP_VARINT_U64, covt.OP_FPF_ZZ_DELTA_I32, covt.OP_FPF_ZZ_DELTA_XY, covt.OP_FPF_DELTA_MORTON)
     # every stream has exactly one result entry, and non-split descriptors map 1:1
     assert len(set(st["desc_index"].tolist())) == plan.num_streams
     assert np.array_equal(plan.desc_streams[st["desc_index"]], np.arange(plan.num_streams))

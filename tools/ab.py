@@ -3,6 +3,7 @@
 twice to average out drift): config-5 grouped launch, each family alone, BASELINE configs 2-4.
 
   python tools/ab.py libcovt_base.so libcovt.so [...]      (files in cov-tiles_amd/)
+  python tools/ab.py libcovt.so libcovt.so:COVT_SPLIT_MIN=0 (same build, env knobs per variant)
   python tools/ab.py --one libcovt.so                        (one measurement, internal)
 """
 import json
@@ -71,8 +72,10 @@ def main():
     res = {v: [] for v in variants}
     for _ in range(2):
         for v in variants:
-            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", v], capture_output=True, text=True,
-                               timeout=600, env=dict(os.environ, COVT_LIB_VARIANT=v))
+            lib, *kv = v.split(":")  # "libcovt.so:KNOB=1:KNOB2=0" -> env knobs for that variant
+            env = dict(os.environ, COVT_LIB_VARIANT=lib, **dict(x.split("=", 1) for x in kv))
+            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", lib], capture_output=True,
+                               text=True, timeout=600, env=env)
             if p.returncode != 0:
                 print(p.stderr[-3000:])
                 sys.exit(p.returncode)
