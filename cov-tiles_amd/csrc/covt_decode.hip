@@ -972,6 +972,8 @@ __device__ void run_rle_byte(Ctx& c) {
     w.valid = false;
     int32_t pos = 0, done = 0;
     bool bad = false;
+    uint32_t cpk[4] = {0u, 0u, 0u, 0u};  // the carried partial packet (uniform) at output byte cpos
+    int32_t cpos = -1;
     while (done < c.n && !c.err) {
         if (pos >= c.avail) { c.err = COVT_ERR_TRUNCATED; break; }
         COVT_PHASE(c, 7);
@@ -981,27 +983,65 @@ __device__ void run_rle_byte(Ctx& c) {
         const int32_t vend = (c.avail - woff) < kWin ? (c.avail - woff) : kWin;
         int32_t pj = pos - woff, out = done;
         bool lbad = false, first = true;
+        // Jump tables: N1[j] = where the next group starts if a header sat at j (kWin: no group completes
+        // there; a header's length follows from its byte alone), N8 = N1 applied eight times (three
+        // in-place doublings; all reads of a round precede its writes within the wave).  Position kWin-1
+        // never completes a group (groups take >= 2 bytes), so reads clamp the sentinel to it.
+        lds_cu16* const N1 = (lds_cu16*)&sm.u.v.next[0];
+        lds_cu16* const N8 = (lds_cu16*)&sm.u.v.list[0];
+        {
+            const uint32_t dw[4] = {w.d.x, w.d.y, w.d.z, w.d.w};
+            uint32_t nx2[8];  // this lane's 16 entries, two per register
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int32_t j = 16 * l + k;
+                const int32_t cbk = (int32_t)((dw[k >> 2] >> (8 * (k & 3))) & 0xffu);
+                const int32_t e = cbk < 0x80 ? j + 2 : j + 0x101 - cbk;
+                const uint32_t v = (j < vend && e <= vend) ? (uint32_t)e : (uint32_t)kWin;
+                nx2[k >> 1] = (k & 1) ? (nx2[k >> 1] | (v << 16)) : v;
+            }
+            auto put = [&](uint16_t* t) {
+                ((uint4*)t)[2 * l] = make_uint4(nx2[0], nx2[1], nx2[2], nx2[3]);
+                ((uint4*)t)[2 * l + 1] = make_uint4(nx2[4], nx2[5], nx2[6], nx2[7]);
+            };
+            put(sm.u.v.next);
+            wave_sync();
+            lds_cu16* src = N1;
+#pragma unroll 1
+            for (int r = 0; r < 3; ++r) {  // N2 = N1 o N1, N4 = N2 o N2, N8 = N4 o N4
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t lo = src[min(nx2[k] & 0xffffu, (uint32_t)kWin - 1u)];
+                    const uint32_t hi = src[min(nx2[k] >> 16, (uint32_t)kWin - 1u)];
+                    nx2[k] = lo | (hi << 16);
+                }
+                put(sm.u.v.list);
+                wave_sync();
+                src = N8;
+            }
+        }
+        COVT_PHASE(c, 1);
         while (true) {  // 64 groups at a time (lane g of `gs` = start of group g), each batch expanded
             int32_t G = 0;
             uint32_t gs = 0;
             const int32_t out0 = out;
-            {  // branch-free steps, eight per scalar test (as in run_rle_int)
-                int32_t cur = pj;
-                bool live = pj < vend;
-                gs = ~0u;
-                for (int32_t g0 = 0; g0 < 64 && uni(live ? 1 : 0); g0 += 8) {
+            {  // lane g: g steps from pj = (g >> 3) N8 steps, then (g & 7) N1 steps (14 dependent reads)
+                uint32_t cur = (uint32_t)pj;
+                const int a = l >> 3, b = l & 7;
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int32_t cb = (int32_t)win_byte(sm, min(cur, kWin - 1));
-                        const int32_t nx = cb < 0x80 ? cur + 2 : cur + 0x101 - cb;
-                        live = live && nx <= vend;
-                        gs = (live && l == g0 + k) ? (uint32_t)cur : gs;
-                        cur = live ? nx : cur;
-                        live = live && cur < vend;
-                    }
+                for (int i = 0; i < 7; ++i) {
+                    const uint32_t t = N8[min(cur, (uint32_t)kWin - 1u)];
+                    cur = i < a ? t : cur;
                 }
-                G = __popcll(__ballot(gs != ~0u));
-                pj = uni(cur);
+#pragma unroll
+                for (int i = 0; i < 7; ++i) {
+                    const uint32_t t = N1[min(cur, (uint32_t)kWin - 1u)];
+                    cur = i < b ? t : cur;
+                }
+                const uint32_t succ = N1[min(cur, (uint32_t)kWin - 1u)];  // group g completes iff != kWin
+                G = __popcll(__ballot(succ != (uint32_t)kWin));
+                gs = l < G ? cur : ~0u;
+                pj = (int32_t)(G < 64 ? lane_bcast(cur, G) : lane_bcast(succ, 63));
             }
             COVT_PHASE(c, 2);
             if (G == 0) {
@@ -1024,53 +1064,74 @@ __device__ void run_rle_byte(Ctx& c) {
                 const uint32_t nxt = lane_bcast(gs, gl + 1 < 64 ? gl + 1 : 63);
                 pj = gl + 1 < G ? (int32_t)nxt : pj;
             }
-            // runs as in run_rle_int: one lane per run of at most 8 bytes, the wave per longer run
+            // (3) the batch's bytes [out0, outE) as aligned 16-byte packets, one per lane per step (full
+            // nontemporal stores; a run-by-run expansion wrote partial lines, ~500 clocks per run).  A
+            // packet's first group: binary search over the groups' output starts (ds_bpermute); then its
+            // bytes group by group, a run's value or literal bytes straight from the window.  The packet
+            // straddling the batch's end is carried into the next batch in registers.
             const bool isrun = cb < 0x80u;
             const uint32_t rv = win_byte(sm, pg + 1);  // a run's value
-            const bool runv = gv && isrun && take > 0;
-            lbad |= runv && rv > 5u;
-            const bool small = runv && take <= 8;
-            const int32_t tmax = (int32_t)wave_max((uint32_t)(small ? take : 0));
-            if (small) {  // uniform trip count; lanes past their end repeat the last byte
-                for (int32_t i0 = 0; i0 < tmax; ++i0) {
-                    const int32_t i = i0 < take ? i0 : take - 1;
-                    st_out(c.out + goff + i, (uint8_t)rv);
+            lbad |= gv && isrun && take > 0 && rv > 5u;
+            const int32_t outE = out < c.n ? out : c.n;
+            const int32_t gst = gv ? goff : INT32_MAX, gen = gv ? goff + take : INT32_MAX;
+            const int32_t gsrc = !gv ? 0 : (isrun ? (int32_t)(0x10000u | rv) : pg + 1);
+            const int32_t P0 = out0 & ~15;
+            for (int32_t s0 = P0; s0 < outE; s0 += 64 * 16) {
+                const int32_t P = s0 + 16 * l, qe = min(P + 16, outE);
+                int32_t q = max(P, out0);
+                int32_t gi = 0;  // the last group starting at or before q
+#pragma unroll
+                for (int st = 32; st > 0; st >>= 1) {
+                    const int32_t cand = gi + st;
+                    const int32_t v = lane_get(gst, min(cand, 63));
+                    gi = (cand < G && v <= q) ? cand : gi;
                 }
-            }
-            uint64_t bigm = __ballot(runv && take > 8);
-            while (bigm) {
-                const int src = __ffsll((long long)bigm) - 1;
-                bigm &= bigm - 1;
-                store_run<1>(c.out, (int32_t)lane_bcast((uint32_t)goff, src), (int32_t)lane_bcast((uint32_t)take, src),
-                             (int64_t)lane_bcast(rv, src), 0);
-            }
-            COVT_PHASE(c, 3);
-            // literal bytes of the batch, 64 per step across groups (the run_rle_int scheme: value u
-            // of the batch's literals is window byte u + (pg + 1 - ust) of its group)
-            const bool lv = gv && !isrun && take > 0;
-            const uint32_t lc = lv ? (uint32_t)take : 0u;
-            const uint32_t linc = incl_scan(lc);
-            const int32_t U = (int32_t)lane_bcast(linc, 63);
-            if (U > 0) {
-                const uint64_t lm = __ballot(lv), below = (1ull << l) - 1ull;
-                const int32_t nl = __popcll(lm);
-                const int32_t dst = lv ? __popcll(lm & below) : nl + __popcll(~lm & below);
-                const int32_t ust = (int32_t)(linc - lc);
-                const uint32_t pk = (uint32_t)(pg + 1 - ust + 16384) | ((uint32_t)(goff - out0 - ust) << 15);
-                const int32_t cust = __builtin_amdgcn_ds_permute(dst << 2, lv ? ust : 0x3fffffff);
-                const uint32_t cpk = (uint32_t)__builtin_amdgcn_ds_permute(dst << 2, (int32_t)pk);
-                for (int32_t u0 = 0; u0 < U; u0 += 64) {
-                    const int32_t s = cust - u0;
-                    const uint64_t mask = wave_or64(s >= 0 && s < 64 ? 1ull << s : 0ull);
-                    const int32_t gb = __popcll(__ballot(cust <= u0)) - 1;
-                    const int32_t gk = gb + __popcll(mask & ((2ull << l) - 1ull) & ~1ull);
-                    const uint32_t info = (uint32_t)lane_get((int32_t)cpk, gk);
-                    const int32_t u = u0 + l;
-                    if (u < U) {
-                        const uint32_t v = win_byte(sm, u + (int32_t)(info & 0x7fffu) - 16384);
-                        st_out(c.out + out0 + u + (int32_t)(info >> 15), (uint8_t)v);
-                        lbad |= v > 5u;
+                const bool hc = P == cpos;  // bytes before out0 come from the carried packet
+                uint32_t pk[4] = {hc ? cpk[0] : 0u, hc ? cpk[1] : 0u, hc ? cpk[2] : 0u, hc ? cpk[3] : 0u};
+                bool act = q < qe;
+                while (__any(act)) {
+                    const int32_t g = min(gi, 63);
+                    const int32_t gs = lane_get(gst, g), ge = lane_get(gen, g), src = lane_get(gsrc, g);
+                    const int32_t hi = min(ge, qe);
+                    const int32_t a = q - P, b = hi - P;  // packet bytes [a, b) from group g
+                    uint32_t x[4];
+                    const bool lit = !(src & 0x10000);
+                    if (lit) {
+                        const int32_t A = src + (P - gs);  // window byte of packet byte 0 (may be < 0: masked)
+                        const int32_t d = A >> 2;
+                        const uint32_t sh = (uint32_t)(A & 3);
+                        const uint32_t w0 = sm.u.v.win[d], w1 = sm.u.v.win[d + 1], w2 = sm.u.v.win[d + 2],
+                                       w3 = sm.u.v.win[d + 3], w4 = sm.u.v.win[d + 4];
+                        x[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                        x[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                        x[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+                        x[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+                    } else {
+                        const uint32_t r4 = ((uint32_t)src & 0xffu) * 0x01010101u;
+                        x[0] = x[1] = x[2] = x[3] = r4;
                     }
+                    if (act) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const uint32_t m = bytemask(b - 4 * k) & ~bytemask(a - 4 * k);
+                            pk[k] = (pk[k] & ~m) | (x[k] & m);
+                            const uint32_t v = x[k] & m;  // GeometryType.values()[b]: bytes > 5
+                            lbad |= lit && (((v | ((v & 0x7f7f7f7fu) + 0x7a7a7a7au)) & 0x80808080u & m) != 0u);
+                        }
+                        q = hi;
+                        ++gi;
+                    }
+                    act = q < qe;
+                }
+                if (P + 16 <= outE) {
+                    st_out16((int32_t*)(c.out + P), make_int4((int)pk[0], (int)pk[1], (int)pk[2], (int)pk[3]));
+                }
+                const uint64_t part = __ballot(P < outE && P + 16 > outE);
+                if (part) {  // the batch's last packet, partial: carried
+                    const int src = __ffsll((long long)part) - 1;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) cpk[k] = lane_bcast(pk[k], src);
+                    cpos = (int32_t)lane_bcast((uint32_t)P, src);
                 }
             }
             COVT_PHASE(c, 4);
@@ -1081,6 +1142,9 @@ __device__ void run_rle_byte(Ctx& c) {
         pos = woff + pj;
         wave_sync();
     }
+    // the last partial packet, stored whole: a stream's output slice is padded to 16 bytes
+    if (cpos >= 0 && (done & 15) && cpos == (done & ~15) && l == 0)
+        st_out16((int32_t*)(c.out + cpos), make_int4((int)cpk[0], (int)cpk[1], (int)cpk[2], (int)cpk[3]));
     if (!c.err && bad && c.op == COVT_OP_BYTE_RLE_U8) c.err = COVT_ERR_BAD_HEADER;  // GeometryType.values()[b]
     c.consumed = pos;
 }
@@ -1149,9 +1213,16 @@ __device__ __forceinline__ void sum_values(const uint32_t (&v)[K], int64_t base,
     }
 }
 // (sum_only is a run-time flag: two template copies inlined into one chunk kernel made it 248 VGPRs)
+// `skip`: a split chunk's state at its first block (header offset, packed-word offset, exception
+// cursors), filled by the first pass and reused by the second.
+struct FpfSkip {
+    int32_t done = -1;  // page start (values) the state belongs to; -1: none
+    int32_t cur0, pk;
+    int xc;  // lane k: values of dataTobePacked[k] consumed before the chunk's first block
+};
 template <int OP>
 __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Carry cr0 = Carry{0, 0},
-                             bool sum_only = false, Carry* sums = nullptr) {
+                             bool sum_only = false, Carry* sums = nullptr, FpfSkip* skip = nullptr) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
     const Words W{c.sb, c.byte_length / 4};
@@ -1314,11 +1385,33 @@ __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Car
             FpfPre pre;
             int32_t pk = (int32_t)p0 + 1;
             int32_t cur0 = 0;
-            // headers of the page's blocks before the range: walked (offsets, exception cursors) only
-            for (int32_t j = 0; j < jb0 && jb0 < nblocks && !c.err; ++j) {
-                c.err = walk(cur0, h);
-                pk = uni(pk + 8 * h.b);
-                cur0 = uni(h.next);
+            // headers of the page's blocks before the range: only their offsets, packed words and exception
+            // cursors, one LDS read per header (each block is checked by the chunk that decodes it; the
+            // container bound keeps this walk's reads in place), once per chunk
+            if (jb0 > 0 && jb0 < nblocks && !c.err) {
+                if (skip && skip->done == done) {
+                    cur0 = skip->cur0;
+                    pk = skip->pk;
+                    xc_v = skip->xc;
+                } else {
+                    int32_t cur = 0, pkk = pk;
+                    for (int32_t j = 0; j < jb0; ++j) {
+                        if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 8)) chunk_load(cur);
+                        const int32_t jj = cur - cbase;
+                        const uint32_t hw = uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(jj >> 2) + 1],
+                                                                            sm.u.f.cbuf[jj >> 2], (uint32_t)jj & 3u));
+                        const int32_t b = (int32_t)(int8_t)(hw & 0xffu);
+                        const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
+                        const int32_t idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - b;
+                        pkk += 8 * b;
+                        xc_v += (ce > 0 && idx >= 2 && idx <= 32 && l == idx) ? ce : 0;
+                        cur += ce > 0 ? 3 + ce : 2;
+                        if (cur > bclen) { c.err = COVT_ERR_BAD_HEADER; break; }
+                    }
+                    cur0 = uni(cur);
+                    pk = uni(pkk);
+                    if (skip) *skip = FpfSkip{done, cur0, pk, xc_v};
+                }
             }
             if (jb0 < nblocks && !c.err) {
                 c.err = walk(cur0, h);
@@ -1708,11 +1801,12 @@ __device__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v1, int32_t chunk
     constexpr bool kXY = OP == COVT_OP_FPF_ZZ_DELTA_XY;
     Carry carry{0u, 0u};
     int32_t err = 0;
+    FpfSkip skip;
 #pragma nounroll
     for (int pass = 0; pass < 2; ++pass) {  // one inlined copy of the decoder for both passes
         Carry sums{0u, 0u};
         c.err = 0;
-        run_fastpfor<OP>(c, v0, v1, carry, pass == 0, &sums);
+        run_fastpfor<OP>(c, v0, v1, carry, pass == 0, &sums, &skip);
         if (pass == 1) {
             err = c.err;
             break;
@@ -1744,13 +1838,13 @@ __device__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v1, int32_t chunk
 // One split chunk per wave, chunks in ticket order (tickets from a counter in the split region's
 // result entries).
 template <bool FPF>
-__device__ void decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in, const covt_stream_desc* __restrict__ descs,
-                                   int64_t n_chunks, uint8_t* __restrict__ out, covt_stream_result* __restrict__ res) {
+__device__ int64_t decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in, const covt_stream_desc* __restrict__ descs,
+                                      int64_t n_chunks, uint8_t* __restrict__ out, covt_stream_result* __restrict__ res) {
     uint32_t* ctr = (uint32_t*)(res + kRecTicket);  // the first chunk's ticket entry
     uint32_t tk = 0;
     if (lane_id() == 0) tk = atomicAdd(ctr, 1u);
     const int64_t t = (int64_t)lane_bcast(tk, 0);
-    if (t >= n_chunks) return;
+    if (t >= n_chunks) return -1;
     const covt_stream_desc d = descs[kSplitSlots * t];
     const covt_stream_desc rg = descs[kSplitSlots * t + 1];  // the chunk's byte range
     Ctx c;
@@ -1771,7 +1865,7 @@ __device__ void decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in,
         case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor_chunk<COVT_OP_FPF_ZZ_DELTA_XY>(c, s, e, chunk, res, t); break;
         default: run_fastpfor_chunk<COVT_OP_FPF_DELTA_MORTON>(c, s, e, chunk, res, t); break;
         }
-        return;
+        return t;
     }
     switch (d.op) {
     case COVT_OP_VARINT_I32: run_varint_chunk<COVT_OP_VARINT_I32>(c, s, e, chunk, res, t); break;
@@ -1785,6 +1879,7 @@ __device__ void decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in,
     case COVT_OP_VARINT_U64: run_varint_chunk<COVT_OP_VARINT_U64>(c, s, e, chunk, res, t); break;
     default: run_varint_chunk<COVT_OP_VARINT_ZZ_S64>(c, s, e, chunk, res, t); break;
     }
+    return t;
 }
 
 __host__ __device__ constexpr int op_family(int op) {
@@ -1809,11 +1904,24 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const
     constexpr int kStride = FPF ? kFamSmemFpf : kFamSmemVarint;
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kStride];
     const int wv = uni((int)(threadIdx.x >> 6));
-    decode_split_chunk<FPF>((WaveSmem*)(smem + wv * kStride), in, descs, n_chunks, out, res);
+#ifdef COVT_TIMING  // profiling build: a chunk's (duration, start) in 100 MHz ticks -> phase row of its descriptor
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int64_t t = decode_split_chunk<FPF>((WaveSmem*)(smem + wv * kStride), in, descs, n_chunks, out, res);
+#ifdef COVT_TIMING
+    if (t >= 0 && covt_phase_buf && lane_id() == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        uint32_t* row = covt_phase_buf + (descs + kSplitSlots * t - covt_phase_desc0) * kPhases;
+        row[0] = (uint32_t)(t_end - t_start);
+        row[1] = (uint32_t)t_start;
+    }
+#else
+    (void)t;
+#endif
 }
 
 template <int FAM>
-__global__ __launch_bounds__(64 * kWavesPerBlock) void decode_family_kernel(const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(7))) void decode_family_kernel(const uint8_t* __restrict__ in,
                                                             const covt_stream_desc* __restrict__ descs,
                                                             int64_t n_streams, uint8_t* __restrict__ out,
                                                             covt_stream_result* __restrict__ res) {

@@ -602,34 +602,34 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
     int64_t off[COVT_NUM_FAMILIES];
     off[0] = 0;
     for (int k = 1; k < COVT_NUM_FAMILIES; ++k) off[k] = off[k - 1] + counts[k - 1];
-    // Four launches (the varint one also carries the split chunks), longest-running first: the first
-    // with work goes on the caller's stream, the others on up to three auxiliary streams forked from
-    // and joined back into it -- four hardware queues with the caller's, HIP's default per process (a
-    // fifth stream would share a queue and serialise behind another family).  A launch with a single
-    // family forks nothing.  (Measured: where the lane family runs -- own stream, before or after RLE,
-    // behind varint -- does not change the bench launch.)
-    // Up to four queues (the caller's stream and three auxiliary ones), longest-running first:
-    // FastPFOR, varint, RLE, lane.  When the plan split long streams, their chunk kernels (varint,
-    // then FastPFOR) take the last queue and the lane family runs behind RLE on its queue: the chunks
-    // start at once beside the families instead of in front of one.
-    const int64_t n_sv = counts[COVT_FAMILY_SPLIT], n_sf = counts[COVT_FAMILY_SPLIT_FPF];
-    const bool splits = n_sv + n_sf > 0;
+    // Up to four queues: the first with work runs on the caller's stream, the others on up to three
+    // auxiliary streams forked from and joined back into it -- four hardware queues with the caller's,
+    // HIP's default per process (a fifth stream would share a queue and serialise behind another).  A
+    // launch that needs one queue forks nothing.  Without split streams: FastPFOR, varint, RLE, lane.
+    // With them: the varint chunks run ahead of the varint family on its queue (no extra fork for a
+    // varint-only launch such as BASELINE config 2), the FastPFOR chunks get a queue of their own
+    // (their waves walk a page's block headers and outlast the families), and lane shares RLE's queue
+    // (the plan makes lane streams only for large batches, which split nothing).  Each split kernel's
+    // look-back records (its result entries) are zeroed on its own queue just before it.
+    constexpr int kSplitV = COVT_FAMILY_SPLIT, kSplitF = COVT_FAMILY_SPLIT_FPF;
+    const bool splits = counts[kSplitV] + counts[kSplitF] > 0;
     struct Q {
         int fam[2];
     };
     Q qs[4];
     int nq = 0;
     auto add = [&](int a, int b2) {
-        const int64_t na = a < 0 ? 0 : (a == COVT_FAMILY_SPLIT ? n_sv + n_sf : counts[a]);
-        const int64_t nb = b2 < 0 ? 0 : counts[b2];
+        const int64_t na = a < 0 ? 0 : counts[a], nb = b2 < 0 ? 0 : counts[b2];
         if (na + nb > 0) qs[nq++] = Q{{na > 0 ? a : b2, na > 0 && nb > 0 ? b2 : -1}};
     };
-    add(COVT_FAMILY_FASTPFOR, -1);
-    add(COVT_FAMILY_VARINT, -1);
     if (splits) {
+        add(kSplitV, COVT_FAMILY_VARINT);
+        add(COVT_FAMILY_FASTPFOR, -1);
         add(COVT_FAMILY_RLE, COVT_FAMILY_LANE);
-        add(COVT_FAMILY_SPLIT, -1);
+        add(kSplitF, -1);
     } else {
+        add(COVT_FAMILY_FASTPFOR, -1);
+        add(COVT_FAMILY_VARINT, -1);
         add(COVT_FAMILY_RLE, -1);
         add(COVT_FAMILY_LANE, -1);
     }
@@ -646,20 +646,17 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
         for (int k = 0; k < 2 && !st; ++k) {
             const int fam = qs[i].fam[k];
             if (fam < 0) continue;
-            if (fam != COVT_FAMILY_SPLIT) {
+            if (fam != kSplitV && fam != kSplitF) {
                 st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], q);
                 continue;
             }
-            // split chunks: look-back records and the ticket counters live in their result entries
-            for (int sf : {COVT_FAMILY_SPLIT, COVT_FAMILY_SPLIT_FPF}) {
-                if (counts[sf] <= 0 || st) continue;
-                covt_stream_result* sres = d_res + off[sf];
-                if (hipMemsetAsync(sres, 0, (size_t)counts[sf] * sizeof(covt_stream_result), q) != hipSuccess)
-                    st = COVT_ERR_DEVICE;
-                if (!st)
-                    st = covt_launch_family_split(sf == COVT_FAMILY_SPLIT ? COVT_FAMILY_VARINT : COVT_FAMILY_FASTPFOR,
-                                                  d_in, nullptr, 0, d_out, nullptr, d_desc + off[sf], counts[sf], sres, q);
-            }
+            // split chunks: look-back records and the ticket counter live in their result entries
+            covt_stream_result* sres = d_res + off[fam];
+            if (hipMemsetAsync(sres, 0, (size_t)counts[fam] * sizeof(covt_stream_result), q) != hipSuccess)
+                st = COVT_ERR_DEVICE;
+            if (!st)
+                st = covt_launch_family_split(fam == kSplitV ? COVT_FAMILY_VARINT : COVT_FAMILY_FASTPFOR, d_in, nullptr,
+                                              0, d_out, nullptr, d_desc + off[fam], counts[fam], sres, q);
         }
     }
     for (int i = 0; i < nforked; ++i) {

@@ -4,7 +4,9 @@
 For each config: HIP-event time of the launch, the in-kernel span (first stream start -> last stream
 end, s_memrealtime at 100 MHz), and the slowest streams -- to tell launch overhead from long poles.
 Split streams (their chunks run in the split kernels, which keep real results) are listed apart:
-only the whole-stream kernels write timestamps."""
+only the whole-stream kernels write timestamps.  Phase clocks (thousands of shader clocks) per stream:
+RLE 0 window 1 next[] 2 walk 3 runs 4 literals 5 long literal 7 loop; FastPFOR as stream_timeline.py."""
+import ctypes
 import os
 import sys
 
@@ -27,7 +29,10 @@ def main():
         mask = bench.config_mask(plan, name)
         batch = covt.DeviceBatch(plan, "cuda")
         sub = batch.subset(mask)
+        sub_descs = plan.subset_descs(mask)[0].view(np.uint8)
         s = torch.cuda.current_stream()
+        phase = torch.zeros(max(sub.num_descs, 1) * 8, dtype=torch.int32, device="cuda")
+        covt.lib().covt_debug_set_phase_buffer(ctypes.c_void_p(phase.data_ptr()), ctypes.c_void_p(sub.d_desc.data_ptr()))
         for _ in range(3):
             sub.decode(s)
         torch.cuda.synchronize()
@@ -37,12 +42,18 @@ def main():
         ev[1].record(s)
         torch.cuda.synchronize()
         _, res, idx = sub.results()
+        ph = phase.cpu().numpy().view(np.uint32).reshape(-1, 8)[:sub.num_descs][sub.stream_index >= 0]
         st = plan.streams
         fam0 = int(plan.family_counts[:covt.FAMILY_SPLIT].sum())
         split = st["desc_index"][idx] >= fam0
         print("%s: %d split streams (%s)" % (name, int(split.sum()), ", ".join(
             "%s %d B" % (NAMES.get(int(st["op"][j]), st["op"][j]), st["byte_length"][j]) for j in idx[split][:8])))
-        res, idx = res[~split], idx[~split]
+        res, idx, ph = res[~split], idx[~split], ph[~split]
+        # split chunks: (duration, start) in their chunk descriptor's phase row
+        sd = sub_descs.reshape(-1, 32)
+        flags = sd[:, 26].astype(np.int64) | (sd[:, 27].astype(np.int64) << 8)
+        allph = phase.cpu().numpy().view(np.uint32).reshape(-1, 8)[:sub.num_descs]
+        chunk_rows = np.nonzero((flags & covt.DESC_SPLIT) != 0)[0]
         dur = res[:, 0].astype(np.int64)
         start = res[:, 1].astype(np.int64) & 0xffffffff
         end = start + dur
@@ -51,11 +62,27 @@ def main():
         ops = st["op"][idx]
         print("%s: %d streams, event %.1f us, in-kernel span %.1f us, last start %.1f us" % (
             name, len(idx), ev[0].elapsed_time(ev[1]) * 1e3, (end.max() - t0) * TICK_US, (start.max() - t0) * TICK_US))
+        if chunk_rows.size:
+            cdur = allph[chunk_rows, 0].astype(np.int64)
+            cst = allph[chunk_rows, 1].astype(np.int64)
+            fpf = (flags[chunk_rows] & covt.DESC_SPLIT_FPF) != 0
+            for f, fname in ((False, "SPLIT"), (True, "SPLIT_FPF")):
+                m = fpf == f
+                if not m.any():
+                    continue
+                k = np.nonzero(m)[0][np.argmax(cdur[m])]
+                row = sd[chunk_rows[k]]
+                op, nv, bl = int(row[24]), int(row[20:24].view(np.int32)[0]), int(row[28:32].view(np.int32)[0])
+                print("   family %-9s chunks=%4d first start %6.1f last start %6.1f last end %6.1f us; longest chunk "
+                      "%.1f us (start %.1f) of %s %d B %d vals" % (
+                          fname, int(m.sum()), (cst[m].min() - t0) * TICK_US, (cst[m].max() - t0) * TICK_US,
+                          (cst[m] + cdur[m] - t0).max() * TICK_US, cdur[k] * TICK_US, (cst[k] - t0) * TICK_US,
+                          NAMES.get(op, op), bl, nv))
         for i in np.argsort(-end)[:6]:
             j = idx[i]
             print("   %-12s bytes %7d values %7d  start %7.1f us  dur %7.1f us" % (
                 NAMES.get(int(ops[i]), ops[i]), st["byte_length"][j], st["num_values"][j], (start[i] - t0) * TICK_US,
-                dur[i] * TICK_US))
+                dur[i] * TICK_US) + "  phase kclk " + " ".join("%d" % (x // 1000) for x in ph[i]))
         fl = plan.descs.reshape(-1, 32)[st["desc_index"][idx], 26]
         fam = np.where(fl & 1, 3, np.where(np.isin(ops, (10, 11, 12)), 2,
                                            np.where(np.isin(ops, (1, 2, 3, 4, 16)), 0, 1)))
