@@ -36,9 +36,10 @@ ERR_DEVICE = -5
 ERR_INVALID_ARG = -6
 INPUT_PADDING = 4096
 FORMAT_GENC, FORMAT_GEND = 0, 1
-FAMILY_RLE, FAMILY_VARINT, FAMILY_FASTPFOR, FAMILY_LANE, FAMILY_SPLIT, FAMILY_SPLIT_FPF = 0, 1, 2, 3, 4, 5
-NUM_FAMILIES = 6
+FAMILY_RLE, FAMILY_VARINT, FAMILY_FASTPFOR, FAMILY_LANE, FAMILY_SPLIT, FAMILY_SPLIT_FPF, FAMILY_SPLIT_RLE = range(7)
+NUM_FAMILIES = 7
 DESC_LANE, DESC_SPLIT, DESC_SPLIT_PAD, DESC_SPLIT_FPF = 0x1, 0x2, 0x4, 0x8
+DESC_SPLIT_RLE = 0x10
 SPLIT_SLOTS = 8
 ID_FORMAT, ID_JAVA = 0, 1
 

@@ -755,14 +755,16 @@ __device__ __forceinline__ uint32_t win_vulong_lo32(const WaveSmem& sm, int32_t 
 // (256-c)-th varint from j+1) -- fully lane-parallel; (2) one wave-uniform walk follows that chain
 // (one LDS read per group) and records the group starts; (3) groups expand lane-parallel: small
 // groups one per lane, groups of more than 8 values with the whole wave.
-__device__ void run_rle_int(Ctx& c) {
+// o0: output index of the first value (a split chunk of a stream: its stream bytes start at c.sb, its
+// values are [o0, c.n) of the stream's output at c.out)
+__device__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
     const bool is_signed = c.op == COVT_OP_RLE_S64;
     const bool to_i32 = c.op == COVT_OP_RLE_I32;
     Win w;
     w.valid = false;
-    int32_t pos = 0, done = 0;
+    int32_t pos = 0, done = o0;
     auto store = [&](int64_t i, uint64_t raw) {
         const int64_t v = is_signed ? zz64(raw) : (int64_t)raw;
         if (to_i32) st_out((int32_t*)c.out + i, (int32_t)v);
@@ -844,7 +846,8 @@ __device__ void run_rle_int(Ctx& c) {
                 // the group at pos does not complete inside this window
                 const uint32_t cb = uniu(win_byte(sm, jlo));
                 const int32_t aligned = (int32_t)(((uintptr_t)(c.sb + pos) & ~(uintptr_t)15) - (uintptr_t)c.sb);
-                if (cb >= 0x80u && woff == aligned && woff + kWin < c.avail) {
+                // (<=: a literal ending exactly at the window end has next[] = next[kWin], the sentinel)
+                if (cb >= 0x80u && woff == aligned && woff + kWin <= c.avail) {
                     // a literal group longer than a window (up to 128 x 10 B): multi-window varint path
                     const int32_t cnt = 0x100 - (int32_t)cb, lim = c.n - done, d0 = done;
                     int32_t p1 = pos + 1;
@@ -962,15 +965,24 @@ __device__ void run_rle_int(Ctx& c) {
     c.consumed = pos;
 }
 
+// bytes [a, b) of a 16-byte packet (per lane; a split chunk's edge packets)
+__device__ __forceinline__ void store_packet_bytes(uint8_t* dst, const uint32_t (&pk)[4], int32_t a, int32_t b) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k >= a && k < b) st_out(dst + k, (uint8_t)(pk[k >> 2] >> (8 * (k & 3))));
+}
+
 // ORC RLE v1 byte reader (RunLengthByteReader); GeometryType.values()[b] range-checked for
 // COVT_OP_BYTE_RLE_U8 (present / boolean bitsets: COVT_OP_BYTE_RLE_RAW, no check).
 // Same window structure as run_rle_int; a byte-RLE group's length follows from its header byte.
-__device__ void run_rle_byte(Ctx& c) {
+// o0 as in run_rle_int; `exact`: bytes outside [o0, c.n) are never written (a split chunk shares its
+// first and last 16-byte packets with its neighbours)
+__device__ void run_rle_byte(Ctx& c, int32_t o0 = 0, bool exact = false) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
     Win w;
     w.valid = false;
-    int32_t pos = 0, done = 0;
+    int32_t pos = 0, done = o0;
     bool bad = false;
     uint32_t cpk[4] = {0u, 0u, 0u, 0u};  // the carried partial packet (uniform) at output byte cpos
     int32_t cpos = -1;
@@ -1124,7 +1136,8 @@ __device__ void run_rle_byte(Ctx& c) {
                     act = q < qe;
                 }
                 if (P + 16 <= outE) {
-                    st_out16((int32_t*)(c.out + P), make_int4((int)pk[0], (int)pk[1], (int)pk[2], (int)pk[3]));
+                    if (P >= o0) st_out16((int32_t*)(c.out + P), make_int4((int)pk[0], (int)pk[1], (int)pk[2], (int)pk[3]));
+                    else store_packet_bytes(c.out + P, pk, o0 - P, 16);  // a chunk's first packet
                 }
                 const uint64_t part = __ballot(P < outE && P + 16 > outE);
                 if (part) {  // the batch's last packet, partial: carried
@@ -1142,9 +1155,12 @@ __device__ void run_rle_byte(Ctx& c) {
         pos = woff + pj;
         wave_sync();
     }
-    // the last partial packet, stored whole: a stream's output slice is padded to 16 bytes
-    if (cpos >= 0 && (done & 15) && cpos == (done & ~15) && l == 0)
-        st_out16((int32_t*)(c.out + cpos), make_int4((int)cpk[0], (int)cpk[1], (int)cpk[2], (int)cpk[3]));
+    // the last partial packet, stored whole (a stream's output slice is padded to 16 bytes) or, for a
+    // chunk, byte by byte
+    if (cpos >= 0 && (done & 15) && cpos == (done & ~15) && l == 0) {
+        if (exact) store_packet_bytes(c.out + cpos, cpk, max(o0 - cpos, 0), done - cpos);
+        else st_out16((int32_t*)(c.out + cpos), make_int4((int)cpk[0], (int)cpk[1], (int)cpk[2], (int)cpk[3]));
+    }
     if (!c.err && bad && c.op == COVT_OP_BYTE_RLE_U8) c.err = COVT_ERR_BAD_HEADER;  // GeometryType.values()[b]
     c.consumed = pos;
 }
@@ -1835,11 +1851,35 @@ __device__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v1, int32_t chunk
     }
 }
 
+// One chunk of a split ORC RLE stream: whole groups, located by the plan's host walk (pads: [1] the
+// chunk's bytes [s, e), [2] its values [v0, v0 + nv), [3] the stream's consumed bytes).  Groups carry
+// no state across, so a chunk needs no look-back: it decodes like a stream of its own into its slice
+// of the stream's output.  The stream's result entry (zeroed before the launch) takes the first chunk's
+// consumed count and the lowest failing status (the plan splits only streams whose group structure it
+// walked: what remains is the GeometryType range check, BAD_HEADER from any chunk).
+__device__ void run_rle_chunk(Ctx& c, const covt_stream_desc* __restrict__ cd, int32_t chunk, covt_stream_result* res,
+                              int64_t t) {
+    const int32_t s = (int32_t)cd[1].in_off, e = (int32_t)cd[1].out_off;
+    const int32_t v0 = (int32_t)cd[2].in_off, nv = (int32_t)cd[2].out_off;
+    c.sb += s;
+    c.avail = c.byte_length = e - s;
+    c.n = v0 + nv;
+    if (c.op == COVT_OP_BYTE_RLE_U8 || c.op == COVT_OP_BYTE_RLE_RAW) run_rle_byte(c, v0, true);
+    else run_rle_int(c, v0);
+    if (lane_id() == 0) {
+        covt_stream_result* r0 = res + kSplitSlots * (t - chunk);
+        if (c.err) atomicMin(&r0->status, c.err);
+        if (chunk == 0) r0->consumed = (int32_t)cd[3].in_off;
+    }
+}
+
 // One split chunk per wave, chunks in ticket order (tickets from a counter in the split region's
-// result entries).
-template <bool FPF>
+// result entries).  K: kSplitVarint, kSplitFpf, kSplitRle (COVT_FAMILY_SPLIT, _SPLIT_FPF, _SPLIT_RLE).
+constexpr int kSplitVarint = 0, kSplitFpf = 1, kSplitRle = 2;
+template <int K>
 __device__ int64_t decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in, const covt_stream_desc* __restrict__ descs,
                                       int64_t n_chunks, uint8_t* __restrict__ out, covt_stream_result* __restrict__ res) {
+    constexpr bool FPF = K == kSplitFpf;
     uint32_t* ctr = (uint32_t*)(res + kRecTicket);  // the first chunk's ticket entry
     uint32_t tk = 0;
     if (lane_id() == 0) tk = atomicAdd(ctr, 1u);
@@ -1859,6 +1899,10 @@ __device__ int64_t decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ 
     c.err = 0;
     c.consumed = 0;
     const int32_t chunk = d.avail, s = (int32_t)rg.in_off, e = (int32_t)rg.out_off;
+    if constexpr (K == kSplitRle) {
+        run_rle_chunk(c, descs + kSplitSlots * t, chunk, res, t);
+        return t;
+    }
     if constexpr (FPF) {
         switch (d.op) {
         case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor_chunk<COVT_OP_FPF_ZZ_DELTA_I32>(c, s, e, chunk, res, t); break;
@@ -1896,18 +1940,18 @@ __host__ __device__ constexpr int op_family(int op) {
 // Split chunks (COVT_FAMILY_SPLIT) have a kernel of their own: inside the varint family kernel their
 // code raised it from 31 to 72 VGPRs with a scratch spill (varint family alone 0.63 -> 0.88 ms).
 // (FPF: the FastPFOR chunks, COVT_FAMILY_SPLIT_FPF, their own kernel and ticket sequence for the same reason)
-template <bool FPF>
+template <int K>
 __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const uint8_t* __restrict__ in,
                                                                            const covt_stream_desc* __restrict__ descs,
                                                                            int64_t n_chunks, uint8_t* __restrict__ out,
                                                                            covt_stream_result* __restrict__ res) {
-    constexpr int kStride = FPF ? kFamSmemFpf : kFamSmemVarint;
+    constexpr int kStride = K == kSplitFpf ? kFamSmemFpf : K == kSplitRle ? kFamSmemRle : kFamSmemVarint;
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kStride];
     const int wv = uni((int)(threadIdx.x >> 6));
 #ifdef COVT_TIMING  // profiling build: a chunk's (duration, start) in 100 MHz ticks -> phase row of its descriptor
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int64_t t = decode_split_chunk<FPF>((WaveSmem*)(smem + wv * kStride), in, descs, n_chunks, out, res);
+    const int64_t t = decode_split_chunk<K>((WaveSmem*)(smem + wv * kStride), in, descs, n_chunks, out, res);
 #ifdef COVT_TIMING
     if (t >= 0 && covt_phase_buf && lane_id() == 0) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
@@ -2255,7 +2299,8 @@ extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt
                                         const covt_stream_desc* d_split, int64_t n_split, covt_stream_result* d_split_res,
                                         hipStream_t stream) {
     if (n_split < 0 || n_split % covt::kSplitSlots) return COVT_ERR_INVALID_ARG;
-    if (n_split && fam != COVT_FAMILY_VARINT && fam != COVT_FAMILY_FASTPFOR) return COVT_ERR_INVALID_ARG;
+    if (n_split && fam != COVT_FAMILY_VARINT && fam != COVT_FAMILY_FASTPFOR && fam != COVT_FAMILY_RLE)
+        return COVT_ERR_INVALID_ARG;
     if (n_streams <= 0 && n_split == 0) return COVT_OK;
     if (n_streams < 0) n_streams = 0;
     if (fam == COVT_FAMILY_LANE) {
@@ -2271,11 +2316,14 @@ extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt
         const int64_t sblocks = (n_chunks + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
         if (sblocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
         if (fam == COVT_FAMILY_FASTPFOR)
-            hipLaunchKernelGGL(covt::decode_split_kernel<true>, dim3((unsigned)sblocks), block, 0, stream, d_in,
-                               d_split, n_chunks, d_out, d_split_res);
+            hipLaunchKernelGGL(covt::decode_split_kernel<covt::kSplitFpf>, dim3((unsigned)sblocks), block, 0, stream,
+                               d_in, d_split, n_chunks, d_out, d_split_res);
+        else if (fam == COVT_FAMILY_RLE)
+            hipLaunchKernelGGL(covt::decode_split_kernel<covt::kSplitRle>, dim3((unsigned)sblocks), block, 0, stream,
+                               d_in, d_split, n_chunks, d_out, d_split_res);
         else
-            hipLaunchKernelGGL(covt::decode_split_kernel<false>, dim3((unsigned)sblocks), block, 0, stream, d_in,
-                               d_split, n_chunks, d_out, d_split_res);
+            hipLaunchKernelGGL(covt::decode_split_kernel<covt::kSplitVarint>, dim3((unsigned)sblocks), block, 0,
+                               stream, d_in, d_split, n_chunks, d_out, d_split_res);
         if (hipGetLastError() != hipSuccess) return COVT_ERR_DEVICE;
     }
     if (n_streams <= 0) return COVT_OK;

@@ -15,6 +15,7 @@
 #include <mutex>
 #include <numeric>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "covt.h"
@@ -606,32 +607,39 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
     // auxiliary streams forked from and joined back into it -- four hardware queues with the caller's,
     // HIP's default per process (a fifth stream would share a queue and serialise behind another).  A
     // launch that needs one queue forks nothing.  Without split streams: FastPFOR, varint, RLE, lane.
-    // With them: the varint chunks run ahead of the varint family on its queue (no extra fork for a
-    // varint-only launch such as BASELINE config 2), the FastPFOR chunks get a queue of their own
-    // (their waves walk a page's block headers and outlast the families), and lane shares RLE's queue
-    // (the plan makes lane streams only for large batches, which split nothing).  Each split kernel's
-    // look-back records (its result entries) are zeroed on its own queue just before it.
-    constexpr int kSplitV = COVT_FAMILY_SPLIT, kSplitF = COVT_FAMILY_SPLIT_FPF;
-    const bool splits = counts[kSplitV] + counts[kSplitF] > 0;
+    // With them: varint chunks ahead of the varint family (no extra fork for a varint-only launch such
+    // as BASELINE config 2), RLE chunks ahead of the RLE family (and lane, which the plan makes only for
+    // large batches that split nothing), and the FastPFOR chunks on a queue of their own (their waves
+    // walk a page's block headers and outlast the families).  The split regions' look-back records and
+    // ticket counters (their result entries) are zeroed on the caller's stream before the fork.
+    constexpr int kSplitV = COVT_FAMILY_SPLIT, kSplitF = COVT_FAMILY_SPLIT_FPF, kSplitR = COVT_FAMILY_SPLIT_RLE;
+    const int64_t n_split = counts[kSplitV] + counts[kSplitF] + counts[kSplitR];  // contiguous regions
+    const bool splits = n_split > 0;
+    auto n_of = [&](int fam) { return fam < 0 ? 0 : counts[fam]; };
     struct Q {
-        int fam[2];
+        int fam[3];
     };
     Q qs[4];
     int nq = 0;
-    auto add = [&](int a, int b2) {
-        const int64_t na = a < 0 ? 0 : counts[a], nb = b2 < 0 ? 0 : counts[b2];
-        if (na + nb > 0) qs[nq++] = Q{{na > 0 ? a : b2, na > 0 && nb > 0 ? b2 : -1}};
+    auto add = [&](int a, int b2, int c3) {
+        Q q{{-1, -1, -1}};
+        int k = 0;
+        for (int f : {a, b2, c3})
+            if (n_of(f) > 0) q.fam[k++] = f;
+        if (k) qs[nq++] = q;
     };
     if (splits) {
-        add(kSplitV, COVT_FAMILY_VARINT);
-        add(COVT_FAMILY_FASTPFOR, -1);
-        add(COVT_FAMILY_RLE, COVT_FAMILY_LANE);
-        add(kSplitF, -1);
+        if (hipMemsetAsync(d_res + off[kSplitV], 0, (size_t)n_split * sizeof(covt_stream_result), s) != hipSuccess)
+            return COVT_ERR_DEVICE;
+        add(kSplitV, COVT_FAMILY_VARINT, -1);
+        add(COVT_FAMILY_FASTPFOR, -1, -1);
+        add(kSplitR, COVT_FAMILY_RLE, COVT_FAMILY_LANE);
+        add(kSplitF, -1, -1);
     } else {
-        add(COVT_FAMILY_FASTPFOR, -1);
-        add(COVT_FAMILY_VARINT, -1);
-        add(COVT_FAMILY_RLE, -1);
-        add(COVT_FAMILY_LANE, -1);
+        add(COVT_FAMILY_FASTPFOR, -1, -1);
+        add(COVT_FAMILY_VARINT, -1, -1);
+        add(COVT_FAMILY_RLE, -1, -1);
+        add(COVT_FAMILY_LANE, -1, -1);
     }
     if (nq > 1 && hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
     int st = COVT_OK;
@@ -643,20 +651,16 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
             if (hipStreamWaitEvent(q, f.fork, 0) != hipSuccess) return COVT_ERR_DEVICE;
             nforked = i;
         }
-        for (int k = 0; k < 2 && !st; ++k) {
+        for (int k = 0; k < 3 && !st; ++k) {
             const int fam = qs[i].fam[k];
             if (fam < 0) continue;
-            if (fam != kSplitV && fam != kSplitF) {
+            if (fam != kSplitV && fam != kSplitF && fam != kSplitR) {
                 st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], q);
                 continue;
             }
-            // split chunks: look-back records and the ticket counter live in their result entries
-            covt_stream_result* sres = d_res + off[fam];
-            if (hipMemsetAsync(sres, 0, (size_t)counts[fam] * sizeof(covt_stream_result), q) != hipSuccess)
-                st = COVT_ERR_DEVICE;
-            if (!st)
-                st = covt_launch_family_split(fam == kSplitV ? COVT_FAMILY_VARINT : COVT_FAMILY_FASTPFOR, d_in, nullptr,
-                                              0, d_out, nullptr, d_desc + off[fam], counts[fam], sres, q);
+            const int kind = fam == kSplitV ? COVT_FAMILY_VARINT : fam == kSplitR ? COVT_FAMILY_RLE : COVT_FAMILY_FASTPFOR;
+            st = covt_launch_family_split(kind, d_in, nullptr, 0, d_out, nullptr, d_desc + off[fam], counts[fam],
+                                          d_res + off[fam], q);
         }
     }
     for (int i = 0; i < nforked; ++i) {
@@ -721,7 +725,7 @@ struct HostShard {
     int64_t out_lo = 0, out_len = 0; // plan output bytes [out_lo, out_lo + out_len) <- d_out
     std::vector<covt_stream_desc> descs;  // launch order, offsets rebased
     std::vector<int64_t> stream;          // plan-order stream index of each descriptor
-    int64_t fam[COVT_NUM_FAMILIES] = {0, 0, 0, 0, 0, 0};
+    int64_t fam[COVT_NUM_FAMILIES] = {};
     std::vector<covt_stream_result> res;
     hipStream_t s = nullptr;
     uint8_t *d_in = nullptr, *d_out = nullptr;
@@ -789,7 +793,7 @@ struct covt_plan {
     std::vector<covt_stream_info> info;   // tile order
     std::vector<covt_stream_desc> descs;  // launch order: grouped by family, largest first
     std::vector<int64_t> desc_stream;     // plan-order stream of each descriptor
-    int64_t fam_counts[COVT_NUM_FAMILIES] = {0, 0, 0, 0, 0, 0};
+    int64_t fam_counts[COVT_NUM_FAMILIES] = {};
     int64_t out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
     int32_t format = COVT_FORMAT_GENC;
     std::vector<covt_geom_info> ginfo;   // geometry columns, tile order
@@ -1146,6 +1150,64 @@ int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const u
     return covt_plan_create_ex(bytes, tile_offsets, tile_sizes, n_tiles, format, id_mode, 0u, out);
 }
 
+namespace {
+// Chunks of a long ORC RLE v1 stream for the split kernel: a host walk of its group headers (orc-core
+// RunLengthIntegerReader / RunLengthByteReader framing: run = header, [delta,] base varint or byte;
+// literal = header + 256 - h varints or bytes) cut at group starts every `unit` of cost (bytes +
+// output bytes / 4).  Each chunk: {first byte, end byte, first value, values}; `consumed` = the bytes
+// the one-wave decode reads (through the group that reaches num_values).  Empty when the stream does
+// not frame num_values values in byte_length bytes: its one-wave decode then reports the error.
+struct RleChunk {
+    int32_t s, e, v0, nv;
+};
+std::vector<RleChunk> rle_chunks(const uint8_t* b, int32_t len, int op, int32_t n, int32_t elem, int64_t unit,
+                                 int32_t& consumed) {
+    const bool byte_rle = op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_BYTE_RLE_RAW;
+    std::vector<RleChunk> ch;
+    int32_t pos = 0, v = 0, cs = 0, cv = 0;
+    auto varint = [&]() {
+        do {
+            if (pos >= len) return false;
+        } while (b[pos++] & 0x80);
+        return true;
+    };
+    while (v < n) {
+        if (pos >= len) return {};
+        if ((int64_t)(pos - cs) + (int64_t)(v - cv) * elem / 4 >= unit) {  // cut before this group
+            ch.push_back(RleChunk{cs, pos, cv, v - cv});
+            cs = pos;
+            cv = v;
+        }
+        const uint8_t h = b[pos];
+        if (h < 0x80) {
+            if (byte_rle) {
+                if (pos + 2 > len) return {};
+                pos += 2;
+            } else {
+                pos += 2;
+                if (pos > len || !varint()) return {};
+            }
+            v += h + 3;
+        } else {
+            const int32_t cnt = 256 - h;
+            ++pos;
+            if (byte_rle) {
+                if (pos + cnt > len) return {};
+                pos += cnt;
+            } else {
+                for (int32_t k = 0; k < cnt; ++k)
+                    if (!varint()) return {};
+            }
+            v += cnt;
+        }
+    }
+    ch.push_back(RleChunk{cs, pos, cv, n - cv});
+    consumed = pos;
+    if (ch.size() < 2) ch.clear();
+    return ch;
+}
+}  // namespace
+
 int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
                         int32_t n_tiles, int32_t format, int32_t id_mode, uint32_t flags, covt_plan** out) {
     if (!out || n_tiles < 0 || (n_tiles && (!bytes || !tile_offsets || !tile_sizes))) return COVT_ERR_INVALID_ARG;
@@ -1271,11 +1333,26 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
     const int64_t split_chunk = std::max<int64_t>(64, env_i64("COVT_SPLIT_CHUNK", COVT_SPLIT_CHUNK));
     const int64_t split_values =
         std::max<int64_t>(256, env_i64("COVT_SPLIT_VALUES", COVT_SPLIT_VALUES) / 256 * 256);  // FastPFOR
+    // long RLE streams: chunk boundaries from the host walk (stream index -> chunks, consumed)
+    std::unordered_map<size_t, std::pair<std::vector<RleChunk>, int32_t>> rle_split;
+    if (split_min >= 0) {
+        for (size_t i = 0; i < ns; ++i) {
+            const auto& s = p->info[i];
+            if (!split_rle_op(s.op) || stream_cost(s) <= split_min || s.desc_index <= 0) continue;
+            int32_t consumed = 0;
+            auto ch = rle_chunks(bytes + s.in_off, s.byte_length, s.op, s.desc_index, s.elem_bytes, split_chunk,
+                                 consumed);
+            if (!ch.empty()) rle_split.emplace(i, std::make_pair(std::move(ch), consumed));
+        }
+    }
     for (size_t i = 0; i < ns; ++i) {
         const auto& s = p->info[i];
         const bool lane = lane_stream(s.op, s.desc_index, s.byte_length, lane_max);
-        const bool split = split_stream(s.op, s.desc_index, stream_cost(s), split_min, split_values);
-        const uint64_t fam = split ? (uint64_t)(split_fpf_op(s.op) ? COVT_FAMILY_SPLIT_FPF : COVT_FAMILY_SPLIT)
+        const bool split = split_stream(s.op, s.desc_index, stream_cost(s), split_min, split_values) ||
+                           rle_split.count(i);
+        const uint64_t fam = split ? (uint64_t)(split_fpf_op(s.op)   ? COVT_FAMILY_SPLIT_FPF
+                                                : rle_split.count(i) ? COVT_FAMILY_SPLIT_RLE
+                                                                     : COVT_FAMILY_SPLIT)
                              : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);
         const uint64_t cost = std::min<uint64_t>((uint64_t)stream_cost(s), (1ull << 48) - 1);
         keys[i] = Key{(fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost), (uint32_t)i};
@@ -1297,10 +1374,32 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         d.byte_length = si.byte_length;
         d.flags = fam == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
         si.desc_index = (int32_t)p->descs.size();
-        if (fam != COVT_FAMILY_SPLIT && fam != COVT_FAMILY_SPLIT_FPF) {
+        if (fam != COVT_FAMILY_SPLIT && fam != COVT_FAMILY_SPLIT_FPF && fam != COVT_FAMILY_SPLIT_RLE) {
             p->descs.push_back(d);
             p->desc_stream.push_back((int64_t)i);
             p->fam_counts[fam]++;
+            continue;
+        }
+        // RLE: the host walk's chunks
+        auto rs = rle_split.find(i);
+        if (rs != rle_split.end()) {
+            const auto& ch = rs->second.first;
+            for (size_t c = 0; c < ch.size(); ++c) {
+                covt_stream_desc cd = d;
+                cd.flags = COVT_DESC_SPLIT | COVT_DESC_SPLIT_RLE;
+                cd.avail = (int32_t)c;
+                p->descs.push_back(cd);
+                for (int q = 1; q < COVT_SPLIT_SLOTS; ++q) {
+                    covt_stream_desc pd{};
+                    pd.flags = COVT_DESC_SPLIT_PAD | COVT_DESC_SPLIT_RLE;
+                    if (q == 1) pd.in_off = (uint64_t)ch[c].s, pd.out_off = (uint64_t)ch[c].e;
+                    if (q == 2) pd.in_off = (uint64_t)ch[c].v0, pd.out_off = (uint64_t)ch[c].nv;
+                    if (q == 3) pd.in_off = (uint64_t)rs->second.second;
+                    p->descs.push_back(pd);
+                }
+                for (int q = 0; q < COVT_SPLIT_SLOTS; ++q) p->desc_stream.push_back((int64_t)i);
+            }
+            p->fam_counts[fam] += (int64_t)ch.size() * COVT_SPLIT_SLOTS;
             continue;
         }
         // chunk c: bytes [c * split_chunk, min((c + 1) * split_chunk, byte_length)) of a varint stream,
@@ -1370,7 +1469,7 @@ int covt_decode_streams_device(const uint8_t* d_in, const covt_stream_desc* d_de
     if (n_streams < 0 || (n_streams && (!d_in || !d_desc || !d_res))) return COVT_ERR_INVALID_ARG;
     if ((uintptr_t)d_in & 15) return COVT_ERR_INVALID_ARG;
     for (int f = 0; f < COVT_NUM_FAMILIES; ++f) {  // any order: each family kernel skips the others
-        if (f == COVT_FAMILY_SPLIT || f == COVT_FAMILY_SPLIT_FPF) continue;  // split chunks need the grouped launch
+        if (f >= COVT_FAMILY_SPLIT) continue;  // split chunks need the grouped launch
         const int st = covt_launch_family(f, d_in, d_desc, n_streams, d_out, d_res, (hipStream_t)hip_stream);
         if (st) return st;
     }

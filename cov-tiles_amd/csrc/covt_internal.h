@@ -12,8 +12,9 @@ extern "C" {
 // [0, n_streams); descriptors of other families are skipped.
 int covt_launch_family(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
                        uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream);
-// The varint family's launch with the split chunks (COVT_FAMILY_SPLIT descriptors d_split[0, n_split),
-// their results / look-back records at d_split_res) carried in the same kernel.
+// Split chunks (descriptors d_split[0, n_split), their results / look-back records at d_split_res) of
+// kind fam (VARINT: COVT_FAMILY_SPLIT, RLE: COVT_FAMILY_SPLIT_RLE, FASTPFOR: COVT_FAMILY_SPLIT_FPF),
+// then family fam over d_desc[0, n_streams) on the same stream.
 int covt_launch_family_split(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
                              uint8_t* d_out, covt_stream_result* d_res, const covt_stream_desc* d_split,
                              int64_t n_split, covt_stream_result* d_split_res, hipStream_t stream);
@@ -32,7 +33,9 @@ inline bool lane_stream(int op, int32_t num_values, int32_t byte_length, int32_t
 }
 inline int desc_family(const covt_stream_desc& d) {
     if (d.flags & (COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD))
-        return (d.flags & COVT_DESC_SPLIT_FPF) ? COVT_FAMILY_SPLIT_FPF : COVT_FAMILY_SPLIT;
+        return (d.flags & COVT_DESC_SPLIT_FPF)   ? COVT_FAMILY_SPLIT_FPF
+               : (d.flags & COVT_DESC_SPLIT_RLE) ? COVT_FAMILY_SPLIT_RLE
+                                                 : COVT_FAMILY_SPLIT;
     return (d.flags & COVT_DESC_LANE) ? COVT_FAMILY_LANE : covt_op_family_of(d.op);
 }
 // Plan rule for split streams: the Java-capped int32 varint ops (value ends are local: every byte
@@ -45,6 +48,10 @@ inline bool split_op(int op) {
 }
 inline bool split_fpf_op(int op) {
     return op == COVT_OP_FPF_ZZ_DELTA_I32 || op == COVT_OP_FPF_ZZ_DELTA_XY || op == COVT_OP_FPF_DELTA_MORTON;
+}
+inline bool split_rle_op(int op) {
+    return op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_I32 || op == COVT_OP_RLE_S64 || op == COVT_OP_BYTE_RLE_U8 ||
+           op == COVT_OP_BYTE_RLE_RAW;
 }
 // FastPFOR streams split by values into chunks of whole blocks (their own headers and page directories
 // locate every block), at least two chunks

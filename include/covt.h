@@ -135,7 +135,8 @@ enum covt_op {
 #define COVT_FAMILY_LANE 3     /* small RLE streams (flag COVT_DESC_LANE): one lane per stream */
 #define COVT_FAMILY_SPLIT 4    /* long varint streams cut into chunks decoded by separate waves (COVT_DESC_SPLIT) */
 #define COVT_FAMILY_SPLIT_FPF 5 /* long FastPFOR streams cut into chunks (COVT_DESC_SPLIT | COVT_DESC_SPLIT_FPF) */
-#define COVT_NUM_FAMILIES 6
+#define COVT_FAMILY_SPLIT_RLE 6 /* long ORC RLE streams cut at group starts (COVT_DESC_SPLIT | COVT_DESC_SPLIT_RLE) */
+#define COVT_NUM_FAMILIES 7
 
 /* covt_stream_desc.flags */
 #define COVT_DESC_LANE 0x1u /* decoded by the lane-per-stream kernel (set by the plan for small streams) */
@@ -151,6 +152,8 @@ enum covt_op {
 #define COVT_DESC_SPLIT 0x2u
 #define COVT_DESC_SPLIT_PAD 0x4u
 #define COVT_DESC_SPLIT_FPF 0x8u /* with SPLIT / SPLIT_PAD: a FastPFOR stream's chunk */
+#define COVT_DESC_SPLIT_RLE 0x10u /* with SPLIT / SPLIT_PAD: an ORC RLE stream's chunk (whole groups, located by the
+                                   * plan; pads [1] bytes [s, e), [2] values (first, count), [3] consumed) */
 #define COVT_SPLIT_SLOTS 8
 #define COVT_SPLIT_CHUNK 2048 /* default varint chunk bytes (env COVT_SPLIT_CHUNK at plan creation) */
 #define COVT_SPLIT_VALUES 2048 /* default FastPFOR chunk values, whole blocks (env COVT_SPLIT_VALUES) */

@@ -37,6 +37,7 @@ def test_fixtures_forced_split(covt, gpu_available, golden_streams, monkeypatch,
     tiles = [open(p, "rb").read() for p in paths]
     plan = covt.Plan.from_tiles(tiles, covt.FORMAT_GENC, id_mode)
     assert plan.family_counts[covt.FAMILY_SPLIT] > 1000 and plan.family_counts[covt.FAMILY_SPLIT_FPF] > 100
+    assert plan.family_counts[covt.FAMILY_SPLIT_RLE] > 100
     db = covt.DeviceBatch(plan, "cuda")
     for _ in range(2):  # the look-back records are reset per launch
         db.decode()
@@ -262,3 +263,148 @@ def test_u64_streams_split(covt, oracle, gpu_available, chunk):
                     n_err += 1
                 n_checked += 1
     assert n_checked > 100 and n_err > 10
+
+
+def _rle_chunks(buf: bytes, n: int, byte_rle: bool, elem: int, unit: int):
+    """Mirror of the plan's host walk (covt_host.cpp rle_chunks): chunks of whole ORC RLE groups,
+    cut every `unit` of bytes + output bytes / 4; (chunks, consumed) or None if n values do not fit."""
+    pos = v = cs = cv = 0
+    ch = []
+
+    def varint():
+        nonlocal pos
+        while True:
+            if pos >= len(buf):
+                return False
+            b = buf[pos]
+            pos += 1
+            if not b & 0x80:
+                return True
+
+    while v < n:
+        if pos >= len(buf):
+            return None
+        if (pos - cs) + (v - cv) * elem // 4 >= unit:
+            ch.append((cs, pos, cv, v - cv))
+            cs, cv = pos, v
+        h = buf[pos]
+        if h < 0x80:
+            if byte_rle:
+                if pos + 2 > len(buf):
+                    return None
+                pos += 2
+            else:
+                pos += 2
+                if pos > len(buf) or not varint():
+                    return None
+            v += h + 3
+        else:
+            cnt = 256 - h
+            pos += 1
+            if byte_rle:
+                if pos + cnt > len(buf):
+                    return None
+                pos += cnt
+            else:
+                for _ in range(cnt):
+                    if not varint():
+                        return None
+            v += cnt
+    ch.append((cs, pos, cv, n - cv))
+    return ch, pos
+
+
+def _rle_values(rng, n, big=False):
+    """Runs (constant and stepped, negative deltas), literal stretches, optionally 64-bit magnitudes."""
+    out = []
+    while len(out) < n:
+        k = int(rng.integers(1, 300))
+        kind = int(rng.integers(0, 3))
+        base = int(rng.integers(0, 1 << 62)) if big else int(rng.integers(0, 1 << 20))
+        if kind == 0:
+            out += [base] * k
+        elif kind == 1:
+            d = int(rng.integers(-128, 128))
+            out += [max(base + d * i, 0) for i in range(k)]
+        else:
+            hi = (1 << 62) if big else (1 << 20)
+            out += [int(x) for x in rng.integers(0, hi, size=k)]
+    return np.array(out[:n], dtype=np.uint64)
+
+
+@pytest.mark.parametrize("unit", [64, 700, 4096])
+def test_rle_streams_split(covt, oracle, gpu_available, unit):
+    """Long ORC RLE streams split at group starts by the plan's host walk: each chunk decodes its groups
+    into its slice of the stream's output (byte RLE: shared edge packets written byte-exact), the
+    stream's result = the lowest chunk status + the walked consumed bytes."""
+    import ctypes as C
+
+    import torch
+
+    rng = np.random.default_rng(unit)
+    cases = []
+    for n in (3000, 20000):
+        v = _rle_values(rng, n)
+        cases.append((covt.OP_RLE_U64, oracle.encode_rle(v, False), n, 8))
+        cases.append((covt.OP_RLE_I32, oracle.encode_rle(v, False), n, 4))
+        vb = _rle_values(rng, n, big=True)
+        cases.append((covt.OP_RLE_U64, oracle.encode_rle(vb, False), n, 8))
+        s = vb.view(np.int64) >> np.int64(1)
+        s[::3] = -s[::3]
+        cases.append((covt.OP_RLE_S64, oracle.encode_rle(s, True), n, 8))
+        bts = np.minimum(_rle_values(rng, n) % 7, 5).astype(np.uint8)
+        cases.append((covt.OP_BYTE_RLE_U8, oracle.encode_byte_rle(bts), n, 1))
+        raw = (_rle_values(rng, n) % 256).astype(np.uint8)
+        cases.append((covt.OP_BYTE_RLE_RAW, oracle.encode_byte_rle(raw), n, 1))
+        bad = bts.copy()
+        bad[int(n * 0.9)] = 9  # GeometryType out of range in a late chunk
+        cases.append((covt.OP_BYTE_RLE_U8, oracle.encode_byte_rle(bad), n, 1))
+    dev = torch.device("cuda")
+    n_checked = n_bad = 0
+    for op, buf, total, elem in cases:
+        byte_rle = op in (covt.OP_BYTE_RLE_U8, covt.OP_BYTE_RLE_RAW)
+        for n in (total, total - 1, total // 3 + 1):
+            walked = _rle_chunks(buf, n, byte_rle, elem, unit)
+            if walked is None or len(walked[0]) < 2:
+                continue
+            ch, consumed = walked
+            d = np.zeros(len(ch) * covt.SPLIT_SLOTS, dtype=DESC)
+            for c, (s0, e0, v0, nv) in enumerate(ch):
+                k = c * covt.SPLIT_SLOTS
+                d[k] = (0, 0, c, n, op, 0, covt.DESC_SPLIT | covt.DESC_SPLIT_RLE, len(buf))
+                d[k + 1 : k + covt.SPLIT_SLOTS]["flags"] = covt.DESC_SPLIT_PAD | covt.DESC_SPLIT_RLE
+                d[k + 1]["in_off"], d[k + 1]["out_off"] = s0, e0
+                d[k + 2]["in_off"], d[k + 2]["out_off"] = v0, nv
+                d[k + 3]["in_off"] = consumed
+            counts = np.zeros(covt.NUM_FAMILIES, dtype=np.int64)
+            counts[covt.FAMILY_SPLIT_RLE] = d.size
+            d_in = torch.zeros(len(buf) + covt.INPUT_PADDING + 16, dtype=torch.uint8, device=dev)
+            d_in[:len(buf)] = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(dev)
+            d_desc = torch.from_numpy(d.view(np.uint8)).to(dev)
+            nbytes = n * elem
+            d_out = torch.full((nbytes + 32,), 0x5A, dtype=torch.uint8, device=dev)
+            d_res = torch.full((d.size * 2,), 0x33, dtype=torch.int32, device=dev)
+            st = covt.lib().covt_decode_streams_device_grouped(d_in.data_ptr(), d_desc.data_ptr(),
+                                                               counts.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                               d_out.data_ptr(), d_res.data_ptr(),
+                                                               torch.cuda.current_stream().cuda_stream)
+            assert st == 0
+            torch.cuda.synchronize()
+            out = d_out.cpu().numpy()
+            r = d_res.cpu().numpy().reshape(-1, 2)[0]
+            if byte_rle:
+                o_st, o_arr, _, o_cons = oracle.decode_byte_rle(buf, n, 0, len(buf))
+                if op == covt.OP_BYTE_RLE_U8 and o_st == 0 and (np.asarray(o_arr) > 5).any():
+                    o_st = covt.ERR_BAD_HEADER
+            else:
+                o_st, o_arr, _, o_cons = oracle.decode_rle(buf, n, 0, op == covt.OP_RLE_S64)
+            assert (int(r[0]) == 0) == (o_st == 0), (op, n, unit, int(r[0]), o_st)
+            n_bad += o_st != 0
+            if o_st == 0:
+                assert int(r[1]) == o_cons, (op, n, unit)
+                dt = {1: np.uint8, 4: np.int32, 8: np.int64}[elem]
+                got = out[:nbytes].view(dt)
+                assert np.array_equal(got, np.asarray(o_arr).astype(np.int64).astype(dt)), (op, n, unit)
+                assert (out[nbytes:] == 0x5A).all(), (op, n, unit)  # chunks write nothing past the stream
+            n_checked += 1
+    assert n_checked > 20 and n_bad > 0

@@ -32,18 +32,24 @@ def test_split_layout(covt, monkeypatch, chunk):
     assert sp.size % covt.SPLIT_SLOTS == 0 and sp.size > 0
     st = plan.streams
     split_streams = set()
+    rle_ranges = {}
     for k in range(0, sp.size, covt.SPLIT_SLOTS):
         cd, rg = sp[k], sp[k + 1]
         fpf = bool(cd["flags"] & covt.DESC_SPLIT_FPF)
-        assert cd["flags"] == covt.DESC_SPLIT | (covt.DESC_SPLIT_FPF if fpf else 0)
-        assert fpf == (k >= int(plan.family_counts[covt.FAMILY_SPLIT]))  # varint chunks, then FastPFOR chunks
-        assert all(sp[k + q]["flags"] == covt.DESC_SPLIT_PAD | (cd["flags"] & covt.DESC_SPLIT_FPF)
-                   for q in range(1, covt.SPLIT_SLOTS))
+        rle = bool(cd["flags"] & covt.DESC_SPLIT_RLE)
+        kind = cd["flags"] & (covt.DESC_SPLIT_FPF | covt.DESC_SPLIT_RLE)
+        assert cd["flags"] == covt.DESC_SPLIT | kind and not (fpf and rle)
+        c4, c5 = int(plan.family_counts[covt.FAMILY_SPLIT]), int(plan.family_counts[covt.FAMILY_SPLIT_FPF])
+        assert (fpf, rle) == (c4 <= k < c4 + c5, k >= c4 + c5)  # varint, FastPFOR, then RLE chunks
+        assert all(sp[k + q]["flags"] == covt.DESC_SPLIT_PAD | kind for q in range(1, covt.SPLIT_SLOTS))
         i = int(plan.desc_streams[fam0 + k])
         assert all(plan.desc_streams[fam0 + k + q] == i for q in range(covt.SPLIT_SLOTS))
         c = int(cd["avail"])
         if fpf:  # FastPFOR: value ranges of COVT_SPLIT_VALUES
             assert (int(rg["in_off"]), int(rg["out_off"])) == (c * 512, min((c + 1) * 512, int(st["num_values"][i])))
+        elif rle:  # RLE: whole groups from the host walk (checked below)
+            rle_ranges.setdefault(i, []).append((c, int(rg["in_off"]), int(rg["out_off"]), int(sp[k + 2]["in_off"]),
+                                                 int(sp[k + 2]["out_off"]), int(sp[k + 3]["in_off"])))
         else:
             assert (int(rg["in_off"]), int(rg["out_off"])) == (c * chunk, min((c + 1) * chunk,
                                                                                int(st["byte_length"][i])))
@@ -56,7 +62,18 @@ def test_split_layout(covt, monkeypatch, chunk):
         cost = int(st["byte_length"][i]) + int(st["out_elems"][i]) * int(st["elem_bytes"][i]) // 4
         assert cost > 256 and st["op"][i] in (
             covt.OP_VARINT_ZZ_DELTA_I32, covt.OP_VARINT_ZZ_DELTA_XY, covt.OP_VARINT_DELTA_MORTON, covt.OP_VARINT_I32,
-            covt.OP_VARINT_U64, covt.OP_FPF_ZZ_DELTA_I32, covt.OP_FPF_ZZ_DELTA_XY, covt.OP_FPF_DELTA_MORTON)
+            covt.OP_VARINT_U64, covt.OP_FPF_ZZ_DELTA_I32, covt.OP_FPF_ZZ_DELTA_XY, covt.OP_FPF_DELTA_MORTON,
+            covt.OP_RLE_U64, covt.OP_RLE_I32, covt.OP_RLE_S64, covt.OP_BYTE_RLE_U8, covt.OP_BYTE_RLE_RAW)
+    # RLE chunks tile the stream's bytes and values; the last one ends at the stream's consumed bytes
+    assert rle_ranges
+    for i, rows in rle_ranges.items():
+        rows.sort()
+        assert [r[0] for r in rows] == list(range(len(rows))) and len(rows) >= 2
+        assert rows[0][1] == 0 and rows[0][3] == 0
+        for a, b in zip(rows, rows[1:]):
+            assert a[2] == b[1] and a[3] + a[4] == b[3]  # contiguous bytes, contiguous values
+        assert rows[-1][3] + rows[-1][4] == int(st["num_values"][i]) and rows[-1][2] == rows[0][5]
+        assert rows[0][5] <= int(st["byte_length"][i])
     # every stream has exactly one result entry, and non-split descriptors map 1:1
     assert len(set(st["desc_index"].tolist())) == plan.num_streams
     assert np.array_equal(plan.desc_streams[st["desc_index"]], np.arange(plan.num_streams))

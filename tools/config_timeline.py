@@ -65,9 +65,10 @@ def main():
         if chunk_rows.size:
             cdur = allph[chunk_rows, 0].astype(np.int64)
             cst = allph[chunk_rows, 1].astype(np.int64)
-            fpf = (flags[chunk_rows] & covt.DESC_SPLIT_FPF) != 0
-            for f, fname in ((False, "SPLIT"), (True, "SPLIT_FPF")):
-                m = fpf == f
+            kind = np.where((flags[chunk_rows] & covt.DESC_SPLIT_FPF) != 0, 1,
+                            np.where((flags[chunk_rows] & covt.DESC_SPLIT_RLE) != 0, 2, 0))
+            for f, fname in ((0, "SPLIT"), (1, "SPLIT_FPF"), (2, "SPLIT_RLE")):
+                m = kind == f
                 if not m.any():
                     continue
                 k = np.nonzero(m)[0][np.argmax(cdur[m])]
