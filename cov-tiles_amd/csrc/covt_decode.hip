@@ -1235,6 +1235,10 @@ struct FpfSkip {
     int32_t done = -1;  // page start (values) the state belongs to; -1: none
     int32_t cur0, pk;
     int xc;  // lane k: values of dataTobePacked[k] consumed before the chunk's first block
+    // the page holding the chunk's first value: its start (values, -1: none) and word, and its parsed
+    // directory (so the second pass neither re-walks earlier pages' directories nor this one's)
+    int32_t pdone = -1, p_page, bytesize, ie_end;
+    int xs, xz;
 };
 template <int OP>
 __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Carry cr0 = Carry{0, 0},
@@ -1278,41 +1282,68 @@ __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Car
         };
         while (!c.err && done < L) {
             done = uni(done);
+            const bool cached = skip && skip->pdone >= 0;
+            if (cached && done < skip->pdone) {  // second pass: pages before the chunk's, skipped outright
+                done = skip->pdone;
+                p = skip->p_page;
+                continue;
+            }
             const int32_t thissize = uni((L - done) < kFpfPage ? (L - done) : kFpfPage);
             const int64_t p0 = uni64(p);
             if (p0 >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
-            int64_t ie = p0 + (int32_t)W.uniform(p0);
-            if (ie < 0 || ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
-            const int32_t bytesize = (int32_t)W.uniform(ie++);
-            if (bytesize < 0 || bytesize > kFpfBcCap) { c.err = COVT_ERR_BAD_HEADER; break; }
+            int64_t ie;
+            int32_t bytesize;
+            xc_v = 0;
+            if (cached && done == skip->pdone) {
+                bytesize = skip->bytesize;
+                ie = p0 + (int32_t)W.uniform(p0) + 1;  // the byte container
+                xs_v = skip->xs;
+                xz_v = skip->xz;
+            } else {
+                ie = p0 + (int32_t)W.uniform(p0);
+                if (ie < 0 || ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+                bytesize = (int32_t)W.uniform(ie++);
+                if (bytesize < 0 || bytesize > kFpfBcCap) { c.err = COVT_ERR_BAD_HEADER; break; }
+            }
             const int64_t bcw = (bytesize + 3) / 4;
             const int64_t bc = ie;
             if (bc + bcw >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
             ie += bcw;
-            // exception-array directory (bitmap, then size + packed words per set bit), parsed from a
-            // 1 KiB LDS window of words; the arrays' start/size/cursor live in lanes 2..32 of VGPRs
-            int64_t dbase = load_words(sm.u.f.stage, ie);
-            auto dword = [&](int64_t w) -> uint32_t {
-                if (w < dbase || w >= dbase + 255) dbase = load_words(sm.u.f.stage, w);
-                return uniu(sm.u.f.stage[w - dbase]);
-            };
-            uint32_t bm = dword(ie++) & ~1u;  // bit k-1 set: dataTobePacked[k] present (k >= 2)
-            xs_v = 0;
-            xz_v = -1;
-            xc_v = 0;
-            while (bm) {
-                const int32_t k = __builtin_ctz(bm) + 1;
-                bm &= bm - 1;
-                if (ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
-                const int32_t size = (int32_t)dword(ie++);
-                if (size < 0) { c.err = COVT_ERR_BAD_HEADER; break; }
-                const int64_t groups = ((int64_t)size + 31) / 32;
-                xs_v = l == k ? (int)(uint32_t)ie : xs_v;
-                xz_v = l == k ? size : xz_v;
-                ie += groups * k;
-                ie -= ((groups * 32 - size) * k) / 32;
+            if (cached && done == skip->pdone) {
+                ie = skip->ie_end;
+            } else {
+                // exception-array directory (bitmap, then size + packed words per set bit), parsed from a
+                // 1 KiB LDS window of words; the arrays' start/size/cursor live in lanes 2..32 of VGPRs
+                int64_t dbase = load_words(sm.u.f.stage, ie);
+                auto dword = [&](int64_t w) -> uint32_t {
+                    if (w < dbase || w >= dbase + 255) dbase = load_words(sm.u.f.stage, w);
+                    return uniu(sm.u.f.stage[w - dbase]);
+                };
+                uint32_t bm = dword(ie++) & ~1u;  // bit k-1 set: dataTobePacked[k] present (k >= 2)
+                xs_v = 0;
+                xz_v = -1;
+                while (bm) {
+                    const int32_t k = __builtin_ctz(bm) + 1;
+                    bm &= bm - 1;
+                    if (ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+                    const int32_t size = (int32_t)dword(ie++);
+                    if (size < 0) { c.err = COVT_ERR_BAD_HEADER; break; }
+                    const int64_t groups = ((int64_t)size + 31) / 32;
+                    xs_v = l == k ? (int)(uint32_t)ie : xs_v;
+                    xz_v = l == k ? size : xz_v;
+                    ie += groups * k;
+                    ie -= ((groups * 32 - size) * k) / 32;
+                }
+                if (c.err) break;
+                if (skip && v0 >= done && v0 < done + thissize) {  // the chunk's first page: kept for pass two
+                    skip->pdone = done;
+                    skip->p_page = (int32_t)p0;
+                    skip->bytesize = bytesize;
+                    skip->ie_end = (int32_t)ie;
+                    skip->xs = xs_v;
+                    skip->xz = xz_v;
+                }
             }
-            if (c.err) break;
             COVT_PHASE(c, 0);
             const int32_t nblocks_page = uni(thissize / kFpfBlock);
             // blocks of this page holding values of [v0, v1)
@@ -1405,7 +1436,7 @@ __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Car
             // cursors, one LDS read per header (each block is checked by the chunk that decodes it; the
             // container bound keeps this walk's reads in place), once per chunk
             if (jb0 > 0 && jb0 < nblocks && !c.err) {
-                if (skip && skip->done == done) {
+                if (skip && skip->done == done) {  // (FpfSkip::done: set by the pre-walk below)
                     cur0 = skip->cur0;
                     pk = skip->pk;
                     xc_v = skip->xc;
@@ -1426,8 +1457,14 @@ __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Car
                     }
                     cur0 = uni(cur);
                     pk = uni(pkk);
-                    if (skip) *skip = FpfSkip{done, cur0, pk, xc_v};
+                    if (skip) {
+                        skip->done = done;
+                        skip->cur0 = cur0;
+                        skip->pk = pk;
+                        skip->xc = xc_v;
+                    }
                 }
+                COVT_PHASE(c, 0);  // (the pre-walk counts with the directory)
             }
             if (jb0 < nblocks && !c.err) {
                 c.err = walk(cur0, h);
@@ -1898,6 +1935,20 @@ __device__ int64_t decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ 
     c.byte_length = d.byte_length;
     c.err = 0;
     c.consumed = 0;
+#ifdef COVT_TIMING  // phase clocks -> entries 2..7 of the chunk descriptor's phase row (0, 1: duration, start)
+    c.ph_last = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k < kPhases; ++k) c.ph[k] = 0;
+    struct PhaseOut {
+        Ctx& c;
+        const covt_stream_desc* row;
+        __device__ ~PhaseOut() {
+            if (covt_phase_buf && lane_id() == 0) {
+                uint32_t* r = covt_phase_buf + (row - covt_phase_desc0) * kPhases;
+                for (int k = 0; k < kPhases - 2; ++k) r[2 + k] = c.ph[k];
+            }
+        }
+    } phase_out{c, descs + kSplitSlots * t};
+#endif
     const int32_t chunk = d.avail, s = (int32_t)rg.in_off, e = (int32_t)rg.out_off;
     if constexpr (K == kSplitRle) {
         run_rle_chunk(c, descs + kSplitSlots * t, chunk, res, t);

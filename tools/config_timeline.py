@@ -75,10 +75,10 @@ def main():
                 row = sd[chunk_rows[k]]
                 op, nv, bl = int(row[24]), int(row[20:24].view(np.int32)[0]), int(row[28:32].view(np.int32)[0])
                 print("   family %-9s chunks=%4d first start %6.1f last start %6.1f last end %6.1f us; longest chunk "
-                      "%.1f us (start %.1f) of %s %d B %d vals" % (
+                      "%.1f us (start %.1f) of %s %d B %d vals, phase kclk %s" % (
                           fname, int(m.sum()), (cst[m].min() - t0) * TICK_US, (cst[m].max() - t0) * TICK_US,
                           (cst[m] + cdur[m] - t0).max() * TICK_US, cdur[k] * TICK_US, (cst[k] - t0) * TICK_US,
-                          NAMES.get(op, op), bl, nv))
+                          NAMES.get(op, op), bl, nv, " ".join("%d" % (x // 1000) for x in allph[chunk_rows[k], 2:])))
         for i in np.argsort(-end)[:6]:
             j = idx[i]
             print("   %-12s bytes %7d values %7d  start %7.1f us  dur %7.1f us" % (
