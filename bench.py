@@ -191,10 +191,18 @@ def end_to_end(plan, batch, stream, torch, dev, reps):
             "note": "pinned host tile bytes + descriptors H2D, one decode launch, all outputs + results D2H"}
 
 
+def torch_device_index():
+    import torch
+
+    return torch.cuda.current_device()
+
+
 def abi_host_leg(plan, t_plan, reps):
     """The C-ABI host entry a JNI/ctypes caller would use (include/covt.h covt_plan_decode_host): pageable
-    tile bytes in, device buffers allocated per call, H2D, one decode launch, D2H into pageable host memory
-    (fresh buffers each call, so first-touch page faults are included).  Not `value`."""
+    tile bytes in, device buffers cached on the plan after the first call, H2D, one decode launch, D2H into
+    pageable host memory (fresh buffers each call, so first-touch page faults are included; then reused
+    caller buffers, and the same through covt_plan_decode_host_shards with two shards on this device, the
+    multi-GPU path's per-shard H2D / launch / D2H).  Not `value`."""
     plan.decode_host()  # warm: HIP context, allocator
     t = time.perf_counter()
     for _ in range(reps):
@@ -209,11 +217,18 @@ def abi_host_leg(plan, t_plan, reps):
     for _ in range(reps):
         plan.decode_host(out=out, res=res)
     ms_reuse = (time.perf_counter() - t) * 1e3 / reps
+    dev = torch_device_index()
+    plan.decode_host(out=out, res=res, shard_devices=[dev, dev])
+    t = time.perf_counter()
+    for _ in range(reps):
+        plan.decode_host(out=out, res=res, shard_devices=[dev, dev])
+    ms_shards = (time.perf_counter() - t) * 1e3 / reps
     return {"ms": round(ms, 3), "value": round(plan.in_bytes / (ms * 1e-3) / 1e9, 3), "unit": "GB/s",
-            "ms_reused_buffers": round(ms_reuse, 3),
+            "ms_reused_buffers": round(ms_reuse, 3), "ms_two_shards_reused": round(ms_shards, 3),
             "raw_tiles_to_host_ms": round(ms + t_plan * 1e3, 1), "reps": reps,
-            "note": "covt_plan_decode_host wall clock (pageable bytes, per-call device alloc, H2D + decode + "
-                    "D2H) into fresh host buffers; ms_reused_buffers: into caller buffers reused across calls; "
+            "note": "covt_plan_decode_host wall clock (pageable bytes, device buffers cached on the plan, H2D + "
+                    "decode + D2H) into fresh host buffers; ms_reused_buffers: into caller buffers reused across "
+                    "calls; ms_two_shards_reused: covt_plan_decode_host_shards, 2 shards on this device; "
                     "raw_tiles_to_host_ms adds the host metadata walk (covt_plan_create)"}
 
 
