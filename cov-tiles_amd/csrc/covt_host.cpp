@@ -111,7 +111,7 @@ int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::ve
     if (version != 1) return COVT_ERR_BAD_HEADER;
     struct SM { int type, enc; int64_t nv, bl, name_off, name_len, off; };
     struct CM { int kind, dtype, ctype; int64_t name_off, name_len; std::vector<SM> s; };
-    std::vector<CM> cols;
+    static thread_local std::vector<CM> cols;  // reused across tiles: no allocation per column
     for (uint64_t L = 0; L < nlayers; ++L) {
         uint64_t nlen, extent, nfeat, ncols;
         if (!rd_uv(t, len, o, nlen) || o + nlen > len) return COVT_ERR_TRUNCATED;
@@ -364,6 +364,31 @@ void choose_op(const RawStream& s, int id_mode, int& op, int64_t& nvals, int& el
 }
 
 inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
+
+// Launch-order keys: a stable LSD radix sort (11-bit digits, passes whose digit is the same for every
+// key skipped), so equal keys keep plan (tile) order.  std::sort of the 432k keys of a 10k-tile plan
+// took ~50 ms of the plan; this takes a few.
+struct SortKey {
+    uint64_t k;
+    uint32_t i;
+};
+void radix_sort(std::vector<SortKey>& a) {
+    const size_t n = a.size();
+    if (n < 2) return;
+    std::vector<SortKey> tmp(n);
+    uint64_t all_or = 0, all_and = ~0ull;
+    for (const SortKey& x : a) all_or |= x.k, all_and &= x.k;
+    const uint64_t varying = all_or ^ all_and;
+    for (int sh = 0; sh < 64; sh += 11) {
+        if (!((varying >> sh) & 0x7ffull)) continue;
+        size_t cnt[2048] = {};
+        for (const SortKey& x : a) ++cnt[(x.k >> sh) & 0x7ff];
+        size_t s = 0;
+        for (size_t& c : cnt) { const size_t v = c; c = s; s += v; }
+        for (const SortKey& x : a) tmp[cnt[(x.k >> sh) & 0x7ff]++] = x;
+        a.swap(tmp);
+    }
+}
 
 // ---- per-thread device context for the stream-level API -----------------------------------------
 struct DevCtx {
@@ -819,6 +844,7 @@ namespace {
 void plan_geometry(covt_plan* p) {
     const size_t ns = p->info.size();
     int64_t off = 0;
+    p->ginfo.reserve(ns / 4);
     for (size_t i = 0; i < ns;) {
         const covt_stream_info& s0 = p->info[i];
         if (s0.column_kind != 1) { ++i; continue; }
@@ -860,14 +886,14 @@ void plan_geometry(covt_plan* p) {
     }
     p->asm_bytes = off;
     const size_t nc = p->ginfo.size();
-    std::vector<size_t> order(nc);
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
-        return p->ginfo[a].coord_cap + p->ginfo[a].n_features > p->ginfo[b].coord_cap + p->ginfo[b].n_features;
-    });
+    std::vector<SortKey> order(nc);  // largest (coordinates + features) first, ties in tile order
+    for (size_t k = 0; k < nc; ++k)
+        order[k] = SortKey{(1ull << 40) - (uint64_t)((int64_t)p->ginfo[k].coord_cap + p->ginfo[k].n_features),
+                           (uint32_t)k};
+    radix_sort(order);
     p->gdescs.resize(nc);
     for (size_t k = 0; k < nc; ++k) {
-        covt_geom_info& g = p->ginfo[order[k]];
+        covt_geom_info& g = p->ginfo[order[k].i];
         covt_geom_desc d{};
         for (int m = 0; m < 6; ++m) {
             const int32_t si = g.stream[m];
@@ -1230,6 +1256,9 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         1, std::min<int64_t>({(int64_t)std::thread::hardware_concurrency(), 16, ((int64_t)n_tiles + 63) / 64}));
     std::vector<Chunk> chunks((size_t)n_thr);
     auto walk_chunk = [&](Chunk* c) {
+        c->rs.reserve((size_t)(c->t1 - c->t0) * 64);  // ~43 Id/Geometry streams per tile
+        c->rs_end.reserve((size_t)(c->t1 - c->t0));
+        c->props_end.reserve((size_t)(c->t1 - c->t0));
         for (int32_t t = c->t0; t < c->t1; ++t) {
             const uint8_t* tile = bytes + tile_offsets[t];
             const size_t r0 = c->rs.size(), q0 = c->props.size();
@@ -1300,11 +1329,7 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
     // streams first inside a family so the long poles start early (static wave->stream map); one
     // precomputed key per stream, ties in tile order
     const size_t ns = p->info.size();
-    struct Key {
-        uint64_t k;
-        uint32_t i;
-    };
-    std::vector<Key> keys(ns);
+    std::vector<SortKey> keys(ns);
     // split a stream only where one wave decoding it would outlast the launch.  A stream's cost is its
     // bytes + output bytes / 4 (the launch-order key below; FastPFOR and RLE time follows the values as
     // much as the bytes): split above COVT_SPLIT_MIN and above the batch's total cost /
@@ -1355,9 +1380,9 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
                                                                      : COVT_FAMILY_SPLIT)
                              : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);
         const uint64_t cost = std::min<uint64_t>((uint64_t)stream_cost(s), (1ull << 48) - 1);
-        keys[i] = Key{(fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost), (uint32_t)i};
+        keys[i] = SortKey{(fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost), (uint32_t)i};
     }
-    std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) { return a.k != b.k ? a.k < b.k : a.i < b.i; });
+    radix_sort(keys);  // stable: ties in tile order
     p->descs.reserve(ns);
     p->desc_stream.reserve(ns);
     for (size_t k = 0; k < ns; ++k) {
