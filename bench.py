@@ -143,6 +143,11 @@ def cpu_baseline(plan, args):
     times = [run(threads)[0] for _ in range(max(args.cpu_iters, 1))]
     _, ib, vx = run(threads)
     med = float(np.median(times))
+    # the same with one thread per CPU the OS reports (os.cpu_count(); on the box 256 while the cgroup
+    # quota allows 16 at a time): recorded beside `value`, which uses the usable cores
+    nproc = os.cpu_count() or threads
+    run(nproc)
+    med_np = float(np.median([run(nproc)[0] for _ in range(5)]))
     el1, _, _ = run(1)  # 1 thread: one warm-up-free pass is already seconds long; take the median of 3
     times1 = [el1] + [run(1)[0] for _ in range(2 if el1 < 10 else 0)]
     med1 = float(np.median(times1))
@@ -152,6 +157,8 @@ def cpu_baseline(plan, args):
                       "FastPFOR) built -O3 -march=%s here, %d threads, one tile per task" %
                       (plan.n_tiles, ib / 1e6, len(times), med * 1e3, march, threads),
             "mvert_per_s": round(vx / med / 1e6, 3),
+            "value_nproc_threads": round(ib / med_np / 1e9, 4), "nproc_threads": nproc,
+            "ms_nproc_threads": round(med_np * 1e3, 1),
             "value_1thread": round(ib / med1 / 1e9, 4), "ms_1thread": round(med1 * 1e3, 1),
             "iters_1thread": len(times1),
             "host": dict(cpus, cpu_model=cpu_model())}
