@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <sys/mman.h>
@@ -364,6 +365,21 @@ void choose_op(const RawStream& s, int id_mode, int& op, int64_t& nvals, int& el
 }
 
 inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
+
+// f(begin, end) over [0, n) split into nthr contiguous ranges, one host thread each (the caller's thread
+// takes the first); small inputs run on the caller's thread alone
+template <class F>
+void par_for(int32_t nthr, int64_t n, F&& f) {
+    if (nthr <= 1 || n < 2) {
+        f((int64_t)0, n);
+        return;
+    }
+    const int64_t nt = std::min<int64_t>(nthr, n);
+    std::vector<std::thread> th;
+    for (int64_t k = 1; k < nt; ++k) th.emplace_back([&f, k, n, nt] { f(n * k / nt, n * (k + 1) / nt); });
+    f((int64_t)0, n / nt);
+    for (auto& x : th) x.join();
+}
 
 // Launch-order keys: a stable LSD radix sort (11-bit digits, passes whose digit is the same for every
 // key skipped), so equal keys keep plan (tile) order.  std::sort of the 432k keys of a 10k-tile plan
@@ -841,20 +857,19 @@ namespace {
 // data-independent bounds (every point part/ring consumes one source vertex, every line part one
 // partOffsets entry, every polygon ring one ringOffsets entry):
 //   parts <= Vs + n_po, rings <= Vs + n_po + n_ro, coordinates <= Vs (+ n_ro closing vertices).
-void plan_geometry(covt_plan* p) {
+void plan_geometry(covt_plan* p, int32_t nthr) {
     const size_t ns = p->info.size();
-    int64_t off = 0;
-    p->ginfo.reserve(ns / 4);
-    for (size_t i = 0; i < ns;) {
+    // the column starting at stream i (the streams of one (tile, layer) geometry column are adjacent);
+    // its record with assembly offsets from `off`, which it advances
+    auto column = [&](size_t i, size_t& j, int64_t& off) {
         const covt_stream_info& s0 = p->info[i];
-        if (s0.column_kind != 1) { ++i; continue; }
         covt_geom_info g{};
         g.tile = s0.tile;
         g.layer = s0.layer;
         g.column_type = s0.column_type;
         for (int k = 0; k < 6; ++k) g.stream[k] = -1;
         int64_t len[6] = {0, 0, 0, 0, 0, 0};
-        size_t j = i;
+        j = i;
         for (; j < ns && p->info[j].tile == s0.tile && p->info[j].layer == s0.layer && p->info[j].column_kind == 1; ++j) {
             const covt_stream_info& s = p->info[j];
             const int k = s.stream_type - ST_GEOMETRY_TYPES;
@@ -863,7 +878,6 @@ void plan_geometry(covt_plan* p) {
             len[k] = k == 5 ? s.out_elems / 2 : s.out_elems;  // vertexBuffer: x,y pairs
             if (k == 5) g.column_type = s.column_type;
         }
-        i = j;
         g.n_features = (int32_t)len[0];
         const int64_t vs = g.stream[4] >= 0 ? len[4] : len[5];
         const int64_t pcap = vs + len[2], rcap = vs + len[2] + len[3];
@@ -882,33 +896,78 @@ void plan_geometry(covt_plan* p) {
             g.out_off[k] = off;
             off = align16(off + bytes[k]);
         }
-        p->ginfo.push_back(g);
+        return g;
+    };
+    // stream ranges, one per thread, starting at column boundaries; each range's columns with assembly
+    // offsets local to the range (16-byte aligned slices), rebased and concatenated in order
+    const int64_t nt = std::max<int64_t>(1, std::min<int64_t>(nthr, (int64_t)ns / 4096 + 1));
+    std::vector<size_t> cut((size_t)nt + 1);
+    for (int64_t k = 0; k <= nt; ++k) {
+        size_t i = (size_t)((int64_t)ns * k / nt);
+        while (i > 0 && i < ns && p->info[i].column_kind == 1 && p->info[i - 1].column_kind == 1 &&
+               p->info[i].tile == p->info[i - 1].tile && p->info[i].layer == p->info[i - 1].layer)
+            ++i;  // (inside a column: move to its end)
+        cut[(size_t)k] = k == nt ? ns : std::max(i, k ? cut[(size_t)k - 1] : (size_t)0);
+    }
+    std::vector<std::vector<covt_geom_info>> part((size_t)nt);
+    std::vector<int64_t> part_off((size_t)nt);
+    par_for((int32_t)nt, nt, [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; ++k) {
+            int64_t off = 0;
+            for (size_t i = cut[(size_t)k]; i < cut[(size_t)k + 1];) {
+                if (p->info[i].column_kind != 1) { ++i; continue; }
+                size_t j;
+                part[(size_t)k].push_back(column(i, j, off));
+                i = j;
+            }
+            part_off[(size_t)k] = off;
+        }
+    });
+    int64_t off = 0;
+    size_t nc = 0;
+    std::vector<int64_t> base((size_t)nt);
+    std::vector<size_t> first((size_t)nt);
+    for (int64_t k = 0; k < nt; ++k) {
+        base[(size_t)k] = off;
+        first[(size_t)k] = nc;
+        off += part_off[(size_t)k];
+        nc += part[(size_t)k].size();
     }
     p->asm_bytes = off;
-    const size_t nc = p->ginfo.size();
+    p->ginfo.resize(nc);
     std::vector<SortKey> order(nc);  // largest (coordinates + features) first, ties in tile order
-    for (size_t k = 0; k < nc; ++k)
-        order[k] = SortKey{(1ull << 40) - (uint64_t)((int64_t)p->ginfo[k].coord_cap + p->ginfo[k].n_features),
-                           (uint32_t)k};
+    par_for((int32_t)nt, nt, [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; ++k)
+            for (size_t q = 0; q < part[(size_t)k].size(); ++q) {
+                covt_geom_info g = part[(size_t)k][q];
+                for (int m = 0; m < 6; ++m) g.out_off[m] += base[(size_t)k];
+                const size_t c = first[(size_t)k] + q;
+                p->ginfo[c] = g;
+                order[c] = SortKey{(1ull << 40) - (uint64_t)((int64_t)g.coord_cap + g.n_features), (uint32_t)c};
+            }
+    });
     radix_sort(order);
     p->gdescs.resize(nc);
-    for (size_t k = 0; k < nc; ++k) {
-        covt_geom_info& g = p->ginfo[order[k].i];
-        covt_geom_desc d{};
-        for (int m = 0; m < 6; ++m) {
-            const int32_t si = g.stream[m];
-            d.in_off[m] = si >= 0 ? p->info[(size_t)si].out_off : -1;
-            d.in_len[m] = si >= 0 ? (int32_t)(m == 5 ? p->info[(size_t)si].out_elems / 2 : p->info[(size_t)si].out_elems) : 0;
-            d.in_res[m] = si >= 0 ? p->info[(size_t)si].desc_index : -1;  // its decode status gates the column
-            d.out_off[m] = g.out_off[m];
+    par_for(nthr, (int64_t)nc, [&](int64_t k0, int64_t k1) {
+        for (int64_t kk = k0; kk < k1; ++kk) {
+            const size_t k = (size_t)kk;
+            covt_geom_info& g = p->ginfo[order[k].i];
+            covt_geom_desc d{};
+            for (int m = 0; m < 6; ++m) {
+                const int32_t si = g.stream[m];
+                d.in_off[m] = si >= 0 ? p->info[(size_t)si].out_off : -1;
+                d.in_len[m] = si >= 0 ? (int32_t)(m == 5 ? p->info[(size_t)si].out_elems / 2 : p->info[(size_t)si].out_elems) : 0;
+                d.in_res[m] = si >= 0 ? p->info[(size_t)si].desc_index : -1;  // its decode status gates the column
+                d.out_off[m] = g.out_off[m];
+            }
+            d.part_cap = g.part_cap;
+            d.ring_cap = g.ring_cap;
+            d.coord_cap = g.coord_cap;
+            d.flags = (int32_t)g.flags;
+            g.desc_index = (int32_t)k;
+            p->gdescs[k] = d;
         }
-        d.part_cap = g.part_cap;
-        d.ring_cap = g.ring_cap;
-        d.coord_cap = g.coord_cap;
-        d.flags = (int32_t)g.flags;
-        g.desc_index = (int32_t)k;
-        p->gdescs[k] = d;
-    }
+    });
 }
 
 // Property (sub)columns (include/covt.h "Property columns"; CovtParser.decodePropertyColumn
@@ -916,7 +975,15 @@ void plan_geometry(covt_plan* p) {
 // record remembers where the materialization finds them.  Unsupported shapes get a flag instead of
 // streams, in the order Java would throw: before anything (type, missing streams) or after the
 // present stream was decoded (data encodings, non-dictionary strings).
-void plan_property(covt_plan* p, int32_t t, int64_t tile_off, const PropRaw& q, int id_mode, int64_t& out_off) {
+// Stream / property records of a range of tiles, built by one host thread with output offsets and
+// stream indices local to the range; covt_plan_create_ex rebases and concatenates the parts.
+struct PlanPart {
+    std::vector<covt_stream_info> info;
+    std::vector<covt_prop_info> pinfo;
+    std::vector<uint16_t> pflags;
+    int64_t out_off = 0, in_bytes = 0, out_payload = 0, vertices = 0;
+};
+void plan_property(PlanPart* p, int32_t t, int64_t tile_off, const PropRaw& q, int id_mode, int64_t& out_off) {
     covt_prop_info pi{};
     pi.tile = t;
     pi.layer = q.layer;
@@ -1042,11 +1109,12 @@ void plan_property_layout(covt_plan* p) {
         }
     }
     p->prop_bytes = off;
+    std::vector<SortKey> korder(np);  // largest (features + dictionary entries) first, ties in tile order
+    for (size_t k = 0; k < np; ++k)
+        korder[k] = SortKey{(1ull << 40) - (uint64_t)((int64_t)p->pinfo[k].n_features + p->pinfo[k].n_dict), (uint32_t)k};
+    radix_sort(korder);
     std::vector<size_t> order(np);
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
-        return (int64_t)p->pinfo[a].n_features + p->pinfo[a].n_dict > (int64_t)p->pinfo[b].n_features + p->pinfo[b].n_dict;
-    });
+    for (size_t k = 0; k < np; ++k) order[k] = korder[k].i;
     p->pdescs.resize(np);
     for (size_t k = 0; k < np; ++k) {
         covt_prop_info& pi = p->pinfo[order[k]];
@@ -1253,7 +1321,8 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         std::vector<int32_t> rs_end, props_end;  // per tile of the chunk: end index in rs / props
     };
     const int32_t n_thr = (int32_t)std::max<int64_t>(
-        1, std::min<int64_t>({(int64_t)std::thread::hardware_concurrency(), 16, ((int64_t)n_tiles + 63) / 64}));
+        1, std::min<int64_t>({env_i64("COVT_PLAN_THREADS", std::min<int64_t>(std::thread::hardware_concurrency(), 16)),
+                              ((int64_t)n_tiles + 63) / 64}));
     std::vector<Chunk> chunks((size_t)n_thr);
     auto walk_chunk = [&](Chunk* c) {
         c->rs.reserve((size_t)(c->t1 - c->t0) * 64);  // ~43 Id/Geometry streams per tile
@@ -1284,47 +1353,89 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         walk_chunk(&chunks[(size_t)n_thr - 1]);
         for (auto& x : th) x.join();
     }
-    // 2. stream records and output slices in tile order
-    int64_t out_off = 0;
-    size_t total = 0;
-    for (const Chunk& c : chunks) total += c.rs.size();
-    p->info.reserve(total);
-    for (const Chunk& c : chunks) {
-      int32_t r = 0, q = 0;
-      for (int32_t t = c.t0; t < c.t1; ++t) {
-        const int32_t re = c.rs_end[(size_t)(t - c.t0)], qe = c.props_end[(size_t)(t - c.t0)];
-        for (; r < re; ++r) {
-            const RawStream& s = c.rs[(size_t)r];
-            int op, elem;
-            int64_t nvals, out_elems;
-            choose_op(s, id_mode, op, nvals, elem, out_elems);
-            covt_stream_info si{};
-            si.tile = t;
-            si.layer = s.layer;
-            si.column_kind = s.kind;
-            si.stream_type = s.type;
-            si.encoding = s.enc;
-            si.column_type = s.ctype;
-            si.num_values = s.nv;
-            si.byte_length = s.bl;
-            si.num_bits = s.nb;
-            si.op = op;
-            si.elem_bytes = elem;
-            si.in_off = (int64_t)tile_offsets[t] + s.off;
-            si.out_elems = op == COVT_OP_NONE ? 0 : out_elems;
-            si.out_off = out_off;
-            out_off = align16(out_off + si.out_elems * elem);
-            p->in_bytes += s.bl;
-            p->out_payload += si.out_elems * elem;
-            if (s.kind == 1 && s.type == ST_VERTEX_BUFFER)
-                p->vertices += (s.ctype == CT_ICE || s.ctype == CT_ICE_MORTON) ? s.nv : s.nv / 2;
-            si.desc_index = (int32_t)nvals;  // temporarily: values to decode
-            p->info.push_back(si);
+    // 2. stream records and output slices in tile order: each thread builds its tiles' records with
+    // output offsets and stream indices local to its range (every slice is 16-byte aligned, so a range's
+    // layout does not depend on where it starts), then the parts are rebased and concatenated
+    std::vector<PlanPart> parts((size_t)n_thr);
+    par_for(n_thr, n_thr, [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; ++k) {
+            const Chunk& c = chunks[(size_t)k];
+            PlanPart& pp = parts[(size_t)k];
+            pp.info.reserve(c.rs.size());
+            int32_t r = 0, q = 0;
+            for (int32_t t = c.t0; t < c.t1; ++t) {
+                const int32_t re = c.rs_end[(size_t)(t - c.t0)], qe = c.props_end[(size_t)(t - c.t0)];
+                for (; r < re; ++r) {
+                    const RawStream& s = c.rs[(size_t)r];
+                    int op, elem;
+                    int64_t nvals, out_elems;
+                    choose_op(s, id_mode, op, nvals, elem, out_elems);
+                    covt_stream_info si{};
+                    si.tile = t;
+                    si.layer = s.layer;
+                    si.column_kind = s.kind;
+                    si.stream_type = s.type;
+                    si.encoding = s.enc;
+                    si.column_type = s.ctype;
+                    si.num_values = s.nv;
+                    si.byte_length = s.bl;
+                    si.num_bits = s.nb;
+                    si.op = op;
+                    si.elem_bytes = elem;
+                    si.in_off = (int64_t)tile_offsets[t] + s.off;
+                    si.out_elems = op == COVT_OP_NONE ? 0 : out_elems;
+                    si.out_off = pp.out_off;
+                    pp.out_off = align16(pp.out_off + si.out_elems * elem);
+                    pp.in_bytes += s.bl;
+                    pp.out_payload += si.out_elems * elem;
+                    if (s.kind == 1 && s.type == ST_VERTEX_BUFFER)
+                        pp.vertices += (s.ctype == CT_ICE || s.ctype == CT_ICE_MORTON) ? s.nv : s.nv / 2;
+                    si.desc_index = (int32_t)nvals;  // temporarily: values to decode
+                    pp.info.push_back(si);
+                }
+                for (; q < qe; ++q) plan_property(&pp, t, (int64_t)tile_offsets[t], c.props[(size_t)q], id_mode, pp.out_off);
+            }
         }
-        for (; q < qe; ++q) plan_property(p, t, (int64_t)tile_offsets[t], c.props[(size_t)q], id_mode, out_off);
-      }
+    });
+    {
+        std::vector<int64_t> out_base((size_t)n_thr), info_base((size_t)n_thr), pinfo_base((size_t)n_thr);
+        int64_t ob = 0, ib = 0, pb = 0;
+        for (int32_t k = 0; k < n_thr; ++k) {
+            const PlanPart& pp = parts[(size_t)k];
+            out_base[(size_t)k] = ob;
+            info_base[(size_t)k] = ib;
+            pinfo_base[(size_t)k] = pb;
+            ob += pp.out_off;
+            ib += (int64_t)pp.info.size();
+            pb += (int64_t)pp.pinfo.size();
+            p->in_bytes += pp.in_bytes;
+            p->out_payload += pp.out_payload;
+            p->vertices += pp.vertices;
+        }
+        p->out_bytes = ob;
+        p->info.resize((size_t)ib);
+        p->pinfo.resize((size_t)pb);
+        p->pflags.resize((size_t)pb);
+        par_for(n_thr, n_thr, [&](int64_t k0, int64_t k1) {
+            for (int64_t k = k0; k < k1; ++k) {
+                PlanPart& pp = parts[(size_t)k];
+                const int64_t o = out_base[(size_t)k], i0 = info_base[(size_t)k], q0 = pinfo_base[(size_t)k];
+                for (size_t i = 0; i < pp.info.size(); ++i) {
+                    covt_stream_info si = pp.info[i];
+                    si.out_off += o;
+                    p->info[(size_t)i0 + i] = si;
+                }
+                for (size_t i = 0; i < pp.pinfo.size(); ++i) {
+                    covt_prop_info pi = pp.pinfo[i];
+                    for (int m = 0; m < 3; ++m)
+                        if (pi.stream[m] >= 0) pi.stream[m] += (int32_t)i0;
+                    p->pinfo[(size_t)q0 + i] = pi;
+                    p->pflags[(size_t)q0 + i] = pp.pflags[i];
+                }
+                PlanPart().info.swap(pp.info);  // free as we go
+            }
+        });
     }
-    p->out_bytes = out_off;
     // 3. launch order: grouped by family (the lane family also by op, for op-uniform waves), largest
     // streams first inside a family so the long poles start early (static wave->stream map); one
     // precomputed key per stream, ties in tile order
@@ -1341,18 +1452,24 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
     };
     int64_t split_min = env_i64("COVT_SPLIT_MIN", COVT_SPLIT_MIN);
     const int64_t split_ratio = env_i64("COVT_SPLIT_RATIO", COVT_SPLIT_RATIO);
-    if (split_min >= 0 && split_ratio > 0) {
-        int64_t total = 0;
-        for (const auto& si : p->info) total += stream_cost(si);
-        split_min = std::max<int64_t>(split_min, total / split_ratio);
-    }
     int32_t lane_max = (int32_t)env_i64("COVT_LANE_MAX_BYTES", kLaneMaxBytes);  // A/B knob
-    // The lane kernel pays off only where tiny RLE streams outnumber the wave slots (it decodes 64
-    // streams per wave, each serially: a wave of 100-250-value streams takes ~80-110 us); in smaller
-    // batches every RLE stream gets a wave of its own.
     {
-        int64_t n_lane = 0;
-        for (const auto& si : p->info) n_lane += lane_stream(si.op, si.desc_index, si.byte_length, lane_max);
+        // batch totals: cost (split threshold) and the streams the lane kernel would take (it decodes 64
+        // streams per wave, each serially: a wave of 100-250-value streams takes ~80-110 us, worth it only
+        // where tiny RLE streams outnumber the wave slots; in smaller batches every RLE stream gets a wave)
+        std::atomic<int64_t> tot_cost{0}, tot_lane{0};
+        par_for(n_thr, (int64_t)ns, [&](int64_t i0, int64_t i1) {
+            int64_t cst = 0, nl = 0;
+            for (int64_t i = i0; i < i1; ++i) {
+                const auto& si = p->info[(size_t)i];
+                cst += stream_cost(si);
+                nl += lane_stream(si.op, si.desc_index, si.byte_length, lane_max);
+            }
+            tot_cost += cst;
+            tot_lane += nl;
+        });
+        const int64_t total = tot_cost.load(), n_lane = tot_lane.load();
+        if (split_min >= 0 && split_ratio > 0) split_min = std::max<int64_t>(split_min, total / split_ratio);
         if (n_lane < env_i64("COVT_LANE_MIN_STREAMS", kLaneMinStreams)) lane_max = -1;
     }
     const int64_t split_chunk = std::max<int64_t>(64, env_i64("COVT_SPLIT_CHUNK", COVT_SPLIT_CHUNK));
@@ -1370,88 +1487,110 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
             if (!ch.empty()) rle_split.emplace(i, std::make_pair(std::move(ch), consumed));
         }
     }
-    for (size_t i = 0; i < ns; ++i) {
-        const auto& s = p->info[i];
-        const bool lane = lane_stream(s.op, s.desc_index, s.byte_length, lane_max);
-        const bool split = split_stream(s.op, s.desc_index, stream_cost(s), split_min, split_values) ||
-                           rle_split.count(i);
-        const uint64_t fam = split ? (uint64_t)(split_fpf_op(s.op)   ? COVT_FAMILY_SPLIT_FPF
-                                                : rle_split.count(i) ? COVT_FAMILY_SPLIT_RLE
-                                                                     : COVT_FAMILY_SPLIT)
-                             : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);
-        const uint64_t cost = std::min<uint64_t>((uint64_t)stream_cost(s), (1ull << 48) - 1);
-        keys[i] = SortKey{(fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost), (uint32_t)i};
-    }
-    radix_sort(keys);  // stable: ties in tile order
-    p->descs.reserve(ns);
-    p->desc_stream.reserve(ns);
-    for (size_t k = 0; k < ns; ++k) {
-        const size_t i = keys[k].i;
-        covt_stream_info& si = p->info[i];
-        const int fam = (int)(keys[k].k >> 60);
-        covt_stream_desc d{};
-        d.in_off = (uint64_t)si.in_off;
-        d.out_off = (uint64_t)si.out_off;
-        d.avail = si.byte_length;
-        d.num_values = si.desc_index;
-        d.op = (uint8_t)si.op;
-        d.num_bits = (uint8_t)si.num_bits;
-        d.byte_length = si.byte_length;
-        d.flags = fam == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
-        si.desc_index = (int32_t)p->descs.size();
-        if (fam != COVT_FAMILY_SPLIT && fam != COVT_FAMILY_SPLIT_FPF && fam != COVT_FAMILY_SPLIT_RLE) {
-            p->descs.push_back(d);
-            p->desc_stream.push_back((int64_t)i);
-            p->fam_counts[fam]++;
-            continue;
+    // descriptors per stream: 1, or COVT_SPLIT_SLOTS per chunk of a split stream
+    std::vector<int32_t> ndesc(ns);
+    par_for(n_thr, (int64_t)ns, [&](int64_t i0, int64_t i1) {
+        for (int64_t ii = i0; ii < i1; ++ii) {
+            const size_t i = (size_t)ii;
+            const auto& s = p->info[i];
+            const bool lane = lane_stream(s.op, s.desc_index, s.byte_length, lane_max);
+            const auto rs = rle_split.empty() ? rle_split.end() : rle_split.find(i);
+            const bool rsplit = rs != rle_split.end();
+            const bool split = split_stream(s.op, s.desc_index, stream_cost(s), split_min, split_values) || rsplit;
+            const uint64_t fam = split ? (uint64_t)(split_fpf_op(s.op) ? COVT_FAMILY_SPLIT_FPF
+                                                    : rsplit           ? COVT_FAMILY_SPLIT_RLE
+                                                                       : COVT_FAMILY_SPLIT)
+                                 : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);
+            const uint64_t cost = std::min<uint64_t>((uint64_t)stream_cost(s), (1ull << 48) - 1);
+            keys[i] = SortKey{(fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost),
+                              (uint32_t)i};
+            int64_t nd = 1;
+            if (rsplit) {
+                nd = (int64_t)rs->second.first.size() * COVT_SPLIT_SLOTS;
+            } else if (split) {
+                const bool fpf = fam == COVT_FAMILY_SPLIT_FPF;
+                const int64_t unit = fpf ? split_values : split_chunk, tot = fpf ? s.desc_index : s.byte_length;
+                nd = (tot + unit - 1) / unit * COVT_SPLIT_SLOTS;
+            }
+            ndesc[i] = (int32_t)nd;
         }
-        // RLE: the host walk's chunks
-        auto rs = rle_split.find(i);
-        if (rs != rle_split.end()) {
-            const auto& ch = rs->second.first;
-            for (size_t c = 0; c < ch.size(); ++c) {
+    });
+    radix_sort(keys);  // stable: ties in tile order
+    // 4. descriptors in launch order: offsets by a prefix sum over the sorted streams, filled in parallel
+    std::vector<int64_t> dpos(ns + 1);
+    dpos[0] = 0;
+    for (size_t k = 0; k < ns; ++k) {
+        dpos[k + 1] = dpos[k] + ndesc[keys[k].i];
+        p->fam_counts[keys[k].k >> 60] += ndesc[keys[k].i];
+    }
+    p->descs.resize((size_t)dpos[ns]);
+    p->desc_stream.resize((size_t)dpos[ns]);
+    par_for(n_thr, (int64_t)ns, [&](int64_t k0, int64_t k1) {
+        for (int64_t kk = k0; kk < k1; ++kk) {
+            const size_t k = (size_t)kk;
+            const size_t i = keys[k].i;
+            covt_stream_info& si = p->info[i];
+            const int fam = (int)(keys[k].k >> 60);
+            size_t o = (size_t)dpos[k];
+            covt_stream_desc d{};
+            d.in_off = (uint64_t)si.in_off;
+            d.out_off = (uint64_t)si.out_off;
+            d.avail = si.byte_length;
+            d.num_values = si.desc_index;
+            d.op = (uint8_t)si.op;
+            d.num_bits = (uint8_t)si.num_bits;
+            d.byte_length = si.byte_length;
+            d.flags = fam == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
+            si.desc_index = (int32_t)o;
+            for (int64_t q = 0; q < ndesc[i]; ++q) p->desc_stream[o + (size_t)q] = (int64_t)i;
+            if (fam != COVT_FAMILY_SPLIT && fam != COVT_FAMILY_SPLIT_FPF && fam != COVT_FAMILY_SPLIT_RLE) {
+                p->descs[o] = d;
+                continue;
+            }
+            // RLE: the host walk's chunks
+            auto rs = rle_split.find(i);
+            if (rs != rle_split.end()) {
+                const auto& ch = rs->second.first;
+                for (size_t c = 0; c < ch.size(); ++c) {
+                    covt_stream_desc cd = d;
+                    cd.flags = COVT_DESC_SPLIT | COVT_DESC_SPLIT_RLE;
+                    cd.avail = (int32_t)c;
+                    p->descs[o++] = cd;
+                    for (int q = 1; q < COVT_SPLIT_SLOTS; ++q) {
+                        covt_stream_desc pd{};
+                        pd.flags = COVT_DESC_SPLIT_PAD | COVT_DESC_SPLIT_RLE;
+                        if (q == 1) pd.in_off = (uint64_t)ch[c].s, pd.out_off = (uint64_t)ch[c].e;
+                        if (q == 2) pd.in_off = (uint64_t)ch[c].v0, pd.out_off = (uint64_t)ch[c].nv;
+                        if (q == 3) pd.in_off = (uint64_t)rs->second.second;
+                        p->descs[o++] = pd;
+                    }
+                }
+                continue;
+            }
+            // chunk c: bytes [c * split_chunk, min((c + 1) * split_chunk, byte_length)) of a varint stream,
+            // values [c * split_values, min((c + 1) * split_values, num_values)) of a FastPFOR stream
+            const bool fpf = fam == COVT_FAMILY_SPLIT_FPF;
+            const uint16_t fflag = fpf ? COVT_DESC_SPLIT_FPF : 0;
+            const int64_t unit = fpf ? split_values : split_chunk, total = fpf ? d.num_values : d.byte_length;
+            const int64_t nch = (total + unit - 1) / unit;
+            for (int64_t c = 0; c < nch; ++c) {
                 covt_stream_desc cd = d;
-                cd.flags = COVT_DESC_SPLIT | COVT_DESC_SPLIT_RLE;
+                cd.flags = COVT_DESC_SPLIT | fflag;
                 cd.avail = (int32_t)c;
-                p->descs.push_back(cd);
+                p->descs[o++] = cd;
                 for (int q = 1; q < COVT_SPLIT_SLOTS; ++q) {
                     covt_stream_desc pd{};
-                    pd.flags = COVT_DESC_SPLIT_PAD | COVT_DESC_SPLIT_RLE;
-                    if (q == 1) pd.in_off = (uint64_t)ch[c].s, pd.out_off = (uint64_t)ch[c].e;
-                    if (q == 2) pd.in_off = (uint64_t)ch[c].v0, pd.out_off = (uint64_t)ch[c].nv;
-                    if (q == 3) pd.in_off = (uint64_t)rs->second.second;
-                    p->descs.push_back(pd);
+                    pd.flags = COVT_DESC_SPLIT_PAD | fflag;
+                    if (q == 1) {
+                        pd.in_off = (uint64_t)(c * unit);
+                        pd.out_off = (uint64_t)std::min<int64_t>((c + 1) * unit, total);
+                    }
+                    p->descs[o++] = pd;
                 }
-                for (int q = 0; q < COVT_SPLIT_SLOTS; ++q) p->desc_stream.push_back((int64_t)i);
             }
-            p->fam_counts[fam] += (int64_t)ch.size() * COVT_SPLIT_SLOTS;
-            continue;
         }
-        // chunk c: bytes [c * split_chunk, min((c + 1) * split_chunk, byte_length)) of a varint stream,
-        // values [c * split_values, min((c + 1) * split_values, num_values)) of a FastPFOR stream
-        const bool fpf = fam == COVT_FAMILY_SPLIT_FPF;
-        const uint16_t fflag = fpf ? COVT_DESC_SPLIT_FPF : 0;
-        const int64_t unit = fpf ? split_values : split_chunk, total = fpf ? d.num_values : d.byte_length;
-        const int64_t nch = (total + unit - 1) / unit;
-        for (int64_t c = 0; c < nch; ++c) {
-            covt_stream_desc cd = d;
-            cd.flags = COVT_DESC_SPLIT | fflag;
-            cd.avail = (int32_t)c;
-            p->descs.push_back(cd);
-            for (int q = 1; q < COVT_SPLIT_SLOTS; ++q) {
-                covt_stream_desc pd{};
-                pd.flags = COVT_DESC_SPLIT_PAD | fflag;
-                if (q == 1) {
-                    pd.in_off = (uint64_t)(c * unit);
-                    pd.out_off = (uint64_t)std::min<int64_t>((c + 1) * unit, total);
-                }
-                p->descs.push_back(pd);
-            }
-            for (int q = 0; q < COVT_SPLIT_SLOTS; ++q) p->desc_stream.push_back((int64_t)i);
-        }
-        p->fam_counts[fam] += nch * COVT_SPLIT_SLOTS;
-    }
-    plan_geometry(p);
+    });
+    plan_geometry(p, n_thr);
     plan_property_layout(p);
     *out = p;
     return COVT_OK;
