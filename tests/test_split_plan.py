@@ -104,3 +104,29 @@ def test_split_threshold_relative_to_batch(covt, monkeypatch):
     assert one.family_counts[covt.FAMILY_SPLIT] > 0
     many = covt.Plan.from_tiles([_tile()] * 1000)
     assert many.family_counts[covt.FAMILY_SPLIT] == 0
+
+
+@pytest.mark.parametrize("props", [False, True])
+def test_plan_independent_of_host_threads(covt, monkeypatch, props):
+    """The plan's host phases (walk, records, launch keys, descriptors, geometry columns) run on ranges
+    of tiles / streams per thread with local offsets rebased afterwards: the plan must be byte-identical
+    for any thread count (COVT_PLAN_THREADS), splits and properties included."""
+    import glob
+
+    names = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "tiles", "omt", "*.covt")))[:40]
+    tiles = [open(n, "rb").read() for n in names] * 25  # 1000 tiles: up to 16 walk ranges (>= 64 tiles each)
+    flags = covt.PLAN_PROPERTIES if props else 0
+    monkeypatch.setenv("COVT_SPLIT_MIN", "4096")
+    plans = []
+    for thr in ("1", "3", "16"):
+        monkeypatch.setenv("COVT_PLAN_THREADS", thr)
+        p = covt.Plan.from_tiles(tiles, flags=flags)
+        plans.append(p)
+    a = plans[0]
+    assert a.family_counts[covt.FAMILY_SPLIT:].sum() > 0  # split descriptors exercised
+    for b in plans[1:]:
+        for f in ("descs", "desc_streams", "family_counts", "streams", "tile_status", "geom", "gdescs", "props",
+                  "pdescs"):
+            assert np.array_equal(getattr(a, f), getattr(b, f)), f
+        assert (a.in_bytes, a.out_bytes, a.vertices, a.output_bytes, a.assembly_bytes, a.property_bytes) == \
+               (b.in_bytes, b.out_bytes, b.vertices, b.output_bytes, b.assembly_bytes, b.property_bytes)
