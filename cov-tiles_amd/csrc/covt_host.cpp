@@ -1246,6 +1246,8 @@ int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const u
     return covt_plan_create_ex(bytes, tile_offsets, tile_sizes, n_tiles, format, id_mode, 0u, out);
 }
 
+}  // extern "C"
+
 namespace {
 // Chunks of a long ORC RLE v1 stream for the split kernel: a host walk of its group headers (orc-core
 // RunLengthIntegerReader / RunLengthByteReader framing: run = header, [delta,] base varint or byte;
@@ -1303,6 +1305,8 @@ std::vector<RleChunk> rle_chunks(const uint8_t* b, int32_t len, int op, int32_t 
     return ch;
 }
 }  // namespace
+
+extern "C" {
 
 int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
                         int32_t n_tiles, int32_t format, int32_t id_mode, uint32_t flags, covt_plan** out) {
