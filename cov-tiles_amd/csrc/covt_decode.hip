@@ -1850,11 +1850,23 @@ __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, co
 // the block headers before its range itself, so chunks depend on each other only through the sums.
 template <int OP>
 __device__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v1, int32_t chunk, covt_stream_result* res,
-                                   int64_t t) {
+                                   int64_t t, const covt_stream_desc* __restrict__ cd) {
     constexpr bool kXY = OP == COVT_OP_FPF_ZZ_DELTA_XY;
     Carry carry{0u, 0u};
     int32_t err = 0;
     FpfSkip skip;
+    {  // the plan's walk of the headers before the chunk (pads [2..7], covt_host.cpp fpf_chunk_states)
+        auto slot = [&](int i) -> const int32_t* {
+            return (const int32_t*)((const uint8_t*)(cd + 2 + i / 7) + covt_fpf_state_byte(i % 7));
+        };
+        if (uni(*slot(0)) == 1) {
+            const int l = lane_id();
+            skip.done = uni(*slot(1));
+            skip.cur0 = uni(*slot(2));
+            skip.pk = uni(*slot(3));
+            skip.xc = l <= 32 ? *slot(4 + l) : 0;
+        }
+    }
 #pragma nounroll
     for (int pass = 0; pass < 2; ++pass) {  // one inlined copy of the decoder for both passes
         Carry sums{0u, 0u};
@@ -1956,9 +1968,9 @@ __device__ int64_t decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ 
     }
     if constexpr (FPF) {
         switch (d.op) {
-        case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor_chunk<COVT_OP_FPF_ZZ_DELTA_I32>(c, s, e, chunk, res, t); break;
-        case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor_chunk<COVT_OP_FPF_ZZ_DELTA_XY>(c, s, e, chunk, res, t); break;
-        default: run_fastpfor_chunk<COVT_OP_FPF_DELTA_MORTON>(c, s, e, chunk, res, t); break;
+        case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor_chunk<COVT_OP_FPF_ZZ_DELTA_I32>(c, s, e, chunk, res, t, descs + kSplitSlots * t); break;
+        case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor_chunk<COVT_OP_FPF_ZZ_DELTA_XY>(c, s, e, chunk, res, t, descs + kSplitSlots * t); break;
+        default: run_fastpfor_chunk<COVT_OP_FPF_DELTA_MORTON>(c, s, e, chunk, res, t, descs + kSplitSlots * t); break;
         }
         return t;
     }

@@ -1304,6 +1304,76 @@ std::vector<RleChunk> rle_chunks(const uint8_t* b, int32_t len, int op, int32_t 
     if (ch.size() < 2) ch.clear();
     return ch;
 }
+
+// FastPFOR split chunks: each chunk's state at its first block, from a host walk of the page directories
+// and block headers (JavaFastPFOR FastPFOR.decodePage framing, read exactly as run_fastpfor's pre-walk
+// does): the container offset of the block's header, its packed-word index and the exception cursor of
+// every dataTobePacked array.  The chunk then skips walking up to 255 headers before its range (the
+// critical path of BASELINE config 3).  Stored in the chunk's pads [2..7], seven int32 slots each (all
+// fields but op / num_bits / flags; covt_fpf_state_slot): [0] 1 = present, [1] the page's first value,
+// [2] header offset, [3] packed word, [4 + k] cursor of array k (k = 0..32).  Where the walk cannot
+// follow the framing it stops: later chunks get no state and walk (and report the error) on the device.
+void fpf_chunk_states(const uint8_t* b, int32_t byte_length, int32_t n, int64_t unit, int64_t nch,
+                      std::vector<int32_t>& st) {
+    st.assign((size_t)nch * kFpfStateSlots, 0);
+    const int64_t nw = byte_length / 4;
+    if (nw <= 0 || unit % 256) return;
+    auto W = [&](int64_t i) -> uint32_t {
+        return ((uint32_t)b[4 * i] << 24) | ((uint32_t)b[4 * i + 1] << 16) | ((uint32_t)b[4 * i + 2] << 8) | b[4 * i + 3];
+    };
+    int32_t L = (int32_t)W(0);
+    if (L < 0) return;
+    L -= L % 256;
+    if (L > n) return;
+    int64_t p = 1;
+    int32_t done = 0;
+    while (done < L) {
+        const int32_t thissize = std::min<int32_t>(L - done, 65536);
+        const int64_t p0 = p;
+        if (p0 >= nw) return;
+        int64_t ie = p0 + (int32_t)W(p0);
+        if (ie < 0 || ie >= nw) return;
+        const int32_t bytesize = (int32_t)W(ie++);
+        if (bytesize < 0 || bytesize > 3 * 65536 / 256 + 65536) return;
+        const int64_t bcw = (bytesize + 3) / 4, bc = ie;
+        if (bc + bcw >= nw) return;
+        ie += bcw;
+        uint32_t bm = W(ie++) & ~1u;  // (bc + bcw < nw)
+        while (bm) {
+            const int32_t k = __builtin_ctz(bm) + 1;
+            bm &= bm - 1;
+            if (ie >= nw) return;
+            const int32_t size = (int32_t)W(ie++);
+            if (size < 0) return;
+            const int64_t groups = ((int64_t)size + 31) / 32;
+            ie += groups * k - ((groups * 32 - size) * k) / 32;
+        }
+        const int32_t bclen = (int32_t)(bcw * 4), nblk = thissize / 256;
+        auto cb = [&](int32_t q) -> uint32_t { return b[4 * bc + (q ^ 3)]; };  // container byte q
+        int32_t cur = 0, xc[33] = {};
+        int64_t pk = p0 + 1;
+        for (int32_t j = 0; j < nblk; ++j) {
+            const int64_t v = (int64_t)done + (int64_t)j * 256;
+            if (j > 0 && v % unit == 0 && v / unit < nch) {  // chunk v / unit starts at block j of this page
+                int32_t* s = st.data() + (size_t)(v / unit) * kFpfStateSlots;
+                s[0] = 1;
+                s[1] = done;
+                s[2] = cur;
+                s[3] = (int32_t)pk;
+                for (int k = 0; k <= 32; ++k) s[4 + k] = xc[k];
+            }
+            if (cur + 3 > bclen + 1) return;  // (the device reads the header word through its window)
+            const int32_t hb = (int32_t)(int8_t)cb(cur), ce = (int32_t)cb(cur + 1);
+            const int32_t idx = ce > 0 && cur + 2 < bclen ? (int32_t)(int8_t)cb(cur + 2) - hb : 0;
+            pk += 8 * hb;
+            if (ce > 0 && idx >= 2 && idx <= 32) xc[idx] += ce;
+            cur += ce > 0 ? 3 + ce : 2;
+            if (cur > bclen) return;
+        }
+        done += thissize;
+        p = ie;
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -1579,6 +1649,8 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
             const uint16_t fflag = fpf ? COVT_DESC_SPLIT_FPF : 0;
             const int64_t unit = fpf ? split_values : split_chunk, total = fpf ? d.num_values : d.byte_length;
             const int64_t nch = (total + unit - 1) / unit;
+            std::vector<int32_t> fst;
+            if (fpf) fpf_chunk_states(bytes + si.in_off, si.byte_length, d.num_values, unit, nch, fst);
             for (int64_t c = 0; c < nch; ++c) {
                 covt_stream_desc cd = d;
                 cd.flags = COVT_DESC_SPLIT | fflag;
@@ -1591,6 +1663,10 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
                         pd.in_off = (uint64_t)(c * unit);
                         pd.out_off = (uint64_t)std::min<int64_t>((c + 1) * unit, total);
                     }
+                    if (fpf && q >= 2)
+                        for (int k = 0; k < 7; ++k)
+                            std::memcpy((uint8_t*)&pd + covt_fpf_state_byte(k), &fst[(size_t)c * kFpfStateSlots + (size_t)(q - 2) * 7 + (size_t)k],
+                                        4);
                     p->descs[o++] = pd;
                 }
             }

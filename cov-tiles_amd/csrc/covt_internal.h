@@ -62,4 +62,9 @@ inline bool split_stream(int op, int32_t num_values, int64_t cost, int64_t split
     return split_op(op) && !(op == COVT_OP_VARINT_ZZ_DELTA_XY && (num_values & 1));
 }
 
+// FastPFOR split chunks: the host-walked start state in pads [2..7] of the chunk (covt_host.cpp
+// fpf_chunk_states): seven int32 slots per pad, every field but op / num_bits / flags
+constexpr int kFpfStateSlots = 42;
+__host__ __device__ constexpr int covt_fpf_state_byte(int k) { return k < 6 ? 4 * k : 28; }
+
 #endif
