@@ -151,7 +151,9 @@ enum covt_op {
  * written to its chunk 0's entry.  Split descriptors need the grouped launch. */
 #define COVT_DESC_SPLIT 0x2u
 #define COVT_DESC_SPLIT_PAD 0x4u
-#define COVT_DESC_SPLIT_FPF 0x8u /* with SPLIT / SPLIT_PAD: a FastPFOR stream's chunk */
+#define COVT_DESC_SPLIT_FPF 0x8u /* with SPLIT / SPLIT_PAD: a FastPFOR stream's chunk (pads [2..7]: the plan's
+                                  * host walk of the headers before it -- int32 slots in every field but
+                                  * op / num_bits / flags; all zero = none, the chunk walks them itself) */
 #define COVT_DESC_SPLIT_RLE 0x10u /* with SPLIT / SPLIT_PAD: an ORC RLE stream's chunk (whole groups, located by the
                                    * plan; pads [1] bytes [s, e), [2] values (first, count), [3] consumed) */
 #define COVT_SPLIT_SLOTS 8
