@@ -677,10 +677,17 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
         add(kSplitR, COVT_FAMILY_RLE, COVT_FAMILY_LANE);
         add(kSplitF, -1, -1);
     } else {
-        add(COVT_FAMILY_FASTPFOR, -1, -1);
-        add(COVT_FAMILY_VARINT, -1, -1);
-        add(COVT_FAMILY_RLE, -1, -1);
-        add(COVT_FAMILY_LANE, -1, -1);
+        // queue order (A/B knob COVT_QUEUE_ORDER: four family digits, e.g. 2103 = FastPFOR, varint, RLE, lane)
+        const int64_t ord = env_i64("COVT_QUEUE_ORDER", 2103);
+        int fo[4] = {COVT_FAMILY_FASTPFOR, COVT_FAMILY_VARINT, COVT_FAMILY_RLE, COVT_FAMILY_LANE};
+        bool seen[4] = {false, false, false, false}, ok = ord >= 0 && ord <= 3333;
+        for (int i = 0; i < 4 && ok; ++i) {
+            const int f = (int)(ord / (int64_t)(i == 0 ? 1000 : i == 1 ? 100 : i == 2 ? 10 : 1) % 10);
+            ok = f <= 3 && !seen[f];
+            if (ok) seen[f] = true, fo[i] = f;
+        }
+        if (!ok) fo[0] = COVT_FAMILY_FASTPFOR, fo[1] = COVT_FAMILY_VARINT, fo[2] = COVT_FAMILY_RLE, fo[3] = COVT_FAMILY_LANE;
+        for (int f : fo) add(f, -1, -1);
     }
     if (nq > 1 && hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
     int st = COVT_OK;
