@@ -130,3 +130,88 @@ def test_plan_independent_of_host_threads(covt, monkeypatch, props):
             assert np.array_equal(getattr(a, f), getattr(b, f)), f
         assert (a.in_bytes, a.out_bytes, a.vertices, a.output_bytes, a.assembly_bytes, a.property_bytes) == \
                (b.in_bytes, b.out_bytes, b.vertices, b.output_bytes, b.assembly_bytes, b.property_bytes)
+
+
+def _fpf_states_py(b, n, unit, nch):
+    """Independent restatement of the chunk start states (JavaFastPFOR FastPFOR.decodePage framing):
+    per chunk starting inside a page at block j > 0, (page's first value, header offset, packed word,
+    exception cursor per array 0..32); None where the chunk starts a page or lies past the blocks."""
+    W = np.frombuffer(b[: len(b) // 4 * 4], dtype=">u4").astype(np.int64)
+    L = int(W[0]) if W[0] < 2 ** 31 else -1
+    out = [None] * nch
+    if L < 0:
+        return out
+    L -= L % 256
+    p, done = 1, 0
+    while done < L:
+        size = min(L - done, 65536)
+        ie = p + int(W[p])
+        bcw = (int(W[ie]) + 3) // 4
+        bc = ie + 1
+        ie = bc + bcw
+        bm = int(W[ie]) & ~1
+        ie += 1
+        for k in range(2, 33):
+            if bm >> (k - 1) & 1:
+                sz = int(W[ie])
+                ie += 1
+                g = (sz + 31) // 32
+                ie += g * k - ((g * 32 - sz) * k) // 32
+        cont = b"".join(int(x).to_bytes(4, "little") for x in W[bc: bc + bcw])  # container byte order
+        cur, pk, xc = 0, p + 1, [0] * 33
+        for j in range(size // 256):
+            v = done + 256 * j
+            if j > 0 and v % unit == 0 and v // unit < nch:
+                out[v // unit] = (done, cur, pk, tuple(xc))
+            bb = int(np.int8(cont[cur])) if cur < len(cont) else 0
+            ce = cont[cur + 1]
+            if ce:
+                idx = int(np.int8(cont[cur + 2])) - bb
+                if 2 <= idx <= 32:
+                    xc[idx] += ce
+                cur += 3 + ce
+            else:
+                cur += 2
+            pk += 8 * bb
+        done += size
+        p = ie
+    return out
+
+
+def test_fastpfor_chunk_states(covt, monkeypatch):
+    """The plan's host walk of the FastPFOR block headers before each split chunk (pads [2..7] of the
+    chunk, int32 slots in every field but op / num_bits / flags) equals an independent Python walk."""
+    monkeypatch.setenv("COVT_SPLIT_MIN", "256")
+    monkeypatch.setenv("COVT_SPLIT_RATIO", "0")
+    monkeypatch.setenv("COVT_SPLIT_VALUES", "512")
+    plan = covt.Plan.from_tiles([_tile("14_8298_10748"), _tile()])
+    raw = plan.descs.reshape(-1, 32)
+    d = plan.descs.view(DESC)
+    f0 = int(plan.family_counts[:covt.FAMILY_SPLIT_FPF].sum())
+    nf = int(plan.family_counts[covt.FAMILY_SPLIT_FPF])
+    offs = [0, 4, 8, 12, 16, 20, 28]
+
+    def slots(k):
+        return [int(np.frombuffer(raw[k + 2 + i // 7][offs[i % 7]:offs[i % 7] + 4].tobytes(), dtype="<i4")[0])
+                for i in range(37)]
+
+    st = plan.streams
+    checked = 0
+    cache = {}
+    for k in range(f0, f0 + nf, covt.SPLIT_SLOTS):
+        i = int(plan.desc_streams[k])
+        s = st[i]
+        if i not in cache:
+            b = plan.blob[int(s["in_off"]): int(s["in_off"]) + int(s["byte_length"])].tobytes()
+            nch = -(-int(s["num_values"]) // 512)
+            cache[i] = _fpf_states_py(b, int(s["num_values"]), 512, nch)
+        c = int(d[k]["avail"])
+        got = slots(k)
+        want = cache[i][c]
+        if want is None:
+            assert got[0] == 0
+            continue
+        assert got[0] == 1
+        assert (got[1], got[2], got[3], tuple(got[4:37])) == want
+        checked += 1
+    assert checked > 10
