@@ -759,6 +759,26 @@ class DeviceSubset:
                                                         self.d_res.data_ptr(), s.cuda_stream),
                "covt_decode_streams_device_grouped")
 
+    def decode_graph(self):
+        """This subset's launch replayed from a captured HIP graph on the current torch stream (as
+        DeviceBatch.decode_graph): the split-record memset, the fork, every family and chunk kernel on
+        its queue and the join become one graph launch."""
+        import torch
+
+        g = getattr(self, "_graph", None)
+        if g is None:
+            dev = self.batch.device
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):  # the fork streams and events exist before the capture
+                self.decode(side)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.decode(torch.cuda.current_stream(dev))
+            self._graph = g
+        g.replay()
+
     def results(self):
         """(full output bytes, results[k, 2] of the subset's k streams, their plan-order indices)."""
         out = self.batch.d_out.cpu().numpy()[:self.batch.plan.output_bytes]
