@@ -1578,6 +1578,7 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
             if (!ch.empty()) rle_split.emplace(i, std::make_pair(std::move(ch), consumed));
         }
     }
+    const int64_t fpf_w = std::max<int64_t>(1, env_i64("COVT_FPF_SPLIT_WEIGHT", 1));
     // descriptors per stream: 1, or COVT_SPLIT_SLOTS per chunk of a split stream
     std::vector<int32_t> ndesc(ns);
     par_for(n_thr, (int64_t)ns, [&](int64_t i0, int64_t i1) {
@@ -1587,7 +1588,10 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
             const bool lane = lane_stream(s.op, s.desc_index, s.byte_length, lane_max);
             const auto rs = rle_split.empty() ? rle_split.end() : rle_split.find(i);
             const bool rsplit = rs != rle_split.end();
-            const bool split = split_stream(s.op, s.desc_index, stream_cost(s), split_min, split_values) || rsplit;
+            // (FastPFOR: a wave's time follows the blocks, i.e. the values: their output counts fpf_w times)
+            const int64_t scost = split_fpf_op(s.op) ? stream_cost(s) + (fpf_w - 1) * (s.out_elems * s.elem_bytes / 4)
+                                                     : stream_cost(s);
+            const bool split = split_stream(s.op, s.desc_index, scost, split_min, split_values) || rsplit;
             const uint64_t fam = split ? (uint64_t)(split_fpf_op(s.op) ? COVT_FAMILY_SPLIT_FPF
                                                     : rsplit           ? COVT_FAMILY_SPLIT_RLE
                                                                        : COVT_FAMILY_SPLIT)
