@@ -1256,6 +1256,11 @@ int covt_decode_fastpfor_delta_morton_codes(const uint8_t* buf, size_t buf_len, 
                     2 * (size_t)std::max(n_vertices, 0));
 }
 
+// Test hook (not in covt.h): the plan's FastPFOR chunk start states for one stream, nch x 42 int32
+// (the slots of pads [2..7], covt_internal.h kFpfStateSlots), as fpf_chunk_states computes them.
+int covt_debug_fpf_chunk_states(const uint8_t* stream, int32_t byte_length, int32_t num_values, int64_t unit,
+                                int64_t nch, int32_t* out);
+
 int covt_plan_create(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
                      int32_t n_tiles, int32_t format, int32_t id_mode, covt_plan** out) {
     return covt_plan_create_ex(bytes, tile_offsets, tile_sizes, n_tiles, format, id_mode, 0u, out);
@@ -2048,3 +2053,12 @@ int covt_plan_properties_host(const covt_plan* p, const uint8_t* bytes, uint64_t
 }
 
 }  // extern "C"
+
+extern "C" int covt_debug_fpf_chunk_states(const uint8_t* stream, int32_t byte_length, int32_t num_values, int64_t unit,
+                                           int64_t nch, int32_t* out) {
+    if (!out || nch < 0 || byte_length < 0 || (!stream && byte_length)) return COVT_ERR_INVALID_ARG;
+    std::vector<int32_t> st;
+    fpf_chunk_states(stream, byte_length, num_values, unit, nch, st);
+    std::copy(st.begin(), st.end(), out);
+    return COVT_OK;
+}

@@ -78,8 +78,9 @@ def _j4_count(b: bytes) -> int:
     return n
 
 
-def _split_launch(covt, buf: bytes, op: int, n: int, nb: int, chunk: int, out_bytes: int, fpf=False):
-    """One split stream through the grouped launch: byte chunks (varint) or value chunks (FastPFOR)."""
+def _split_launch(covt, buf: bytes, op: int, n: int, nb: int, chunk: int, out_bytes: int, fpf=False, states=None):
+    """One split stream through the grouped launch: byte chunks (varint) or value chunks (FastPFOR).
+    states: FastPFOR chunk start states (nch x 42 int32, the plan's host walk) for pads [2..7]."""
     import ctypes as C
 
     import torch
@@ -94,6 +95,11 @@ def _split_launch(covt, buf: bytes, op: int, n: int, nb: int, chunk: int, out_by
         d[k] = (0, 0, c, n, op, nb, covt.DESC_SPLIT | fl, bl)
         d[k + 1 : k + covt.SPLIT_SLOTS]["flags"] = covt.DESC_SPLIT_PAD | fl
         d[k + 1]["in_off"], d[k + 1]["out_off"] = c * chunk, min((c + 1) * chunk, total)
+        if states is not None:  # seven int32 slots per pad, every field but op / num_bits / flags
+            raw = d.view(np.uint8).reshape(-1, 32)
+            for i in range(42):
+                o = (0, 4, 8, 12, 16, 20, 28)[i % 7]
+                raw[k + 2 + i // 7, o:o + 4] = np.frombuffer(np.int32(states[c, i]).tobytes(), dtype=np.uint8)
     counts = np.zeros(covt.NUM_FAMILIES, dtype=np.int64)
     counts[covt.FAMILY_SPLIT_FPF if fpf else covt.FAMILY_SPLIT] = d.size
     dev = torch.device("cuda")
@@ -222,6 +228,50 @@ def test_fastpfor_streams_split(covt, oracle, gpu_available, values):
             assert int(r[0]) == 0 and np.array_equal(out.view(np.int32), np.asarray(o[1], dtype=np.int32))
         n_checked += 1
     assert n_checked > 40
+
+
+@pytest.mark.parametrize("values", [256, 2048])
+def test_fastpfor_split_host_states(covt, oracle, gpu_available, values):
+    """FastPFOR chunks given the plan's host walk of the headers before them (pads [2..7], as
+    covt_plan_create leaves them; covt_debug_fpf_chunk_states): bit-exact with the oracle on well-formed
+    single- and multi-page streams; on bit-flipped ones a status, and the oracle's arrays whenever it
+    decodes (states present before the damage, absent after it)."""
+    from test_gpu_synthetic import _fpf_values
+    from test_split_plan import _states_hook
+
+    rng = np.random.default_rng(100 + values)
+    n_checked = 0
+    for n in (1000, 4096 + 77, 65536 + 256 + 13, 140000):
+        enc = oracle.encode_fastpfor(_fpf_values(rng, n))
+        st = _states_hook(covt, enc, n, values)
+        assert st[:, 0].sum() > 0 or n <= values  # (one chunk: nothing before it to walk)
+        for op, nb in ((covt.OP_FPF_ZZ_DELTA_I32, 0), (covt.OP_FPF_ZZ_DELTA_XY, 0), (covt.OP_FPF_DELTA_MORTON, 14)):
+            if op == covt.OP_FPF_ZZ_DELTA_XY and n & 1:
+                continue
+            if op == covt.OP_FPF_ZZ_DELTA_I32:
+                o = oracle.decode_fastpfor_zigzag_delta(enc, n, len(enc), 0)
+            elif op == covt.OP_FPF_ZZ_DELTA_XY:
+                o = oracle.decode_fastpfor_delta_coordinates(enc, n, len(enc), 0)
+            else:
+                o = oracle.decode_fastpfor_delta_morton_codes(enc, n, len(enc), 0, nb)
+            ne = 2 * n if nb else n
+            out, r = _split_launch(covt, enc, op, n, nb, values, 4 * ne, fpf=True, states=st)
+            assert o[0] == 0 and int(r[0]) == 0 and int(r[1]) == len(enc), (n, op)
+            assert np.array_equal(out.view(np.int32), np.asarray(o[1], dtype=np.int32)), (n, op)
+            n_checked += 1
+    enc = oracle.encode_fastpfor(_fpf_values(rng, 70000))
+    for _ in range(16):
+        e = bytearray(enc)
+        for _ in range(int(rng.integers(1, 4))):
+            e[int(rng.integers(0, len(e)))] ^= 1 << int(rng.integers(0, 8))
+        e = bytes(e)
+        st = _states_hook(covt, e, 70000, values)
+        o = oracle.decode_fastpfor_zigzag_delta(e, 70000, len(e), 0)
+        out, r = _split_launch(covt, e, covt.OP_FPF_ZZ_DELTA_I32, 70000, 0, values, 4 * 70000, fpf=True, states=st)
+        if o[0] == 0:  # (as the one-wave test: a status always, the oracle's arrays whenever it decodes)
+            assert int(r[0]) == 0 and np.array_equal(out.view(np.int32), np.asarray(o[1], dtype=np.int32))
+        n_checked += 1
+    assert n_checked > 20
 
 
 def _u64_count(b: bytes) -> int:

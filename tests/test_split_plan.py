@@ -215,3 +215,48 @@ def test_fastpfor_chunk_states(covt, monkeypatch):
         assert (got[1], got[2], got[3], tuple(got[4:37])) == want
         checked += 1
     assert checked > 10
+
+
+def _states_hook(covt, body, n, unit):
+    import ctypes as C
+
+    nch = -(-n // unit)
+    out = np.zeros(max(nch, 1) * 42, dtype=np.int32)
+    buf = np.frombuffer(body, dtype=np.uint8) if body else np.zeros(1, dtype=np.uint8)
+    st = covt.lib().covt_debug_fpf_chunk_states(buf.ctypes.data_as(C.POINTER(C.c_uint8)), len(body), n,
+                                                C.c_int64(unit), C.c_int64(nch),
+                                                out.ctypes.data_as(C.POINTER(C.c_int32)))
+    assert st == 0
+    return out[: nch * 42].reshape(nch, 42)
+
+
+def test_fastpfor_chunk_states_synthetic(covt, oracle):
+    """The plan's FastPFOR chunk-state walk (covt_debug_fpf_chunk_states) on synthetic streams: equal to
+    the Python restatement on well-formed single- and multi-page streams at several chunk sizes; on
+    bit-flipped streams it never reads outside the stream and marks states present or absent (0 / 1)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_gpu_synthetic import _fpf_values
+
+    rng = np.random.default_rng(7)
+    checked = 0
+    for n in (1000, 4096 + 77, 65536 + 256 + 13, 140000):
+        enc = oracle.encode_fastpfor(_fpf_values(rng, n))
+        for unit in (256, 1024, 2048):
+            got = _states_hook(covt, enc, n, unit)
+            want = _fpf_states_py(enc, n, unit, got.shape[0])
+            for c, w in enumerate(want):
+                if w is None:
+                    assert got[c, 0] == 0, (n, unit, c)
+                    continue
+                assert got[c, 0] == 1 and (got[c, 1], got[c, 2], got[c, 3], tuple(got[c, 4:37])) == w, (n, unit, c)
+                checked += 1
+    assert checked > 100
+    enc = oracle.encode_fastpfor(_fpf_values(rng, 70000))
+    for _ in range(40):
+        e = bytearray(enc)
+        for _ in range(int(rng.integers(1, 4))):
+            e[int(rng.integers(0, len(e)))] ^= 1 << int(rng.integers(0, 8))
+        got = _states_hook(covt, bytes(e), 70000, 512)
+        assert set(np.unique(got[:, 0]).tolist()) <= {0, 1}
