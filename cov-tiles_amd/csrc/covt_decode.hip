@@ -59,6 +59,7 @@ struct __attribute__((aligned(16))) WaveSmem {
             uint32_t win[kWin / 4 + 4];    // window bytes (+16 B slack for 12-byte reads)
             uint16_t list[kWin];           // terminator positions (window-relative)
             uint16_t next[kWin + 8];       // RLE: start of the next group if a header sat at j (+sentinel)
+            uint16_t grec[64];             // RLE: the chain walk's successor of each step (int RLE)
         } v;
         struct {
             uint32_t stage[324];  // packed words of one FastPFOR block (<= 1024 + 15 B)
@@ -69,7 +70,7 @@ struct __attribute__((aligned(16))) WaveSmem {
     } u;
 };
 constexpr int kSmemHdr = 272;  // offsetof(WaveSmem, u), checked below
-constexpr int kFamSmemRle = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2 + (kWin + 8) * 2;
+constexpr int kFamSmemRle = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2 + (kWin + 8) * 2 + 64 * 2;
 constexpr int kFamSmemVarint = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2;
 constexpr int kFamSmemFpf = kSmemHdr + (324 + 256 + 260) * 4 + 384 > kFamSmemVarint
                                 ? kSmemHdr + (324 + 256 + 260) * 4 + 384
@@ -822,23 +823,30 @@ __device__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
                 // Eight steps per scalar test, branch-free: the chain's critical path is one LDS read
                 // whose result is the next read's address.  Steps past the end are no-ops (the sentinel
                 // points at itself); lanes left at ~0 hold no group.
-                gs = ~0u;
                 auto rd = [](uint32_t a) -> uint32_t { return *(lds_cu16*)(uintptr_t)a; };
-                uint32_t cur = nb + 2u * (uint32_t)pj, nx = rd(cur);
+                uint16_t* const rec = sm.u.v.grec;
+                const uint32_t c0 = nb + 2u * (uint32_t)pj;
+                uint32_t nx = rd(c0);
+                int32_t steps = 64;
                 for (int32_t g0 = 0; g0 < 64; g0 += 8) {
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
-                        const uint32_t nn = rd(nx);
-                        const bool ok = nx != sent;
-                        gs = (ok && l == g0 + k) ? cur : gs;
-                        cur = ok ? nx : cur;
-                        nx = nn;
+                        rec[g0 + k] = (uint16_t)nx;
+                        nx = rd(nx);
                     }
-                    if (uniu(nx) == sent) break;
+                    if (uniu(nx) == sent) {
+                        steps = g0 + 8;
+                        break;
+                    }
                 }
-                G = __popcll(__ballot(gs != ~0u));
-                gs = gs != ~0u ? (gs - nb) >> 1 : gs;  // positions
-                pj = (int32_t)((uniu(cur) - nb) >> 1);
+                wave_sync();
+                const uint32_t mine = l < steps ? (uint32_t)rec[l] : sent;
+                const uint32_t prev = l == 0 ? c0 : (l <= steps ? (uint32_t)rec[l - 1] : sent);
+                const bool gv0 = mine != sent;
+                G = __popcll(__ballot(gv0));
+                gs = gv0 ? (prev - nb) >> 1 : ~0u;  // positions
+                pj = G > 0 ? (int32_t)((lane_bcast(mine, G - 1) - nb) >> 1) : pj;
+                wave_sync();
             }
             COVT_PHASE(c, 2);
             if (G == 0) {
