@@ -239,6 +239,40 @@ def abi_host_leg(plan, t_plan, reps):
                     "raw_tiles_to_host_ms adds the host metadata walk (covt_plan_create)"}
 
 
+def device_plan_leg(plan, batch, torch, dev, covt, args, t_plan):
+    """covt_device_plan_create on the batch already in HBM (include/covt.h "Device-side plan"): the
+    container walk, prefix sums, launch-order sort and descriptor fill on the GPU, wall-clock per
+    creation (it synchronises twice: the stream count sizes its arrays), median over --device-plan-reps
+    after one warm-up.  Its descriptors must equal the host plan's (nothing splits at this size), and
+    the decode launch from them runs at the same speed."""
+    offs = torch.from_numpy(plan.offsets.astype(np.int64)).to(dev)
+    sizes = torch.from_numpy(plan.sizes.astype(np.int64)).to(dev)
+    dp = covt.DevicePlan(batch.d_in, offs, sizes, covt.FORMAT_GENC, args.id_mode)
+    _, descs, st = dp.host_copy()
+    same = bool(descs.tobytes() == plan.descs.tobytes() and np.array_equal(st, plan.tile_status))
+    dp.close()
+    times = []
+    for k in range(args.device_plan_reps):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        dp = covt.DevicePlan(batch.d_in, offs, sizes, covt.FORMAT_GENC, args.id_mode)
+        times.append(time.perf_counter() - t0)
+        if k < args.device_plan_reps - 1:
+            dp.close()
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for s_, e_ in ev:
+        s_.record(stream)
+        dp.decode(batch.d_out, batch.d_res, stream)
+        e_.record(stream)
+    torch.cuda.synchronize(dev)
+    _, res = batch.results()
+    return {"ms_median": round(float(np.median(times)) * 1e3, 3), "ms_min": round(min(times) * 1e3, 3),
+            "host_plan_ms": round(t_plan * 1e3, 1), "streams": dp.num_streams,
+            "descs_equal_host_plan": same, "decode_ms": round(float(np.mean([a.elapsed_time(b) for a, b in ev])), 4),
+            "decode_errors": int((res[:, 0] != 0).sum()), "reps": args.device_plan_reps}
+
+
 def assembly_leg(batch, plan, stream, args, dist, torch, dev):
     """GPU geometry assembly (nested offsets + ICE gather) over the decoded batch,
     timed on its own (decode output resident); not part of `value`."""
@@ -463,6 +497,7 @@ def main():
     ap.add_argument("--e2e-reps", type=int, default=3, help="end-to-end (PCIe-inclusive) reps; 0 skips")
     ap.add_argument("--no-props", action="store_true", help="skip the property-column leg")
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE config 2-4 legs")
+    ap.add_argument("--device-plan-reps", type=int, default=5, help="device-side plan creations timed; 0 skips")
     ap.add_argument("--abi-host-reps", type=int, default=2,
                     help="reps of the C-ABI host entry covt_plan_decode_host (pageable in/out); 0 skips")
     ap.add_argument("--dry-run", action="store_true",
@@ -556,6 +591,8 @@ def main():
             legs["end_to_end"] = end_to_end(plan, batch, stream, torch, dev, args.e2e_reps)
         if args.abi_host_reps > 0 and rank == 0:
             legs["c_abi_host"] = abi_host_leg(plan, t_plan, args.abi_host_reps)
+        if args.device_plan_reps > 0:
+            legs["device_plan"] = device_plan_leg(plan, batch, torch, dev, covt, args, t_plan)
         if not args.no_assemble and plan.num_geometry_columns:
             legs["assembly"] = assembly_leg(batch, plan, stream, args, dist, torch, dev)
         if not args.no_props:

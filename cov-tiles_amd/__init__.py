@@ -159,6 +159,10 @@ EXPORTED_SYMBOLS = (
     "covt_plan_property_columns", "covt_plan_property_descs", "covt_materialize_properties_device",
     "covt_plan_properties_host", "covt_decode_byte_rle_reencode", "covt_decode_floats_le", "covt_decode_string",
     "covt_plan_decode_host_shards", "covt_plan_release_device", "covt_plan_num_descs", "covt_plan_desc_streams",
+    "covt_device_plan_create", "covt_device_plan_destroy", "covt_device_plan_num_streams",
+    "covt_device_plan_output_bytes", "covt_device_plan_totals", "covt_device_plan_family_counts",
+    "covt_device_plan_descs_device", "covt_device_plan_streams_device", "covt_device_plan_tile_status_device",
+    "covt_device_plan_order_device", "covt_device_plan_copy", "covt_device_plan_decode",
 )
 
 
@@ -240,6 +244,21 @@ def lib() -> C.CDLL:
     L.covt_plan_property_descs.argtypes = [vp, vp]
     L.covt_materialize_properties_device.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp]
     L.covt_plan_properties_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
+    L.covt_device_plan_create.argtypes = [vp, C.c_uint64, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp,
+                                          C.POINTER(vp)]
+    L.covt_device_plan_destroy.argtypes = [vp]
+    L.covt_device_plan_destroy.restype = None
+    for name in ("covt_device_plan_num_streams", "covt_device_plan_output_bytes"):
+        getattr(L, name).argtypes = [vp]
+        getattr(L, name).restype = C.c_int64
+    L.covt_device_plan_totals.argtypes = [vp, i64p, i64p, i64p]
+    L.covt_device_plan_family_counts.argtypes = [vp, i64p]
+    for name in ("covt_device_plan_descs_device", "covt_device_plan_streams_device",
+                 "covt_device_plan_tile_status_device", "covt_device_plan_order_device"):
+        getattr(L, name).argtypes = [vp]
+        getattr(L, name).restype = vp
+    L.covt_device_plan_copy.argtypes = [vp, vp, vp, i32p]
+    L.covt_device_plan_decode.argtypes = [vp, vp, vp, vp, vp]
     L.covt_version.restype = C.c_char_p
     L.covt_device_count.argtypes = [i32p]
     _lib = L
@@ -732,6 +751,79 @@ class DeviceBatch:
         res_launch = self.d_res.cpu().numpy().reshape(-1, 2)[:self.plan.num_descs]
         res = res_launch[self.plan.streams["desc_index"]] if self.plan.num_streams else res_launch
         return out, res
+
+
+class DevicePlan:
+    """covt_device_plan_create: the Id / Geometry plan built on the GPU from tiles already in HBM.
+
+    `d_blob` is a uint8 torch tensor on the device holding the tiles, `offsets` / `sizes` the tiles'
+    byte ranges in it (host arrays or device tensors).  The walk, prefix sums, launch-order sort and
+    descriptor fill run on the current torch stream; the result has the host plan's layout exactly
+    (Plan.streams / Plan.descs / Plan.family_counts for a batch that splits nothing)."""
+
+    def __init__(self, d_blob, offsets, sizes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT, stream=None):
+        import torch
+
+        self.device = d_blob.device
+        if d_blob.dtype != torch.uint8 or not d_blob.is_contiguous() or d_blob.device.type != "cuda":
+            raise IllegalArgumentException("d_blob must be a contiguous uint8 device tensor")
+        self.d_in = d_blob
+        as_dev = lambda a: torch.as_tensor(np.asarray(a, dtype=np.int64) if not torch.is_tensor(a) else a,
+                                           dtype=torch.int64).to(self.device).contiguous()
+        self.d_off, self.d_size = as_dev(offsets), as_dev(sizes)
+        if self.d_off.numel() != self.d_size.numel():
+            raise IllegalArgumentException("offsets and sizes differ in length")
+        self.n_tiles = int(self.d_off.numel())
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            _raise(lib().covt_device_plan_create(d_blob.data_ptr(), d_blob.numel(), self.d_off.data_ptr(),
+                                                 self.d_size.data_ptr(), self.n_tiles, fmt, id_mode,
+                                                 s.cuda_stream, C.byref(h)), "covt_device_plan_create")
+        self._h = h
+        L = lib()
+        self.num_streams = L.covt_device_plan_num_streams(h)
+        self.output_bytes = L.covt_device_plan_output_bytes(h)
+        self.family_counts = np.zeros(NUM_FAMILIES, dtype=np.int64)
+        L.covt_device_plan_family_counts(h, _ptr(self.family_counts, C.c_int64))
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        L.covt_device_plan_totals(h, C.byref(a), C.byref(b), C.byref(c))
+        self.in_bytes, self.out_payload, self.vertices = a.value, b.value, c.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().covt_device_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def host_copy(self):
+        """(stream records in tile order, descriptors in launch order, tile statuses) as host arrays."""
+        info = np.zeros(self.num_streams, dtype=STREAM_INFO_DTYPE)
+        descs = np.zeros(self.num_streams * 32, dtype=np.uint8)
+        st = np.zeros(max(self.n_tiles, 1), dtype=np.int32)
+        _raise(lib().covt_device_plan_copy(self._h, info.ctypes.data, descs.ctypes.data, _ptr(st, C.c_int32)),
+               "covt_device_plan_copy")
+        return info, descs, st[:self.n_tiles]
+
+    def alloc(self):
+        """(output buffer, result buffer) on the device, sized for this plan."""
+        import torch
+
+        return (torch.zeros(max(self.output_bytes, 16), dtype=torch.uint8, device=self.device),
+                torch.zeros(max(self.num_streams, 1) * 2, dtype=torch.int32, device=self.device))
+
+    def decode(self, d_out, d_res, stream=None):
+        """Enqueue the grouped decode launch over this plan's descriptors."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _raise(lib().covt_device_plan_decode(self._h, self.d_in.data_ptr(), d_out.data_ptr(), d_res.data_ptr(),
+                                             s.cuda_stream), "covt_device_plan_decode")
 
 
 class DeviceSubset:

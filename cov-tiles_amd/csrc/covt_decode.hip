@@ -26,6 +26,7 @@
 #include "covt.h"
 #include "covt_internal.h"
 #include "covt_wave.h"
+#include "covt_walk.h"
 
 namespace covt {
 
@@ -1997,14 +1998,7 @@ __device__ int64_t decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ 
     return t;
 }
 
-__host__ __device__ constexpr int op_family(int op) {
-    return (op >= COVT_OP_FPF_ZZ_DELTA_I32 && op <= COVT_OP_FPF_DELTA_MORTON) ? COVT_FAMILY_FASTPFOR
-           : ((op >= COVT_OP_VARINT_I32 && op <= COVT_OP_VARINT_DELTA_MORTON) ||
-              (op >= COVT_OP_VARINT_U64 && op <= COVT_OP_VARINT_ZZ_DELTA_I64) ||
-              (op >= COVT_OP_VARINT_ZZ_I32_AS_I64 && op <= COVT_OP_VARINT_ZZ_DELTA_S64))
-               ? COVT_FAMILY_VARINT
-               : COVT_FAMILY_RLE;  // RLE ops and COVT_OP_NONE / unknown ops (reported as unsupported)
-}
+__host__ __device__ constexpr int op_family(int op) { return covt_op_family(op); }
 
 // One wave per descriptor; waves whose descriptor belongs to another family return at once (used
 // when the caller's descriptors are not grouped by family).

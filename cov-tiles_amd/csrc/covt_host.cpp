@@ -21,20 +21,9 @@
 
 #include "covt.h"
 #include "covt_internal.h"
+#include "covt_walk.h"
 
 namespace {
-
-// ---- wire enums --------------------------------------------------
-enum StreamType { ST_PRESENT = 0, ST_DATA = 1, ST_LENGTH = 2, ST_DICTIONARY = 3, ST_GEOMETRY_TYPES = 4,
-                  ST_GEOMETRY_OFFSETS = 5, ST_PART_OFFSETS = 6, ST_RING_OFFSETS = 7, ST_VERTEX_OFFSETS = 8,
-                  ST_VERTEX_BUFFER = 9, ST_Z = 10, ST_M = 11 };
-enum Encoding { ENC_PLAIN = 0, ENC_VARINT = 1, ENC_VARINT_DELTA_ZZ = 4, ENC_RLE = 5, ENC_FPF_DELTA_ZZ = 9 };
-enum ColumnType { CT_PLAIN = 0, CT_ICE = 3, CT_ICE_MORTON = 4 };
-
-struct RawStream {
-    int32_t layer, kind, type, enc, ctype, nv, bl, nb;
-    int64_t off;  // tile-relative payload offset
-};
 
 // One property (sub)column found by a walker (CovtParser.decodePropertyColumn, CovtParser.java:276-354).
 // Streams by role 0 present, 1 data, 2 length, 3 dictionary; offsets tile-relative (-1: absent).
@@ -90,10 +79,6 @@ bool rd_j4(const uint8_t* t, size_t len, size_t& o, int32_t& v) {
     v = (int32_t)r;
     return true;
 }
-int nbits_of_extent(uint64_t extent) {  // 32 - Integer.numberOfLeadingZeros(extent), CovtParser.java:77
-    const uint32_t e = (uint32_t)extent;
-    return e ? 32 - __builtin_clz(e) : 0;
-}
 int genc_stream_type(const uint8_t* s, uint64_t n) {
     static const char* kNames[] = {"present", "data", "length", "dictionary", "geometry_types",
                                    "geometry_offsets", "part_offsets", "ring_offsets", "vertex_offsets",
@@ -115,7 +100,7 @@ int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::ve
     static thread_local std::vector<CM> cols;  // reused across tiles: no allocation per column
     for (uint64_t L = 0; L < nlayers; ++L) {
         uint64_t nlen, extent, nfeat, ncols;
-        if (!rd_uv(t, len, o, nlen) || o + nlen > len) return COVT_ERR_TRUNCATED;
+        if (!rd_uv(t, len, o, nlen) || nlen > len - o) return COVT_ERR_TRUNCATED;  // (no wrap)
         o += nlen;
         if (!rd_uv(t, len, o, extent) || !rd_uv(t, len, o, nfeat) || !rd_uv(t, len, o, ncols))
             return COVT_ERR_TRUNCATED;
@@ -123,7 +108,7 @@ int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::ve
         cols.assign(ncols, CM{});
         for (auto& c : cols) {
             uint64_t cn, ns;
-            if (!rd_uv(t, len, o, cn) || o + cn + 2 > len) return COVT_ERR_TRUNCATED;
+            if (!rd_uv(t, len, o, cn) || cn > len - o || len - o - cn < 2) return COVT_ERR_TRUNCATED;
             const uint8_t* name = t + o;
             c.name_off = (int64_t)o;
             c.name_len = (int64_t)cn;
@@ -137,7 +122,7 @@ int walk_genc(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::ve
             c.s.resize(ns);
             for (auto& s : c.s) {
                 uint64_t sn, nv, bl;
-                if (!rd_uv(t, len, o, sn) || o + sn > len) return COVT_ERR_TRUNCATED;
+                if (!rd_uv(t, len, o, sn) || sn > len - o) return COVT_ERR_TRUNCATED;
                 // stream names matter for Id / Geometry columns; property streams only when planned
                 s.type = (c.kind != 2 || props) ? genc_stream_type(t + o, sn) : -1;
                 s.name_off = (int64_t)o;
@@ -321,47 +306,6 @@ int walk_gend(const uint8_t* t, size_t len, std::vector<RawStream>& out, std::ve
         ++layer;
     }
     return COVT_OK;
-}
-
-// CovtParser dispatch: decodeGeometryColumn (:392-511) and decodedIds (:552-572)
-void choose_op(const RawStream& s, int id_mode, int& op, int64_t& nvals, int& elem, int64_t& out_elems) {
-    op = COVT_OP_NONE;
-    nvals = s.nv;
-    elem = 4;
-    out_elems = s.nv;
-    if (s.kind == 0) {
-        elem = 8;
-        if (s.enc == ENC_RLE) op = COVT_OP_RLE_U64;
-        else if (s.enc == ENC_VARINT) op = id_mode == COVT_ID_JAVA ? COVT_OP_VARINT_I32_AS_I64 : COVT_OP_VARINT_U64;
-        else if (s.enc == ENC_VARINT_DELTA_ZZ)
-            op = id_mode == COVT_ID_JAVA ? COVT_OP_VARINT_ZZ_DELTA_I64 : COVT_OP_RLE_U64;
-        return;
-    }
-    switch (s.type) {
-    case ST_GEOMETRY_TYPES: op = COVT_OP_BYTE_RLE_U8; elem = 1; return;
-    case ST_GEOMETRY_OFFSETS:
-    case ST_PART_OFFSETS:
-    case ST_RING_OFFSETS:
-        if (s.enc == ENC_RLE) op = COVT_OP_RLE_I32;
-        else if (s.enc == ENC_FPF_DELTA_ZZ) op = COVT_OP_FPF_ZZ_DELTA_I32;
-        return;
-    case ST_VERTEX_OFFSETS:
-        if (s.enc == ENC_VARINT_DELTA_ZZ) op = COVT_OP_VARINT_ZZ_DELTA_I32;
-        else if (s.enc == ENC_FPF_DELTA_ZZ) op = COVT_OP_FPF_ZZ_DELTA_I32;
-        return;
-    case ST_VERTEX_BUFFER:
-        if (s.ctype == CT_ICE_MORTON) {
-            out_elems = 2 * (int64_t)s.nv;
-            if (s.enc == ENC_VARINT_DELTA_ZZ) op = COVT_OP_VARINT_DELTA_MORTON;
-            else if (s.enc == ENC_FPF_DELTA_ZZ) op = COVT_OP_FPF_DELTA_MORTON;
-        } else {
-            if (s.ctype == CT_ICE) nvals = out_elems = 2 * (int64_t)s.nv;  // SURVEY Q4 build rule
-            if (s.enc == ENC_VARINT_DELTA_ZZ) op = COVT_OP_VARINT_ZZ_DELTA_XY;
-            else if (s.enc == ENC_FPF_DELTA_ZZ) op = COVT_OP_FPF_ZZ_DELTA_XY;
-        }
-        return;
-    default: return;
-    }
 }
 
 inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }

@@ -26,7 +26,7 @@ int covt_op_family_of(int op);
 constexpr int32_t kLaneMaxValues = 256;
 constexpr int64_t kLaneMinStreams = 16384;  // plans with fewer lane-eligible streams use no lane kernel
 constexpr int32_t kLaneMaxBytes = 64;  // the lane's first 68-byte window: no reloads (A/B: COVT_LANE_MAX_BYTES)
-inline bool lane_stream(int op, int32_t num_values, int32_t byte_length, int32_t max_bytes = kLaneMaxBytes) {
+__host__ __device__ inline bool lane_stream(int op, int32_t num_values, int32_t byte_length, int32_t max_bytes = kLaneMaxBytes) {
     return (op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_BYTE_RLE_RAW || op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_S64 ||
             op == COVT_OP_RLE_I32) &&
            num_values >= 0 && num_values <= kLaneMaxValues && byte_length >= 0 && byte_length <= max_bytes;

@@ -1,0 +1,621 @@
+// covt_plan_device.hip -- the Id / Geometry plan built on the GPU from tiles already resident in HBM
+// (include/covt.h "Device-side plan").
+//
+// The host plan (covt_plan_create, covt_host.cpp) walks each tile's container metadata on host
+// threads -- the host half of CovtParser.decodeCovt (CovtParser.java:53-133) and decodeLayerMetadata
+// (:574-652) -- and turns every Id / Geometry stream into a descriptor.  This file does the same walk
+// with one lane per tile, so a caller whose tiles are already in HBM gets a decodable descriptor table
+// without a round trip through the host:
+//   1. walk_count   one lane per tile: the container walk, counting the tile's streams and output bytes
+//   2. prefix sums  (hipcub) of the per-tile counts and output bytes -> each tile's first stream and
+//                   output offset; one 16-byte D2H of the totals to size the stream arrays
+//   3. walk_emit    the same walk again, writing each stream's covt_stream_info (output slices
+//                   16-byte aligned, in tile order: the host plan's layout, byte for byte)
+//   4. stream_keys  launch-order key per stream (family, lane op, cost descending), as the host plan
+//   5. radix sort   (hipcub, stable: ties in tile order) -> launch order
+//   6. fill_descs   descriptor k from the k-th stream in launch order; family counts
+// Streams are never split into chunks here (the host plan splits only streams longer than 1/3000 of a
+// batch's cost, i.e. long poles of small batches; a batch big enough to be worth a device plan splits
+// nothing, so the descriptor tables are identical -- tests/test_gpu_device_plan.py).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <stdint.h>
+#include <cstdlib>
+#include <cstring>
+#include <algorithm>
+
+#include "covt.h"
+#include "covt_internal.h"
+#include "covt_walk.h"
+
+struct covt_device_plan {
+    int dev = 0;
+    int32_t n_tiles = 0, format = 0, id_mode = 0;
+    int64_t n_streams = 0, out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
+    int64_t fam_counts[COVT_NUM_FAMILIES] = {};
+    void* tile_arena = nullptr;    // status, per-tile counts and prefix sums, totals, scan scratch
+    void* stream_arena = nullptr;  // infos, values, keys, launch order, descriptors, sort scratch
+    int32_t* d_status = nullptr;
+    covt_stream_info* d_info = nullptr;
+    covt_stream_desc* d_desc = nullptr;
+    uint32_t* d_order = nullptr;  // descriptor k decodes stream d_order[k]
+};
+
+namespace {
+
+// device totals (int64 slots)
+enum { T_STREAMS = 0, T_OUT = 1, T_IN = 2, T_PAYLOAD = 3, T_VERTS = 4, T_LANE = 5, T_FAM = 8, T_N = 8 + COVT_NUM_FAMILIES };
+
+// One tile's bytes, read through a 64-byte window held in registers: four 16-byte loads issued
+// together (one memory latency per 64 bytes of the front-to-back metadata walk instead of four).
+// Only granules overlapping the tile are loaded (each lies inside the allocation holding the tile);
+// every byte the walk uses is inside [0, len).
+struct Rd {
+    const uint8_t* t;
+    int64_t len;
+    uintptr_t wb;  // window base (64-byte aligned)
+    uint32_t w0, w1, w2, w3, w4, w5, w6, w7, w8, w9, w10, w11, w12, w13, w14, w15;  // the window (scalars: registers)
+    uintptr_t cb;  // address of the dword in `cur`
+    uint32_t cur;
+    __device__ __forceinline__ uint4 ld(uintptr_t b) const {
+        const uintptr_t lo = (uintptr_t)t, hi = lo + (uintptr_t)len;
+        return (b + 16 > lo && b < hi) ? *reinterpret_cast<const uint4*>(b) : make_uint4(0, 0, 0, 0);
+    }
+    __device__ __forceinline__ int at(int64_t i) {
+        const uintptr_t a = (uintptr_t)(t + i), d = a & ~(uintptr_t)3;
+        if (d != cb) {
+            const uintptr_t b = a & ~(uintptr_t)63;
+            if (b != wb) {
+                const uint4 v0 = ld(b), v1 = ld(b + 16), v2 = ld(b + 32), v3 = ld(b + 48);
+                w0 = v0.x, w1 = v0.y, w2 = v0.z, w3 = v0.w, w4 = v1.x, w5 = v1.y, w6 = v1.z, w7 = v1.w;
+                w8 = v2.x, w9 = v2.y, w10 = v2.z, w11 = v2.w, w12 = v3.x, w13 = v3.y, w14 = v3.z, w15 = v3.w;
+                wb = b;
+            }
+            // binary select tree on the dword index (values, never an indexed access: an indexed access
+            // would put the window in scratch)
+            const uint32_t q = (uint32_t)(a >> 2) & 15u;
+            const bool b0 = q & 1u, b1 = q & 2u, b2 = q & 4u, b3 = q & 8u;
+            const uint32_t a0 = b0 ? w1 : w0, a1 = b0 ? w3 : w2, a2 = b0 ? w5 : w4, a3 = b0 ? w7 : w6;
+            const uint32_t a4 = b0 ? w9 : w8, a5 = b0 ? w11 : w10, a6 = b0 ? w13 : w12, a7 = b0 ? w15 : w14;
+            const uint32_t c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2, c2 = b1 ? a5 : a4, c3 = b1 ? a7 : a6;
+            const uint32_t e0 = b2 ? c1 : c0, e1 = b2 ? c3 : c2;
+            cur = b3 ? e1 : e0;
+            cb = d;
+        }
+        return (int)((cur >> (8 * (a & 3))) & 0xffu);
+    }
+    // rd_uv (covt_host.cpp): 64-bit LEB128, at most 10 bytes
+    __device__ __forceinline__ bool uv(int64_t& o, uint64_t& v) {
+        v = 0;
+        for (int i = 0; i < 10; ++i) {
+            if (o >= len) return false;
+            const int b = at(o++);
+            v |= (uint64_t)(b & 0x7f) << (7 * i);
+            if (!(b & 0x80)) return true;
+        }
+        return false;
+    }
+    // rd_j4: DecodingUtils.decodeVarint with its 4-byte cap (DecodingUtils.java:157-186)
+    __device__ __forceinline__ bool j4(int64_t& o, int32_t& v) {
+        uint32_t r = 0;
+        for (int i = 0; i < 4; ++i) {
+            if (o >= len) return false;
+            const int b = at(o++);
+            r |= (uint32_t)(b & 0x7f) << (7 * i);
+            if (i < 3 && !(b & 0x80)) break;
+        }
+        v = (int32_t)r;
+        return true;
+    }
+    __device__ __forceinline__ bool is(int64_t o, uint64_t n, const char* s) {
+        int k = 0;
+        while (s[k]) ++k;
+        if (n != (uint64_t)k) return false;
+        for (int i = 0; i < k; ++i)
+            if (at(o + i) != (uint8_t)s[i]) return false;
+        return true;
+    }
+    // genc_stream_type: Gen C stream name -> StreamType (-1: other), dispatched on the name's length
+    __device__ __forceinline__ int stream_type(int64_t o, uint64_t n) {
+        switch (n) {
+        case 4: return is(o, n, "data") ? ST_DATA : -1;
+        case 6: return is(o, n, "length") ? ST_LENGTH : -1;
+        case 7: return is(o, n, "present") ? ST_PRESENT : -1;
+        case 10: return is(o, n, "dictionary") ? ST_DICTIONARY : -1;
+        case 12: return is(o, n, "part_offsets") ? ST_PART_OFFSETS : is(o, n, "ring_offsets") ? ST_RING_OFFSETS : -1;
+        case 13: return is(o, n, "vertex_buffer") ? ST_VERTEX_BUFFER : -1;
+        case 14:
+            return is(o, n, "geometry_types") ? ST_GEOMETRY_TYPES : is(o, n, "vertex_offsets") ? ST_VERTEX_OFFSETS : -1;
+        case 16: return is(o, n, "geometry_offsets") ? ST_GEOMETRY_OFFSETS : -1;
+        default: return -1;
+        }
+    }
+    // byte_rle_length: bytes of an ORC byte-RLE stream of n values at o (-1: runs past the tile)
+    __device__ __forceinline__ int32_t byte_rle_length(int64_t o, int32_t n) {
+        int64_t q = o, done = 0;
+        while (done < n) {
+            if (q >= len) return -1;
+            const int c = at(q++);
+            if (c < 0x80) done += c + 3, q += 1;
+            else done += 0x100 - c, q += 0x100 - c;
+            if (q > len) return -1;
+        }
+        return (int32_t)(q - o);
+    }
+};
+
+// Gen C container (walk_genc, covt_host.cpp) in one pass over each layer's
+// column metadata: the host walk's metadata checks in the same order (same first failing status), data
+// offsets relative to the layer's data start (known once its metadata is read: the emitter rebases the
+// layer's streams then), and the host's per-column data bound checked once at the end of the layer (the
+// data cursor only grows, so the last column's check fires iff any column's does).  Geometry streams
+// are laid out in StreamType order (a rescan of that column's few streams).
+template <class E>
+__device__ __forceinline__ int walk_genc_dev(Rd& r, E& emit) {
+    const int64_t len = r.len;
+    int64_t o = 0;
+    uint64_t version, nlayers;
+    if (!r.uv(o, version) || !r.uv(o, nlayers)) return COVT_ERR_TRUNCATED;
+    if (version != 1) return COVT_ERR_BAD_HEADER;
+    for (uint64_t L = 0; L < nlayers; ++L) {
+        uint64_t nlen, extent, nfeat, ncols;
+        if (!r.uv(o, nlen) || nlen > (uint64_t)(len - o)) return COVT_ERR_TRUNCATED;
+        o += (int64_t)nlen;
+        if (!r.uv(o, extent) || !r.uv(o, nfeat) || !r.uv(o, ncols)) return COVT_ERR_TRUNCATED;
+        if (ncols > 4096) return COVT_ERR_BAD_HEADER;
+        const int nb = nbits_of_extent(extent);
+        int64_t d = 0;  // data bytes of the layer's columns so far
+        emit.layer_begin();
+        for (uint64_t c = 0; c < ncols; ++c) {
+            uint64_t cn, ns, sn, nv, bl;
+            if (!r.uv(o, cn) || cn > (uint64_t)(len - o) || (uint64_t)(len - o) - cn < 2) return COVT_ERR_TRUNCATED;
+            const int64_t name = o;
+            o += (int64_t)cn;
+            const int dtype = r.at(o), ctype = r.at(o + 1);
+            o += 2;
+            if (!r.uv(o, ns)) return COVT_ERR_TRUNCATED;
+            if (ns > 256) return COVT_ERR_BAD_HEADER;
+            const int kind = r.is(name, cn, "id") ? 0 : (r.is(name, cn, "geometry") || dtype == 6) ? 1 : 2;
+            const int64_t s0 = o;
+            for (uint64_t s = 0; s < ns; ++s) {
+                if (!r.uv(o, sn) || sn > (uint64_t)(len - o)) return COVT_ERR_TRUNCATED;
+                const int type = kind == 0 ? r.stream_type(o, sn) : -1;
+                o += (int64_t)sn;
+                if (!r.uv(o, nv) || !r.uv(o, bl) || o >= len) return COVT_ERR_TRUNCATED;
+                const int enc = r.at(o++);
+                if (nv > 0x7fffffff || bl > 0x7fffffff) return COVT_ERR_BAD_HEADER;
+                if (type == ST_DATA) emit(RawStream{(int32_t)L, 0, ST_DATA, enc, ctype, (int32_t)nv, (int32_t)bl, nb, d});
+                if (kind != 1) d += (int64_t)bl;
+            }
+            if (kind == 1) {  // streams of types 4..9 in type order, then the rest (all checked above)
+                for (int want = ST_GEOMETRY_TYPES; want <= ST_VERTEX_BUFFER + 1; ++want) {
+                    int64_t q = s0;
+                    for (uint64_t s = 0; s < ns; ++s) {
+                        r.uv(q, sn);
+                        const int type = r.stream_type(q, sn);
+                        q += (int64_t)sn;
+                        r.uv(q, nv);
+                        r.uv(q, bl);
+                        const int enc = r.at(q++);
+                        const bool geo = type >= ST_GEOMETRY_TYPES && type <= ST_VERTEX_BUFFER;
+                        if (want <= ST_VERTEX_BUFFER ? type != want : geo) continue;
+                        if (geo) emit(RawStream{(int32_t)L, 1, type, enc, ctype, (int32_t)nv, (int32_t)bl, nb, d});
+                        d += (int64_t)bl;
+                    }
+                }
+            }
+        }
+        if (d > len - o) return COVT_ERR_TRUNCATED;
+        emit.layer_end(o);  // the layer's data starts where its metadata ends
+        o += d;
+    }
+    return o == len ? COVT_OK : COVT_ERR_BAD_HEADER;
+}
+
+// Gen D container (walk_gend, covt_host.cpp; CovtParser.decodeLayerMetadata, CovtParser.java:574-652).
+// A column's streams follow TreeMap<StreamType> order, the last metadata entry of a type winning.
+template <class E>
+__device__ __forceinline__ int walk_gend_dev(Rd& r, E& emit) {
+    const int64_t len = r.len;
+    int64_t o = 0;
+    int32_t layer = 0;
+    while (o < len) {
+        const bool optimized = r.at(o++) & 1;
+        int32_t v, extent, nfeat, ncols;
+        if (!r.j4(o, v)) return COVT_ERR_TRUNCATED;
+        if (!optimized) {
+            if (v < 0 || (int64_t)v > len - o) return COVT_ERR_TRUNCATED;
+            o += v;
+        }
+        if (!r.j4(o, extent) || !r.j4(o, nfeat) || !r.j4(o, ncols)) return COVT_ERR_TRUNCATED;
+        if (ncols < 0 || ncols > 4096) return COVT_ERR_BAD_HEADER;
+        const int64_t meta = o;
+        for (int32_t ci = 0; ci < ncols; ++ci) {  // metadata checks
+            int32_t x;
+            if (optimized || ci == 0) {
+                if (!r.j4(o, x)) return COVT_ERR_TRUNCATED;
+            } else {
+                if (!r.j4(o, x) || x < 0 || (int64_t)x > len - o) return COVT_ERR_TRUNCATED;
+                o += x;
+            }
+            if (o >= len) return COVT_ERR_TRUNCATED;
+            const int desc = r.at(o++), dtype = (desc >> 3) & 0xF, ctype = desc & 0x7;
+            if (ctype > 4) return COVT_ERR_BAD_HEADER;
+            for (;;) {
+                if (o >= len) return COVT_ERR_TRUNCATED;
+                const int sd = r.at(o++), type = sd >> 4, enc = sd & 0xF;
+                if (type > ST_M || enc > 9) return COVT_ERR_BAD_HEADER;
+                int32_t nv, bl;
+                if (!r.j4(o, nv) || !r.j4(o, bl)) return COVT_ERR_TRUNCATED;
+                if ((dtype == 8 && type == ST_VERTEX_BUFFER) || (type == ST_DATA && ctype == CT_PLAIN) ||
+                    type == ST_DICTIONARY)
+                    break;
+            }
+        }
+        const int nb = nbits_of_extent((uint32_t)extent);
+        int64_t m = meta, d = o;
+        emit.layer_begin();
+        for (int32_t ci = 0; ci < ncols; ++ci) {
+            int32_t x, kind;
+            if (optimized || ci == 0) {
+                r.j4(m, x);
+                kind = x == 0 ? 0 : (x == 1 ? 1 : 2);
+            } else {
+                r.j4(m, x);
+                kind = r.is(m, (uint64_t)x, "id") ? 0 : r.is(m, (uint64_t)x, "geometry") ? 1 : 2;
+                m += x;
+            }
+            const int desc = r.at(m++), dtype = (desc >> 3) & 0xF, ctype = desc & 0x7;
+            const int64_t s0 = m;
+            uint32_t have = 0;  // stream types present
+            for (;;) {
+                const int sd = r.at(m++), type = sd >> 4;
+                int32_t nv, bl;
+                r.j4(m, nv);
+                r.j4(m, bl);
+                have |= 1u << type;
+                if ((dtype == 8 && type == ST_VERTEX_BUFFER) || (type == ST_DATA && ctype == CT_PLAIN) ||
+                    type == ST_DICTIONARY)
+                    break;
+            }
+            if (kind == 2 && dtype != 0) {  // implicit present stream (walk_gend)
+                const int32_t pl = r.byte_rle_length(d, nfeat < 0 ? 0 : (int32_t)(((int64_t)nfeat + 7) / 8));
+                if (pl < 0) return COVT_ERR_TRUNCATED;
+                d += pl;
+            }
+            for (int type = 0; type < 12; ++type) {
+                if (!(have >> type & 1) || (kind == 2 && type == ST_PRESENT)) continue;
+                int enc = 0;
+                int32_t nv = 0, bl = 0;
+                for (int64_t q = s0; q < m;) {  // the last entry of this type
+                    const int sd = r.at(q++);
+                    int32_t a, b;
+                    r.j4(q, a);
+                    r.j4(q, b);
+                    if ((sd >> 4) == type) enc = sd & 0xF, nv = a, bl = b;
+                }
+                const bool hot = (kind == 0 && type == ST_DATA) ||
+                                 (kind == 1 && type >= ST_GEOMETRY_TYPES && type <= ST_VERTEX_BUFFER);
+                if (hot) emit(RawStream{layer, kind, type, enc, ctype, nv, bl, nb, d});
+                if (bl < 0) return COVT_ERR_BAD_HEADER;
+                d += bl;
+            }
+            if (d > len) return COVT_ERR_TRUNCATED;
+        }
+        emit.layer_end(0);
+        o = d;
+        ++layer;
+    }
+    return COVT_OK;
+}
+
+__device__ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
+
+template <class E>
+__device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes, uint64_t off, uint64_t size, int32_t format, E& emit) {
+    if (off > n_bytes || size > n_bytes - off) return COVT_ERR_INVALID_ARG;
+    Rd r;
+    r.t = bytes + off;
+    r.len = (int64_t)size;
+    r.wb = r.cb = ~(uintptr_t)0;
+    return format == COVT_FORMAT_GENC ? walk_genc_dev(r, emit) : walk_gend_dev(r, emit);
+}
+
+struct CountEmit {
+    int32_t id_mode;
+    int64_t n = 0, out = 0;
+    __device__ void operator()(const RawStream& s) {
+        int op, elem;
+        int64_t nvals, oe;
+        choose_op(s, id_mode, op, nvals, elem, oe);
+        ++n;
+        out = align16(out + (op == COVT_OP_NONE ? 0 : oe) * elem);
+    }
+    __device__ void layer_begin() {}
+    __device__ void layer_end(int64_t) {}
+};
+
+// Walk kernels: one lane per tile, COVT_DPLAN_LANES lanes per workgroup (default 1: a wave per tile
+// with one lane active -- the lanes' walks diverge, so a wave holding several tiles runs the union of
+// their paths; measured on the bench batch, 1 / 2 / 4 / 16 / 64 lanes: 11.5 / 13.3 / 12.8 / 20.4 /
+// 21.5 ms for the whole device plan).  A wave walking one tile with its lanes in lockstep (uniform,
+// scalar code) was tried: the compiler kept the walk on the VALU with divergent branches.
+__global__ void walk_count(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
+                           const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
+                           int32_t* __restrict__ status, int64_t* __restrict__ cnt, int64_t* __restrict__ ob) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > n_tiles) return;
+    if (t == n_tiles) {  // the prefix sums' total slot
+        cnt[t] = 0;
+        ob[t] = 0;
+        return;
+    }
+    CountEmit e{id_mode};
+    const int st = walk_tile(bytes, n_bytes, offs[t], sizes[t], format, e);
+    status[t] = st;
+    cnt[t] = st ? 0 : e.n;  // a failed tile contributes nothing
+    ob[t] = st ? 0 : e.out;
+}
+
+struct InfoEmit {
+    int32_t tile, id_mode;
+    int64_t tile_off;
+    covt_stream_info* info;
+    int32_t* nvals;
+    int64_t k, out, in_bytes = 0, payload = 0, verts = 0, lane = 0, k0 = 0;
+    int32_t lane_max;
+    __device__ void layer_begin() { k0 = k; }
+    __device__ void layer_end(int64_t data_start) {  // rebase the layer's data offsets (this lane's own stores)
+        if (data_start)
+            for (int64_t j = k0; j < k; ++j) info[j].in_off += data_start;
+    }
+    __device__ void operator()(const RawStream& s) {
+        int op, elem;
+        int64_t nv, oe;
+        choose_op(s, id_mode, op, nv, elem, oe);
+        covt_stream_info si;
+        si.tile = tile;
+        si.layer = s.layer;
+        si.column_kind = s.kind;
+        si.stream_type = s.type;
+        si.encoding = s.enc;
+        si.column_type = s.ctype;
+        si.num_values = s.nv;
+        si.byte_length = s.bl;
+        si.num_bits = s.nb;
+        si.op = op;
+        si.elem_bytes = elem;
+        si.desc_index = -1;
+        si.in_off = tile_off + s.off;
+        si.out_elems = op == COVT_OP_NONE ? 0 : oe;
+        si.out_off = out;
+        out = align16(out + si.out_elems * elem);
+        in_bytes += s.bl;
+        payload += si.out_elems * elem;
+        if (s.kind == 1 && s.type == ST_VERTEX_BUFFER) verts += (s.ctype == CT_ICE || s.ctype == CT_ICE_MORTON) ? s.nv : s.nv / 2;
+        lane += lane_stream(op, (int32_t)nv, s.bl, lane_max);
+        info[k] = si;
+        nvals[k] = (int32_t)nv;
+        ++k;
+    }
+};
+
+__global__ void walk_emit(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
+                          const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
+                          const int32_t* __restrict__ status, const int64_t* __restrict__ cnt_base,
+                          const int64_t* __restrict__ ob_base, int32_t lane_max, covt_stream_info* __restrict__ info,
+                          int32_t* __restrict__ nvals, unsigned long long* __restrict__ totals) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_tiles || status[t]) return;
+    InfoEmit e{t, id_mode, (int64_t)offs[t], info, nvals, cnt_base[t], ob_base[t]};
+    e.lane_max = lane_max;
+    walk_tile(bytes, n_bytes, offs[t], sizes[t], format, e);
+    atomicAdd(&totals[T_IN], (unsigned long long)e.in_bytes);
+    atomicAdd(&totals[T_PAYLOAD], (unsigned long long)e.payload);
+    atomicAdd(&totals[T_VERTS], (unsigned long long)e.verts);
+    atomicAdd(&totals[T_LANE], (unsigned long long)e.lane);
+}
+
+// launch-order key of covt_plan_create_ex step 3 (no splits): family, lane op, cost descending
+__global__ void stream_keys(const covt_stream_info* info, const int32_t* nvals, int64_t n, int32_t lane_max,
+                            int64_t lane_min, unsigned long long* totals, uint64_t* keys, uint32_t* vals) {
+    __shared__ unsigned int fam_n[COVT_NUM_FAMILIES];
+    if (threadIdx.x < COVT_NUM_FAMILIES) fam_n[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const covt_stream_info& s = info[i];
+        const int32_t lm = (int64_t)totals[T_LANE] < lane_min ? -1 : lane_max;
+        const bool lane = lane_stream(s.op, nvals[i], s.byte_length, lm);
+        const uint64_t fam = lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family(s.op);
+        const int64_t c = (int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4;
+        const uint64_t cost = c < ((1ll << 48) - 1) ? (uint64_t)c : (1ull << 48) - 1;
+        keys[i] = (fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost);
+        vals[i] = (uint32_t)i;
+        atomicAdd(&fam_n[fam], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < COVT_NUM_FAMILIES && fam_n[threadIdx.x])
+        atomicAdd(&totals[T_FAM + threadIdx.x], (unsigned long long)fam_n[threadIdx.x]);
+}
+
+__global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const uint64_t* keys, const uint32_t* order,
+                           int64_t n, covt_stream_desc* desc) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t i = order[k];
+    covt_stream_info& si = info[i];
+    covt_stream_desc d;
+    d.in_off = (uint64_t)si.in_off;
+    d.out_off = (uint64_t)si.out_off;
+    d.avail = si.byte_length;
+    d.num_values = nvals[i];
+    d.op = (uint8_t)si.op;
+    d.num_bits = (uint8_t)si.num_bits;
+    d.flags = (keys[k] >> 60) == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
+    d.byte_length = si.byte_length;
+    desc[k] = d;
+    si.desc_index = (int32_t)k;
+}
+
+int64_t env_or(const char* name, int64_t dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::strtoll(v, nullptr, 10) : dflt;
+}
+
+size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Lanes per workgroup of the walk kernels (A/B knob COVT_DPLAN_LANES; see walk_count)
+constexpr int kWalkLanes = 1;
+
+}  // namespace
+
+extern "C" {
+
+int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_tile_offsets,
+                            const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
+                            void* hip_stream, covt_device_plan** out) {
+    if (!out || n_tiles < 0 || (n_tiles && (!d_bytes || !d_tile_offsets || !d_tile_sizes))) return COVT_ERR_INVALID_ARG;
+    if (format != COVT_FORMAT_GENC && format != COVT_FORMAT_GEND) return COVT_ERR_INVALID_ARG;
+    if (id_mode != COVT_ID_FORMAT && id_mode != COVT_ID_JAVA) return COVT_ERR_INVALID_ARG;
+    *out = nullptr;
+    auto* p = new covt_device_plan();
+    p->n_tiles = n_tiles;
+    p->format = format;
+    p->id_mode = id_mode;
+    hipStream_t s = (hipStream_t)hip_stream;
+    auto fail = [&](int st) {
+        covt_device_plan_destroy(p);
+        return st;
+    };
+#define DCHK(x)                                   \
+    do {                                          \
+        if ((x) != hipSuccess) return fail(COVT_ERR_DEVICE); \
+    } while (0)
+    DCHK(hipGetDevice(&p->dev));
+    const size_t nt1 = (size_t)n_tiles + 1;
+    // tile arena: status | cnt | ob | cnt_base | ob_base | totals | scan scratch
+    size_t scan_tmp = 0;
+    DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)nt1, s));
+    const size_t o_cnt = up256(nt1 * 4), o_ob = o_cnt + up256(nt1 * 8), o_cb = o_ob + up256(nt1 * 8),
+                 o_obb = o_cb + up256(nt1 * 8), o_tot = o_obb + up256(nt1 * 8), o_tmp = o_tot + up256(T_N * 8),
+                 tile_bytes = o_tmp + up256(scan_tmp);
+    DCHK(hipMalloc(&p->tile_arena, tile_bytes));
+    uint8_t* ta = (uint8_t*)p->tile_arena;
+    p->d_status = (int32_t*)ta;
+    int64_t *cnt = (int64_t*)(ta + o_cnt), *ob = (int64_t*)(ta + o_ob), *cb = (int64_t*)(ta + o_cb),
+            *obb = (int64_t*)(ta + o_obb);
+    auto* totals = (unsigned long long*)(ta + o_tot);
+    DCHK(hipMemsetAsync(totals, 0, T_N * 8, s));
+    const int wl = (int)std::min<int64_t>(256, std::max<int64_t>(1, env_or("COVT_DPLAN_LANES", kWalkLanes)));
+    walk_count<<<(int)((nt1 + wl - 1) / wl), wl, 0, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
+                                                        format, id_mode, p->d_status, cnt, ob);
+    DCHK(hipGetLastError());
+    DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, cnt, cb, (int)nt1, s));
+    DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, ob, obb, (int)nt1, s));
+    int64_t tot2[2];
+    DCHK(hipMemcpyAsync(&tot2[0], cb + n_tiles, 8, hipMemcpyDeviceToHost, s));
+    DCHK(hipMemcpyAsync(&tot2[1], obb + n_tiles, 8, hipMemcpyDeviceToHost, s));
+    DCHK(hipStreamSynchronize(s));
+    const int64_t ns = tot2[0];
+    p->n_streams = ns;
+    p->out_bytes = tot2[1];
+    if (ns > 0x7fffffff) return fail(COVT_ERR_INVALID_ARG);
+    // stream arena: info | nvals | keys in/out | vals in/out | descs | sort scratch
+    size_t sort_tmp = 0;
+    DCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                            (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ns, 0, 63, s));
+    const size_t n = (size_t)(ns > 0 ? ns : 1);
+    const size_t o_nv = up256(n * sizeof(covt_stream_info)), o_k0 = o_nv + up256(n * 4), o_k1 = o_k0 + up256(n * 8),
+                 o_v0 = o_k1 + up256(n * 8), o_v1 = o_v0 + up256(n * 4), o_d = o_v1 + up256(n * 4),
+                 o_st = o_d + up256(n * sizeof(covt_stream_desc)), stream_bytes = o_st + up256(sort_tmp);
+    DCHK(hipMalloc(&p->stream_arena, stream_bytes));
+    uint8_t* sa = (uint8_t*)p->stream_arena;
+    p->d_info = (covt_stream_info*)sa;
+    int32_t* nvals = (int32_t*)(sa + o_nv);
+    uint64_t *k0 = (uint64_t*)(sa + o_k0), *k1 = (uint64_t*)(sa + o_k1);
+    uint32_t *v0 = (uint32_t*)(sa + o_v0), *v1 = (uint32_t*)(sa + o_v1);
+    p->d_order = v1;
+    p->d_desc = (covt_stream_desc*)(sa + o_d);
+    const int32_t lane_max = (int32_t)env_or("COVT_LANE_MAX_BYTES", kLaneMaxBytes);
+    const int64_t lane_min = env_or("COVT_LANE_MIN_STREAMS", kLaneMinStreams);
+    if (n_tiles) {
+        walk_emit<<<(n_tiles + wl - 1) / wl, wl, 0, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
+                                                        format, id_mode, p->d_status, cb, obb, lane_max, p->d_info,
+                                                        nvals, totals);
+        DCHK(hipGetLastError());
+    }
+    if (ns > 0) {
+        const int blocks_s = (int)((ns + 255) / 256);
+        stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, k0, v0);
+        DCHK(hipGetLastError());
+        DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, k0, k1, v0, v1, (int)ns, 0, 63, s));
+        fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, k1, v1, ns, p->d_desc);
+        DCHK(hipGetLastError());
+    }
+    unsigned long long tot[T_N];
+    DCHK(hipMemcpyAsync(tot, totals, sizeof(tot), hipMemcpyDeviceToHost, s));
+    DCHK(hipStreamSynchronize(s));
+#undef DCHK
+    p->in_bytes = (int64_t)tot[T_IN];
+    p->out_payload = (int64_t)tot[T_PAYLOAD];
+    p->vertices = (int64_t)tot[T_VERTS];
+    for (int f = 0; f < COVT_NUM_FAMILIES; ++f) p->fam_counts[f] = (int64_t)tot[T_FAM + f];
+    *out = p;
+    return COVT_OK;
+}
+
+void covt_device_plan_destroy(covt_device_plan* p) {
+    if (!p) return;
+    int cur = 0;
+    const bool sw = hipGetDevice(&cur) == hipSuccess && cur != p->dev && hipSetDevice(p->dev) == hipSuccess;
+    if (p->tile_arena) (void)hipFree(p->tile_arena);
+    if (p->stream_arena) (void)hipFree(p->stream_arena);
+    if (sw) (void)hipSetDevice(cur);
+    delete p;
+}
+
+int64_t covt_device_plan_num_streams(const covt_device_plan* p) { return p ? p->n_streams : 0; }
+int64_t covt_device_plan_output_bytes(const covt_device_plan* p) { return p ? p->out_bytes : 0; }
+
+int covt_device_plan_totals(const covt_device_plan* p, int64_t* in_bytes, int64_t* out_bytes, int64_t* vertices) {
+    if (!p) return COVT_ERR_INVALID_ARG;
+    if (in_bytes) *in_bytes = p->in_bytes;
+    if (out_bytes) *out_bytes = p->out_payload;
+    if (vertices) *vertices = p->vertices;
+    return COVT_OK;
+}
+
+int covt_device_plan_family_counts(const covt_device_plan* p, int64_t counts[COVT_NUM_FAMILIES]) {
+    if (!p || !counts) return COVT_ERR_INVALID_ARG;
+    for (int f = 0; f < COVT_NUM_FAMILIES; ++f) counts[f] = p->fam_counts[f];
+    return COVT_OK;
+}
+
+const covt_stream_desc* covt_device_plan_descs_device(const covt_device_plan* p) { return p ? p->d_desc : nullptr; }
+const covt_stream_info* covt_device_plan_streams_device(const covt_device_plan* p) { return p ? p->d_info : nullptr; }
+const int32_t* covt_device_plan_tile_status_device(const covt_device_plan* p) { return p ? p->d_status : nullptr; }
+const uint32_t* covt_device_plan_order_device(const covt_device_plan* p) { return p ? p->d_order : nullptr; }
+
+int covt_device_plan_copy(const covt_device_plan* p, covt_stream_info* streams, covt_stream_desc* descs,
+                          int32_t* tile_status) {
+    if (!p) return COVT_ERR_INVALID_ARG;
+    const size_t ns = (size_t)p->n_streams;
+    if (streams && ns && hipMemcpy(streams, p->d_info, ns * sizeof(covt_stream_info), hipMemcpyDeviceToHost) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    if (descs && ns && hipMemcpy(descs, p->d_desc, ns * sizeof(covt_stream_desc), hipMemcpyDeviceToHost) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    if (tile_status && p->n_tiles &&
+        hipMemcpy(tile_status, p->d_status, (size_t)p->n_tiles * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    return COVT_OK;
+}
+
+int covt_device_plan_decode(const covt_device_plan* p, const uint8_t* d_in, uint8_t* d_out, covt_stream_result* d_res,
+                            void* hip_stream) {
+    if (!p || (p->n_streams && (!d_in || !d_res || (p->out_bytes && !d_out)))) return COVT_ERR_INVALID_ARG;
+    return covt_decode_streams_device_grouped(d_in, p->d_desc, p->fam_counts, d_out, d_res, hip_stream);
+}
+
+}  // extern "C"

@@ -412,6 +412,39 @@ int covt_materialize_properties_device(const uint8_t* d_in, const uint8_t* d_dec
 int covt_plan_properties_host(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_props,
                               covt_prop_result* host_pres);
 
+/* ---- Device-side plan ------------------------------------------------------------------------
+ * covt_plan_create's Id / Geometry walk run on the GPU, for tiles already resident in HBM (the host
+ * half of CovtParser.decodeCovt, CovtParser.java:53-133 / :574-652, without the round trip through
+ * host memory).  d_bytes / n_bytes: the batch on the current device; d_tile_offsets / d_tile_sizes:
+ * n_tiles uint64 each, on the device (a tile outside [0, n_bytes) gets COVT_ERR_INVALID_ARG as its
+ * status).  The result is the host plan's layout exactly: streams in tile order with the same
+ * covt_stream_info fields and 16-byte aligned output slices, descriptors in the same launch order
+ * and families.  Long streams are not split into chunks (covt_plan_create splits only the long poles
+ * of small batches).  Property columns, geometry assembly and multi-GPU shards stay with the host
+ * plan.  Runs on `hip_stream` and synchronises it twice (the stream count sizes the arrays). */
+typedef struct covt_device_plan covt_device_plan;
+int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_tile_offsets,
+                            const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
+                            void* hip_stream, covt_device_plan** out);
+void covt_device_plan_destroy(covt_device_plan* plan);
+int64_t covt_device_plan_num_streams(const covt_device_plan* plan); /* = its descriptors */
+int64_t covt_device_plan_output_bytes(const covt_device_plan* plan);
+int covt_device_plan_totals(const covt_device_plan* plan, int64_t* in_bytes, int64_t* out_bytes, int64_t* vertices);
+int covt_device_plan_family_counts(const covt_device_plan* plan, int64_t counts[COVT_NUM_FAMILIES]);
+/* device arrays owned by the plan: num_streams descriptors (launch order), stream records (tile
+ * order, desc_index set), n_tiles statuses, and the stream index of each descriptor */
+const covt_stream_desc* covt_device_plan_descs_device(const covt_device_plan* plan);
+const covt_stream_info* covt_device_plan_streams_device(const covt_device_plan* plan);
+const int32_t* covt_device_plan_tile_status_device(const covt_device_plan* plan);
+const uint32_t* covt_device_plan_order_device(const covt_device_plan* plan);
+/* copies of the device arrays into host memory (any pointer may be NULL) */
+int covt_device_plan_copy(const covt_device_plan* plan, covt_stream_info* streams, covt_stream_desc* descs,
+                          int32_t* tile_status);
+/* the grouped decode launch over the plan's descriptors (covt_decode_streams_device_grouped):
+ * d_out covt_device_plan_output_bytes bytes, d_res num_streams results.  Asynchronous. */
+int covt_device_plan_decode(const covt_device_plan* plan, const uint8_t* d_in, uint8_t* d_out,
+                            covt_stream_result* d_res, void* hip_stream);
+
 /* Library info */
 const char* covt_version(void);
 int covt_device_count(int32_t* n);

@@ -35,8 +35,8 @@ def test_header_symbols_exported(covt):
 def test_kernel_compiled_for_gfx950():
     """The fat binary embedded in libcovt.so carries a gfx950 code object (and nothing else)."""
     blob = open(os.path.join(ROOT, "cov-tiles_amd", "libcovt.so"), "rb").read()
-    assert b"amdgcn-amd-amdhsa--gfx950" in blob
-    assert b"gfx942" not in blob and b"gfx90a" not in blob
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}  # (hipcub's host-side arch tables name other targets as strings)
 
 
 def test_struct_layouts(covt):

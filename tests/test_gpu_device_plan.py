@@ -1,0 +1,137 @@
+"""Device-side plan (covt_device_plan_create, cov-tiles_amd/csrc/covt_plan_device.hip) against the host
+plan (covt_plan_create), which the oracle pins (test_capi.py::test_plan_matches_oracle_walk,
+test_gpu_parity.py): the GPU's walk of the container metadata (CovtParser.decodeCovt,
+CovtParser.java:53-133; decodeLayerMetadata :574-652) must give the host plan's stream records,
+tile statuses, output layout, launch order and family counts byte for byte, on Gen C fixtures, Gen D
+conversions, malformed tiles and the full BASELINE config-5 batch -- and decoding through it must give
+the host plan's outputs.  The host plan here is built with splitting off (COVT_SPLIT_MIN=-1): the device
+plan never splits."""
+import os
+
+import numpy as np
+import pytest
+
+import covt_gend_rt as RT
+from conftest import tile_paths
+
+pytestmark = pytest.mark.gpu
+
+
+def _host_plan(covt, tiles, fmt, id_mode, split=False):
+    old = os.environ.get("COVT_SPLIT_MIN")
+    if not split:
+        os.environ["COVT_SPLIT_MIN"] = "-1"
+    try:
+        return covt.Plan.from_tiles(tiles, fmt, id_mode)
+    finally:
+        if old is None:
+            os.environ.pop("COVT_SPLIT_MIN", None)
+        else:
+            os.environ["COVT_SPLIT_MIN"] = old
+
+
+def _device_plan(covt, hp, fmt, id_mode):
+    import torch
+
+    d_blob = torch.from_numpy(hp.blob).cuda()
+    return covt.DevicePlan(d_blob, hp.offsets.astype(np.int64), hp.sizes.astype(np.int64), fmt, id_mode)
+
+
+def _assert_same_plan(hp, dp):
+    info, descs, st = dp.host_copy()
+    assert np.array_equal(st, hp.tile_status)
+    assert dp.num_streams == hp.num_streams == hp.num_descs
+    assert dp.output_bytes == hp.output_bytes
+    assert (dp.in_bytes, dp.out_payload, dp.vertices) == (hp.in_bytes, hp.out_bytes, hp.vertices)
+    assert np.array_equal(dp.family_counts, hp.family_counts)
+    assert info.tobytes() == hp.streams.tobytes()
+    assert descs.tobytes() == hp.descs.tobytes()
+
+
+def _assert_same_decode(covt, hp, dp):
+    import torch
+
+    d_out, d_res = dp.alloc()
+    dp.decode(d_out, d_res)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()[:dp.output_bytes]
+    res = d_res.cpu().numpy().reshape(-1, 2)[:dp.num_streams][hp.streams["desc_index"]]
+    h_out, h_res = hp.decode_host()
+    assert np.array_equal(res, h_res)
+    for i in range(hp.num_streams):
+        assert np.array_equal(hp.stream_array(out, i), hp.stream_array(h_out, i)), i
+
+
+@pytest.mark.parametrize("id_mode", [0, 1], ids=["id_format", "id_java"])
+def test_fixtures_genc(covt, gpu_available, id_mode):
+    """Every committed fixture tile (decodable or not), in one batch."""
+    tiles = [open(p, "rb").read() for p in tile_paths()]
+    hp = _host_plan(covt, tiles, covt.FORMAT_GENC, id_mode)
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, id_mode)
+    _assert_same_plan(hp, dp)
+    _assert_same_decode(covt, hp, dp)
+
+
+@pytest.mark.parametrize("optimized", [False, True], ids=["named", "optimized"])
+def test_fixtures_gend(covt, gpu_available, decodable_tiles, optimized):
+    """Gen D conversions of the decodable fixtures (implicit present streams, TreeMap stream order)."""
+    tiles = [RT.genc_to_gend(t, optimized=optimized)[0] for _, t in decodable_tiles[::3]]
+    hp = _host_plan(covt, tiles, covt.FORMAT_GEND, 0)
+    dp = _device_plan(covt, hp, covt.FORMAT_GEND, 0)
+    assert (hp.tile_status == 0).all() and hp.num_streams > 0
+    _assert_same_plan(hp, dp)
+    _assert_same_decode(covt, hp, dp)
+
+
+@pytest.mark.parametrize("fmt", [0, 1], ids=["genc", "gend"])
+def test_malformed_tiles(covt, gpu_available, decodable_tiles, fmt):
+    """Truncations, garbage and bit flips in the metadata: the same status per tile as the host walk
+    (first failing check), a failed tile contributing no streams, the rest laid out identically."""
+    rng = np.random.default_rng(11 + fmt)
+    base = [t for _, t in decodable_tiles[:40]]
+    if fmt == 1:
+        base = [RT.genc_to_gend(t, optimized=bool(k & 1))[0] for k, t in enumerate(base)]
+    tiles = [b"", b"\x01", b"\x01\x05garbage", bytes(rng.integers(0, 256, 500).astype(np.uint8))]
+    for t in base:
+        tiles.append(t[:int(rng.integers(1, len(t)))])
+        b = bytearray(t)
+        for _ in range(3):  # flips in the first 256 bytes: mostly metadata
+            b[int(rng.integers(0, min(256, len(b))))] ^= 1 << int(rng.integers(0, 8))
+        tiles.append(bytes(b))
+        tiles.append(t)
+    hp = _host_plan(covt, tiles, fmt, 0)
+    dp = _device_plan(covt, hp, fmt, 0)
+    assert (hp.tile_status != 0).sum() >= 40
+    _assert_same_plan(hp, dp)
+
+
+def test_tile_outside_buffer(covt, gpu_available, decodable_tiles):
+    """A tile range past the device buffer gets COVT_ERR_INVALID_ARG and no streams (never read)."""
+    import torch
+
+    tiles = [t for _, t in decodable_tiles[:3]]
+    blob, offs, sizes = covt.pack_tiles(tiles)
+    offs, sizes = offs.astype(np.int64), sizes.astype(np.int64)
+    d_blob = torch.from_numpy(blob).cuda()
+    offs2, sizes2 = offs.copy(), sizes.copy()
+    sizes2[1] = len(blob) + 1
+    offs2[2] = len(blob) + 100
+    dp = covt.DevicePlan(d_blob, offs2, sizes2)
+    _, _, st = dp.host_copy()
+    assert st[0] == 0 and st[1] == covt.ERR_INVALID_ARG and st[2] == covt.ERR_INVALID_ARG
+    one = covt.Plan.from_tiles(tiles[:1])
+    assert dp.num_streams == one.num_streams and dp.output_bytes == one.output_bytes
+    empty = covt.DevicePlan(d_blob, offs[:0], sizes[:0])
+    assert empty.num_streams == 0 and empty.output_bytes == 0
+
+
+def test_full_batch_plan(covt, gpu_available):
+    """BASELINE config 5 (the bench's 10k-tile batch): the host plan splits nothing there, and the device
+    plan equals it (records, descriptors, families: the lane family is on at this size)."""
+    import bench
+
+    picks = bench.sample_batch(bench.tile_library(), 10000, bench.SEED)
+    hp = _host_plan(covt, [t for _, t in picks], covt.FORMAT_GENC, 0, split=True)
+    assert hp.num_descs == hp.num_streams and hp.family_counts[3] > 0  # COVT_FAMILY_LANE
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
+    _assert_same_plan(hp, dp)

@@ -1,0 +1,49 @@
+"""Device-side plan timing on the bench batch (BASELINE config 5), in one process: wall-clock of
+covt_device_plan_create per setting of the lanes-per-workgroup knob (COVT_DPLAN_LANES), interleaved
+rounds so box drift hits every setting alike, plus the host plan for comparison.  Each setting's plan
+is checked equal to the host plan's descriptors.  Usage: python tools/device_plan_ab.py [lanes ...]"""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    import torch
+
+    lanes = [int(x) for x in sys.argv[1:]] or [1, 4, 16, 64]
+    covt = bench.load_covt()
+    picks = bench.sample_batch(bench.tile_library(), 10000, bench.SEED)
+    blob, offs, sizes = covt.pack_tiles([t for _, t in picks])
+    t0 = time.perf_counter()
+    hp = covt.Plan(blob, offs, sizes)
+    t_host = time.perf_counter() - t0
+    d_blob = torch.from_numpy(blob).cuda()
+    d_off = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d_size = torch.from_numpy(sizes.astype(np.int64)).cuda()
+    times = {k: [] for k in lanes}
+    for rnd in range(6):
+        for k in lanes:
+            os.environ["COVT_DPLAN_LANES"] = str(k)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dp = covt.DevicePlan(d_blob, d_off, d_size)
+            dt = time.perf_counter() - t0
+            if rnd == 0:
+                _, descs, _ = dp.host_copy()
+                assert descs.tobytes() == hp.descs.tobytes(), k
+            else:
+                times[k].append(dt)
+            dp.close()
+    print("host plan (covt_plan_create): %.1f ms" % (t_host * 1e3))
+    for k in lanes:
+        print("COVT_DPLAN_LANES=%-3d device plan median %.3f ms  min %.3f ms" %
+              (k, np.median(times[k]) * 1e3, min(times[k]) * 1e3))
+
+
+if __name__ == "__main__":
+    main()
