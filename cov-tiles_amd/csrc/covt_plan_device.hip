@@ -51,85 +51,130 @@ enum { T_STREAMS = 0, T_OUT = 1, T_IN = 2, T_PAYLOAD = 3, T_VERTS = 4, T_LANE = 
 // together (one memory latency per 64 bytes of the front-to-back metadata walk instead of four).
 // Only granules overlapping the tile are loaded (each lies inside the allocation holding the tile);
 // every byte the walk uses is inside [0, len).
+// compile-time packing of a name literal (bytes [from, from + 8) of its first len bytes)
+__host__ __device__ constexpr uint64_t cstrlen(const char* s) { return *s ? 1 + cstrlen(s + 1) : 0; }
+__host__ __device__ constexpr uint64_t pk(const char* s, uint64_t from, uint64_t len) {
+    uint64_t v = 0;
+    for (uint64_t i = from; i < from + 8 && i < len; ++i) v |= (uint64_t)(uint8_t)s[i] << (8 * (i - from));
+    return v;
+}
+
+// the walking lanes' 64-byte windows (dynamic LDS: 64 bytes per lane of the workgroup)
+extern __shared__ uint4 covt_walk_win[];
+
 struct Rd {
     const uint8_t* t;
     int64_t len;
-    uintptr_t wb;  // window base (64-byte aligned)
-    uint32_t w0, w1, w2, w3, w4, w5, w6, w7, w8, w9, w10, w11, w12, w13, w14, w15;  // the window (scalars: registers)
-    uintptr_t cb;  // address of the dword in `cur`
-    uint32_t cur;
+    uintptr_t wb;  // window base (16-byte aligned)
     __device__ __forceinline__ uint4 ld(uintptr_t b) const {
         const uintptr_t lo = (uintptr_t)t, hi = lo + (uintptr_t)len;
         return (b + 16 > lo && b < hi) ? *reinterpret_cast<const uint4*>(b) : make_uint4(0, 0, 0, 0);
     }
-    __device__ __forceinline__ int at(int64_t i) {
-        const uintptr_t a = (uintptr_t)(t + i), d = a & ~(uintptr_t)3;
-        if (d != cb) {
-            const uintptr_t b = a & ~(uintptr_t)63;
-            if (b != wb) {
-                const uint4 v0 = ld(b), v1 = ld(b + 16), v2 = ld(b + 32), v3 = ld(b + 48);
-                w0 = v0.x, w1 = v0.y, w2 = v0.z, w3 = v0.w, w4 = v1.x, w5 = v1.y, w6 = v1.z, w7 = v1.w;
-                w8 = v2.x, w9 = v2.y, w10 = v2.z, w11 = v2.w, w12 = v3.x, w13 = v3.y, w14 = v3.z, w15 = v3.w;
-                wb = b;
-            }
-            // binary select tree on the dword index (values, never an indexed access: an indexed access
-            // would put the window in scratch)
-            const uint32_t q = (uint32_t)(a >> 2) & 15u;
-            const bool b0 = q & 1u, b1 = q & 2u, b2 = q & 4u, b3 = q & 8u;
-            const uint32_t a0 = b0 ? w1 : w0, a1 = b0 ? w3 : w2, a2 = b0 ? w5 : w4, a3 = b0 ? w7 : w6;
-            const uint32_t a4 = b0 ? w9 : w8, a5 = b0 ? w11 : w10, a6 = b0 ? w13 : w12, a7 = b0 ? w15 : w14;
-            const uint32_t c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2, c2 = b1 ? a5 : a4, c3 = b1 ? a7 : a6;
-            const uint32_t e0 = b2 ? c1 : c0, e1 = b2 ? c3 : c2;
-            cur = b3 ? e1 : e0;
-            cb = d;
+    // 8 bytes at tile offset i, from a 64-byte window at a 16-byte aligned base kept in LDS (only the
+    // base is carried through the walk's loops: a register window of 16 dwords cost ~1,400 64-bit
+    // moves per kernel at loop edges).  Bytes past the tile are unspecified: callers mask by len.
+    __device__ __forceinline__ uint64_t peek8(int64_t i) {
+        const uintptr_t a = (uintptr_t)(t + i);
+        uint4* w = covt_walk_win + threadIdx.x * 4;
+        if (a < wb || a + 8 > wb + 64) {
+            const uintptr_t b = a & ~(uintptr_t)15;
+            const uint4 v0 = ld(b), v1 = ld(b + 16), v2 = ld(b + 32), v3 = ld(b + 48);
+            w[0] = v0;
+            w[1] = v1;
+            w[2] = v2;
+            w[3] = v3;
+            wb = b;
         }
-        return (int)((cur >> (8 * (a & 3))) & 0xffu);
+        const uint32_t off = (uint32_t)(a - wb), k = off >> 3, sh = (off & 7) * 8;  // off <= 56
+        const uint64_t* q = reinterpret_cast<const uint64_t*>(w);
+        const uint64_t lo = q[k];
+        return sh ? (lo >> sh) | (q[k + 1] << (64 - sh)) : lo;  // (sh != 0: k + 1 <= 7)
     }
-    // rd_uv (covt_host.cpp): 64-bit LEB128, at most 10 bytes
+    __device__ __forceinline__ int at(int64_t i) { return (int)(peek8(i) & 0xff); }
+    // low n bytes (n <= 8) of x's 7-bit groups packed (LEB128 payload)
+    __device__ __forceinline__ static uint64_t leb_pack(uint64_t x, int n) {
+        x = (n >= 8 ? x : x & ((1ull << (8 * n)) - 1)) & 0x7f7f7f7f7f7f7f7full;
+        x = (x & 0x007f007f007f007full) | ((x & 0x7f007f007f007f00ull) >> 1);
+        x = (x & 0x00003fff00003fffull) | ((x & 0x3fff00003fff0000ull) >> 2);
+        return (x & 0x000000000fffffffull) | ((x & 0x0fffffff00000000ull) >> 4);
+    }
+    // rd_uv (covt_host.cpp): 64-bit LEB128, at most 10 bytes; up to 8 bytes decoded from one word
     __device__ __forceinline__ bool uv(int64_t& o, uint64_t& v) {
-        v = 0;
-        for (int i = 0; i < 10; ++i) {
-            if (o >= len) return false;
-            const int b = at(o++);
+        const int64_t avail = len - o;
+        if (avail <= 0) return false;
+        const uint64_t w = peek8(o);
+        uint64_t stop = ~w & 0x8080808080808080ull;
+        if (avail < 8) stop &= (1ull << (8 * avail)) - 1;  // only the tile's bytes
+        if (stop) {
+            const int n = (__builtin_ctzll(stop) >> 3) + 1;
+            v = leb_pack(w, n);
+            o += n;
+            return true;
+        }
+        if (avail < 8) return false;  // no terminator before the tile's end
+        v = leb_pack(w, 8);           // 9- or 10-byte value
+        int64_t q = o + 8;
+#pragma unroll 1
+        for (int i = 8; i < 10; ++i) {
+            if (q >= len) return false;
+            const int b = at(q++);
             v |= (uint64_t)(b & 0x7f) << (7 * i);
-            if (!(b & 0x80)) return true;
+            if (!(b & 0x80)) {
+                o = q;
+                return true;
+            }
         }
         return false;
     }
-    // rd_j4: DecodingUtils.decodeVarint with its 4-byte cap (DecodingUtils.java:157-186)
+    // rd_j4: DecodingUtils.decodeVarint with its 4-byte cap (DecodingUtils.java:157-186): a byte
+    // without bit 7 among the first three ends the value, else the fourth byte does
     __device__ __forceinline__ bool j4(int64_t& o, int32_t& v) {
-        uint32_t r = 0;
-        for (int i = 0; i < 4; ++i) {
-            if (o >= len) return false;
-            const int b = at(o++);
-            r |= (uint32_t)(b & 0x7f) << (7 * i);
-            if (i < 3 && !(b & 0x80)) break;
+        const int64_t avail = len - o;
+        if (avail <= 0) return false;
+        const uint64_t w = peek8(o);
+        const uint64_t stop = ~w & 0x808080ull;
+        const int n = stop ? (__builtin_ctzll(stop) >> 3) + 1 : 4;
+        if (n > avail) return false;
+        v = (int32_t)(uint32_t)leb_pack(w, n);
+        o += n;
+        return true;
+    }
+    // the first 16 bytes of a name at o (n <= 16) packed little-endian (register compares below)
+    __device__ __forceinline__ void pack16(int64_t o, uint64_t n, uint64_t& lo, uint64_t& hi) {
+        lo = peek8(o);
+        if (n < 8) lo &= (1ull << (8 * n)) - 1;
+        hi = 0;
+        if (n > 8) {
+            hi = peek8(o + 8);
+            if (n < 16) hi &= (1ull << (8 * (n - 8))) - 1;
         }
-        v = (int32_t)r;
-        return true;
     }
-    __device__ __forceinline__ bool is(int64_t o, uint64_t n, const char* s) {
-        int k = 0;
-        while (s[k]) ++k;
-        if (n != (uint64_t)k) return false;
-        for (int i = 0; i < k; ++i)
-            if (at(o + i) != (uint8_t)s[i]) return false;
-        return true;
+    __device__ __forceinline__ bool is(int64_t o, uint64_t n, const char* s) {  // n <= 16 names only
+        const uint64_t k = cstrlen(s);
+        if (n != k) return false;
+        uint64_t lo, hi;
+        pack16(o, n, lo, hi);
+        return lo == pk(s, 0, k) && hi == pk(s, 8, k);
     }
-    // genc_stream_type: Gen C stream name -> StreamType (-1: other), dispatched on the name's length
+    // genc_stream_type: Gen C stream name -> StreamType (-1: other)
     __device__ __forceinline__ int stream_type(int64_t o, uint64_t n) {
-        switch (n) {
-        case 4: return is(o, n, "data") ? ST_DATA : -1;
-        case 6: return is(o, n, "length") ? ST_LENGTH : -1;
-        case 7: return is(o, n, "present") ? ST_PRESENT : -1;
-        case 10: return is(o, n, "dictionary") ? ST_DICTIONARY : -1;
-        case 12: return is(o, n, "part_offsets") ? ST_PART_OFFSETS : is(o, n, "ring_offsets") ? ST_RING_OFFSETS : -1;
-        case 13: return is(o, n, "vertex_buffer") ? ST_VERTEX_BUFFER : -1;
-        case 14:
-            return is(o, n, "geometry_types") ? ST_GEOMETRY_TYPES : is(o, n, "vertex_offsets") ? ST_VERTEX_OFFSETS : -1;
-        case 16: return is(o, n, "geometry_offsets") ? ST_GEOMETRY_OFFSETS : -1;
-        default: return -1;
-        }
+        if (n < 4 || n > 16) return -1;
+        uint64_t lo, hi;
+        pack16(o, n, lo, hi);
+#define COVT_NAME(str, v) \
+    if (n == cstrlen(str) && lo == pk(str, 0, cstrlen(str)) && hi == pk(str, 8, cstrlen(str))) return v;
+        COVT_NAME("data", ST_DATA)
+        COVT_NAME("length", ST_LENGTH)
+        COVT_NAME("present", ST_PRESENT)
+        COVT_NAME("dictionary", ST_DICTIONARY)
+        COVT_NAME("geometry_types", ST_GEOMETRY_TYPES)
+        COVT_NAME("geometry_offsets", ST_GEOMETRY_OFFSETS)
+        COVT_NAME("part_offsets", ST_PART_OFFSETS)
+        COVT_NAME("ring_offsets", ST_RING_OFFSETS)
+        COVT_NAME("vertex_offsets", ST_VERTEX_OFFSETS)
+        COVT_NAME("vertex_buffer", ST_VERTEX_BUFFER)
+#undef COVT_NAME
+        return -1;
     }
     // byte_rle_length: bytes of an ORC byte-RLE stream of n values at o (-1: runs past the tile)
     __device__ __forceinline__ int32_t byte_rle_length(int64_t o, int32_t n) {
@@ -318,7 +363,7 @@ __device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes,
     Rd r;
     r.t = bytes + off;
     r.len = (int64_t)size;
-    r.wb = r.cb = ~(uintptr_t)0;
+    r.wb = ~(uintptr_t)0;
     return format == COVT_FORMAT_GENC ? walk_genc_dev(r, emit) : walk_gend_dev(r, emit);
 }
 
@@ -509,7 +554,7 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
     auto* totals = (unsigned long long*)(ta + o_tot);
     DCHK(hipMemsetAsync(totals, 0, T_N * 8, s));
     const int wl = (int)std::min<int64_t>(256, std::max<int64_t>(1, env_or("COVT_DPLAN_LANES", kWalkLanes)));
-    walk_count<<<(int)((nt1 + wl - 1) / wl), wl, 0, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
+    walk_count<<<(int)((nt1 + wl - 1) / wl), wl, (size_t)wl * 64, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
                                                         format, id_mode, p->d_status, cnt, ob);
     DCHK(hipGetLastError());
     DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, cnt, cb, (int)nt1, s));
@@ -541,7 +586,7 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
     const int32_t lane_max = (int32_t)env_or("COVT_LANE_MAX_BYTES", kLaneMaxBytes);
     const int64_t lane_min = env_or("COVT_LANE_MIN_STREAMS", kLaneMinStreams);
     if (n_tiles) {
-        walk_emit<<<(n_tiles + wl - 1) / wl, wl, 0, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
+        walk_emit<<<(n_tiles + wl - 1) / wl, wl, (size_t)wl * 64, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
                                                         format, id_mode, p->d_status, cb, obb, lane_max, p->d_info,
                                                         nvals, totals);
         DCHK(hipGetLastError());
