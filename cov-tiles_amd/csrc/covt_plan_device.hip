@@ -4,9 +4,9 @@
 // The host plan (covt_plan_create, covt_host.cpp) walks each tile's container metadata on host
 // threads -- the host half of CovtParser.decodeCovt (CovtParser.java:53-133) and decodeLayerMetadata
 // (:574-652) -- and turns every Id / Geometry stream into a descriptor.  This file does the same walk
-// with one lane per tile, so a caller whose tiles are already in HBM gets a decodable descriptor table
+// with one wave per tile, so a caller whose tiles are already in HBM gets a decodable descriptor table
 // without a round trip through the host:
-//   1. walk_count   one lane per tile: the container walk, counting the tile's streams and output bytes
+//   1. walk_count   one wave per tile: the container walk, counting the tile's streams and output bytes
 //   2. prefix sums  (hipcub) of the per-tile counts and output bytes -> each tile's first stream and
 //                   output offset; one 16-byte D2H of the totals to size the stream arrays
 //   3. walk_emit    the same walk again, writing each stream's covt_stream_info (output slices
@@ -62,6 +62,7 @@ __host__ __device__ constexpr uint64_t pk(const char* s, uint64_t from, uint64_t
 // the walking lanes' 64-byte windows (dynamic LDS: 64 bytes per lane of the workgroup)
 extern __shared__ uint4 covt_walk_win[];
 
+template <bool kWave>
 struct Rd {
     const uint8_t* t;
     int64_t len;
@@ -70,25 +71,36 @@ struct Rd {
         const uintptr_t lo = (uintptr_t)t, hi = lo + (uintptr_t)len;
         return (b + 16 > lo && b < hi) ? *reinterpret_cast<const uint4*>(b) : make_uint4(0, 0, 0, 0);
     }
-    // 8 bytes at tile offset i, from a 64-byte window at a 16-byte aligned base kept in LDS (only the
-    // base is carried through the walk's loops: a register window of 16 dwords cost ~1,400 64-bit
-    // moves per kernel at loop edges).  Bytes past the tile are unspecified: callers mask by len.
+    // 8 bytes at tile offset i from a window of the tile kept in LDS (only its base is carried through
+    // the walk's loops: a register window of 16 dwords cost ~1,400 64-bit moves per kernel at loop edges).
+    // Lane layout: 64 bytes per lane, refilled by that lane.  Wave layout: 512 bytes per wave, refilled by
+    // 32 lanes at once (one 16-byte load each) starting 128 bytes before the byte wanted, so the walk's
+    // look-backs (a column's name, the geometry column's type-ordered rescans) stay inside the window.
+    // Bytes past the tile are unspecified: callers mask by len.
+    static constexpr uint32_t kWin = kWave ? 512 : 64;
     __device__ __forceinline__ uint64_t peek8(int64_t i) {
         const uintptr_t a = (uintptr_t)(t + i);
-        uint4* w = covt_walk_win + threadIdx.x * 4;
-        if (a < wb || a + 8 > wb + 64) {
-            const uintptr_t b = a & ~(uintptr_t)15;
-            const uint4 v0 = ld(b), v1 = ld(b + 16), v2 = ld(b + 32), v3 = ld(b + 48);
-            w[0] = v0;
-            w[1] = v1;
-            w[2] = v2;
-            w[3] = v3;
-            wb = b;
+        uint4* w = covt_walk_win + (kWave ? 0 : threadIdx.x * 4);
+        if (a < wb || a + 8 > wb + kWin) {
+            if (kWave) {
+                const uintptr_t lo = (uintptr_t)t;
+                const uintptr_t b = (a - lo > 128 ? a - 128 : lo) & ~(uintptr_t)15;
+                if (threadIdx.x < kWin / 16) w[threadIdx.x] = ld(b + 16 * threadIdx.x);
+                wb = b;
+            } else {
+                const uintptr_t b = a & ~(uintptr_t)15;
+                const uint4 v0 = ld(b), v1 = ld(b + 16), v2 = ld(b + 32), v3 = ld(b + 48);
+                w[0] = v0;
+                w[1] = v1;
+                w[2] = v2;
+                w[3] = v3;
+                wb = b;
+            }
         }
-        const uint32_t off = (uint32_t)(a - wb), k = off >> 3, sh = (off & 7) * 8;  // off <= 56
+        const uint32_t off = (uint32_t)(a - wb), k = off >> 3, sh = (off & 7) * 8;  // off <= kWin - 8
         const uint64_t* q = reinterpret_cast<const uint64_t*>(w);
         const uint64_t lo = q[k];
-        return sh ? (lo >> sh) | (q[k + 1] << (64 - sh)) : lo;  // (sh != 0: k + 1 <= 7)
+        return sh ? (lo >> sh) | (q[k + 1] << (64 - sh)) : lo;  // (sh != 0: k + 1 < kWin / 8)
     }
     __device__ __forceinline__ int at(int64_t i) { return (int)(peek8(i) & 0xff); }
     // low n bytes (n <= 8) of x's 7-bit groups packed (LEB128 payload)
@@ -149,20 +161,27 @@ struct Rd {
             if (n < 16) hi &= (1ull << (8 * (n - 8))) - 1;
         }
     }
-    __device__ __forceinline__ bool is(int64_t o, uint64_t n, const char* s) {  // n <= 16 names only
-        const uint64_t k = cstrlen(s);
-        if (n != k) return false;
-        uint64_t lo, hi;
-        pack16(o, n, lo, hi);
-        return lo == pk(s, 0, k) && hi == pk(s, 8, k);
-    }
+    // name at o (n bytes) == the literal (constants evaluated at compile time: a runtime walk of the
+    // literal's bytes would be a memory load per character)
+#define COVT_IS(o, n, str)                                                                             \
+    ([&]() {                                                                                           \
+        constexpr uint64_t n_ = cstrlen(str), l_ = pk(str, 0, n_), h_ = pk(str, 8, n_);                \
+        static_assert(n_ <= 16, "names up to 16 bytes");                                               \
+        if ((uint64_t)(n) != n_) return false;                                                         \
+        uint64_t lo_, hi_;                                                                             \
+        r.pack16((o), n_, lo_, hi_);                                                                   \
+        return lo_ == l_ && hi_ == h_;                                                                 \
+    }())
     // genc_stream_type: Gen C stream name -> StreamType (-1: other)
     __device__ __forceinline__ int stream_type(int64_t o, uint64_t n) {
         if (n < 4 || n > 16) return -1;
         uint64_t lo, hi;
         pack16(o, n, lo, hi);
-#define COVT_NAME(str, v) \
-    if (n == cstrlen(str) && lo == pk(str, 0, cstrlen(str)) && hi == pk(str, 8, cstrlen(str))) return v;
+#define COVT_NAME(str, v)                                                              \
+    {                                                                                  \
+        constexpr uint64_t n_ = cstrlen(str), l_ = pk(str, 0, n_), h_ = pk(str, 8, n_); \
+        if (n == n_ && lo == l_ && hi == h_) return v;                                 \
+    }
         COVT_NAME("data", ST_DATA)
         COVT_NAME("length", ST_LENGTH)
         COVT_NAME("present", ST_PRESENT)
@@ -196,8 +215,8 @@ struct Rd {
 // layer's streams then), and the host's per-column data bound checked once at the end of the layer (the
 // data cursor only grows, so the last column's check fires iff any column's does).  Geometry streams
 // are laid out in StreamType order (a rescan of that column's few streams).
-template <class E>
-__device__ __forceinline__ int walk_genc_dev(Rd& r, E& emit) {
+template <bool kWave, class E>
+__device__ __forceinline__ int walk_genc_dev(Rd<kWave>& r, E& emit) {
     const int64_t len = r.len;
     int64_t o = 0;
     uint64_t version, nlayers;
@@ -221,7 +240,7 @@ __device__ __forceinline__ int walk_genc_dev(Rd& r, E& emit) {
             o += 2;
             if (!r.uv(o, ns)) return COVT_ERR_TRUNCATED;
             if (ns > 256) return COVT_ERR_BAD_HEADER;
-            const int kind = r.is(name, cn, "id") ? 0 : (r.is(name, cn, "geometry") || dtype == 6) ? 1 : 2;
+            const int kind = COVT_IS(name, cn, "id") ? 0 : (COVT_IS(name, cn, "geometry") || dtype == 6) ? 1 : 2;
             const int64_t s0 = o;
             for (uint64_t s = 0; s < ns; ++s) {
                 if (!r.uv(o, sn) || sn > (uint64_t)(len - o)) return COVT_ERR_TRUNCATED;
@@ -260,8 +279,8 @@ __device__ __forceinline__ int walk_genc_dev(Rd& r, E& emit) {
 
 // Gen D container (walk_gend, covt_host.cpp; CovtParser.decodeLayerMetadata, CovtParser.java:574-652).
 // A column's streams follow TreeMap<StreamType> order, the last metadata entry of a type winning.
-template <class E>
-__device__ __forceinline__ int walk_gend_dev(Rd& r, E& emit) {
+template <bool kWave, class E>
+__device__ __forceinline__ int walk_gend_dev(Rd<kWave>& r, E& emit) {
     const int64_t len = r.len;
     int64_t o = 0;
     int32_t layer = 0;
@@ -308,7 +327,7 @@ __device__ __forceinline__ int walk_gend_dev(Rd& r, E& emit) {
                 kind = x == 0 ? 0 : (x == 1 ? 1 : 2);
             } else {
                 r.j4(m, x);
-                kind = r.is(m, (uint64_t)x, "id") ? 0 : r.is(m, (uint64_t)x, "geometry") ? 1 : 2;
+                kind = COVT_IS(m, x, "id") ? 0 : COVT_IS(m, x, "geometry") ? 1 : 2;
                 m += x;
             }
             const int desc = r.at(m++), dtype = (desc >> 3) & 0xF, ctype = desc & 0x7;
@@ -357,10 +376,10 @@ __device__ __forceinline__ int walk_gend_dev(Rd& r, E& emit) {
 
 __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
-template <class E>
+template <bool kWave, class E>
 __device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes, uint64_t off, uint64_t size, int32_t format, E& emit) {
     if (off > n_bytes || size > n_bytes - off) return COVT_ERR_INVALID_ARG;
-    Rd r;
+    Rd<kWave> r;
     r.t = bytes + off;
     r.len = (int64_t)size;
     r.wb = ~(uintptr_t)0;
@@ -381,26 +400,32 @@ struct CountEmit {
     __device__ void layer_end(int64_t) {}
 };
 
-// Walk kernels: one lane per tile, COVT_DPLAN_LANES lanes per workgroup (default 1: a wave per tile
-// with one lane active -- the lanes' walks diverge, so a wave holding several tiles runs the union of
-// their paths; measured on the bench batch, 1 / 2 / 4 / 16 / 64 lanes: 11.5 / 13.3 / 12.8 / 20.4 /
-// 21.5 ms for the whole device plan).  A wave walking one tile with its lanes in lockstep (uniform,
-// scalar code) was tried: the compiler kept the walk on the VALU with divergent branches.
+// Walk kernels in two layouts (A/B knob COVT_DPLAN_LANES):
+//  * 0 (default): a wave per tile, its lanes in lockstep on values the compiler proves uniform (the
+//    walk compiles to scalar code, 32-54 VGPRs), a 512-byte LDS window refilled by 32 lanes at once,
+//    lane 0 writing the records and all lanes rebasing a layer's offsets;
+//  * k > 0: k lanes per workgroup, a lane per tile with a 64-byte window (lanes diverge, so k = 1 is
+//    best: 1 / 2 / 4 / 16 lanes measured 7.9 / 8.6 / 8.1 / 11.9 ms for the whole plan).
+// Both take ~0.7 ms for one tile alone and ~3.6 ms per walk kernel for the 10k-tile batch
+// (profiles/r02/device_plan_ab.txt); the walk is a serial chain per tile whose step time neither the
+// scalar nor the lane layout changes.
+template <bool kWave>
 __global__ void walk_count(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
                            const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                            int32_t* __restrict__ status, int64_t* __restrict__ cnt, int64_t* __restrict__ ob) {
-    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int32_t t = kWave ? (int32_t)blockIdx.x : (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t > n_tiles) return;
     if (t == n_tiles) {  // the prefix sums' total slot
-        cnt[t] = 0;
-        ob[t] = 0;
+        if (!kWave || threadIdx.x == 0) cnt[t] = 0, ob[t] = 0;
         return;
     }
     CountEmit e{id_mode};
-    const int st = walk_tile(bytes, n_bytes, offs[t], sizes[t], format, e);
-    status[t] = st;
-    cnt[t] = st ? 0 : e.n;  // a failed tile contributes nothing
-    ob[t] = st ? 0 : e.out;
+    const int st = walk_tile<kWave>(bytes, n_bytes, offs[t], sizes[t], format, e);
+    if (!kWave || threadIdx.x == 0) {
+        status[t] = st;
+        cnt[t] = st ? 0 : e.n;  // a failed tile contributes nothing
+        ob[t] = st ? 0 : e.out;
+    }
 }
 
 struct InfoEmit {
@@ -410,10 +435,17 @@ struct InfoEmit {
     int32_t* nvals;
     int64_t k, out, in_bytes = 0, payload = 0, verts = 0, lane = 0, k0 = 0;
     int32_t lane_max;
+    bool writer, wave;
     __device__ void layer_begin() { k0 = k; }
     __device__ void layer_end(int64_t data_start) {  // rebase the layer's data offsets (this lane's own stores)
-        if (data_start)
+        if (!data_start) return;
+        if (wave) {  // the layer's records, one lane each (lane 0 wrote them: a barrier-free wave is in order)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            for (int64_t j = k0 + threadIdx.x; j < k; j += 64) info[j].in_off += data_start;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        } else {
             for (int64_t j = k0; j < k; ++j) info[j].in_off += data_start;
+        }
     }
     __device__ void operator()(const RawStream& s) {
         int op, elem;
@@ -440,26 +472,33 @@ struct InfoEmit {
         payload += si.out_elems * elem;
         if (s.kind == 1 && s.type == ST_VERTEX_BUFFER) verts += (s.ctype == CT_ICE || s.ctype == CT_ICE_MORTON) ? s.nv : s.nv / 2;
         lane += lane_stream(op, (int32_t)nv, s.bl, lane_max);
-        info[k] = si;
-        nvals[k] = (int32_t)nv;
+        if (writer) {
+            info[k] = si;
+            nvals[k] = (int32_t)nv;
+        }
         ++k;
     }
 };
 
+template <bool kWave>
 __global__ void walk_emit(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
                           const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                           const int32_t* __restrict__ status, const int64_t* __restrict__ cnt_base,
                           const int64_t* __restrict__ ob_base, int32_t lane_max, covt_stream_info* __restrict__ info,
                           int32_t* __restrict__ nvals, unsigned long long* __restrict__ totals) {
-    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int32_t t = kWave ? (int32_t)blockIdx.x : (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t >= n_tiles || status[t]) return;
     InfoEmit e{t, id_mode, (int64_t)offs[t], info, nvals, cnt_base[t], ob_base[t]};
     e.lane_max = lane_max;
-    walk_tile(bytes, n_bytes, offs[t], sizes[t], format, e);
-    atomicAdd(&totals[T_IN], (unsigned long long)e.in_bytes);
-    atomicAdd(&totals[T_PAYLOAD], (unsigned long long)e.payload);
-    atomicAdd(&totals[T_VERTS], (unsigned long long)e.verts);
-    atomicAdd(&totals[T_LANE], (unsigned long long)e.lane);
+    e.writer = !kWave || threadIdx.x == 0;
+    e.wave = kWave;
+    walk_tile<kWave>(bytes, n_bytes, offs[t], sizes[t], format, e);
+    if (e.writer) {
+        atomicAdd(&totals[T_IN], (unsigned long long)e.in_bytes);
+        atomicAdd(&totals[T_PAYLOAD], (unsigned long long)e.payload);
+        atomicAdd(&totals[T_VERTS], (unsigned long long)e.verts);
+        atomicAdd(&totals[T_LANE], (unsigned long long)e.lane);
+    }
 }
 
 // launch-order key of covt_plan_create_ex step 3 (no splits): family, lane op, cost descending
@@ -512,7 +551,7 @@ int64_t env_or(const char* name, int64_t dflt) {
 size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Lanes per workgroup of the walk kernels (A/B knob COVT_DPLAN_LANES; see walk_count)
-constexpr int kWalkLanes = 1;
+constexpr int kWalkLanes = 0;
 
 }  // namespace
 
@@ -553,9 +592,14 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
             *obb = (int64_t*)(ta + o_obb);
     auto* totals = (unsigned long long*)(ta + o_tot);
     DCHK(hipMemsetAsync(totals, 0, T_N * 8, s));
-    const int wl = (int)std::min<int64_t>(256, std::max<int64_t>(1, env_or("COVT_DPLAN_LANES", kWalkLanes)));
-    walk_count<<<(int)((nt1 + wl - 1) / wl), wl, (size_t)wl * 64, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
-                                                        format, id_mode, p->d_status, cnt, ob);
+    // 0: a wave per tile, its lanes in lockstep; k > 0: k lanes per workgroup, a lane per tile
+    const int wl = (int)std::min<int64_t>(256, std::max<int64_t>(0, env_or("COVT_DPLAN_LANES", kWalkLanes)));
+    if (wl == 0)
+        walk_count<true><<<(int)nt1, 64, 512, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
+                                                  id_mode, p->d_status, cnt, ob);
+    else
+        walk_count<false><<<(int)((nt1 + wl - 1) / wl), wl, (size_t)wl * 64, s>>>(
+            d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cnt, ob);
     DCHK(hipGetLastError());
     DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, cnt, cb, (int)nt1, s));
     DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, ob, obb, (int)nt1, s));
@@ -586,9 +630,13 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
     const int32_t lane_max = (int32_t)env_or("COVT_LANE_MAX_BYTES", kLaneMaxBytes);
     const int64_t lane_min = env_or("COVT_LANE_MIN_STREAMS", kLaneMinStreams);
     if (n_tiles) {
-        walk_emit<<<(n_tiles + wl - 1) / wl, wl, (size_t)wl * 64, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
-                                                        format, id_mode, p->d_status, cb, obb, lane_max, p->d_info,
-                                                        nvals, totals);
+        if (wl == 0)
+            walk_emit<true><<<n_tiles, 64, 512, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
+                                                    id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, totals);
+        else
+            walk_emit<false><<<(n_tiles + wl - 1) / wl, wl, (size_t)wl * 64, s>>>(
+                d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cb, obb,
+                lane_max, p->d_info, nvals, totals);
         DCHK(hipGetLastError());
     }
     if (ns > 0) {

@@ -45,5 +45,33 @@ def main():
               (k, np.median(times[k]) * 1e3, min(times[k]) * 1e3))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("COVT_DPLAN_PROBE"):
     main()
+
+
+def probe():
+    """Where the walk's time goes: one tile alone vs 10k copies, for the smallest and the largest tile."""
+    import torch
+
+    covt = bench.load_covt()
+    lib = [t for z in bench.tile_library().values() for _, t in z]
+    lib.sort(key=len)
+    for name, tile in (("smallest", lib[0]), ("largest", lib[-1])):
+        for n in (1, 100, 10000):
+            blob, offs, sizes = covt.pack_tiles([tile] * n)
+            d_blob = torch.from_numpy(blob).cuda()
+            d_off = torch.from_numpy(offs.astype(np.int64)).cuda()
+            d_size = torch.from_numpy(sizes.astype(np.int64)).cuda()
+            ts = []
+            for r in range(6):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                dp = covt.DevicePlan(d_blob, d_off, d_size)
+                ts.append(time.perf_counter() - t0)
+                dp.close()
+            print("%-8s tile (%d bytes) x %-5d device plan median %.3f ms" % (name, len(tile), n, np.median(ts[1:]) * 1e3))
+            del d_blob
+
+
+if __name__ == "__main__" and os.environ.get("COVT_DPLAN_PROBE"):
+    probe()
