@@ -62,15 +62,37 @@ __host__ __device__ constexpr uint64_t pk(const char* s, uint64_t from, uint64_t
 // the walking lanes' 64-byte windows (dynamic LDS: 64 bytes per lane of the workgroup)
 extern __shared__ uint4 covt_walk_win[];
 
+// Window refill (Rd::peek8): loads the window for byte address a into LDS and returns its base.  Out
+// of line and with value arguments only, so the walk has one copy of it (inlined at every read site, the
+// walk kernels were ~12k instructions) and the reader's state stays in registers.
+__device__ __forceinline__ uint4 window_ld(const uint8_t* t, int64_t len, uintptr_t b) {
+    const uintptr_t lo = (uintptr_t)t, hi = lo + (uintptr_t)len;
+    return (b + 16 > lo && b < hi) ? *reinterpret_cast<const uint4*>(b) : make_uint4(0, 0, 0, 0);
+}
+template <bool kWave>
+__device__ __noinline__ uintptr_t window_refill(const uint8_t* t, int64_t len, uintptr_t a) {
+    if (kWave) {
+        const uintptr_t lo = (uintptr_t)t;
+        const uintptr_t b = (a - lo > 128 ? a - 128 : lo) & ~(uintptr_t)15;
+        if (threadIdx.x < 32) covt_walk_win[threadIdx.x] = window_ld(t, len, b + 16 * threadIdx.x);
+        return b;
+    }
+    const uintptr_t b = a & ~(uintptr_t)15;
+    uint4* w = covt_walk_win + threadIdx.x * 4;
+    const uint4 v0 = window_ld(t, len, b), v1 = window_ld(t, len, b + 16), v2 = window_ld(t, len, b + 32),
+                v3 = window_ld(t, len, b + 48);
+    w[0] = v0;
+    w[1] = v1;
+    w[2] = v2;
+    w[3] = v3;
+    return b;
+}
+
 template <bool kWave>
 struct Rd {
     const uint8_t* t;
     int64_t len;
     uintptr_t wb;  // window base (16-byte aligned)
-    __device__ __forceinline__ uint4 ld(uintptr_t b) const {
-        const uintptr_t lo = (uintptr_t)t, hi = lo + (uintptr_t)len;
-        return (b + 16 > lo && b < hi) ? *reinterpret_cast<const uint4*>(b) : make_uint4(0, 0, 0, 0);
-    }
     // 8 bytes at tile offset i from a window of the tile kept in LDS (only its base is carried through
     // the walk's loops: a register window of 16 dwords cost ~1,400 64-bit moves per kernel at loop edges).
     // Lane layout: 64 bytes per lane, refilled by that lane.  Wave layout: 512 bytes per wave, refilled by
@@ -80,22 +102,11 @@ struct Rd {
     static constexpr uint32_t kWin = kWave ? 512 : 64;
     __device__ __forceinline__ uint64_t peek8(int64_t i) {
         const uintptr_t a = (uintptr_t)(t + i);
-        uint4* w = covt_walk_win + (kWave ? 0 : threadIdx.x * 4);
+        const uint4* w = covt_walk_win + (kWave ? 0 : threadIdx.x * 4);
         if (a < wb || a + 8 > wb + kWin) {
-            if (kWave) {
-                const uintptr_t lo = (uintptr_t)t;
-                const uintptr_t b = (a - lo > 128 ? a - 128 : lo) & ~(uintptr_t)15;
-                if (threadIdx.x < kWin / 16) w[threadIdx.x] = ld(b + 16 * threadIdx.x);
-                wb = b;
-            } else {
-                const uintptr_t b = a & ~(uintptr_t)15;
-                const uint4 v0 = ld(b), v1 = ld(b + 16), v2 = ld(b + 32), v3 = ld(b + 48);
-                w[0] = v0;
-                w[1] = v1;
-                w[2] = v2;
-                w[3] = v3;
-                wb = b;
-            }
+            wb = window_refill<kWave>(t, len, a);  // out of line: one copy of the refill code
+            if (kWave) wb = ((uintptr_t)__builtin_amdgcn_readfirstlane((int)(wb >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wb);
         }
         const uint32_t off = (uint32_t)(a - wb), k = off >> 3, sh = (off & 7) * 8;  // off <= kWin - 8
         const uint64_t* q = reinterpret_cast<const uint64_t*>(w);
