@@ -397,18 +397,35 @@ __device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes,
     return format == COVT_FORMAT_GENC ? walk_genc_dev(r, emit) : walk_gend_dev(r, emit);
 }
 
+// Records a tile's walk leaves for emit_slots: up to kSlots per tile (the fixture library's busiest
+// tile has 67 Id / Geometry streams); a tile with more is walked again by walk_emit
+constexpr int kSlots = 128;
+
 struct CountEmit {
     int32_t id_mode;
-    int64_t n = 0, out = 0;
+    RawStream* slots = nullptr;  // this tile's kSlots record slots, or null
+    bool writer = true, wave = false;
+    int64_t n = 0, out = 0, k0 = 0;
     __device__ void operator()(const RawStream& s) {
         int op, elem;
         int64_t nvals, oe;
         choose_op(s, id_mode, op, nvals, elem, oe);
+        if (slots && writer && n < kSlots) slots[n] = s;
         ++n;
         out = align16(out + (op == COVT_OP_NONE ? 0 : oe) * elem);
     }
-    __device__ void layer_begin() {}
-    __device__ void layer_end(int64_t) {}
+    __device__ void layer_begin() { k0 = n; }
+    __device__ void layer_end(int64_t data_start) {  // rebase the layer's recorded data offsets
+        if (!data_start || !slots) return;
+        const int64_t e = n < kSlots ? n : kSlots;
+        if (wave) {  // one lane per record (lane 0 wrote them)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            for (int64_t j = k0 + threadIdx.x; j < e; j += 64) slots[j].off += data_start;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        } else {
+            for (int64_t j = k0; j < e; ++j) slots[j].off += data_start;
+        }
+    }
 };
 
 // Walk kernels in two layouts (A/B knob COVT_DPLAN_LANES):
@@ -423,7 +440,8 @@ struct CountEmit {
 template <bool kWave>
 __global__ void walk_count(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
                            const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
-                           int32_t* __restrict__ status, int64_t* __restrict__ cnt, int64_t* __restrict__ ob) {
+                           int32_t* __restrict__ status, int64_t* __restrict__ cnt, int64_t* __restrict__ ob,
+                           RawStream* __restrict__ slots) {
     const int32_t t = kWave ? (int32_t)blockIdx.x : (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t > n_tiles) return;
     if (t == n_tiles) {  // the prefix sums' total slot
@@ -431,6 +449,9 @@ __global__ void walk_count(const uint8_t* __restrict__ bytes, uint64_t n_bytes, 
         return;
     }
     CountEmit e{id_mode};
+    e.slots = slots ? slots + (size_t)t * kSlots : nullptr;
+    e.writer = !kWave || threadIdx.x == 0;
+    e.wave = kWave;
     const int st = walk_tile<kWave>(bytes, n_bytes, offs[t], sizes[t], format, e);
     if (!kWave || threadIdx.x == 0) {
         status[t] = st;
@@ -496,9 +517,11 @@ __global__ void walk_emit(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
                           const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                           const int32_t* __restrict__ status, const int64_t* __restrict__ cnt_base,
                           const int64_t* __restrict__ ob_base, int32_t lane_max, covt_stream_info* __restrict__ info,
-                          int32_t* __restrict__ nvals, unsigned long long* __restrict__ totals) {
+                          int32_t* __restrict__ nvals, unsigned long long* __restrict__ totals,
+                          const int64_t* __restrict__ cnt) {
     const int32_t t = kWave ? (int32_t)blockIdx.x : (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t >= n_tiles || status[t]) return;
+    if (cnt && cnt[t] <= kSlots) return;  // emit_slots has this tile's records
     InfoEmit e{t, id_mode, (int64_t)offs[t], info, nvals, cnt_base[t], ob_base[t]};
     e.lane_max = lane_max;
     e.writer = !kWave || threadIdx.x == 0;
@@ -509,6 +532,82 @@ __global__ void walk_emit(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
         atomicAdd(&totals[T_PAYLOAD], (unsigned long long)e.payload);
         atomicAdd(&totals[T_VERTS], (unsigned long long)e.verts);
         atomicAdd(&totals[T_LANE], (unsigned long long)e.lane);
+    }
+}
+
+// The records walk_count left in a tile's slots -> covt_stream_info, one lane per record: output slices
+// by a wave prefix sum of their aligned sizes (the walk's running align16 sum), totals by a wave
+// reduction.  Tiles with more than kSlots streams are left to walk_emit.
+__global__ void emit_slots(const uint64_t* __restrict__ offs, int32_t n_tiles, int32_t id_mode,
+                           const int32_t* __restrict__ status, const int64_t* __restrict__ cnt,
+                           const int64_t* __restrict__ cnt_base, const int64_t* __restrict__ ob_base,
+                           const RawStream* __restrict__ slots, int32_t lane_max, covt_stream_info* __restrict__ info,
+                           int32_t* __restrict__ nvals, unsigned long long* __restrict__ totals) {
+    const int32_t t = blockIdx.x;
+    if (t >= n_tiles || status[t]) return;
+    const int64_t n = cnt[t];
+    if (n > kSlots) return;
+    const int lane = threadIdx.x;
+    const int64_t base = cnt_base[t], tile_off = (int64_t)offs[t];
+    int64_t out = ob_base[t];
+    long long in_bytes = 0, payload = 0, verts = 0, nlane = 0;
+    for (int64_t j0 = 0; j0 < n; j0 += 64) {
+        const int64_t j = j0 + lane;
+        const bool valid = j < n;
+        RawStream s{};
+        int op = COVT_OP_NONE, elem = 4;
+        int64_t nv = 0, oe = 0;
+        if (valid) {
+            s = slots[(size_t)t * kSlots + j];
+            choose_op(s, id_mode, op, nv, elem, oe);
+        }
+        const int64_t out_elems = op == COVT_OP_NONE ? 0 : oe;
+        const long long size = valid ? align16(out_elems * elem) : 0;
+        long long incl = size;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const long long u = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += u;
+        }
+        if (valid) {
+            covt_stream_info si;
+            si.tile = t;
+            si.layer = s.layer;
+            si.column_kind = s.kind;
+            si.stream_type = s.type;
+            si.encoding = s.enc;
+            si.column_type = s.ctype;
+            si.num_values = s.nv;
+            si.byte_length = s.bl;
+            si.num_bits = s.nb;
+            si.op = op;
+            si.elem_bytes = elem;
+            si.desc_index = -1;
+            si.in_off = tile_off + s.off;
+            si.out_elems = out_elems;
+            si.out_off = out + (incl - size);
+            info[base + j] = si;
+            nvals[base + j] = (int32_t)nv;
+            in_bytes += s.bl;
+            payload += out_elems * elem;
+            if (s.kind == 1 && s.type == ST_VERTEX_BUFFER)
+                verts += (s.ctype == CT_ICE || s.ctype == CT_ICE_MORTON) ? s.nv : s.nv / 2;
+            nlane += lane_stream(op, (int32_t)nv, s.bl, lane_max);
+        }
+        out += __shfl(incl, 63, 64);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        in_bytes += __shfl_xor(in_bytes, d, 64);
+        payload += __shfl_xor(payload, d, 64);
+        verts += __shfl_xor(verts, d, 64);
+        nlane += __shfl_xor(nlane, d, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(&totals[T_IN], (unsigned long long)in_bytes);
+        atomicAdd(&totals[T_PAYLOAD], (unsigned long long)payload);
+        atomicAdd(&totals[T_VERTS], (unsigned long long)verts);
+        atomicAdd(&totals[T_LANE], (unsigned long long)nlane);
     }
 }
 
@@ -595,7 +694,10 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
     DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)nt1, s));
     const size_t o_cnt = up256(nt1 * 4), o_ob = o_cnt + up256(nt1 * 8), o_cb = o_ob + up256(nt1 * 8),
                  o_obb = o_cb + up256(nt1 * 8), o_tot = o_obb + up256(nt1 * 8), o_tmp = o_tot + up256(T_N * 8),
-                 tile_bytes = o_tmp + up256(scan_tmp);
+                 o_slots = o_tmp + up256(scan_tmp);
+    const int wl = (int)std::min<int64_t>(256, std::max<int64_t>(0, env_or("COVT_DPLAN_LANES", kWalkLanes)));
+    const bool use_slots = wl == 0 && env_or("COVT_DPLAN_SLOTS", 1) != 0;  // A/B knob: 0 = walk twice
+    const size_t tile_bytes = o_slots + (use_slots ? up256((size_t)n_tiles * kSlots * sizeof(RawStream)) : 0);
     DCHK(hipMalloc(&p->tile_arena, tile_bytes));
     uint8_t* ta = (uint8_t*)p->tile_arena;
     p->d_status = (int32_t*)ta;
@@ -604,13 +706,13 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
     auto* totals = (unsigned long long*)(ta + o_tot);
     DCHK(hipMemsetAsync(totals, 0, T_N * 8, s));
     // 0: a wave per tile, its lanes in lockstep; k > 0: k lanes per workgroup, a lane per tile
-    const int wl = (int)std::min<int64_t>(256, std::max<int64_t>(0, env_or("COVT_DPLAN_LANES", kWalkLanes)));
+    RawStream* slots = use_slots ? (RawStream*)(ta + o_slots) : nullptr;
     if (wl == 0)
         walk_count<true><<<(int)nt1, 64, 512, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
-                                                  id_mode, p->d_status, cnt, ob);
+                                                  id_mode, p->d_status, cnt, ob, slots);
     else
         walk_count<false><<<(int)((nt1 + wl - 1) / wl), wl, (size_t)wl * 64, s>>>(
-            d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cnt, ob);
+            d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cnt, ob, nullptr);
     DCHK(hipGetLastError());
     DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, cnt, cb, (int)nt1, s));
     DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, ob, obb, (int)nt1, s));
@@ -641,13 +743,19 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
     const int32_t lane_max = (int32_t)env_or("COVT_LANE_MAX_BYTES", kLaneMaxBytes);
     const int64_t lane_min = env_or("COVT_LANE_MIN_STREAMS", kLaneMinStreams);
     if (n_tiles) {
-        if (wl == 0)
+        if (slots) {
+            emit_slots<<<n_tiles, 64, 0, s>>>(d_tile_offsets, n_tiles, id_mode, p->d_status, cnt, cb, obb, slots,
+                                              lane_max, p->d_info, nvals, totals);
+            DCHK(hipGetLastError());
+        }
+        if (wl == 0)  // (with slots: only tiles with more than kSlots streams walk again)
             walk_emit<true><<<n_tiles, 64, 512, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
-                                                    id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, totals);
+                                                    id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, totals,
+                                                    slots ? cnt : nullptr);
         else
             walk_emit<false><<<(n_tiles + wl - 1) / wl, wl, (size_t)wl * 64, s>>>(
                 d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cb, obb,
-                lane_max, p->d_info, nvals, totals);
+                lane_max, p->d_info, nvals, totals, nullptr);
         DCHK(hipGetLastError());
     }
     if (ns > 0) {
