@@ -91,8 +91,8 @@ __device__ __noinline__ uintptr_t window_refill(const uint8_t* t, int64_t len, u
 template <bool kWave>
 struct Rd {
     const uint8_t* t;
-    int64_t len;
-    uintptr_t wb;  // window base (16-byte aligned)
+    int64_t len;   // < 2^31 (walk_tile), so tile offsets compare as 32-bit values below
+    int64_t wo;    // the window's start as a tile offset (its address is 16-byte aligned)
     // 8 bytes at tile offset i from a window of the tile kept in LDS (only its base is carried through
     // the walk's loops: a register window of 16 dwords cost ~1,400 64-bit moves per kernel at loop edges).
     // Lane layout: 64 bytes per lane, refilled by that lane.  Wave layout: 512 bytes per wave, refilled by
@@ -101,14 +101,15 @@ struct Rd {
     // Bytes past the tile are unspecified: callers mask by len.
     static constexpr uint32_t kWin = kWave ? 512 : 64;
     __device__ __forceinline__ uint64_t peek8(int64_t i) {
-        const uintptr_t a = (uintptr_t)(t + i);
         const uint4* w = covt_walk_win + (kWave ? 0 : threadIdx.x * 4);
-        if (a < wb || a + 8 > wb + kWin) {
-            wb = window_refill<kWave>(t, len, a);  // out of line: one copy of the refill code
-            if (kWave) wb = ((uintptr_t)__builtin_amdgcn_readfirstlane((int)(wb >> 32)) << 32) |
-                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wb);
+        uint32_t off = (uint32_t)i - (uint32_t)wo;  // wraps when i < wo
+        if (off > kWin - 8) {
+            const uintptr_t b = window_refill<kWave>(t, len, (uintptr_t)(t + i));  // out of line: one copy
+            wo = (int64_t)(b - (uintptr_t)t);
+            if (kWave) wo = (int64_t)(int32_t)__builtin_amdgcn_readfirstlane((int)(int32_t)wo);
+            off = (uint32_t)i - (uint32_t)wo;
         }
-        const uint32_t off = (uint32_t)(a - wb), k = off >> 3, sh = (off & 7) * 8;  // off <= kWin - 8
+        const uint32_t k = off >> 3, sh = (off & 7) * 8;  // off <= kWin - 8
         const uint64_t* q = reinterpret_cast<const uint64_t*>(w);
         const uint64_t lo = q[k];
         return sh ? (lo >> sh) | (q[k + 1] << (64 - sh)) : lo;  // (sh != 0: k + 1 < kWin / 8)
@@ -123,9 +124,22 @@ struct Rd {
     }
     // rd_uv (covt_host.cpp): 64-bit LEB128, at most 10 bytes; up to 8 bytes decoded from one word
     __device__ __forceinline__ bool uv(int64_t& o, uint64_t& v) {
-        const int64_t avail = len - o;
+        const int32_t avail = (int32_t)len - (int32_t)o;
         if (avail <= 0) return false;
         const uint64_t w = peek8(o);
+        {  // values of up to 4 bytes (nearly all metadata) in 32-bit arithmetic
+            const uint32_t w4 = (uint32_t)w;
+            uint32_t stop4 = ~w4 & 0x80808080u;
+            if (avail < 4) stop4 &= (1u << (8 * avail)) - 1;
+            if (stop4) {
+                const int n = (__builtin_ctz(stop4) >> 3) + 1;
+                uint32_t x = (n >= 4 ? w4 : w4 & ((1u << (8 * n)) - 1)) & 0x7f7f7f7fu;
+                x = (x & 0x007f007fu) | ((x & 0x7f007f00u) >> 1);
+                v = (x & 0x3fffu) | ((x & 0x3fff0000u) >> 2);
+                o += n;
+                return true;
+            }
+        }
         uint64_t stop = ~w & 0x8080808080808080ull;
         if (avail < 8) stop &= (1ull << (8 * avail)) - 1;  // only the tile's bytes
         if (stop) {
@@ -152,13 +166,15 @@ struct Rd {
     // rd_j4: DecodingUtils.decodeVarint with its 4-byte cap (DecodingUtils.java:157-186): a byte
     // without bit 7 among the first three ends the value, else the fourth byte does
     __device__ __forceinline__ bool j4(int64_t& o, int32_t& v) {
-        const int64_t avail = len - o;
+        const int32_t avail = (int32_t)len - (int32_t)o;
         if (avail <= 0) return false;
-        const uint64_t w = peek8(o);
-        const uint64_t stop = ~w & 0x808080ull;
-        const int n = stop ? (__builtin_ctzll(stop) >> 3) + 1 : 4;
+        const uint32_t w4 = (uint32_t)peek8(o);
+        const uint32_t stop = ~w4 & 0x808080u;
+        const int n = stop ? (__builtin_ctz(stop) >> 3) + 1 : 4;
         if (n > avail) return false;
-        v = (int32_t)(uint32_t)leb_pack(w, n);
+        uint32_t x = (n >= 4 ? w4 : w4 & ((1u << (8 * n)) - 1)) & 0x7f7f7f7fu;
+        x = (x & 0x007f007fu) | ((x & 0x7f007f00u) >> 1);
+        v = (int32_t)((x & 0x3fffu) | ((x & 0x3fff0000u) >> 2));
         o += n;
         return true;
     }
@@ -390,10 +406,11 @@ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 template <bool kWave, class E>
 __device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes, uint64_t off, uint64_t size, int32_t format, E& emit) {
     if (off > n_bytes || size > n_bytes - off) return COVT_ERR_INVALID_ARG;
+    if (size > 0x7fffffffull) return COVT_ERR_INVALID_ARG;  // device plan limit: tiles under 2 GiB
     Rd<kWave> r;
     r.t = bytes + off;
     r.len = (int64_t)size;
-    r.wb = ~(uintptr_t)0;
+    r.wo = -(int64_t)0x40000000;  // no window yet (every offset misses it)
     return format == COVT_FORMAT_GENC ? walk_genc_dev(r, emit) : walk_gend_dev(r, emit);
 }
 

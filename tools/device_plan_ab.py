@@ -56,8 +56,9 @@ def probe():
     covt = bench.load_covt()
     lib = [t for z in bench.tile_library().values() for _, t in z]
     lib.sort(key=len)
-    for name, tile in (("smallest", lib[0]), ("largest", lib[-1])):
-        for n in (1, 100, 10000):
+    one = os.environ.get("COVT_DPLAN_PROBE") == "2"  # counter runs: the smallest tile alone
+    for name, tile in (("smallest", lib[0]),) + ((("largest", lib[-1]),) if not one else ()):
+        for n in ((1,) if one else (1, 100, 10000)):
             blob, offs, sizes = covt.pack_tiles([tile] * n)
             d_blob = torch.from_numpy(blob).cuda()
             d_off = torch.from_numpy(offs.astype(np.int64)).cuda()
