@@ -100,7 +100,7 @@ struct Rd {
     // look-backs (a column's name, the geometry column's type-ordered rescans) stay inside the window.
     // Bytes past the tile are unspecified: callers mask by len.
     static constexpr uint32_t kWin = kWave ? 512 : 64;
-    __device__ __forceinline__ uint64_t peek8(int64_t i) {
+    __device__ __forceinline__ uint64_t peek8(int32_t i) {
         const uint4* w = covt_walk_win + (kWave ? 0 : threadIdx.x * 4);
         uint32_t off = (uint32_t)i - (uint32_t)wo;  // wraps when i < wo
         if (off > kWin - 8) {
@@ -114,7 +114,7 @@ struct Rd {
         const uint64_t lo = q[k];
         return sh ? (lo >> sh) | (q[k + 1] << (64 - sh)) : lo;  // (sh != 0: k + 1 < kWin / 8)
     }
-    __device__ __forceinline__ int at(int64_t i) { return (int)(peek8(i) & 0xff); }
+    __device__ __forceinline__ int at(int32_t i) { return (int)(peek8(i) & 0xff); }
     // low n bytes (n <= 8) of x's 7-bit groups packed (LEB128 payload)
     __device__ __forceinline__ static uint64_t leb_pack(uint64_t x, int n) {
         x = (n >= 8 ? x : x & ((1ull << (8 * n)) - 1)) & 0x7f7f7f7f7f7f7f7full;
@@ -123,7 +123,7 @@ struct Rd {
         return (x & 0x000000000fffffffull) | ((x & 0x0fffffff00000000ull) >> 4);
     }
     // rd_uv (covt_host.cpp): 64-bit LEB128, at most 10 bytes; up to 8 bytes decoded from one word
-    __device__ __forceinline__ bool uv(int64_t& o, uint64_t& v) {
+    __device__ __forceinline__ bool uv(int32_t& o, uint64_t& v) {
         const int32_t avail = (int32_t)len - (int32_t)o;
         if (avail <= 0) return false;
         const uint64_t w = peek8(o);
@@ -150,7 +150,7 @@ struct Rd {
         }
         if (avail < 8) return false;  // no terminator before the tile's end
         v = leb_pack(w, 8);           // 9- or 10-byte value
-        int64_t q = o + 8;
+        int32_t q = o + 8;
 #pragma unroll 1
         for (int i = 8; i < 10; ++i) {
             if (q >= len) return false;
@@ -165,7 +165,7 @@ struct Rd {
     }
     // rd_j4: DecodingUtils.decodeVarint with its 4-byte cap (DecodingUtils.java:157-186): a byte
     // without bit 7 among the first three ends the value, else the fourth byte does
-    __device__ __forceinline__ bool j4(int64_t& o, int32_t& v) {
+    __device__ __forceinline__ bool j4(int32_t& o, int32_t& v) {
         const int32_t avail = (int32_t)len - (int32_t)o;
         if (avail <= 0) return false;
         const uint32_t w4 = (uint32_t)peek8(o);
@@ -179,7 +179,7 @@ struct Rd {
         return true;
     }
     // the first 16 bytes of a name at o (n <= 16) packed little-endian (register compares below)
-    __device__ __forceinline__ void pack16(int64_t o, uint64_t n, uint64_t& lo, uint64_t& hi) {
+    __device__ __forceinline__ void pack16(int32_t o, uint64_t n, uint64_t& lo, uint64_t& hi) {
         lo = peek8(o);
         if (n < 8) lo &= (1ull << (8 * n)) - 1;
         hi = 0;
@@ -200,7 +200,7 @@ struct Rd {
         return lo_ == l_ && hi_ == h_;                                                                 \
     }())
     // genc_stream_type: Gen C stream name -> StreamType (-1: other)
-    __device__ __forceinline__ int stream_type(int64_t o, uint64_t n) {
+    __device__ __forceinline__ int stream_type(int32_t o, uint64_t n) {
         if (n < 4 || n > 16) return -1;
         uint64_t lo, hi;
         pack16(o, n, lo, hi);
@@ -223,8 +223,9 @@ struct Rd {
         return -1;
     }
     // byte_rle_length: bytes of an ORC byte-RLE stream of n values at o (-1: runs past the tile)
-    __device__ __forceinline__ int32_t byte_rle_length(int64_t o, int32_t n) {
-        int64_t q = o, done = 0;
+    __device__ __forceinline__ int32_t byte_rle_length(int32_t o, int32_t n) {
+        int32_t q = o;
+        int64_t done = 0;
         while (done < n) {
             if (q >= len) return -1;
             const int c = at(q++);
@@ -244,35 +245,35 @@ struct Rd {
 // are laid out in StreamType order (a rescan of that column's few streams).
 template <bool kWave, class E>
 __device__ __forceinline__ int walk_genc_dev(Rd<kWave>& r, E& emit) {
-    const int64_t len = r.len;
-    int64_t o = 0;
+    const int32_t len = (int32_t)r.len;  // 32-bit cursors (walk_tile: tiles under 2 GiB)
+    int32_t o = 0;
     uint64_t version, nlayers;
     if (!r.uv(o, version) || !r.uv(o, nlayers)) return COVT_ERR_TRUNCATED;
     if (version != 1) return COVT_ERR_BAD_HEADER;
     for (uint64_t L = 0; L < nlayers; ++L) {
         uint64_t nlen, extent, nfeat, ncols;
         if (!r.uv(o, nlen) || nlen > (uint64_t)(len - o)) return COVT_ERR_TRUNCATED;
-        o += (int64_t)nlen;
+        o += (int32_t)nlen;
         if (!r.uv(o, extent) || !r.uv(o, nfeat) || !r.uv(o, ncols)) return COVT_ERR_TRUNCATED;
         if (ncols > 4096) return COVT_ERR_BAD_HEADER;
         const int nb = nbits_of_extent(extent);
         int64_t d = 0;  // data bytes of the layer's columns so far
         emit.layer_begin();
-        for (uint64_t c = 0; c < ncols; ++c) {
+        for (uint32_t c = 0; c < (uint32_t)ncols; ++c) {
             uint64_t cn, ns, sn, nv, bl;
             if (!r.uv(o, cn) || cn > (uint64_t)(len - o) || (uint64_t)(len - o) - cn < 2) return COVT_ERR_TRUNCATED;
-            const int64_t name = o;
-            o += (int64_t)cn;
+            const int32_t name = o;
+            o += (int32_t)cn;
             const int dtype = r.at(o), ctype = r.at(o + 1);
             o += 2;
             if (!r.uv(o, ns)) return COVT_ERR_TRUNCATED;
             if (ns > 256) return COVT_ERR_BAD_HEADER;
             const int kind = COVT_IS(name, cn, "id") ? 0 : (COVT_IS(name, cn, "geometry") || dtype == 6) ? 1 : 2;
-            const int64_t s0 = o;
-            for (uint64_t s = 0; s < ns; ++s) {
+            const int32_t s0 = o;
+            for (uint32_t s = 0; s < (uint32_t)ns; ++s) {
                 if (!r.uv(o, sn) || sn > (uint64_t)(len - o)) return COVT_ERR_TRUNCATED;
                 const int type = kind == 0 ? r.stream_type(o, sn) : -1;
-                o += (int64_t)sn;
+                o += (int32_t)sn;
                 if (!r.uv(o, nv) || !r.uv(o, bl) || o >= len) return COVT_ERR_TRUNCATED;
                 const int enc = r.at(o++);
                 if (nv > 0x7fffffff || bl > 0x7fffffff) return COVT_ERR_BAD_HEADER;
@@ -281,11 +282,11 @@ __device__ __forceinline__ int walk_genc_dev(Rd<kWave>& r, E& emit) {
             }
             if (kind == 1) {  // streams of types 4..9 in type order, then the rest (all checked above)
                 for (int want = ST_GEOMETRY_TYPES; want <= ST_VERTEX_BUFFER + 1; ++want) {
-                    int64_t q = s0;
-                    for (uint64_t s = 0; s < ns; ++s) {
+                    int32_t q = s0;
+                    for (uint32_t s = 0; s < (uint32_t)ns; ++s) {
                         r.uv(q, sn);
                         const int type = r.stream_type(q, sn);
-                        q += (int64_t)sn;
+                        q += (int32_t)sn;
                         r.uv(q, nv);
                         r.uv(q, bl);
                         const int enc = r.at(q++);
@@ -297,9 +298,9 @@ __device__ __forceinline__ int walk_genc_dev(Rd<kWave>& r, E& emit) {
                 }
             }
         }
-        if (d > len - o) return COVT_ERR_TRUNCATED;
+        if (d > (int64_t)(len - o)) return COVT_ERR_TRUNCATED;
         emit.layer_end(o);  // the layer's data starts where its metadata ends
-        o += d;
+        o += (int32_t)d;
     }
     return o == len ? COVT_OK : COVT_ERR_BAD_HEADER;
 }
@@ -308,26 +309,26 @@ __device__ __forceinline__ int walk_genc_dev(Rd<kWave>& r, E& emit) {
 // A column's streams follow TreeMap<StreamType> order, the last metadata entry of a type winning.
 template <bool kWave, class E>
 __device__ __forceinline__ int walk_gend_dev(Rd<kWave>& r, E& emit) {
-    const int64_t len = r.len;
-    int64_t o = 0;
+    const int32_t len = (int32_t)r.len;  // 32-bit cursors (walk_tile: tiles under 2 GiB)
+    int32_t o = 0;
     int32_t layer = 0;
     while (o < len) {
         const bool optimized = r.at(o++) & 1;
         int32_t v, extent, nfeat, ncols;
         if (!r.j4(o, v)) return COVT_ERR_TRUNCATED;
         if (!optimized) {
-            if (v < 0 || (int64_t)v > len - o) return COVT_ERR_TRUNCATED;
+            if (v < 0 || v > len - o) return COVT_ERR_TRUNCATED;
             o += v;
         }
         if (!r.j4(o, extent) || !r.j4(o, nfeat) || !r.j4(o, ncols)) return COVT_ERR_TRUNCATED;
         if (ncols < 0 || ncols > 4096) return COVT_ERR_BAD_HEADER;
-        const int64_t meta = o;
+        const int32_t meta = o;
         for (int32_t ci = 0; ci < ncols; ++ci) {  // metadata checks
             int32_t x;
             if (optimized || ci == 0) {
                 if (!r.j4(o, x)) return COVT_ERR_TRUNCATED;
             } else {
-                if (!r.j4(o, x) || x < 0 || (int64_t)x > len - o) return COVT_ERR_TRUNCATED;
+                if (!r.j4(o, x) || x < 0 || x > len - o) return COVT_ERR_TRUNCATED;
                 o += x;
             }
             if (o >= len) return COVT_ERR_TRUNCATED;
@@ -345,7 +346,8 @@ __device__ __forceinline__ int walk_gend_dev(Rd<kWave>& r, E& emit) {
             }
         }
         const int nb = nbits_of_extent((uint32_t)extent);
-        int64_t m = meta, d = o;
+        int32_t m = meta;
+        int64_t d = o;  // data cursor (64-bit: a column's streams may sum past 2^31 before its bound check)
         emit.layer_begin();
         for (int32_t ci = 0; ci < ncols; ++ci) {
             int32_t x, kind;
@@ -358,7 +360,7 @@ __device__ __forceinline__ int walk_gend_dev(Rd<kWave>& r, E& emit) {
                 m += x;
             }
             const int desc = r.at(m++), dtype = (desc >> 3) & 0xF, ctype = desc & 0x7;
-            const int64_t s0 = m;
+            const int32_t s0 = m;
             uint32_t have = 0;  // stream types present
             for (;;) {
                 const int sd = r.at(m++), type = sd >> 4;
@@ -371,7 +373,7 @@ __device__ __forceinline__ int walk_gend_dev(Rd<kWave>& r, E& emit) {
                     break;
             }
             if (kind == 2 && dtype != 0) {  // implicit present stream (walk_gend)
-                const int32_t pl = r.byte_rle_length(d, nfeat < 0 ? 0 : (int32_t)(((int64_t)nfeat + 7) / 8));
+                const int32_t pl = r.byte_rle_length((int32_t)d, nfeat < 0 ? 0 : (int32_t)(((int64_t)nfeat + 7) / 8));
                 if (pl < 0) return COVT_ERR_TRUNCATED;
                 d += pl;
             }
@@ -379,7 +381,7 @@ __device__ __forceinline__ int walk_gend_dev(Rd<kWave>& r, E& emit) {
                 if (!(have >> type & 1) || (kind == 2 && type == ST_PRESENT)) continue;
                 int enc = 0;
                 int32_t nv = 0, bl = 0;
-                for (int64_t q = s0; q < m;) {  // the last entry of this type
+                for (int32_t q = s0; q < m;) {  // the last entry of this type
                     const int sd = r.at(q++);
                     int32_t a, b;
                     r.j4(q, a);
@@ -395,7 +397,7 @@ __device__ __forceinline__ int walk_gend_dev(Rd<kWave>& r, E& emit) {
             if (d > len) return COVT_ERR_TRUNCATED;
         }
         emit.layer_end(0);
-        o = d;
+        o = (int32_t)d;
         ++layer;
     }
     return COVT_OK;
@@ -406,7 +408,7 @@ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 template <bool kWave, class E>
 __device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes, uint64_t off, uint64_t size, int32_t format, E& emit) {
     if (off > n_bytes || size > n_bytes - off) return COVT_ERR_INVALID_ARG;
-    if (size > 0x7fffffffull) return COVT_ERR_INVALID_ARG;  // device plan limit: tiles under 2 GiB
+    if (size > 0x7ff00000ull) return COVT_ERR_INVALID_ARG;  // device plan limit: tiles under 2 GiB
     Rd<kWave> r;
     r.t = bytes + off;
     r.len = (int64_t)size;
