@@ -270,17 +270,43 @@ __device__ __forceinline__ int walk_genc_dev(Rd<kWave>& r, E& emit) {
             if (ns > 256) return COVT_ERR_BAD_HEADER;
             const int kind = COVT_IS(name, cn, "id") ? 0 : (COVT_IS(name, cn, "geometry") || dtype == 6) ? 1 : 2;
             const int32_t s0 = o;
+            // wave layout: the geometry column's streams (type, encoding, sizes) go to an LDS table as
+            // they are read, and the type-ordered layout below reads the table; the lane layout
+            // re-reads the column's metadata once per type instead (each re-read parses the names)
+            uint4* geo = covt_walk_win + Rd<kWave>::kWin / 16;
+            constexpr bool kTable = kWave;
+            uint32_t present = 0;  // geometry stream types seen
             for (uint32_t s = 0; s < (uint32_t)ns; ++s) {
                 if (!r.uv(o, sn) || sn > (uint64_t)(len - o)) return COVT_ERR_TRUNCATED;
-                const int type = kind == 0 ? r.stream_type(o, sn) : -1;
+                const int type = kind == 0 || (kTable && kind == 1) ? r.stream_type(o, sn) : -1;
                 o += (int32_t)sn;
                 if (!r.uv(o, nv) || !r.uv(o, bl) || o >= len) return COVT_ERR_TRUNCATED;
                 const int enc = r.at(o++);
                 if (nv > 0x7fffffff || bl > 0x7fffffff) return COVT_ERR_BAD_HEADER;
-                if (type == ST_DATA) emit(RawStream{(int32_t)L, 0, ST_DATA, enc, ctype, (int32_t)nv, (int32_t)bl, nb, d});
+                if (kind == 0 && type == ST_DATA)
+                    emit(RawStream{(int32_t)L, 0, ST_DATA, enc, ctype, (int32_t)nv, (int32_t)bl, nb, d});
                 if (kind != 1) d += (int64_t)bl;
+                if (kTable && kind == 1) {
+                    geo[s] = make_uint4((uint32_t)(type & 0xff) | ((uint32_t)enc << 8), (uint32_t)nv, (uint32_t)bl, 0);
+                    if (type >= ST_GEOMETRY_TYPES && type <= ST_VERTEX_BUFFER) present |= 1u << type;
+                }
             }
-            if (kind == 1) {  // streams of types 4..9 in type order, then the rest (all checked above)
+            if (kind == 1 && kTable) {  // types 4..9 in type order (metadata order within a type), then the rest
+                for (int want = ST_GEOMETRY_TYPES; want <= ST_VERTEX_BUFFER; ++want) {
+                    if (!(present >> want & 1)) continue;
+                    for (uint32_t s = 0; s < (uint32_t)ns; ++s) {
+                        const uint4 g = geo[s];
+                        if ((int)(g.x & 0xff) != want) continue;
+                        emit(RawStream{(int32_t)L, 1, want, (int)(g.x >> 8), ctype, (int32_t)g.y, (int32_t)g.z, nb, d});
+                        d += (int64_t)g.z;
+                    }
+                }
+                for (uint32_t s = 0; s < (uint32_t)ns; ++s) {
+                    const uint4 g = geo[s];
+                    const int type = (int)(int8_t)(g.x & 0xff);
+                    if (type < ST_GEOMETRY_TYPES || type > ST_VERTEX_BUFFER) d += (int64_t)g.z;
+                }
+            } else if (kind == 1) {  // streams of types 4..9 in type order, then the rest (all checked above)
                 for (int want = ST_GEOMETRY_TYPES; want <= ST_VERTEX_BUFFER + 1; ++want) {
                     int32_t q = s0;
                     for (uint32_t s = 0; s < (uint32_t)ns; ++s) {
@@ -290,9 +316,9 @@ __device__ __forceinline__ int walk_genc_dev(Rd<kWave>& r, E& emit) {
                         r.uv(q, nv);
                         r.uv(q, bl);
                         const int enc = r.at(q++);
-                        const bool geo = type >= ST_GEOMETRY_TYPES && type <= ST_VERTEX_BUFFER;
-                        if (want <= ST_VERTEX_BUFFER ? type != want : geo) continue;
-                        if (geo) emit(RawStream{(int32_t)L, 1, type, enc, ctype, (int32_t)nv, (int32_t)bl, nb, d});
+                        const bool isgeo = type >= ST_GEOMETRY_TYPES && type <= ST_VERTEX_BUFFER;
+                        if (want <= ST_VERTEX_BUFFER ? type != want : isgeo) continue;
+                        if (isgeo) emit(RawStream{(int32_t)L, 1, type, enc, ctype, (int32_t)nv, (int32_t)bl, nb, d});
                         d += (int64_t)bl;
                     }
                 }
@@ -727,7 +753,7 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
     // 0: a wave per tile, its lanes in lockstep; k > 0: k lanes per workgroup, a lane per tile
     RawStream* slots = use_slots ? (RawStream*)(ta + o_slots) : nullptr;
     if (wl == 0)
-        walk_count<true><<<(int)nt1, 64, 512, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
+        walk_count<true><<<(int)nt1, 64, 512 + 256 * 16, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
                                                   id_mode, p->d_status, cnt, ob, slots);
     else
         walk_count<false><<<(int)((nt1 + wl - 1) / wl), wl, (size_t)wl * 64, s>>>(
@@ -768,7 +794,7 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
             DCHK(hipGetLastError());
         }
         if (wl == 0)  // (with slots: only tiles with more than kSlots streams walk again)
-            walk_emit<true><<<n_tiles, 64, 512, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
+            walk_emit<true><<<n_tiles, 64, 512 + 256 * 16, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
                                                     id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, totals,
                                                     slots ? cnt : nullptr);
         else
