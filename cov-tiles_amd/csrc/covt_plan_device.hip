@@ -163,6 +163,34 @@ struct Rd {
         }
         return false;
     }
+    // LEB128 payload of the low n (<= 4) bytes of x
+    __device__ __forceinline__ static uint32_t leb_pack4(uint32_t x, int n) {
+        x = (n >= 4 ? x : x & ((1u << (8 * n)) - 1)) & 0x7f7f7f7fu;
+        x = (x & 0x007f007fu) | ((x & 0x7f007f00u) >> 1);
+        return (x & 0x3fffu) | ((x & 0x3fff0000u) >> 2);
+    }
+    // Gen C stream record tail (numValues, byteLength varints and the encoding byte) from one 64-bit word
+    // when both varints have at most 4 bytes and all of it lies in the tile; false (nothing consumed)
+    // otherwise, and the caller reads the fields one by one (same values and statuses)
+    __device__ __forceinline__ bool rec3(int32_t& o, uint64_t& nv, uint64_t& bl, int& enc) {
+        const int32_t avail = (int32_t)len - o;
+        if (avail < 3) return false;
+        const uint64_t w = peek8(o);
+        uint64_t stop = ~w & 0x8080808080808080ull;
+        if (avail < 8) stop &= (1ull << (8 * avail)) - 1;
+        if (!stop) return false;
+        const int e1 = __builtin_ctzll(stop) >> 3;  // numValues' last byte
+        if (e1 > 3) return false;
+        const uint64_t stop2 = stop & (~0ull << (8 * (e1 + 1)));
+        if (!stop2) return false;
+        const int e2 = __builtin_ctzll(stop2) >> 3;  // byteLength's last byte
+        if (e2 - e1 > 4 || e2 + 1 >= avail || e2 + 1 >= 8) return false;
+        nv = leb_pack4((uint32_t)w, e1 + 1);
+        bl = leb_pack4((uint32_t)(w >> (8 * (e1 + 1))), e2 - e1);
+        enc = (int)((w >> (8 * (e2 + 1))) & 0xff);
+        o += e2 + 2;
+        return true;
+    }
     // rd_j4: DecodingUtils.decodeVarint with its 4-byte cap (DecodingUtils.java:157-186): a byte
     // without bit 7 among the first three ends the value, else the fourth byte does
     __device__ __forceinline__ bool j4(int32_t& o, int32_t& v) {
@@ -280,8 +308,11 @@ __device__ __forceinline__ int walk_genc_dev(Rd<kWave>& r, E& emit) {
                 if (!r.uv(o, sn) || sn > (uint64_t)(len - o)) return COVT_ERR_TRUNCATED;
                 const int type = kind == 0 || (kTable && kind == 1) ? r.stream_type(o, sn) : -1;
                 o += (int32_t)sn;
-                if (!r.uv(o, nv) || !r.uv(o, bl) || o >= len) return COVT_ERR_TRUNCATED;
-                const int enc = r.at(o++);
+                int enc;
+                if (!r.rec3(o, nv, bl, enc)) {
+                    if (!r.uv(o, nv) || !r.uv(o, bl) || o >= len) return COVT_ERR_TRUNCATED;
+                    enc = r.at(o++);
+                }
                 if (nv > 0x7fffffff || bl > 0x7fffffff) return COVT_ERR_BAD_HEADER;
                 if (kind == 0 && type == ST_DATA)
                     emit(RawStream{(int32_t)L, 0, ST_DATA, enc, ctype, (int32_t)nv, (int32_t)bl, nb, d});
