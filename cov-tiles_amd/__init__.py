@@ -140,6 +140,27 @@ GEOM_TOO_LARGE = 0x80000000
 GEOM_MAX_CAP = 1 << 25
 assert C.sizeof(GeomDesc) == 160 and GEOM_INFO_DTYPE.itemsize == 112
 
+class PlanOptions(C.Structure):
+    """covt_plan_options (include/covt.h): the plan-layout options.  ``PlanOptions()`` holds the
+    library defaults (covt_plan_options_init); keyword arguments override fields, e.g.
+    ``PlanOptions(split_min=-1)`` plans no split streams."""
+    _fields_ = [("size", C.c_uint32), ("flags", C.c_uint32), ("split_min", C.c_int64), ("split_ratio", C.c_int64),
+                ("split_chunk", C.c_int64), ("split_values", C.c_int64), ("fpf_split_weight", C.c_int32),
+                ("lane_max_bytes", C.c_int32), ("lane_min_streams", C.c_int64), ("plan_threads", C.c_int32),
+                ("host_prefault", C.c_int32), ("prefault_threads", C.c_int32), ("device_walk", C.c_int32)]
+
+    def __init__(self, **kw):
+        super().__init__()
+        lib().covt_plan_options_init(C.byref(self))
+        for k, v in kw.items():
+            if k not in {f[0] for f in self._fields_} or k == "size":
+                raise TypeError("unknown plan option %r" % k)
+            setattr(self, k, v)
+
+    def __repr__(self):
+        return "PlanOptions(%s)" % ", ".join("%s=%r" % (f, getattr(self, f)) for f, _ in self._fields_[1:])
+
+
 STREAM_INFO_DTYPE = np.dtype([(n, np.int32 if t is C.c_int32 else np.int64) for n, t in StreamInfo._fields_])
 assert STREAM_INFO_DTYPE.itemsize == C.sizeof(StreamInfo)
 assert C.sizeof(StreamDesc) == 32
@@ -163,6 +184,7 @@ EXPORTED_SYMBOLS = (
     "covt_device_plan_output_bytes", "covt_device_plan_totals", "covt_device_plan_family_counts",
     "covt_device_plan_descs_device", "covt_device_plan_streams_device", "covt_device_plan_tile_status_device",
     "covt_device_plan_order_device", "covt_device_plan_copy", "covt_device_plan_decode",
+    "covt_plan_options_init", "covt_plan_create_opts", "covt_device_plan_create_opts",
 )
 
 
@@ -236,6 +258,12 @@ def lib() -> C.CDLL:
     L.covt_plan_assemble_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
     L.covt_plan_create_ex.argtypes = [u8p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
                                       C.c_int32, C.c_uint32, C.POINTER(vp)]
+    L.covt_plan_options_init.argtypes = [vp]
+    L.covt_plan_options_init.restype = None
+    L.covt_plan_create_opts.argtypes = [u8p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
+                                        C.c_int32, vp, C.POINTER(vp)]
+    L.covt_device_plan_create_opts.argtypes = [vp, C.c_uint64, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, vp,
+                                               C.POINTER(vp)]
     L.covt_plan_num_property_columns.argtypes = [vp]
     L.covt_plan_num_property_columns.restype = C.c_int64
     L.covt_plan_property_bytes.argtypes = [vp]
@@ -460,16 +488,20 @@ class Plan:
     """Host-side container walk of a tile batch -> per-stream descriptors (covt_plan_create)."""
 
     def __init__(self, blob: np.ndarray, offsets, sizes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT,
-                 flags: int = 0):
+                 flags: int = 0, options: Optional[PlanOptions] = None):
         L = lib()
         self.blob = np.ascontiguousarray(blob, dtype=np.uint8)
         self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         self.sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
         self.n_tiles = int(self.offsets.size)
+        opts = PlanOptions() if options is None else PlanOptions(**{f: getattr(options, f) for f, _ in
+                                                                   PlanOptions._fields_[1:]})
+        opts.flags |= flags
+        self.options = opts
         h = C.c_void_p()
-        _raise(L.covt_plan_create_ex(_ptr(self.blob, C.c_uint8), _ptr(self.offsets, C.c_uint64),
-                                     _ptr(self.sizes, C.c_uint64), self.n_tiles, fmt, id_mode, flags, C.byref(h)),
-               "covt_plan_create")
+        _raise(L.covt_plan_create_opts(_ptr(self.blob, C.c_uint8), _ptr(self.offsets, C.c_uint64),
+                                       _ptr(self.sizes, C.c_uint64), self.n_tiles, fmt, id_mode, C.byref(opts),
+                                       C.byref(h)), "covt_plan_create")
         self._h = h
         self.num_streams = int(L.covt_plan_num_streams(h))
         self.output_bytes = int(L.covt_plan_output_bytes(h))
@@ -508,9 +540,10 @@ class Plan:
             L.covt_plan_property_descs(h, self.pdescs.ctypes.data)
 
     @classmethod
-    def from_tiles(cls, tiles: List[bytes], fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT, flags: int = 0):
+    def from_tiles(cls, tiles: List[bytes], fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT, flags: int = 0,
+                   options: Optional[PlanOptions] = None):
         blob, offs, sizes = pack_tiles(tiles)
-        return cls(blob, offs, sizes, fmt, id_mode, flags)
+        return cls(blob, offs, sizes, fmt, id_mode, flags, options)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -761,7 +794,8 @@ class DevicePlan:
     descriptor fill run on the current torch stream; the result has the host plan's layout exactly
     (Plan.streams / Plan.descs / Plan.family_counts for a batch that splits nothing)."""
 
-    def __init__(self, d_blob, offsets, sizes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT, stream=None):
+    def __init__(self, d_blob, offsets, sizes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT, stream=None,
+                 options: Optional[PlanOptions] = None):
         import torch
 
         self.device = d_blob.device
@@ -777,9 +811,10 @@ class DevicePlan:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         h = C.c_void_p()
         with torch.cuda.device(self.device):
-            _raise(lib().covt_device_plan_create(d_blob.data_ptr(), d_blob.numel(), self.d_off.data_ptr(),
-                                                 self.d_size.data_ptr(), self.n_tiles, fmt, id_mode,
-                                                 s.cuda_stream, C.byref(h)), "covt_device_plan_create")
+            _raise(lib().covt_device_plan_create_opts(d_blob.data_ptr(), d_blob.numel(), self.d_off.data_ptr(),
+                                                      self.d_size.data_ptr(), self.n_tiles, fmt, id_mode,
+                                                      C.byref(options) if options is not None else None,
+                                                      s.cuda_stream, C.byref(h)), "covt_device_plan_create")
         self._h = h
         L = lib()
         self.num_streams = L.covt_device_plan_num_streams(h)

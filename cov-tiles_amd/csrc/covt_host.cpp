@@ -432,11 +432,6 @@ int run_one(const uint8_t* region, size_t region_len, size_t pad_to, int op, int
 }
 
 // stream-level wrappers: varint / RLE ops read [pos, buf_len) (Java reads up to the array end)
-int64_t env_i64(const char* name, int64_t dflt) {
-    const char* e = std::getenv(name);
-    return (e && *e) ? std::strtoll(e, nullptr, 10) : dflt;
-}
-
 // Most bytes decoding n values of `op` can read from *pos on: Java's capped varints take <= 4 bytes
 // each (DecodingUtils.java:157-186); an ORC RLE reader reads whole groups, so past n values it may
 // still read the rest of the last group (<= 128 literal varints of <= 10 bytes, RunLengthIntegerReader;
@@ -581,6 +576,10 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
                    uint8_t* d_out, covt_stream_result* d_res, hipStream_t s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return COVT_ERR_DEVICE;
+    if (s) {  // the auxiliary streams must belong to the device of the caller's stream
+        int sdev = -1;
+        if (hipStreamGetDevice(s, &sdev) != hipSuccess || sdev != dev) return COVT_ERR_DEVICE;
+    }
     ForkCtx* fp = fork_acquire(dev);
     if (!fp) return COVT_ERR_DEVICE;
     struct Back { ForkCtx* f; ~Back() { fork_release(f); } } back{fp};
@@ -617,29 +616,14 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
     if (splits) {
         if (hipMemsetAsync(d_res + off[kSplitV], 0, (size_t)n_split * sizeof(covt_stream_result), s) != hipSuccess)
             return COVT_ERR_DEVICE;
-        if (env_i64("COVT_SPLIT_QUEUES", 2) == 2) {  // RLE chunks behind the varint queue (1: with the RLE family)
-            add(kSplitV, COVT_FAMILY_VARINT, kSplitR);
-            add(COVT_FAMILY_FASTPFOR, -1, -1);
-            add(COVT_FAMILY_RLE, COVT_FAMILY_LANE, -1);
-            add(kSplitF, -1, -1);
-        } else {
-            add(kSplitV, COVT_FAMILY_VARINT, -1);
-            add(COVT_FAMILY_FASTPFOR, -1, -1);
-            add(kSplitR, COVT_FAMILY_RLE, COVT_FAMILY_LANE);
-            add(kSplitF, -1, -1);
-        }
+        // RLE chunks behind the varint queue (round 2 A/B: with the RLE family, config 3 0.132 -> 0.150 ms)
+        add(kSplitV, COVT_FAMILY_VARINT, kSplitR);
+        add(COVT_FAMILY_FASTPFOR, -1, -1);
+        add(COVT_FAMILY_RLE, COVT_FAMILY_LANE, -1);
+        add(kSplitF, -1, -1);
     } else {
-        // queue order (A/B knob COVT_QUEUE_ORDER: four family digits, e.g. 2103 = FastPFOR, varint, RLE, lane)
-        const int64_t ord = env_i64("COVT_QUEUE_ORDER", 2103);
-        int fo[4] = {COVT_FAMILY_FASTPFOR, COVT_FAMILY_VARINT, COVT_FAMILY_RLE, COVT_FAMILY_LANE};
-        bool seen[4] = {false, false, false, false}, ok = ord >= 0 && ord <= 3333;
-        for (int i = 0; i < 4 && ok; ++i) {
-            const int f = (int)(ord / (int64_t)(i == 0 ? 1000 : i == 1 ? 100 : i == 2 ? 10 : 1) % 10);
-            ok = f <= 3 && !seen[f];
-            if (ok) seen[f] = true, fo[i] = f;
-        }
-        if (!ok) fo[0] = COVT_FAMILY_FASTPFOR, fo[1] = COVT_FAMILY_VARINT, fo[2] = COVT_FAMILY_RLE, fo[3] = COVT_FAMILY_LANE;
-        for (int f : fo) add(f, -1, -1);
+        // queue order FastPFOR, varint, RLE, lane (round 2 A/B of all orders: within noise)
+        for (int f : {COVT_FAMILY_FASTPFOR, COVT_FAMILY_VARINT, COVT_FAMILY_RLE, COVT_FAMILY_LANE}) add(f, -1, -1);
     }
     if (nq > 1 && hipEventRecord(f.fork, s) != hipSuccess) return COVT_ERR_DEVICE;
     int st = COVT_OK;
@@ -679,21 +663,19 @@ namespace {
 
 // Pageable caller memory for the D2H: fault its pages in on host threads (MADV_POPULATE_WRITE) while
 // the device runs H2D + decode, so the copy itself meets resident pages.  Started
-// before the H2D is queued and joined just before the output D2H.  COVT_HOST_PREFAULT=0 turns it
-// off.  Kernels without MADV_POPULATE_WRITE (< 5.14) touch each page.
+// before the H2D is queued and joined just before the output D2H.  covt_plan_options.host_prefault = 0
+// turns it off.  Kernels without MADV_POPULATE_WRITE (< 5.14) touch each page.
 struct Prefault {
     std::vector<std::thread> th;
-    Prefault(uint8_t* p, size_t n) {
-        const char* e = std::getenv("COVT_HOST_PREFAULT");
-        if ((e && e[0] == '0') || n < (64u << 20)) return;
+    Prefault(uint8_t* p, size_t n, bool on, int threads) {
+        if (!on || n < (64u << 20)) return;
 #ifdef MADV_POPULATE_WRITE
         const uintptr_t pg = 4096, lo = ((uintptr_t)p + pg - 1) & ~(pg - 1), hi = ((uintptr_t)p + n) & ~(pg - 1);
         if (hi <= lo) return;
         const size_t len = hi - lo;
         const unsigned hw = std::thread::hardware_concurrency();
         // (fresh pages are zeroed by the kernel on first touch: ~2.5 us a page on one thread)
-        const size_t nthr = std::max<size_t>(
-            1, std::min<size_t>((size_t)env_i64("COVT_HOST_PREFAULT_THREADS", 8), hw ? hw : 1));
+        const size_t nthr = std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), hw ? hw : 1));
         for (size_t k = 0; k < nthr; ++k) {
             const uintptr_t a = lo + ((len * k / nthr) & ~(pg - 1));
             const uintptr_t b = k + 1 == nthr ? hi : lo + ((len * (k + 1) / nthr) & ~(pg - 1));
@@ -708,6 +690,7 @@ struct Prefault {
         }
 #else
         (void)p;
+        (void)threads;
 #endif
     }
     void join() {
@@ -723,6 +706,8 @@ struct Prefault {
 // rebased to that range (built once), and the device buffers, kept on the plan across calls.
 struct HostShard {
     int device = -1;
+    bool prefault = true;
+    int prefault_threads = 8;
     uint64_t in_lo = 0, in_len = 0;  // caller bytes [in_lo, in_lo + in_len) -> d_in
     int64_t out_lo = 0, out_len = 0; // plan output bytes [out_lo, out_lo + out_len) <- d_out
     std::vector<covt_stream_desc> descs;  // launch order, offsets rebased
@@ -766,13 +751,17 @@ struct HostShard {
         return hipStreamSynchronize(s) == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
     }
 
-    // one H2D of the shard's tile bytes, one grouped launch, one D2H straight into the caller's buffer
+    // one H2D of the shard's tile bytes, one grouped launch, one D2H straight into the caller's buffer.
+    // The shard's device is selected on every call, not only when open() creates the buffers: a later
+    // call may run on a fresh host thread (current device 0) and launch_grouped takes its auxiliary
+    // streams from the current device.
     int run(const uint8_t* bytes, uint8_t* host_out, covt_stream_result* host_res) {
+        if (device < 0 || hipSetDevice(device) != hipSuccess) return COVT_ERR_DEVICE;
         int st = open();
         if (st) return st;
         if (descs.empty()) return COVT_OK;
         auto chk = [&](hipError_t e) { if (e != hipSuccess && st == COVT_OK) st = COVT_ERR_DEVICE; };
-        Prefault pf(host_out + out_lo, (size_t)out_len);
+        Prefault pf(host_out + out_lo, (size_t)out_len, prefault, prefault_threads);
         if (in_len) chk(hipMemcpyAsync(d_in, bytes + in_lo, in_len, hipMemcpyHostToDevice, s));
         if (st == COVT_OK) st = launch_grouped(d_in, d_desc, fam, d_out, d_res, s);
         if (st == COVT_OK) chk(hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(covt_stream_result),
@@ -789,6 +778,7 @@ struct HostShard {
 };
 
 struct covt_plan {
+    covt_plan_options opts{};  // resolved options the plan was made with
     int32_t n_tiles = 0;
     std::vector<int32_t> tile_status;
     std::vector<uint64_t> tile_off, tile_size;
@@ -1342,12 +1332,59 @@ void fpf_chunk_states(const uint8_t* b, int32_t byte_length, int32_t n, int64_t 
 
 extern "C" {
 
+}  // extern "C"
+
+bool covt_resolve_options(const covt_plan_options* in, covt_plan_options& o) {
+    if (!in) {
+        covt_plan_options_init(&o);
+        return true;
+    }
+    if (in->size != sizeof(covt_plan_options)) return false;
+    o = *in;
+    return o.split_ratio >= 0 && o.split_chunk >= 64 && o.split_values >= 256 && o.split_values % 256 == 0 &&
+           o.fpf_split_weight >= 1 && o.lane_min_streams >= 0 && o.plan_threads >= 0 && o.prefault_threads >= 1 &&
+           o.device_walk >= 0 && o.device_walk <= 256 && (o.host_prefault == 0 || o.host_prefault == 1);
+}
+
+extern "C" {
+
+void covt_plan_options_init(covt_plan_options* o) {
+    if (!o) return;
+    *o = covt_plan_options{};
+    o->size = (uint32_t)sizeof(covt_plan_options);
+    o->flags = 0;
+    o->split_min = COVT_SPLIT_MIN;
+    o->split_ratio = COVT_SPLIT_RATIO;
+    o->split_chunk = COVT_SPLIT_CHUNK;
+    o->split_values = COVT_SPLIT_VALUES;
+    o->fpf_split_weight = 1;
+    o->lane_max_bytes = COVT_LANE_MAX_BYTES;
+    o->lane_min_streams = COVT_LANE_MIN_STREAMS;
+    o->plan_threads = 0;
+    o->host_prefault = 1;
+    o->prefault_threads = 8;
+    o->device_walk = 0;
+}
+
 int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
                         int32_t n_tiles, int32_t format, int32_t id_mode, uint32_t flags, covt_plan** out) {
+    covt_plan_options o;
+    covt_plan_options_init(&o);
+    o.flags = flags;
+    return covt_plan_create_opts(bytes, tile_offsets, tile_sizes, n_tiles, format, id_mode, &o, out);
+}
+
+int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
+                          int32_t n_tiles, int32_t format, int32_t id_mode, const covt_plan_options* opts,
+                          covt_plan** out) {
+    covt_plan_options o;
+    if (!covt_resolve_options(opts, o)) return COVT_ERR_INVALID_ARG;
+    const uint32_t flags = o.flags;
     if (!out || n_tiles < 0 || (n_tiles && (!bytes || !tile_offsets || !tile_sizes))) return COVT_ERR_INVALID_ARG;
     if (flags & ~COVT_PLAN_PROPERTIES) return COVT_ERR_INVALID_ARG;
     if (format != COVT_FORMAT_GENC && format != COVT_FORMAT_GEND) return COVT_ERR_INVALID_ARG;
     auto* p = new covt_plan();
+    p->opts = o;
     p->n_tiles = n_tiles;
     p->format = format;
     p->tile_status.assign((size_t)n_tiles, 0);
@@ -1361,7 +1398,8 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         std::vector<int32_t> rs_end, props_end;  // per tile of the chunk: end index in rs / props
     };
     const int32_t n_thr = (int32_t)std::max<int64_t>(
-        1, std::min<int64_t>({env_i64("COVT_PLAN_THREADS", std::min<int64_t>(std::thread::hardware_concurrency(), 16)),
+        1, std::min<int64_t>({o.plan_threads > 0 ? (int64_t)o.plan_threads
+                                                 : std::min<int64_t>(std::thread::hardware_concurrency(), 16),
                               ((int64_t)n_tiles + 63) / 64}));
     std::vector<Chunk> chunks((size_t)n_thr);
     auto walk_chunk = [&](Chunk* c) {
@@ -1490,9 +1528,9 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
     auto stream_cost = [](const covt_stream_info& s) {
         return (int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4;
     };
-    int64_t split_min = env_i64("COVT_SPLIT_MIN", COVT_SPLIT_MIN);
-    const int64_t split_ratio = env_i64("COVT_SPLIT_RATIO", COVT_SPLIT_RATIO);
-    int32_t lane_max = (int32_t)env_i64("COVT_LANE_MAX_BYTES", kLaneMaxBytes);  // A/B knob
+    int64_t split_min = o.split_min;
+    const int64_t split_ratio = o.split_ratio;
+    int32_t lane_max = o.lane_max_bytes;
     {
         // batch totals: cost (split threshold) and the streams the lane kernel would take (it decodes 64
         // streams per wave, each serially: a wave of 100-250-value streams takes ~80-110 us, worth it only
@@ -1510,11 +1548,10 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
         });
         const int64_t total = tot_cost.load(), n_lane = tot_lane.load();
         if (split_min >= 0 && split_ratio > 0) split_min = std::max<int64_t>(split_min, total / split_ratio);
-        if (n_lane < env_i64("COVT_LANE_MIN_STREAMS", kLaneMinStreams)) lane_max = -1;
+        if (n_lane < o.lane_min_streams) lane_max = -1;
     }
-    const int64_t split_chunk = std::max<int64_t>(64, env_i64("COVT_SPLIT_CHUNK", COVT_SPLIT_CHUNK));
-    const int64_t split_values =
-        std::max<int64_t>(256, env_i64("COVT_SPLIT_VALUES", COVT_SPLIT_VALUES) / 256 * 256);  // FastPFOR
+    const int64_t split_chunk = o.split_chunk;
+    const int64_t split_values = o.split_values;  // FastPFOR: whole blocks
     // long RLE streams: chunk boundaries from the host walk (stream index -> chunks, consumed)
     std::unordered_map<size_t, std::pair<std::vector<RleChunk>, int32_t>> rle_split;
     if (split_min >= 0) {
@@ -1527,7 +1564,7 @@ int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, cons
             if (!ch.empty()) rle_split.emplace(i, std::make_pair(std::move(ch), consumed));
         }
     }
-    const int64_t fpf_w = std::max<int64_t>(1, env_i64("COVT_FPF_SPLIT_WEIGHT", 1));
+    const int64_t fpf_w = o.fpf_split_weight;
     // descriptors per stream: 1, or COVT_SPLIT_SLOTS per chunk of a split stream
     std::vector<int32_t> ndesc(ns);
     par_for(n_thr, (int64_t)ns, [&](int64_t i0, int64_t i1) {
@@ -1742,6 +1779,8 @@ void build_shards(const covt_plan* p, const std::vector<int32_t>& devs, std::vec
     for (size_t g = 0; g < rng.size(); ++g) {
         auto h = std::make_unique<HostShard>();
         h->device = devs[g];
+        h->prefault = p->opts.host_prefault != 0;
+        h->prefault_threads = p->opts.prefault_threads;
         const int32_t t0 = rng[g].first, t1 = rng[g].second;
         uint64_t lo = UINT64_MAX, hi = 0;
         for (int32_t t = t0; t < t1; ++t) {

@@ -24,8 +24,12 @@ int covt_op_family_of(int op);
 // Plan rule for the lane-per-stream kernel: RLE streams of at most kLaneMaxValues values and
 // kLaneMaxBytes bytes (a lane decodes serially; larger streams amortise a wave's window setup).
 constexpr int32_t kLaneMaxValues = 256;
-constexpr int64_t kLaneMinStreams = 16384;  // plans with fewer lane-eligible streams use no lane kernel
-constexpr int32_t kLaneMaxBytes = 64;  // the lane's first 68-byte window: no reloads (A/B: COVT_LANE_MAX_BYTES)
+constexpr int64_t kLaneMinStreams = COVT_LANE_MIN_STREAMS;  // plans with fewer lane-eligible streams use no lane kernel
+constexpr int32_t kLaneMaxBytes = COVT_LANE_MAX_BYTES;  // the lane's first 68-byte window: no reloads
+
+// The caller's plan options checked and completed (NULL: the defaults); false for a wrong struct
+// size or out-of-range fields.  Shared by the host and the device plan.
+bool covt_resolve_options(const covt_plan_options* in, covt_plan_options& out);
 __host__ __device__ inline bool lane_stream(int op, int32_t num_values, int32_t byte_length, int32_t max_bytes = kLaneMaxBytes) {
     return (op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_BYTE_RLE_RAW || op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_S64 ||
             op == COVT_OP_RLE_I32) &&

@@ -504,11 +504,11 @@ struct CountEmit {
     }
 };
 
-// Walk kernels in two layouts (A/B knob COVT_DPLAN_LANES):
+// Walk kernels in two layouts (covt_plan_options.device_walk):
 //  * 0 (default): a wave per tile, its lanes in lockstep on values the compiler proves uniform (the
 //    walk compiles to scalar code, 32-54 VGPRs), a 512-byte LDS window refilled by 32 lanes at once,
 //    lane 0 writing the records and all lanes rebasing a layer's offsets;
-//  * k > 0: k lanes per workgroup, a lane per tile with a 64-byte window (lanes diverge, so k = 1 is
+//  * k >= 2: k lanes per workgroup, a lane per tile with a 64-byte window (lanes diverge, so k = 1 is
 //    best: 1 / 2 / 4 / 16 lanes measured 7.9 / 8.6 / 8.1 / 11.9 ms for the whole plan).
 // Both take ~0.7 ms for one tile alone and ~3.6 ms per walk kernel for the 10k-tile batch
 // (profiles/r02/device_plan_ab.txt); the walk is a serial chain per tile whose step time neither the
@@ -729,15 +729,8 @@ __global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const u
     si.desc_index = (int32_t)k;
 }
 
-int64_t env_or(const char* name, int64_t dflt) {
-    const char* v = std::getenv(name);
-    return v && *v ? std::strtoll(v, nullptr, 10) : dflt;
-}
-
 size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Lanes per workgroup of the walk kernels (A/B knob COVT_DPLAN_LANES; see walk_count)
-constexpr int kWalkLanes = 0;
 
 }  // namespace
 
@@ -746,6 +739,15 @@ extern "C" {
 int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_tile_offsets,
                             const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                             void* hip_stream, covt_device_plan** out) {
+    return covt_device_plan_create_opts(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode,
+                                        nullptr, hip_stream, out);
+}
+
+int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_tile_offsets,
+                                 const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
+                                 const covt_plan_options* opts, void* hip_stream, covt_device_plan** out) {
+    covt_plan_options o;
+    if (!covt_resolve_options(opts, o) || o.flags) return COVT_ERR_INVALID_ARG;
     if (!out || n_tiles < 0 || (n_tiles && (!d_bytes || !d_tile_offsets || !d_tile_sizes))) return COVT_ERR_INVALID_ARG;
     if (format != COVT_FORMAT_GENC && format != COVT_FORMAT_GEND) return COVT_ERR_INVALID_ARG;
     if (id_mode != COVT_ID_FORMAT && id_mode != COVT_ID_JAVA) return COVT_ERR_INVALID_ARG;
@@ -771,8 +773,9 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
     const size_t o_cnt = up256(nt1 * 4), o_ob = o_cnt + up256(nt1 * 8), o_cb = o_ob + up256(nt1 * 8),
                  o_obb = o_cb + up256(nt1 * 8), o_tot = o_obb + up256(nt1 * 8), o_tmp = o_tot + up256(T_N * 8),
                  o_slots = o_tmp + up256(scan_tmp);
-    const int wl = (int)std::min<int64_t>(256, std::max<int64_t>(0, env_or("COVT_DPLAN_LANES", kWalkLanes)));
-    const bool use_slots = wl == 0 && env_or("COVT_DPLAN_SLOTS", 1) != 0;  // A/B knob: 0 = walk twice
+    // device_walk 0: a wave per tile with per-tile slots; 1: the same walk twice; k >= 2: k lanes per workgroup
+    const int wl = o.device_walk >= 2 ? o.device_walk : 0;
+    const bool use_slots = o.device_walk == 0;
     const size_t tile_bytes = o_slots + (use_slots ? up256((size_t)n_tiles * kSlots * sizeof(RawStream)) : 0);
     DCHK(hipMalloc(&p->tile_arena, tile_bytes));
     uint8_t* ta = (uint8_t*)p->tile_arena;
@@ -816,8 +819,8 @@ int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint
     uint32_t *v0 = (uint32_t*)(sa + o_v0), *v1 = (uint32_t*)(sa + o_v1);
     p->d_order = v1;
     p->d_desc = (covt_stream_desc*)(sa + o_d);
-    const int32_t lane_max = (int32_t)env_or("COVT_LANE_MAX_BYTES", kLaneMaxBytes);
-    const int64_t lane_min = env_or("COVT_LANE_MIN_STREAMS", kLaneMinStreams);
+    const int32_t lane_max = o.lane_max_bytes;
+    const int64_t lane_min = o.lane_min_streams;
     if (n_tiles) {
         if (slots) {
             emit_slots<<<n_tiles, 64, 0, s>>>(d_tile_offsets, n_tiles, id_mode, p->d_status, cnt, cb, obb, slots,

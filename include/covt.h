@@ -157,10 +157,37 @@ enum covt_op {
 #define COVT_DESC_SPLIT_RLE 0x10u /* with SPLIT / SPLIT_PAD: an ORC RLE stream's chunk (whole groups, located by the
                                    * plan; pads [1] bytes [s, e), [2] values (first, count), [3] consumed) */
 #define COVT_SPLIT_SLOTS 8
-#define COVT_SPLIT_CHUNK 2048 /* default varint chunk bytes (env COVT_SPLIT_CHUNK at plan creation) */
-#define COVT_SPLIT_VALUES 2048 /* default FastPFOR chunk values, whole blocks (env COVT_SPLIT_VALUES) */
-#define COVT_SPLIT_MIN 8192   /* default: streams longer than this are split (env COVT_SPLIT_MIN; -1: never) */
-#define COVT_SPLIT_RATIO 3000 /* ... and longer than the plan's stream bytes / this (env COVT_SPLIT_RATIO; 0: off) */
+#define COVT_SPLIT_CHUNK 2048 /* default varint / RLE chunk bytes (covt_plan_options.split_chunk) */
+#define COVT_SPLIT_VALUES 2048 /* default FastPFOR chunk values, whole blocks (covt_plan_options.split_values) */
+#define COVT_SPLIT_MIN 8192   /* default: streams costlier than this are split (covt_plan_options.split_min) */
+#define COVT_SPLIT_RATIO 3000 /* ... and than the plan's total cost / this (covt_plan_options.split_ratio) */
+#define COVT_LANE_MAX_BYTES 64      /* default covt_plan_options.lane_max_bytes */
+#define COVT_LANE_MIN_STREAMS 16384 /* default covt_plan_options.lane_min_streams */
+
+/* Plan-layout options.  Every plan property that used to be steered by the environment is a field
+ * here: a library inside a JVM or tile server plans the same way whatever its process inherited.
+ * Initialise with covt_plan_options_init (the defaults below), change fields, pass to
+ * covt_plan_create_opts / covt_device_plan_create_opts.  Plans made with equal options from equal
+ * tiles are byte-identical, host or device. */
+typedef struct covt_plan_options {
+    uint32_t size;             /* sizeof(covt_plan_options), set by covt_plan_options_init */
+    uint32_t flags;            /* COVT_PLAN_PROPERTIES (host plans only) */
+    int64_t split_min;         /* split streams whose cost (bytes + output bytes / 4) exceeds this and ... */
+    int64_t split_ratio;       /* ... the plan's total cost / split_ratio (0: no batch-relative bound);
+                                  split_min < 0: never split */
+    int64_t split_chunk;       /* bytes of cost per varint / RLE chunk (>= 64) */
+    int64_t split_values;      /* values per FastPFOR chunk (a multiple of 256, >= 256) */
+    int32_t fpf_split_weight;  /* a FastPFOR stream's output counted this many times in its split cost (>= 1) */
+    int32_t lane_max_bytes;    /* RLE streams of <= this many bytes and <= 256 values go to the lane family ... */
+    int64_t lane_min_streams;  /* ... when the plan holds at least this many of them (lane_max_bytes < 0: never) */
+    int32_t plan_threads;      /* host threads of covt_plan_create (0: min(hardware threads, 16)) */
+    int32_t host_prefault;     /* decode_host into pageable memory: fault the output pages in on host threads
+                                  while the device works (1, default) or not (0) */
+    int32_t prefault_threads;  /* those threads (default 8) */
+    int32_t device_walk;       /* covt_device_plan: 0 = a wave per tile with per-tile slots (default),
+                                  1 = the same walk twice (no slots), k >= 2: k tiles per workgroup, a lane each */
+} covt_plan_options;
+void covt_plan_options_init(covt_plan_options* opts);
 
 /* One device-resident plan entry (32 bytes). */
 typedef struct covt_stream_desc {
@@ -391,9 +418,14 @@ typedef struct covt_prop_info {
     int64_t out_off[4];
 } covt_prop_info;
 
-/* covt_plan_create plus flags (COVT_PLAN_PROPERTIES). */
+/* covt_plan_create plus flags (COVT_PLAN_PROPERTIES), default options otherwise. */
 int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
                         int32_t n_tiles, int32_t format, int32_t id_mode, uint32_t flags, covt_plan** out);
+/* covt_plan_create with explicit options (NULL: the defaults).  COVT_ERR_INVALID_ARG for an
+ * options struct of the wrong size or out-of-range fields. */
+int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
+                          int32_t n_tiles, int32_t format, int32_t id_mode, const covt_plan_options* opts,
+                          covt_plan** out);
 int64_t covt_plan_num_property_columns(const covt_plan* plan);
 int64_t covt_plan_property_bytes(const covt_plan* plan); /* size of the property output buffer */
 int covt_plan_property_columns(const covt_plan* plan, covt_prop_info* out); /* tile order */
@@ -421,11 +453,19 @@ int covt_plan_properties_host(const covt_plan* plan, const uint8_t* bytes, uint6
  * covt_stream_info fields and 16-byte aligned output slices, descriptors in the same launch order
  * and families.  Long streams are not split into chunks (covt_plan_create splits only the long poles
  * of small batches).  Property columns, geometry assembly and multi-GPU shards stay with the host
- * plan.  Runs on `hip_stream` and synchronises it twice (the stream count sizes the arrays). */
+ * plan.  Runs on `hip_stream` and synchronises it twice (the stream count sizes the arrays).
+ * Limits and memory: a tile of 0x7ff00000 bytes or more gets COVT_ERR_INVALID_ARG as its status
+ * (32-bit cursors; the host plan walks such tiles); besides the stream arrays the plan holds ~5 KiB
+ * of per-tile walk slots on the device (128 stream records of 40 bytes per tile: ~0.5 GB at 100k
+ * tiles) unless opts->device_walk != 0. */
 typedef struct covt_device_plan covt_device_plan;
 int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_tile_offsets,
                             const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                             void* hip_stream, covt_device_plan** out);
+/* the same with explicit options (NULL: the defaults; flags must be 0) */
+int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_tile_offsets,
+                                 const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
+                                 const covt_plan_options* opts, void* hip_stream, covt_device_plan** out);
 void covt_device_plan_destroy(covt_device_plan* plan);
 int64_t covt_device_plan_num_streams(const covt_device_plan* plan); /* = its descriptors */
 int64_t covt_device_plan_output_bytes(const covt_device_plan* plan);

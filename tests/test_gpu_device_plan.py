@@ -4,9 +4,8 @@ test_gpu_parity.py): the GPU's walk of the container metadata (CovtParser.decode
 CovtParser.java:53-133; decodeLayerMetadata :574-652) must give the host plan's stream records,
 tile statuses, output layout, launch order and family counts byte for byte, on Gen C fixtures, Gen D
 conversions, malformed tiles and the full BASELINE config-5 batch -- and decoding through it must give
-the host plan's outputs.  The host plan here is built with splitting off (COVT_SPLIT_MIN=-1): the device
-plan never splits."""
-import os
+the host plan's outputs.  Both plans are made with the same covt_plan_options; splitting is off
+(split_min = -1) where the device plan does not split."""
 
 import numpy as np
 import pytest
@@ -17,24 +16,17 @@ from conftest import tile_paths
 pytestmark = pytest.mark.gpu
 
 
-def _host_plan(covt, tiles, fmt, id_mode, split=False):
-    old = os.environ.get("COVT_SPLIT_MIN")
-    if not split:
-        os.environ["COVT_SPLIT_MIN"] = "-1"
-    try:
-        return covt.Plan.from_tiles(tiles, fmt, id_mode)
-    finally:
-        if old is None:
-            os.environ.pop("COVT_SPLIT_MIN", None)
-        else:
-            os.environ["COVT_SPLIT_MIN"] = old
+def _host_plan(covt, tiles, fmt, id_mode, split=False, **kw):
+    opts = covt.PlanOptions(**kw) if split else covt.PlanOptions(split_min=-1, **kw)
+    return covt.Plan.from_tiles(tiles, fmt, id_mode, options=opts)
 
 
 def _device_plan(covt, hp, fmt, id_mode):
     import torch
 
     d_blob = torch.from_numpy(hp.blob).cuda()
-    return covt.DevicePlan(d_blob, hp.offsets.astype(np.int64), hp.sizes.astype(np.int64), fmt, id_mode)
+    return covt.DevicePlan(d_blob, hp.offsets.astype(np.int64), hp.sizes.astype(np.int64), fmt, id_mode,
+                           options=hp.options)
 
 
 def _assert_same_plan(hp, dp):

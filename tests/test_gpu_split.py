@@ -25,17 +25,14 @@ DESC = np.dtype([("in_off", np.uint64), ("out_off", np.uint64), ("avail", np.int
 
 @pytest.mark.parametrize("chunk,values", [(100, 256), (1024, 2048)])
 @pytest.mark.parametrize("id_mode", [0, 1], ids=["id_format", "id_java"])
-def test_fixtures_forced_split(covt, gpu_available, golden_streams, monkeypatch, chunk, values, id_mode):
+def test_fixtures_forced_split(covt, gpu_available, golden_streams, chunk, values, id_mode):
     import torch
 
-    monkeypatch.setenv("COVT_SPLIT_MIN", "200")
-    monkeypatch.setenv("COVT_SPLIT_RATIO", "0")
-    monkeypatch.setenv("COVT_SPLIT_CHUNK", str(chunk))
-    monkeypatch.setenv("COVT_SPLIT_VALUES", str(values))
     paths = tile_paths()
     keys = [tile_key(p) for p in paths]
     tiles = [open(p, "rb").read() for p in paths]
-    plan = covt.Plan.from_tiles(tiles, covt.FORMAT_GENC, id_mode)
+    opts = covt.PlanOptions(split_min=200, split_ratio=0, split_chunk=chunk, split_values=values)
+    plan = covt.Plan.from_tiles(tiles, covt.FORMAT_GENC, id_mode, options=opts)
     assert plan.family_counts[covt.FAMILY_SPLIT] > 1000 and plan.family_counts[covt.FAMILY_SPLIT_FPF] > 100
     assert plan.family_counts[covt.FAMILY_SPLIT_RLE] > 100
     db = covt.DeviceBatch(plan, "cuda")

@@ -1,7 +1,7 @@
 """Split-stream plan layout (CPU): long Java-capped varint streams become chunks of COVT_SPLIT_SLOTS
 descriptors (include/covt.h), contiguous byte ranges covering the stream, family counts and the
-descriptor -> stream map consistent; the env knobs COVT_SPLIT_MIN / COVT_SPLIT_CHUNK are read at plan
-creation."""
+descriptor -> stream map consistent; the split rule follows the plan's covt_plan_options, and the
+library ignores the environment (no COVT_* variable changes a plan)."""
 import os
 
 import numpy as np
@@ -18,12 +18,9 @@ def _tile(name="5_16_20"):
 
 
 @pytest.mark.parametrize("chunk", [64, 1000, 4096])
-def test_split_layout(covt, monkeypatch, chunk):
-    monkeypatch.setenv("COVT_SPLIT_MIN", "256")
-    monkeypatch.setenv("COVT_SPLIT_RATIO", "0")
-    monkeypatch.setenv("COVT_SPLIT_CHUNK", str(chunk))
-    monkeypatch.setenv("COVT_SPLIT_VALUES", "512")
-    plan = covt.Plan.from_tiles([_tile(), _tile("14_8298_10748")])
+def test_split_layout(covt, chunk):
+    opts = covt.PlanOptions(split_min=256, split_ratio=0, split_chunk=chunk, split_values=512)
+    plan = covt.Plan.from_tiles([_tile(), _tile("14_8298_10748")], options=opts)
     d = plan.descs.view(DESC)
     assert d.size == plan.num_descs == plan.family_counts.sum()
     fam0 = int(plan.family_counts[:covt.FAMILY_SPLIT].sum())
@@ -79,14 +76,10 @@ def test_split_layout(covt, monkeypatch, chunk):
     assert np.array_equal(plan.desc_streams[st["desc_index"]], np.arange(plan.num_streams))
 
 
-def test_split_disabled_and_subset(covt, monkeypatch):
-    monkeypatch.setenv("COVT_SPLIT_MIN", "-1")
-    plan = covt.Plan.from_tiles([_tile()])
+def test_split_disabled_and_subset(covt):
+    plan = covt.Plan.from_tiles([_tile()], options=covt.PlanOptions(split_min=-1))
     assert plan.family_counts[covt.FAMILY_SPLIT] == 0 and plan.num_descs == plan.num_streams
-    monkeypatch.setenv("COVT_SPLIT_MIN", "256")
-    monkeypatch.setenv("COVT_SPLIT_RATIO", "0")
-    monkeypatch.setenv("COVT_SPLIT_CHUNK", "512")
-    plan = covt.Plan.from_tiles([_tile()])
+    plan = covt.Plan.from_tiles([_tile()], options=covt.PlanOptions(split_min=256, split_ratio=0, split_chunk=512))
     assert plan.family_counts[covt.FAMILY_SPLIT] > 0
     mask = plan.streams["stream_type"] == covt.VERTEX_BUFFER
     descs, counts, prim = plan.subset_descs(mask)
@@ -95,11 +88,9 @@ def test_split_disabled_and_subset(covt, monkeypatch):
     assert counts[covt.FAMILY_SPLIT] % covt.SPLIT_SLOTS == 0
 
 
-def test_split_threshold_relative_to_batch(covt, monkeypatch):
+def test_split_threshold_relative_to_batch(covt):
     """Default policy: a stream is split only above COVT_SPLIT_MIN and above the batch's stream bytes /
     COVT_SPLIT_RATIO -- one tile splits its long streams, a big batch of the same tiles splits none."""
-    monkeypatch.delenv("COVT_SPLIT_MIN", raising=False)
-    monkeypatch.delenv("COVT_SPLIT_RATIO", raising=False)
     one = covt.Plan.from_tiles([_tile()])
     assert one.family_counts[covt.FAMILY_SPLIT] > 0
     many = covt.Plan.from_tiles([_tile()] * 1000)
@@ -107,20 +98,18 @@ def test_split_threshold_relative_to_batch(covt, monkeypatch):
 
 
 @pytest.mark.parametrize("props", [False, True])
-def test_plan_independent_of_host_threads(covt, monkeypatch, props):
+def test_plan_independent_of_host_threads(covt, props):
     """The plan's host phases (walk, records, launch keys, descriptors, geometry columns) run on ranges
     of tiles / streams per thread with local offsets rebased afterwards: the plan must be byte-identical
-    for any thread count (COVT_PLAN_THREADS), splits and properties included."""
+    for any thread count (covt_plan_options.plan_threads), splits and properties included."""
     import glob
 
     names = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "tiles", "omt", "*.covt")))[:40]
     tiles = [open(n, "rb").read() for n in names] * 25  # 1000 tiles: up to 16 walk ranges (>= 64 tiles each)
     flags = covt.PLAN_PROPERTIES if props else 0
-    monkeypatch.setenv("COVT_SPLIT_MIN", "4096")
     plans = []
-    for thr in ("1", "3", "16"):
-        monkeypatch.setenv("COVT_PLAN_THREADS", thr)
-        p = covt.Plan.from_tiles(tiles, flags=flags)
+    for thr in (1, 3, 16):
+        p = covt.Plan.from_tiles(tiles, flags=flags, options=covt.PlanOptions(split_min=4096, plan_threads=thr))
         plans.append(p)
     a = plans[0]
     assert a.family_counts[covt.FAMILY_SPLIT:].sum() > 0  # split descriptors exercised
@@ -178,13 +167,11 @@ def _fpf_states_py(b, n, unit, nch):
     return out
 
 
-def test_fastpfor_chunk_states(covt, monkeypatch):
+def test_fastpfor_chunk_states(covt):
     """The plan's host walk of the FastPFOR block headers before each split chunk (pads [2..7] of the
     chunk, int32 slots in every field but op / num_bits / flags) equals an independent Python walk."""
-    monkeypatch.setenv("COVT_SPLIT_MIN", "256")
-    monkeypatch.setenv("COVT_SPLIT_RATIO", "0")
-    monkeypatch.setenv("COVT_SPLIT_VALUES", "512")
-    plan = covt.Plan.from_tiles([_tile("14_8298_10748"), _tile()])
+    plan = covt.Plan.from_tiles([_tile("14_8298_10748"), _tile()],
+                                options=covt.PlanOptions(split_min=256, split_ratio=0, split_values=512))
     raw = plan.descs.reshape(-1, 32)
     d = plan.descs.view(DESC)
     f0 = int(plan.family_counts[:covt.FAMILY_SPLIT_FPF].sum())
@@ -260,3 +247,29 @@ def test_fastpfor_chunk_states_synthetic(covt, oracle):
             e[int(rng.integers(0, len(e)))] ^= 1 << int(rng.integers(0, 8))
         got = _states_hook(covt, bytes(e), 70000, 512)
         assert set(np.unique(got[:, 0]).tolist()) <= {0, 1}
+
+
+def test_environment_ignored(covt, monkeypatch):
+    """The library reads no COVT_* environment variable: a process that inherits the round-1/2 A/B knobs
+    plans exactly as one that does not (covt_plan_options replaced them)."""
+    base = covt.Plan.from_tiles([_tile()])
+    for k, v in (("COVT_SPLIT_MIN", "-1"), ("COVT_SPLIT_RATIO", "1"), ("COVT_SPLIT_CHUNK", "64"),
+                 ("COVT_SPLIT_VALUES", "256"), ("COVT_LANE_MAX_BYTES", "1000"), ("COVT_LANE_MIN_STREAMS", "0"),
+                 ("COVT_PLAN_THREADS", "3"), ("COVT_FPF_SPLIT_WEIGHT", "8"), ("COVT_QUEUE_ORDER", "3012"),
+                 ("COVT_SPLIT_QUEUES", "1"), ("COVT_HOST_PREFAULT", "0")):
+        monkeypatch.setenv(k, v)
+    p = covt.Plan.from_tiles([_tile()])
+    for f in ("descs", "desc_streams", "family_counts", "streams"):
+        assert np.array_equal(getattr(base, f), getattr(p, f)), f
+
+
+def test_options_validated(covt):
+    """Out-of-range options are COVT_ERR_INVALID_ARG (IllegalArgumentException), not silently clamped."""
+    for kw in ({"split_chunk": 63}, {"split_values": 300}, {"split_values": 0}, {"fpf_split_weight": 0},
+               {"split_ratio": -1}, {"plan_threads": -2}, {"prefault_threads": 0}, {"host_prefault": 2},
+               {"device_walk": 257}, {"flags": 0x80}):
+        with pytest.raises(covt.IllegalArgumentException):
+            covt.Plan.from_tiles([_tile()], options=covt.PlanOptions(**kw))
+    o = covt.PlanOptions()
+    assert (o.split_min, o.split_ratio, o.split_chunk, o.split_values, o.lane_max_bytes, o.lane_min_streams) == \
+        (8192, 3000, 2048, 2048, 64, 16384)

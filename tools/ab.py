@@ -3,7 +3,7 @@
 twice to average out drift): config-5 grouped launch, each family alone, BASELINE configs 2-4.
 
   python tools/ab.py libcovt_base.so libcovt.so [...]      (files in cov-tiles_amd/)
-  python tools/ab.py libcovt.so libcovt.so:COVT_SPLIT_MIN=0 (same build, env knobs per variant)
+  python tools/ab.py libcovt.so libcovt.so:split_min=0       (same build, plan options per variant)
   python tools/ab.py --one libcovt.so                        (one measurement, internal)
 """
 import json
@@ -27,7 +27,8 @@ def measure():
     covt = bench.load_covt()
     lib = bench.tile_library()
     picks = bench.sample_batch(lib, 10000, bench.SEED)
-    plan = covt.Plan.from_tiles([t for _, t in picks])
+    opts = covt.PlanOptions(**json.loads(os.environ.get("AB_PLAN_OPTIONS", "{}")))
+    plan = covt.Plan.from_tiles([t for _, t in picks], options=opts)
     batch = covt.DeviceBatch(plan, "cuda")
     s = torch.cuda.current_stream()
     L = covt.lib()
@@ -54,7 +55,7 @@ def measure():
         del sub
     for name in bench.CONFIG_LEGS:
         cp = bench.config_tiles(lib, name)
-        cplan = covt.Plan.from_tiles([t for _, t in cp])
+        cplan = covt.Plan.from_tiles([t for _, t in cp], options=opts)
         cb = covt.DeviceBatch(cplan, "cuda")
         sub = cb.subset(bench.config_mask(cplan, name))
         out[name] = timed(lambda: sub.decode(s), reps=50)
@@ -72,8 +73,9 @@ def main():
     res = {v: [] for v in variants}
     for _ in range(2):
         for v in variants:
-            lib, *kv = v.split(":")  # "libcovt.so:KNOB=1:KNOB2=0" -> env knobs for that variant
-            env = dict(os.environ, COVT_LIB_VARIANT=lib, **dict(x.split("=", 1) for x in kv))
+            lib, *kv = v.split(":")  # "libcovt.so:split_min=0:split_chunk=1024" -> plan options of that variant
+            env = dict(os.environ, COVT_LIB_VARIANT=lib,
+                       AB_PLAN_OPTIONS=json.dumps({k: int(x) for k, x in (y.split("=", 1) for y in kv)}))
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", lib], capture_output=True,
                                text=True, timeout=600, env=env)
             if p.returncode != 0:

@@ -1,7 +1,8 @@
 """Device-side plan timing on the bench batch (BASELINE config 5), in one process: wall-clock of
-covt_device_plan_create per setting of the lanes-per-workgroup knob (COVT_DPLAN_LANES), interleaved
-rounds so box drift hits every setting alike, plus the host plan for comparison.  Each setting's plan
-is checked equal to the host plan's descriptors.  Usage: python tools/device_plan_ab.py [lanes ...]"""
+covt_device_plan_create per walk layout (covt_plan_options.device_walk: 0 = wave per tile with slots,
+1 = walk twice, k >= 2 = k lanes per workgroup), interleaved rounds so box drift hits every setting
+alike, plus the host plan for comparison.  Each setting's plan is checked equal to the host plan's
+descriptors.  Usage: python tools/device_plan_ab.py [device_walk ...]"""
 import os
 import sys
 import time
@@ -15,7 +16,7 @@ import bench  # noqa: E402
 def main():
     import torch
 
-    lanes = [int(x) for x in sys.argv[1:]] or [1, 4, 16, 64]
+    lanes = [int(x) for x in sys.argv[1:]] or [0, 1]
     covt = bench.load_covt()
     picks = bench.sample_batch(bench.tile_library(), 10000, bench.SEED)
     blob, offs, sizes = covt.pack_tiles([t for _, t in picks])
@@ -28,10 +29,9 @@ def main():
     times = {k: [] for k in lanes}
     for rnd in range(6):
         for k in lanes:
-            os.environ["COVT_DPLAN_LANES"] = str(k)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            dp = covt.DevicePlan(d_blob, d_off, d_size)
+            dp = covt.DevicePlan(d_blob, d_off, d_size, options=covt.PlanOptions(device_walk=k))
             dt = time.perf_counter() - t0
             if rnd == 0:
                 _, descs, _ = dp.host_copy()
@@ -41,7 +41,7 @@ def main():
             dp.close()
     print("host plan (covt_plan_create): %.1f ms" % (t_host * 1e3))
     for k in lanes:
-        print("COVT_DPLAN_LANES=%-3d device plan median %.3f ms  min %.3f ms" %
+        print("device_walk=%-3d device plan median %.3f ms  min %.3f ms" %
               (k, np.median(times[k]) * 1e3, min(times[k]) * 1e3))
 
 
