@@ -111,6 +111,14 @@ __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {  // any alignmen
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 __device__ __forceinline__ uint32_t ld_be32(const uint8_t* p) { return __builtin_bswap32(ld_le32(p)); }
+// v_perm_b32 selector of "bytes [sh, sh + 4) of {hi:lo}, byte-swapped": the big-endian word that starts
+// sh bytes into lo, in one instruction (alignbyte + bswap would be two)
+__host__ __device__ constexpr uint32_t be_sel(uint32_t sh) {
+    return (sh + 3u) | ((sh + 2u) << 8) | ((sh + 1u) << 16) | (sh << 24);
+}
+__device__ __forceinline__ uint32_t be_word(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
 // loads from a wave-uniform address through the scalar data cache (constant address space)
 typedef __attribute__((address_space(4))) const uint32_t c_u32;
 typedef __attribute__((address_space(4))) const u32x4 c_v4;
@@ -404,17 +412,22 @@ __device__ void win_load(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t p, int
     const int l = lane_id();
     uint4 d;
     int32_t woff;
+    // lanes whose 16 bytes start at or past `end` load nothing: a short stream's window would otherwise
+    // fetch up to 1 KiB of its neighbours (bytes past `end` are never used)
     if (MODE == MODE_RAW) {
         const uintptr_t a = ((uintptr_t)(sb + p)) & ~(uintptr_t)15;
         woff = uni((int32_t)((intptr_t)a - (intptr_t)sb));
-        d = ld128(a + 16 * (uintptr_t)l);
+        d = woff + 16 * l < end ? ld128(a + 16 * (uintptr_t)l) : make_uint4(0, 0, 0, 0);
     } else {
         woff = p & ~15;
         const uint8_t* q = sb + woff + 16 * l;
-        d.x = ld_be32(q);
-        d.y = ld_be32(q + 4);
-        d.z = ld_be32(q + 8);
-        d.w = ld_be32(q + 12);
+        d = make_uint4(0, 0, 0, 0);
+        if (woff + 16 * l < end) {
+            d.x = ld_be32(q);
+            d.y = ld_be32(q + 4);
+            d.z = ld_be32(q + 8);
+            d.w = ld_be32(q + 12);
+        }
     }
     ((uint4*)sm.u.v.win)[l] = d;
     if (VAL == VAL_NONE) {  // byte-oriented readers: no terminator index
@@ -692,7 +705,7 @@ __device__ __forceinline__ void sink_u64(const uint32_t (&lo)[4], const uint32_t
 }
 
 template <int OP>
-__device__ void run_varint_stream(Ctx& c) {
+__device__ __forceinline__ void run_varint_stream(Ctx& c) {
     int32_t pos = 0;
     Carry cr{0, 0};
     Win w;
@@ -759,7 +772,7 @@ __device__ __forceinline__ uint32_t win_vulong_lo32(const WaveSmem& sm, int32_t 
 // groups one per lane, groups of more than 8 values with the whole wave.
 // o0: output index of the first value (a split chunk of a stream: its stream bytes start at c.sb, its
 // values are [o0, c.n) of the stream's output at c.out)
-__device__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
+__device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
     const bool is_signed = c.op == COVT_OP_RLE_S64;
@@ -986,7 +999,7 @@ __device__ __forceinline__ void store_packet_bytes(uint8_t* dst, const uint32_t 
 // Same window structure as run_rle_int; a byte-RLE group's length follows from its header byte.
 // o0 as in run_rle_int; `exact`: bytes outside [o0, c.n) are never written (a split chunk shares its
 // first and last 16-byte packets with its neighbours)
-__device__ void run_rle_byte(Ctx& c, int32_t o0 = 0, bool exact = false) {
+__device__ __forceinline__ void run_rle_byte(Ctx& c, int32_t o0 = 0, bool exact = false) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
     Win w;
@@ -1199,7 +1212,7 @@ struct FpfHdr {
     int32_t b, ce, idx;  // bit width, exception count, maxbits - b
     uint32_t xcur;       // cursor into dataTobePacked[idx] for this block
     int32_t bcoff;       // container offset of the exception positions
-    int32_t next;        // container offset of the next block header
+    int32_t pk;          // stream word of the block's first packed word
 };
 // Registers prefetched for one block.
 struct FpfPre {
@@ -1250,13 +1263,14 @@ struct FpfSkip {
     int xs, xz;
 };
 template <int OP>
-__device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Carry cr0 = Carry{0, 0},
+__device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Carry cr0 = Carry{0, 0},
                              bool sum_only = false, Carry* sums = nullptr, FpfSkip* skip = nullptr) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
     const Words W{c.sb, c.byte_length / 4};
     const int64_t nw = W.nw;
     const uint32_t sbmis = (uint32_t)((uintptr_t)c.sb & 15);  // stream base misalignment (uniform)
+    const uint32_t bsel = be_sel(sbmis & 3u);  // a stream word from the 4-byte grid: one v_perm_b32
     Carry cr = cr0;
     uint32_t ax = 0, ay = 0;                  // sum_only: per-lane sums
     const bool has_end = v1 >= c.n;           // this range holds the stream's last value
@@ -1280,10 +1294,11 @@ __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Car
             const uint4 r = ld128(a16 + 16 * (uintptr_t)l);
             const uint32_t nx = lane_next(r.x);
             uint4 wv;
-            wv.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(r.y, r.x, sh));
-            wv.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(r.z, r.y, sh));
-            wv.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(r.w, r.z, sh));
-            wv.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(nx, r.w, sh));
+            const uint32_t sel = be_sel(sh);
+            wv.x = be_word(r.y, r.x, sel);
+            wv.y = be_word(r.z, r.y, sel);
+            wv.z = be_word(r.w, r.z, sel);
+            wv.w = be_word(nx, r.w, sel);
             wave_sync();
             ((uint4*)dst)[l] = wv;
             wave_sync();
@@ -1360,39 +1375,11 @@ __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Car
             const int32_t nblocks = v1 <= done ? 0 : uni(min(nblocks_page, (int32_t)(((int64_t)v1 - done + kFpfBlock - 1) / kFpfBlock)));
             const int32_t nw32 = (int32_t)nw;
             const int32_t bclen = uni((int32_t)(bcw * 4));
-            const uint8_t* cb8 = (const uint8_t*)sm.u.f.cbuf;
+            // byteContainer byte q is stream byte 4 bc + (q ^ 3): the LE bytes of the big-endian words W[bc..]
+            const g_u8* cbyte = (const g_u8*)(c.sb + 4 * bc);
             int32_t cbase = INT32_MIN / 2;
             auto chunk_load = [&](int32_t at) {  // container bytes [cbase, cbase + 1020), cbase in (at - 16, at]
                 cbase = (int32_t)(4 * (load_words(sm.u.f.cbuf, bc + (at >> 2)) - bc));
-            };
-            // One block header (FastPFOR.decodePage loop body): all checks merged into one uniform test.
-            // The chunk is (re)loaded so that the header and up to 255 exception positions are inside.
-            auto walk = [&](int32_t cur, FpfHdr& h) -> int32_t {
-                cur = uni(cur);
-                cbase = uni(cbase);
-                if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 260)) chunk_load(cur);
-                const int32_t j = cur - cbase;
-                const uint32_t hw =
-                    uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(j >> 2) + 1], sm.u.f.cbuf[j >> 2], (uint32_t)j & 3u));
-                const int32_t b = (int32_t)(int8_t)(hw & 0xffu);
-                const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
-                const int32_t idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - b;
-                const bool hasx = ce > 0;
-                const bool arr = hasx && idx >= 2 && idx <= 32;  // exceptions from dataTobePacked[idx]
-                const int32_t k = arr ? idx : 0;
-                const int32_t xsz = __builtin_amdgcn_readlane(xz_v, k);
-                const int32_t xc = __builtin_amdgcn_readlane(xc_v, k);
-                bool bad = (uint32_t)b > 32u || cur + 2 > bclen;
-                bad |= hasx && (cur + 3 + ce > bclen || (idx != 1 && !arr));
-                bad |= arr && (xsz < 0 || xc + ce > xsz);
-                h.b = b;
-                h.ce = ce;
-                h.idx = hasx ? idx : 0;
-                h.xcur = arr ? (uint32_t)xc : 0u;
-                h.bcoff = cur + (hasx ? 3 : 2);
-                h.next = h.bcoff + ce;
-                xc_v += (l == (arr ? idx : 64)) ? ce : 0;
-                return bad ? COVT_ERR_BAD_HEADER : COVT_OK;
             };
             // (32-bit: a stream holds < 2^29 words)
             auto xword = [&](int32_t k, uint32_t xs, uint32_t i, uint32_t& xbit) -> int32_t {
@@ -1401,23 +1388,30 @@ __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Car
                 xbit = bit & 31u;
                 return (int32_t)(xs + __umul24(i >> 5, (uint32_t)k) + (bit >> 5));
             };
-            auto prefetch = [&](const FpfHdr& hv, int32_t pkv, FpfPre& pr, int slot) {
-                FpfHdr h;
-                h.idx = uni(hv.idx);
-                h.ce = uni(hv.ce);
-                h.xcur = uniu(hv.xcur);
-                h.bcoff = uni(hv.bcoff);
-                const int32_t pk = uni(pkv);
-                // loads consumed only in the next iteration (the vmcnt wait lands there).  The packed
-                // words are requested only by the lanes whose 16 bytes the unpack reads (8b words from
-                // word qoff <= 3, plus the next lane's first word): 2b + 2 lanes, not all 64.
-                // Both loads are issued by every lane with no exec mask and from a uniform base plus a
-                // 32-bit lane offset (the `saddr` form, no 64-bit address math per lane): lanes past the
-                // 2b + 2 whose 16 bytes the unpack reads repeat the last one's address, lanes without an
-                // exception read word 0.  A masked load or a select of its address under a branch made
-                // the compiler drain every outstanding load (vmcnt(0)) right after issuing the prefetch.
-                const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pk) & ~(uintptr_t)15;
-                const uint32_t lraw = min((uint32_t)l, 2u * (uint32_t)uni(hv.b) + 1u);
+            // Blocks run in batches of up to 64.  Per batch, (1) one serial walk of the header chain (a
+            // header at container byte q is followed by one at q + 2, or q + 3 + c with c exceptions;
+            // one LDS read per header) leaves block g's header bytes and offset in lane g; (2) lane-
+            // parallel, every block's packed-word offset (prefix sum of 8 b), its cursor into its
+            // exception array (a prefix sum per exception width) and all of FastPFOR.decodePage's
+            // checks, the first failing block's status taken by one ballot; (3) the blocks decode with
+            // each block's state read from those lanes (v_readlane) and the next block's loads in flight.
+            int32_t cur = 0, pk = (int32_t)p0 + 1, jstart = 0;
+            if (jb0 > 0 && jb0 < nblocks && skip && skip->done == done) {  // the chunk's start state
+                cur = skip->cur0;
+                pk = skip->pk;
+                xc_v = skip->xc;
+                jstart = jb0;
+            }
+            auto prefetch = [&](const FpfHdr& h, FpfPre& pr) {
+                // loads consumed only in the next block (the vmcnt wait lands there).  The packed words are
+                // requested only by the lanes whose 16 bytes the unpack reads (8b words from word qoff <= 3,
+                // plus the next lane's first word): 2b + 2 lanes, not all 64.  Every load is issued by every
+                // lane with no exec mask, from a uniform base plus a 32-bit lane offset (the `saddr` form):
+                // lanes past the 2b + 2 repeat the last one's address, lanes without an exception read word
+                // 0 / the block's first position.  A masked load or a select of its address under a branch
+                // made the compiler drain every outstanding load (vmcnt(0)) right after issuing the prefetch.
+                const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)h.pk) & ~(uintptr_t)15;
+                const uint32_t lraw = min((uint32_t)l, 2u * (uint32_t)h.b + 1u);
                 pr.raw = ld128_off((const g_u8*)a16, 16u * lraw);
                 const int32_t k = h.idx;
                 const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
@@ -1429,178 +1423,241 @@ __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Car
                 pr.x0 = xv.x;
                 pr.x1 = xv.y;
                 pr.x2 = xv.z;
-                const int32_t pb = h.bcoff - cbase;  // positions of exception e at cbuf byte pb + e
-                pr.pos = cb8[min(pb + l, 4 * 260 - 1)];
-                if (h.ce > 64) {  // rare: keep positions 64.. in LDS (the chunk may move on)
-#pragma unroll
-                    for (int q = 1; q < 4; ++q)
-                        sm.u.f.posx[slot][64 * (q - 1) + l] = cb8[min(pb + l + 64 * q, 4 * 260 - 1)];
-                }
+                // exception e = lane: its position, container byte bcoff + e, from the LDS window (pos_window
+                // has put the block's positions inside it)
+                const int32_t pb = h.bcoff - cbase;
+                pr.pos = ((const uint8_t*)sm.u.f.cbuf)[min(pb + l, 4 * 260 - 1)];
             };
-            FpfHdr h;
-            FpfPre pre;
-            int32_t pk = (int32_t)p0 + 1;
-            int32_t cur0 = 0;
-            // headers of the page's blocks before the range: only their offsets, packed words and exception
-            // cursors, one LDS read per header (each block is checked by the chunk that decodes it; the
-            // container bound keeps this walk's reads in place), once per chunk
-            if (jb0 > 0 && jb0 < nblocks && !c.err) {
-                if (skip && skip->done == done) {  // (FpfSkip::done: set by the pre-walk below)
-                    cur0 = skip->cur0;
-                    pk = skip->pk;
-                    xc_v = skip->xc;
-                } else {
-                    int32_t cur = 0, pkk = pk;
-                    for (int32_t j = 0; j < jb0; ++j) {
-                        if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 8)) chunk_load(cur);
-                        const int32_t jj = cur - cbase;
-                        const uint32_t hw = uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(jj >> 2) + 1],
-                                                                            sm.u.f.cbuf[jj >> 2], (uint32_t)jj & 3u));
-                        const int32_t b = (int32_t)(int8_t)(hw & 0xffu);
-                        const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
-                        const int32_t idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - b;
-                        pkk += 8 * b;
-                        xc_v += (ce > 0 && idx >= 2 && idx <= 32 && l == idx) ? ce : 0;
-                        cur += ce > 0 ? 3 + ce : 2;
-                        if (cur > bclen) { c.err = COVT_ERR_BAD_HEADER; break; }
-                    }
-                    cur0 = uni(cur);
-                    pk = uni(pkk);
-                    if (skip) {
-                        skip->done = done;
-                        skip->cur0 = cur0;
-                        skip->pk = pk;
-                        skip->xc = xc_v;
-                    }
+            // the container window holding block h's exception positions (up to 64 read here; more from
+            // global memory in the block): reloaded before the block's loads are issued
+            auto pos_window = [&](const FpfHdr& h) {
+                cbase = uni(cbase);
+                if (h.ce > 0 && (uint32_t)(h.bcoff - cbase) > (uint32_t)(1020 - 64)) chunk_load(h.bcoff);
+            };
+            for (int32_t jbat = jb0 < nblocks ? jstart : nblocks; jbat < nblocks && !c.err; jbat += 64) {
+                jbat = uni(jbat);
+                const int32_t nbat = uni(min(64, nblocks - jbat));
+                // block jbat's header sits where the chain starts: its loads go out before the batch's walk
+                // and checks (a block that fails them reports its status before any of its data is used;
+                // its loads stay inside the stream's buffer and padding whatever the header says)
+                FpfHdr h;  // the next block to decode (its loads in flight)
+                FpfPre pre, preB;
+                const bool early = jbat >= jb0;
+                if (early) {
+                    cur = uni(cur);
+                    cbase = uni(cbase);
+                    if ((uint32_t)(cur - cbase) > 953u) chunk_load(cur);  // the header and 64 positions
+                    const int32_t q = cur - cbase;
+                    const uint32_t hw =
+                        uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(q >> 2) + 1], sm.u.f.cbuf[q >> 2], (uint32_t)q & 3u));
+                    h.b = (int32_t)(int8_t)(hw & 0xffu);
+                    h.ce = (int32_t)((hw >> 8) & 0xffu);
+                    const int32_t idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - h.b;
+                    h.idx = h.ce > 0 ? idx : 0;
+                    h.xcur = h.ce > 0 && idx >= 2 && idx <= 32 ? (uint32_t)__builtin_amdgcn_readlane(xc_v, idx) : 0u;
+                    h.bcoff = cur + (h.ce > 0 ? 3 : 2);
+                    h.pk = pk;
+                    prefetch(h, pre);
                 }
-                COVT_PHASE(c, 0);  // (the pre-walk counts with the directory)
-            }
-            if (jb0 < nblocks && !c.err) {
-                c.err = walk(cur0, h);
-                if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
-                if (!c.err) prefetch(h, pk, pre, 0);
-            }
-            // one block; the loop below alternates two register sets so that no in-flight prefetch
-            // register is ever copied (a copy would force the vmcnt wait at the end of the iteration)
-            auto block = [&](int32_t j, const FpfPre& pc, FpfPre& pn, int slot) {
-                FpfHdr hc;
-                hc.b = uni(h.b);
-                hc.ce = uni(h.ce);
-                hc.idx = uni(h.idx);
-                hc.xcur = uniu(h.xcur);
-                hc.bcoff = uni(h.bcoff);
-                hc.next = uni(h.next);
-                const int32_t pkc = uni(pk);
-                const int32_t b = hc.b;
-                // stage block j: LDS dword qoff + i = packed word i (aligned, byte-swapped)
-                const uint32_t o = (sbmis + 4u * (uint32_t)pkc) & 15u;
-                const uint32_t sh = o & 3u;
-                const int32_t qoff = (int32_t)(o >> 2);
-                {
-                    uint4 raw2 = make_uint4(0, 0, 0, 0);
-                    if (b == 32) {  // rare: the 16 bytes past the first KiB (same for every lane; scalar load)
-                        const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pkc) & ~(uintptr_t)15;
-                        raw2 = sld128(a16 + 1024);
-                    }
-                    const uint32_t nxt = lane_next(pc.raw.x, raw2.x);
-                    uint4 wv;
-                    wv.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.y, pc.raw.x, sh));
-                    wv.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.z, pc.raw.y, sh));
-                    wv.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.raw.w, pc.raw.z, sh));
-                    wv.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(nxt, pc.raw.w, sh));
-                    ((uint4*)sm.u.f.stage)[l] = wv;
-                    if (b == 32 && l == 0) {
-                        uint4 w2;
-                        w2.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(raw2.y, raw2.x, sh));
-                        w2.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(raw2.z, raw2.y, sh));
-                        w2.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(raw2.w, raw2.z, sh));
-                        w2.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(0u, raw2.w, sh));
-                        ((uint4*)sm.u.f.stage)[64] = w2;
-                    }
+                uint32_t hw_v = 0;          // lane g: header bytes (b, c, maxbits, ...) of block jbat + g
+                int32_t cur_v = bclen + 1;  // ... and its container offset (past the container: no header)
+                for (int32_t g = 0; g < nbat; ++g) {
+                    cur = uni(cur);
+                    cbase = uni(cbase);
+                    if (cur > bclen) break;  // the chain has left the container: no later block has a header
+                    if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 8)) chunk_load(cur);
+                    const int32_t q = cur - cbase;
+                    const uint32_t hw =
+                        uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(q >> 2) + 1], sm.u.f.cbuf[q >> 2], (uint32_t)q & 3u));
+                    hw_v = l == g ? hw : hw_v;
+                    cur_v = l == g ? cur : cur_v;
+                    const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
+                    cur += ce > 0 ? 3 + ce : 2;
                 }
-                if (hc.ce > 0) ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
-                wave_sync();
                 COVT_PHASE(c, 1);
-                // walk block j+1 and put its loads in flight.  The loads are issued unconditionally (the
-                // last block re-reads its own words) so that every path has the same number of memory
-                // ops in flight and the waits for this block's exception words stay partial.
-                if (j + 1 < nblocks) {
-                    c.err = walk(hc.next, h);
-                    pk = pkc + 8 * b;
-                    if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
-                    if (c.err) return;
+                const bool in = l < nbat;
+                const int32_t b_v = (int32_t)(int8_t)(hw_v & 0xffu);
+                const int32_t ce_v = (int32_t)((hw_v >> 8) & 0xffu);
+                const int32_t idx_v = (int32_t)(int8_t)((hw_v >> 16) & 0xffu) - b_v;
+                const bool hasx = ce_v > 0;
+                const bool arr_k = hasx && idx_v >= 2 && idx_v <= 32;  // exceptions from dataTobePacked[idx]
+                const bool arr = in && arr_k;
+                // exception cursors: the values of dataTobePacked[k] consumed before the batch (lane k of
+                // xc_v) + the exceptions of the batch's earlier blocks of width k
+                const bool cap = skip && jb0 > jbat && jb0 < jbat + nbat && skip->done != done;  // pass one: keep the state at jb0
+                const int32_t gj = jb0 - jbat;
+                int32_t xcur_v = 0, xc_at = xc_v;
+                for (uint64_t todo = __ballot(arr); todo;) {
+                    const int32_t kk = __builtin_amdgcn_readlane(idx_v, (int32_t)__builtin_ctzll(todo));
+                    const bool mine = arr && idx_v == kk;
+                    const uint32_t v = mine ? (uint32_t)ce_v : 0u;
+                    const uint32_t s = incl_scan(v);
+                    const int32_t base = __builtin_amdgcn_readlane(xc_v, kk);
+                    xcur_v = mine ? base + (int32_t)(s - v) : xcur_v;
+                    if (cap) xc_at = l == kk ? base + (int32_t)lane_bcast(s, gj - 1) : xc_at;
+                    xc_v += l == kk ? (int32_t)lane_bcast(s, 63) : 0;
+                    todo &= ~__ballot(mine);
                 }
-                prefetch(h, pk, pn, slot ^ 1);
-                COVT_PHASE(c, 2);
-                // unpack: lane l -> values 4l..4l+3 of miniblock l/8
-                uint32_t v[4];
+                // packed words: block g starts 8 b words after block g - 1
+                const uint32_t w8 = in ? 8u * (uint32_t)b_v : 0u;
+                const uint32_t pinc = incl_scan(w8);
+                const int32_t pk_v = pk + (int32_t)(pinc - w8);
+                pk += (int32_t)lane_bcast(pinc, 63);
+                if (cap) {
+                    skip->done = done;
+                    skip->cur0 = __builtin_amdgcn_readlane(cur_v, gj);
+                    skip->pk = __builtin_amdgcn_readlane(pk_v, gj);
+                    skip->xc = xc_at;
+                }
+                // FastPFOR.decodePage's checks for the blocks this range decodes (the blocks before jb0 are
+                // checked by the range that decodes them; a chain that left the container reaches jb0 too)
                 {
-                    const uint32_t mask = b == 32 ? 0xffffffffu : ((1u << b) - 1u);
-                    uint32_t bit = __umul24((uint32_t)(l & 7) * 4u, (uint32_t)b);
-                    const int32_t wb = (int32_t)__umul24((uint32_t)(l >> 3), (uint32_t)b) + qoff;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int32_t wi = wb + (int32_t)(bit >> 5);
-                        const uint32_t lo = sm.u.f.stage[wi], hi = sm.u.f.stage[wi + 1];
-                        v[k] = __builtin_amdgcn_alignbit(hi, lo, bit & 31u) & mask;
-                        bit += (uint32_t)b;
+                    const int32_t xsz = lane_get(xz_v, arr_k ? idx_v : 0);
+                    bool bad = (uint32_t)b_v > 32u || cur_v + 2 > bclen;
+                    bad |= hasx && (cur_v + 3 + ce_v > bclen || (idx_v != 1 && !arr_k));
+                    bad |= arr_k && (xsz < 0 || xcur_v + ce_v > xsz);
+                    const bool trunc = pk_v + 8 * b_v > nw32;
+                    const uint64_t fail = __ballot(in && jbat + l >= jb0 && (bad || trunc));
+                    if (fail) {
+                        c.err = __builtin_amdgcn_readlane(bad ? COVT_ERR_BAD_HEADER : COVT_ERR_TRUNCATED,
+                                                          (int32_t)__builtin_ctzll(fail));
+                        break;
                     }
                 }
-                COVT_PHASE(c, 3);
-#if defined(COVT_ABL_NOEXC)  // ablation build: exceptions not applied
-                if (false) {
-#else
-                if (hc.ce > 0) {  // out[pos] |= (index == 1 ? 1 : exceptvalue) << b
-#endif
-                    const int32_t k = hc.idx;
-                    const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
-                    const bool el = l < hc.ce;
-                    uint32_t ex = 1u;
-                    if (k != 1) {  // uniform
-                        uint32_t xbit;
-                        const int32_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
-                        const uint32_t ob = sbmis & 3u;
-                        uint64_t lo = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.x1, pc.x0, ob));
-                        uint64_t hi = __builtin_bswap32(__builtin_amdgcn_alignbyte(pc.x2, pc.x1, ob));
-                        lo = wi < nw32 ? lo : 0ull;  // words past the stream read as 0
-                        hi = (wi + 1 < nw32 && xbit + (uint32_t)k > 32u) ? hi : 0ull;
-                        const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
-                        ex = (uint32_t)(((lo | (hi << 32)) >> xbit) & m);
-                    }
-                    // lanes without an exception OR 0 into their own slot: no branch, no conflict
-                    atomicOr(&sm.u.f.patch[el ? pc.pos : (uint32_t)(4 * l)], el ? ex << (b & 31) : 0u);
-                    if (hc.ce > 64) {  // rare: more than 64 exceptions in the block
-                        for (int q = 1; q < 4; ++q) {
-                            const int32_t e = l + 64 * q;
-                            if (e < hc.ce) {
-                                const uint32_t ex = k == 1 ? 1u : xget(W, xs, k, hc.xcur + (uint32_t)e);
-                                atomicOr(&sm.u.f.patch[sm.u.f.posx[slot][64 * (q - 1) + l]], ex << (b & 31));
-                            }
+                COVT_PHASE(c, 2);
+                // block jbat + g's state (uniform) from lane g
+                auto rec = [&](int32_t g, FpfHdr& h) {
+                    const uint32_t hw = (uint32_t)__builtin_amdgcn_readlane((int32_t)hw_v, g);
+                    h.b = (int32_t)(int8_t)(hw & 0xffu);
+                    h.ce = (int32_t)((hw >> 8) & 0xffu);
+                    h.idx = h.ce > 0 ? (int32_t)(int8_t)((hw >> 16) & 0xffu) - h.b : 0;
+                    h.xcur = (uint32_t)__builtin_amdgcn_readlane(xcur_v, g);
+                    h.bcoff = __builtin_amdgcn_readlane(cur_v, g) + (h.ce > 0 ? 3 : 2);
+                    h.pk = __builtin_amdgcn_readlane(pk_v, g);
+                };
+                const int32_t jend = jbat + nbat;
+                int32_t j = uni(max(jbat, jb0));
+                if (!early) {
+                    rec(j - jbat, h);
+                    pos_window(h);
+                    prefetch(h, pre);
+                }
+                // one block; the loop below alternates two register sets so that no in-flight prefetch
+                // register is ever copied (a copy would force the vmcnt wait at the end of the iteration)
+                auto block = [&](int32_t j, const FpfPre& pc, FpfPre& pn) {
+                    FpfHdr hc;
+                    hc.b = uni(h.b);
+                    hc.ce = uni(h.ce);
+                    hc.idx = uni(h.idx);
+                    hc.xcur = uniu(h.xcur);
+                    hc.bcoff = uni(h.bcoff);
+                    hc.pk = uni(h.pk);
+                    const int32_t b = hc.b;
+                    // stage block j: LDS dword qoff + i = packed word i (aligned, byte-swapped)
+                    const uint32_t o = (sbmis + 4u * (uint32_t)hc.pk) & 15u;
+                    const int32_t qoff = (int32_t)(o >> 2);
+                    {
+                        uint4 raw2 = make_uint4(0, 0, 0, 0);
+                        if (b == 32) {  // rare: the 16 bytes past the first KiB (same for every lane; scalar load)
+                            const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)hc.pk) & ~(uintptr_t)15;
+                            raw2 = sld128(a16 + 1024);
+                        }
+                        const uint32_t nxt = lane_next(pc.raw.x, raw2.x);
+                        uint4 wv;
+                        wv.x = be_word(pc.raw.y, pc.raw.x, bsel);
+                        wv.y = be_word(pc.raw.z, pc.raw.y, bsel);
+                        wv.z = be_word(pc.raw.w, pc.raw.z, bsel);
+                        wv.w = be_word(nxt, pc.raw.w, bsel);
+                        ((uint4*)sm.u.f.stage)[l] = wv;
+                        if (b == 32 && l == 0) {
+                            uint4 w2;
+                            w2.x = be_word(raw2.y, raw2.x, bsel);
+                            w2.y = be_word(raw2.z, raw2.y, bsel);
+                            w2.z = be_word(raw2.w, raw2.z, bsel);
+                            w2.w = be_word(0u, raw2.w, bsel);
+                            ((uint4*)sm.u.f.stage)[64] = w2;
                         }
                     }
+                    if (hc.ce > 0) ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
                     wave_sync();
-                    const uint4 pt = ((const uint4*)sm.u.f.patch)[l];
-                    v[0] |= pt.x;
-                    v[1] |= pt.y;
-                    v[2] |= pt.z;
-                    v[3] |= pt.w;
-                }
-                COVT_PHASE(c, 4);
-#if defined(COVT_ABL_NOSTORE)  // ablation build: every block's output to the same 1 KiB (L2-resident)
-                sink_values<OP, 4>(v, 0, 0, kFpfBlock, c.nb, c.out, cr);
+                    COVT_PHASE(c, 3);
+                    // block j + 1's loads in flight.  Issued unconditionally (the batch's last block re-reads
+                    // its own words) so that every path has the same number of memory ops in flight and the
+                    // waits for this block's exception words stay partial.
+                    if (j + 1 < jend) {
+                        rec(j + 1 - jbat, h);
+                        pos_window(h);
+                    }
+                    prefetch(h, pn);
+                    // unpack: lane l -> values 4l..4l+3 of miniblock l/8
+                    uint32_t v[4];
+                    {
+                        const uint32_t mask = b == 32 ? 0xffffffffu : ((1u << b) - 1u);
+                        uint32_t bit = __umul24((uint32_t)(l & 7) * 4u, (uint32_t)b);
+                        const int32_t wb = (int32_t)__umul24((uint32_t)(l >> 3), (uint32_t)b) + qoff;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const int32_t wi = wb + (int32_t)(bit >> 5);
+                            const uint32_t lo = sm.u.f.stage[wi], hi = sm.u.f.stage[wi + 1];
+                            v[k] = __builtin_amdgcn_alignbit(hi, lo, bit & 31u) & mask;
+                            bit += (uint32_t)b;
+                        }
+                    }
+                    COVT_PHASE(c, 4);
+#if defined(COVT_ABL_NOEXC)  // ablation build: exceptions not applied
+                    if (false) {
 #else
-                if (sum_only)
-                    sum_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, ax, ay);
-                else
-                    sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, 0, kFpfBlock, c.nb, c.out, cr);
+                    if (hc.ce > 0) {  // out[pos] |= (index == 1 ? 1 : exceptvalue) << b
 #endif
-                wave_sync();
-                COVT_PHASE(c, 5);
-            };
-            FpfPre preB;
-            for (int32_t j = jb0; j < nblocks && !c.err; j += 2) {
-                block(j, pre, preB, 0);
-                if (j + 1 < nblocks && !c.err) block(j + 1, preB, pre, 1);
+                        const int32_t k = hc.idx;
+                        const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
+                        const bool el = l < hc.ce;
+                        uint32_t ex = 1u;
+                        if (k != 1) {  // uniform
+                            uint32_t xbit;
+                            const int32_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
+                            uint64_t lo = be_word(pc.x1, pc.x0, bsel);
+                            uint64_t hi = be_word(pc.x2, pc.x1, bsel);
+                            lo = wi < nw32 ? lo : 0ull;  // words past the stream read as 0
+                            hi = (wi + 1 < nw32 && xbit + (uint32_t)k > 32u) ? hi : 0ull;
+                            const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
+                            ex = (uint32_t)(((lo | (hi << 32)) >> xbit) & m);
+                        }
+                        // lanes without an exception OR 0 into their own slot: no branch, no conflict
+                        atomicOr(&sm.u.f.patch[el ? pc.pos : (uint32_t)(4 * l)], el ? ex << (b & 31) : 0u);
+                        if (hc.ce > 64) {  // rare: more than 64 exceptions in the block
+                            for (int q = 1; q < 4; ++q) {
+                                const int32_t e = l + 64 * q;
+                                if (e < hc.ce) {
+                                    const uint32_t ex2 = k == 1 ? 1u : xget(W, xs, k, hc.xcur + (uint32_t)e);
+                                    const uint32_t pos2 = cbyte[((uint32_t)(hc.bcoff + e)) ^ 3u];
+                                    atomicOr(&sm.u.f.patch[pos2], ex2 << (b & 31));
+                                }
+                            }
+                        }
+                        wave_sync();
+                        const uint4 pt = ((const uint4*)sm.u.f.patch)[l];
+                        v[0] |= pt.x;
+                        v[1] |= pt.y;
+                        v[2] |= pt.z;
+                        v[3] |= pt.w;
+                    }
+                    COVT_PHASE(c, 5);
+#if defined(COVT_ABL_NOSTORE)  // ablation build: every block's output to the same 1 KiB (L2-resident)
+                    sink_values<OP, 4>(v, 0, 0, kFpfBlock, c.nb, c.out, cr);
+#else
+                    if (sum_only)
+                        sum_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, ax, ay);
+                    else
+                        sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, 0, kFpfBlock, c.nb, c.out, cr);
+#endif
+                    wave_sync();
+                    COVT_PHASE(c, 6);
+                };
+                for (; j < jend; j += 2) {
+                    block(j, pre, preB);
+                    if (j + 1 < jend) block(j + 1, preB, pre);
+                }
             }
             done += thissize;
             p = ie;
@@ -1630,7 +1687,7 @@ __device__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Car
         }
         if (OP == COVT_OP_FPF_ZZ_DELTA_XY && (c.n & 1)) c.err = COVT_ERR_COUNT_MISMATCH;
     }
-    COVT_PHASE(c, 6);
+    COVT_PHASE(c, 7);
     c.consumed = c.byte_length;
     if (sum_only) {
         sums->x = lane_bcast(incl_scan(ax), 63);
@@ -1727,7 +1784,7 @@ __device__ Agg lookback(covt_stream_result* res, int64_t t, int32_t chunk, bool 
 // no further): a chunk that meets one counts the values before it and publishes an error record
 // carrying its index, and whichever chunk finds that index below num_values reports the status.
 template <int OP>
-__device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, covt_stream_result* res, int64_t t) {
+__device__ __forceinline__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, covt_stream_result* res, int64_t t) {
     // (COVT_OP_VARINT_ZZ_DELTA_S64 is not split: its 64-bit running sums took this kernel from 65 to 113
     // VGPRs with a scratch spill)
     constexpr bool kU64 = OP == COVT_OP_VARINT_U64 || OP == COVT_OP_VARINT_ZZ_S64;
@@ -1858,7 +1915,7 @@ __device__ void run_varint_chunk(Ctx& c, int32_t s, int32_t e, int32_t chunk, co
 // sums without storing, pass two stores with the carry).  Each chunk walks the page directories and
 // the block headers before its range itself, so chunks depend on each other only through the sums.
 template <int OP>
-__device__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v1, int32_t chunk, covt_stream_result* res,
+__device__ __forceinline__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v1, int32_t chunk, covt_stream_result* res,
                                    int64_t t, const covt_stream_desc* __restrict__ cd) {
     constexpr bool kXY = OP == COVT_OP_FPF_ZZ_DELTA_XY;
     Carry carry{0u, 0u};
@@ -1915,7 +1972,7 @@ __device__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v1, int32_t chunk
 // of the stream's output.  The stream's result entry (zeroed before the launch) takes the first chunk's
 // consumed count and the lowest failing status (the plan splits only streams whose group structure it
 // walked: what remains is the GeometryType range check, BAD_HEADER from any chunk).
-__device__ void run_rle_chunk(Ctx& c, const covt_stream_desc* __restrict__ cd, int32_t chunk, covt_stream_result* res,
+__device__ __forceinline__ void run_rle_chunk(Ctx& c, const covt_stream_desc* __restrict__ cd, int32_t chunk, covt_stream_result* res,
                               int64_t t) {
     const int32_t s = (int32_t)cd[1].in_off, e = (int32_t)cd[1].out_off;
     const int32_t v0 = (int32_t)cd[2].in_off, nv = (int32_t)cd[2].out_off;
@@ -1935,7 +1992,7 @@ __device__ void run_rle_chunk(Ctx& c, const covt_stream_desc* __restrict__ cd, i
 // result entries).  K: kSplitVarint, kSplitFpf, kSplitRle (COVT_FAMILY_SPLIT, _SPLIT_FPF, _SPLIT_RLE).
 constexpr int kSplitVarint = 0, kSplitFpf = 1, kSplitRle = 2;
 template <int K>
-__device__ int64_t decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in, const covt_stream_desc* __restrict__ descs,
+__device__ __forceinline__ int64_t decode_split_chunk(WaveSmem* sm, const uint8_t* __restrict__ in, const covt_stream_desc* __restrict__ descs,
                                       int64_t n_chunks, uint8_t* __restrict__ out, covt_stream_result* __restrict__ res) {
     constexpr bool FPF = K == kSplitFpf;
     uint32_t* ctr = (uint32_t*)(res + kRecTicket);  // the first chunk's ticket entry
@@ -2029,17 +2086,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const
 #endif
 }
 
+// One stream of family FAM on this wave (descriptor sid; `smem`: the wave's scratch).
 template <int FAM>
-__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(7))) void decode_family_kernel(const uint8_t* __restrict__ in,
-                                                            const covt_stream_desc* __restrict__ descs,
-                                                            int64_t n_streams, uint8_t* __restrict__ out,
-                                                            covt_stream_result* __restrict__ res) {
-    constexpr int kStride = FAM == COVT_FAMILY_RLE ? kFamSmemRle
-                            : FAM == COVT_FAMILY_VARINT ? kFamSmemVarint : kFamSmemFpf;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kStride];
-    const int wv = uni((int)(threadIdx.x >> 6));
-    const int64_t sid = (int64_t)blockIdx.x * kWavesPerBlock + wv;
-    if (sid >= n_streams) return;
+__device__ __forceinline__ void decode_family_wave(uint8_t* smem, const uint8_t* __restrict__ in,
+                                                   const covt_stream_desc* __restrict__ descs, int64_t sid,
+                                                   uint8_t* __restrict__ out, covt_stream_result* __restrict__ res) {
     const covt_stream_desc d = descs[sid];
     if ((d.flags & (COVT_DESC_LANE | COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD)) || op_family(d.op) != FAM) return;
     // long streams are the kernel's critical path: let their waves win instruction arbitration
@@ -2048,7 +2099,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     Ctx c;
-    c.sm = (WaveSmem*)(smem + wv * kStride);
+    c.sm = (WaveSmem*)smem;
     c.sb = in + d.in_off;
     c.out = out + d.out_off;
     c.avail = d.avail;
@@ -2111,6 +2162,23 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
     }
 }
 
+#ifndef COVT_FPF_WAVES
+#define COVT_FPF_WAVES 7  // A/B: waves per SIMD the FastPFOR family kernel is register-budgeted for
+#endif
+template <int FAM>
+__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(FAM == COVT_FAMILY_FASTPFOR ? COVT_FPF_WAVES : 7))) void decode_family_kernel(const uint8_t* __restrict__ in,
+                                                            const covt_stream_desc* __restrict__ descs,
+                                                            int64_t n_streams, uint8_t* __restrict__ out,
+                                                            covt_stream_result* __restrict__ res) {
+    constexpr int kStride = FAM == COVT_FAMILY_RLE ? kFamSmemRle
+                            : FAM == COVT_FAMILY_VARINT ? kFamSmemVarint : kFamSmemFpf;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWavesPerBlock * kStride];
+    const int wv = uni((int)(threadIdx.x >> 6));
+    const int64_t sid = (int64_t)blockIdx.x * kWavesPerBlock + wv;
+    if (sid >= n_streams) return;
+    decode_family_wave<FAM>(smem + wv * kStride, in, descs, sid, out, res);
+}
+
 // --------------------------------------------------------------------------------------------
 // lane-per-stream path: small RLE streams (<= kLaneMaxValues values, flagged by the plan), one
 // stream per lane, decoded serially the way RunLengthIntegerReader / RunLengthByteReader read them.
@@ -2125,20 +2193,23 @@ struct LaneBytes {  // the lane's stream through a window in its LDS slot; one-d
     int32_t w0;  // stream offset of slot byte 0 (4-byte aligned in memory)
     int32_t cq;
     uint32_t cw;
-    // window = stream bytes [w0, w0 + 68) from p's 4-byte aligned address; 4 x 16 B + 4 B loads at once
+    // window = stream bytes [w0, w0 + 68) from p's 4-byte aligned address; up to 4 x 16 B + 4 B loads at
+    // once, only those holding stream bytes (a 10-byte stream loads 16 bytes, not 68)
     __device__ __forceinline__ void load(int32_t p) {
         const uintptr_t a = (uintptr_t)(sb + p), a4 = a & ~(uintptr_t)3;
         w0 = p - (int32_t)(a & 3u);
+        const int32_t need = avail - w0;  // window bytes that are stream bytes
         uint32_t st[kLaneSlot];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(a4 + 16 * k);
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (16 * k < need) v = *(const __attribute__((address_space(1))) u32x4*)(a4 + 16 * k);
             st[4 * k] = v.x;
             st[4 * k + 1] = v.y;
             st[4 * k + 2] = v.z;
             st[4 * k + 3] = v.w;
         }
-        st[16] = *g32(a4 + 64);
+        st[16] = 64 < need ? *g32(a4 + 64) : 0u;
 #pragma unroll
         for (int k = 0; k < kLaneSlot; ++k) slot[k * 256] = st[k];
         cq = -1;
@@ -2324,13 +2395,10 @@ __device__ void lane_rle_byte(LaneBytes& in, int32_t n, uint8_t* out, bool check
     consumed = o;
 }
 
-__global__ __launch_bounds__(256) void decode_lane_kernel(const uint8_t* __restrict__ in,
-                                                          const covt_stream_desc* __restrict__ descs,
-                                                          int64_t n_streams, uint8_t* __restrict__ out,
-                                                          covt_stream_result* __restrict__ res) {
-    __shared__ uint32_t slots[256 * kLaneSlot];
-    const int64_t sid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (sid >= n_streams) return;
+// One lane-family stream on this lane (`slot`: the lane's column of a [kLaneSlot][256] dword array)
+__device__ __forceinline__ void decode_lane_one(uint32_t* slot, const uint8_t* __restrict__ in,
+                                                const covt_stream_desc* __restrict__ descs, int64_t sid,
+                                                uint8_t* __restrict__ out, covt_stream_result* __restrict__ res) {
     const covt_stream_desc d = descs[sid];
     if (!(d.flags & COVT_DESC_LANE)) return;
 #ifdef COVT_TIMING
@@ -2338,7 +2406,7 @@ __global__ __launch_bounds__(256) void decode_lane_kernel(const uint8_t* __restr
 #endif
     int32_t err = 0, consumed = 0;
     // the stream's first 68 bytes into the lane's slot (dword k of lane t at slots[k * 256 + t])
-    LaneBytes lb{in + d.in_off, slots + threadIdx.x, d.avail, 0, -1, 0u};
+    LaneBytes lb{in + d.in_off, slot, d.avail, 0, -1, 0u};
     lb.load(0);
     if (d.num_values < 0 || d.avail < 0) err = COVT_ERR_INVALID_ARG;
     else if (d.op == COVT_OP_BYTE_RLE_U8 || d.op == COVT_OP_BYTE_RLE_RAW)
@@ -2357,7 +2425,120 @@ __global__ __launch_bounds__(256) void decode_lane_kernel(const uint8_t* __restr
     res[sid] = r;
 }
 
+__global__ __launch_bounds__(256) void decode_lane_kernel(const uint8_t* __restrict__ in,
+                                                          const covt_stream_desc* __restrict__ descs,
+                                                          int64_t n_streams, uint8_t* __restrict__ out,
+                                                          covt_stream_result* __restrict__ res) {
+    __shared__ uint32_t slots[256 * kLaneSlot];
+    const int64_t sid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (sid >= n_streams) return;
+    decode_lane_one(slots + threadIdx.x, in, descs, sid, out, res);
+}
+
+// ---- small batches: every family and split region in ONE launch ----------------------------------------
+// The grouped launch forks up to four HIP streams so the families run concurrently; for a batch far
+// smaller than the GPU (BASELINE configs 2-4: one tile to 61 tiles) the fork / event / join overhead and
+// the hardware-queue start-up (a queue's first kernel started up to 26 us late behind another queue's,
+// profiles/r02/config_timeline_fpf_state.txt) exceed the decode itself.  This kernel holds every family
+// as a segment of one grid, longest work first (workgroups dispatch in blockIdx order): FastPFOR chunks,
+// varint chunks, RLE chunks, FastPFOR, RLE, varint streams, then the lane family (128 streams per
+// workgroup).  Each segment runs the same device code as its own kernel.
+struct FusedSegs {
+    const covt_stream_desc* desc[COVT_NUM_FAMILIES];
+    covt_stream_result* res[COVT_NUM_FAMILIES];
+    int64_t n[COVT_NUM_FAMILIES];  // descriptors (split regions: chunks x kSplitSlots)
+    uint32_t wg_end[COVT_NUM_FAMILIES];  // cumulative workgroups, segment order kFusedOrder
+};
+constexpr int kFusedOrder[COVT_NUM_FAMILIES] = {COVT_FAMILY_SPLIT_FPF, COVT_FAMILY_SPLIT, COVT_FAMILY_SPLIT_RLE,
+                                                COVT_FAMILY_FASTPFOR, COVT_FAMILY_RLE, COVT_FAMILY_VARINT,
+                                                COVT_FAMILY_LANE};
+constexpr int kFusedLds = (kWavesPerBlock * kFamSmemRle > 256 * kLaneSlot * 4) ? kWavesPerBlock * kFamSmemRle
+                                                                              : 256 * kLaneSlot * 4;
+static_assert(kFamSmemRle >= kFamSmemFpf && kFamSmemRle >= kFamSmemVarint, "RLE scratch is the largest");
+
+__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(4))) void decode_fused_kernel(const uint8_t* __restrict__ in,
+                                                                           uint8_t* __restrict__ out, FusedSegs sg) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kFusedLds];
+    const uint32_t b = blockIdx.x;
+    // the segment of this workgroup (constant indices only: a dynamically indexed kernel argument would be
+    // copied to scratch)
+    int fam = COVT_FAMILY_LANE;
+    uint32_t local = 0, prev = 0;
+    const covt_stream_desc* d = nullptr;
+    covt_stream_result* r = nullptr;
+    int64_t n = 0;
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < COVT_NUM_FAMILIES; ++k) {
+        const int f = kFusedOrder[k];
+        if (!found && b < sg.wg_end[k]) {
+            found = true;
+            fam = f;
+            local = b - prev;
+            d = sg.desc[f];
+            r = sg.res[f];
+            n = sg.n[f];
+        }
+        prev = sg.wg_end[k];
+    }
+    if (!found) return;
+    const int wv = uni((int)(threadIdx.x >> 6));
+    uint8_t* wsm = smem + wv * kFamSmemRle;
+    switch (fam) {
+    case COVT_FAMILY_SPLIT_FPF:
+        decode_split_chunk<kSplitFpf>((WaveSmem*)wsm, in, d, n / kSplitSlots, out, r);
+        break;
+    case COVT_FAMILY_SPLIT:
+        decode_split_chunk<kSplitVarint>((WaveSmem*)wsm, in, d, n / kSplitSlots, out, r);
+        break;
+    case COVT_FAMILY_SPLIT_RLE:
+        decode_split_chunk<kSplitRle>((WaveSmem*)wsm, in, d, n / kSplitSlots, out, r);
+        break;
+    case COVT_FAMILY_LANE: {
+        const int64_t sid = (int64_t)local * (64 * kWavesPerBlock) + threadIdx.x;
+        if (sid < n) decode_lane_one((uint32_t*)smem + threadIdx.x, in, d, sid, out, r);
+        break;
+    }
+    default: {
+        const int64_t sid = (int64_t)local * kWavesPerBlock + wv;
+        if (sid >= n) break;
+        if (fam == COVT_FAMILY_FASTPFOR) decode_family_wave<COVT_FAMILY_FASTPFOR>(wsm, in, d, sid, out, r);
+        else if (fam == COVT_FAMILY_RLE) decode_family_wave<COVT_FAMILY_RLE>(wsm, in, d, sid, out, r);
+        else decode_family_wave<COVT_FAMILY_VARINT>(wsm, in, d, sid, out, r);
+    }
+    }
+}
+
 }  // namespace covt
+
+// The fused small-batch launch (covt::decode_fused_kernel): family f's descriptors at d_desc + off[f],
+// its results at d_res + off[f].  Split regions' records must be zeroed before (launch_grouped does).
+extern "C" int covt_launch_fused(const uint8_t* d_in, const covt_stream_desc* d_desc, const int64_t counts[COVT_NUM_FAMILIES],
+                                 uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream) {
+    covt::FusedSegs sg{};
+    int64_t off = 0;
+    for (int f = 0; f < COVT_NUM_FAMILIES; ++f) {
+        if (counts[f] < 0) return COVT_ERR_INVALID_ARG;
+        sg.desc[f] = d_desc + off;
+        sg.res[f] = d_res + off;
+        sg.n[f] = counts[f];
+        off += counts[f];
+    }
+    uint64_t wg = 0;
+    for (int k = 0; k < COVT_NUM_FAMILIES; ++k) {
+        const int f = covt::kFusedOrder[k];
+        const int64_t n = f == COVT_FAMILY_SPLIT || f == COVT_FAMILY_SPLIT_FPF || f == COVT_FAMILY_SPLIT_RLE
+                              ? counts[f] / covt::kSplitSlots : counts[f];
+        const int64_t per = f == COVT_FAMILY_LANE ? 64 * covt::kWavesPerBlock : covt::kWavesPerBlock;
+        wg += (uint64_t)((n + per - 1) / per);
+        if (wg > 0x7fffffffull) return COVT_ERR_INVALID_ARG;
+        sg.wg_end[k] = (uint32_t)wg;
+    }
+    if (wg == 0) return COVT_OK;
+    hipLaunchKernelGGL(covt::decode_fused_kernel, dim3((unsigned)wg), dim3(64 * covt::kWavesPerBlock), 0, stream,
+                       d_in, d_out, sg);
+    return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
+}
 
 extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc,
                                         int64_t n_streams, uint8_t* d_out, covt_stream_result* d_res,

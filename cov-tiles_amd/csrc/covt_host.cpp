@@ -613,9 +613,14 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
             if (n_of(f) > 0) q.fam[k++] = f;
         if (k) qs[nq++] = q;
     };
+    if (splits && hipMemsetAsync(d_res + off[kSplitV], 0, (size_t)n_split * sizeof(covt_stream_result), s) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    {  // a small batch: one fused launch on the caller's stream (no fork / join)
+        const int64_t waves = n_split / COVT_SPLIT_SLOTS + counts[COVT_FAMILY_FASTPFOR] + counts[COVT_FAMILY_RLE] +
+                              counts[COVT_FAMILY_VARINT] + (counts[COVT_FAMILY_LANE] + 127) / 128;
+        if (waves <= kFusedMaxWaves) return covt_launch_fused(d_in, d_desc, counts, d_out, d_res, s);
+    }
     if (splits) {
-        if (hipMemsetAsync(d_res + off[kSplitV], 0, (size_t)n_split * sizeof(covt_stream_result), s) != hipSuccess)
-            return COVT_ERR_DEVICE;
         // RLE chunks behind the varint queue (round 2 A/B: with the RLE family, config 3 0.132 -> 0.150 ms)
         add(kSplitV, COVT_FAMILY_VARINT, kSplitR);
         add(COVT_FAMILY_FASTPFOR, -1, -1);

@@ -19,7 +19,14 @@ int covt_launch_family_split(int fam, const uint8_t* d_in, const covt_stream_des
                              uint8_t* d_out, covt_stream_result* d_res, const covt_stream_desc* d_split,
                              int64_t n_split, covt_stream_result* d_split_res, hipStream_t stream);
 int covt_op_family_of(int op);
+// Every family of a grouped descriptor table (family f at offset sum(counts[0..f))) in ONE kernel launch
+// on `stream` (small batches; split regions' records zeroed beforehand).
+int covt_launch_fused(const uint8_t* d_in, const covt_stream_desc* d_desc, const int64_t counts[COVT_NUM_FAMILIES],
+                      uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream);
 }
+// Batches of at most this many waves (split chunks + wave-per-stream descriptors + lane streams / 128)
+// decode in one fused launch instead of the forked per-family launches
+constexpr int64_t kFusedMaxWaves = 4096;
 
 // Plan rule for the lane-per-stream kernel: RLE streams of at most kLaneMaxValues values and
 // kLaneMaxBytes bytes (a lane decodes serially; larger streams amortise a wave's window setup).

@@ -462,6 +462,232 @@ __device__ __forceinline__ int walk_gend_dev(Rd<kWave>& r, E& emit) {
 
 __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
+// ---- speculative Gen C walk (one wave per tile) -------------------------------------------------------
+// The serial walk spends ~90 scalar instructions per metadata varint (~75k per tile: 2.2 ms for the 10k-
+// tile bench batch, profiles/r02).  Most of a Gen C tile's metadata is a chain of records of two shapes:
+// column headers (name, dataType, columnType, numStreams) and stream records (name, numValues, byteLength,
+// encoding).  So the wave stages 1 KiB of metadata (+ 256 bytes of look-ahead) in LDS and every lane
+// parses, at each of its 16 positions, the record that WOULD start there -- a stream record's length and
+// byteLength, a column header's length, stream count, kind (id / geometry / other) and columnType -- into
+// two tables; the walk then follows the chain one LDS read per record and parses fields only for the
+// Id / Geometry streams it emits.  Anything outside the fast grammar (a name or varint longer than the
+// tables hold, a record past the tile, a check the serial walk would fail) makes the tile fall back to the
+// serial walk (walk_genc_dev), which then gives the exact statuses; a successful fast walk emits the same
+// records in the same order.
+constexpr int kFwSpan = 1024;   // table positions per window
+constexpr int kFwBytes = 1280;  // window bytes: the positions + 256 bytes of look-ahead
+constexpr int kFastFallback = 1;
+struct FastSmem {
+    uint32_t win[kFwBytes / 4 + 4];
+    uint32_t stab[kFwSpan];  // stream record at j: length | byteLength << 8 (0: not fast)
+    uint32_t ctab[kFwSpan];  // column header at j: length | numStreams << 8 | kind << 17 | columnType << 19 (0: not fast)
+};
+constexpr size_t kFastSmemOffset = 512 + 256 * 16;  // after Rd<true>'s window and geometry table
+
+struct FastGenc {
+    const uint8_t* t;
+    int32_t len;
+    int32_t wb;  // tile offset of window byte 0 (16-byte aligned address; may be < 0 at the tile start)
+    FastSmem* fs;
+    // bytes [q, q + 8) of the window, q per lane (q <= kFwBytes - 8)
+    __device__ __forceinline__ uint64_t peek8(int32_t q) const {
+        const uint32_t* w = fs->win;
+        const int32_t k = q >> 2;
+        const uint32_t s = (uint32_t)q & 3u;
+        const uint32_t d0 = w[k], d1 = w[k + 1], d2 = w[k + 2];
+        return ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32) | __builtin_amdgcn_alignbyte(d1, d0, s);
+    }
+    __device__ __forceinline__ uint64_t upeek8(int32_t q) const {  // uniform q
+        const uint64_t v = peek8(q);
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+               (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    }
+    // the window holding tile offset `at`, and the record tables of its first kFwSpan positions
+    __device__ void load(int32_t at) {
+        const int l = threadIdx.x;
+        const uintptr_t lo = (uintptr_t)t;
+        const uintptr_t b = (lo + (uintptr_t)(int64_t)at) & ~(uintptr_t)15;
+        wb = (int32_t)(int64_t)(b - lo);
+        wb = __builtin_amdgcn_readfirstlane(wb);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        ((uint4*)fs->win)[l] = window_ld(t, len, b + 16 * (uintptr_t)l);
+        if (l < kFwBytes / 16 - 64) ((uint4*)fs->win)[64 + l] = window_ld(t, len, b + 16 * (uintptr_t)(64 + l));
+        if (l == 0) ((uint4*)fs->win)[kFwBytes / 16] = make_uint4(0, 0, 0, 0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        constexpr uint64_t kId = pk("id", 0, 2), kGeo = pk("geometry", 0, 8);
+#pragma unroll 2
+        for (int i = 0; i < kFwSpan / 64; ++i) {
+            const int32_t q = l + 64 * i, j = wb + q;
+            uint32_t se = 0, ce = 0;
+            const uint64_t nm = peek8(q + 1);              // name bytes (a stream / column name)
+            const uint32_t n = fs->win[q >> 2] >> (8 * (q & 3)) & 0xffu;  // its length (one LEB128 byte)
+            if (j >= 0 && n < 0x80u) {
+                const int32_t p = q + 1 + (int32_t)n;
+                const uint64_t w = peek8(p);
+                // stream record: numValues (<= 4 bytes), byteLength (<= 4 bytes, < 2^24), encoding
+                const uint64_t stop = ~w & 0x8080808080808080ull;
+                const int e1 = stop ? __builtin_ctzll(stop) >> 3 : 8;
+                const uint64_t stop2 = e1 < 7 ? stop & (~0ull << (8 * (e1 + 1))) : 0ull;
+                const int e2 = stop2 ? __builtin_ctzll(stop2) >> 3 : 8;
+                if (e1 <= 3 && e2 - e1 <= 4 && e2 <= 6) {
+                    uint32_t x = (uint32_t)(w >> (8 * (e1 + 1)));
+                    const int nb = e2 - e1;
+                    x = (nb >= 4 ? x : x & ((1u << (8 * nb)) - 1u)) & 0x7f7f7f7fu;
+                    x = (x & 0x007f007fu) | ((x & 0x7f007f00u) >> 1);
+                    const uint32_t bl = (x & 0x3fffu) | ((x & 0x3fff0000u) >> 2);
+                    const int32_t slen = 1 + (int32_t)n + e2 + 2;
+                    if (bl < (1u << 24) && j + slen <= len) se = (uint32_t)slen | (bl << 8);
+                }
+                // column header: dataType, columnType, numStreams (1-2 byte LEB128, <= 256)
+                const uint32_t b2 = (uint32_t)(w >> 16) & 0xffu, b3 = (uint32_t)(w >> 24) & 0xffu;
+                const uint32_t ns = b2 < 0x80u ? b2 : ((b2 & 0x7fu) | (b3 << 7));
+                const int32_t nsb = b2 < 0x80u ? 1 : (b3 < 0x80u ? 2 : 0);
+                const int32_t clen = 1 + (int32_t)n + 2 + nsb;
+                if (nsb && ns <= 256u && j + clen <= len) {
+                    const uint32_t dtype = (uint32_t)w & 0xffu, ctype = (uint32_t)(w >> 8) & 0xffu;
+                    const bool id = n == 2 && (nm & 0xffffull) == kId;
+                    const bool geo = (n == 8 && nm == kGeo) || dtype == 6;
+                    const uint32_t kind = id ? 0u : geo ? 1u : 2u;
+                    ce = (uint32_t)clen | (ns << 8) | (kind << 17) | (ctype << 19);
+                }
+            }
+            fs->stab[q] = se;
+            fs->ctab[q] = ce;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+    __device__ __forceinline__ int32_t at(int32_t o) {  // the window offset of tile offset o (reloads)
+        if ((uint32_t)(o - wb) >= (uint32_t)kFwSpan) load(o);
+        return o - wb;
+    }
+    // a uniform LEB128 value of at most 4 bytes at o (false: longer, or past the tile)
+    __device__ __forceinline__ bool uv4(int32_t& o, uint32_t& v) {
+        if (o >= len) return false;
+        const int32_t q = at(o);
+        const uint32_t w = (uint32_t)upeek8(q);
+        const uint32_t stop = ~w & 0x80808080u;
+        if (!stop) return false;
+        const int nb = (__builtin_ctz(stop) >> 3) + 1;
+        if (o + nb > len) return false;
+        uint32_t x = (nb >= 4 ? w : w & ((1u << (8 * nb)) - 1u)) & 0x7f7f7f7fu;
+        x = (x & 0x007f007fu) | ((x & 0x7f007f00u) >> 1);
+        v = (x & 0x3fffu) | ((x & 0x3fff0000u) >> 2);
+        o += nb;
+        return true;
+    }
+    // a fast stream record at o (its table entry se != 0): StreamType of its name, numValues, encoding
+    __device__ __forceinline__ void rec(int32_t q, uint32_t se, int& type, int32_t& nv, int& enc) {
+        const uint64_t w0 = upeek8(q);
+        const uint32_t n = (uint32_t)w0 & 0xffu;
+        uint64_t lo = upeek8(q + 1), hi = 0;
+        if (n < 8) lo &= (1ull << (8 * n)) - 1;
+        if (n > 8) {
+            hi = upeek8(q + 9);
+            if (n < 16) hi &= (1ull << (8 * (n - 8))) - 1;
+        }
+        type = -1;
+        if (n >= 4 && n <= 16) {
+#define COVT_FNAME(str, v)                                                              \
+    {                                                                                   \
+        constexpr uint64_t n_ = cstrlen(str), l_ = pk(str, 0, n_), h_ = pk(str, 8, n_); \
+        if (n == n_ && lo == l_ && hi == h_) type = v;                                  \
+    }
+            COVT_FNAME("data", ST_DATA)
+            COVT_FNAME("length", ST_LENGTH)
+            COVT_FNAME("present", ST_PRESENT)
+            COVT_FNAME("dictionary", ST_DICTIONARY)
+            COVT_FNAME("geometry_types", ST_GEOMETRY_TYPES)
+            COVT_FNAME("geometry_offsets", ST_GEOMETRY_OFFSETS)
+            COVT_FNAME("part_offsets", ST_PART_OFFSETS)
+            COVT_FNAME("ring_offsets", ST_RING_OFFSETS)
+            COVT_FNAME("vertex_offsets", ST_VERTEX_OFFSETS)
+            COVT_FNAME("vertex_buffer", ST_VERTEX_BUFFER)
+#undef COVT_FNAME
+        }
+        const uint64_t w = upeek8(q + 1 + (int32_t)n);
+        const uint64_t stop = ~w & 0x8080808080808080ull;  // (the table checked: numValues <= 4 bytes)
+        const int e1 = __builtin_ctzll(stop) >> 3;
+        uint32_t x = (uint32_t)w;
+        x = (e1 >= 3 ? x : x & ((1u << (8 * (e1 + 1))) - 1u)) & 0x7f7f7f7fu;
+        x = (x & 0x007f007fu) | ((x & 0x7f007f00u) >> 1);
+        nv = (int32_t)((x & 0x3fffu) | ((x & 0x3fff0000u) >> 2));
+        enc = (int)((w >> (8 * ((se & 0xffu) - 2 - n))) & 0xffu);  // the record's last byte
+    }
+};
+
+// The fast walk of one Gen C tile (walk_genc_dev's grammar and emission order); kFastFallback when the
+// tile leaves the fast grammar (the caller then runs walk_genc_dev from scratch with a fresh emitter).
+template <class E>
+__device__ int walk_genc_fast(FastGenc& f, E& emit) {
+    const int32_t len = f.len;
+    int32_t o = 0;
+    uint32_t version, nlayers;
+    if (!f.uv4(o, version) || !f.uv4(o, nlayers) || version != 1) return kFastFallback;
+    uint4* geo = covt_walk_win + Rd<true>::kWin / 16;  // the geometry column's streams (as walk_genc_dev)
+    for (uint32_t L = 0; L < nlayers; ++L) {
+        uint32_t nlen, extent, nfeat, ncols;
+        if (!f.uv4(o, nlen) || nlen > (uint32_t)(len - o)) return kFastFallback;
+        o += (int32_t)nlen;
+        if (!f.uv4(o, extent) || !f.uv4(o, nfeat) || !f.uv4(o, ncols) || ncols > 4096) return kFastFallback;
+        const int nb = nbits_of_extent(extent);
+        int64_t d = 0;
+        emit.layer_begin();
+        for (uint32_t c = 0; c < ncols; ++c) {
+            const uint32_t ce = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->ctab[f.at(o)]);
+            if (!ce) return kFastFallback;
+            const uint32_t ns = (ce >> 8) & 0x1ffu, kind = (ce >> 17) & 3u;
+            const int ctype = (int)(ce >> 19) & 0xff;
+            o += (int32_t)(ce & 0xffu);
+            uint32_t present = 0;
+            for (uint32_t s = 0; s < ns; ++s) {
+                const int32_t q = f.at(o);
+                const uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[q]);
+                if (!se) return kFastFallback;
+                const int32_t bl = (int32_t)(se >> 8);
+                if (kind != 2) {
+                    int type, enc;
+                    int32_t nv;
+                    f.rec(q, se, type, nv, enc);
+                    if (kind == 0) {
+                        if (type == ST_DATA) emit(RawStream{(int32_t)L, 0, ST_DATA, enc, ctype, nv, bl, nb, d});
+                    } else {
+                        if (threadIdx.x == 0) geo[s] = make_uint4((uint32_t)(type & 0xff) | ((uint32_t)enc << 8), (uint32_t)nv, (uint32_t)bl, 0);
+                        if (type >= ST_GEOMETRY_TYPES && type <= ST_VERTEX_BUFFER) present |= 1u << type;
+                    }
+                }
+                if (kind != 1) d += bl;
+                o += (int32_t)(se & 0xffu);
+            }
+            if (kind == 1) {  // types 4..9 in type order (metadata order within a type), then the rest
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                for (int want = ST_GEOMETRY_TYPES; want <= ST_VERTEX_BUFFER; ++want) {
+                    if (!(present >> want & 1)) continue;
+                    for (uint32_t s = 0; s < ns; ++s) {
+                        const uint4 g = geo[s];
+                        if ((int)(g.x & 0xff) != want) continue;
+                        emit(RawStream{(int32_t)L, 1, want, (int)(g.x >> 8), ctype, (int32_t)g.y, (int32_t)g.z, nb, d});
+                        d += (int64_t)g.z;
+                    }
+                }
+                for (uint32_t s = 0; s < ns; ++s) {
+                    const uint4 g = geo[s];
+                    const int type = (int)(int8_t)(g.x & 0xff);
+                    if (type < ST_GEOMETRY_TYPES || type > ST_VERTEX_BUFFER) d += (int64_t)g.z;
+                }
+            }
+        }
+        if (d > (int64_t)(len - o)) return kFastFallback;
+        emit.layer_end(o);
+        o += (int32_t)d;
+    }
+    return o == len ? COVT_OK : kFastFallback;
+}
+
 template <bool kWave, class E>
 __device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes, uint64_t off, uint64_t size, int32_t format, E& emit) {
     if (off > n_bytes || size > n_bytes - off) return COVT_ERR_INVALID_ARG;
@@ -470,6 +696,17 @@ __device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes,
     r.t = bytes + off;
     r.len = (int64_t)size;
     r.wo = -(int64_t)0x40000000;  // no window yet (every offset misses it)
+    if (kWave && format == COVT_FORMAT_GENC) {  // the speculative walk first; the serial one on a fallback
+        FastGenc f;
+        f.t = r.t;
+        f.len = (int32_t)size;
+        f.wb = -(int32_t)0x40000000;
+        f.fs = (FastSmem*)((uint8_t*)covt_walk_win + kFastSmemOffset);
+        const E fresh = emit;
+        const int st = walk_genc_fast(f, emit);
+        if (st != kFastFallback) return st;
+        emit = fresh;
+    }
     return format == COVT_FORMAT_GENC ? walk_genc_dev(r, emit) : walk_gend_dev(r, emit);
 }
 
@@ -787,7 +1024,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     // 0: a wave per tile, its lanes in lockstep; k > 0: k lanes per workgroup, a lane per tile
     RawStream* slots = use_slots ? (RawStream*)(ta + o_slots) : nullptr;
     if (wl == 0)
-        walk_count<true><<<(int)nt1, 64, 512 + 256 * 16, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
+        walk_count<true><<<(int)nt1, 64, kFastSmemOffset + sizeof(FastSmem), s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
                                                   id_mode, p->d_status, cnt, ob, slots);
     else
         walk_count<false><<<(int)((nt1 + wl - 1) / wl), wl, (size_t)wl * 64, s>>>(
@@ -828,7 +1065,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
             DCHK(hipGetLastError());
         }
         if (wl == 0)  // (with slots: only tiles with more than kSlots streams walk again)
-            walk_emit<true><<<n_tiles, 64, 512 + 256 * 16, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
+            walk_emit<true><<<n_tiles, 64, kFastSmemOffset + sizeof(FastSmem), s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
                                                     id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, totals,
                                                     slots ? cnt : nullptr);
         else

@@ -19,7 +19,8 @@ step() {  # step NAME LIMIT cmd...
 }
 for s in "$@"; do
     case $s in
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    abfpf) step ab_fpf 900 python tools/ab.py ${AB_VARIANTS:-libcovt_base.so libcovt.so} ;;
     tests_asm) step pytest_gpu_asm 600 python -m pytest tests/test_gpu_assembly.py -m gpu -q -p no:cacheprovider --durations=5 ;;
     asm_ab) for v in libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so; do
             COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/asm_run.py 20 2>&1 | grep -v amdgpu.ids || fatal asm_ab $?
