@@ -111,11 +111,14 @@ def host_cpus():
     return n, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota}
 
 
-def cpu_baseline(plan, args):
+def cpu_baseline(plan, args, config1_tile=None):
     """SURVEY §8(d) "CPU timing": the oracle (C restatement of the Java DecodingUtils semantics; the Java
     decoder cannot run, §8(c)) built -O3 -march=native on this host, over the SAME batch as the GPU run
     (every tile walked + every Id/Geometry stream decoded, one tile per task), all usable host cores:
-    median of >= 20 timed iterations after 3 warm-ups; plus a 1-thread figure on the same batch."""
+    median of >= 20 timed iterations after 3 warm-ups; plus a 1-thread figure on the same batch.  At N > 1
+    rank 0 runs it over its own batch (every rank's batch has the same size and zoom mix).
+    `config1_tile`: BASELINE configs[0] -- that one tile decoded whole (CovtParser.decodeCovt: walk, Id /
+    Geometry streams, geometry assembly, property columns) on one thread, and its Id / Geometry part alone."""
     import tempfile
 
     sys.path.insert(0, ROOT)
@@ -151,7 +154,34 @@ def cpu_baseline(plan, args):
     el1, _, _ = run(1)  # 1 thread: one warm-up-free pass is already seconds long; take the median of 3
     times1 = [el1] + [run(1)[0] for _ in range(2 if el1 < 10 else 0)]
     med1 = float(np.median(times1))
-    return {"value": round(ib / med / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+    c1 = None
+    if config1_tile is not None:
+        st, cnt = O.decode_tile_full(config1_tile, O.FMT_GENC, args.id_mode, L)
+        if st != 0:
+            raise RuntimeError("oracle full-tile decode failed: %d" % st)
+        one = np.frombuffer(config1_tile, dtype=np.uint8)
+        o1, s1 = np.zeros(1, dtype=np.uint64), np.array([len(config1_tile)], dtype=np.uint64)
+
+        def idgeom():
+            return O.decode_tiles_mt(one, o1, s1, O.FMT_GENC, args.id_mode, 1, L)
+
+        def med_ms(fn, reps=30):
+            for _ in range(3):
+                fn()
+            ts = []
+            for _ in range(reps):
+                t = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t)
+            return float(np.median(ts)) * 1e3
+
+        c1 = {"cpu_full_ms_1thread": round(med_ms(lambda: O.decode_tile_full(config1_tile, O.FMT_GENC,
+                                                                            args.id_mode, L)), 4),
+              "cpu_id_geometry_ms_1thread": round(med_ms(idgeom), 4), "cpu_counts": cnt,
+              "cpu_note": "oracle/covt_oracle_tile.c (walk + Id/Geometry streams + geometry assembly + property "
+                          "columns, as CovtParser.decodeCovt) and the Id/Geometry part alone, one thread, median "
+                          "of 30 after 3 warm-ups"}
+    return {"value": round(ib / med / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port", "config1": c1,
             "sample": "the full bench batch (%d tiles, %.1f MB stream bytes), median of %d iterations after 3 "
                       "warm-ups (%.1f ms); oracle/covt_oracle.c (C restatement of DecodingUtils + ORC + "
                       "FastPFOR) built -O3 -march=%s here, %d threads, one tile per task" %
@@ -400,17 +430,79 @@ def config_mask(plan, name):
     return (geom & (st["encoding"] == 9) & (st["stream_type"] != 9)) | (st["column_kind"] == 0)
 
 
+CONFIG1_TILE = "omt/5_16_20"  # BASELINE configs[0]: test/fixtures/omt/covt/5_16_20.covt
+
+
+def config1_tile(lib):
+    return dict(lib[5])[CONFIG1_TILE]
+
+
+def config1_leg(lib, args, torch, dev, covt, stream):
+    """BASELINE configs[0] (the reference's single-tile CPU decode, CovtParser.decodeCovt :53-133) on the
+    GPU: the z5 tile 5_16_20 decoded whole -- every Id / Geometry / property stream in one decode launch,
+    then geometry assembly and property materialization, on one stream -- as one tile's latency (HIP events
+    around the three launches, mean of --steps after --warmup), plus the decode launch alone.  The CPU
+    figures for the same tile come from the cpu_baseline leg (merged into this object)."""
+    tile = config1_tile(lib)
+    plan = covt.Plan.from_tiles([tile], covt.FORMAT_GENC, args.id_mode, covt.PLAN_PROPERTIES)
+    batch = covt.DeviceBatch(plan, dev)
+
+    def full():
+        batch.decode(stream)
+        batch.assemble(stream)
+        batch.materialize_properties(stream)
+
+    def timed(fn):
+        with torch.cuda.stream(stream):
+            for _ in range(max(args.warmup, 3)):
+                fn()
+            torch.cuda.synchronize(dev)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(max(args.steps, 20))]
+            for s_, e_ in ev:
+                s_.record(stream)
+                fn()
+                e_.record(stream)
+            torch.cuda.synchronize(dev)
+        return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    ms_full = timed(full)
+    ms_dec = timed(lambda: batch.decode(stream))
+    full()
+    torch.cuda.synchronize(dev)
+    _, res = batch.results()
+    _, gres = batch.assembly_results()
+    _, pres = batch.property_results()
+    idgeom = plan.streams["column_kind"] != 2
+    if (res[idgeom][:, 0] != 0).any() or (gres["status"] != 0).any():
+        raise RuntimeError("config1: Id/Geometry decode or assembly reported errors")
+    return {"workload": "config1: one z5 tile (%s) decoded whole -- Id, Geometry and property streams, "
+                        "geometry assembly, property materialization (CovtParser.decodeCovt)" % CONFIG1_TILE,
+            "tiles": 1, "tile_bytes": len(tile), "streams": plan.num_streams,
+            "id_geometry_stream_bytes": int(plan.streams["byte_length"][idgeom].sum()),
+            "gpu_full_ms": round(ms_full, 5), "gpu_decode_ms": round(ms_dec, 5),
+            "property_columns": plan.num_property_columns,
+            "property_columns_rejected": int((pres["status"] != 0).sum())}
+
+
+def config_launch(lib, name, covt, dev, id_mode=0):
+    """The launch a BASELINE config 2-4 leg times: the config's tiles planned with the default options,
+    uploaded, and a DeviceSubset over exactly the config's streams -> (picks, plan, mask, batch, subset).
+    tests/test_gpu_configs.py checks this very launch against the oracle digests."""
+    picks = config_tiles(lib, name)
+    plan = covt.Plan.from_tiles([t for _, t in picks], covt.FORMAT_GENC, id_mode)
+    mask = config_mask(plan, name)
+    batch = covt.DeviceBatch(plan, dev)
+    return picks, plan, mask, batch, batch.subset(mask)
+
+
 def config_legs(lib, args, torch, dev, covt, stream):
     """BASELINE configs 2-4 on one GPU: kernel-only time of one decode launch over exactly the config's
     streams (inputs + descriptors resident, HIP events on the launch stream, mean of --steps after
     --warmup), bit-exactness of those streams' statuses, and their own roofline.  Not `value`."""
-    out = {}
+    out = {"config1": config1_leg(lib, args, torch, dev, covt, stream)}
     for name, desc in CONFIG_LEGS.items():
-        picks = config_tiles(lib, name)
-        plan = covt.Plan.from_tiles([t for _, t in picks], covt.FORMAT_GENC, args.id_mode)
-        mask = config_mask(plan, name)
-        batch = covt.DeviceBatch(plan, dev)
-        sub = batch.subset(mask)
+        picks, plan, mask, batch, sub = config_launch(lib, name, covt, dev, args.id_mode)
         with torch.cuda.stream(stream):
             for _ in range(max(args.warmup, 1)):
                 sub.decode(stream)
@@ -457,7 +549,7 @@ def launch_ranks(args):
         import torch
 
         have = torch.cuda.device_count()  # does not initialise the GPU on this image
-        if have < n:
+        if have < (1 if args.share_device else n):
             print("bench.py: --gpus %d but only %d GPU(s) visible" % (n, have), file=sys.stderr, flush=True)
             sys.exit(2)
     port = str(free_port())
@@ -500,6 +592,8 @@ def main():
     ap.add_argument("--device-plan-reps", type=int, default=5, help="device-side plan creations timed; 0 skips")
     ap.add_argument("--abi-host-reps", type=int, default=2,
                     help="reps of the C-ABI host entry covt_plan_decode_host (pageable in/out); 0 skips")
+    ap.add_argument("--share-device", action="store_true",
+                    help="every rank on cuda:0 (runs the real N-rank path on a one-GPU box; not a scaling figure)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: sample + plan per rank, time an empty step, print the aggregated line "
                          "(tests the rank launch and aggregation on CPU)")
@@ -524,9 +618,9 @@ def main():
         # gloo carries the timing barriers and the max/sum of per-rank numbers on the host
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
     if not args.dry_run:
-        if torch.cuda.device_count() < world:
+        if torch.cuda.device_count() < (1 if args.share_device else world):
             raise SystemExit("bench.py: %d ranks but only %d GPU(s) visible" % (world, torch.cuda.device_count()))
-        dev = torch.device("cuda", local_rank)
+        dev = torch.device("cuda", 0 if args.share_device else local_rank)
         torch.cuda.set_device(dev)
     covt = load_covt()
 
@@ -664,8 +758,15 @@ def main():
         line.update(legs)
         line["host_plan_ms"] = round(t_plan * 1e3, 1)  # covt_plan_create: metadata walk, descriptors, host
         line["host_pack_ms"] = round(t_pack * 1e3, 1)  # pack_tiles: copying the tiles into one buffer
-        if len(ranks) == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(plan, args)
+        if not args.no_cpu:  # rank 0, over its own batch, at every N
+            cb = cpu_baseline(plan, args, config1_tile(lib))
+            c1 = cb.pop("config1")
+            line["cpu_baseline"] = cb
+            if c1 is not None and "configs" in line:
+                c1["cpu_over_gpu_full"] = round(c1["cpu_full_ms_1thread"] / line["configs"]["config1"]["gpu_full_ms"], 2)
+                line["configs"]["config1"].update(c1)
+        if args.share_device:
+            line["shared_device"] = True  # every rank on cuda:0: the N-rank path exercised, not a scaling figure
         if args.dry_run:
             line["dry_run"] = True
         print(json.dumps(line), flush=True)

@@ -1212,7 +1212,7 @@ struct FpfHdr {
     int32_t b, ce, idx;  // bit width, exception count, maxbits - b
     uint32_t xcur;       // cursor into dataTobePacked[idx] for this block
     int32_t bcoff;       // container offset of the exception positions
-    int32_t pk;          // stream word of the block's first packed word
+    int32_t next;        // container offset of the next block header
 };
 // Registers prefetched for one block.
 struct FpfPre {
@@ -1375,11 +1375,39 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
             const int32_t nblocks = v1 <= done ? 0 : uni(min(nblocks_page, (int32_t)(((int64_t)v1 - done + kFpfBlock - 1) / kFpfBlock)));
             const int32_t nw32 = (int32_t)nw;
             const int32_t bclen = uni((int32_t)(bcw * 4));
-            // byteContainer byte q is stream byte 4 bc + (q ^ 3): the LE bytes of the big-endian words W[bc..]
-            const g_u8* cbyte = (const g_u8*)(c.sb + 4 * bc);
+            const uint8_t* cb8 = (const uint8_t*)sm.u.f.cbuf;
             int32_t cbase = INT32_MIN / 2;
             auto chunk_load = [&](int32_t at) {  // container bytes [cbase, cbase + 1020), cbase in (at - 16, at]
                 cbase = (int32_t)(4 * (load_words(sm.u.f.cbuf, bc + (at >> 2)) - bc));
+            };
+            // One block header (FastPFOR.decodePage loop body): all checks merged into one uniform test.
+            // The chunk is (re)loaded so that the header and up to 255 exception positions are inside.
+            auto walk = [&](int32_t cur, FpfHdr& h) -> int32_t {
+                cur = uni(cur);
+                cbase = uni(cbase);
+                if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 260)) chunk_load(cur);
+                const int32_t j = cur - cbase;
+                const uint32_t hw =
+                    uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(j >> 2) + 1], sm.u.f.cbuf[j >> 2], (uint32_t)j & 3u));
+                const int32_t b = (int32_t)(int8_t)(hw & 0xffu);
+                const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
+                const int32_t idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - b;
+                const bool hasx = ce > 0;
+                const bool arr = hasx && idx >= 2 && idx <= 32;  // exceptions from dataTobePacked[idx]
+                const int32_t k = arr ? idx : 0;
+                const int32_t xsz = __builtin_amdgcn_readlane(xz_v, k);
+                const int32_t xc = __builtin_amdgcn_readlane(xc_v, k);
+                bool bad = (uint32_t)b > 32u || cur + 2 > bclen;
+                bad |= hasx && (cur + 3 + ce > bclen || (idx != 1 && !arr));
+                bad |= arr && (xsz < 0 || xc + ce > xsz);
+                h.b = b;
+                h.ce = ce;
+                h.idx = hasx ? idx : 0;
+                h.xcur = arr ? (uint32_t)xc : 0u;
+                h.bcoff = cur + (hasx ? 3 : 2);
+                h.next = h.bcoff + ce;
+                xc_v += (l == (arr ? idx : 64)) ? ce : 0;
+                return bad ? COVT_ERR_BAD_HEADER : COVT_OK;
             };
             // (32-bit: a stream holds < 2^29 words)
             auto xword = [&](int32_t k, uint32_t xs, uint32_t i, uint32_t& xbit) -> int32_t {
@@ -1388,30 +1416,23 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                 xbit = bit & 31u;
                 return (int32_t)(xs + __umul24(i >> 5, (uint32_t)k) + (bit >> 5));
             };
-            // Blocks run in batches of up to 64.  Per batch, (1) one serial walk of the header chain (a
-            // header at container byte q is followed by one at q + 2, or q + 3 + c with c exceptions;
-            // one LDS read per header) leaves block g's header bytes and offset in lane g; (2) lane-
-            // parallel, every block's packed-word offset (prefix sum of 8 b), its cursor into its
-            // exception array (a prefix sum per exception width) and all of FastPFOR.decodePage's
-            // checks, the first failing block's status taken by one ballot; (3) the blocks decode with
-            // each block's state read from those lanes (v_readlane) and the next block's loads in flight.
-            int32_t cur = 0, pk = (int32_t)p0 + 1, jstart = 0;
-            if (jb0 > 0 && jb0 < nblocks && skip && skip->done == done) {  // the chunk's start state
-                cur = skip->cur0;
-                pk = skip->pk;
-                xc_v = skip->xc;
-                jstart = jb0;
-            }
-            auto prefetch = [&](const FpfHdr& h, FpfPre& pr) {
-                // loads consumed only in the next block (the vmcnt wait lands there).  The packed words are
-                // requested only by the lanes whose 16 bytes the unpack reads (8b words from word qoff <= 3,
-                // plus the next lane's first word): 2b + 2 lanes, not all 64.  Every load is issued by every
-                // lane with no exec mask, from a uniform base plus a 32-bit lane offset (the `saddr` form):
-                // lanes past the 2b + 2 repeat the last one's address, lanes without an exception read word
-                // 0 / the block's first position.  A masked load or a select of its address under a branch
-                // made the compiler drain every outstanding load (vmcnt(0)) right after issuing the prefetch.
-                const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)h.pk) & ~(uintptr_t)15;
-                const uint32_t lraw = min((uint32_t)l, 2u * (uint32_t)h.b + 1u);
+            auto prefetch = [&](const FpfHdr& hv, int32_t pkv, FpfPre& pr, int slot) {
+                FpfHdr h;
+                h.idx = uni(hv.idx);
+                h.ce = uni(hv.ce);
+                h.xcur = uniu(hv.xcur);
+                h.bcoff = uni(hv.bcoff);
+                const int32_t pk = uni(pkv);
+                // loads consumed only in the next iteration (the vmcnt wait lands there).  The packed
+                // words are requested only by the lanes whose 16 bytes the unpack reads (8b words from
+                // word qoff <= 3, plus the next lane's first word): 2b + 2 lanes, not all 64.
+                // Both loads are issued by every lane with no exec mask and from a uniform base plus a
+                // 32-bit lane offset (the `saddr` form, no 64-bit address math per lane): lanes past the
+                // 2b + 2 whose 16 bytes the unpack reads repeat the last one's address, lanes without an
+                // exception read word 0.  A masked load or a select of its address under a branch made
+                // the compiler drain every outstanding load (vmcnt(0)) right after issuing the prefetch.
+                const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pk) & ~(uintptr_t)15;
+                const uint32_t lraw = min((uint32_t)l, 2u * (uint32_t)uni(hv.b) + 1u);
                 pr.raw = ld128_off((const g_u8*)a16, 16u * lraw);
                 const int32_t k = h.idx;
                 const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
@@ -1423,241 +1444,176 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                 pr.x0 = xv.x;
                 pr.x1 = xv.y;
                 pr.x2 = xv.z;
-                // exception e = lane: its position, container byte bcoff + e, from the LDS window (pos_window
-                // has put the block's positions inside it)
-                const int32_t pb = h.bcoff - cbase;
-                pr.pos = ((const uint8_t*)sm.u.f.cbuf)[min(pb + l, 4 * 260 - 1)];
-            };
-            // the container window holding block h's exception positions (up to 64 read here; more from
-            // global memory in the block): reloaded before the block's loads are issued
-            auto pos_window = [&](const FpfHdr& h) {
-                cbase = uni(cbase);
-                if (h.ce > 0 && (uint32_t)(h.bcoff - cbase) > (uint32_t)(1020 - 64)) chunk_load(h.bcoff);
-            };
-            for (int32_t jbat = jb0 < nblocks ? jstart : nblocks; jbat < nblocks && !c.err; jbat += 64) {
-                jbat = uni(jbat);
-                const int32_t nbat = uni(min(64, nblocks - jbat));
-                // block jbat's header sits where the chain starts: its loads go out before the batch's walk
-                // and checks (a block that fails them reports its status before any of its data is used;
-                // its loads stay inside the stream's buffer and padding whatever the header says)
-                FpfHdr h;  // the next block to decode (its loads in flight)
-                FpfPre pre, preB;
-                const bool early = jbat >= jb0;
-                if (early) {
-                    cur = uni(cur);
-                    cbase = uni(cbase);
-                    if ((uint32_t)(cur - cbase) > 953u) chunk_load(cur);  // the header and 64 positions
-                    const int32_t q = cur - cbase;
-                    const uint32_t hw =
-                        uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(q >> 2) + 1], sm.u.f.cbuf[q >> 2], (uint32_t)q & 3u));
-                    h.b = (int32_t)(int8_t)(hw & 0xffu);
-                    h.ce = (int32_t)((hw >> 8) & 0xffu);
-                    const int32_t idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - h.b;
-                    h.idx = h.ce > 0 ? idx : 0;
-                    h.xcur = h.ce > 0 && idx >= 2 && idx <= 32 ? (uint32_t)__builtin_amdgcn_readlane(xc_v, idx) : 0u;
-                    h.bcoff = cur + (h.ce > 0 ? 3 : 2);
-                    h.pk = pk;
-                    prefetch(h, pre);
-                }
-                uint32_t hw_v = 0;          // lane g: header bytes (b, c, maxbits, ...) of block jbat + g
-                int32_t cur_v = bclen + 1;  // ... and its container offset (past the container: no header)
-                for (int32_t g = 0; g < nbat; ++g) {
-                    cur = uni(cur);
-                    cbase = uni(cbase);
-                    if (cur > bclen) break;  // the chain has left the container: no later block has a header
-                    if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 8)) chunk_load(cur);
-                    const int32_t q = cur - cbase;
-                    const uint32_t hw =
-                        uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(q >> 2) + 1], sm.u.f.cbuf[q >> 2], (uint32_t)q & 3u));
-                    hw_v = l == g ? hw : hw_v;
-                    cur_v = l == g ? cur : cur_v;
-                    const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
-                    cur += ce > 0 ? 3 + ce : 2;
-                }
-                COVT_PHASE(c, 1);
-                const bool in = l < nbat;
-                const int32_t b_v = (int32_t)(int8_t)(hw_v & 0xffu);
-                const int32_t ce_v = (int32_t)((hw_v >> 8) & 0xffu);
-                const int32_t idx_v = (int32_t)(int8_t)((hw_v >> 16) & 0xffu) - b_v;
-                const bool hasx = ce_v > 0;
-                const bool arr_k = hasx && idx_v >= 2 && idx_v <= 32;  // exceptions from dataTobePacked[idx]
-                const bool arr = in && arr_k;
-                // exception cursors: the values of dataTobePacked[k] consumed before the batch (lane k of
-                // xc_v) + the exceptions of the batch's earlier blocks of width k
-                const bool cap = skip && jb0 > jbat && jb0 < jbat + nbat && skip->done != done;  // pass one: keep the state at jb0
-                const int32_t gj = jb0 - jbat;
-                int32_t xcur_v = 0, xc_at = xc_v;
-                for (uint64_t todo = __ballot(arr); todo;) {
-                    const int32_t kk = __builtin_amdgcn_readlane(idx_v, (int32_t)__builtin_ctzll(todo));
-                    const bool mine = arr && idx_v == kk;
-                    const uint32_t v = mine ? (uint32_t)ce_v : 0u;
-                    const uint32_t s = incl_scan(v);
-                    const int32_t base = __builtin_amdgcn_readlane(xc_v, kk);
-                    xcur_v = mine ? base + (int32_t)(s - v) : xcur_v;
-                    if (cap) xc_at = l == kk ? base + (int32_t)lane_bcast(s, gj - 1) : xc_at;
-                    xc_v += l == kk ? (int32_t)lane_bcast(s, 63) : 0;
-                    todo &= ~__ballot(mine);
-                }
-                // packed words: block g starts 8 b words after block g - 1
-                const uint32_t w8 = in ? 8u * (uint32_t)b_v : 0u;
-                const uint32_t pinc = incl_scan(w8);
-                const int32_t pk_v = pk + (int32_t)(pinc - w8);
-                pk += (int32_t)lane_bcast(pinc, 63);
-                if (cap) {
-                    skip->done = done;
-                    skip->cur0 = __builtin_amdgcn_readlane(cur_v, gj);
-                    skip->pk = __builtin_amdgcn_readlane(pk_v, gj);
-                    skip->xc = xc_at;
-                }
-                // FastPFOR.decodePage's checks for the blocks this range decodes (the blocks before jb0 are
-                // checked by the range that decodes them; a chain that left the container reaches jb0 too)
-                {
-                    const int32_t xsz = lane_get(xz_v, arr_k ? idx_v : 0);
-                    bool bad = (uint32_t)b_v > 32u || cur_v + 2 > bclen;
-                    bad |= hasx && (cur_v + 3 + ce_v > bclen || (idx_v != 1 && !arr_k));
-                    bad |= arr_k && (xsz < 0 || xcur_v + ce_v > xsz);
-                    const bool trunc = pk_v + 8 * b_v > nw32;
-                    const uint64_t fail = __ballot(in && jbat + l >= jb0 && (bad || trunc));
-                    if (fail) {
-                        c.err = __builtin_amdgcn_readlane(bad ? COVT_ERR_BAD_HEADER : COVT_ERR_TRUNCATED,
-                                                          (int32_t)__builtin_ctzll(fail));
-                        break;
-                    }
-                }
-                COVT_PHASE(c, 2);
-                // block jbat + g's state (uniform) from lane g
-                auto rec = [&](int32_t g, FpfHdr& h) {
-                    const uint32_t hw = (uint32_t)__builtin_amdgcn_readlane((int32_t)hw_v, g);
-                    h.b = (int32_t)(int8_t)(hw & 0xffu);
-                    h.ce = (int32_t)((hw >> 8) & 0xffu);
-                    h.idx = h.ce > 0 ? (int32_t)(int8_t)((hw >> 16) & 0xffu) - h.b : 0;
-                    h.xcur = (uint32_t)__builtin_amdgcn_readlane(xcur_v, g);
-                    h.bcoff = __builtin_amdgcn_readlane(cur_v, g) + (h.ce > 0 ? 3 : 2);
-                    h.pk = __builtin_amdgcn_readlane(pk_v, g);
-                };
-                const int32_t jend = jbat + nbat;
-                int32_t j = uni(max(jbat, jb0));
-                if (!early) {
-                    rec(j - jbat, h);
-                    pos_window(h);
-                    prefetch(h, pre);
-                }
-                // one block; the loop below alternates two register sets so that no in-flight prefetch
-                // register is ever copied (a copy would force the vmcnt wait at the end of the iteration)
-                auto block = [&](int32_t j, const FpfPre& pc, FpfPre& pn) {
-                    FpfHdr hc;
-                    hc.b = uni(h.b);
-                    hc.ce = uni(h.ce);
-                    hc.idx = uni(h.idx);
-                    hc.xcur = uniu(h.xcur);
-                    hc.bcoff = uni(h.bcoff);
-                    hc.pk = uni(h.pk);
-                    const int32_t b = hc.b;
-                    // stage block j: LDS dword qoff + i = packed word i (aligned, byte-swapped)
-                    const uint32_t o = (sbmis + 4u * (uint32_t)hc.pk) & 15u;
-                    const int32_t qoff = (int32_t)(o >> 2);
-                    {
-                        uint4 raw2 = make_uint4(0, 0, 0, 0);
-                        if (b == 32) {  // rare: the 16 bytes past the first KiB (same for every lane; scalar load)
-                            const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)hc.pk) & ~(uintptr_t)15;
-                            raw2 = sld128(a16 + 1024);
-                        }
-                        const uint32_t nxt = lane_next(pc.raw.x, raw2.x);
-                        uint4 wv;
-                        wv.x = be_word(pc.raw.y, pc.raw.x, bsel);
-                        wv.y = be_word(pc.raw.z, pc.raw.y, bsel);
-                        wv.z = be_word(pc.raw.w, pc.raw.z, bsel);
-                        wv.w = be_word(nxt, pc.raw.w, bsel);
-                        ((uint4*)sm.u.f.stage)[l] = wv;
-                        if (b == 32 && l == 0) {
-                            uint4 w2;
-                            w2.x = be_word(raw2.y, raw2.x, bsel);
-                            w2.y = be_word(raw2.z, raw2.y, bsel);
-                            w2.z = be_word(raw2.w, raw2.z, bsel);
-                            w2.w = be_word(0u, raw2.w, bsel);
-                            ((uint4*)sm.u.f.stage)[64] = w2;
-                        }
-                    }
-                    if (hc.ce > 0) ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
-                    wave_sync();
-                    COVT_PHASE(c, 3);
-                    // block j + 1's loads in flight.  Issued unconditionally (the batch's last block re-reads
-                    // its own words) so that every path has the same number of memory ops in flight and the
-                    // waits for this block's exception words stay partial.
-                    if (j + 1 < jend) {
-                        rec(j + 1 - jbat, h);
-                        pos_window(h);
-                    }
-                    prefetch(h, pn);
-                    // unpack: lane l -> values 4l..4l+3 of miniblock l/8
-                    uint32_t v[4];
-                    {
-                        const uint32_t mask = b == 32 ? 0xffffffffu : ((1u << b) - 1u);
-                        uint32_t bit = __umul24((uint32_t)(l & 7) * 4u, (uint32_t)b);
-                        const int32_t wb = (int32_t)__umul24((uint32_t)(l >> 3), (uint32_t)b) + qoff;
+                const int32_t pb = h.bcoff - cbase;  // positions of exception e at cbuf byte pb + e
+                pr.pos = cb8[min(pb + l, 4 * 260 - 1)];
+                if (h.ce > 64) {  // rare: keep positions 64.. in LDS (the chunk may move on)
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const int32_t wi = wb + (int32_t)(bit >> 5);
-                            const uint32_t lo = sm.u.f.stage[wi], hi = sm.u.f.stage[wi + 1];
-                            v[k] = __builtin_amdgcn_alignbit(hi, lo, bit & 31u) & mask;
-                            bit += (uint32_t)b;
-                        }
+                    for (int q = 1; q < 4; ++q)
+                        sm.u.f.posx[slot][64 * (q - 1) + l] = cb8[min(pb + l + 64 * q, 4 * 260 - 1)];
+                }
+            };
+            FpfHdr h;
+            FpfPre pre;
+            int32_t pk = (int32_t)p0 + 1;
+            int32_t cur0 = 0;
+            // headers of the page's blocks before the range: only their offsets, packed words and exception
+            // cursors, one LDS read per header (each block is checked by the chunk that decodes it; the
+            // container bound keeps this walk's reads in place), once per chunk
+            if (jb0 > 0 && jb0 < nblocks && !c.err) {
+                if (skip && skip->done == done) {  // (FpfSkip::done: set by the pre-walk below)
+                    cur0 = skip->cur0;
+                    pk = skip->pk;
+                    xc_v = skip->xc;
+                } else {
+                    int32_t cur = 0, pkk = pk;
+                    for (int32_t j = 0; j < jb0; ++j) {
+                        if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 8)) chunk_load(cur);
+                        const int32_t jj = cur - cbase;
+                        const uint32_t hw = uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(jj >> 2) + 1],
+                                                                            sm.u.f.cbuf[jj >> 2], (uint32_t)jj & 3u));
+                        const int32_t b = (int32_t)(int8_t)(hw & 0xffu);
+                        const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
+                        const int32_t idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - b;
+                        pkk += 8 * b;
+                        xc_v += (ce > 0 && idx >= 2 && idx <= 32 && l == idx) ? ce : 0;
+                        cur += ce > 0 ? 3 + ce : 2;
+                        if (cur > bclen) { c.err = COVT_ERR_BAD_HEADER; break; }
                     }
-                    COVT_PHASE(c, 4);
+                    cur0 = uni(cur);
+                    pk = uni(pkk);
+                    if (skip) {
+                        skip->done = done;
+                        skip->cur0 = cur0;
+                        skip->pk = pk;
+                        skip->xc = xc_v;
+                    }
+                }
+                COVT_PHASE(c, 0);  // (the pre-walk counts with the directory)
+            }
+            if (jb0 < nblocks && !c.err) {
+                c.err = walk(cur0, h);
+                if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
+                if (!c.err) prefetch(h, pk, pre, 0);
+            }
+            // one block; the loop below alternates two register sets so that no in-flight prefetch
+            // register is ever copied (a copy would force the vmcnt wait at the end of the iteration)
+            auto block = [&](int32_t j, const FpfPre& pc, FpfPre& pn, int slot) {
+                FpfHdr hc;
+                hc.b = uni(h.b);
+                hc.ce = uni(h.ce);
+                hc.idx = uni(h.idx);
+                hc.xcur = uniu(h.xcur);
+                hc.bcoff = uni(h.bcoff);
+                hc.next = uni(h.next);
+                const int32_t pkc = uni(pk);
+                const int32_t b = hc.b;
+                // stage block j: LDS dword qoff + i = packed word i (aligned, byte-swapped)
+                const uint32_t o = (sbmis + 4u * (uint32_t)pkc) & 15u;
+                const int32_t qoff = (int32_t)(o >> 2);
+                {
+                    uint4 raw2 = make_uint4(0, 0, 0, 0);
+                    if (b == 32) {  // rare: the 16 bytes past the first KiB (same for every lane; scalar load)
+                        const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pkc) & ~(uintptr_t)15;
+                        raw2 = sld128(a16 + 1024);
+                    }
+                    const uint32_t nxt = lane_next(pc.raw.x, raw2.x);
+                    uint4 wv;
+                    wv.x = be_word(pc.raw.y, pc.raw.x, bsel);
+                    wv.y = be_word(pc.raw.z, pc.raw.y, bsel);
+                    wv.z = be_word(pc.raw.w, pc.raw.z, bsel);
+                    wv.w = be_word(nxt, pc.raw.w, bsel);
+                    ((uint4*)sm.u.f.stage)[l] = wv;
+                    if (b == 32 && l == 0) {
+                        uint4 w2;
+                        w2.x = be_word(raw2.y, raw2.x, bsel);
+                        w2.y = be_word(raw2.z, raw2.y, bsel);
+                        w2.z = be_word(raw2.w, raw2.z, bsel);
+                        w2.w = be_word(0u, raw2.w, bsel);
+                        ((uint4*)sm.u.f.stage)[64] = w2;
+                    }
+                }
+                if (hc.ce > 0) ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
+                wave_sync();
+                COVT_PHASE(c, 1);
+                // walk block j+1 and put its loads in flight.  The loads are issued unconditionally (the
+                // last block re-reads its own words) so that every path has the same number of memory
+                // ops in flight and the waits for this block's exception words stay partial.
+                if (j + 1 < nblocks) {
+                    c.err = walk(hc.next, h);
+                    pk = pkc + 8 * b;
+                    if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
+                    if (c.err) return;
+                }
+                prefetch(h, pk, pn, slot ^ 1);
+                COVT_PHASE(c, 2);
+                // unpack: lane l -> values 4l..4l+3 of miniblock l/8
+                uint32_t v[4];
+                {
+                    const uint32_t mask = b == 32 ? 0xffffffffu : ((1u << b) - 1u);
+                    uint32_t bit = __umul24((uint32_t)(l & 7) * 4u, (uint32_t)b);
+                    const int32_t wb = (int32_t)__umul24((uint32_t)(l >> 3), (uint32_t)b) + qoff;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int32_t wi = wb + (int32_t)(bit >> 5);
+                        const uint32_t lo = sm.u.f.stage[wi], hi = sm.u.f.stage[wi + 1];
+                        v[k] = __builtin_amdgcn_alignbit(hi, lo, bit & 31u) & mask;
+                        bit += (uint32_t)b;
+                    }
+                }
+                COVT_PHASE(c, 3);
 #if defined(COVT_ABL_NOEXC)  // ablation build: exceptions not applied
-                    if (false) {
+                if (false) {
 #else
-                    if (hc.ce > 0) {  // out[pos] |= (index == 1 ? 1 : exceptvalue) << b
+                if (hc.ce > 0) {  // out[pos] |= (index == 1 ? 1 : exceptvalue) << b
 #endif
-                        const int32_t k = hc.idx;
-                        const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
-                        const bool el = l < hc.ce;
-                        uint32_t ex = 1u;
-                        if (k != 1) {  // uniform
-                            uint32_t xbit;
-                            const int32_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
-                            uint64_t lo = be_word(pc.x1, pc.x0, bsel);
-                            uint64_t hi = be_word(pc.x2, pc.x1, bsel);
-                            lo = wi < nw32 ? lo : 0ull;  // words past the stream read as 0
-                            hi = (wi + 1 < nw32 && xbit + (uint32_t)k > 32u) ? hi : 0ull;
-                            const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
-                            ex = (uint32_t)(((lo | (hi << 32)) >> xbit) & m);
-                        }
-                        // lanes without an exception OR 0 into their own slot: no branch, no conflict
-                        atomicOr(&sm.u.f.patch[el ? pc.pos : (uint32_t)(4 * l)], el ? ex << (b & 31) : 0u);
-                        if (hc.ce > 64) {  // rare: more than 64 exceptions in the block
-                            for (int q = 1; q < 4; ++q) {
-                                const int32_t e = l + 64 * q;
-                                if (e < hc.ce) {
-                                    const uint32_t ex2 = k == 1 ? 1u : xget(W, xs, k, hc.xcur + (uint32_t)e);
-                                    const uint32_t pos2 = cbyte[((uint32_t)(hc.bcoff + e)) ^ 3u];
-                                    atomicOr(&sm.u.f.patch[pos2], ex2 << (b & 31));
-                                }
+                    const int32_t k = hc.idx;
+                    const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
+                    const bool el = l < hc.ce;
+                    uint32_t ex = 1u;
+                    if (k != 1) {  // uniform
+                        uint32_t xbit;
+                        const int32_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
+                        uint64_t lo = be_word(pc.x1, pc.x0, bsel);
+                        uint64_t hi = be_word(pc.x2, pc.x1, bsel);
+                        lo = wi < nw32 ? lo : 0ull;  // words past the stream read as 0
+                        hi = (wi + 1 < nw32 && xbit + (uint32_t)k > 32u) ? hi : 0ull;
+                        const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
+                        ex = (uint32_t)(((lo | (hi << 32)) >> xbit) & m);
+                    }
+                    // lanes without an exception OR 0 into their own slot: no branch, no conflict
+                    atomicOr(&sm.u.f.patch[el ? pc.pos : (uint32_t)(4 * l)], el ? ex << (b & 31) : 0u);
+                    if (hc.ce > 64) {  // rare: more than 64 exceptions in the block
+                        for (int q = 1; q < 4; ++q) {
+                            const int32_t e = l + 64 * q;
+                            if (e < hc.ce) {
+                                const uint32_t ex = k == 1 ? 1u : xget(W, xs, k, hc.xcur + (uint32_t)e);
+                                atomicOr(&sm.u.f.patch[sm.u.f.posx[slot][64 * (q - 1) + l]], ex << (b & 31));
                             }
                         }
-                        wave_sync();
-                        const uint4 pt = ((const uint4*)sm.u.f.patch)[l];
-                        v[0] |= pt.x;
-                        v[1] |= pt.y;
-                        v[2] |= pt.z;
-                        v[3] |= pt.w;
                     }
-                    COVT_PHASE(c, 5);
-#if defined(COVT_ABL_NOSTORE)  // ablation build: every block's output to the same 1 KiB (L2-resident)
-                    sink_values<OP, 4>(v, 0, 0, kFpfBlock, c.nb, c.out, cr);
-#else
-                    if (sum_only)
-                        sum_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, ax, ay);
-                    else
-                        sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, 0, kFpfBlock, c.nb, c.out, cr);
-#endif
                     wave_sync();
-                    COVT_PHASE(c, 6);
-                };
-                for (; j < jend; j += 2) {
-                    block(j, pre, preB);
-                    if (j + 1 < jend) block(j + 1, preB, pre);
+                    const uint4 pt = ((const uint4*)sm.u.f.patch)[l];
+                    v[0] |= pt.x;
+                    v[1] |= pt.y;
+                    v[2] |= pt.z;
+                    v[3] |= pt.w;
                 }
+                COVT_PHASE(c, 4);
+#if defined(COVT_ABL_NOSTORE)  // ablation build: every block's output to the same 1 KiB (L2-resident)
+                sink_values<OP, 4>(v, 0, 0, kFpfBlock, c.nb, c.out, cr);
+#else
+                if (sum_only)
+                    sum_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, kFpfBlock, ax, ay);
+                else
+                    sink_values<OP, 4>(v, (int64_t)done + (int64_t)j * kFpfBlock, 0, kFpfBlock, c.nb, c.out, cr);
+#endif
+                wave_sync();
+                COVT_PHASE(c, 5);
+            };
+            FpfPre preB;
+            for (int32_t j = jb0; j < nblocks && !c.err; j += 2) {
+                block(j, pre, preB, 0);
+                if (j + 1 < nblocks && !c.err) block(j + 1, preB, pre, 1);
             }
             done += thissize;
             p = ie;

@@ -68,7 +68,8 @@ def build_native(out_dir: str) -> str:
     """The same restatement built with -march=native into `out_dir` (bench.py's cpu_baseline leg builds it on
     the GPU box's own host, SURVEY §8(d) "CPU timing"); returns the library path."""
     out = os.path.join(out_dir, "liboracle_covt_native.so")
-    srcs = [os.path.join(_HERE, f) for f in ("covt_oracle.c", "covt_oracle_props.c", "mvt_decode.c")]
+    srcs = [os.path.join(_HERE, f) for f in ("covt_oracle.c", "covt_oracle_props.c", "covt_oracle_tile.c",
+                                             "mvt_decode.c")]
     subprocess.check_call([os.environ.get("CC", "gcc"), "-O3", "-march=native", "-fPIC", "-std=c11", "-shared",
                            "-o", out] + srcs + ["-lpthread"])
     return out
@@ -96,6 +97,8 @@ def _bind(L):
     L.mvt_decode_tile.argtypes = [u8p, C.c_int64, C.c_int, i32p, C.c_int64, i64p, C.POINTER(C.c_uint64)]
     L.oracle_decode_stream.argtypes = [u8p, sz, C.POINTER(OracleStream), C.c_int, C.c_void_p, i32p]
     L.oracle_stream_output.argtypes = [C.POINTER(OracleStream), C.c_int, i32p, i64p]
+    L.oracle_decode_tile_full.argtypes = [C.POINTER(C.c_uint8), C.c_size_t, C.c_int, C.c_int,
+                                          C.POINTER(C.c_int64)]
     L.oracle_decode_tiles_mt.argtypes = [u8p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int32,
                                          C.c_int, C.c_int, C.c_int32, i64p, i64p, i64p]
     L.oracle_encode_varints_u64.restype = C.c_int64
@@ -390,6 +393,16 @@ def decode_tiles_mt(blob: np.ndarray, offsets, sizes, fmt=FMT_GENC, id_mode=ID_F
 # ---------------------------------------------------------------------------
 # geometry assembly (CovtParser.convertGeometryColumn, CovtParser.java:135-274)
 # ---------------------------------------------------------------------------
+def decode_tile_full(tile: bytes, fmt=FMT_GENC, id_mode=ID_FORMAT, L=None):
+    """BASELINE configs[0]: one tile decoded the way CovtParser.decodeCovt does (walk, Id / Geometry streams,
+    geometry assembly, property columns), one thread -> (status, dict of counts)."""
+    L = L or lib()
+    buf = (C.c_uint8 * max(len(tile), 1)).from_buffer_copy(tile if tile else b"\0")
+    cnt = (C.c_int64 * 4)()
+    st = L.oracle_decode_tile_full(buf, len(tile), fmt, id_mode, cnt)
+    return st, {"streams": cnt[0], "vertices": cnt[1], "coords": cnt[2], "property_columns": cnt[3]}
+
+
 def assemble_geometry(types, go, po, ro, vo, vb, closed_in_stream: bool, caps=None):
     """Nested-offset assembly of one decoded GeometryColumn (count arrays may be None).
     vb: int32 x,y interleaved.  Returns (status, geo_off, part_off, ring_off, coords[k,2])."""

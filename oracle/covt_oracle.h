@@ -175,6 +175,11 @@ int oracle_decode_tiles_mt(const uint8_t* bytes, const uint64_t* offsets, const 
                            int format, int id_mode, int32_t n_threads, int64_t* in_bytes, int64_t* out_bytes,
                            int64_t* vertices);
 
+/* BASELINE configs[0]: one whole tile as CovtParser.decodeCovt decodes it, single-threaded: walk, every
+ * Id / Geometry stream, every geometry column assembled, every property column (covt_oracle_tile.c).
+ * counts (optional): streams, vertices, assembled coordinates, property columns. */
+int oracle_decode_tile_full(const uint8_t* tile, size_t len, int format, int id_mode, int64_t counts[4]);
+
 #ifdef __cplusplus
 }
 #endif

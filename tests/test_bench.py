@@ -20,7 +20,7 @@ def _run(args, timeout=240):
 
 
 def test_gpus2_dry_run_spawns_two_ranks():
-    p, lines = _run(["--gpus", "2", "--dry-run", "--tiles", "40", "--steps", "2", "--warmup", "1"])
+    p, lines = _run(["--gpus", "2", "--dry-run", "--tiles", "40", "--steps", "2", "--warmup", "1", "--cpu-iters", "2"])
     assert p.returncode == 0, p.stderr[-2000:]
     assert len(lines) == 1, p.stdout  # rank 0 only
     line = json.loads(lines[0])
@@ -30,7 +30,8 @@ def test_gpus2_dry_run_spawns_two_ranks():
     assert len({r["seed"] for r in pr}) == 2  # weak scaling: distinct per-rank batches
     assert all(r["tiles"] == 40 for r in pr)
     assert line["config"]["parallelism"].startswith("dp2")
-    assert line["cpu_baseline"] is None  # CPU baseline on rank 0 at N=1 only
+    cb = line["cpu_baseline"]  # rank 0's batch, at every N (north_star: "next to the Java CPU decoder ... in the same run")
+    assert cb is not None and cb["value"] > 0 and cb["kind"] == "port"
 
 
 def test_gpus2_strong_dry_run_shards_one_batch():
@@ -86,3 +87,18 @@ def test_cpu_baseline_leg_uses_host_cpus():
     assert cb["cores"] == n and cb["host"]["nproc"] == os.cpu_count()
     assert cb["kind"] == "port" and "full bench batch (30 tiles" in cb["sample"]
     assert cb["value"] > 0 and cb["value_1thread"] > 0
+    assert "config1" not in cb  # merged into configs.config1 (absent in a dry run)
+
+
+def test_config1_cpu_leg():
+    """BASELINE configs[0]: the oracle decodes omt/5_16_20 whole (walk, 41 Id/Geometry streams, assembly,
+    property columns) -- the figure the bench line puts beside the GPU's one-tile latency."""
+    import bench
+
+    sys.path.insert(0, ROOT)
+    import oracle as O
+
+    lib = bench.tile_library()
+    t = bench.config1_tile(lib)
+    st, cnt = O.decode_tile_full(t)
+    assert st == 0 and cnt["streams"] == 41 and cnt["vertices"] == 19285 and cnt["property_columns"] > 0

@@ -127,3 +127,72 @@ def test_full_batch_plan(covt, gpu_available):
     assert hp.num_descs == hp.num_streams and hp.family_counts[3] > 0  # COVT_FAMILY_LANE
     dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
     _assert_same_plan(hp, dp)
+
+
+def _genc_layers(t: bytes):
+    """Byte ranges [(start, end)] of a Gen C tile's layers (metadata + data, Appendix A.1)."""
+    def vu(o):
+        r = sh = 0
+        while True:
+            b = t[o]
+            o += 1
+            r |= (b & 0x7F) << sh
+            sh += 7
+            if b < 0x80:
+                return r, o
+
+    _, o = vu(0)
+    nl, o = vu(o)
+    out = []
+    for _ in range(nl):
+        s = o
+        n, o = vu(o)
+        o += n
+        _, o = vu(o)
+        _, o = vu(o)
+        nc, o = vu(o)
+        tot = 0
+        for _ in range(nc):
+            n, o = vu(o)
+            o += n + 2
+            ns, o = vu(o)
+            for _ in range(ns):
+                n, o = vu(o)
+                o += n
+                _, o = vu(o)
+                bl, o = vu(o)
+                o += 1
+                tot += bl
+        o += tot
+        out.append((s, o))
+    assert o == len(t)
+    return out
+
+
+def _merge_genc(tiles):
+    """One Gen C tile holding every layer of `tiles` (layers are self-contained: metadata, then data)."""
+    layers = [t[s:e] for t in tiles for s, e in _genc_layers(t)]
+    n = len(layers)
+    hdr = bytes([1]) + (bytes([n]) if n < 128 else bytes([0x80 | (n & 0x7F), n >> 7]))
+    return hdr + b"".join(layers)
+
+
+@pytest.mark.parametrize("walk", [0, 1, 4], ids=["slots", "walk_twice", "lanes4"])
+@pytest.mark.parametrize("fmt", [0, 1], ids=["genc", "gend"])
+def test_tiles_past_slot_capacity(covt, gpu_available, decodable_tiles, walk, fmt):
+    """Tiles with more Id / Geometry streams than the count walk's 128 per-tile slots (merged fixture layers:
+    164-200+ streams) beside ordinary tiles, in every walk layout (covt_plan_options.device_walk): the slot
+    path and the re-walk of the big tiles write one stream array together; it must equal the host plan."""
+    omt = [t for k, t in decodable_tiles if k.startswith("omt/")]
+    big = [_merge_genc(omt[i:i + 5]) for i in range(0, 20, 5)]
+    tiles = []
+    for i, b in enumerate(big):
+        tiles += omt[20 + 3 * i: 23 + 3 * i] + [b]
+    if fmt == 1:
+        tiles = [RT.genc_to_gend(t)[0] for t in tiles]
+    hp = _host_plan(covt, tiles, fmt, 0, device_walk=walk)
+    per_tile = np.bincount(hp.streams["tile"], minlength=len(tiles))
+    assert per_tile.max() > 128 and (hp.tile_status == 0).all()
+    dp = _device_plan(covt, hp, fmt, 0)
+    _assert_same_plan(hp, dp)
+    _assert_same_decode(covt, hp, dp)
