@@ -466,28 +466,38 @@ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 // The serial walk spends ~90 scalar instructions per metadata varint (~75k per tile: 2.2 ms for the 10k-
 // tile bench batch, profiles/r02).  Most of a Gen C tile's metadata is a chain of records of two shapes:
 // column headers (name, dataType, columnType, numStreams) and stream records (name, numValues, byteLength,
-// encoding).  So the wave stages 1 KiB of metadata (+ 256 bytes of look-ahead) in LDS and every lane
-// parses, at each of its 16 positions, the record that WOULD start there -- a stream record's length and
+// encoding).  So the wave stages kFwSpan bytes of metadata (+ 256 bytes of look-ahead) in LDS and every lane
+// parses, at each position (256 at a time, as the walk reaches them), the record that WOULD start there -- a stream record's length and
 // byteLength, a column header's length, stream count, kind (id / geometry / other) and columnType -- into
 // two tables; the walk then follows the chain one LDS read per record and parses fields only for the
 // Id / Geometry streams it emits.  Anything outside the fast grammar (a name or varint longer than the
 // tables hold, a record past the tile, a check the serial walk would fail) makes the tile fall back to the
 // serial walk (walk_genc_dev), which then gives the exact statuses; a successful fast walk emits the same
 // records in the same order.
-constexpr int kFwSpan = 1024;   // table positions per window
-constexpr int kFwBytes = 1280;  // window bytes: the positions + 256 bytes of look-ahead
+#ifndef COVT_FW_SPAN
+#define COVT_FW_SPAN 512
+#endif
+constexpr int kFwSpan = COVT_FW_SPAN;  // table positions per window (a multiple of 256)
+constexpr int kFwBytes = kFwSpan + 256;  // window bytes: the positions + 256 bytes of look-ahead
+constexpr int kFwGeo = 32;  // geometry streams per column the fast walk holds (more: the serial walk)
 constexpr int kFastFallback = 1;
 struct FastSmem {
     uint32_t win[kFwBytes / 4 + 4];
     uint32_t stab[kFwSpan];  // stream record at j: length | byteLength << 8 (0: not fast)
     uint32_t ctab[kFwSpan];  // column header at j: length | numStreams << 8 | kind << 17 | columnType << 19 (0: not fast)
 };
-constexpr size_t kFastSmemOffset = 512 + 256 * 16;  // after Rd<true>'s window and geometry table
+// LDS: Rd<true>'s 512-byte window, then the geometry table (kFwGeo entries for the fast walk, 256 for the
+// serial one, which overlaps the fast walk's tables: it only runs once they are abandoned).  Small
+// enough for ~6 waves per SIMD: the walk is a latency-bound chain, so resident tiles set its rate.
+constexpr size_t kFastSmemOffset = 512 + kFwGeo * 16;
+constexpr size_t kWalkLds = kFastSmemOffset + sizeof(FastSmem) > 512 + 256 * 16 ? kFastSmemOffset + sizeof(FastSmem)
+                                                                                  : 512 + 256 * 16;
 
 struct FastGenc {
     const uint8_t* t;
     int32_t len;
     int32_t wb;  // tile offset of window byte 0 (16-byte aligned address; may be < 0 at the tile start)
+    uint32_t segs;  // window positions [256 k, 256 k + 256) whose record tables are built: bit k
     FastSmem* fs;
     // bytes [q, q + 8) of the window, q per lane (q <= kFwBytes - 8)
     __device__ __forceinline__ uint64_t peek8(int32_t q) const {
@@ -502,23 +512,31 @@ struct FastGenc {
         return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
     }
-    // the window holding tile offset `at`, and the record tables of its first kFwSpan positions
+    // the window holding tile offset `at` (its record tables are built on demand, 256 positions at a time:
+    // a layer's metadata is often a few hundred bytes)
     __device__ void load(int32_t at) {
         const int l = threadIdx.x;
         const uintptr_t lo = (uintptr_t)t;
         const uintptr_t b = (lo + (uintptr_t)(int64_t)at) & ~(uintptr_t)15;
         wb = (int32_t)(int64_t)(b - lo);
         wb = __builtin_amdgcn_readfirstlane(wb);
+        segs = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        ((uint4*)fs->win)[l] = window_ld(t, len, b + 16 * (uintptr_t)l);
-        if (l < kFwBytes / 16 - 64) ((uint4*)fs->win)[64 + l] = window_ld(t, len, b + 16 * (uintptr_t)(64 + l));
+#pragma unroll
+        for (int i = 0; i < kFwBytes / 16; i += 64)
+            if (i + 64 <= kFwBytes / 16 || i + l < kFwBytes / 16)
+                ((uint4*)fs->win)[i + l] = window_ld(t, len, b + 16 * (uintptr_t)(i + l));
         if (l == 0) ((uint4*)fs->win)[kFwBytes / 16] = make_uint4(0, 0, 0, 0);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         __builtin_amdgcn_wave_barrier();
+    }
+    // the record tables of window positions [256 sg, 256 sg + 256)
+    __device__ void build(int sg) {
+        const int l = threadIdx.x;
         constexpr uint64_t kId = pk("id", 0, 2), kGeo = pk("geometry", 0, 8);
-#pragma unroll 2
-        for (int i = 0; i < kFwSpan / 64; ++i) {
-            const int32_t q = l + 64 * i, j = wb + q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int32_t q = 256 * sg + l + 64 * i, j = wb + q;
             uint32_t se = 0, ce = 0;
             const uint64_t nm = peek8(q + 1);              // name bytes (a stream / column name)
             const uint32_t n = fs->win[q >> 2] >> (8 * (q & 3)) & 0xffu;  // its length (one LEB128 byte)
@@ -555,18 +573,26 @@ struct FastGenc {
             fs->stab[q] = se;
             fs->ctab[q] = ce;
         }
+        segs |= 1u << sg;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         __builtin_amdgcn_wave_barrier();
     }
-    __device__ __forceinline__ int32_t at(int32_t o) {  // the window offset of tile offset o (reloads)
+    __device__ __forceinline__ int32_t at(int32_t o) {  // the window offset of tile offset o (loads, builds)
+        if ((uint32_t)(o - wb) >= (uint32_t)kFwSpan) load(o);
+        const int32_t q = o - wb;
+        if (!((segs >> (q >> 8)) & 1u)) build(q >> 8);
+        return q;
+    }
+    // window offset of tile offset o for plain byte reads (no tables needed)
+    __device__ __forceinline__ int32_t at_bytes(int32_t o) {
         if ((uint32_t)(o - wb) >= (uint32_t)kFwSpan) load(o);
         return o - wb;
     }
     // a uniform LEB128 value of at most 4 bytes at o (false: longer, or past the tile)
     __device__ __forceinline__ bool uv4(int32_t& o, uint32_t& v) {
         if (o >= len) return false;
-        const int32_t q = at(o);
+        const int32_t q = at_bytes(o);
         const uint32_t w = (uint32_t)upeek8(q);
         const uint32_t stop = ~w & 0x80808080u;
         if (!stop) return false;
@@ -640,6 +666,7 @@ __device__ int walk_genc_fast(FastGenc& f, E& emit) {
             if (!ce) return kFastFallback;
             const uint32_t ns = (ce >> 8) & 0x1ffu, kind = (ce >> 17) & 3u;
             const int ctype = (int)(ce >> 19) & 0xff;
+            if (kind == 1 && ns > (uint32_t)kFwGeo) return kFastFallback;
             o += (int32_t)(ce & 0xffu);
             uint32_t present = 0;
             for (uint32_t s = 0; s < ns; ++s) {
@@ -701,6 +728,7 @@ __device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes,
         f.t = r.t;
         f.len = (int32_t)size;
         f.wb = -(int32_t)0x40000000;
+        f.segs = 0;
         f.fs = (FastSmem*)((uint8_t*)covt_walk_win + kFastSmemOffset);
         const E fresh = emit;
         const int st = walk_genc_fast(f, emit);
@@ -830,7 +858,7 @@ __global__ void walk_emit(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
                           const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                           const int32_t* __restrict__ status, const int64_t* __restrict__ cnt_base,
                           const int64_t* __restrict__ ob_base, int32_t lane_max, covt_stream_info* __restrict__ info,
-                          int32_t* __restrict__ nvals, unsigned long long* __restrict__ totals,
+                          int32_t* __restrict__ nvals, long long* __restrict__ tsum,
                           const int64_t* __restrict__ cnt) {
     const int32_t t = kWave ? (int32_t)blockIdx.x : (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t >= n_tiles || status[t]) return;
@@ -840,12 +868,7 @@ __global__ void walk_emit(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
     e.writer = !kWave || threadIdx.x == 0;
     e.wave = kWave;
     walk_tile<kWave>(bytes, n_bytes, offs[t], sizes[t], format, e);
-    if (e.writer) {
-        atomicAdd(&totals[T_IN], (unsigned long long)e.in_bytes);
-        atomicAdd(&totals[T_PAYLOAD], (unsigned long long)e.payload);
-        atomicAdd(&totals[T_VERTS], (unsigned long long)e.verts);
-        atomicAdd(&totals[T_LANE], (unsigned long long)e.lane);
-    }
+    if (e.writer) *(longlong4*)(tsum + 4 * (size_t)t) = make_longlong4(e.in_bytes, e.payload, e.verts, e.lane);
 }
 
 // The records walk_count left in a tile's slots -> covt_stream_info, one lane per record: output slices
@@ -855,7 +878,7 @@ __global__ void emit_slots(const uint64_t* __restrict__ offs, int32_t n_tiles, i
                            const int32_t* __restrict__ status, const int64_t* __restrict__ cnt,
                            const int64_t* __restrict__ cnt_base, const int64_t* __restrict__ ob_base,
                            const RawStream* __restrict__ slots, int32_t lane_max, covt_stream_info* __restrict__ info,
-                           int32_t* __restrict__ nvals, unsigned long long* __restrict__ totals) {
+                           int32_t* __restrict__ nvals, long long* __restrict__ tsum) {
     const int32_t t = blockIdx.x;
     if (t >= n_tiles || status[t]) return;
     const int64_t n = cnt[t];
@@ -916,11 +939,31 @@ __global__ void emit_slots(const uint64_t* __restrict__ offs, int32_t n_tiles, i
         verts += __shfl_xor(verts, d, 64);
         nlane += __shfl_xor(nlane, d, 64);
     }
-    if (lane == 0) {
-        atomicAdd(&totals[T_IN], (unsigned long long)in_bytes);
-        atomicAdd(&totals[T_PAYLOAD], (unsigned long long)payload);
-        atomicAdd(&totals[T_VERTS], (unsigned long long)verts);
-        atomicAdd(&totals[T_LANE], (unsigned long long)nlane);
+    if (lane == 0) *(longlong4*)(tsum + 4 * (size_t)t) = make_longlong4(in_bytes, payload, verts, nlane);
+}
+
+// The per-tile sums (input bytes, payload, vertices, lane streams; zero for failed tiles) -> totals: one
+// workgroup (same-address atomics from every tile serialise in L2: ~0.5 ms for 10k tiles)
+__global__ void __launch_bounds__(1024) reduce_tiles(const long long* __restrict__ tsum, int32_t n_tiles,
+                                                     unsigned long long* __restrict__ totals) {
+    __shared__ long long part[16][4];
+    long long a[4] = {0, 0, 0, 0};
+    for (int32_t t = threadIdx.x; t < n_tiles; t += 1024) {
+        const longlong4 v = *(const longlong4*)(tsum + 4 * (size_t)t);
+        a[0] += v.x, a[1] += v.y, a[2] += v.z, a[3] += v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) a[k] += __shfl_xor(a[k], d, 64);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 4; ++k) part[w][k] = a[k];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        long long x = 0;
+        for (int i = 0; i < 16; ++i) x += part[i][threadIdx.x];
+        totals[T_IN + threadIdx.x] = (unsigned long long)x;  // T_IN, T_PAYLOAD, T_VERTS, T_LANE
     }
 }
 
@@ -1004,11 +1047,12 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     } while (0)
     DCHK(hipGetDevice(&p->dev));
     const size_t nt1 = (size_t)n_tiles + 1;
-    // tile arena: status | cnt | ob | cnt_base | ob_base | totals | scan scratch
+    // tile arena: status | cnt | ob | cnt_base | ob_base | totals | per-tile sums | scan scratch | slots
     size_t scan_tmp = 0;
     DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)nt1, s));
     const size_t o_cnt = up256(nt1 * 4), o_ob = o_cnt + up256(nt1 * 8), o_cb = o_ob + up256(nt1 * 8),
-                 o_obb = o_cb + up256(nt1 * 8), o_tot = o_obb + up256(nt1 * 8), o_tmp = o_tot + up256(T_N * 8),
+                 o_obb = o_cb + up256(nt1 * 8), o_tot = o_obb + up256(nt1 * 8), o_ts = o_tot + up256(T_N * 8),
+                 o_tmp = o_ts + up256(nt1 * 32),
                  o_slots = o_tmp + up256(scan_tmp);
     // device_walk 0: a wave per tile with per-tile slots; 1: the same walk twice; k >= 2: k lanes per workgroup
     const int wl = o.device_walk >= 2 ? o.device_walk : 0;
@@ -1020,11 +1064,13 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     int64_t *cnt = (int64_t*)(ta + o_cnt), *ob = (int64_t*)(ta + o_ob), *cb = (int64_t*)(ta + o_cb),
             *obb = (int64_t*)(ta + o_obb);
     auto* totals = (unsigned long long*)(ta + o_tot);
+    auto* tsum = (long long*)(ta + o_ts);
     DCHK(hipMemsetAsync(totals, 0, T_N * 8, s));
+    DCHK(hipMemsetAsync(tsum, 0, nt1 * 32, s));  // failed tiles leave zeros
     // 0: a wave per tile, its lanes in lockstep; k > 0: k lanes per workgroup, a lane per tile
     RawStream* slots = use_slots ? (RawStream*)(ta + o_slots) : nullptr;
     if (wl == 0)
-        walk_count<true><<<(int)nt1, 64, kFastSmemOffset + sizeof(FastSmem), s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
+        walk_count<true><<<(int)nt1, 64, kWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
                                                   id_mode, p->d_status, cnt, ob, slots);
     else
         walk_count<false><<<(int)((nt1 + wl - 1) / wl), wl, (size_t)wl * 64, s>>>(
@@ -1061,17 +1107,19 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     if (n_tiles) {
         if (slots) {
             emit_slots<<<n_tiles, 64, 0, s>>>(d_tile_offsets, n_tiles, id_mode, p->d_status, cnt, cb, obb, slots,
-                                              lane_max, p->d_info, nvals, totals);
+                                              lane_max, p->d_info, nvals, tsum);
             DCHK(hipGetLastError());
         }
         if (wl == 0)  // (with slots: only tiles with more than kSlots streams walk again)
-            walk_emit<true><<<n_tiles, 64, kFastSmemOffset + sizeof(FastSmem), s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
-                                                    id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, totals,
+            walk_emit<true><<<n_tiles, 64, kWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
+                                                    id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, tsum,
                                                     slots ? cnt : nullptr);
         else
             walk_emit<false><<<(n_tiles + wl - 1) / wl, wl, (size_t)wl * 64, s>>>(
                 d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cb, obb,
-                lane_max, p->d_info, nvals, totals, nullptr);
+                lane_max, p->d_info, nvals, tsum, nullptr);
+        DCHK(hipGetLastError());
+        reduce_tiles<<<1, 1024, 0, s>>>(tsum, n_tiles, totals);
         DCHK(hipGetLastError());
     }
     if (ns > 0) {

@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Profiling target: covt_device_plan_create on the bench batch (BASELINE config 5) N times, wall-clock per
+creation printed (run under rocprofv3 --kernel-trace --stats [--hip-trace] for the per-kernel / per-call
+breakdown).  usage: device_plan_prof.py [reps] [--sweep]
+--sweep: also batches of 1 tile (the library's largest), 256, 2048 and 4096 tiles (latency vs. occupancy)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    import torch
+
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    reps = int(args[0]) if args else 10
+    covt = bench.load_covt()
+    lib = bench.tile_library()
+    if "--sweep" in sys.argv:
+        big = max((t for z in lib.values() for _, t in z), key=len)
+        for n in (1, 256, 2048, 4096):
+            tiles = [big] if n == 1 else [t for _, t in bench.sample_batch(lib, n, bench.SEED)]
+            run(covt, tiles, reps, "%5d tiles" % n)
+    picks = bench.sample_batch(lib, 10000, bench.SEED)
+    run(covt, [t for _, t in picks], reps, "10000 tiles")
+
+
+def run(covt, tiles, reps, label):
+    import torch
+
+    blob, offs, sizes = covt.pack_tiles(tiles)
+    d_blob = torch.from_numpy(blob).cuda()
+    d_off = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d_size = torch.from_numpy(sizes.astype(np.int64)).cuda()
+    ts = []
+    for _ in range(reps + 2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dp = covt.DevicePlan(d_blob, d_off, d_size)
+        ts.append(time.perf_counter() - t0)
+        dp.close()
+    print("%s %s device plan: median %.3f ms, min %.3f ms over %d" % (os.environ.get("COVT_LIB_VARIANT", "libcovt.so"), label,
+                                                                   np.median(ts[2:]) * 1e3, min(ts[2:]) * 1e3, reps))
+
+
+if __name__ == "__main__":
+    main()
