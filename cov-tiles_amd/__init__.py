@@ -185,6 +185,7 @@ EXPORTED_SYMBOLS = (
     "covt_device_plan_descs_device", "covt_device_plan_streams_device", "covt_device_plan_tile_status_device",
     "covt_device_plan_order_device", "covt_device_plan_copy", "covt_device_plan_decode",
     "covt_plan_options_init", "covt_plan_create_opts", "covt_device_plan_create_opts",
+    "covt_device_plan_num_descs",
 )
 
 
@@ -276,7 +277,7 @@ def lib() -> C.CDLL:
                                           C.POINTER(vp)]
     L.covt_device_plan_destroy.argtypes = [vp]
     L.covt_device_plan_destroy.restype = None
-    for name in ("covt_device_plan_num_streams", "covt_device_plan_output_bytes"):
+    for name in ("covt_device_plan_num_streams", "covt_device_plan_num_descs", "covt_device_plan_output_bytes"):
         getattr(L, name).argtypes = [vp]
         getattr(L, name).restype = C.c_int64
     L.covt_device_plan_totals.argtypes = [vp, i64p, i64p, i64p]
@@ -792,7 +793,7 @@ class DevicePlan:
     `d_blob` is a uint8 torch tensor on the device holding the tiles, `offsets` / `sizes` the tiles'
     byte ranges in it (host arrays or device tensors).  The walk, prefix sums, launch-order sort and
     descriptor fill run on the current torch stream; the result has the host plan's layout exactly
-    (Plan.streams / Plan.descs / Plan.family_counts for a batch that splits nothing)."""
+    (Plan.streams / Plan.descs / Plan.family_counts with the same options, split chunks included)."""
 
     def __init__(self, d_blob, offsets, sizes, fmt: int = FORMAT_GENC, id_mode: int = ID_FORMAT, stream=None,
                  options: Optional[PlanOptions] = None):
@@ -818,6 +819,7 @@ class DevicePlan:
         self._h = h
         L = lib()
         self.num_streams = L.covt_device_plan_num_streams(h)
+        self.num_descs = L.covt_device_plan_num_descs(h)
         self.output_bytes = L.covt_device_plan_output_bytes(h)
         self.family_counts = np.zeros(NUM_FAMILIES, dtype=np.int64)
         L.covt_device_plan_family_counts(h, _ptr(self.family_counts, C.c_int64))
@@ -839,7 +841,7 @@ class DevicePlan:
     def host_copy(self):
         """(stream records in tile order, descriptors in launch order, tile statuses) as host arrays."""
         info = np.zeros(self.num_streams, dtype=STREAM_INFO_DTYPE)
-        descs = np.zeros(self.num_streams * 32, dtype=np.uint8)
+        descs = np.zeros(self.num_descs * 32, dtype=np.uint8)
         st = np.zeros(max(self.n_tiles, 1), dtype=np.int32)
         _raise(lib().covt_device_plan_copy(self._h, info.ctypes.data, descs.ctypes.data, _ptr(st, C.c_int32)),
                "covt_device_plan_copy")
@@ -850,7 +852,7 @@ class DevicePlan:
         import torch
 
         return (torch.zeros(max(self.output_bytes, 16), dtype=torch.uint8, device=self.device),
-                torch.zeros(max(self.num_streams, 1) * 2, dtype=torch.int32, device=self.device))
+                torch.zeros(max(self.num_descs, 1) * 2, dtype=torch.int32, device=self.device))
 
     def decode(self, d_out, d_res, stream=None):
         """Enqueue the grouped decode launch over this plan's descriptors."""

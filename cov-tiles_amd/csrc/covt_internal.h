@@ -51,23 +51,23 @@ inline int desc_family(const covt_stream_desc& d) {
 }
 // Plan rule for split streams: the Java-capped int32 varint ops (value ends are local: every byte
 // with bit 7 clear ends a value, DecodingUtils.java:157-186), longer than split_min bytes.
-inline bool split_op(int op) {
+__host__ __device__ inline bool split_op(int op) {
     return op == COVT_OP_VARINT_I32 || op == COVT_OP_VARINT_ZZ_I32 || op == COVT_OP_VARINT_ZZ_DELTA_I32 ||
            op == COVT_OP_VARINT_ZZ_DELTA_XY || op == COVT_OP_VARINT_DELTA_MORTON || op == COVT_OP_VARINT_I32_AS_I64 ||
            op == COVT_OP_VARINT_ZZ_I32_AS_I64 || op == COVT_OP_VARINT_ZZ_DELTA_I64 || op == COVT_OP_VARINT_U64 ||
            op == COVT_OP_VARINT_ZZ_S64;
 }
-inline bool split_fpf_op(int op) {
+__host__ __device__ inline bool split_fpf_op(int op) {
     return op == COVT_OP_FPF_ZZ_DELTA_I32 || op == COVT_OP_FPF_ZZ_DELTA_XY || op == COVT_OP_FPF_DELTA_MORTON;
 }
-inline bool split_rle_op(int op) {
+__host__ __device__ inline bool split_rle_op(int op) {
     return op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_I32 || op == COVT_OP_RLE_S64 || op == COVT_OP_BYTE_RLE_U8 ||
            op == COVT_OP_BYTE_RLE_RAW;
 }
 // FastPFOR streams split by values into chunks of whole blocks (their own headers and page directories
 // locate every block), at least two chunks
 // cost: the stream's bytes + output bytes / 4 (covt_plan_create's launch-order key)
-inline bool split_stream(int op, int32_t num_values, int64_t cost, int64_t split_min, int64_t split_values) {
+__host__ __device__ inline bool split_stream(int op, int32_t num_values, int64_t cost, int64_t split_min, int64_t split_values) {
     if (split_min < 0 || num_values <= 0 || cost <= split_min) return false;
     if (split_fpf_op(op)) return num_values > split_values && !(op == COVT_OP_FPF_ZZ_DELTA_XY && (num_values & 1));
     return split_op(op) && !(op == COVT_OP_VARINT_ZZ_DELTA_XY && (num_values & 1));

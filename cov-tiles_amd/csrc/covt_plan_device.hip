@@ -32,20 +32,22 @@
 struct covt_device_plan {
     int dev = 0;
     int32_t n_tiles = 0, format = 0, id_mode = 0;
-    int64_t n_streams = 0, out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
+    int64_t n_streams = 0, n_descs = 0, out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
     int64_t fam_counts[COVT_NUM_FAMILIES] = {};
     void* tile_arena = nullptr;    // status, per-tile counts and prefix sums, totals, scan scratch
     void* stream_arena = nullptr;  // infos, values, keys, launch order, descriptors, sort scratch
+    void* desc_arena = nullptr;    // split plans: the descriptors and their streams (n_descs each)
     int32_t* d_status = nullptr;
     covt_stream_info* d_info = nullptr;
     covt_stream_desc* d_desc = nullptr;
-    uint32_t* d_order = nullptr;  // descriptor k decodes stream d_order[k]
+    uint32_t* d_order = nullptr;  // descriptor k decodes (a chunk of) stream d_order[k]
 };
 
 namespace {
 
 // device totals (int64 slots)
-enum { T_STREAMS = 0, T_OUT = 1, T_IN = 2, T_PAYLOAD = 3, T_VERTS = 4, T_LANE = 5, T_FAM = 8, T_N = 8 + COVT_NUM_FAMILIES };
+enum { T_STREAMS = 0, T_OUT = 1, T_IN = 2, T_PAYLOAD = 3, T_VERTS = 4, T_LANE = 5, T_FAM = 8,
+       T_RCH = 8 + COVT_NUM_FAMILIES, T_N = T_RCH + 1 };
 
 // One tile's bytes, read through a 64-byte window held in registers: four 16-byte loads issued
 // together (one memory latency per 64 bytes of the front-to-back metadata walk instead of four).
@@ -88,6 +90,14 @@ __device__ __noinline__ uintptr_t window_refill(const uint8_t* t, int64_t len, u
     return b;
 }
 
+// bytes [off, off + 8) of an LDS window: three dword reads issued together (one LDS latency; the window
+// is readable 4 bytes past off + 8) and two byte-aligns, no branch on the alignment
+__device__ __forceinline__ uint64_t win_bytes8(const uint32_t* w, uint32_t off) {
+    const uint32_t k = off >> 2, s = off & 3u;
+    const uint32_t d0 = w[k], d1 = w[k + 1], d2 = w[k + 2];
+    return ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32) | __builtin_amdgcn_alignbyte(d1, d0, s);
+}
+
 template <bool kWave>
 struct Rd {
     const uint8_t* t;
@@ -109,12 +119,19 @@ struct Rd {
             if (kWave) wo = (int64_t)(int32_t)__builtin_amdgcn_readfirstlane((int)(int32_t)wo);
             off = (uint32_t)i - (uint32_t)wo;
         }
-        const uint32_t k = off >> 3, sh = (off & 7) * 8;  // off <= kWin - 8
-        const uint64_t* q = reinterpret_cast<const uint64_t*>(w);
-        const uint64_t lo = q[k];
-        return sh ? (lo >> sh) | (q[k + 1] << (64 - sh)) : lo;  // (sh != 0: k + 1 < kWin / 8)
+        return win_bytes8(reinterpret_cast<const uint32_t*>(w), off);  // (off <= kWin - 8)
     }
     __device__ __forceinline__ int at(int32_t i) { return (int)(peek8(i) & 0xff); }
+    // (wave layout) the window holds bytes [i, i + n) (n <= 384); returns i's offset in it
+    __device__ __forceinline__ uint32_t ensure(int32_t i, uint32_t n) {
+        uint32_t off = (uint32_t)i - (uint32_t)wo;
+        if (off > kWin - n) {
+            const uintptr_t b = window_refill<kWave>(t, len, (uintptr_t)(t + i));
+            wo = (int64_t)(int32_t)__builtin_amdgcn_readfirstlane((int)(int32_t)(int64_t)(b - (uintptr_t)t));
+            off = (uint32_t)i - (uint32_t)wo;
+        }
+        return off;
+    }
     // low n bytes (n <= 8) of x's 7-bit groups packed (LEB128 payload)
     __device__ __forceinline__ static uint64_t leb_pack(uint64_t x, int n) {
         x = (n >= 8 ? x : x & ((1ull << (8 * n)) - 1)) & 0x7f7f7f7f7f7f7f7full;
@@ -747,13 +764,19 @@ struct CountEmit {
     RawStream* slots = nullptr;  // this tile's kSlots record slots, or null
     bool writer = true, wave = false;
     int64_t n = 0, out = 0, k0 = 0;
+    int64_t fpf_w = 1, cost = 0, cmax = 0;  // the split rule's cost: sum, and the largest split cost
     __device__ void operator()(const RawStream& s) {
         int op, elem;
         int64_t nvals, oe;
         choose_op(s, id_mode, op, nvals, elem, oe);
         if (slots && writer && n < kSlots) slots[n] = s;
         ++n;
-        out = align16(out + (op == COVT_OP_NONE ? 0 : oe) * elem);
+        const int64_t ob = (op == COVT_OP_NONE ? 0 : oe) * elem;
+        out = align16(out + ob);
+        const int64_t c = (int64_t)s.bl + ob / 4;  // covt_plan_create's stream_cost
+        cost += c;
+        const int64_t sc = split_fpf_op(op) ? c + (fpf_w - 1) * (ob / 4) : c;
+        cmax = sc > cmax ? sc : cmax;
     }
     __device__ void layer_begin() { k0 = n; }
     __device__ void layer_end(int64_t data_start) {  // rebase the layer's recorded data offsets
@@ -782,7 +805,7 @@ template <bool kWave>
 __global__ void walk_count(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
                            const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                            int32_t* __restrict__ status, int64_t* __restrict__ cnt, int64_t* __restrict__ ob,
-                           RawStream* __restrict__ slots) {
+                           RawStream* __restrict__ slots, int64_t fpf_w, int64_t* __restrict__ tcost) {
     const int32_t t = kWave ? (int32_t)blockIdx.x : (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t > n_tiles) return;
     if (t == n_tiles) {  // the prefix sums' total slot
@@ -793,11 +816,44 @@ __global__ void walk_count(const uint8_t* __restrict__ bytes, uint64_t n_bytes, 
     e.slots = slots ? slots + (size_t)t * kSlots : nullptr;
     e.writer = !kWave || threadIdx.x == 0;
     e.wave = kWave;
+    e.fpf_w = fpf_w;
     const int st = walk_tile<kWave>(bytes, n_bytes, offs[t], sizes[t], format, e);
     if (!kWave || threadIdx.x == 0) {
         status[t] = st;
         cnt[t] = st ? 0 : e.n;  // a failed tile contributes nothing
         ob[t] = st ? 0 : e.out;
+        tcost[2 * (size_t)t] = st ? 0 : e.cost;
+        tcost[2 * (size_t)t + 1] = st ? 0 : e.cmax;
+    }
+}
+
+// The first plan totals in one 32-byte block (one D2H): streams, output bytes, the batch's split cost and
+// its largest stream split cost (covt_plan_create_ex step 3: nothing splits unless that passes the threshold)
+__global__ void __launch_bounds__(1024) plan_head(const int64_t* __restrict__ cb, const int64_t* __restrict__ obb,
+                                                  const int64_t* __restrict__ tcost, int32_t n_tiles,
+                                                  int64_t* __restrict__ head) {
+    __shared__ int64_t part[16][2];
+    int64_t sum = 0, mx = 0;
+    for (int32_t t = threadIdx.x; t < n_tiles; t += 1024) {
+        sum += tcost[2 * (size_t)t];
+        const int64_t m = tcost[2 * (size_t)t + 1];
+        mx = m > mx ? m : mx;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        sum += __shfl_xor(sum, d, 64);
+        const int64_t m = __shfl_xor(mx, d, 64);
+        mx = m > mx ? m : mx;
+    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6][0] = sum, part[threadIdx.x >> 6][1] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t a = 0, b = 0;
+        for (int i = 0; i < 16; ++i) a += part[i][0], b = part[i][1] > b ? part[i][1] : b;
+        head[0] = cb[n_tiles];
+        head[1] = obb[n_tiles];
+        head[2] = a;
+        head[3] = b;
     }
 }
 
@@ -968,9 +1024,11 @@ __global__ void __launch_bounds__(1024) reduce_tiles(const long long* __restrict
 }
 
 // launch-order key of covt_plan_create_ex step 3 (no splits): family, lane op, cost descending
+// (split plans: the family and descriptor count of each stream from split_mark / rle_chunks_walk)
 __global__ void stream_keys(const covt_stream_info* info, const int32_t* nvals, int64_t n, int32_t lane_max,
-                            int64_t lane_min, unsigned long long* totals, uint64_t* keys, uint32_t* vals) {
-    __shared__ unsigned int fam_n[COVT_NUM_FAMILIES];
+                            int64_t lane_min, unsigned long long* totals, uint64_t* keys, uint32_t* vals,
+                            const uint8_t* sfam, const int64_t* sndesc) {
+    __shared__ unsigned long long fam_n[COVT_NUM_FAMILIES];
     if (threadIdx.x < COVT_NUM_FAMILIES) fam_n[threadIdx.x] = 0;
     __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -978,16 +1036,16 @@ __global__ void stream_keys(const covt_stream_info* info, const int32_t* nvals, 
         const covt_stream_info& s = info[i];
         const int32_t lm = (int64_t)totals[T_LANE] < lane_min ? -1 : lane_max;
         const bool lane = lane_stream(s.op, nvals[i], s.byte_length, lm);
-        const uint64_t fam = lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family(s.op);
+        const uint64_t fam = sfam ? (uint64_t)sfam[i] : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family(s.op);
         const int64_t c = (int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4;
         const uint64_t cost = c < ((1ll << 48) - 1) ? (uint64_t)c : (1ull << 48) - 1;
         keys[i] = (fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost);
         vals[i] = (uint32_t)i;
-        atomicAdd(&fam_n[fam], 1u);
+        atomicAdd(&fam_n[fam], sndesc ? (unsigned long long)sndesc[i] : 1ull);
     }
     __syncthreads();
     if (threadIdx.x < COVT_NUM_FAMILIES && fam_n[threadIdx.x])
-        atomicAdd(&totals[T_FAM + threadIdx.x], (unsigned long long)fam_n[threadIdx.x]);
+        atomicAdd(&totals[T_FAM + threadIdx.x], fam_n[threadIdx.x]);
 }
 
 __global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const uint64_t* keys, const uint32_t* order,
@@ -1007,6 +1065,366 @@ __global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const u
     d.byte_length = si.byte_length;
     desc[k] = d;
     si.desc_index = (int32_t)k;
+}
+
+// ---- Split plans (covt_plan_create_ex step 3 on the device; only when some stream's split cost passes
+// the batch's threshold, i.e. small batches: their long poles are cut into chunks decoded by separate
+// waves).  The same rule, chunk layout and descriptor order as the host plan:
+//   split_mark       one thread per stream: family, descriptor count (varint: byte chunks, FastPFOR: value
+//                    chunks of whole blocks), and the lists of RLE candidates and split FastPFOR streams
+//   rle_chunks_walk  one wave per RLE candidate: its group framing (rle_chunks in covt_host.cpp) and chunk
+//                    records; a stream it frames in two chunks or more becomes COVT_FAMILY_SPLIT_RLE
+//   stream_keys / sort, then the descriptor offsets (a scan of the counts in launch order; one D2H)
+//   fill_split_descs one thread per descriptor (RLE chunks from the walk's records); then fpf_states_walk
+//                    writes the FastPFOR chunks' start states (fpf_chunk_states in covt_host.cpp)
+enum { T_NRLE = 6, T_NFPF = 7 };  // list lengths (totals slots)
+
+__global__ void split_mark(const covt_stream_info* __restrict__ info, const int32_t* __restrict__ nvals, int64_t n,
+                           int32_t lane_max, int64_t lane_min, int64_t smin, int64_t split_chunk, int64_t split_values,
+                           int64_t fpf_w, unsigned long long* __restrict__ totals, uint8_t* __restrict__ sfam,
+                           int64_t* __restrict__ sndesc, uint32_t* __restrict__ rle_list, uint32_t* __restrict__ fpf_list) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const covt_stream_info& s = info[i];
+    const int32_t nv = nvals[i];
+    const int32_t lm = (int64_t)totals[T_LANE] < lane_min ? -1 : lane_max;
+    const bool lane = lane_stream(s.op, nv, s.byte_length, lm);
+    const int64_t ob4 = s.out_elems * s.elem_bytes / 4, cost = (int64_t)s.byte_length + ob4;
+    const bool fpf = split_fpf_op(s.op);
+    const int64_t scost = fpf ? cost + (fpf_w - 1) * ob4 : cost;
+    const bool split = split_stream(s.op, nv, scost, smin, split_values);
+    int fam = split ? (fpf ? COVT_FAMILY_SPLIT_FPF : COVT_FAMILY_SPLIT) : lane ? COVT_FAMILY_LANE : covt_op_family(s.op);
+    int64_t nd = 1;
+    if (split) {
+        const int64_t unit = fpf ? split_values : split_chunk, tot = fpf ? nv : s.byte_length;
+        nd = (tot + unit - 1) / unit * COVT_SPLIT_SLOTS;
+        if (fpf) fpf_list[atomicAdd(&totals[T_NFPF], 1ull)] = (uint32_t)i;
+    } else if (split_rle_op(s.op) && cost > smin && nv > 0) {
+        rle_list[atomicAdd(&totals[T_NRLE], 1ull)] = (uint32_t)i;
+    }
+    sfam[i] = (uint8_t)fam;
+    sndesc[i] = nd;
+}
+
+// One stream's bytes for the split walkers (a wave each, lanes in lockstep): a 4 KiB LDS window refilled
+// by all 64 lanes at once (four 16-byte loads each, one memory latency per 4 KiB of a long stream)
+struct StreamRd {
+    static constexpr uint32_t kWin = 4096;
+    const uint8_t* t;
+    int64_t len;
+    int32_t wo;  // the window's start as a stream offset (16-byte aligned address)
+    __device__ void refill(int32_t i) {
+        const uintptr_t lo = (uintptr_t)t;
+        const uintptr_t b = (lo + (uintptr_t)(int64_t)i) & ~(uintptr_t)15;
+        wo = __builtin_amdgcn_readfirstlane((int32_t)(int64_t)(b - lo));
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = window_ld(t, len, b + 16 * (uintptr_t)(threadIdx.x + 64 * k));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+        for (int k = 0; k < 4; ++k) covt_walk_win[threadIdx.x + 64 * k] = v[k];
+        if (threadIdx.x == 0) covt_walk_win[kWin / 16] = make_uint4(0, 0, 0, 0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+    // the window holds bytes [i, i + n) (n <= 512); returns i's offset in it
+    __device__ __forceinline__ uint32_t ensure(int32_t i, uint32_t n) {
+        if ((uint32_t)(i - wo) > kWin - n) refill(i);
+        return (uint32_t)(i - wo);
+    }
+    // bytes [i, i + 8) (past the stream: unspecified, callers mask by len)
+    __device__ __forceinline__ uint64_t peek8(int32_t i) {
+        return win_bytes8(reinterpret_cast<const uint32_t*>(covt_walk_win), ensure(i, 8));
+    }
+    __device__ __forceinline__ int at(int32_t i) { return (int)(peek8(i) & 0xff); }
+};
+constexpr size_t kStreamRdLds = StreamRd::kWin + 16;
+
+// skips cnt LEB128 values from pos (false: the stream ends first): 64 bytes per step, a lane per byte
+__device__ __forceinline__ bool skip_varints(StreamRd& r, int32_t& pos, int32_t len, int32_t cnt) {
+    const int lane = threadIdx.x;
+    while (cnt > 0) {
+        if (pos >= len) return false;
+        const uint32_t off = r.ensure(pos, 64);
+        const uint8_t* w = (const uint8_t*)covt_walk_win + off;
+        const bool term = pos + lane < len && !(w[lane] & 0x80);
+        const uint64_t m = __ballot(term);
+        const int pc = __builtin_popcountll(m);
+        if (pc < cnt) {
+            if (len - pos <= 64) return false;
+            pos += 64;
+            cnt -= pc;
+            continue;
+        }
+        const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint64_t sel = __ballot(term && below == cnt - 1);
+        pos += __builtin_ctzll(sel) + 1;
+        return true;
+    }
+    return true;
+}
+
+// rle_chunks (covt_host.cpp) for one stream: its chunks {first byte, end byte, first value, values} into
+// rec[0, cap) (cap: the bound (cost / unit + 2)), the chunk count (0: not framed), the consumed bytes
+__device__ int32_t rle_walk(StreamRd& r, int32_t len, int op, int32_t n, int32_t elem, int64_t unit, int32_t& consumed,
+                            int4* rec, int64_t cap) {
+    const bool byte_rle = op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_BYTE_RLE_RAW;
+    int32_t pos = 0, v = 0, cs = 0, cv = 0, nch = 0;
+    auto chunk = [&](int32_t e, int32_t nvc) {
+        if (threadIdx.x == 0 && nch < cap) rec[nch] = make_int4(cs, e, cv, nvc);
+        ++nch;
+    };
+    while (v < n) {
+        if (pos >= len) return 0;
+        if ((int64_t)(pos - cs) + (int64_t)(v - cv) * elem / 4 >= unit) {  // cut before this group
+            chunk(pos, v - cv);
+            cs = pos;
+            cv = v;
+        }
+        const uint64_t w = r.peek8(pos);
+        const int32_t h = (int32_t)(w & 0xff);
+        if (h < 0x80) {
+            if (byte_rle) {
+                if (pos + 2 > len) return 0;
+                pos += 2;
+            } else {  // header, delta byte, base varint (ends within the word: one step)
+                const int32_t avail = len - pos;
+                uint64_t x = w | (avail < 8 ? 0x8080808080808080ull & (~0ull << (8 * (avail > 0 ? avail : 0))) : 0ull);
+                const uint64_t term = ~x & 0x8080808080808080ull & ~0xffffull;
+                if (pos + 2 > len) return 0;
+                if (term) {
+                    pos += (__builtin_ctzll(term) >> 3) + 1;
+                } else {
+                    pos += 2;
+                    if (!skip_varints(r, pos, len, 1)) return 0;
+                }
+            }
+            v += h + 3;
+        } else {
+            const int32_t cnt = 256 - h;
+            ++pos;
+            if (byte_rle) {
+                if (pos + cnt > len) return 0;
+                pos += cnt;
+            } else if (!skip_varints(r, pos, len, cnt)) {
+                return 0;
+            }
+            v += cnt;
+        }
+    }
+    chunk(pos, n - cv);
+    consumed = pos;
+    return nch;
+}
+
+// one wave per RLE candidate: a stream framed in >= 2 chunks becomes a split RLE stream, its chunk records
+// at rle_base[i] of the chunk scratch (cap records reserved per candidate) and its consumed bytes
+__global__ void rle_chunks_walk(const uint8_t* __restrict__ bytes, const covt_stream_info* __restrict__ info,
+                                const int32_t* __restrict__ nvals, unsigned long long* __restrict__ totals,
+                                const uint32_t* __restrict__ rle_list, int64_t unit, uint8_t* __restrict__ sfam,
+                                int64_t* __restrict__ sndesc, int4* __restrict__ chunks, int64_t chunk_cap,
+                                int64_t* __restrict__ rle_base, int32_t* __restrict__ rle_cons) {
+    const int64_t nl = (int64_t)totals[T_NRLE];
+    for (int64_t c = blockIdx.x; c < nl; c += gridDim.x) {
+        const uint32_t i = rle_list[c];
+        const covt_stream_info& si = info[i];
+        const int32_t nv = nvals[i];
+        const int64_t cap = ((int64_t)si.byte_length + (int64_t)nv * si.elem_bytes / 4) / unit + 2;
+        unsigned long long base = 0;
+        if (threadIdx.x == 0) base = atomicAdd(&totals[T_RCH], (unsigned long long)cap);
+        base = __shfl(base, 0, 64);
+        if ((int64_t)base + cap > chunk_cap) continue;  // (cannot happen: the host sized the scratch for every bound)
+        StreamRd r;
+        r.t = bytes + si.in_off;
+        r.len = si.byte_length;
+        r.wo = -0x40000000;
+        int32_t consumed = 0;
+        const int32_t nch = rle_walk(r, si.byte_length, si.op, nv, si.elem_bytes, unit, consumed, chunks + base, cap);
+        if (nch >= 2 && threadIdx.x == 0) {
+            sfam[i] = COVT_FAMILY_SPLIT_RLE;
+            sndesc[i] = (int64_t)nch * COVT_SPLIT_SLOTS;
+            rle_base[i] = (int64_t)base;
+            rle_cons[i] = consumed;
+        }
+    }
+}
+
+// descriptor counts in launch order (for their exclusive scan)
+__global__ void gather_ndesc(const uint32_t* __restrict__ order, const int64_t* __restrict__ sndesc, int64_t n,
+                             int64_t* __restrict__ dn) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) dn[k] = sndesc[order[k]];
+    if (k == n) dn[k] = 0;
+}
+
+// descriptor j: its stream (binary search of the launch-order offsets), then the stream's descriptor or the
+// chunk / pad j - dpos of a split varint or FastPFOR stream (FastPFOR states: fpf_states_walk; split RLE
+// streams: rle_chunks_walk<true>).  The first descriptor of a stream sets its desc_index.
+__global__ void fill_split_descs(covt_stream_info* __restrict__ info, const int32_t* __restrict__ nvals,
+                                 const uint32_t* __restrict__ order, const int64_t* __restrict__ dpos, int64_t ns,
+                                 int64_t n_desc, const uint8_t* __restrict__ sfam, int64_t split_chunk,
+                                 int64_t split_values, const int4* __restrict__ chunks, const int64_t* __restrict__ rle_base,
+                                 const int32_t* __restrict__ rle_cons, covt_stream_desc* __restrict__ desc,
+                                 uint32_t* __restrict__ dorder) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_desc) return;
+    int64_t lo = 0, hi = ns;  // the last k with dpos[k] <= j
+    while (hi - lo > 1) {
+        const int64_t m = (lo + hi) >> 1;
+        if (dpos[m] <= j) lo = m;
+        else hi = m;
+    }
+    const int64_t k = lo, q = j - dpos[k];
+    const uint32_t i = order[k];
+    dorder[j] = i;
+    covt_stream_info& si = info[i];
+    const int fam = sfam[i];
+    if (q == 0) si.desc_index = (int32_t)j;
+    covt_stream_desc d;
+    d.in_off = (uint64_t)si.in_off;
+    d.out_off = (uint64_t)si.out_off;
+    d.avail = si.byte_length;
+    d.num_values = nvals[i];
+    d.op = (uint8_t)si.op;
+    d.num_bits = (uint8_t)si.num_bits;
+    d.flags = fam == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
+    d.byte_length = si.byte_length;
+    if (fam != COVT_FAMILY_SPLIT && fam != COVT_FAMILY_SPLIT_FPF && fam != COVT_FAMILY_SPLIT_RLE) {
+        desc[j] = d;
+        return;
+    }
+    const int64_t c = q / COVT_SPLIT_SLOTS, slot = q % COVT_SPLIT_SLOTS;
+    if (fam == COVT_FAMILY_SPLIT_RLE) {  // the chunk records of rle_chunks_walk
+        covt_stream_desc x{};
+        if (slot == 0) {
+            x = d;
+            x.flags = COVT_DESC_SPLIT | COVT_DESC_SPLIT_RLE;
+            x.avail = (int32_t)c;
+        } else {
+            x.flags = COVT_DESC_SPLIT_PAD | COVT_DESC_SPLIT_RLE;
+            const int4 r = chunks[rle_base[i] + c];
+            if (slot == 1) x.in_off = (uint64_t)r.x, x.out_off = (uint64_t)r.y;
+            if (slot == 2) x.in_off = (uint64_t)r.z, x.out_off = (uint64_t)r.w;
+            if (slot == 3) x.in_off = (uint64_t)rle_cons[i];
+        }
+        desc[j] = x;
+        return;
+    }
+    const bool fpf = fam == COVT_FAMILY_SPLIT_FPF;
+    const uint16_t fflag = fpf ? COVT_DESC_SPLIT_FPF : 0;
+    if (slot == 0) {
+        d.flags = COVT_DESC_SPLIT | fflag;
+        d.avail = (int32_t)c;
+        desc[j] = d;
+        return;
+    }
+    covt_stream_desc pd{};
+    pd.flags = COVT_DESC_SPLIT_PAD | fflag;
+    if (slot == 1) {
+        const int64_t unit = fpf ? split_values : split_chunk, total = fpf ? (int64_t)d.num_values : (int64_t)d.byte_length;
+        pd.in_off = (uint64_t)(c * unit);
+        pd.out_off = (uint64_t)((c + 1) * unit < total ? (c + 1) * unit : total);
+    }
+    desc[j] = pd;
+}
+
+// fpf_chunk_states (covt_host.cpp) for each split FastPFOR stream, one wave each (lanes in lockstep; lane
+// k <= 32 holds the exception cursor of array k): the start state of every chunk the page / block header
+// walk reaches, in the chunk's pads [2..7] (state slot m: pad 2 + m / 7, field m % 7)
+__global__ void fpf_states_walk(const uint8_t* __restrict__ bytes, const covt_stream_info* __restrict__ info,
+                                const int32_t* __restrict__ nvals, const unsigned long long* __restrict__ totals,
+                                const uint32_t* __restrict__ fpf_list, int64_t unit, covt_stream_desc* __restrict__ desc) {
+    const int64_t nl = (int64_t)totals[T_NFPF];
+    const int lane = threadIdx.x;
+    for (int64_t li = blockIdx.x; li < nl; li += gridDim.x) {
+        const uint32_t i = fpf_list[li];
+        const covt_stream_info& si = info[i];
+        const int32_t n = nvals[i], byte_length = si.byte_length;
+        const int64_t nch = ((int64_t)n + unit - 1) / unit;
+        covt_stream_desc* out = desc + si.desc_index;
+        StreamRd r;
+        r.t = bytes + si.in_off;
+        r.len = byte_length;
+        r.wo = -0x40000000;
+        auto W = [&](int64_t w) -> uint32_t { return __builtin_bswap32((uint32_t)r.peek8((int32_t)(4 * w))); };
+        const int64_t nw = byte_length / 4;
+        if (nw <= 0 || unit % 256) continue;
+        int32_t L = (int32_t)W(0);
+        if (L < 0) continue;
+        L -= L % 256;
+        if (L > n) continue;
+        int64_t p = 1;
+        int32_t done = 0;
+        bool stop = false;
+        while (done < L && !stop) {
+            const int32_t thissize = L - done < 65536 ? L - done : 65536;
+            const int64_t p0 = p;
+            if (p0 >= nw) break;
+            int64_t ie = p0 + (int32_t)W(p0);
+            if (ie < 0 || ie >= nw) break;
+            const int32_t bytesize = (int32_t)W(ie++);
+            if (bytesize < 0 || bytesize > 3 * 65536 / 256 + 65536) break;
+            const int64_t bcw = (bytesize + 3) / 4, bc = ie;
+            if (bc + bcw >= nw) break;
+            ie += bcw;
+            uint32_t bm = W(ie++) & ~1u;
+            while (bm) {
+                const int32_t k = __builtin_ctz(bm) + 1;
+                bm &= bm - 1;
+                if (ie >= nw) {
+                    stop = true;
+                    break;
+                }
+                const int32_t size = (int32_t)W(ie++);
+                if (size < 0) {
+                    stop = true;
+                    break;
+                }
+                const int64_t groups = ((int64_t)size + 31) / 32;
+                ie += groups * k - ((groups * 32 - size) * k) / 32;
+            }
+            if (stop) break;
+            const int32_t bclen = (int32_t)(bcw * 4), nblk = thissize / 256;
+            // container bytes cur, cur + 1, cur + 2 (byte q at stream byte 4 bc + (q ^ 3)): one 8-byte read
+            // of the two words holding them
+            const int32_t cbase = (int32_t)(4 * bc);
+            int32_t cur = 0, xc = 0;  // xc: this lane's array cursor (lane k <= 32)
+            int64_t pk = p0 + 1;
+            // the next chunk start past the page's first block (a multiple of unit; no 64-bit division per block)
+            int64_t ci = ((int64_t)done + 256 + unit - 1) / unit, cut = ci * unit;
+            for (int32_t j = 0; j < nblk; ++j) {
+                const int64_t v = (int64_t)done + (int64_t)j * 256;
+                if (v == cut) {  // chunk ci starts at block j (> 0) of this page
+                    const bool own = ci < nch;
+                    covt_stream_desc* o = out + (size_t)ci * COVT_SPLIT_SLOTS;
+                    ++ci;
+                    cut += unit;
+                    const int32_t xv = __shfl(xc, lane >= 4 ? lane - 4 : 0, 64);
+                    const int32_t val = lane == 0 ? 1 : lane == 1 ? done : lane == 2 ? cur : lane == 3 ? (int32_t)pk : xv;
+                    if (own && lane < 37) *(int32_t*)((uint8_t*)(o + 2 + lane / 7) + covt_fpf_state_byte(lane % 7)) = val;
+                }
+                if (cur + 3 > bclen + 1) {
+                    stop = true;
+                    break;
+                }
+                const uint64_t x = r.peek8(cbase + 4 * (cur >> 2));
+                auto cb = [&](int32_t q) -> uint32_t {
+                    return (uint32_t)(x >> (8 * (4 * ((q >> 2) - (cur >> 2)) + ((q & 3) ^ 3)))) & 0xffu;
+                };
+                const int32_t hb = (int32_t)(int8_t)cb(cur), ce = (int32_t)cb(cur + 1);
+                const int32_t idx = ce > 0 && cur + 2 < bclen ? (int32_t)(int8_t)cb(cur + 2) - hb : 0;
+                pk += 8 * hb;
+                if (ce > 0 && idx >= 2 && idx <= 32 && lane == idx) xc += ce;
+                cur += ce > 0 ? 3 + ce : 2;
+                if (cur > bclen) {
+                    stop = true;
+                    break;
+                }
+            }
+            done += thissize;
+            p = ie;
+        }
+    }
 }
 
 size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1047,12 +1465,13 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     } while (0)
     DCHK(hipGetDevice(&p->dev));
     const size_t nt1 = (size_t)n_tiles + 1;
-    // tile arena: status | cnt | ob | cnt_base | ob_base | totals | per-tile sums | scan scratch | slots
+    // tile arena: status | cnt | ob | cnt_base | ob_base | totals | head | per-tile sums | per-tile costs |
+    // scan scratch | slots
     size_t scan_tmp = 0;
     DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)nt1, s));
     const size_t o_cnt = up256(nt1 * 4), o_ob = o_cnt + up256(nt1 * 8), o_cb = o_ob + up256(nt1 * 8),
-                 o_obb = o_cb + up256(nt1 * 8), o_tot = o_obb + up256(nt1 * 8), o_ts = o_tot + up256(T_N * 8),
-                 o_tmp = o_ts + up256(nt1 * 32),
+                 o_obb = o_cb + up256(nt1 * 8), o_tot = o_obb + up256(nt1 * 8), o_head = o_tot + up256(T_N * 8),
+                 o_ts = o_head + 256, o_tc = o_ts + up256(nt1 * 32), o_tmp = o_tc + up256(nt1 * 16),
                  o_slots = o_tmp + up256(scan_tmp);
     // device_walk 0: a wave per tile with per-tile slots; 1: the same walk twice; k >= 2: k lanes per workgroup
     const int wl = o.device_walk >= 2 ? o.device_walk : 0;
@@ -1062,38 +1481,55 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     uint8_t* ta = (uint8_t*)p->tile_arena;
     p->d_status = (int32_t*)ta;
     int64_t *cnt = (int64_t*)(ta + o_cnt), *ob = (int64_t*)(ta + o_ob), *cb = (int64_t*)(ta + o_cb),
-            *obb = (int64_t*)(ta + o_obb);
+            *obb = (int64_t*)(ta + o_obb), *head = (int64_t*)(ta + o_head), *tcost = (int64_t*)(ta + o_tc);
     auto* totals = (unsigned long long*)(ta + o_tot);
     auto* tsum = (long long*)(ta + o_ts);
     DCHK(hipMemsetAsync(totals, 0, T_N * 8, s));
     DCHK(hipMemsetAsync(tsum, 0, nt1 * 32, s));  // failed tiles leave zeros
+    const int64_t fpf_w = o.fpf_split_weight;
     // 0: a wave per tile, its lanes in lockstep; k > 0: k lanes per workgroup, a lane per tile
     RawStream* slots = use_slots ? (RawStream*)(ta + o_slots) : nullptr;
     if (wl == 0)
         walk_count<true><<<(int)nt1, 64, kWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
-                                                  id_mode, p->d_status, cnt, ob, slots);
+                                                        id_mode, p->d_status, cnt, ob, slots, fpf_w, tcost);
     else
-        walk_count<false><<<(int)((nt1 + wl - 1) / wl), wl, (size_t)wl * 64, s>>>(
-            d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cnt, ob, nullptr);
+        walk_count<false><<<(int)((nt1 + wl - 1) / wl), wl, (size_t)wl * 64 + 16, s>>>(
+            d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cnt, ob, nullptr,
+            fpf_w, tcost);
     DCHK(hipGetLastError());
     DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, cnt, cb, (int)nt1, s));
     DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, ob, obb, (int)nt1, s));
-    int64_t tot2[2];
-    DCHK(hipMemcpyAsync(&tot2[0], cb + n_tiles, 8, hipMemcpyDeviceToHost, s));
-    DCHK(hipMemcpyAsync(&tot2[1], obb + n_tiles, 8, hipMemcpyDeviceToHost, s));
+    plan_head<<<1, 1024, 0, s>>>(cb, obb, tcost, n_tiles, head);
+    DCHK(hipGetLastError());
+    int64_t hd[4];
+    DCHK(hipMemcpyAsync(hd, head, sizeof(hd), hipMemcpyDeviceToHost, s));
     DCHK(hipStreamSynchronize(s));
-    const int64_t ns = tot2[0];
+    const int64_t ns = hd[0];
     p->n_streams = ns;
-    p->out_bytes = tot2[1];
+    p->n_descs = ns;
+    p->out_bytes = hd[1];
     if (ns > 0x7fffffff) return fail(COVT_ERR_INVALID_ARG);
-    // stream arena: info | nvals | keys in/out | vals in/out | descs | sort scratch
-    size_t sort_tmp = 0;
+    // the split threshold (covt_plan_create_ex step 3): nothing splits unless the largest cost passes it
+    int64_t smin = o.split_min;
+    if (smin >= 0 && o.split_ratio > 0) smin = std::max<int64_t>(smin, hd[2] / o.split_ratio);
+    const bool splitting = smin >= 0 && ns > 0 && hd[3] > smin;
+    // stream arena: info | nvals | keys in/out | vals in/out | descs | sort scratch [| split: family | desc
+    // counts | offsets | RLE list | FastPFOR list | scan scratch]
+    size_t sort_tmp = 0, dscan_tmp = 0;
     DCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint64_t*)nullptr, (uint64_t*)nullptr,
                                             (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ns, 0, 63, s));
+    if (splitting)
+        DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, dscan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)(ns + 1), s));
     const size_t n = (size_t)(ns > 0 ? ns : 1);
+    // RLE chunk records: every candidate reserves (its cost / split_chunk + 2) <= the batch's
+    const int64_t chunk_cap = splitting ? hd[2] / o.split_chunk + 2 * ns + 2 : 0;
     const size_t o_nv = up256(n * sizeof(covt_stream_info)), o_k0 = o_nv + up256(n * 4), o_k1 = o_k0 + up256(n * 8),
                  o_v0 = o_k1 + up256(n * 8), o_v1 = o_v0 + up256(n * 4), o_d = o_v1 + up256(n * 4),
-                 o_st = o_d + up256(n * sizeof(covt_stream_desc)), stream_bytes = o_st + up256(sort_tmp);
+                 o_st = o_d + up256(n * sizeof(covt_stream_desc)), o_sf = o_st + up256(sort_tmp),
+                 o_sn = o_sf + up256(n), o_dn = o_sn + up256(n * 8), o_dp = o_dn + up256((n + 1) * 8),
+                 o_rl = o_dp + up256((n + 1) * 8), o_fl = o_rl + up256(n * 4), o_rb = o_fl + up256(n * 4),
+                 o_rc = o_rb + up256(n * 8), o_ch = o_rc + up256(n * 4), o_ds = o_ch + up256((size_t)chunk_cap * 16),
+                 stream_bytes = splitting ? o_ds + up256(dscan_tmp) : o_sf;
     DCHK(hipMalloc(&p->stream_arena, stream_bytes));
     uint8_t* sa = (uint8_t*)p->stream_arena;
     p->d_info = (covt_stream_info*)sa;
@@ -1112,22 +1548,56 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         }
         if (wl == 0)  // (with slots: only tiles with more than kSlots streams walk again)
             walk_emit<true><<<n_tiles, 64, kWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
-                                                    id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, tsum,
-                                                    slots ? cnt : nullptr);
+                                                          id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, tsum,
+                                                          slots ? cnt : nullptr);
         else
-            walk_emit<false><<<(n_tiles + wl - 1) / wl, wl, (size_t)wl * 64, s>>>(
+            walk_emit<false><<<(n_tiles + wl - 1) / wl, wl, (size_t)wl * 64 + 16, s>>>(
                 d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cb, obb,
                 lane_max, p->d_info, nvals, tsum, nullptr);
         DCHK(hipGetLastError());
         reduce_tiles<<<1, 1024, 0, s>>>(tsum, n_tiles, totals);
         DCHK(hipGetLastError());
     }
-    if (ns > 0) {
-        const int blocks_s = (int)((ns + 255) / 256);
-        stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, k0, v0);
+    const int blocks_s = (int)((ns + 255) / 256);
+    if (ns > 0 && !splitting) {
+        stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, k0, v0, nullptr, nullptr);
         DCHK(hipGetLastError());
         DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, k0, k1, v0, v1, (int)ns, 0, 63, s));
         fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, k1, v1, ns, p->d_desc);
+        DCHK(hipGetLastError());
+    } else if (splitting) {
+        auto* sfam = (uint8_t*)(sa + o_sf);
+        auto *sndesc = (int64_t*)(sa + o_sn), *dn = (int64_t*)(sa + o_dn), *dpos = (int64_t*)(sa + o_dp);
+        auto *rle_list = (uint32_t*)(sa + o_rl), *fpf_list = (uint32_t*)(sa + o_fl);
+        const int walkers = (int)std::min<int64_t>(ns, 1024);
+        split_mark<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, smin, o.split_chunk,
+                                            o.split_values, fpf_w, totals, sfam, sndesc, rle_list, fpf_list);
+        DCHK(hipGetLastError());
+        auto* chunks = (int4*)(sa + o_ch);
+        auto* rle_base = (int64_t*)(sa + o_rb);
+        auto* rle_cons = (int32_t*)(sa + o_rc);
+        rle_chunks_walk<<<walkers, 64, kStreamRdLds, s>>>(d_bytes, p->d_info, nvals, totals, rle_list, o.split_chunk, sfam,
+                                                 sndesc, chunks, chunk_cap, rle_base, rle_cons);
+        DCHK(hipGetLastError());
+        stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, k0, v0, sfam, sndesc);
+        DCHK(hipGetLastError());
+        DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, k0, k1, v0, v1, (int)ns, 0, 63, s));
+        gather_ndesc<<<(int)((ns + 256) / 256), 256, 0, s>>>(v1, sndesc, ns, dn);
+        DCHK(hipGetLastError());
+        DCHK(hipcub::DeviceScan::ExclusiveSum(sa + o_ds, dscan_tmp, dn, dpos, (int)(ns + 1), s));
+        int64_t nd = 0;
+        DCHK(hipMemcpyAsync(&nd, dpos + ns, 8, hipMemcpyDeviceToHost, s));
+        DCHK(hipStreamSynchronize(s));
+        // descriptor arena: descriptors | the stream of each
+        DCHK(hipMalloc(&p->desc_arena, up256((size_t)nd * sizeof(covt_stream_desc)) + up256((size_t)nd * 4)));
+        p->n_descs = nd;
+        p->d_desc = (covt_stream_desc*)p->desc_arena;
+        p->d_order = (uint32_t*)((uint8_t*)p->desc_arena + up256((size_t)nd * sizeof(covt_stream_desc)));
+        fill_split_descs<<<(int)((nd + 255) / 256), 256, 0, s>>>(p->d_info, nvals, v1, dpos, ns, nd, sfam, o.split_chunk,
+                                                                 o.split_values, chunks, rle_base, rle_cons, p->d_desc,
+                                                                 p->d_order);
+        DCHK(hipGetLastError());
+        fpf_states_walk<<<walkers, 64, kStreamRdLds, s>>>(d_bytes, p->d_info, nvals, totals, fpf_list, o.split_values, p->d_desc);
         DCHK(hipGetLastError());
     }
     unsigned long long tot[T_N];
@@ -1148,11 +1618,13 @@ void covt_device_plan_destroy(covt_device_plan* p) {
     const bool sw = hipGetDevice(&cur) == hipSuccess && cur != p->dev && hipSetDevice(p->dev) == hipSuccess;
     if (p->tile_arena) (void)hipFree(p->tile_arena);
     if (p->stream_arena) (void)hipFree(p->stream_arena);
+    if (p->desc_arena) (void)hipFree(p->desc_arena);
     if (sw) (void)hipSetDevice(cur);
     delete p;
 }
 
 int64_t covt_device_plan_num_streams(const covt_device_plan* p) { return p ? p->n_streams : 0; }
+int64_t covt_device_plan_num_descs(const covt_device_plan* p) { return p ? p->n_descs : 0; }
 int64_t covt_device_plan_output_bytes(const covt_device_plan* p) { return p ? p->out_bytes : 0; }
 
 int covt_device_plan_totals(const covt_device_plan* p, int64_t* in_bytes, int64_t* out_bytes, int64_t* vertices) {
@@ -1177,10 +1649,10 @@ const uint32_t* covt_device_plan_order_device(const covt_device_plan* p) { retur
 int covt_device_plan_copy(const covt_device_plan* p, covt_stream_info* streams, covt_stream_desc* descs,
                           int32_t* tile_status) {
     if (!p) return COVT_ERR_INVALID_ARG;
-    const size_t ns = (size_t)p->n_streams;
+    const size_t ns = (size_t)p->n_streams, nd = (size_t)p->n_descs;
     if (streams && ns && hipMemcpy(streams, p->d_info, ns * sizeof(covt_stream_info), hipMemcpyDeviceToHost) != hipSuccess)
         return COVT_ERR_DEVICE;
-    if (descs && ns && hipMemcpy(descs, p->d_desc, ns * sizeof(covt_stream_desc), hipMemcpyDeviceToHost) != hipSuccess)
+    if (descs && nd && hipMemcpy(descs, p->d_desc, nd * sizeof(covt_stream_desc), hipMemcpyDeviceToHost) != hipSuccess)
         return COVT_ERR_DEVICE;
     if (tile_status && p->n_tiles &&
         hipMemcpy(tile_status, p->d_status, (size_t)p->n_tiles * 4, hipMemcpyDeviceToHost) != hipSuccess)
@@ -1190,7 +1662,7 @@ int covt_device_plan_copy(const covt_device_plan* p, covt_stream_info* streams, 
 
 int covt_device_plan_decode(const covt_device_plan* p, const uint8_t* d_in, uint8_t* d_out, covt_stream_result* d_res,
                             void* hip_stream) {
-    if (!p || (p->n_streams && (!d_in || !d_res || (p->out_bytes && !d_out)))) return COVT_ERR_INVALID_ARG;
+    if (!p || (p->n_descs && (!d_in || !d_res || (p->out_bytes && !d_out)))) return COVT_ERR_INVALID_ARG;
     return covt_decode_streams_device_grouped(d_in, p->d_desc, p->fam_counts, d_out, d_res, hip_stream);
 }
 

@@ -451,9 +451,11 @@ int covt_plan_properties_host(const covt_plan* plan, const uint8_t* bytes, uint6
  * n_tiles uint64 each, on the device (a tile outside [0, n_bytes) gets COVT_ERR_INVALID_ARG as its
  * status).  The result is the host plan's layout exactly: streams in tile order with the same
  * covt_stream_info fields and 16-byte aligned output slices, descriptors in the same launch order
- * and families.  Long streams are not split into chunks (covt_plan_create splits only the long poles
- * of small batches).  Property columns, geometry assembly and multi-GPU shards stay with the host
- * plan.  Runs on `hip_stream` and synchronises it twice (the stream count sizes the arrays).
+ * and families, including the split rule: with the same options, the long poles of a small batch are
+ * cut into the same chunks (varint byte chunks, FastPFOR value chunks with their start states, ORC RLE
+ * group chunks).  Property columns, geometry assembly and multi-GPU shards stay with the host plan.
+ * Runs on `hip_stream` and synchronises it twice (three times when it splits: the stream count and
+ * the descriptor count size the arrays).
  * Limits and memory: a tile of 0x7ff00000 bytes or more gets COVT_ERR_INVALID_ARG as its status
  * (32-bit cursors; the host plan walks such tiles); besides the stream arrays the plan holds ~5 KiB
  * of per-tile walk slots on the device (128 stream records of 40 bytes per tile: ~0.5 GB at 100k
@@ -467,12 +469,14 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
                                  const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                                  const covt_plan_options* opts, void* hip_stream, covt_device_plan** out);
 void covt_device_plan_destroy(covt_device_plan* plan);
-int64_t covt_device_plan_num_streams(const covt_device_plan* plan); /* = its descriptors */
+int64_t covt_device_plan_num_streams(const covt_device_plan* plan);
+int64_t covt_device_plan_num_descs(const covt_device_plan* plan); /* = num_streams unless it splits */
 int64_t covt_device_plan_output_bytes(const covt_device_plan* plan);
 int covt_device_plan_totals(const covt_device_plan* plan, int64_t* in_bytes, int64_t* out_bytes, int64_t* vertices);
 int covt_device_plan_family_counts(const covt_device_plan* plan, int64_t counts[COVT_NUM_FAMILIES]);
-/* device arrays owned by the plan: num_streams descriptors (launch order), stream records (tile
- * order, desc_index set), n_tiles statuses, and the stream index of each descriptor */
+/* device arrays owned by the plan: num_descs descriptors (launch order), num_streams stream records
+ * (tile order, desc_index = the stream's first descriptor), n_tiles statuses, and the stream index of
+ * each descriptor (num_descs) */
 const covt_stream_desc* covt_device_plan_descs_device(const covt_device_plan* plan);
 const covt_stream_info* covt_device_plan_streams_device(const covt_device_plan* plan);
 const int32_t* covt_device_plan_tile_status_device(const covt_device_plan* plan);
@@ -481,7 +485,8 @@ const uint32_t* covt_device_plan_order_device(const covt_device_plan* plan);
 int covt_device_plan_copy(const covt_device_plan* plan, covt_stream_info* streams, covt_stream_desc* descs,
                           int32_t* tile_status);
 /* the grouped decode launch over the plan's descriptors (covt_decode_streams_device_grouped):
- * d_out covt_device_plan_output_bytes bytes, d_res num_streams results.  Asynchronous. */
+ * d_out covt_device_plan_output_bytes bytes, d_res num_descs results (stream i's at its desc_index).
+ * Asynchronous. */
 int covt_device_plan_decode(const covt_device_plan* plan, const uint8_t* d_in, uint8_t* d_out,
                             covt_stream_result* d_res, void* hip_stream);
 

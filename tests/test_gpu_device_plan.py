@@ -4,8 +4,10 @@ test_gpu_parity.py): the GPU's walk of the container metadata (CovtParser.decode
 CovtParser.java:53-133; decodeLayerMetadata :574-652) must give the host plan's stream records,
 tile statuses, output layout, launch order and family counts byte for byte, on Gen C fixtures, Gen D
 conversions, malformed tiles and the full BASELINE config-5 batch -- and decoding through it must give
-the host plan's outputs.  Both plans are made with the same covt_plan_options; splitting is off
-(split_min = -1) where the device plan does not split."""
+the host plan's outputs.  Both plans are made with the same covt_plan_options: splitting off
+(split_min = -1) for the walk tests, and on (the defaults, and forced small chunks) for the split rule,
+where decoding through the device plan is also checked against the golden oracle digests."""
+import hashlib
 
 import numpy as np
 import pytest
@@ -32,7 +34,7 @@ def _device_plan(covt, hp, fmt, id_mode):
 def _assert_same_plan(hp, dp):
     info, descs, st = dp.host_copy()
     assert np.array_equal(st, hp.tile_status)
-    assert dp.num_streams == hp.num_streams == hp.num_descs
+    assert dp.num_streams == hp.num_streams and dp.num_descs == hp.num_descs
     assert dp.output_bytes == hp.output_bytes
     assert (dp.in_bytes, dp.out_payload, dp.vertices) == (hp.in_bytes, hp.out_bytes, hp.vertices)
     assert np.array_equal(dp.family_counts, hp.family_counts)
@@ -47,7 +49,7 @@ def _assert_same_decode(covt, hp, dp):
     dp.decode(d_out, d_res)
     torch.cuda.synchronize()
     out = d_out.cpu().numpy()[:dp.output_bytes]
-    res = d_res.cpu().numpy().reshape(-1, 2)[:dp.num_streams][hp.streams["desc_index"]]
+    res = d_res.cpu().numpy().reshape(-1, 2)[:dp.num_descs][hp.streams["desc_index"]]
     h_out, h_res = hp.decode_host()
     assert np.array_equal(res, h_res)
     for i in range(hp.num_streams):
@@ -194,5 +196,91 @@ def test_tiles_past_slot_capacity(covt, gpu_available, decodable_tiles, walk, fm
     per_tile = np.bincount(hp.streams["tile"], minlength=len(tiles))
     assert per_tile.max() > 128 and (hp.tile_status == 0).all()
     dp = _device_plan(covt, hp, fmt, 0)
+    _assert_same_plan(hp, dp)
+    _assert_same_decode(covt, hp, dp)
+
+
+def _assert_golden(covt, hp, dp, keys, golden_streams):
+    """Decode through the device plan; every stream's status, consumed bytes and output SHA-256 equal
+    the oracle's digests of its tile (tests/golden/oracle_streams.json)."""
+    import torch
+
+    d_out, d_res = dp.alloc()
+    for _ in range(2):  # the split look-back records are reset per launch
+        dp.decode(d_out, d_res)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()[:dp.output_bytes]
+    res = d_res.cpu().numpy().reshape(-1, 2)[:dp.num_descs][hp.streams["desc_index"]]
+    col = golden_streams["columns"]
+    ish, ist, ico = col.index("fmt_sha256"), col.index("fmt_status"), col.index("fmt_consumed")
+    st = hp.streams
+    checked = 0
+    for t, key in enumerate(keys):
+        rows = golden_streams["tiles"][key]["streams"]
+        idx = np.nonzero(st["tile"] == t)[0]
+        assert len(idx) == len(rows), key
+        for i, row in zip(idx, rows):
+            assert int(res[i][0]) == row[ist] and int(res[i][1]) == row[ico], (key, int(i))
+            if row[ist] == 0:
+                assert hashlib.sha256(hp.stream_array(out, int(i)).tobytes()).hexdigest() == row[ish], (key, int(i))
+            checked += 1
+    assert checked == hp.num_streams
+
+
+@pytest.mark.parametrize("n_tiles", [1, 3, 12])
+def test_split_default_options(covt, gpu_available, decodable_tiles, golden_streams, n_tiles):
+    """Small batches with the default options split their long poles (varint, FastPFOR and RLE chunks):
+    the device plan cuts the same chunks (FastPFOR start states included) and decodes to the digests."""
+    omt = [(k, t) for k, t in decodable_tiles if k.startswith("omt/")]
+    picks = sorted(omt, key=lambda kt: -len(kt[1]))[:n_tiles]
+    keys, tiles = [k for k, _ in picks], [t for _, t in picks]
+    hp = _host_plan(covt, tiles, covt.FORMAT_GENC, 0, split=True)
+    fc = hp.family_counts
+    assert hp.num_descs > hp.num_streams and fc[covt.FAMILY_SPLIT:].sum() > 0
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
+    _assert_same_plan(hp, dp)
+    _assert_golden(covt, hp, dp, keys, golden_streams)
+
+
+@pytest.mark.parametrize("kw", [dict(split_min=0, split_ratio=0, split_chunk=64, split_values=256),
+                                dict(split_min=512, split_ratio=0, split_chunk=300, split_values=512,
+                                     fpf_split_weight=3),
+                                dict(split_min=0, split_ratio=0, split_chunk=64, split_values=256,
+                                     lane_min_streams=0)],
+                         ids=["tiny_chunks", "weighted", "lane_and_split"])
+def test_split_forced(covt, gpu_available, decodable_tiles, golden_streams, kw):
+    """Forced small chunks over a mixed batch: every family splits (all three split families present),
+    lane streams beside split ones; the same plan and the golden digests."""
+    picks = decodable_tiles[::4][:24]
+    keys, tiles = [k for k, _ in picks], [t for _, t in picks]
+    id_mode = 1 if "lane_min_streams" in kw else 0
+    hp = _host_plan(covt, tiles, covt.FORMAT_GENC, id_mode, split=True, **kw)
+    fc = hp.family_counts
+    assert (fc[covt.FAMILY_SPLIT:] > 0).all(), fc
+    if "lane_min_streams" in kw:
+        assert fc[covt.FAMILY_LANE] > 0, fc
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, id_mode)
+    _assert_same_plan(hp, dp)
+    if id_mode == 0:
+        _assert_golden(covt, hp, dp, keys, golden_streams)
+    else:
+        _assert_same_decode(covt, hp, dp)
+
+
+def test_split_malformed_streams(covt, gpu_available, decodable_tiles):
+    """Split candidates whose payload bytes are corrupted (metadata intact): the RLE group walk and the
+    FastPFOR header walk stop where the host's do -- unframed RLE streams stay whole, FastPFOR chunks
+    past the break get no start state -- and decoding reports the host plan's statuses."""
+    rng = np.random.default_rng(5)
+    tiles = []
+    for k, t in decodable_tiles[:30]:
+        b = bytearray(t)
+        for _ in range(40):  # flips across the tile: mostly stream payloads
+            b[int(rng.integers(len(b) // 4, len(b)))] ^= 1 << int(rng.integers(0, 8))
+        tiles.append(bytes(b))
+    hp = _host_plan(covt, tiles, covt.FORMAT_GENC, 0, split=True, split_min=0, split_ratio=0, split_chunk=64,
+                    split_values=256)
+    assert hp.num_descs > hp.num_streams
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
     _assert_same_plan(hp, dp)
     _assert_same_decode(covt, hp, dp)

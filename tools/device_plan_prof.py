@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Profiling target: covt_device_plan_create on the bench batch (BASELINE config 5) N times, wall-clock per
 creation printed (run under rocprofv3 --kernel-trace --stats [--hip-trace] for the per-kernel / per-call
-breakdown).  usage: device_plan_prof.py [reps] [--sweep]
+breakdown).  usage: device_plan_prof.py [reps] [--sweep | --small]
 --sweep: also batches of 1 tile (the library's largest), 256, 2048 and 4096 tiles (latency vs. occupancy)."""
 import os
 import sys
@@ -25,6 +25,9 @@ def main():
         for n in (1, 256, 2048, 4096):
             tiles = [big] if n == 1 else [t for _, t in bench.sample_batch(lib, n, bench.SEED)]
             run(covt, tiles, reps, "%5d tiles" % n)
+    if "--small" in sys.argv:  # the single largest tile only (a split plan)
+        run(covt, [max((t for z in lib.values() for _, t in z), key=len)], reps, "    1 tiles")
+        return
     picks = bench.sample_batch(lib, 10000, bench.SEED)
     run(covt, [t for _, t in picks], reps, "10000 tiles")
 

@@ -68,6 +68,7 @@ for s in "$@"; do
     dplan_var) for v in ${AB_VARIANTS:-libcovt.so}; do
             COVT_LIB_VARIANT=$v timeout -k 10 200 python tools/device_plan_prof.py 20 --sweep 2>&1 | grep -v amdgpu.ids || fatal dplan_var $?
         done ;;
+    dplan_prof_small) step dplan_prof_small 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_prof_small -o run --output-format csv -- python tools/device_plan_prof.py 5 --small ;;
     dplan_prof) step dplan_prof 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_prof -o run --output-format csv -- python tools/device_plan_prof.py 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
