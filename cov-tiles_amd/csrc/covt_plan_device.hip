@@ -1023,11 +1023,17 @@ __global__ void __launch_bounds__(1024) reduce_tiles(const long long* __restrict
     }
 }
 
-// launch-order key of covt_plan_create_ex step 3 (no splits): family, lane op, cost descending
-// (split plans: the family and descriptor count of each stream from split_mark / rle_chunks_walk)
+// launch-order key of covt_plan_create_ex step 3: family, lane op, cost descending
+// (split plans: the family and descriptor count of each stream from split_mark / rle_chunks_walk).
+// Packed into cb + 8 bits (family << (cb + 5) | lane op << cb | 2^cb - 1 - cost) where every stream's
+// cost is below 2^cb: the host plan's order exactly (its 64-bit key orders the same fields the same
+// way), in 32-bit keys and cb + 8 sort bits when they fit (the bench batch: 26 bits, 4 radix passes
+// instead of 8 over 64-bit keys)
+static_assert(COVT_OP_COUNT <= 32, "the lane op takes 5 key bits");
+template <class K>
 __global__ void stream_keys(const covt_stream_info* info, const int32_t* nvals, int64_t n, int32_t lane_max,
-                            int64_t lane_min, unsigned long long* totals, uint64_t* keys, uint32_t* vals,
-                            const uint8_t* sfam, const int64_t* sndesc) {
+                            int64_t lane_min, unsigned long long* totals, K* keys, uint32_t* vals,
+                            const uint8_t* sfam, const int64_t* sndesc, int cb) {
     __shared__ unsigned long long fam_n[COVT_NUM_FAMILIES];
     if (threadIdx.x < COVT_NUM_FAMILIES) fam_n[threadIdx.x] = 0;
     __syncthreads();
@@ -1037,9 +1043,10 @@ __global__ void stream_keys(const covt_stream_info* info, const int32_t* nvals, 
         const int32_t lm = (int64_t)totals[T_LANE] < lane_min ? -1 : lane_max;
         const bool lane = lane_stream(s.op, nvals[i], s.byte_length, lm);
         const uint64_t fam = sfam ? (uint64_t)sfam[i] : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family(s.op);
+        const uint64_t cmax = (1ull << cb) - 1;
         const int64_t c = (int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4;
-        const uint64_t cost = c < ((1ll << 48) - 1) ? (uint64_t)c : (1ull << 48) - 1;
-        keys[i] = (fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost);
+        const uint64_t cost = (uint64_t)c < cmax ? (uint64_t)c : cmax;
+        keys[i] = (K)((fam << (cb + 5)) | ((lane ? (uint64_t)s.op : 0ull) << cb) | (cmax - cost));
         vals[i] = (uint32_t)i;
         atomicAdd(&fam_n[fam], sndesc ? (unsigned long long)sndesc[i] : 1ull);
     }
@@ -1048,8 +1055,9 @@ __global__ void stream_keys(const covt_stream_info* info, const int32_t* nvals, 
         atomicAdd(&totals[T_FAM + threadIdx.x], fam_n[threadIdx.x]);
 }
 
-__global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const uint64_t* keys, const uint32_t* order,
-                           int64_t n, covt_stream_desc* desc) {
+template <class K>
+__global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const K* keys, const uint32_t* order,
+                           int64_t n, int cb, covt_stream_desc* desc) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const uint32_t i = order[k];
@@ -1061,7 +1069,7 @@ __global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const u
     d.num_values = nvals[i];
     d.op = (uint8_t)si.op;
     d.num_bits = (uint8_t)si.num_bits;
-    d.flags = (keys[k] >> 60) == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
+    d.flags = ((uint64_t)keys[k] >> (cb + 5)) == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
     d.byte_length = si.byte_length;
     desc[k] = d;
     si.desc_index = (int32_t)k;
@@ -1515,9 +1523,19 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     const bool splitting = smin >= 0 && ns > 0 && hd[3] > smin;
     // stream arena: info | nvals | keys in/out | vals in/out | descs | sort scratch [| split: family | desc
     // counts | offsets | RLE list | FastPFOR list | scan scratch]
+    // sort keys: cost bits kcb (every stream's cost <= the largest split cost hd[3] < 2^kcb; 48 as the
+    // host plan's key at most), 32-bit keys when cb + 8 bits fit
+    int kcb = 1;
+    while (kcb < 48 && (hd[3] >> kcb) != 0) ++kcb;
+    const bool k32 = kcb + 8 <= 32;
+    const int kbits = kcb + 8;
     size_t sort_tmp = 0, dscan_tmp = 0;
-    DCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint64_t*)nullptr, (uint64_t*)nullptr,
-                                            (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ns, 0, 63, s));
+    if (k32)
+        DCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ns, 0, kbits, s));
+    else
+        DCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ns, 0, kbits, s));
     if (splitting)
         DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, dscan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)(ns + 1), s));
     const size_t n = (size_t)(ns > 0 ? ns : 1);
@@ -1535,6 +1553,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     p->d_info = (covt_stream_info*)sa;
     int32_t* nvals = (int32_t*)(sa + o_nv);
     uint64_t *k0 = (uint64_t*)(sa + o_k0), *k1 = (uint64_t*)(sa + o_k1);
+    uint32_t *q0 = (uint32_t*)k0, *q1 = (uint32_t*)k1;  // (32-bit keys)
     uint32_t *v0 = (uint32_t*)(sa + o_v0), *v1 = (uint32_t*)(sa + o_v1);
     p->d_order = v1;
     p->d_desc = (covt_stream_desc*)(sa + o_d);
@@ -1560,10 +1579,19 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     }
     const int blocks_s = (int)((ns + 255) / 256);
     if (ns > 0 && !splitting) {
-        stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, k0, v0, nullptr, nullptr);
-        DCHK(hipGetLastError());
-        DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, k0, k1, v0, v1, (int)ns, 0, 63, s));
-        fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, k1, v1, ns, p->d_desc);
+        if (k32) {
+            stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, q0, v0, nullptr,
+                                                 nullptr, kcb);
+            DCHK(hipGetLastError());
+            DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, q0, q1, v0, v1, (int)ns, 0, kbits, s));
+            fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, q1, v1, ns, kcb, p->d_desc);
+        } else {
+            stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, k0, v0, nullptr,
+                                                 nullptr, kcb);
+            DCHK(hipGetLastError());
+            DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, k0, k1, v0, v1, (int)ns, 0, kbits, s));
+            fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, k1, v1, ns, kcb, p->d_desc);
+        }
         DCHK(hipGetLastError());
     } else if (splitting) {
         auto* sfam = (uint8_t*)(sa + o_sf);
@@ -1579,9 +1607,15 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         rle_chunks_walk<<<walkers, 64, kStreamRdLds, s>>>(d_bytes, p->d_info, nvals, totals, rle_list, o.split_chunk, sfam,
                                                  sndesc, chunks, chunk_cap, rle_base, rle_cons);
         DCHK(hipGetLastError());
-        stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, k0, v0, sfam, sndesc);
-        DCHK(hipGetLastError());
-        DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, k0, k1, v0, v1, (int)ns, 0, 63, s));
+        if (k32) {
+            stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, q0, v0, sfam, sndesc, kcb);
+            DCHK(hipGetLastError());
+            DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, q0, q1, v0, v1, (int)ns, 0, kbits, s));
+        } else {
+            stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, k0, v0, sfam, sndesc, kcb);
+            DCHK(hipGetLastError());
+            DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, k0, k1, v0, v1, (int)ns, 0, kbits, s));
+        }
         gather_ndesc<<<(int)((ns + 256) / 256), 256, 0, s>>>(v1, sndesc, ns, dn);
         DCHK(hipGetLastError());
         DCHK(hipcub::DeviceScan::ExclusiveSum(sa + o_ds, dscan_tmp, dn, dpos, (int)(ns + 1), s));

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Profiling target: covt_device_plan_create on the bench batch (BASELINE config 5) N times, wall-clock per
 creation printed (run under rocprofv3 --kernel-trace --stats [--hip-trace] for the per-kernel / per-call
-breakdown).  usage: device_plan_prof.py [reps] [--sweep | --small]
+breakdown).  usage: device_plan_prof.py [reps] [--sweep | --small | --n256] [--nosplit] [--sorted]
 --sweep: also batches of 1 tile (the library's largest), 256, 2048 and 4096 tiles (latency vs. occupancy)."""
 import os
 import sys
@@ -28,8 +28,13 @@ def main():
     if "--small" in sys.argv:  # the single largest tile only (a split plan)
         run(covt, [max((t for z in lib.values() for _, t in z), key=len)], reps, "    1 tiles")
         return
+    if "--n256" in sys.argv:  # 256 sampled tiles (a split plan)
+        run(covt, [t for _, t in bench.sample_batch(lib, 256, bench.SEED)], reps, "  256 tiles")
+        return
     picks = bench.sample_batch(lib, 10000, bench.SEED)
     run(covt, [t for _, t in picks], reps, "10000 tiles")
+    if "--sorted" in sys.argv:  # the same batch, largest tiles first (walk launch order experiment)
+        run(covt, sorted((t for _, t in picks), key=len, reverse=True), reps, "10000 tiles, largest first")
 
 
 def run(covt, tiles, reps, label):
@@ -43,7 +48,7 @@ def run(covt, tiles, reps, label):
     for _ in range(reps + 2):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        dp = covt.DevicePlan(d_blob, d_off, d_size)
+        dp = covt.DevicePlan(d_blob, d_off, d_size, options=covt.PlanOptions(split_min=-1) if "--nosplit" in sys.argv else None)
         ts.append(time.perf_counter() - t0)
         dp.close()
     print("%s %s device plan: median %.3f ms, min %.3f ms over %d" % (os.environ.get("COVT_LIB_VARIANT", "libcovt.so"), label,

@@ -69,6 +69,10 @@ for s in "$@"; do
             COVT_LIB_VARIANT=$v timeout -k 10 200 python tools/device_plan_prof.py 20 --sweep 2>&1 | grep -v amdgpu.ids || fatal dplan_var $?
         done ;;
     dplan_prof_small) step dplan_prof_small 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_prof_small -o run --output-format csv -- python tools/device_plan_prof.py 5 --small ;;
+    dplan_prof_256) step dplan_prof_256 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_prof_256 -o run --output-format csv -- python tools/device_plan_prof.py 5 --n256 ;;
+    dplan_api_small) step dplan_api_small 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_api_small -o run --output-format csv -- python tools/device_plan_prof.py 20 --small --nosplit ;;
+    dplan_sq_small) step dplan_sq_small 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_BRANCH -d gpurun_out/dplan_sq_small -o run --output-format csv -- python tools/device_plan_prof.py 3 --small --nosplit ;;
+    dplan_sorted) step dplan_sorted 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_sorted -o run --output-format csv -- python tools/device_plan_prof.py 10 --sorted ;;
     dplan_prof) step dplan_prof 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_prof -o run --output-format csv -- python tools/device_plan_prof.py 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
