@@ -50,6 +50,23 @@ def load_covt():
     return mod
 
 
+# sources that decide the decode launch's traffic: the kernels and the plan that lays out their work
+KERNEL_SOURCES = ("cov-tiles_amd/csrc/covt_decode.hip", "cov-tiles_amd/csrc/covt_wave.h",
+                  "cov-tiles_amd/csrc/covt_internal.h", "cov-tiles_amd/csrc/covt_host.cpp", "include/covt.h")
+
+
+def kernel_sources_sha256():
+    """Fingerprint of KERNEL_SOURCES: profiles/pmc_traffic.json carries the one it was measured on, and
+    the bench line reports its traffic only while they match (a kernel change makes it stale, not wrong)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def tile_library():
     """Decodable OMT + Bing fixtures -> {zoom: [(key, bytes)]}."""
     with open(os.path.join(ROOT, "tests", "golden", "oracle_streams.json")) as f:
@@ -712,14 +729,20 @@ def main():
         value = tot_in * args.steps / wall / 1e9
         alg_bytes = plan.in_bytes + plan.out_bytes  # stream bytes read + decoded bytes written
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, traffic_note = None, "no profiles/pmc_traffic.json"
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
                 with open(pmc) as f:
                     pm = json.load(f)
-                if pm.get("tiles") == args.tiles and pm.get("scaling") == args.scaling:
+                if pm.get("tiles") != args.tiles or pm.get("scaling") != args.scaling:
+                    traffic_note = "profiles/pmc_traffic.json measured on another workload"
+                elif pm.get("kernel_sources_sha256") != kernel_sources_sha256():
+                    traffic_note = "stale: profiles/pmc_traffic.json measured on other decode / plan sources"
+                else:
                     traffic = pm.get("hbm_bytes_per_launch")
+                    traffic_note = ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the last launch (tools/profile_round.sh), "
+                                    "same kernel sources (sha256 %s)" % pm["kernel_sources_sha256"][:12])
             except Exception:  # noqa: BLE001
                 traffic = None
         line = {
@@ -744,7 +767,7 @@ def main():
             "mvert_per_s": round(tot_vx * args.steps / wall / 1e6, 2),
             "kernel_ms": round(kern_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_note": traffic_note,
                          "kernel": "covt decode launch = decode_family_kernel<RLE|VARINT|FASTPFOR> + "
                                    "decode_lane_kernel run concurrently between fork/join events; "
                                    "duration = HIP events on the launch stream (max over ranks)",

@@ -102,3 +102,13 @@ def test_config1_cpu_leg():
     t = bench.config1_tile(lib)
     st, cnt = O.decode_tile_full(t)
     assert st == 0 and cnt["streams"] == 41 and cnt["vertices"] == 19285 and cnt["property_columns"] > 0
+
+
+def test_kernel_sources_fingerprint():
+    """roofline.traffic comes from profiles/pmc_traffic.json only while it was measured on the same decode
+    and plan sources: the fingerprint is a stable sha256 over bench.KERNEL_SOURCES."""
+    import bench
+
+    a, b = bench.kernel_sources_sha256(), bench.kernel_sources_sha256()
+    assert a == b and len(a) == 64
+    assert all(os.path.exists(os.path.join(bench.ROOT, p)) for p in bench.KERNEL_SOURCES)

@@ -73,6 +73,12 @@ for s in "$@"; do
     dplan_api_small) step dplan_api_small 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_api_small -o run --output-format csv -- python tools/device_plan_prof.py 20 --small --nosplit ;;
     dplan_sq_small) step dplan_sq_small 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_BRANCH -d gpurun_out/dplan_sq_small -o run --output-format csv -- python tools/device_plan_prof.py 3 --small --nosplit ;;
     dplan_sorted) step dplan_sorted 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_sorted -o run --output-format csv -- python tools/device_plan_prof.py 10 --sorted ;;
+    ops_props) OPB_PROPS=1 step ops_props 600 python tools/op_breakdown.py ;;
+    props_time) step props_time 300 python tools/props_run.py ;;
+    fetch_rle|fetch_lane|fetch_rle_props|fetch_lane_props) fam=${s#fetch_}; fam=${fam%_props}
+        if [ "${s%_props}" != "$s" ]; then export OPB_PROPS=1; else unset OPB_PROPS; fi
+        step $s 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
+    sq_rle_props) OPB_PROPS=1 step $s 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_WAVES -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py rle 2 ;;
     dplan_prof) step dplan_prof 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_prof -o run --output-format csv -- python tools/device_plan_prof.py 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac

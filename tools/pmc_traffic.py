@@ -29,7 +29,11 @@ def main():
     write = last_launch(os.path.join(out, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     fb = sum(fetch.values()) * 1024 * 2  # gfx950 FETCH_SIZE under-count correction
     wb = sum(write.values()) * 1024
-    res = {"tiles": 10000, "scaling": "weak", "fetch_kib_raw": fetch, "write_kib_raw": write,
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    res = {"tiles": 10000, "scaling": "weak", "kernel_sources_sha256": bench.kernel_sources_sha256(),
+           "fetch_kib_raw": fetch, "write_kib_raw": write,
            "read_bytes_corrected": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
            "note": "FETCH_SIZE x2 (gfx950 wide-read correction), WRITE_SIZE as is; KiB -> bytes"}
     os.makedirs("profiles", exist_ok=True)

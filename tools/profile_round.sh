@@ -7,7 +7,7 @@
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-R=${1:-r02}
+R=${1:-r03}
 mkdir -p gpurun_out "gpurun_out/$R"
 LEAN="--no-cpu --no-props --no-assemble --no-configs --e2e-reps 0 --abi-host-reps 0 --device-plan-reps 0"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
