@@ -43,7 +43,14 @@ namespace covt {
 #define COVT_ASM_WAVES 4
 #endif
 constexpr int kAsmWaves = COVT_ASM_WAVES;  // independent waves (columns) per workgroup
-constexpr int kW = 256;       // items per step: 4 consecutive items per lane
+// Small batches (at most kCoopMaxColumns columns: one tile's latency, BASELINE config 1): columns with
+// at least kCoopMinItems features / parts / rings / coordinates are assembled by a whole workgroup of
+// kCoopWaves waves (4 x 64 x kCoopWaves items per step), the rest by single waves as in a batch.  A
+// column's passes are chains of dependent gathers, one step per 256 items on one wave (the config-1
+// tile's 35k-feature, 72k-coordinate line column: ~700 steps, 0.78 ms); sixteen waves take 16x fewer.
+constexpr int kCoopWaves = 16;
+constexpr int kCoopMaxColumns = 4096;
+constexpr int32_t kCoopMinItems = 8192;
 
 typedef __attribute__((address_space(1))) const int32_t g_i32;
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
@@ -52,21 +59,61 @@ typedef __attribute__((address_space(1))) const uint64_t g_u64;
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const i32x4 g_i32x4;
 
-struct __attribute__((aligned(16))) AsmSmem {
-    int32_t slot[kW];  // expansion: segment-end marks of the current step
-    int32_t ends[kW];  // expansion: the step's 256 segment ends
+template <int NW>
+struct __attribute__((aligned(16))) AsmSmemT {
+    int32_t slot[4 * 64 * NW];  // expansion: segment-end marks of the current step
+    int32_t ends[4 * 64 * NW];  // expansion: the step's segment ends
+    uint32_t red[2][NW];        // cooperative scans / reductions: per-wave totals (two buffers)
+};
+typedef AsmSmemT<1> AsmSmem;
+
+// The threads assembling one column: a wave (NW = 1: lane_id, wave primitives, no barrier) or a whole
+// workgroup of NW waves (thread index, per-wave partials through LDS and workgroup barriers).  Items
+// of a step: 4 consecutive per thread, K = 256 NW per step.
+template <int NW>
+struct Coop {
+    static constexpr int K = 4 * 64 * NW;
+    __device__ __forceinline__ static int tid() { return NW == 1 ? lane_id() : (int)threadIdx.x; }
+    __device__ __forceinline__ static int wid() { return NW == 1 ? 0 : (int)(threadIdx.x >> 6); }
+    __device__ __forceinline__ static void sync() {
+        if (NW == 1) wave_sync();
+        else __syncthreads();
+    }
+    __device__ __forceinline__ static bool any(bool p) { return NW == 1 ? __ballot(p) != 0ull : __syncthreads_or(p) != 0; }
+    // exclusive prefix of a per-thread value over the group (wave inclusive `inc` given), group total
+    __device__ __forceinline__ static uint32_t group_prefix(AsmSmemT<NW>& sm, uint32_t inc, uint32_t own,
+                                                           uint32_t& tot, int buf) {
+        if (NW == 1) {
+            tot = lane_bcast(inc, 63);
+            return inc - own;
+        }
+        if (lane_id() == 63) sm.red[buf][wid()] = inc;
+        __syncthreads();
+        uint32_t pre = 0, all = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const uint32_t t = sm.red[buf][i];
+            pre += i < wid() ? t : 0u;
+            all += t;
+        }
+        tot = all;
+        return pre + inc - own;
+    }
 };
 
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {  // lane l - 1's value (lane 0: 0), DPP wave_shr:1
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
 }
 
-// exclusive scan of 256 items held 4 per lane (items 4l .. 4l+3); `tot` gets the uniform total
-__device__ __forceinline__ void excl_scan4(const uint32_t x[4], uint32_t ex[4], uint32_t& tot) {
+// exclusive scan of the step's items held 4 per thread (items 4t .. 4t+3); `tot` gets the uniform total.
+// Cooperative groups alternate the two partial buffers (each buffer is rewritten only after a barrier
+// that follows every read of its previous contents).
+template <int NW>
+__device__ __forceinline__ void excl_scan4(AsmSmemT<NW>& sm, int& buf, const uint32_t x[4], uint32_t ex[4], uint32_t& tot) {
     const uint32_t s = x[0] + x[1] + x[2] + x[3];
     const uint32_t inc = incl_scan(s);
-    tot = lane_bcast(inc, 63);
-    uint32_t run = inc - s;
+    uint32_t run = Coop<NW>::group_prefix(sm, inc, s, tot, buf);
+    buf ^= 1;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         ex[k] = run;
@@ -76,8 +123,9 @@ __device__ __forceinline__ void excl_scan4(const uint32_t x[4], uint32_t ex[4], 
 
 // items q + 4l + k (k < 4) of a step of L: one 16-byte store when the lane's four are valid and
 // aligned (arrays are 16-byte aligned; aligned when q % 4 == 0), else element stores
+template <int NW>
 __device__ __forceinline__ void store4(int32_t* a, int32_t q, int32_t L, const uint32_t v[4]) {
-    const int32_t i0 = 4 * lane_id();
+    const int32_t i0 = 4 * Coop<NW>::tid();
     if ((q & 3) == 0 && i0 + 4 <= L) {
         *(i32x4*)(a + q + i0) = i32x4{(int32_t)v[0], (int32_t)v[1], (int32_t)v[2], (int32_t)v[3]};
     } else {
@@ -87,8 +135,9 @@ __device__ __forceinline__ void store4(int32_t* a, int32_t q, int32_t L, const u
     }
 }
 // coordinates (8 bytes each): two 16-byte nontemporal stores for four aligned valid items
+template <int NW>
 __device__ __forceinline__ void store4_xy(uint64_t* a, int32_t q, int32_t L, const uint64_t v[4]) {
-    const int32_t i0 = 4 * lane_id();
+    const int32_t i0 = 4 * Coop<NW>::tid();
     if ((q & 3) == 0 && i0 + 4 <= L) {
         i32x4* p = (i32x4*)(a + q + i0);
         __builtin_nontemporal_store(i32x4{(int32_t)v[0], (int32_t)(v[0] >> 32), (int32_t)v[1], (int32_t)(v[1] >> 32)}, p);
@@ -101,59 +150,78 @@ __device__ __forceinline__ void store4_xy(uint64_t* a, int32_t q, int32_t L, con
     }
 }
 
-// Segmented expansion cursor over O[0..S] (nondecreasing, O[0] = 0, O[S] = total), wave-uniform.
-// A step covers up to 256 items, lane l the four items q + 4l + k.
+// Segmented expansion cursor over O[0..S] (nondecreasing, O[0] = 0, O[S] = total), uniform over the
+// group.  A step covers up to K items, thread t the four items q + 4t + k.
+template <int NW>
 struct Expand {
+    static constexpr int K = Coop<NW>::K;
     const int32_t* O;
     int32_t S, total;
     int32_t base;   // segment index with O[base] <= q
     int32_t obase;  // O[base]
     int32_t q;      // first item of the next step
 
-    // one step: L items (uniform); item k of the lane (valid if 4l + k < L) gets its segment, the
+    // one step: L items (uniform); item k of the thread (valid if 4t + k < L) gets its segment, the
     // segment's start and end
-    __device__ __forceinline__ int32_t step(AsmSmem& sm, int32_t seg[4], int32_t start[4], int32_t end[4]) {
-        const int l = lane_id();
+    __device__ __forceinline__ int32_t step(AsmSmemT<NW>& sm, int& buf, int32_t seg[4], int32_t start[4],
+                                            int32_t end[4]) {
+        const int t = Coop<NW>::tid();
         int32_t e[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {  // end of segment base + 1 + 4l + k
-            const int32_t j = base + 1 + 4 * l + k;
+        for (int k = 0; k < 4; ++k) {  // end of segment base + 1 + 4t + k
+            const int32_t j = base + 1 + 4 * t + k;
             e[k] = j <= S ? ((const g_i32*)O)[j] : 0x7fffffff;
         }
-        *(i32x4*)&sm.ends[4 * l] = i32x4{e[0], e[1], e[2], e[3]};
-        *(i32x4*)&sm.slot[4 * l] = i32x4{0, 0, 0, 0};
-        wave_sync();
+        *(i32x4*)&sm.ends[4 * t] = i32x4{e[0], e[1], e[2], e[3]};
+        *(i32x4*)&sm.slot[4 * t] = i32x4{0, 0, 0, 0};
+        Coop<NW>::sync();
         int32_t r[5];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) r[k] = max(e[k] - q, 0);  // item offset where segment base+2+4l+k starts
-        r[4] = (int32_t)lane_next((uint32_t)r[0], 0x7fffffffu);
+        for (int k = 0; k < 4; ++k) r[k] = max(e[k] - q, 0);  // item offset where segment base+2+4t+k starts
+        if (NW == 1) r[4] = (int32_t)lane_next((uint32_t)r[0], 0x7fffffffu);
+        else r[4] = 4 * t + 4 < K ? max(sm.ends[4 * t + 4] - q, 0) : 0x7fffffff;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            if (r[k] < kW && r[k + 1] != r[k]) sm.slot[r[k]] = 4 * l + k + 1;  // the last of equal ends wins
-        wave_sync();
-        const i32x4 sl = *(const i32x4*)&sm.slot[4 * l];
+            if (r[k] < K && r[k + 1] != r[k]) sm.slot[r[k]] = 4 * t + k + 1;  // the last of equal ends wins
+        Coop<NW>::sync();
+        const i32x4 sl = *(const i32x4*)&sm.slot[4 * t];
         uint32_t m[4];
         m[0] = (uint32_t)sl.x;
         m[1] = max(m[0], (uint32_t)sl.y);
         m[2] = max(m[1], (uint32_t)sl.z);
         m[3] = max(m[2], (uint32_t)sl.w);
-        const uint32_t prev = wave_shr1(incl_max_scan(m[3]));
+        const uint32_t wincl = incl_max_scan(m[3]);
+        uint32_t prev = wave_shr1(wincl);
+        if (NW > 1) {  // the maximum over the lower waves' marks
+            if (lane_id() == 63) sm.red[buf][Coop<NW>::wid()] = wincl;
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < NW; ++i)
+                if (i < Coop<NW>::wid()) prev = max(prev, sm.red[buf][i]);
+            buf ^= 1;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int32_t cnt = (int32_t)max(prev, m[k]);  // segment ends <= q + 4l + k
+            const int32_t cnt = (int32_t)max(prev, m[k]);  // segment ends <= q + 4t + k
             start[k] = cnt == 0 ? obase : sm.ends[cnt - 1];
-            end[k] = sm.ends[min(cnt, kW - 1)];
+            end[k] = sm.ends[min(cnt, K - 1)];
             seg[k] = base + cnt;
         }
-        // items this step: at most 256, the rest of the column, and what the 256 loaded ends cover
-        int32_t L = min(kW, total - q);
-        if (base + kW < S) L = min(L, (int32_t)lane_bcast((uint32_t)e[3], 63) - q);
+        // items this step: at most K, the rest of the column, and what the K loaded ends cover
+        int32_t L = min(K, total - q);
+        if (base + K < S) L = min(L, (NW == 1 ? (int32_t)lane_bcast((uint32_t)e[3], 63) : sm.ends[K - 1]) - q);
         L = max(L, 0);
         int adv = 0;  // segments ending at or before the next q
 #pragma unroll
         for (int k = 0; k < 4; ++k) adv += __popcll(__ballot(e[k] <= q + L));
+        if (NW > 1) {
+            uint32_t tot;
+            (void)Coop<NW>::group_prefix(sm, lane_id() == 63 ? (uint32_t)adv : 0u, 0u, tot, buf);
+            buf ^= 1;
+            adv = (int)tot;
+        }
         const int32_t nob = adv > 0 ? uni(sm.ends[adv - 1]) : obase;
-        wave_sync();
+        Coop<NW>::sync();
         obase = nob;
         base += adv;
         q += L;
@@ -161,15 +229,20 @@ struct Expand {
     }
 };
 
-__device__ __forceinline__ void mem_publish() {  // this wave's global stores visible to its own loads
+template <int NW>
+__device__ __forceinline__ void mem_publish() {  // the group's global stores visible to its own loads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (NW > 1) __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+template <int NW>
 __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stream_result* __restrict__ dres,
                                 const covt_geom_desc& d, uint8_t* __restrict__ outb, covt_geom_result& res,
-                                AsmSmem& sm) {
-    const int l = lane_id();
+                                AsmSmemT<NW>& sm) {
+    constexpr int K = Coop<NW>::K;
+    const int l = Coop<NW>::tid();
+    int buf = 0;  // cooperative partials buffer (see excl_scan4)
     res.num_parts = res.num_rings = res.num_coords = 0;
     if ((uint32_t)d.flags & COVT_GEOM_TOO_LARGE) { res.status = COVT_ERR_INVALID_ARG; return; }
     for (int k = 0; k < 6; ++k) {  // a failed source stream fails the column
@@ -205,7 +278,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
 
     // ---- pass 1: features -> parts (items: features) ----
     uint32_t go_base = 0, P = 0;
-    for (int32_t f0 = 0; f0 < n; f0 += kW) {
+    for (int32_t f0 = 0; f0 < n; f0 += K) {
         const int32_t fl = f0 + 4 * l;  // this lane's first feature; types are 16-byte aligned
         const uint32_t tw = fl < n ? ((const g_u32*)types)[fl >> 2] : 0u;
         uint32_t t[4], multi[4], gi[4], pf[4], ex[4], nm, tot;
@@ -217,7 +290,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
             multi[k] = (valid && t[k] >= 3u && t[k] <= 5u) ? 1u : 0u;
             pf[k] = valid ? 1u : 0u;
         }
-        excl_scan4(multi, gi, nm);
+        excl_scan4(sm, buf, multi, gi, nm);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (multi[k]) {
@@ -231,18 +304,18 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 }
             }
         }
-        excl_scan4(pf, ex, tot);
+        excl_scan4(sm, buf, pf, ex, tot);
 #pragma unroll
         for (int k = 0; k < 4; ++k) ex[k] += P;
-        store4(geo_off, f0, n - f0, ex);
+        store4<NW>(geo_off, f0, n - f0, ex);
         go_base += nm;
         P += tot;
-        if (__ballot(bad_type || bad_cnt) || P > pcap) break;
+        if (Coop<NW>::any(bad_type || bad_cnt) || P > pcap) break;
     }
-    if (__ballot(bad_type)) { res.status = COVT_ERR_BAD_HEADER; return; }  // GeometryType.values()[b]
-    if (__ballot(bad_cnt) || P > pcap) { res.status = COVT_ERR_COUNT_MISMATCH; return; }
+    if (Coop<NW>::any(bad_type)) { res.status = COVT_ERR_BAD_HEADER; return; }  // GeometryType.values()[b]
+    if (Coop<NW>::any(bad_cnt) || P > pcap) { res.status = COVT_ERR_COUNT_MISMATCH; return; }
     if (l == 0) geo_off[n] = (int32_t)P;
-    mem_publish();
+    mem_publish<NW>();
 
 #if defined(COVT_ASM_PASSES) && COVT_ASM_PASSES < 2  // ablation build: stop here
     res.status = COVT_OK;
@@ -251,11 +324,11 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     // ---- pass 2: parts -> rings (items: parts, segments: features) ----
     uint32_t po_base = 0, R = 0;
     {
-        Expand x{geo_off, n, (int32_t)P, 0, 0, 0};
+        Expand<NW> x{geo_off, n, (int32_t)P, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t p0 = x.q;
             int32_t f[4], fs[4], fe[4];
-            const int32_t L = x.step(sm, f, fs, fe);
+            const int32_t L = x.step(sm, buf, f, fs, fe);
             uint32_t t[4], usep[4], pi[4], rp[4], scr[4], ex[4], npo, tot;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -263,7 +336,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 t[k] = valid ? (uint32_t)((const g_u8*)types)[f[k]] : 0u;
                 usep[k] = (valid && t[k] != 0u && t[k] != 3u) ? 1u : 0u;  // line and polygon parts
             }
-            excl_scan4(usep, pi, npo);
+            excl_scan4(sm, buf, usep, pi, npo);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool valid = 4 * l + k < L;
@@ -283,19 +356,19 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 const uint32_t vcount = (t[k] == 1u || t[k] == 4u) ? c : 1u;  // vertices of a line / point part
                 scr[k] = poly ? 1u : (min(vcount, ccap + 1u) << 1);
             }
-            excl_scan4(rp, ex, tot);
+            excl_scan4(sm, buf, rp, ex, tot);
 #pragma unroll
             for (int k = 0; k < 4; ++k) ex[k] += R;
-            store4(part_off, p0, L, ex);
-            store4(part_scr, p0, L, scr);
+            store4<NW>(part_off, p0, L, ex);
+            store4<NW>(part_scr, p0, L, scr);
             po_base += npo;
             R += tot;
-            if (__ballot(bad_cnt) || R > rcap) break;
+            if (Coop<NW>::any(bad_cnt) || R > rcap) break;
         }
     }
-    if (__ballot(bad_cnt) || R > rcap) { res.status = COVT_ERR_COUNT_MISMATCH; return; }
+    if (Coop<NW>::any(bad_cnt) || R > rcap) { res.status = COVT_ERR_COUNT_MISMATCH; return; }
     if (l == 0) part_off[P] = (int32_t)R;
-    mem_publish();
+    mem_publish<NW>();
 
 #if defined(COVT_ASM_PASSES) && COVT_ASM_PASSES < 3  // ablation build: stop here
     res.status = COVT_OK;
@@ -304,11 +377,11 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     // ---- pass 3: rings -> coordinates (items: rings, segments: parts) ----
     uint32_t ro_base = 0, V = 0, VS = 0;
     {
-        Expand x{part_off, (int32_t)P, (int32_t)R, 0, 0, 0};
+        Expand<NW> x{part_off, (int32_t)P, (int32_t)R, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t r0 = x.q;
             int32_t p[4], ps[4], pe[4];
-            const int32_t L = x.step(sm, p, ps, pe);
+            const int32_t L = x.step(sm, buf, p, ps, pe);
             uint32_t poly[4], ri[4], vs[4], vo_[4], ex[4], src[4], nr, tv, ts;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -317,7 +390,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 poly[k] = (valid && (sp & 1)) ? 1u : 0u;
                 vs[k] = valid ? (uint32_t)sp >> 1 : 0u;
             }
-            excl_scan4(poly, ri, nr);
+            excl_scan4(sm, buf, poly, ri, nr);
             uint32_t closing[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -334,24 +407,24 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 closing[k] = (poly[k] && !closed && vs[k] > 0u) ? 1u : 0u;
                 vo_[k] = vs[k] + closing[k];
             }
-            excl_scan4(vo_, ex, tv);
-            excl_scan4(vs, src, ts);
+            excl_scan4(sm, buf, vo_, ex, tv);
+            excl_scan4(sm, buf, vs, src, ts);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 ex[k] += V;
                 src[k] = (VS + src[k]) | (closing[k] << 31);
             }
-            store4(ring_off, r0, L, ex);
-            store4(ring_scr, r0, L, src);
+            store4<NW>(ring_off, r0, L, ex);
+            store4<NW>(ring_scr, r0, L, src);
             ro_base += nr;
             V += tv;
             VS += ts;
-            if (__ballot(bad_cnt) || V > ccap || VS > (uint32_t)n_src) break;
+            if (Coop<NW>::any(bad_cnt) || V > ccap || VS > (uint32_t)n_src) break;
         }
     }
-    if (__ballot(bad_cnt) || V > ccap || VS > (uint32_t)n_src) { res.status = COVT_ERR_COUNT_MISMATCH; return; }
+    if (Coop<NW>::any(bad_cnt) || V > ccap || VS > (uint32_t)n_src) { res.status = COVT_ERR_COUNT_MISMATCH; return; }
     if (l == 0) ring_off[R] = (int32_t)V;
-    mem_publish();
+    mem_publish<NW>();
 
 #if defined(COVT_ASM_PASSES) && COVT_ASM_PASSES < 4  // ablation build: stop here
     res.status = COVT_OK;
@@ -361,7 +434,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     bool bad_idx = false;
     if (V == VS) {
         // no closing vertex to insert: coordinate v is source vertex v (a straight copy / gather)
-        for (int32_t v0 = 0; v0 < (int32_t)V; v0 += kW) {
+        for (int32_t v0 = 0; v0 < (int32_t)V; v0 += K) {
             const int32_t i0 = v0 + 4 * l;
             const int32_t L = (int32_t)V - v0;
             int32_t idx[4];
@@ -381,14 +454,14 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 bad_idx |= valid && !inr;
                 xy[k] = (valid && inr) ? ((const g_u64*)vb)[idx[k]] : 0ull;
             }
-            store4_xy(coords, v0, L, xy);
+            store4_xy<NW>(coords, v0, L, xy);
         }
     } else {
-        Expand x{ring_off, (int32_t)R, (int32_t)V, 0, 0, 0};
+        Expand<NW> x{ring_off, (int32_t)R, (int32_t)V, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t v0 = x.q;
             int32_t r[4], rs[4], re[4];
-            const int32_t L = x.step(sm, r, rs, re);
+            const int32_t L = x.step(sm, buf, r, rs, re);
             uint64_t xy[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -402,29 +475,55 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 bad_idx |= valid && !inr;  // vertexBuffer[offset] out of range (ArrayIndexOutOfBounds)
                 xy[k] = (valid && inr) ? ((const g_u64*)vb)[idx] : 0ull;
             }
-            store4_xy(coords, v0, L, xy);
+            store4_xy<NW>(coords, v0, L, xy);
         }
     }
-    if (__ballot(bad_idx)) { res.status = COVT_ERR_TRUNCATED; return; }
+    if (Coop<NW>::any(bad_idx)) { res.status = COVT_ERR_TRUNCATED; return; }
     res.status = COVT_OK;
     res.num_parts = (int32_t)P;
     res.num_rings = (int32_t)R;
     res.num_coords = (int32_t)V;
 }
 
+// the items a column's passes step over (features, parts, rings, coordinates): its capacities
+__device__ __forceinline__ int32_t column_items(const covt_geom_desc& d) {
+    const int32_t n = d.in_off[0] >= 0 ? d.in_len[0] : 0;
+    return max(max(n, d.part_cap), max(d.ring_cap, d.coord_cap));
+}
+
+// one wave per column; columns of at least `coop_min` items are left to assemble_coop_kernel
 __global__ __launch_bounds__(64 * kAsmWaves) void assemble_kernel(const uint8_t* __restrict__ dec,
                                                                   const covt_stream_result* __restrict__ dres,
                                                                   const covt_geom_desc* __restrict__ descs,
                                                                   int64_t n_cols, uint8_t* __restrict__ outb,
-                                                                  covt_geom_result* __restrict__ gres) {
+                                                                  covt_geom_result* __restrict__ gres, int32_t coop_min) {
     __shared__ AsmSmem smem[kAsmWaves];
     const int w = threadIdx.x >> 6;
     const int64_t c = uni64((int64_t)blockIdx.x * kAsmWaves + w);
     if (c >= n_cols) return;
     const covt_geom_desc d = descs[c];
+    if (uni(column_items(d)) >= coop_min && !((uint32_t)d.flags & COVT_GEOM_TOO_LARGE)) return;
     covt_geom_result r{COVT_OK, 0, 0, 0};
-    assemble_column(dec, dres, d, outb, r, smem[w]);
+    assemble_column<1>(dec, dres, d, outb, r, smem[w]);
     if (lane_id() == 0) gres[c] = r;
+}
+
+// one workgroup of kCoopWaves waves per column of at least `coop_min` items (small batches only: the
+// grid is one workgroup per column, the others return at once)
+__global__ __launch_bounds__(64 * kCoopWaves) void assemble_coop_kernel(const uint8_t* __restrict__ dec,
+                                                                        const covt_stream_result* __restrict__ dres,
+                                                                        const covt_geom_desc* __restrict__ descs,
+                                                                        int64_t n_cols, uint8_t* __restrict__ outb,
+                                                                        covt_geom_result* __restrict__ gres,
+                                                                        int32_t coop_min) {
+    __shared__ AsmSmemT<kCoopWaves> smem;
+    const int64_t c = blockIdx.x;
+    if (c >= n_cols) return;
+    const covt_geom_desc d = descs[c];
+    if (column_items(d) < coop_min || ((uint32_t)d.flags & COVT_GEOM_TOO_LARGE)) return;  // (uniform)
+    covt_geom_result r{COVT_OK, 0, 0, 0};
+    assemble_column<kCoopWaves>(dec, dres, d, outb, r, smem);
+    if (threadIdx.x == 0) gres[c] = r;
 }
 
 }  // namespace covt
@@ -437,7 +536,13 @@ extern "C" int covt_assemble_geometry_device(const uint8_t* d_decoded, const cov
     if (n_columns == 0) return COVT_OK;
     const int64_t blocks = (n_columns + covt::kAsmWaves - 1) / covt::kAsmWaves;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
+    // small batches: big columns by whole workgroups (launched first: they are the critical path)
+    const bool coop = n_columns <= covt::kCoopMaxColumns;
+    const int32_t coop_min = coop ? covt::kCoopMinItems : 0x7fffffff;
+    if (coop)
+        hipLaunchKernelGGL(covt::assemble_coop_kernel, dim3((unsigned)n_columns), dim3(64 * covt::kCoopWaves), 0,
+                           (hipStream_t)hip_stream, d_decoded, d_res, d_gdesc, n_columns, d_asm, d_gres, coop_min);
     hipLaunchKernelGGL(covt::assemble_kernel, dim3((unsigned)blocks), dim3(64 * covt::kAsmWaves), 0,
-                       (hipStream_t)hip_stream, d_decoded, d_res, d_gdesc, n_columns, d_asm, d_gres);
+                       (hipStream_t)hip_stream, d_decoded, d_res, d_gdesc, n_columns, d_asm, d_gres, coop_min);
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
 }

@@ -153,6 +153,28 @@ def test_assembly_errors(covt, oracle, gpu_available):
     assert gres["status"].tolist() == [0, covt.ERR_TRUNCATED, covt.ERR_INVALID_ARG]
 
 
+def test_assembly_errors_cooperative(covt, oracle, gpu_available):
+    """The same error checks on columns big enough (>= 8192 items, batches of <= 4096 columns) for the
+    workgroup-cooperative path (assemble_coop_kernel): the first failing check's status, as the oracle."""
+    rng = np.random.default_rng(8)
+    base = A.synth_column(rng, 9000, True, False)
+    bad_type = dict(base, types=base["types"].copy())
+    bad_type["types"][8700] = 6
+    vo_out = dict(base, vo=base["vo"].copy())
+    vo_out["vo"][-1] = base["vb"].size // 2
+    poly = A.synth_column(rng, 9000, False, False, probs=[0, 0, 1, 0, 0, 0])
+    neg = dict(poly, ro=poly["ro"].copy())
+    neg["ro"][-5] = -3
+    ok_line = A.synth_column(rng, 12000, True, False, probs=[0, 1, 0, 0, 0, 0])
+    cols = [bad_type, vo_out, neg, base, poly, ok_line]
+    for c in cols:
+        c["caps"] = A.caps(c)
+        assert max(max(c["caps"]), c["types"].size) >= 8192
+    asm, gres, lay = _run_kernel(covt, cols)
+    assert gres["status"].tolist() == [covt.ERR_BAD_HEADER, covt.ERR_TRUNCATED, covt.ERR_COUNT_MISMATCH, 0, 0, 0]
+    _check_vs_oracle(oracle, cols, asm, gres, lay)
+
+
 def test_batch_assembly_properties(covt, oracle, gpu_available):
     """BASELINE config-5 batch (10k sampled tiles): every column equals the oracle's assembly of its source
     tile (goldens reused per source tile), coordinate totals add up."""

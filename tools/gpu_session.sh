@@ -79,6 +79,7 @@ for s in "$@"; do
         if [ "${s%_props}" != "$s" ]; then export OPB_PROPS=1; else unset OPB_PROPS; fi
         step $s 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     sq_rle_props) OPB_PROPS=1 step $s 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_WAVES -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py rle 2 ;;
+    config1_prof) step config1_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/config1_prof -o run --output-format csv -- python tools/config1_prof.py 20 ;;
     dplan_prof) step dplan_prof 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_prof -o run --output-format csv -- python tools/device_plan_prof.py 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
