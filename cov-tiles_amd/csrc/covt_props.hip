@@ -23,6 +23,18 @@ namespace covt {
 #define COVT_PROP_WAVES 2  // A/B: 4 -> +2 %
 #endif
 constexpr int kPropWaves = COVT_PROP_WAVES;  // independent waves (columns) per workgroup
+// Small batches (at most kPropCoopMaxColumns columns, e.g. one tile: BASELINE config 1): columns of at
+// least kPropCoopMinFeatures features are materialized by a whole workgroup of kPropCoopWaves waves
+// (4 x 64 x kPropCoopWaves features per step; a step is a chain of dependent loads: the validity
+// nibbles, then the gathers at the scanned ranks), the rest by single waves.
+constexpr int kPropCoopWaves = 16;
+constexpr int kPropCoopMaxColumns = 4096;
+constexpr int32_t kPropCoopMinFeatures = 8192;
+
+struct PropSmem {
+    uint32_t red[2][kPropCoopWaves];  // per-wave partials (two buffers, alternating)
+    int32_t st;                       // the dictionary's status (wave 0 checks / writes it)
+};
 
 typedef __attribute__((address_space(1))) const uint8_t gp_u8;
 typedef __attribute__((address_space(1))) const uint32_t gp_u32;
@@ -135,9 +147,13 @@ __device__ int32_t dictionary(const uint8_t* in, const uint8_t* dec, const covt_
     return COVT_OK;
 }
 
+// NW = 1: one wave (lane_id, wave primitives); NW > 1: the workgroup's NW waves cooperate on the column
+template <int NW>
 __device__ void materialize(const uint8_t* in, const uint8_t* dec, const covt_stream_result* dres,
-                            const covt_prop_desc& d, uint8_t* outb, covt_prop_result& res) {
-    const int l = lane_id();
+                            const covt_prop_desc& d, uint8_t* outb, covt_prop_result& res, PropSmem* smp) {
+    const int l = NW == 1 ? lane_id() : (int)threadIdx.x;
+    const int wv = NW == 1 ? 0 : (int)(threadIdx.x >> 6);
+    int buf = 0;
     res.status = COVT_OK;
     res.n_valid = 0;
     // Java's order: unsupported shapes, the present stream, encodings rejected after it, the data and
@@ -148,8 +164,18 @@ __device__ void materialize(const uint8_t* in, const uint8_t* dec, const covt_st
     // every sub-column checks its dictionary lengths; the owner also writes the dictionary, whatever
     // its own present / data streams hold (the other languages of a localized column share it)
     int32_t dst = COVT_OK;
-    if (d.type == COVT_PROP_STRING && d.res[2] >= 0 && st[2] == COVT_OK)
-        dst = dictionary(in, dec, d, outb, (d.flags & COVT_PROP_DICT_OWNER) != 0);
+    if (d.type == COVT_PROP_STRING && d.res[2] >= 0 && st[2] == COVT_OK) {
+        if (NW == 1) {
+            dst = dictionary(in, dec, d, outb, (d.flags & COVT_PROP_DICT_OWNER) != 0);
+        } else {  // wave 0 (the dictionary is the owner's, whatever its size), then its status to all
+            if (wv == 0) {
+                const int32_t x = dictionary(in, dec, d, outb, (d.flags & COVT_PROP_DICT_OWNER) != 0);
+                if (lane_id() == 0) smp->st = x;
+            }
+            __syncthreads();
+            dst = smp->st;
+        }
+    }
     for (int k = 0; k < 3; ++k) {
         if (st[k]) { res.status = st[k]; return; }
         if (k == 0 && (d.flags & COVT_PROP_UNSUPPORTED_LATE)) { res.status = COVT_ERR_UNSUPPORTED_ENCODING; return; }
@@ -163,13 +189,28 @@ __device__ void materialize(const uint8_t* in, const uint8_t* dec, const covt_st
     const bool dense_bool = (d.flags & COVT_PROP_DENSE_BOOL) != 0;
     uint32_t carry = 0;  // present features before this step (uniform)
     bool bad = false;
-    for (int32_t f0 = 0; f0 < n; f0 += 256) {
+    for (int32_t f0 = 0; f0 < n; f0 += 4 * 64 * NW) {
         const int32_t f = f0 + 4 * l;
         const uint32_t vb = pres ? nibble(pres, f, n) : all_valid(f, n);
         const uint32_t cnt = (uint32_t)__popc(vb);
         const uint32_t inc = incl_scan(cnt);
-        uint32_t j = carry + inc - cnt;  // rank of this lane's first present feature
-        carry += lane_bcast(inc, 63);
+        uint32_t pre = inc - cnt, tot;  // present features of the step before this thread's, and in all
+        if (NW == 1) {
+            tot = lane_bcast(inc, 63);
+        } else {  // + the lower waves' counts (LDS partials; a buffer is rewritten two barriers later)
+            if (lane_id() == 63) smp->red[buf][wv] = inc;
+            __syncthreads();
+            tot = 0;
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const uint32_t t = smp->red[buf][i];
+                pre += i < wv ? t : 0u;
+                tot += t;
+            }
+            buf ^= 1;
+        }
+        uint32_t j = carry + pre;  // rank of this thread's first present feature
+        carry += tot;
         // lanes 2m and 2m+1 hold the two nibbles of byte m of the step
         const uint32_t vhi = lane_next(vb);
         if (!(l & 1) && f < n) vout[f >> 3] = (uint8_t)(vb | (vhi << 4));
@@ -233,23 +274,44 @@ __device__ void materialize(const uint8_t* in, const uint8_t* dec, const covt_st
             }
         }
     }
-    if (__ballot(bad)) { res.status = COVT_ERR_COUNT_MISMATCH; return; }
+    if (NW == 1 ? __ballot(bad) != 0ull : __syncthreads_or(bad) != 0) { res.status = COVT_ERR_COUNT_MISMATCH; return; }
     res.n_valid = (int32_t)carry;
 }
 
+// one wave per column; columns of at least `coop_min` features are left to props_coop_kernel
 __global__ __launch_bounds__(64 * kPropWaves) void props_kernel(const uint8_t* __restrict__ in,
                                                                 const uint8_t* __restrict__ dec,
                                                                 const covt_stream_result* __restrict__ dres,
                                                                 const covt_prop_desc* __restrict__ descs,
                                                                 int64_t n_cols, uint8_t* __restrict__ outb,
-                                                                covt_prop_result* __restrict__ pres) {
+                                                                covt_prop_result* __restrict__ pres, int32_t coop_min) {
     const int w = threadIdx.x >> 6;
     const int64_t c = uni64((int64_t)blockIdx.x * kPropWaves + w);
     if (c >= n_cols) return;
     const covt_prop_desc d = descs[c];
+    if (uni(d.n_features) >= coop_min) return;
     covt_prop_result r;
-    materialize(in, dec, dres, d, outb, r);
+    materialize<1>(in, dec, dres, d, outb, r, nullptr);
     if (lane_id() == 0) pres[c] = r;
+}
+
+// one workgroup of kPropCoopWaves waves per column of at least `coop_min` features (small batches only:
+// one workgroup per column, the others return at once)
+__global__ __launch_bounds__(64 * kPropCoopWaves) void props_coop_kernel(const uint8_t* __restrict__ in,
+                                                                         const uint8_t* __restrict__ dec,
+                                                                         const covt_stream_result* __restrict__ dres,
+                                                                         const covt_prop_desc* __restrict__ descs,
+                                                                         int64_t n_cols, uint8_t* __restrict__ outb,
+                                                                         covt_prop_result* __restrict__ pres,
+                                                                         int32_t coop_min) {
+    __shared__ PropSmem smem;
+    const int64_t c = blockIdx.x;
+    if (c >= n_cols) return;
+    const covt_prop_desc d = descs[c];
+    if (d.n_features < coop_min) return;  // (uniform)
+    covt_prop_result r;
+    materialize<kPropCoopWaves>(in, dec, dres, d, outb, r, &smem);
+    if (threadIdx.x == 0) pres[c] = r;
 }
 
 }  // namespace covt
@@ -263,7 +325,14 @@ extern "C" int covt_materialize_properties_device(const uint8_t* d_in, const uin
     if (n_columns == 0) return COVT_OK;
     const int64_t blocks = (n_columns + covt::kPropWaves - 1) / covt::kPropWaves;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
+    // small batches: big columns by whole workgroups (launched first: they are the critical path)
+    const bool coop = n_columns <= covt::kPropCoopMaxColumns;
+    const int32_t coop_min = coop ? covt::kPropCoopMinFeatures : 0x7fffffff;
+    if (coop)
+        hipLaunchKernelGGL(covt::props_coop_kernel, dim3((unsigned)n_columns), dim3(64 * covt::kPropCoopWaves), 0,
+                           (hipStream_t)hip_stream, d_in, d_decoded, d_res, d_pdesc, n_columns, d_props, d_pres,
+                           coop_min);
     hipLaunchKernelGGL(covt::props_kernel, dim3((unsigned)blocks), dim3(64 * covt::kPropWaves), 0,
-                       (hipStream_t)hip_stream, d_in, d_decoded, d_res, d_pdesc, n_columns, d_props, d_pres);
+                       (hipStream_t)hip_stream, d_in, d_decoded, d_res, d_pdesc, n_columns, d_props, d_pres, coop_min);
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
 }

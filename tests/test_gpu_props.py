@@ -122,14 +122,16 @@ def test_batch_properties_digests(covt, oracle, gpu_available):
         assert d == ref[key][c - first[int(P["tile"][c])]], (key, c)
 
 
-def test_corrupted_property_streams_status_parity(covt, oracle, gpu_available):
+@pytest.mark.parametrize("n_tiles", [60, 20], ids=["wave_per_column", "cooperative"])
+def test_corrupted_property_streams_status_parity(covt, oracle, gpu_available, n_tiles):
     """Bit flips / truncations inside property streams: the GPU reports exactly the oracle's status and,
-    when that is OK, exactly its column."""
-    rng = np.random.default_rng(11)
+    when that is OK, exactly its column.  20 tiles (2,900 columns) take the small-batch path, where the
+    tile's 35k-feature columns are materialized by whole workgroups (props_coop_kernel)."""
+    rng = np.random.default_rng(11 if n_tiles == 60 else 12)
     base = _tile("5_16_20")
     st, props = oracle.walk_properties(base)
     tiles = []
-    for i in range(60):
+    for i in range(n_tiles):
         p = props[int(rng.integers(0, len(props)))]
         role = int(rng.choice([r for r in range(4) if p.s_off[r] >= 0 and p.s_bl[r] > 0]))
         t = bytearray(base)
@@ -147,4 +149,5 @@ def test_corrupted_property_streams_status_parity(covt, oracle, gpu_available):
         for c, o in zip(idx, outs):
             _check_column(covt, plan, buf, pres, int(c), o, (t, int(c)))
             n_err += o[0] != 0
-    assert n_err >= 5
+    assert n_err >= (5 if n_tiles == 60 else 1)
+    assert (plan.num_property_columns <= 4096) == (n_tiles == 20)
