@@ -433,11 +433,10 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     // ---- pass 4: coordinates (ICE gather) ----
     bool bad_idx = false;
     if (V == VS) {
-        // no closing vertex to insert: coordinate v is source vertex v (a straight copy / gather)
-        for (int32_t v0 = 0; v0 < (int32_t)V; v0 += K) {
-            const int32_t i0 = v0 + 4 * l;
-            const int32_t L = (int32_t)V - v0;
-            int32_t idx[4];
+        // no closing vertex to insert: coordinate v is source vertex v (a straight copy / gather).  Two
+        // steps per iteration, their index loads and gathers issued before any store (stores may alias
+        // the loads as far as the compiler knows, so a one-step loop waits out every chain in turn)
+        auto idx4 = [&](int32_t i0, int32_t (&idx)[4]) {
             if (ice && i0 + 4 <= (int32_t)V) {  // vertexOffsets are 16-byte aligned, i0 % 4 == 0
                 const i32x4 w = *(const g_i32x4*)(vo + i0);
                 idx[0] = w.x; idx[1] = w.y; idx[2] = w.z; idx[3] = w.w;
@@ -446,7 +445,8 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 for (int k = 0; k < 4; ++k)
                     idx[k] = i0 + k < (int32_t)V ? (ice ? ((const g_i32*)vo)[i0 + k] : i0 + k) : 0;
             }
-            uint64_t xy[4];
+        };
+        auto gather4 = [&](int32_t i0, const int32_t (&idx)[4], uint64_t (&xy)[4]) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool valid = i0 + k < (int32_t)V;
@@ -454,7 +454,17 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 bad_idx |= valid && !inr;
                 xy[k] = (valid && inr) ? ((const g_u64*)vb)[idx[k]] : 0ull;
             }
-            store4_xy<NW>(coords, v0, L, xy);
+        };
+        for (int32_t v0 = 0; v0 < (int32_t)V; v0 += 2 * K) {
+            const int32_t i0 = v0 + 4 * l, i1 = i0 + K;
+            int32_t ia[4], ib[4];
+            idx4(i0, ia);
+            idx4(i1, ib);
+            uint64_t xa[4], xb[4];
+            gather4(i0, ia, xa);
+            gather4(i1, ib, xb);
+            store4_xy<NW>(coords, v0, (int32_t)V - v0, xa);
+            if (v0 + K < (int32_t)V) store4_xy<NW>(coords, v0 + K, (int32_t)V - v0 - K, xb);
         }
     } else {
         Expand<NW> x{ring_off, (int32_t)R, (int32_t)V, 0, 0, 0};

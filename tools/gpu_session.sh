@@ -80,6 +80,9 @@ for s in "$@"; do
         step $s 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     sq_rle_props) OPB_PROPS=1 step $s 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_WAVES -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py rle 2 ;;
     config1_prof) step config1_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/config1_prof -o run --output-format csv -- python tools/config1_prof.py 20 ;;
+    config1_passes) for v in libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so; do
+            COVT_LIB_VARIANT=$v step config1_$v 300 rocprofv3 --kernel-trace --stats -d gpurun_out/config1_$v -o run --output-format csv -- python tools/config1_prof.py 20
+        done ;;
     dplan_prof) step dplan_prof 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_prof -o run --output-format csv -- python tools/device_plan_prof.py 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
