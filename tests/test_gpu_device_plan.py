@@ -267,6 +267,19 @@ def test_split_forced(covt, gpu_available, decodable_tiles, golden_streams, kw):
         _assert_same_decode(covt, hp, dp)
 
 
+@pytest.mark.parametrize("optimized", [False, True], ids=["named", "optimized"])
+def test_split_forced_gend(covt, gpu_available, decodable_tiles, optimized):
+    """Forced small chunks over Gen D conversions (implicit present streams, TreeMap stream order): the
+    device walk of the other format feeds the same split rule; the same plan and decode as the host."""
+    tiles = [RT.genc_to_gend(t, optimized=optimized)[0] for _, t in decodable_tiles[1::5][:16]]
+    hp = _host_plan(covt, tiles, covt.FORMAT_GEND, 0, split=True, split_min=0, split_ratio=0, split_chunk=96,
+                    split_values=512)
+    assert (hp.family_counts[covt.FAMILY_SPLIT:] > 0).all(), hp.family_counts
+    dp = _device_plan(covt, hp, covt.FORMAT_GEND, 0)
+    _assert_same_plan(hp, dp)
+    _assert_same_decode(covt, hp, dp)
+
+
 def test_split_malformed_streams(covt, gpu_available, decodable_tiles):
     """Split candidates whose payload bytes are corrupted (metadata intact): the RLE group walk and the
     FastPFOR header walk stop where the host's do -- unframed RLE streams stay whole, FastPFOR chunks
