@@ -185,7 +185,9 @@ EXPORTED_SYMBOLS = (
     "covt_device_plan_descs_device", "covt_device_plan_streams_device", "covt_device_plan_tile_status_device",
     "covt_device_plan_order_device", "covt_device_plan_copy", "covt_device_plan_decode",
     "covt_plan_options_init", "covt_plan_create_opts", "covt_device_plan_create_opts",
-    "covt_device_plan_num_descs",
+    "covt_device_plan_num_descs", "covt_device_plan_geometry", "covt_device_plan_num_geometry_columns",
+    "covt_device_plan_assembly_bytes", "covt_device_plan_geometry_descs_device", "covt_device_plan_geometry_copy",
+    "covt_device_plan_assemble",
 )
 
 
@@ -288,6 +290,15 @@ def lib() -> C.CDLL:
         getattr(L, name).restype = vp
     L.covt_device_plan_copy.argtypes = [vp, vp, vp, i32p]
     L.covt_device_plan_decode.argtypes = [vp, vp, vp, vp, vp]
+    L.covt_device_plan_geometry.argtypes = [vp, vp]
+    L.covt_device_plan_num_geometry_columns.argtypes = [vp]
+    L.covt_device_plan_num_geometry_columns.restype = C.c_int64
+    L.covt_device_plan_assembly_bytes.argtypes = [vp]
+    L.covt_device_plan_assembly_bytes.restype = C.c_int64
+    L.covt_device_plan_geometry_descs_device.argtypes = [vp]
+    L.covt_device_plan_geometry_descs_device.restype = vp
+    L.covt_device_plan_geometry_copy.argtypes = [vp, vp, vp]
+    L.covt_device_plan_assemble.argtypes = [vp, vp, vp, vp, vp, vp]
     L.covt_version.restype = C.c_char_p
     L.covt_device_count.argtypes = [i32p]
     _lib = L
@@ -861,6 +872,44 @@ class DevicePlan:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _raise(lib().covt_device_plan_decode(self._h, self.d_in.data_ptr(), d_out.data_ptr(), d_res.data_ptr(),
                                              s.cuda_stream), "covt_device_plan_decode")
+
+    def geometry(self, stream=None):
+        """Build the geometry-column records and descriptors on the device (once; synchronises the
+        stream): Plan.geom / Plan.gdescs / Plan.assembly_bytes without the host plan."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.device(self.device):
+            _raise(lib().covt_device_plan_geometry(self._h, s.cuda_stream), "covt_device_plan_geometry")
+        self.num_geometry_columns = lib().covt_device_plan_num_geometry_columns(self._h)
+        self.assembly_bytes = lib().covt_device_plan_assembly_bytes(self._h)
+        return self.num_geometry_columns
+
+    def geometry_copy(self):
+        """(geometry records in tile order, geometry descriptors in launch order) as host arrays."""
+        self.geometry()
+        g = np.zeros(self.num_geometry_columns, dtype=GEOM_INFO_DTYPE)
+        d = np.zeros(self.num_geometry_columns * C.sizeof(GeomDesc), dtype=np.uint8)
+        _raise(lib().covt_device_plan_geometry_copy(self._h, g.ctypes.data, d.ctypes.data),
+               "covt_device_plan_geometry_copy")
+        return g, d
+
+    def alloc_assembly(self):
+        """(assembly buffer, geometry results) on the device, sized for this plan's geometry columns."""
+        import torch
+
+        self.geometry()
+        return (torch.empty(max(self.assembly_bytes, 16), dtype=torch.uint8, device=self.device),
+                torch.zeros(max(self.num_geometry_columns, 1) * 4, dtype=torch.int32, device=self.device))
+
+    def assemble(self, d_out, d_res, d_asm, d_gres, stream=None):
+        """Enqueue the geometry assembly over this plan's geometry descriptors (after decode())."""
+        import torch
+
+        self.geometry(stream)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _raise(lib().covt_device_plan_assemble(self._h, d_out.data_ptr(), d_res.data_ptr(), d_asm.data_ptr(),
+                                               d_gres.data_ptr(), s.cuda_stream), "covt_device_plan_assemble")
 
 
 class DeviceSubset:

@@ -37,6 +37,11 @@ struct covt_device_plan {
     void* tile_arena = nullptr;    // status, per-tile counts and prefix sums, totals, scan scratch
     void* stream_arena = nullptr;  // infos, values, keys, launch order, descriptors, sort scratch
     void* desc_arena = nullptr;    // split plans: the descriptors and their streams (n_descs each)
+    void* geo_arena = nullptr;     // geometry columns (covt_device_plan_geometry): records, descriptors
+    bool geo_built = false;
+    int64_t n_geo = 0, asm_bytes = 0;
+    covt_geom_info* d_ginfo = nullptr;
+    covt_geom_desc* d_gdesc = nullptr;
     int32_t* d_status = nullptr;
     covt_stream_info* d_info = nullptr;
     covt_stream_desc* d_desc = nullptr;
@@ -1435,6 +1440,91 @@ __global__ void fpf_states_walk(const uint8_t* __restrict__ bytes, const covt_st
     }
 }
 
+// ---- Geometry columns (covt_device_plan_geometry; covt_host.cpp plan_geometry): a column is a run of
+// adjacent geometry streams of one (tile, layer); its record holds the source streams, the assembly
+// capacities and its six 16-byte aligned output slices; descriptors go largest (coordinates +
+// features) first, ties in tile order.
+__device__ __forceinline__ bool geo_same(const covt_stream_info& a, const covt_stream_info& b) {
+    return a.column_kind == 1 && b.column_kind == 1 && a.tile == b.tile && a.layer == b.layer;
+}
+__global__ void geom_mark(const covt_stream_info* __restrict__ info, int64_t ns, int64_t* __restrict__ gst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > ns) return;
+    gst[i] = i < ns && info[i].column_kind == 1 && !(i > 0 && geo_same(info[i - 1], info[i])) ? 1 : 0;
+}
+__global__ void geom_columns(const covt_stream_info* __restrict__ info, int64_t ns, int32_t format,
+                             const int64_t* __restrict__ gst, const int64_t* __restrict__ gpos,
+                             covt_geom_info* __restrict__ ginfo, int64_t* __restrict__ colbytes) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ns || !gst[i]) return;
+    const covt_stream_info& s0 = info[i];
+    covt_geom_info g{};
+    g.tile = s0.tile;
+    g.layer = s0.layer;
+    g.column_type = s0.column_type;
+    for (int k = 0; k < 6; ++k) g.stream[k] = -1;
+    int64_t len[6] = {0, 0, 0, 0, 0, 0};
+    for (int64_t j = i; j < ns && geo_same(s0, info[j]); ++j) {
+        const covt_stream_info& s = info[j];
+        const int k = s.stream_type - ST_GEOMETRY_TYPES;
+        if (k < 0 || k > 5) continue;
+        g.stream[k] = (int32_t)j;
+        len[k] = k == 5 ? s.out_elems / 2 : s.out_elems;  // vertexBuffer: x,y pairs
+        if (k == 5) g.column_type = s.column_type;
+    }
+    g.n_features = (int32_t)len[0];
+    const int64_t vs = g.stream[4] >= 0 ? len[4] : len[5];
+    const int64_t pcap = vs + len[2], rcap = vs + len[2] + len[3];
+    g.flags = (format == COVT_FORMAT_GENC && (g.column_type == CT_ICE || g.column_type == CT_ICE_MORTON))
+                  ? (int32_t)COVT_GEOM_CLOSED_IN_STREAM : 0;
+    const int64_t ccap = vs + ((g.flags & COVT_GEOM_CLOSED_IN_STREAM) ? 0 : len[3]);
+    const bool fits = rcap <= COVT_GEOM_MAX_CAP && ccap <= COVT_GEOM_MAX_CAP && len[0] <= COVT_GEOM_MAX_CAP;
+    g.part_cap = fits ? (int32_t)pcap : 0;
+    g.ring_cap = fits ? (int32_t)rcap : 0;
+    g.coord_cap = fits ? (int32_t)ccap : 0;
+    if (!fits) g.flags = (int32_t)((uint32_t)g.flags | COVT_GEOM_TOO_LARGE);
+    const int64_t nf = fits ? len[0] : 0;
+    const int64_t bytes[6] = {4 * (nf + 1), 4 * ((int64_t)g.part_cap + 1), 4 * ((int64_t)g.ring_cap + 1),
+                              8 * (int64_t)g.coord_cap, 4 * (int64_t)g.part_cap, 4 * (int64_t)g.ring_cap};
+    int64_t off = 0;
+    for (int k = 0; k < 6; ++k) {  // local to the column; geom_keys adds its base
+        g.out_off[k] = off;
+        off = align16(off + bytes[k]);
+    }
+    const int64_t c = gpos[i];
+    ginfo[c] = g;
+    colbytes[c] = off;
+}
+__global__ void geom_keys(covt_geom_info* __restrict__ ginfo, int64_t nc, const int64_t* __restrict__ coloff,
+                          uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nc) return;
+    covt_geom_info& g = ginfo[c];
+    for (int k = 0; k < 6; ++k) g.out_off[k] += coloff[c];
+    keys[c] = (1ull << 40) - (uint64_t)((int64_t)g.coord_cap + g.n_features);
+    vals[c] = (uint32_t)c;
+}
+__global__ void geom_descs(const covt_stream_info* __restrict__ info, covt_geom_info* __restrict__ ginfo,
+                           const uint32_t* __restrict__ order, int64_t nc, covt_geom_desc* __restrict__ gdesc) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nc) return;
+    covt_geom_info& g = ginfo[order[k]];
+    covt_geom_desc d{};
+    for (int m = 0; m < 6; ++m) {
+        const int32_t si = g.stream[m];
+        d.in_off[m] = si >= 0 ? info[si].out_off : -1;
+        d.in_len[m] = si >= 0 ? (int32_t)(m == 5 ? info[si].out_elems / 2 : info[si].out_elems) : 0;
+        d.in_res[m] = si >= 0 ? info[si].desc_index : -1;  // its decode status gates the column
+        d.out_off[m] = g.out_off[m];
+    }
+    d.part_cap = g.part_cap;
+    d.ring_cap = g.ring_cap;
+    d.coord_cap = g.coord_cap;
+    d.flags = g.flags;
+    g.desc_index = (int32_t)k;
+    gdesc[k] = d;
+}
+
 size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 
@@ -1653,6 +1743,7 @@ void covt_device_plan_destroy(covt_device_plan* p) {
     if (p->tile_arena) (void)hipFree(p->tile_arena);
     if (p->stream_arena) (void)hipFree(p->stream_arena);
     if (p->desc_arena) (void)hipFree(p->desc_arena);
+    if (p->geo_arena) (void)hipFree(p->geo_arena);
     if (sw) (void)hipSetDevice(cur);
     delete p;
 }
@@ -1692,6 +1783,104 @@ int covt_device_plan_copy(const covt_device_plan* p, covt_stream_info* streams, 
         hipMemcpy(tile_status, p->d_status, (size_t)p->n_tiles * 4, hipMemcpyDeviceToHost) != hipSuccess)
         return COVT_ERR_DEVICE;
     return COVT_OK;
+}
+
+int covt_device_plan_geometry(covt_device_plan* p, void* hip_stream) {
+    if (!p) return COVT_ERR_INVALID_ARG;
+    if (p->geo_built) return COVT_OK;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || (cur != p->dev && hipSetDevice(p->dev) != hipSuccess)) return COVT_ERR_DEVICE;
+    struct Restore {
+        int cur, dev;
+        ~Restore() { if (cur != dev) (void)hipSetDevice(cur); }
+    } restore{cur, p->dev};
+    hipStream_t s = (hipStream_t)hip_stream;
+    const int64_t ns = p->n_streams;
+    const size_t n1 = (size_t)ns + 1;
+    size_t scan_tmp = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)n1, s) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    // stage 1 arena: column starts | their indices | scan scratch
+    void* tmp = nullptr;
+    const size_t o_gp = up256(n1 * 8), o_t = o_gp + up256(n1 * 8);
+    if (hipMalloc(&tmp, o_t + up256(scan_tmp)) != hipSuccess) return COVT_ERR_DEVICE;
+    struct Free {
+        void* q;
+        ~Free() { if (q) (void)hipFree(q); }
+    } free_tmp{tmp};
+    int64_t *gst = (int64_t*)tmp, *gpos = (int64_t*)((uint8_t*)tmp + o_gp);
+    const int blocks = (int)((n1 + 255) / 256);
+    geom_mark<<<blocks, 256, 0, s>>>(p->d_info, ns, gst);
+    if (hipGetLastError() != hipSuccess) return COVT_ERR_DEVICE;
+    if (hipcub::DeviceScan::ExclusiveSum((uint8_t*)tmp + o_t, scan_tmp, gst, gpos, (int)n1, s) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    int64_t nc = 0;
+    if (hipMemcpyAsync(&nc, gpos + ns, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    // geometry arena: records | descriptors | column bytes | column offsets | keys in/out | vals in/out | scratch
+    const size_t m = (size_t)(nc > 0 ? nc : 1);
+    size_t sort_tmp = 0, cscan_tmp = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)nc, 0, 41, s) != hipSuccess ||
+        hipcub::DeviceScan::ExclusiveSum(nullptr, cscan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)(nc + 1), s) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    const size_t o_gd = up256(m * sizeof(covt_geom_info)), o_cb = o_gd + up256(m * sizeof(covt_geom_desc)),
+                 o_co = o_cb + up256((m + 1) * 8), o_k0 = o_co + up256((m + 1) * 8), o_k1 = o_k0 + up256(m * 8),
+                 o_v0 = o_k1 + up256(m * 8), o_v1 = o_v0 + up256(m * 4), o_st = o_v1 + up256(m * 4),
+                 o_cs = o_st + up256(sort_tmp), total = o_cs + up256(cscan_tmp);
+    if (hipMalloc(&p->geo_arena, total) != hipSuccess) return COVT_ERR_DEVICE;
+    uint8_t* g = (uint8_t*)p->geo_arena;
+    p->d_ginfo = (covt_geom_info*)g;
+    p->d_gdesc = (covt_geom_desc*)(g + o_gd);
+    int64_t *colbytes = (int64_t*)(g + o_cb), *coloff = (int64_t*)(g + o_co);
+    uint64_t *k0 = (uint64_t*)(g + o_k0), *k1 = (uint64_t*)(g + o_k1);
+    uint32_t *v0 = (uint32_t*)(g + o_v0), *v1 = (uint32_t*)(g + o_v1);
+    if (hipMemsetAsync(colbytes, 0, (m + 1) * 8, s) != hipSuccess) return COVT_ERR_DEVICE;
+    int64_t asm_bytes = 0;
+    if (nc > 0) {
+        geom_columns<<<(int)((ns + 255) / 256), 256, 0, s>>>(p->d_info, ns, p->format, gst, gpos, p->d_ginfo, colbytes);
+        if (hipGetLastError() != hipSuccess) return COVT_ERR_DEVICE;
+        if (hipcub::DeviceScan::ExclusiveSum(g + o_cs, cscan_tmp, colbytes, coloff, (int)(nc + 1), s) != hipSuccess)
+            return COVT_ERR_DEVICE;
+        const int cb = (int)((nc + 255) / 256);
+        geom_keys<<<cb, 256, 0, s>>>(p->d_ginfo, nc, coloff, k0, v0);
+        if (hipGetLastError() != hipSuccess) return COVT_ERR_DEVICE;
+        if (hipcub::DeviceRadixSort::SortPairs(g + o_st, sort_tmp, k0, k1, v0, v1, (int)nc, 0, 41, s) != hipSuccess)
+            return COVT_ERR_DEVICE;
+        geom_descs<<<cb, 256, 0, s>>>(p->d_info, p->d_ginfo, v1, nc, p->d_gdesc);
+        if (hipGetLastError() != hipSuccess) return COVT_ERR_DEVICE;
+        if (hipMemcpyAsync(&asm_bytes, coloff + nc, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return COVT_ERR_DEVICE;
+    }
+    p->n_geo = nc;
+    p->asm_bytes = asm_bytes;
+    p->geo_built = true;
+    return COVT_OK;
+}
+
+int64_t covt_device_plan_num_geometry_columns(const covt_device_plan* p) { return p && p->geo_built ? p->n_geo : 0; }
+int64_t covt_device_plan_assembly_bytes(const covt_device_plan* p) { return p && p->geo_built ? p->asm_bytes : 0; }
+const covt_geom_desc* covt_device_plan_geometry_descs_device(const covt_device_plan* p) {
+    return p && p->geo_built ? p->d_gdesc : nullptr;
+}
+
+int covt_device_plan_geometry_copy(const covt_device_plan* p, covt_geom_info* infos, covt_geom_desc* descs) {
+    if (!p || !p->geo_built) return COVT_ERR_INVALID_ARG;
+    const size_t nc = (size_t)p->n_geo;
+    if (infos && nc && hipMemcpy(infos, p->d_ginfo, nc * sizeof(covt_geom_info), hipMemcpyDeviceToHost) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    if (descs && nc && hipMemcpy(descs, p->d_gdesc, nc * sizeof(covt_geom_desc), hipMemcpyDeviceToHost) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    return COVT_OK;
+}
+
+int covt_device_plan_assemble(covt_device_plan* p, const uint8_t* d_decoded, const covt_stream_result* d_res,
+                              uint8_t* d_asm, covt_geom_result* d_gres, void* hip_stream) {
+    if (!p) return COVT_ERR_INVALID_ARG;
+    const int st = covt_device_plan_geometry(p, hip_stream);
+    if (st) return st;
+    return covt_assemble_geometry_device(d_decoded, d_res, p->d_gdesc, p->n_geo, d_asm, d_gres, hip_stream);
 }
 
 int covt_device_plan_decode(const covt_device_plan* p, const uint8_t* d_in, uint8_t* d_out, covt_stream_result* d_res,

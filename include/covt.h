@@ -453,7 +453,8 @@ int covt_plan_properties_host(const covt_plan* plan, const uint8_t* bytes, uint6
  * covt_stream_info fields and 16-byte aligned output slices, descriptors in the same launch order
  * and families, including the split rule: with the same options, the long poles of a small batch are
  * cut into the same chunks (varint byte chunks, FastPFOR value chunks with their start states, ORC RLE
- * group chunks).  Property columns, geometry assembly and multi-GPU shards stay with the host plan.
+ * group chunks); geometry-column planning on request (covt_device_plan_geometry).  Property columns
+ * and multi-GPU shards stay with the host plan.
  * Runs on `hip_stream` and synchronises it twice (three times when it splits: the stream count and
  * the descriptor count size the arrays).
  * Limits and memory: a tile of 0x7ff00000 bytes or more gets COVT_ERR_INVALID_ARG as its status
@@ -484,6 +485,20 @@ const uint32_t* covt_device_plan_order_device(const covt_device_plan* plan);
 /* copies of the device arrays into host memory (any pointer may be NULL) */
 int covt_device_plan_copy(const covt_device_plan* plan, covt_stream_info* streams, covt_stream_desc* descs,
                           int32_t* tile_status);
+/* Geometry assembly from a device plan (covt_plan_geometry_columns / covt_plan_geometry_descs built on
+ * the device, CovtParser.convertGeometryColumn's input): the first call of covt_device_plan_geometry
+ * (or covt_device_plan_assemble) builds the geometry-column records and launch-ordered descriptors on
+ * `hip_stream` -- the host plan's exactly -- and synchronises it; later calls return at once. */
+int covt_device_plan_geometry(covt_device_plan* plan, void* hip_stream);
+int64_t covt_device_plan_num_geometry_columns(const covt_device_plan* plan); /* 0 before geometry() */
+int64_t covt_device_plan_assembly_bytes(const covt_device_plan* plan);
+const covt_geom_desc* covt_device_plan_geometry_descs_device(const covt_device_plan* plan);
+int covt_device_plan_geometry_copy(const covt_device_plan* plan, covt_geom_info* infos, covt_geom_desc* descs);
+/* covt_assemble_geometry_device over the plan's geometry descriptors (built first if needed), after
+ * covt_device_plan_decode on the same stream: d_asm covt_device_plan_assembly_bytes bytes, d_gres one
+ * result per column in launch order (column c's at its covt_geom_info.desc_index). */
+int covt_device_plan_assemble(covt_device_plan* plan, const uint8_t* d_decoded, const covt_stream_result* d_res,
+                              uint8_t* d_asm, covt_geom_result* d_gres, void* hip_stream);
 /* the grouped decode launch over the plan's descriptors (covt_decode_streams_device_grouped):
  * d_out covt_device_plan_output_bytes bytes, d_res num_descs results (stream i's at its desc_index).
  * Asynchronous. */

@@ -42,6 +42,40 @@ def _assert_same_plan(hp, dp):
     assert descs.tobytes() == hp.descs.tobytes()
 
 
+def _assert_same_geometry(hp, dp):
+    """covt_device_plan_geometry: the host plan's geometry records (capacities, flags, 16-byte aligned
+    output slices, descriptor index) and launch-ordered geometry descriptors, byte for byte."""
+    assert dp.geometry() == hp.num_geometry_columns
+    assert dp.assembly_bytes == hp.assembly_bytes
+    g, d = dp.geometry_copy()
+    assert g.tobytes() == hp.geom.tobytes()
+    assert d.tobytes() == hp.gdescs.tobytes()
+
+
+def _assert_same_assembly(covt, hp, dp):
+    """Decode + assembly through the device plan (covt_device_plan_assemble) equal the host path's
+    (covt_plan_assemble_host), column by column, statuses included."""
+    import torch
+
+    d_out, d_res = dp.alloc()
+    d_asm, d_gres = dp.alloc_assembly()
+    dp.decode(d_out, d_res)
+    dp.assemble(d_out, d_res, d_asm, d_gres)
+    torch.cuda.synchronize()
+    asm_d = d_asm.cpu().numpy()[:dp.assembly_bytes]
+    gres_d = d_gres.cpu().numpy().view(covt.GEOM_RESULT_DTYPE)[:dp.num_geometry_columns]
+    if hp.num_geometry_columns:
+        gres_d = gres_d[hp.geom["desc_index"]]
+    asm_h, gres_h = hp.assemble_host()
+    assert np.array_equal(gres_d, gres_h)
+    for c in range(hp.num_geometry_columns):
+        if int(gres_h["status"][c]) != 0:
+            continue
+        x, y = hp.geometry_arrays(asm_h, gres_h, c), hp.geometry_arrays(asm_d, gres_d, c)
+        for f in ("geometry_offsets", "part_offsets", "ring_offsets", "coords"):
+            assert np.array_equal(getattr(x, f), getattr(y, f)), (c, f)
+
+
 def _assert_same_decode(covt, hp, dp):
     import torch
 
@@ -64,6 +98,8 @@ def test_fixtures_genc(covt, gpu_available, id_mode):
     dp = _device_plan(covt, hp, covt.FORMAT_GENC, id_mode)
     _assert_same_plan(hp, dp)
     _assert_same_decode(covt, hp, dp)
+    _assert_same_geometry(hp, dp)
+    _assert_same_assembly(covt, hp, dp)
 
 
 @pytest.mark.parametrize("optimized", [False, True], ids=["named", "optimized"])
@@ -75,6 +111,8 @@ def test_fixtures_gend(covt, gpu_available, decodable_tiles, optimized):
     assert (hp.tile_status == 0).all() and hp.num_streams > 0
     _assert_same_plan(hp, dp)
     _assert_same_decode(covt, hp, dp)
+    _assert_same_geometry(hp, dp)
+    _assert_same_assembly(covt, hp, dp)
 
 
 @pytest.mark.parametrize("fmt", [0, 1], ids=["genc", "gend"])
@@ -97,6 +135,7 @@ def test_malformed_tiles(covt, gpu_available, decodable_tiles, fmt):
     dp = _device_plan(covt, hp, fmt, 0)
     assert (hp.tile_status != 0).sum() >= 40
     _assert_same_plan(hp, dp)
+    _assert_same_geometry(hp, dp)
 
 
 def test_tile_outside_buffer(covt, gpu_available, decodable_tiles):
@@ -117,6 +156,7 @@ def test_tile_outside_buffer(covt, gpu_available, decodable_tiles):
     assert dp.num_streams == one.num_streams and dp.output_bytes == one.output_bytes
     empty = covt.DevicePlan(d_blob, offs[:0], sizes[:0])
     assert empty.num_streams == 0 and empty.output_bytes == 0
+    assert empty.geometry() == 0 and empty.assembly_bytes == 0
 
 
 def test_full_batch_plan(covt, gpu_available):
@@ -129,6 +169,7 @@ def test_full_batch_plan(covt, gpu_available):
     assert hp.num_descs == hp.num_streams and hp.family_counts[3] > 0  # COVT_FAMILY_LANE
     dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
     _assert_same_plan(hp, dp)
+    _assert_same_geometry(hp, dp)
 
 
 def _genc_layers(t: bytes):
@@ -198,6 +239,7 @@ def test_tiles_past_slot_capacity(covt, gpu_available, decodable_tiles, walk, fm
     dp = _device_plan(covt, hp, fmt, 0)
     _assert_same_plan(hp, dp)
     _assert_same_decode(covt, hp, dp)
+    _assert_same_geometry(hp, dp)
 
 
 def _assert_golden(covt, hp, dp, keys, golden_streams):
@@ -240,6 +282,7 @@ def test_split_default_options(covt, gpu_available, decodable_tiles, golden_stre
     dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
     _assert_same_plan(hp, dp)
     _assert_golden(covt, hp, dp, keys, golden_streams)
+    _assert_same_assembly(covt, hp, dp)  # split descriptors feed the assembly's stream results
 
 
 @pytest.mark.parametrize("kw", [dict(split_min=0, split_ratio=0, split_chunk=64, split_values=256),
@@ -297,3 +340,4 @@ def test_split_malformed_streams(covt, gpu_available, decodable_tiles):
     dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
     _assert_same_plan(hp, dp)
     _assert_same_decode(covt, hp, dp)
+    _assert_same_assembly(covt, hp, dp)

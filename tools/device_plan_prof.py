@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Profiling target: covt_device_plan_create on the bench batch (BASELINE config 5) N times, wall-clock per
 creation printed (run under rocprofv3 --kernel-trace --stats [--hip-trace] for the per-kernel / per-call
-breakdown).  usage: device_plan_prof.py [reps] [--sweep | --small | --n256] [--nosplit] [--sorted]
---sweep: also batches of 1 tile (the library's largest), 256, 2048 and 4096 tiles (latency vs. occupancy)."""
+breakdown).  usage: device_plan_prof.py [reps] [--sweep | --small | --n256] [--nosplit] [--sorted] [--geometry]
+--sweep: also batches of 1 tile (the library's largest), 256, 2048 and 4096 tiles (latency vs. occupancy).
+--geometry: also time covt_device_plan_geometry (the geometry-column planning) after each creation."""
 import os
 import sys
 import time
@@ -44,15 +45,23 @@ def run(covt, tiles, reps, label):
     d_blob = torch.from_numpy(blob).cuda()
     d_off = torch.from_numpy(offs.astype(np.int64)).cuda()
     d_size = torch.from_numpy(sizes.astype(np.int64)).cuda()
-    ts = []
+    ts, tg = [], []
     for _ in range(reps + 2):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         dp = covt.DevicePlan(d_blob, d_off, d_size, options=covt.PlanOptions(split_min=-1) if "--nosplit" in sys.argv else None)
         ts.append(time.perf_counter() - t0)
+        if "--geometry" in sys.argv:
+            t0 = time.perf_counter()
+            dp.geometry()
+            tg.append(time.perf_counter() - t0)
         dp.close()
     print("%s %s device plan: median %.3f ms, min %.3f ms over %d" % (os.environ.get("COVT_LIB_VARIANT", "libcovt.so"), label,
                                                                    np.median(ts[2:]) * 1e3, min(ts[2:]) * 1e3, reps))
+    if tg:
+        print("%s %s geometry planning: median %.3f ms, min %.3f ms (%d columns)"
+              % (os.environ.get("COVT_LIB_VARIANT", "libcovt.so"), label, np.median(tg[2:]) * 1e3, min(tg[2:]) * 1e3,
+                 dp.num_geometry_columns))
 
 
 if __name__ == "__main__":
