@@ -1250,6 +1250,27 @@ __device__ __forceinline__ void sum_values(const uint32_t (&v)[K], int64_t base,
         ay += odd ? z : 0u;
     }
 }
+// The block loop's vmcnt waits.  Loads and stores retire in issue order through one counter (gfx950
+// has no separate store counter), and the compiler sizes each wait at the loop header for the path
+// with the fewest younger operations.  A page's first block is reached from the prefetch alone (no
+// stores after it); every later block from the previous block's output stores.  Without help the wait
+// for block j's prefetched words therefore also waited for block j-1's output stores on every other
+// block (`s_waitcnt vmcnt(1)` instead of vmcnt(3) for Morton).  So the prefetch of the first block is
+// followed by the same number of 16-byte stores as a block's sink issues: zeros, cached (they merge in
+// L2 with the nontemporal stores of the real values that follow to the same addresses, from the same
+// lane, in order).
+template <int OP>
+__device__ __forceinline__ void fpf_prime_stores(uint8_t* __restrict__ out, int64_t base) {
+    const int64_t i0 = base + 4 * (int64_t)lane_id();
+    const int4 z = make_int4(0, 0, 0, 0);
+    if constexpr (OP == COVT_OP_FPF_DELTA_MORTON) {
+        int4* o = (int4*)((int32_t*)out + 2 * i0);
+        o[0] = z;
+        o[1] = z;
+    } else {
+        *(int4*)((int32_t*)out + i0) = z;
+    }
+}
 // (sum_only is a run-time flag: two template copies inlined into one chunk kernel made it 248 VGPRs)
 // `skip`: a split chunk's state at its first block (header offset, packed-word offset, exception
 // cursors), filled by the first pass and reused by the second.
@@ -1490,11 +1511,6 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                 }
                 COVT_PHASE(c, 0);  // (the pre-walk counts with the directory)
             }
-            if (jb0 < nblocks && !c.err) {
-                c.err = walk(cur0, h);
-                if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
-                if (!c.err) prefetch(h, pk, pre, 0);
-            }
             // one block; the loop below alternates two register sets so that no in-flight prefetch
             // register is ever copied (a copy would force the vmcnt wait at the end of the iteration)
             auto block = [&](int32_t j, const FpfPre& pc, FpfPre& pn, int slot) {
@@ -1611,9 +1627,20 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                 COVT_PHASE(c, 5);
             };
             FpfPre preB;
-            for (int32_t j = jb0; j < nblocks && !c.err; j += 2) {
-                block(j, pre, preB, 0);
-                if (j + 1 < nblocks && !c.err) block(j + 1, preB, pre, 1);
+            if (jb0 < nblocks && !c.err) {
+                c.err = walk(cur0, h);
+                if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
+                if (!c.err) {
+                    prefetch(h, pk, pre, 0);
+                    // (the loop is entered only from here, so its header sees these stores on every path)
+                    if (!sum_only) fpf_prime_stores<OP>(c.out, (int64_t)done + (int64_t)jb0 * kFpfBlock);
+                    int32_t j = jb0;
+                    do {
+                        block(j, pre, preB, 0);
+                        if (j + 1 < nblocks && !c.err) block(j + 1, preB, pre, 1);
+                        j += 2;
+                    } while (j < nblocks && !c.err);
+                }
             }
             done += thissize;
             p = ie;
