@@ -947,7 +947,35 @@ __device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
                 const uint32_t lc = lv ? (uint32_t)take : 0u;
                 const uint32_t linc = incl_scan(lc);
                 const int32_t U = (int32_t)lane_bcast(linc, 63);
-                if (U > 0) {
+                // Dictionary-index columns are mostly literal groups of one-byte varints (values < 128):
+                // when every literal value of the batch is one byte (a group's `take` values end on
+                // `take` consecutive terminators right after its header), value u is the window byte
+                // u + (its group's first value byte - the group's first u), no varint parse.
+                const bool one = !lv || (int32_t)sm.u.v.list[lv ? rr + take - 1 : 0] == pg + take;
+                if (U > 0 && __ballot(!one) == 0) {
+                    const uint64_t lm = __ballot(lv), below = (1ull << l) - 1ull;
+                    const int32_t nl = __popcll(lm);
+                    const int32_t dst = lv ? __popcll(lm & below) : nl + __popcll(~lm & below);
+                    const int32_t ust = (int32_t)(linc - lc);
+                    // byte and output offsets relative to u, 15 + 17 bits (pg < 1024, ust and goff - out0 < 2^14)
+                    const uint32_t pk = (uint32_t)(pg + 1 - ust + 16384) | ((uint32_t)(goff - out0 - ust) << 15);
+                    const int32_t cust = __builtin_amdgcn_ds_permute(dst << 2, lv ? ust : 0x3fffffff);
+                    const uint32_t cpk = (uint32_t)__builtin_amdgcn_ds_permute(dst << 2, (int32_t)pk);
+                    for (int32_t u0 = 0; u0 < U; u0 += 64) {
+                        const int32_t s = cust - u0;
+                        const uint64_t mask = wave_or64(s > 0 && s < 64 ? 1ull << s : 0ull);
+                        const int32_t gb = __popcll(__ballot(cust <= u0)) - 1;  // group holding value u0
+                        const int32_t gk = gb + __popcll(mask & ((2ull << l) - 1ull));
+                        const uint32_t info = (uint32_t)lane_get((int32_t)cpk, gk);
+                        const int32_t u = u0 + l;
+                        if (u < U) {
+                            const uint32_t b = win_byte(sm, u + (int32_t)(info & 0x7fffu) - 16384);
+                            const int32_t o = out0 + u + (int32_t)(info >> 15);
+                            if (to_i32) st_out((int32_t*)c.out + o, (int32_t)b);
+                            else store(o, (uint64_t)b);
+                        }
+                    }
+                } else if (U > 0) {
                     const uint64_t lm = __ballot(lv), below = (1ull << l) - 1ull;
                     const int32_t nl = __popcll(lm);
                     const int32_t dst = lv ? __popcll(lm & below) : nl + __popcll(~lm & below);

@@ -5,6 +5,7 @@ twice to average out drift): config-5 grouped launch, each family alone, BASELIN
   python tools/ab.py libcovt_base.so libcovt.so [...]      (files in cov-tiles_amd/)
   python tools/ab.py libcovt.so libcovt.so:split_min=0       (same build, plan options per variant)
   python tools/ab.py --one libcovt.so                        (one measurement, internal)
+  AB_PROPS=1 python tools/ab.py ...                          (the property plan: every column's streams)
 """
 import json
 import os
@@ -28,7 +29,9 @@ def measure():
     lib = bench.tile_library()
     picks = bench.sample_batch(lib, 10000, bench.SEED)
     opts = covt.PlanOptions(**json.loads(os.environ.get("AB_PLAN_OPTIONS", "{}")))
-    plan = covt.Plan.from_tiles([t for _, t in picks], options=opts)
+    # AB_PROPS=1: the plan also decodes every property column's streams (COVT_PLAN_PROPERTIES)
+    flags = covt.PLAN_PROPERTIES if os.environ.get("AB_PROPS") else 0
+    plan = covt.Plan.from_tiles([t for _, t in picks], options=opts, flags=flags)
     batch = covt.DeviceBatch(plan, "cuda")
     s = torch.cuda.current_stream()
     L = covt.lib()
@@ -53,7 +56,7 @@ def measure():
             np.repeat(np.arange(covt.NUM_FAMILIES), plan.family_counts)[plan.streams["desc_index"]] == f)[0]))
         out[name] = timed(lambda: sub.decode(s))
         del sub
-    for name in bench.CONFIG_LEGS:
+    for name in ([] if flags else bench.CONFIG_LEGS):
         cp = bench.config_tiles(lib, name)
         cplan = covt.Plan.from_tiles([t for _, t in cp], options=opts)
         cb = covt.DeviceBatch(cplan, "cuda")
