@@ -914,17 +914,27 @@ __device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
                 int32_t delta = 0;
                 if (rv) {
                     delta = (int32_t)(int8_t)win_byte(sm, pg + 1);
-                    const uint64_t raw = win_vulong(sm, pg + 2, sm.u.v.list[rr]);
-                    b64 = is_signed ? zz64(raw) : (int64_t)raw;
+                    if (to_i32) {  // (int): the low 32 bits of the base, 32-bit arithmetic from here on
+                        b64 = (int64_t)(int32_t)win_vulong_lo32(sm, pg + 2, sm.u.v.list[rr]);
+                    } else {
+                        const uint64_t raw = win_vulong(sm, pg + 2, sm.u.v.list[rr]);
+                        b64 = is_signed ? zz64(raw) : (int64_t)raw;
+                    }
                 }
                 const bool small = rv && take <= 8;
                 const int32_t tmax = (int32_t)wave_max((uint32_t)(small ? take : 0));
-                if (small) {
+                if (small && to_i32) {
+                    int32_t* const o = (int32_t*)c.out + goff;
+                    const uint32_t b32 = (uint32_t)b64;
+                    for (int32_t i0 = 0; i0 < tmax; ++i0) {
+                        const int32_t i = i0 < take ? i0 : take - 1;
+                        st_out(o + i, (int32_t)(b32 + (uint32_t)(i * delta)));
+                    }
+                } else if (small) {
                     for (int32_t i0 = 0; i0 < tmax; ++i0) {
                         const int32_t i = i0 < take ? i0 : take - 1;
                         const int64_t v = (int64_t)((uint64_t)b64 + (uint64_t)(int64_t)(int32_t)(i * delta));
-                        if (to_i32) st_out((int32_t*)c.out + goff + i, (int32_t)v);
-                        else st_out((int64_t*)c.out + goff + i, v);
+                        st_out((int64_t*)c.out + goff + i, v);
                     }
                 }
                 uint64_t bigm = __ballot(rv && take > 8);
