@@ -30,9 +30,12 @@ constexpr int64_t kFusedMaxWaves = 4096;
 
 // Plan rule for the lane-per-stream kernel: RLE streams of at most kLaneMaxValues values and
 // kLaneMaxBytes bytes (a lane decodes serially; larger streams amortise a wave's window setup).
-constexpr int32_t kLaneMaxValues = 256;
+#ifndef COVT_LANE_MAX_VALUES
+#define COVT_LANE_MAX_VALUES 256
+#endif
+constexpr int32_t kLaneMaxValues = COVT_LANE_MAX_VALUES;
 constexpr int64_t kLaneMinStreams = COVT_LANE_MIN_STREAMS;  // plans with fewer lane-eligible streams use no lane kernel
-constexpr int32_t kLaneMaxBytes = COVT_LANE_MAX_BYTES;  // the lane's first 68-byte window: no reloads
+constexpr int32_t kLaneMaxBytes = COVT_LANE_MAX_BYTES;  // the lane slides its 68-byte window forward as it reads
 
 // The caller's plan options checked and completed (NULL: the defaults); false for a wrong struct
 // size or out-of-range fields.  Shared by the host and the device plan.

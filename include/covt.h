@@ -161,7 +161,7 @@ enum covt_op {
 #define COVT_SPLIT_VALUES 2048 /* default FastPFOR chunk values, whole blocks (covt_plan_options.split_values) */
 #define COVT_SPLIT_MIN 8192   /* default: streams costlier than this are split (covt_plan_options.split_min) */
 #define COVT_SPLIT_RATIO 3000 /* ... and than the plan's total cost / this (covt_plan_options.split_ratio) */
-#define COVT_LANE_MAX_BYTES 64      /* default covt_plan_options.lane_max_bytes */
+#define COVT_LANE_MAX_BYTES 256     /* default covt_plan_options.lane_max_bytes */
 #define COVT_LANE_MIN_STREAMS 16384 /* default covt_plan_options.lane_min_streams */
 
 /* Plan-layout options.  Every plan property that used to be steered by the environment is a field

@@ -272,4 +272,4 @@ def test_options_validated(covt):
             covt.Plan.from_tiles([_tile()], options=covt.PlanOptions(**kw))
     o = covt.PlanOptions()
     assert (o.split_min, o.split_ratio, o.split_chunk, o.split_values, o.lane_max_bytes, o.lane_min_streams) == \
-        (8192, 3000, 2048, 2048, 64, 16384)
+        (8192, 3000, 2048, 2048, 256, 16384)
