@@ -921,7 +921,11 @@ __device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
                         b64 = is_signed ? zz64(raw) : (int64_t)raw;
                     }
                 }
+#if defined(COVT_ABL_RLE_NORUN)  // ablation build: runs not expanded (outputs wrong)
+                const bool small = false;
+#else
                 const bool small = rv && take <= 8;
+#endif
                 const int32_t tmax = (int32_t)wave_max((uint32_t)(small ? take : 0));
                 if (small && to_i32) {
                     int32_t* const o = (int32_t*)c.out + goff;
@@ -956,7 +960,11 @@ __device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
                 const bool lv = gv && !isrun && take > 0;
                 const uint32_t lc = lv ? (uint32_t)take : 0u;
                 const uint32_t linc = incl_scan(lc);
+#if defined(COVT_ABL_RLE_NOLIT)  // ablation build: literals not expanded (outputs wrong)
+                const int32_t U = 0 * (int32_t)lane_bcast(linc, 63);
+#else
                 const int32_t U = (int32_t)lane_bcast(linc, 63);
+#endif
                 // Dictionary-index columns are mostly literal groups of one-byte varints (values < 128):
                 // when every literal value of the batch is one byte (a group's `take` values end on
                 // `take` consecutive terminators right after its header), value u is the window byte
