@@ -2209,7 +2209,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
 }
 
 // --------------------------------------------------------------------------------------------
-// lane-per-stream path: small RLE streams (<= kLaneMaxValues values, flagged by the plan), one
+// lane-per-stream path: small RLE streams (the plan's lane limits, flagged by the plan), one
 // stream per lane, decoded serially the way RunLengthIntegerReader / RunLengthByteReader read them.
 // A wave-per-stream decode spends its fixed window/index setup on a handful of values; here 64
 // such streams share one wave's instructions.

@@ -1340,13 +1340,17 @@ extern "C" {
 }  // extern "C"
 
 bool covt_resolve_options(const covt_plan_options* in, covt_plan_options& o) {
+    covt_plan_options d;
     if (!in) {
-        covt_plan_options_init(&o);
-        return true;
+        covt_plan_options_init(&d);
+        in = &d;
     }
     if (in->size != sizeof(covt_plan_options)) return false;
     o = *in;
-    return o.split_ratio >= 0 && o.split_chunk >= 64 && o.split_values >= 256 && o.split_values % 256 == 0 &&
+    const bool props = (o.flags & COVT_PLAN_PROPERTIES) != 0;
+    if (o.lane_max_bytes == 0) o.lane_max_bytes = props ? COVT_LANE_MAX_BYTES_PROPS : COVT_LANE_MAX_BYTES;
+    if (o.lane_max_values == 0) o.lane_max_values = props ? COVT_LANE_MAX_VALUES_PROPS : COVT_LANE_MAX_VALUES;
+    return o.lane_max_bytes <= 65535 && o.lane_max_values > 0 && o.lane_max_values <= 32767 && o.split_ratio >= 0 && o.split_chunk >= 64 && o.split_values >= 256 && o.split_values % 256 == 0 &&
            o.fpf_split_weight >= 1 && o.lane_min_streams >= 0 && o.plan_threads >= 0 && o.prefault_threads >= 1 &&
            o.device_walk >= 0 && o.device_walk <= 256 && (o.host_prefault == 0 || o.host_prefault == 1);
 }
@@ -1363,7 +1367,8 @@ void covt_plan_options_init(covt_plan_options* o) {
     o->split_chunk = COVT_SPLIT_CHUNK;
     o->split_values = COVT_SPLIT_VALUES;
     o->fpf_split_weight = 1;
-    o->lane_max_bytes = COVT_LANE_MAX_BYTES;
+    o->lane_max_bytes = 0;   // auto: COVT_LANE_MAX_BYTES, or COVT_LANE_MAX_BYTES_PROPS with property columns
+    o->lane_max_values = 0;  // auto: COVT_LANE_MAX_VALUES, or COVT_LANE_MAX_VALUES_PROPS
     o->lane_min_streams = COVT_LANE_MIN_STREAMS;
     o->plan_threads = 0;
     o->host_prefault = 1;
@@ -1535,7 +1540,7 @@ int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, co
     };
     int64_t split_min = o.split_min;
     const int64_t split_ratio = o.split_ratio;
-    int32_t lane_max = o.lane_max_bytes;
+    int32_t lane_max = lane_limits(o.lane_max_bytes, o.lane_max_values);
     {
         // batch totals: cost (split threshold) and the streams the lane kernel would take (it decodes 64
         // streams per wave, each serially: a wave of 100-250-value streams takes ~80-110 us, worth it only

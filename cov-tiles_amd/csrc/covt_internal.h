@@ -28,22 +28,22 @@ int covt_launch_fused(const uint8_t* d_in, const covt_stream_desc* d_desc, const
 // decode in one fused launch instead of the forked per-family launches
 constexpr int64_t kFusedMaxWaves = 4096;
 
-// Plan rule for the lane-per-stream kernel: RLE streams of at most kLaneMaxValues values and
-// kLaneMaxBytes bytes (a lane decodes serially; larger streams amortise a wave's window setup).
-#ifndef COVT_LANE_MAX_VALUES
-#define COVT_LANE_MAX_VALUES 256
-#endif
-constexpr int32_t kLaneMaxValues = COVT_LANE_MAX_VALUES;
+// Plan rule for the lane-per-stream kernel: RLE streams of at most max_values values and max_bytes bytes
+// (a lane decodes serially; larger streams amortise a wave's window setup).  The two limits travel
+// packed as one int32 (values << 16 | bytes; < 0: no lane family), see lane_limits.
 constexpr int64_t kLaneMinStreams = COVT_LANE_MIN_STREAMS;  // plans with fewer lane-eligible streams use no lane kernel
-constexpr int32_t kLaneMaxBytes = COVT_LANE_MAX_BYTES;  // the lane slides its 68-byte window forward as it reads
 
-// The caller's plan options checked and completed (NULL: the defaults); false for a wrong struct
-// size or out-of-range fields.  Shared by the host and the device plan.
+// The caller's plan options checked and completed (NULL: the defaults; auto lane limits resolved from the
+// flags); false for a wrong struct size or out-of-range fields.  Shared by the host and the device plan.
 bool covt_resolve_options(const covt_plan_options* in, covt_plan_options& out);
-__host__ __device__ inline bool lane_stream(int op, int32_t num_values, int32_t byte_length, int32_t max_bytes = kLaneMaxBytes) {
-    return (op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_BYTE_RLE_RAW || op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_S64 ||
+__host__ __device__ inline int32_t lane_limits(int32_t max_bytes, int32_t max_values) {
+    return max_bytes < 0 ? -1 : (int32_t)(((uint32_t)max_values << 16) | (uint32_t)max_bytes);
+}
+__host__ __device__ inline bool lane_stream(int op, int32_t num_values, int32_t byte_length, int32_t limits) {
+    return limits >= 0 &&
+           (op == COVT_OP_BYTE_RLE_U8 || op == COVT_OP_BYTE_RLE_RAW || op == COVT_OP_RLE_U64 || op == COVT_OP_RLE_S64 ||
             op == COVT_OP_RLE_I32) &&
-           num_values >= 0 && num_values <= kLaneMaxValues && byte_length >= 0 && byte_length <= max_bytes;
+           num_values >= 0 && num_values <= (limits >> 16) && byte_length >= 0 && byte_length <= (limits & 0xffff);
 }
 inline int desc_family(const covt_stream_desc& d) {
     if (d.flags & (COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD))

@@ -1647,7 +1647,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     uint32_t *v0 = (uint32_t*)(sa + o_v0), *v1 = (uint32_t*)(sa + o_v1);
     p->d_order = v1;
     p->d_desc = (covt_stream_desc*)(sa + o_d);
-    const int32_t lane_max = o.lane_max_bytes;
+    const int32_t lane_max = lane_limits(o.lane_max_bytes, o.lane_max_values);
     const int64_t lane_min = o.lane_min_streams;
     if (n_tiles) {
         if (slots) {

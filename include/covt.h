@@ -161,7 +161,10 @@ enum covt_op {
 #define COVT_SPLIT_VALUES 2048 /* default FastPFOR chunk values, whole blocks (covt_plan_options.split_values) */
 #define COVT_SPLIT_MIN 8192   /* default: streams costlier than this are split (covt_plan_options.split_min) */
 #define COVT_SPLIT_RATIO 3000 /* ... and than the plan's total cost / this (covt_plan_options.split_ratio) */
-#define COVT_LANE_MAX_BYTES 256     /* default covt_plan_options.lane_max_bytes */
+#define COVT_LANE_MAX_BYTES 256     /* covt_plan_options.lane_max_bytes 0 (auto): Id / Geometry plans */
+#define COVT_LANE_MAX_BYTES_PROPS 512 /* ... plans with COVT_PLAN_PROPERTIES */
+#define COVT_LANE_MAX_VALUES 256    /* covt_plan_options.lane_max_values 0 (auto): Id / Geometry plans */
+#define COVT_LANE_MAX_VALUES_PROPS 512 /* ... plans with COVT_PLAN_PROPERTIES */
 #define COVT_LANE_MIN_STREAMS 16384 /* default covt_plan_options.lane_min_streams */
 
 /* Plan-layout options.  Every plan property that used to be steered by the environment is a field
@@ -178,7 +181,8 @@ typedef struct covt_plan_options {
     int64_t split_chunk;       /* bytes of cost per varint / RLE chunk (>= 64) */
     int64_t split_values;      /* values per FastPFOR chunk (a multiple of 256, >= 256) */
     int32_t fpf_split_weight;  /* a FastPFOR stream's output counted this many times in its split cost (>= 1) */
-    int32_t lane_max_bytes;    /* RLE streams of <= this many bytes and <= 256 values go to the lane family ... */
+    int32_t lane_max_bytes;    /* RLE streams of <= this many bytes (<= 65535; 0: auto, COVT_LANE_MAX_BYTES or
+                                  _PROPS with property columns) and <= lane_max_values values go to the lane family ... */
     int64_t lane_min_streams;  /* ... when the plan holds at least this many of them (lane_max_bytes < 0: never) */
     int32_t plan_threads;      /* host threads of covt_plan_create (0: min(hardware threads, 16)) */
     int32_t host_prefault;     /* decode_host into pageable memory: fault the output pages in on host threads
@@ -186,6 +190,8 @@ typedef struct covt_plan_options {
     int32_t prefault_threads;  /* those threads (default 8) */
     int32_t device_walk;       /* covt_device_plan: 0 = a wave per tile with per-tile slots (default),
                                   1 = the same walk twice (no slots), k >= 2: k tiles per workgroup, a lane each */
+    int32_t lane_max_values;   /* the lane family's value limit (<= 32767; 0: auto, COVT_LANE_MAX_VALUES or _PROPS with
+                                  property columns, whose many small dictionary-index streams favour longer lanes) */
 } covt_plan_options;
 void covt_plan_options_init(covt_plan_options* opts);
 

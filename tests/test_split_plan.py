@@ -271,5 +271,8 @@ def test_options_validated(covt):
         with pytest.raises(covt.IllegalArgumentException):
             covt.Plan.from_tiles([_tile()], options=covt.PlanOptions(**kw))
     o = covt.PlanOptions()
-    assert (o.split_min, o.split_ratio, o.split_chunk, o.split_values, o.lane_max_bytes, o.lane_min_streams) == \
-        (8192, 3000, 2048, 2048, 256, 16384)
+    assert (o.split_min, o.split_ratio, o.split_chunk, o.split_values, o.lane_max_bytes, o.lane_min_streams,
+            o.lane_max_values) == (8192, 3000, 2048, 2048, 0, 16384, 0)  # lane limits 0: auto by plan flags
+    for kw in ({"lane_max_bytes": 65536}, {"lane_max_values": 32768}, {"lane_max_values": -1}):
+        with pytest.raises(covt.IllegalArgumentException):
+            covt.Plan.from_tiles([_tile()], options=covt.PlanOptions(**kw))
