@@ -161,7 +161,7 @@ enum covt_op {
 #define COVT_SPLIT_VALUES 2048 /* default FastPFOR chunk values, whole blocks (covt_plan_options.split_values) */
 #define COVT_SPLIT_MIN 8192   /* default: streams costlier than this are split (covt_plan_options.split_min) */
 #define COVT_SPLIT_RATIO 3000 /* ... and than the plan's total cost / this (covt_plan_options.split_ratio) */
-#define COVT_LANE_MAX_BYTES 256     /* covt_plan_options.lane_max_bytes 0 (auto): Id / Geometry plans */
+#define COVT_LANE_MAX_BYTES 128     /* covt_plan_options.lane_max_bytes 0 (auto): Id / Geometry plans */
 #define COVT_LANE_MAX_BYTES_PROPS 512 /* ... plans with COVT_PLAN_PROPERTIES */
 #define COVT_LANE_MAX_VALUES 256    /* covt_plan_options.lane_max_values 0 (auto): Id / Geometry plans */
 #define COVT_LANE_MAX_VALUES_PROPS 512 /* ... plans with COVT_PLAN_PROPERTIES */
