@@ -22,4 +22,6 @@ python tools/pmc_traffic.py gpurun_out > "gpurun_out/$R/pmc_traffic.txt"
 cp profiles/pmc_traffic.json "gpurun_out/$R/pmc_traffic.json"
 timeout -k 10 600 python bench.py > "gpurun_out/$R/bench.json" 2> "gpurun_out/$R/bench.err"
 timeout -k 10 300 python tools/config_timeline.py > "gpurun_out/$R/config_timeline.txt" 2>&1
+timeout -k 10 300 python tools/op_breakdown.py > "gpurun_out/$R/op_breakdown.txt" 2>&1
+OPB_PROPS=1 timeout -k 10 300 python tools/op_breakdown.py > "gpurun_out/$R/op_breakdown_props.txt" 2>&1
 echo "profile session done"
