@@ -2214,7 +2214,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
 // A wave-per-stream decode spends its fixed window/index setup on a handful of values; here 64
 // such streams share one wave's instructions.
 // --------------------------------------------------------------------------------------------
-constexpr int kLaneSlot = 17;  // LDS dwords per lane: a 68-byte sliding window of the lane's stream
+#ifndef COVT_LANE_SLOT
+#define COVT_LANE_SLOT 17
+#endif
+constexpr int kLaneSlot = COVT_LANE_SLOT;  // LDS dwords per lane: a sliding window of 4 * kLaneSlot bytes (68)
+static_assert(kLaneSlot % 4 == 1, "16-byte granules plus one dword");
 struct LaneBytes {  // the lane's stream through a window in its LDS slot; one-dword read cache
     const uint8_t* sb;
     uint32_t* slot;
@@ -2230,7 +2234,7 @@ struct LaneBytes {  // the lane's stream through a window in its LDS slot; one-d
         const int32_t need = avail - w0;  // window bytes that are stream bytes
         uint32_t st[kLaneSlot];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kLaneSlot / 4; ++k) {
             u32x4 v = {0u, 0u, 0u, 0u};
             if (16 * k < need) v = *(const __attribute__((address_space(1))) u32x4*)(a4 + 16 * k);
             st[4 * k] = v.x;
@@ -2238,7 +2242,7 @@ struct LaneBytes {  // the lane's stream through a window in its LDS slot; one-d
             st[4 * k + 2] = v.z;
             st[4 * k + 3] = v.w;
         }
-        st[16] = 64 < need ? *g32(a4 + 64) : 0u;
+        st[kLaneSlot - 1] = 4 * (kLaneSlot - 1) < need ? *g32(a4 + 4 * (kLaneSlot - 1)) : 0u;
 #pragma unroll
         for (int k = 0; k < kLaneSlot; ++k) slot[k * 256] = st[k];
         cq = -1;
