@@ -276,3 +276,26 @@ def test_options_validated(covt):
     for kw in ({"lane_max_bytes": 65536}, {"lane_max_values": 32768}, {"lane_max_values": -1}):
         with pytest.raises(covt.IllegalArgumentException):
             covt.Plan.from_tiles([_tile()], options=covt.PlanOptions(**kw))
+
+
+def test_lane_limits_auto_by_plan_flags(covt):
+    """covt_plan_options.lane_max_bytes / lane_max_values 0 = auto: RLE streams of <= 128 bytes and <= 256
+    values join the lane family of an Id/Geometry plan, <= 512 / 512 in a plan with property columns
+    (DESIGN.md §6.0); explicit limits override the auto ones."""
+    tiles = [_tile(n) for n in ("5_16_20", "10_530_682", "14_8298_10748")]
+    opts = covt.PlanOptions(lane_min_streams=0)  # no batch-size gate: every eligible stream is a lane stream
+
+    def lane_streams(plan):  # the lane family's descriptors (num_values: the values the kernel decodes)
+        d = plan.descs.view(DESC)
+        return d[(d["flags"] & covt.DESC_LANE) != 0]
+
+    for flags, max_b, max_v in ((0, 128, 256), (covt.PLAN_PROPERTIES, 512, 512)):
+        ls = lane_streams(covt.Plan.from_tiles(tiles, flags=flags, options=opts))
+        assert len(ls) > 0
+        assert ls["avail"].max() <= max_b and ls["num_values"].max() <= max_v
+        if flags:  # the property plan's longer lanes are used
+            assert ls["avail"].max() > 128
+    ls = lane_streams(covt.Plan.from_tiles(tiles, flags=covt.PLAN_PROPERTIES,
+                                           options=covt.PlanOptions(lane_min_streams=0, lane_max_bytes=64,
+                                                                    lane_max_values=100)))
+    assert ls["avail"].max() <= 64 and ls["num_values"].max() <= 100
