@@ -4,7 +4,8 @@ Geometry topology streams (GeometryOffsets / PartOffsets / RingOffsets: ORC RLE 
 COVT_OP_RLE_I32; DecodingUtils.decodeRle then the (int) cast of CovtParser.java:135-274) are written
 by the restated Gen D writer (oracle/gend.py) from synthetic int64 sequences chosen to stress the wave
 decoder rather than to be valid geometry: runs of 3-130 with every delta, literal groups of 1-128
-values from 1-byte to 10-byte varints (values past 2^31 truncate in the int cast), group boundaries
+values from 1-byte to 10-byte varints (values past 2^31 truncate in the int cast), long arithmetic
+sequences split into chains of runs with one delta across 2^32, group boundaries
 at every window offset, and long alternations of short runs and short literals (~200 groups/KiB,
 the walk-bound shape of dictionary-index streams).  GeometryType bytes include out-of-range values,
 which the reference rejects (GeometryType.values()[b]).  Streams are decoded in both Id modes."""
@@ -20,7 +21,7 @@ pytestmark = pytest.mark.gpu
 def _counts(rng, n):
     out = []
     while len(out) < n:
-        k = int(rng.integers(0, 6))
+        k = int(rng.integers(0, 7))
         if k == 0:  # arithmetic run, any delta the header can carry
             base = int(rng.integers(0, 1 << int(rng.integers(1, 62))))
             d = int(rng.integers(-128, 128))
@@ -40,8 +41,15 @@ def _counts(rng, n):
             out += [int(x) for x in rng.integers((1 << 31) - 3, (1 << 33), size=int(rng.integers(1, 40)))]
         elif k == 4:  # a long literal stretch (crosses 1 KiB windows)
             out += [int(x) for x in rng.integers(1 << 40, 1 << 56, size=int(rng.integers(100, 600)))]
-        else:  # constant run
+        elif k == 5:  # constant run
             out += [int(rng.integers(0, 1 << 16))] * int(rng.integers(3, 300))
+        else:  # a long arithmetic sequence (chains of runs with one delta, merged by the decoder) across 2^32
+            d = int(rng.integers(-128, 128))
+            m = int(rng.integers(131, 3000))
+            base = (1 << 32) - int(rng.integers(0, 200)) * max(abs(d), 1)
+            if base + d * m < 0:
+                d = abs(d)
+            out += [base + d * i for i in range(m)]
     return np.array(out[:n], dtype=np.int64)
 
 

@@ -75,8 +75,16 @@ def test_varint_java_cap_adversarial(covt, oracle, gpu_available, seed):
 def _rle_values(rng, n, signed):
     out = []
     while len(out) < n:
-        kind = rng.integers(0, 4)
-        if kind == 0:  # run with small delta
+        kind = rng.integers(0, 5)
+        if kind == 4:  # a long arithmetic sequence across a 2^32 multiple: a chain of runs with one delta
+            d = int(rng.integers(1, 128)) * (1 if rng.integers(0, 2) else -1)
+            m = int(rng.integers(131, 2000))
+            edge = int(rng.integers(1, 4)) << 32
+            base = (-edge if signed and rng.integers(0, 2) else edge) - d * int(rng.integers(0, m))
+            if not signed and base + d * m < 0:
+                base, d = edge, abs(d)
+            out += [base + i * d for i in range(m)]
+        elif kind == 0:  # run with small delta
             base = int(rng.integers(-(1 << 40), 1 << 40)) if signed else int(rng.integers(0, 1 << 40))
             d = int(rng.integers(-128, 128))
             out += [base + i * d for i in range(int(rng.integers(3, 300)))]
