@@ -61,11 +61,8 @@ def main():
         y = B["out"][lo:lo + int(A["n"][i]) * 4].view(np.int32)
         for r in range(lo_, hi_):
             w = int(y[r])
+            # (a debug build writing (group << 20 | run << 19 | group start << 4 | lane % 16) per output)
             print(r, "g", w >> 20, "run", (w >> 19) & 1, "gs", (w >> 4) & 0x7fff, "lane%16", w & 15)
-
-
-if __name__ == "__main__":
-    main()
 
 
 def dump(key, i, f):
@@ -80,5 +77,5 @@ def dump(key, i, f):
     open(f, "wb").write(np.asarray(plan.blob).view(np.uint8)[int(s["in_off"]):int(s["in_off"]) + int(s["byte_length"])].tobytes())
 
 
-if __name__ == "__main__" and os.environ.get("RLE_DUMP_RANGE"):
-    pass
+if __name__ == "__main__":
+    main()
