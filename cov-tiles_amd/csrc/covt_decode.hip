@@ -981,9 +981,15 @@ __device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
                     const uint32_t cpk = (uint32_t)__builtin_amdgcn_ds_permute(dst << 2, (int32_t)pk);
                     for (int32_t u0 = 0; u0 < U; u0 += 64) {
                         const int32_t s = cust - u0;
-                        const uint64_t mask = wave_or64(s > 0 && s < 64 ? 1ull << s : 0ull);
                         const int32_t gb = __popcll(__ballot(cust <= u0)) - 1;  // group holding value u0
-                        const int32_t gk = gb + __popcll(mask & ((2ull << l) - 1ull));
+                        // the groups starting inside the step mark their first value's lane (ds_permute: a lane
+                        // no one writes to reads 0, the instruction's defined result; groups without a start
+                        // inside send 0 to lane 0, which no start inside the step reaches), then a running
+                        // max gives each value its group (was: a 64-bit OR reduction and two popcounts;
+                        // property decode 4.44 -> 4.35 ms)
+                        const bool in = s > 0 && s < 64;
+                        const int32_t mk = __builtin_amdgcn_ds_permute(in ? s << 2 : 0, in ? l + 1 : 0);
+                        const int32_t gk = max(gb, (int32_t)incl_max_scan((uint32_t)mk) - 1);
                         const uint32_t info = (uint32_t)lane_get((int32_t)cpk, gk);
                         const int32_t u = u0 + l;
                         if (u < U) {
