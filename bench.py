@@ -712,8 +712,8 @@ def main():
             legs["configs"] = config_legs(lib, args, torch, dev, covt, stream)
 
     mine = {"rank": rank, "device": dev_name, "local_rank": local_rank, "seed": seed, "tiles": len(picks),
-            "stream_bytes": int(plan.in_bytes), "vertices": int(plan.vertices), "wall_s": wall,
-            "kernel_ms": kern_ms}
+            "streams": int(plan.num_streams), "stream_bytes": int(plan.in_bytes), "output_bytes": int(plan.out_bytes),
+            "vertices": int(plan.vertices), "wall_s": wall, "kernel_ms": kern_ms}
     if dist is not None:
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
@@ -727,8 +727,17 @@ def main():
     if rank == 0:
         ms_per_step = wall * 1e3 / args.steps
         value = tot_in * args.steps / wall / 1e9
-        alg_bytes = plan.in_bytes + plan.out_bytes  # stream bytes read + decoded bytes written
-        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        # stream bytes read + decoded bytes written, per rank over that rank's own launch time.
+        # `roofline` is per GPU: at N > 1 the slowest rank's (the minimum of each rank's own bytes over its
+        # own kernel time), with the whole job's aggregate (all ranks' bytes over the max time, against N
+        # peaks) beside it
+        for r in ranks:
+            r["alg_bytes"] = r["stream_bytes"] + r["output_bytes"]
+            r["achieved"] = r["alg_bytes"] / (r["kernel_ms"] * 1e-3) / 1e9 if r["kernel_ms"] > 0 else 0.0
+        slow = min(ranks, key=lambda r: r["achieved"])
+        alg_bytes, achieved = slow["alg_bytes"], slow["achieved"]
+        agg_bytes = sum(r["alg_bytes"] for r in ranks)
+        agg_achieved = agg_bytes / (kern_ms * 1e-3) / 1e9
         traffic, traffic_note = None, "no profiles/pmc_traffic.json"
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
@@ -762,19 +771,37 @@ def main():
                                    "all Id+Geometry streams" % (len(picks), args.scaling),
                        "tiles_per_gpu": len(picks), "streams_per_gpu": plan.num_streams,
                        "stream_bytes_per_gpu": plan.in_bytes, "output_bytes_per_gpu": plan.out_bytes,
-                       "vertices_per_gpu": plan.vertices, "id_mode": "format" if args.id_mode == 0 else "java",
+                       "vertices_per_gpu": plan.vertices,
+                       "per_gpu_note": "*_per_gpu: rank 0's batch; every rank's own in per_rank" if len(ranks) > 1
+                       else "one GPU",
+                       "tiles_total": sum(r["tiles"] for r in ranks), "streams_total": sum(r["streams"] for r in ranks),
+                       "stream_bytes_total": int(tot_in), "output_bytes_total": sum(r["output_bytes"] for r in ranks),
+                       "vertices_total": int(tot_vx), "id_mode": "format" if args.id_mode == 0 else "java",
                        "parallelism": "dp%d (tile shards, no collective)" % len(ranks)},
             "mvert_per_s": round(tot_vx * args.steps / wall / 1e6, 2),
             "kernel_ms": round(kern_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_note": traffic_note,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic if len(ranks) == 1 else None, "traffic_note": traffic_note,
                          "kernel": "covt decode launch = decode_family_kernel<RLE|VARINT|FASTPFOR> + "
                                    "decode_lane_kernel run concurrently between fork/join events; "
-                                   "duration = HIP events on the launch stream (max over ranks)",
-                         "algorithmic_bytes_per_launch": alg_bytes},
+                                   "duration = HIP events on the launch stream",
+                         "per": "GPU: rank %d's own algorithmic bytes over its own mean launch time (the slowest "
+                                "rank of %d)" % (slow["rank"], len(ranks)),
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "aggregate": {"achieved": round(agg_achieved, 2), "peak": HBM_PEAK_GBS * len(ranks),
+                                       "frac": round(agg_achieved / (HBM_PEAK_GBS * len(ranks)), 4),
+                                       "algorithmic_bytes_per_launch": agg_bytes,
+                                       "note": "all ranks' bytes over the max-over-ranks launch time, N peaks"}},
+            "build": {"library": covt.library_build_id(), "sources": covt.source_build_id(),
+                      "match": covt.library_build_id() == covt.source_build_id(),
+                      "note": "sha256 prefix of libcovt's sources compiled into the library (Makefile BUILD_ID) "
+                              "and of the sources in this tree"},
             "cpu_baseline": None,
             "per_rank": [{"rank": r["rank"], "device": r["device"], "seed": r["seed"], "tiles": r["tiles"],
-                          "kernel_ms": round(r["kernel_ms"], 4),
+                          "streams": r["streams"], "stream_bytes": r["stream_bytes"],
+                          "output_bytes": r["output_bytes"], "kernel_ms": round(r["kernel_ms"], 4),
+                          "roofline_frac": round(r["achieved"] / HBM_PEAK_GBS, 4),
                           "gbps": round(r["stream_bytes"] * args.steps / r["wall_s"] / 1e9, 3)
                           if r["wall_s"] > 0 else None} for r in ranks],
         }

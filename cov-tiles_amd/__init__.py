@@ -1088,3 +1088,26 @@ class CovtParser:
 
 def version() -> str:
     return lib().covt_version().decode()
+
+
+# the files whose sha256 (in this order) the Makefile compiles into covt_version() as "src:<16 hex>"
+_BUILD_SOURCES = ("csrc/covt_decode.hip", "csrc/covt_assemble.hip", "csrc/covt_props.hip", "csrc/covt_plan_device.hip",
+                  "csrc/covt_host.cpp", "../include/covt.h", "csrc/covt_internal.h", "csrc/covt_wave.h",
+                  "csrc/covt_walk.h")
+
+
+def source_build_id() -> str:
+    """sha256 prefix of the library sources as they are in this tree (the Makefile's BUILD_ID)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in _BUILD_SOURCES:
+        with open(os.path.join(_HERE, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def library_build_id() -> str:
+    """The build id compiled into the loaded libcovt.so (covt_version)."""
+    v = version()
+    return v.rsplit("src:", 1)[1] if "src:" in v else "unknown"

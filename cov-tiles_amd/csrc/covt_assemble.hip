@@ -80,7 +80,10 @@ struct Coop {
         else __syncthreads();
     }
     __device__ __forceinline__ static bool any(bool p) { return NW == 1 ? __ballot(p) != 0ull : __syncthreads_or(p) != 0; }
-    // exclusive prefix of a per-thread value over the group (wave inclusive `inc` given), group total
+    // exclusive prefix of a per-thread value over the group (wave inclusive `inc` given, saturating),
+    // group total.  Sums saturate at 0xffffffff: every count is checked against a capacity below 2^31, so
+    // a saturated total fails the check, where a wrapped one could pass it (a 4096-item cooperative step
+    // of clamped counts can reach 2^32).  A saturated prefix is only ever stored for a failing column.
     __device__ __forceinline__ static uint32_t group_prefix(AsmSmemT<NW>& sm, uint32_t inc, uint32_t own,
                                                            uint32_t& tot, int buf) {
         if (NW == 1) {
@@ -93,11 +96,11 @@ struct Coop {
 #pragma unroll
         for (int i = 0; i < NW; ++i) {
             const uint32_t t = sm.red[buf][i];
-            pre += i < wid() ? t : 0u;
-            all += t;
+            pre = add_sat(pre, i < wid() ? t : 0u);
+            all = add_sat(all, t);
         }
         tot = all;
-        return pre + inc - own;
+        return add_sat(pre, inc - own);
     }
 };
 
@@ -110,14 +113,14 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {  // lane l - 1's val
 // that follows every read of its previous contents).
 template <int NW>
 __device__ __forceinline__ void excl_scan4(AsmSmemT<NW>& sm, int& buf, const uint32_t x[4], uint32_t ex[4], uint32_t& tot) {
-    const uint32_t s = x[0] + x[1] + x[2] + x[3];
-    const uint32_t inc = incl_scan(s);
+    const uint32_t s = add_sat(add_sat(x[0], x[1]), add_sat(x[2], x[3]));  // saturating: see group_prefix
+    const uint32_t inc = incl_scan_sat(s);
     uint32_t run = Coop<NW>::group_prefix(sm, inc, s, tot, buf);
     buf ^= 1;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         ex[k] = run;
-        run += x[k];
+        run = add_sat(run, x[k]);
     }
 }
 
@@ -298,7 +301,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 if (i < (uint32_t)n_go) {
                     const int32_t c = ((const g_i32*)go)[i];
                     bad_cnt |= c < 0;
-                    pf[k] = min((uint32_t)max(c, 0), pcap + 1u);  // clamped: the scans cannot wrap
+                    pf[k] = min((uint32_t)max(c, 0), pcap + 1u);  // clamped, and the scans saturate (group_prefix)
                 } else {
                     bad_cnt = true;
                 }
@@ -309,7 +312,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
         for (int k = 0; k < 4; ++k) ex[k] += P;
         store4<NW>(geo_off, f0, n - f0, ex);
         go_base += nm;
-        P += tot;
+        P = add_sat(P, tot);
         if (Coop<NW>::any(bad_type || bad_cnt) || P > pcap) break;
     }
     if (Coop<NW>::any(bad_type)) { res.status = COVT_ERR_BAD_HEADER; return; }  // GeometryType.values()[b]
@@ -362,7 +365,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
             store4<NW>(part_off, p0, L, ex);
             store4<NW>(part_scr, p0, L, scr);
             po_base += npo;
-            R += tot;
+            R = add_sat(R, tot);
             if (Coop<NW>::any(bad_cnt) || R > rcap) break;
         }
     }
@@ -417,8 +420,8 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
             store4<NW>(ring_off, r0, L, ex);
             store4<NW>(ring_scr, r0, L, src);
             ro_base += nr;
-            V += tv;
-            VS += ts;
+            V = add_sat(V, tv);
+            VS = add_sat(VS, ts);
             if (Coop<NW>::any(bad_cnt) || V > ccap || VS > (uint32_t)n_src) break;
         }
     }

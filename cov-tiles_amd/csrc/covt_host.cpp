@@ -1097,7 +1097,10 @@ void plan_property_layout(covt_plan* p) {
 
 extern "C" {
 
-const char* covt_version(void) { return "covt-mi355x 0.1 (gfx950)"; }
+#ifndef COVT_BUILD_ID
+#define COVT_BUILD_ID "unknown"
+#endif
+const char* covt_version(void) { return "covt-mi355x 0.4 (gfx950) src:" COVT_BUILD_ID; }
 
 int covt_device_count(int32_t* n) {
     int c = 0;

@@ -37,6 +37,20 @@ __device__ __forceinline__ uint32_t incl_scan(uint32_t x) {
     return x;
 }
 
+// unsigned add saturating at 0xffffffff (v_add_u32 with clamp)
+__device__ __forceinline__ uint32_t add_sat(uint32_t a, uint32_t b) { return __builtin_elementwise_add_sat(a, b); }
+// inclusive prefix sum over the 64 lanes saturating at 0xffffffff (same DPP sequence as incl_scan):
+// a sum that passes 2^32 - 1 stays there instead of wrapping, so a bound check on it cannot be fooled
+__device__ __forceinline__ uint32_t incl_scan_sat(uint32_t x) {
+    x = add_sat(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+    x = add_sat(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+    x = add_sat(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+    x = add_sat(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+    x = add_sat(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    x = add_sat(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return x;
+}
+
 // inclusive prefix sum of 64-bit values over the 64 lanes (same DPP sequence, carry by hand)
 __device__ __forceinline__ uint64_t incl_scan64(uint64_t x) {
     uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);

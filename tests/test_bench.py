@@ -32,6 +32,23 @@ def test_gpus2_dry_run_spawns_two_ranks():
     assert line["config"]["parallelism"].startswith("dp2")
     cb = line["cpu_baseline"]  # rank 0's batch, at every N (north_star: "next to the Java CPU decoder ... in the same run")
     assert cb is not None and cb["value"] > 0 and cb["kind"] == "port"
+    # N > 1 field semantics: byte totals are sums over ranks, each rank's own beside them;
+    # roofline is per GPU (the slowest rank's own bytes over its own time) with the aggregate against N peaks
+    cfg = line["config"]
+    assert cfg["stream_bytes_total"] == sum(r["stream_bytes"] for r in pr)
+    assert cfg["output_bytes_total"] == sum(r["output_bytes"] for r in pr)
+    assert cfg["streams_total"] == sum(r["streams"] for r in pr) and cfg["tiles_total"] == 80
+    assert cfg["stream_bytes_per_gpu"] == pr[0]["stream_bytes"]
+    assert pr[0]["stream_bytes"] != pr[1]["stream_bytes"]  # distinct batches
+    rf = line["roofline"]
+    slow = min(pr, key=lambda r: r["roofline_frac"])
+    assert rf["frac"] == slow["roofline_frac"] and rf["peak"] == 8000.0
+    assert rf["algorithmic_bytes_per_launch"] == slow["stream_bytes"] + slow["output_bytes"]
+    agg = rf["aggregate"]
+    assert agg["peak"] == 16000.0 and agg["algorithmic_bytes_per_launch"] == cfg["stream_bytes_total"] + \
+        cfg["output_bytes_total"]
+    assert rf["traffic"] is None  # the PMC figure is a one-GPU, one-batch measurement
+    assert line["build"]["match"] and line["build"]["library"] == line["build"]["sources"]
 
 
 def test_gpus2_strong_dry_run_shards_one_batch():

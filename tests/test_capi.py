@@ -39,6 +39,12 @@ def test_kernel_compiled_for_gfx950():
     assert targets == {b"gfx950"}  # (hipcub's host-side arch tables name other targets as strings)
 
 
+def test_library_built_from_these_sources(covt):
+    """libcovt.so carries the sha256 of the sources it was compiled from (Makefile BUILD_ID): a library
+    that travels with the tree to the GPU box is the one these sources build (bench.py records both ids)."""
+    assert covt.library_build_id() == covt.source_build_id(), "stale libcovt.so: run __graft_entry__.build()"
+
+
 def test_struct_layouts(covt):
     import ctypes as C
 

@@ -175,6 +175,36 @@ def test_assembly_errors_cooperative(covt, oracle, gpu_available):
     _check_vs_oracle(oracle, cols, asm, gres, lay)
 
 
+def _overflow_column(n_multi, parts_each, n_vertices):
+    """n_multi MULTIPOINT features each claiming `parts_each` parts over a column of n_vertices point
+    vertices: the part total is n_multi * parts_each (2^32 for the cases below), which a wrapping uint32
+    scan would see as 0 <= part_cap and accept."""
+    return {"types": np.full(n_multi, 3, np.uint8), "go": np.full(n_multi, parts_each, np.int32),
+            "po": np.zeros(0, np.int32), "ro": np.zeros(0, np.int32), "vo": None,
+            "vb": np.zeros(2 * n_vertices, np.int32), "closed": False}
+
+
+def test_assembly_part_total_past_2_32(covt, oracle, gpu_available):
+    """clamped per-item counts summed over one step reach 2^32.  The scans saturate,
+    so the total fails the capacity check (COUNT_MISMATCH, as the oracle's 64-bit count says) instead of
+    wrapping to an accepted 0.  Cooperative path: 4096 features x 2^20 parts in one 4096-item step;
+    wave path (a batch of more than 4096 columns): 256 features x 2^24 parts in one 256-item step."""
+    coop = _overflow_column(4096, 1 << 20, 1 << 20)
+    assert A.caps(coop)[0] == 1 << 20  # per-item clamp at pcap + 1 leaves 2^20 each
+    asm, gres, lay = _run_kernel(covt, [coop])
+    assert gres["status"].tolist() == [covt.ERR_COUNT_MISMATCH]
+    o = oracle.assemble_geometry(coop["types"], coop["go"], coop["po"], coop["ro"], coop["vo"], coop["vb"],
+                                 coop["closed"], A.caps(coop))
+    assert o[0] == covt.ERR_COUNT_MISMATCH
+    # the single-wave path: past kCoopMaxColumns columns every column runs on one wave
+    wave = _overflow_column(256, 1 << 24, 1 << 24)
+    tiny = A.synth_column(np.random.default_rng(9), 1, False, False)
+    cols = [wave] + [tiny] * 4096
+    asm, gres, lay = _run_kernel(covt, cols)
+    assert int(gres["status"][0]) == covt.ERR_COUNT_MISMATCH
+    assert (gres["status"][1:] == 0).all()
+
+
 def test_batch_assembly_properties(covt, oracle, gpu_available):
     """BASELINE config-5 batch (10k sampled tiles): every column equals the oracle's assembly of its source
     tile (goldens reused per source tile), coordinate totals add up."""

@@ -36,6 +36,8 @@ for s in "$@"; do
     timeline_props) step timeline_props 300 python tools/stream_timeline.py --props ;;
     hbm) step hbm 300 python tools/hbm_probe.py ;;
     wpat) step wpat 300 python tools/probe/write_pattern.py ;;
+    ceiling) step ceiling 300 python tools/probe/hbm_ceiling.py ;;
+    layout) step layout 300 python tools/probe/layout_ab.py ;;
     ab|ab_props) [ "$s" = ab_props ] && export OPB_PROPS=1
         for v in ${AB_VARIANTS:-libcovt_base.so libcovt.so libcovt_base.so libcovt.so}; do
             echo "== ab $v"; COVT_LIB_VARIANT=$v OPB_QUICK=1 timeout -k 10 300 python tools/op_breakdown.py 2>&1 | grep -v amdgpu.ids || fatal ab $?
