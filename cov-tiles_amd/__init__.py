@@ -42,6 +42,7 @@ DESC_LANE, DESC_SPLIT, DESC_SPLIT_PAD, DESC_SPLIT_FPF = 0x1, 0x2, 0x4, 0x8
 DESC_SPLIT_RLE = 0x10
 SPLIT_SLOTS = 8
 ID_FORMAT, ID_JAVA = 0, 1
+LAUNCH_AUTO, LAUNCH_FUSED, LAUNCH_FORKED = 0, 1, 2
 
 (OP_NONE, OP_BYTE_RLE_U8, OP_RLE_U64, OP_RLE_I32, OP_RLE_S64, OP_VARINT_I32, OP_VARINT_ZZ_I32,
  OP_VARINT_ZZ_DELTA_I32, OP_VARINT_ZZ_DELTA_XY, OP_VARINT_DELTA_MORTON, OP_FPF_ZZ_DELTA_I32, OP_FPF_ZZ_DELTA_XY,
@@ -175,6 +176,7 @@ EXPORTED_SYMBOLS = (
     "covt_plan_totals", "covt_plan_streams", "covt_plan_descs", "covt_plan_tile_status",
     "covt_decode_streams_device", "covt_plan_decode_host", "covt_plan_decode_host_multi", "covt_version",
     "covt_device_count", "covt_plan_family_counts", "covt_decode_streams_device_grouped",
+    "covt_decode_streams_device_grouped_mode",
     "covt_plan_num_geometry_columns", "covt_plan_assembly_bytes", "covt_plan_geometry_columns",
     "covt_plan_geometry_descs", "covt_assemble_geometry_device", "covt_plan_assemble_host",
     "covt_plan_create_ex", "covt_plan_num_property_columns", "covt_plan_property_bytes",
@@ -244,6 +246,7 @@ def lib() -> C.CDLL:
     L.covt_plan_tile_status.argtypes = [vp, i32p]
     L.covt_decode_streams_device.argtypes = [vp, vp, C.c_int64, vp, vp, vp]
     L.covt_decode_streams_device_grouped.argtypes = [vp, vp, i64p, vp, vp, vp]
+    L.covt_decode_streams_device_grouped_mode.argtypes = [vp, vp, i64p, vp, vp, vp, C.c_int32]
     L.covt_plan_family_counts.argtypes = [vp, i64p]
     L.covt_plan_decode_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
     L.covt_plan_decode_host_multi.argtypes = [vp, u8p, C.c_uint64, C.c_int32, vp, vp]
@@ -719,14 +722,16 @@ class DeviceBatch:
             self._graph = g
         g.replay()
 
-    def decode(self, stream=None):
+    def decode(self, stream=None, launch: int = 0):
+        """launch: LAUNCH_AUTO (0), LAUNCH_FUSED or LAUNCH_FORKED (covt_decode_streams_device_grouped_mode)."""
         import torch
 
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        st = lib().covt_decode_streams_device_grouped(self.d_in.data_ptr(), self.d_desc.data_ptr(),
-                                                      _ptr(self.plan.family_counts, C.c_int64),
-                                                      self.d_out.data_ptr(), self.d_res.data_ptr(), s.cuda_stream)
-        _raise(st, "covt_decode_streams_device_grouped")
+        st = lib().covt_decode_streams_device_grouped_mode(self.d_in.data_ptr(), self.d_desc.data_ptr(),
+                                                           _ptr(self.plan.family_counts, C.c_int64),
+                                                           self.d_out.data_ptr(), self.d_res.data_ptr(), s.cuda_stream,
+                                                           launch)
+        _raise(st, "covt_decode_streams_device_grouped_mode")
 
     def subset(self, mask) -> "DeviceSubset":
         """A launch over only the streams selected by `mask` (Plan.subset_descs), sharing this batch's

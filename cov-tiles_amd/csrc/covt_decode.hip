@@ -31,10 +31,7 @@
 namespace covt {
 
 constexpr int kWin = 1024;  // window bytes (64 lanes x 16 B)
-#ifndef COVT_WAVES_PER_BLOCK
-#define COVT_WAVES_PER_BLOCK 2  // A/B: 1 -> +8 %, 4 -> +1 % on the bench launch
-#endif
-constexpr int kWavesPerBlock = COVT_WAVES_PER_BLOCK;  // independent waves (streams) per workgroup
+// kWavesPerBlock (covt_internal.h): independent waves (streams) per workgroup
 constexpr int kFpfBlock = 256;
 constexpr int kFpfPage = 65536;
 constexpr int kFpfBcCap = 3 * kFpfPage / kFpfBlock + kFpfPage;  // JavaFastPFOR byteContainer size
@@ -1359,12 +1356,17 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
         if (!c.err && L > c.n) c.err = COVT_ERR_COUNT_MISMATCH;
         int32_t done = 0;
         // 1 KiB of stream words from word w on the 16-byte grid, byte-swapped into dst[]:
-        // dst[m] = W(base + m) for m < 255, base = w - (0..3) returned.  One 16-byte load per lane.
+        // dst[m] = W(base + m) for m < 255, base = w - (0..3) returned.  One 16-byte load per lane, by the
+        // lanes whose 16 bytes start before the stream's last word ends (like win_load: a short stream's
+        // directory or container window would otherwise fetch up to 1 KiB past it; words past the stream
+        // are never used)
+        const uintptr_t s_end = (uintptr_t)(c.sb + 4 * nw);
         auto load_words = [&](uint32_t* dst, int64_t w) -> int64_t {
             const uintptr_t addr = (uintptr_t)(c.sb + 4 * w);
             const uintptr_t a16 = addr & ~(uintptr_t)15;
             const uint32_t o = (uint32_t)(addr & 15u), sh = o & 3u;
-            const uint4 r = ld128(a16 + 16 * (uintptr_t)l);
+            const uintptr_t al = a16 + 16 * (uintptr_t)l;
+            const uint4 r = al < s_end ? ld128(al) : make_uint4(0, 0, 0, 0);
             const uint32_t nx = lane_next(r.x);
             uint4 wv;
             const uint32_t sel = be_sel(sh);
@@ -2494,6 +2496,9 @@ constexpr int kFusedOrder[COVT_NUM_FAMILIES] = {COVT_FAMILY_SPLIT_FPF, COVT_FAMI
 constexpr int kFusedLds = (kWavesPerBlock * kFamSmemRle > 256 * kLaneSlot * 4) ? kWavesPerBlock * kFamSmemRle
                                                                               : 256 * kLaneSlot * 4;
 static_assert(kFamSmemRle >= kFamSmemFpf && kFamSmemRle >= kFamSmemVarint, "RLE scratch is the largest");
+// the lane segment: one stream per thread, each in its column of the [kLaneSlot][256] slot array
+static_assert(64 * kWavesPerBlock <= 256, "a fused workgroup's threads must fit the 256 lane-slot columns");
+static_assert(kFusedLaneStreams == 64 * kWavesPerBlock, "host wave estimate: lane streams per fused workgroup");
 
 __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(4))) void decode_fused_kernel(const uint8_t* __restrict__ in,
                                                                            uint8_t* __restrict__ out, FusedSegs sg) {
@@ -2568,13 +2573,13 @@ extern "C" int covt_launch_fused(const uint8_t* d_in, const covt_stream_desc* d_
         const int f = covt::kFusedOrder[k];
         const int64_t n = f == COVT_FAMILY_SPLIT || f == COVT_FAMILY_SPLIT_FPF || f == COVT_FAMILY_SPLIT_RLE
                               ? counts[f] / covt::kSplitSlots : counts[f];
-        const int64_t per = f == COVT_FAMILY_LANE ? 64 * covt::kWavesPerBlock : covt::kWavesPerBlock;
+        const int64_t per = f == COVT_FAMILY_LANE ? 64 * kWavesPerBlock : kWavesPerBlock;
         wg += (uint64_t)((n + per - 1) / per);
         if (wg > 0x7fffffffull) return COVT_ERR_INVALID_ARG;
         sg.wg_end[k] = (uint32_t)wg;
     }
     if (wg == 0) return COVT_OK;
-    hipLaunchKernelGGL(covt::decode_fused_kernel, dim3((unsigned)wg), dim3(64 * covt::kWavesPerBlock), 0, stream,
+    hipLaunchKernelGGL(covt::decode_fused_kernel, dim3((unsigned)wg), dim3(64 * kWavesPerBlock), 0, stream,
                        d_in, d_out, sg);
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
 }
@@ -2596,9 +2601,9 @@ extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt
         return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
     }
     const int64_t n_chunks = n_split / covt::kSplitSlots;
-    const dim3 block(64 * covt::kWavesPerBlock);
+    const dim3 block(64 * kWavesPerBlock);
     if (n_chunks > 0) {  // the chunks first, on the same stream (the same hardware queue) as the family
-        const int64_t sblocks = (n_chunks + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
+        const int64_t sblocks = (n_chunks + kWavesPerBlock - 1) / kWavesPerBlock;
         if (sblocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
         if (fam == COVT_FAMILY_FASTPFOR)
             hipLaunchKernelGGL(covt::decode_split_kernel<covt::kSplitFpf>, dim3((unsigned)sblocks), block, 0, stream,
@@ -2612,7 +2617,7 @@ extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt
         if (hipGetLastError() != hipSuccess) return COVT_ERR_DEVICE;
     }
     if (n_streams <= 0) return COVT_OK;
-    const int64_t blocks = (n_streams + covt::kWavesPerBlock - 1) / covt::kWavesPerBlock;
+    const int64_t blocks = (n_streams + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
     const dim3 grid((unsigned)blocks);
     switch (fam) {

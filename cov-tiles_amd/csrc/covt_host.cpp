@@ -573,7 +573,8 @@ void fork_release(ForkCtx* f) {
 }
 
 int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const int64_t counts[COVT_NUM_FAMILIES],
-                   uint8_t* d_out, covt_stream_result* d_res, hipStream_t s) {
+                   uint8_t* d_out, covt_stream_result* d_res, hipStream_t s, int mode = COVT_LAUNCH_AUTO) {
+    if (mode != COVT_LAUNCH_AUTO && mode != COVT_LAUNCH_FUSED && mode != COVT_LAUNCH_FORKED) return COVT_ERR_INVALID_ARG;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return COVT_ERR_DEVICE;
     if (s) {  // the auxiliary streams must belong to the device of the caller's stream
@@ -617,8 +618,10 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
         return COVT_ERR_DEVICE;
     {  // a small batch: one fused launch on the caller's stream (no fork / join)
         const int64_t waves = n_split / COVT_SPLIT_SLOTS + counts[COVT_FAMILY_FASTPFOR] + counts[COVT_FAMILY_RLE] +
-                              counts[COVT_FAMILY_VARINT] + (counts[COVT_FAMILY_LANE] + 127) / 128;
-        if (waves <= kFusedMaxWaves) return covt_launch_fused(d_in, d_desc, counts, d_out, d_res, s);
+                              counts[COVT_FAMILY_VARINT] +
+                              (counts[COVT_FAMILY_LANE] + kFusedLaneStreams - 1) / kFusedLaneStreams;
+        if (mode == COVT_LAUNCH_FUSED || (mode == COVT_LAUNCH_AUTO && waves <= kFusedMaxWaves))
+            return covt_launch_fused(d_in, d_desc, counts, d_out, d_res, s);
     }
     if (splits) {
         // RLE chunks behind the varint queue (round 2 A/B: with the RLE family, config 3 0.132 -> 0.150 ms)
@@ -1751,6 +1754,13 @@ int covt_decode_streams_device_grouped(const uint8_t* d_in, const covt_stream_de
                                        covt_stream_result* d_res, void* hip_stream) {
     if (!family_counts || ((uintptr_t)d_in & 15)) return COVT_ERR_INVALID_ARG;
     return launch_grouped(d_in, d_desc, family_counts, d_out, d_res, (hipStream_t)hip_stream);
+}
+
+int covt_decode_streams_device_grouped_mode(const uint8_t* d_in, const covt_stream_desc* d_desc,
+                                            const int64_t family_counts[COVT_NUM_FAMILIES], uint8_t* d_out,
+                                            covt_stream_result* d_res, void* hip_stream, int32_t launch_mode) {
+    if (!family_counts || ((uintptr_t)d_in & 15)) return COVT_ERR_INVALID_ARG;
+    return launch_grouped(d_in, d_desc, family_counts, d_out, d_res, (hipStream_t)hip_stream, launch_mode);
 }
 
 }  // extern "C"

@@ -24,9 +24,16 @@ int covt_op_family_of(int op);
 int covt_launch_fused(const uint8_t* d_in, const covt_stream_desc* d_desc, const int64_t counts[COVT_NUM_FAMILIES],
                       uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream);
 }
-// Batches of at most this many waves (split chunks + wave-per-stream descriptors + lane streams / 128)
-// decode in one fused launch instead of the forked per-family launches
+// Batches of at most this many waves (split chunks + wave-per-stream descriptors + lane streams /
+// kFusedLaneStreams) decode in one fused launch instead of the forked per-family launches
 constexpr int64_t kFusedMaxWaves = 4096;
+// The decode kernels' workgroup: kWavesPerBlock independent waves (covt_decode.hip); the fused launch's
+// lane segment gives every thread of a workgroup one lane stream
+#ifndef COVT_WAVES_PER_BLOCK
+#define COVT_WAVES_PER_BLOCK 2  // A/B: 1 -> +8 %, 4 -> +1 % on the bench launch
+#endif
+constexpr int kWavesPerBlock = COVT_WAVES_PER_BLOCK;
+constexpr int64_t kFusedLaneStreams = 64 * kWavesPerBlock;
 
 // Plan rule for the lane-per-stream kernel: RLE streams of at most max_values values and max_bytes bytes
 // (a lane decodes serially; larger streams amortise a wave's window setup).  The two limits travel

@@ -1828,8 +1828,11 @@ int covt_device_plan_geometry(covt_device_plan* p, void* hip_stream) {
                  o_co = o_cb + up256((m + 1) * 8), o_k0 = o_co + up256((m + 1) * 8), o_k1 = o_k0 + up256(m * 8),
                  o_v0 = o_k1 + up256(m * 8), o_v1 = o_v0 + up256(m * 4), o_st = o_v1 + up256(m * 4),
                  o_cs = o_st + up256(sort_tmp), total = o_cs + up256(cscan_tmp);
-    if (hipMalloc(&p->geo_arena, total) != hipSuccess) return COVT_ERR_DEVICE;
-    uint8_t* g = (uint8_t*)p->geo_arena;
+    // the arena is the plan's only on success: a failed build frees it (a retry allocates afresh)
+    void* arena = nullptr;
+    if (hipMalloc(&arena, total) != hipSuccess) return COVT_ERR_DEVICE;
+    Free free_arena{arena};
+    uint8_t* g = (uint8_t*)arena;
     p->d_ginfo = (covt_geom_info*)g;
     p->d_gdesc = (covt_geom_desc*)(g + o_gd);
     int64_t *colbytes = (int64_t*)(g + o_cb), *coloff = (int64_t*)(g + o_co);
@@ -1853,6 +1856,9 @@ int covt_device_plan_geometry(covt_device_plan* p, void* hip_stream) {
             hipStreamSynchronize(s) != hipSuccess)
             return COVT_ERR_DEVICE;
     }
+    if (p->geo_arena) (void)hipFree(p->geo_arena);
+    p->geo_arena = arena;
+    free_arena.q = nullptr;
     p->n_geo = nc;
     p->asm_bytes = asm_bytes;
     p->geo_built = true;

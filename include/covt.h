@@ -256,6 +256,16 @@ int covt_decode_streams_device(const uint8_t* d_in, const covt_stream_desc* d_de
 int covt_decode_streams_device_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc,
                                        const int64_t family_counts[COVT_NUM_FAMILIES], uint8_t* d_out,
                                        covt_stream_result* d_res, void* hip_stream);
+/* The same launch with its shape chosen by the caller: COVT_LAUNCH_AUTO (what the call above does: one
+ * fused kernel for batches of at most 4096 waves, else the per-family kernels on forked streams),
+ * COVT_LAUNCH_FUSED or COVT_LAUNCH_FORKED whatever the batch size (tests pin both code paths; outputs
+ * and results are identical). */
+#define COVT_LAUNCH_AUTO 0
+#define COVT_LAUNCH_FUSED 1
+#define COVT_LAUNCH_FORKED 2
+int covt_decode_streams_device_grouped_mode(const uint8_t* d_in, const covt_stream_desc* d_desc,
+                                            const int64_t family_counts[COVT_NUM_FAMILIES], uint8_t* d_out,
+                                            covt_stream_result* d_res, void* hip_stream, int32_t launch_mode);
 
 /* Host entry point: H2D + decode + D2H for host tiles on the current device.
  * bytes/n_bytes: the caller's buffer the plan's tile offsets index (every tile must lie inside

@@ -85,3 +85,14 @@ def test_adversarial_rle_streams_bitexact(covt, oracle, gpu_available, mode):
     # some GeometryType streams must have been rejected, the rest decoded
     gt = plan.streams["op"] == covt.OP_BYTE_RLE_U8
     assert (res[gt, 0] != 0).any() and (res[gt, 0] == 0).any()
+    # both launch shapes of the device path (pin the fused and the forked kernels)
+    import torch
+
+    db = covt.DeviceBatch(plan, "cuda")
+    for launch in (covt.LAUNCH_FUSED, covt.LAUNCH_FORKED):
+        db.d_out.fill_(0x5A)
+        db.decode(launch=launch)
+        torch.cuda.synchronize()
+        dout, dres = db.results()
+        assert np.array_equal(dres, res), launch
+        assert _check_streams(covt, oracle, plan, dout, dres, tiles, mode) >= 100

@@ -23,9 +23,10 @@ DESC = np.dtype([("in_off", np.uint64), ("out_off", np.uint64), ("avail", np.int
                  ("op", np.uint8), ("num_bits", np.uint8), ("flags", np.uint16), ("byte_length", np.int32)])
 
 
-@pytest.mark.parametrize("chunk,values", [(100, 256), (1024, 2048)])
+@pytest.mark.parametrize("chunk,values,launch", [(100, 256, 0), (1024, 2048, 0), (100, 256, 1), (1024, 2048, 2)],
+                         ids=["c100_auto", "c1024_auto", "c100_fused", "c1024_forked"])
 @pytest.mark.parametrize("id_mode", [0, 1], ids=["id_format", "id_java"])
-def test_fixtures_forced_split(covt, gpu_available, golden_streams, chunk, values, id_mode):
+def test_fixtures_forced_split(covt, gpu_available, golden_streams, chunk, values, id_mode, launch):
     import torch
 
     paths = tile_paths()
@@ -37,7 +38,7 @@ def test_fixtures_forced_split(covt, gpu_available, golden_streams, chunk, value
     assert plan.family_counts[covt.FAMILY_SPLIT_RLE] > 100
     db = covt.DeviceBatch(plan, "cuda")
     for _ in range(2):  # the look-back records are reset per launch
-        db.decode()
+        db.decode(launch=launch)
     torch.cuda.synchronize()
     out, res = db.results()
     col = golden_streams["columns"]
@@ -75,7 +76,11 @@ def _j4_count(b: bytes) -> int:
     return n
 
 
-def _split_launch(covt, buf: bytes, op: int, n: int, nb: int, chunk: int, out_bytes: int, fpf=False, states=None):
+LAUNCHES = pytest.mark.parametrize("launch", [1, 2], ids=["fused", "forked"])  # COVT_LAUNCH_FUSED / _FORKED
+
+
+def _split_launch(covt, buf: bytes, op: int, n: int, nb: int, chunk: int, out_bytes: int, fpf=False, states=None,
+                  launch=0):
     """One split stream through the grouped launch: byte chunks (varint) or value chunks (FastPFOR).
     states: FastPFOR chunk start states (nch x 42 int32, the plan's host walk) for pads [2..7]."""
     import ctypes as C
@@ -106,9 +111,9 @@ def _split_launch(covt, buf: bytes, op: int, n: int, nb: int, chunk: int, out_by
     d_out = torch.full((out_bytes + 16,), 0x5A, dtype=torch.uint8, device=dev)
     d_res = torch.full((d.size * 2,), 0x33, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream()
-    st = covt.lib().covt_decode_streams_device_grouped(d_in.data_ptr(), d_desc.data_ptr(),
-                                                       counts.ctypes.data_as(C.POINTER(C.c_int64)),
-                                                       d_out.data_ptr(), d_res.data_ptr(), s.cuda_stream)
+    st = covt.lib().covt_decode_streams_device_grouped_mode(d_in.data_ptr(), d_desc.data_ptr(),
+                                                            counts.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                            d_out.data_ptr(), d_res.data_ptr(), s.cuda_stream, launch)
     assert st == 0
     torch.cuda.synchronize()
     return d_out.cpu().numpy()[:out_bytes], d_res.cpu().numpy().reshape(-1, 2)[0]
@@ -148,8 +153,9 @@ def _streams(rng, oracle):
     return out
 
 
+@LAUNCHES
 @pytest.mark.parametrize("chunk", [16, 64, 100, 1000, 4096])
-def test_adversarial_streams_split(covt, oracle, gpu_available, chunk):
+def test_adversarial_streams_split(covt, oracle, gpu_available, chunk, launch):
     rng = np.random.default_rng(chunk)
     ops = [covt.OP_VARINT_I32, covt.OP_VARINT_ZZ_I32, covt.OP_VARINT_ZZ_DELTA_I32, covt.OP_VARINT_ZZ_DELTA_XY,
            covt.OP_VARINT_DELTA_MORTON, covt.OP_VARINT_I32_AS_I64, covt.OP_VARINT_ZZ_I32_AS_I64,
@@ -168,7 +174,7 @@ def test_adversarial_streams_split(covt, oracle, gpu_available, chunk):
                 ebytes = (8 if op in (covt.OP_VARINT_I32_AS_I64, covt.OP_VARINT_ZZ_I32_AS_I64,
                                       covt.OP_VARINT_ZZ_DELTA_I64) else 4) * (2 * nvals if nb else nvals)
                 o_st, o_arr, o_pos = _oracle(oracle, covt, op, buf, nvals, nb)
-                out, r = _split_launch(covt, buf, op, nvals, nb, chunk, ebytes)
+                out, r = _split_launch(covt, buf, op, nvals, nb, chunk, ebytes, launch=launch)
                 assert (int(r[0]) == 0) == (o_st == 0), (name, op, n, int(r[0]), o_st)
                 if o_st == 0:
                     assert int(r[1]) == o_pos, (name, op, n)
@@ -178,8 +184,9 @@ def test_adversarial_streams_split(covt, oracle, gpu_available, chunk):
     assert n_checked > 150
 
 
+@LAUNCHES
 @pytest.mark.parametrize("values", [256, 512, 4096])
-def test_fastpfor_streams_split(covt, oracle, gpu_available, values):
+def test_fastpfor_streams_split(covt, oracle, gpu_available, values, launch):
     """FastPFOR streams split into chunks of whole blocks: every chunk walks the page directories and the
     block headers before its range, sums its values in a first pass and stores them with its
     predecessors' carry in a second (exceptions of index 1 and > 1, all bit widths, multi-page, VByte
@@ -205,7 +212,7 @@ def test_fastpfor_streams_split(covt, oracle, gpu_available, values):
                 else:
                     o = oracle.decode_fastpfor_delta_morton_codes(body, nv, bl, 0, nb)
                 ne = 2 * nv if nb else nv
-                out, r = _split_launch(covt, body[:bl], op, nv, nb, values, 4 * ne, fpf=True)
+                out, r = _split_launch(covt, body[:bl], op, nv, nb, values, 4 * ne, fpf=True, launch=launch)
                 assert (int(r[0]) == 0) == (o[0] == 0), (n, op, nv, int(r[0]), o[0])
                 if o[0] == 0:
                     assert int(r[1]) == bl
@@ -220,7 +227,8 @@ def test_fastpfor_streams_split(covt, oracle, gpu_available, values):
             e[int(rng.integers(0, len(e)))] ^= 1 << int(rng.integers(0, 8))
         e = bytes(e)
         o = oracle.decode_fastpfor_zigzag_delta(e, 5000, len(e), 0)
-        out, r = _split_launch(covt, e, covt.OP_FPF_ZZ_DELTA_I32, 5000, 0, values, 4 * 5000, fpf=True)
+        out, r = _split_launch(covt, e, covt.OP_FPF_ZZ_DELTA_I32, 5000, 0, values, 4 * 5000, fpf=True,
+                               launch=launch)
         if o[0] == 0:
             assert int(r[0]) == 0 and np.array_equal(out.view(np.int32), np.asarray(o[1], dtype=np.int32))
         n_checked += 1
@@ -379,8 +387,9 @@ def _rle_values(rng, n, big=False):
     return np.array(out[:n], dtype=np.uint64)
 
 
+@LAUNCHES
 @pytest.mark.parametrize("unit", [64, 700, 4096])
-def test_rle_streams_split(covt, oracle, gpu_available, unit):
+def test_rle_streams_split(covt, oracle, gpu_available, unit, launch):
     """Long ORC RLE streams split at group starts by the plan's host walk: each chunk decodes its groups
     into its slice of the stream's output (byte RLE: shared edge packets written byte-exact), the
     stream's result = the lowest chunk status + the walked consumed bytes."""
@@ -431,10 +440,10 @@ def test_rle_streams_split(covt, oracle, gpu_available, unit):
             nbytes = n * elem
             d_out = torch.full((nbytes + 32,), 0x5A, dtype=torch.uint8, device=dev)
             d_res = torch.full((d.size * 2,), 0x33, dtype=torch.int32, device=dev)
-            st = covt.lib().covt_decode_streams_device_grouped(d_in.data_ptr(), d_desc.data_ptr(),
-                                                               counts.ctypes.data_as(C.POINTER(C.c_int64)),
-                                                               d_out.data_ptr(), d_res.data_ptr(),
-                                                               torch.cuda.current_stream().cuda_stream)
+            st = covt.lib().covt_decode_streams_device_grouped_mode(d_in.data_ptr(), d_desc.data_ptr(),
+                                                                    counts.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                                    d_out.data_ptr(), d_res.data_ptr(),
+                                                                    torch.cuda.current_stream().cuda_stream, launch)
             assert st == 0
             torch.cuda.synchronize()
             out = d_out.cpu().numpy()
