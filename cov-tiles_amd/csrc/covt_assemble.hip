@@ -33,6 +33,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "covt.h"
 #include "covt_internal.h"
 #include "covt_wave.h"
@@ -51,6 +55,9 @@ constexpr int kAsmWaves = COVT_ASM_WAVES;  // independent waves (columns) per wo
 constexpr int kCoopWaves = 16;
 constexpr int kCoopMaxColumns = 4096;
 constexpr int32_t kCoopMinItems = 8192;
+// ... and in such batches columns of at least this many items are cut into 4,096-item chunks on separate
+// workgroups (the split passes below) while the chunk budget lasts
+constexpr int32_t kSplitMinItems = 1024;
 
 typedef __attribute__((address_space(1))) const int32_t g_i32;
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
@@ -509,11 +516,13 @@ __global__ __launch_bounds__(64 * kAsmWaves) void assemble_kernel(const uint8_t*
                                                                   const covt_stream_result* __restrict__ dres,
                                                                   const covt_geom_desc* __restrict__ descs,
                                                                   int64_t n_cols, uint8_t* __restrict__ outb,
-                                                                  covt_geom_result* __restrict__ gres, int32_t coop_min) {
+                                                                  covt_geom_result* __restrict__ gres, int32_t coop_min,
+                                                                  const int32_t* __restrict__ split_flag) {
     __shared__ AsmSmem smem[kAsmWaves];
     const int w = threadIdx.x >> 6;
     const int64_t c = uni64((int64_t)blockIdx.x * kAsmWaves + w);
     if (c >= n_cols) return;
+    if (split_flag && split_flag[c]) return;  // assembled by the split passes
     const covt_geom_desc d = descs[c];
     if (uni(column_items(d)) >= coop_min && !((uint32_t)d.flags & COVT_GEOM_TOO_LARGE)) return;
     covt_geom_result r{COVT_OK, 0, 0, 0};
@@ -528,10 +537,12 @@ __global__ __launch_bounds__(64 * kCoopWaves) void assemble_coop_kernel(const ui
                                                                         const covt_geom_desc* __restrict__ descs,
                                                                         int64_t n_cols, uint8_t* __restrict__ outb,
                                                                         covt_geom_result* __restrict__ gres,
-                                                                        int32_t coop_min) {
+                                                                        int32_t coop_min,
+                                                                        const int32_t* __restrict__ split_flag) {
     __shared__ AsmSmemT<kCoopWaves> smem;
     const int64_t c = blockIdx.x;
     if (c >= n_cols) return;
+    if (split_flag && split_flag[c]) return;  // assembled by the split passes
     const covt_geom_desc d = descs[c];
     if (column_items(d) < coop_min || ((uint32_t)d.flags & COVT_GEOM_TOO_LARGE)) return;  // (uniform)
     covt_geom_result r{COVT_OK, 0, 0, 0};
@@ -539,7 +550,720 @@ __global__ __launch_bounds__(64 * kCoopWaves) void assemble_coop_kernel(const ui
     if (threadIdx.x == 0) gres[c] = r;
 }
 
+// ---- multi-workgroup columns (small batches: one tile's latency, BASELINE config 1) -------------------
+// A whole workgroup still walks a big column's passes one 4,096-item step at a time (the config-1 tile's
+// 35k-feature line column: ~45 dependent steps, ~190 us).  Here each pass is a kernel of its own and the
+// column's items are cut into chunks of kSplitK (one workgroup step each) that run on different
+// workgroups at once:
+//   * the scans that carry state from one chunk to the next (rank among MULTI* features / polygon parts /
+//     polygon rings, and the parts / rings / coordinates before the chunk) are a publish-and-gather: a
+//     chunk publishes its own total, then sums its predecessors' published totals (one load per
+//     predecessor, all in flight together; chunks take tickets in order, so a chunk only waits on chunks
+//     that started before it);
+//   * each pass leaves, for every chunk of the next pass, the segment that chunk's first item falls in
+//     (a segment -- a feature / part / ring -- containing a chunk boundary writes it), so the next pass's
+//     expansion starts mid-column without a search;
+//   * a check that fails marks the column with the lowest (pass, chunk) that failed, as the single-
+//     workgroup walk stops at its first failing step (same step size, same status); later passes skip a
+//     marked column.
+// The last chunk of pass 4 to finish writes the column's result.
+constexpr int kSplitK = Coop<kCoopWaves>::K;  // items per chunk: one cooperative step
+constexpr int kSplitMaxChunks = 8192;          // per pass over all split columns (more: the coop path)
+constexpr int kSplitGrid = 256;                // persistent workgroups per pass kernel (tickets)
+constexpr uint32_t kSplitMaxSpins = 1u << 22;  // look-back polls (~seconds) before a column is failed
+
+struct SplitCol {
+    unsigned long long fail;  // min over failures of (stage << 56 | chunk << 32 | -status); ~0: none
+    uint32_t P, R, V, VS;     // totals, written by the last chunk of passes 1 (P), 2 (R), 3 (V, VS)
+    uint32_t done4;           // pass-4 chunks finished
+    uint32_t pad;
+};
+struct SplitScratch {
+    uint32_t ticket[4];                       // next chunk of pass p
+    int32_t n_split;                          // split columns
+    int32_t pad[3];
+    int32_t pre[4][kCoopMaxColumns + 1];      // pass p: chunks of split columns before column k
+    int32_t col[kCoopMaxColumns];             // split column k -> batch column
+    int32_t flag[kCoopMaxColumns];            // batch column c: split (1) or not (0)
+    SplitCol st[kCoopMaxColumns];
+    int2 base[4][kSplitMaxChunks];            // pass p (1..3) chunk: (segment, segment start) of its first item
+    unsigned long long rec[4][3][kSplitMaxChunks];  // pass p, scan s, chunk: (1 << 32 | total), 0 = not yet
+};
+
+// chunks per pass of a column: ceil(capacity / kSplitK) (chunks past the pass's real item count exit)
+__device__ __forceinline__ void split_chunks(const covt_geom_desc& d, int32_t (&c)[4]) {
+    const int32_t n = d.in_off[0] >= 0 ? d.in_len[0] : 0;
+    c[0] = max(1, (n + kSplitK - 1) / kSplitK);  // at least one chunk: chunk 0 writes the terminal offset
+    c[1] = max(1, (d.part_cap + kSplitK - 1) / kSplitK);
+    c[2] = max(1, (d.ring_cap + kSplitK - 1) / kSplitK);
+    c[3] = max(1, (d.coord_cap + kSplitK - 1) / kSplitK);
+}
+
+// one workgroup: the split columns (items >= coop_min, not too large, in batch order while every pass
+// keeps within kSplitMaxChunks) and their chunk prefixes; every workgroup: zeroes the look-back records
+__global__ __launch_bounds__(1024) void split_prep(const covt_geom_desc* __restrict__ descs, int64_t n_cols,
+                                                   int32_t coop_min, SplitScratch* __restrict__ sc) {
+    {  // the records (the largest part), by every workgroup
+        uint4* r = (uint4*)&sc->rec[0][0][0];
+        const int64_t n16 = (int64_t)sizeof(sc->rec) / 16;
+        for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 1024)
+            r[i] = make_uint4(0, 0, 0, 0);
+    }
+    if (blockIdx.x != 0) return;
+    __shared__ int32_t part[4][1024];
+    // every thread takes 4 consecutive columns
+    const int t = threadIdx.x;
+    int32_t ch[4][4] = {}, want[4] = {};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t c = 4 * t + k;
+        if (c < n_cols) {
+            const covt_geom_desc d = descs[c];
+            if (column_items(d) >= coop_min && !((uint32_t)d.flags & COVT_GEOM_TOO_LARGE)) {
+                split_chunks(d, ch[k]);
+                want[k] = 1;
+            }
+        }
+    }
+    // inclusive per-thread sums of chunks per pass, then a workgroup scan (the budget: a column is split
+    // only while every pass's running total stays within kSplitMaxChunks; batch order decides)
+    int32_t s[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) s[p] = ch[0][p] + ch[1][p] + ch[2][p] + ch[3][p];
+    for (int p = 0; p < 4; ++p) part[p][t] = s[p];
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele scan (one-off, small)
+        int32_t v[4];
+        for (int p = 0; p < 4; ++p) v[p] = t >= off ? part[p][t - off] : 0;
+        __syncthreads();
+        for (int p = 0; p < 4; ++p) part[p][t] += v[p];
+        __syncthreads();
+    }
+    int32_t run[4];
+    for (int p = 0; p < 4; ++p) run[p] = part[p][t] - s[p];
+    bool fits = true;
+    for (int p = 0; p < 4; ++p) fits = fits && part[p][t] <= kSplitMaxChunks;
+    // a thread whose columns would pass the budget splits none of them (the budget is generous: config 1
+    // uses ~60 chunks of 8192; a batch past it keeps its big columns on the single-workgroup path)
+    int32_t nsplit = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nsplit += (fits && want[k]) ? 1 : 0;
+    __shared__ int32_t cnt[1024];
+    cnt[t] = nsplit;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int32_t v = t >= off ? cnt[t - off] : 0;
+        __syncthreads();
+        cnt[t] += v;
+        __syncthreads();
+    }
+    int32_t idx = cnt[t] - nsplit;
+    // prefixes over split columns only: recount chunks of the columns kept
+    int32_t keep[4][4] = {};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        for (int p = 0; p < 4; ++p) keep[k][p] = (fits && want[k]) ? ch[k][p] : 0;
+    for (int p = 0; p < 4; ++p) part[p][t] = keep[0][p] + keep[1][p] + keep[2][p] + keep[3][p];
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        int32_t v[4];
+        for (int p = 0; p < 4; ++p) v[p] = t >= off ? part[p][t - off] : 0;
+        __syncthreads();
+        for (int p = 0; p < 4; ++p) part[p][t] += v[p];
+        __syncthreads();
+    }
+    for (int p = 0; p < 4; ++p) run[p] = part[p][t] - (keep[0][p] + keep[1][p] + keep[2][p] + keep[3][p]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t c = 4 * t + k;
+        if (c >= n_cols) continue;
+        const bool sp = fits && want[k];
+        sc->flag[c] = sp ? 1 : 0;
+        if (!sp) continue;
+        sc->col[idx] = (int32_t)c;
+        for (int p = 0; p < 4; ++p) {
+            sc->pre[p][idx] = run[p];
+            run[p] += keep[k][p];
+        }
+        sc->st[idx] = SplitCol{~0ull, 0, 0, 0, 0, 0, 0};
+        ++idx;
+    }
+    if (t == 1023) {
+        sc->n_split = cnt[1023];
+        for (int p = 0; p < 4; ++p) {
+            sc->pre[p][cnt[1023]] = part[p][1023];
+            sc->ticket[p] = 0;
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned long long ld_acq(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rel(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// publish this chunk's totals of NS scans (records rec[s][j]), then the sums of chunks [0, j) of each
+// (saturating; every thread gets them).  Chunks of a column are consecutive record slots from `g0`.
+template <int NS>
+__device__ __forceinline__ void split_gather(AsmSmemT<kCoopWaves>& sm, unsigned long long (*rec)[kSplitMaxChunks],
+                                             int32_t g0, int32_t j, const uint32_t (&own)[NS], uint32_t (&pre)[NS]) {
+    if (threadIdx.x == 0)
+        for (int s = 0; s < NS; ++s) st_rel(&rec[s][g0 + j], (1ull << 32) | own[s]);
+    uint32_t acc[NS];
+    for (int s = 0; s < NS; ++s) acc[s] = 0;
+    bool lost = false;
+    for (int32_t i = threadIdx.x; i < j; i += 1024) {
+        for (int s = 0; s < NS; ++s) {
+            unsigned long long v;
+            // bounded wait: a predecessor that never publishes (a bug, not an input property) fails the
+            // column instead of hanging the launch
+            uint32_t spins = 0;
+            while (!((v = ld_acq(&rec[s][g0 + i])) >> 32) && ++spins < kSplitMaxSpins) __builtin_amdgcn_s_sleep(2);
+            lost |= !(v >> 32);
+            acc[s] = add_sat(acc[s], (uint32_t)v);
+        }
+    }
+    if (__syncthreads_or(lost)) {
+        for (int s = 0; s < NS; ++s) acc[s] = 0xffffffffu;  // saturated: every capacity check fails
+    }
+    // workgroup sums: DPP wave sums, then the 16 wave partials through LDS (one buffer per scan)
+    __syncthreads();
+    for (int s = 0; s < NS; ++s) {
+        const uint32_t w = lane_bcast(incl_scan_sat(acc[s]), 63);
+        if (lane_id() == 0) sm.slot[16 * s + (threadIdx.x >> 6)] = (int32_t)w;
+    }
+    __syncthreads();
+    for (int s = 0; s < NS; ++s) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int i = 0; i < kCoopWaves; ++i) tot = add_sat(tot, (uint32_t)sm.slot[16 * s + i]);
+        pre[s] = tot;
+    }
+    __syncthreads();
+}
+
+// the column's first failure wins (stage = pass, then chunk); status < 0
+__device__ __forceinline__ void split_fail(SplitCol& st, int stage, int32_t chunk, int32_t status) {
+    const unsigned long long key = ((unsigned long long)stage << 56) | ((unsigned long long)(uint32_t)chunk << 32) |
+                                   (uint32_t)(-status);
+    atomicMin(&st.fail, key);
+}
+// failed in an earlier pass (a failure of this pass is only acted on by the chunk that found it: a later
+// chunk that skipped its gather would leave the chunks after it waiting)
+__device__ __forceinline__ bool split_failed_before(const SplitCol& st, int pass) {
+    return (ld_acq(&st.fail) >> 56) < (unsigned long long)pass;
+}
+
+// segments whose item range [s, s + len) contains chunk boundaries b * kSplitK (b < nch) record
+// themselves for those chunks of the next pass
+__device__ __forceinline__ void split_bases(int2* __restrict__ base, int32_t nch, int32_t seg, uint32_t s, uint32_t len) {
+    if (len == 0) return;
+    const uint32_t e = s + len;  // (no wrap: checked against the capacity before this is called)
+    for (uint32_t b = (s + kSplitK - 1) / kSplitK; b * (uint32_t)kSplitK < e && (int32_t)b < nch; ++b)
+        base[b] = make_int2(seg, (int32_t)s);
+}
+
+// one chunk of one pass of split column k (global chunk g of the pass)
+template <int PASS>
+__device__ void split_chunk(const uint8_t* __restrict__ dec, const covt_stream_result* __restrict__ dres,
+                            const covt_geom_desc& d, uint8_t* __restrict__ outb, SplitScratch* __restrict__ sc,
+                            int32_t k, int32_t j, AsmSmemT<kCoopWaves>& sm, covt_geom_result* __restrict__ gres,
+                            int32_t c) {
+    constexpr int NW = kCoopWaves, K = kSplitK;
+    const int l = threadIdx.x;
+    int buf = 0;
+    SplitCol& st = sc->st[k];
+    const int32_t g0 = sc->pre[PASS - 1][k];  // this column's first chunk slot in the pass
+    const uint8_t* types = dec + d.in_off[0];
+    const int32_t* go = (const int32_t*)(dec + d.in_off[1]);
+    const int32_t* po = (const int32_t*)(dec + d.in_off[2]);
+    const int32_t* ro = (const int32_t*)(dec + d.in_off[3]);
+    const int32_t* vo = (const int32_t*)(dec + d.in_off[4]);
+    const uint64_t* vb = (const uint64_t*)(dec + d.in_off[5]);
+    const int32_t n = d.in_off[0] >= 0 ? d.in_len[0] : 0;
+    const int32_t n_go = d.in_off[1] >= 0 ? d.in_len[1] : 0;
+    const int32_t n_po = d.in_off[2] >= 0 ? d.in_len[2] : 0;
+    const int32_t n_ro = d.in_off[3] >= 0 ? d.in_len[3] : 0;
+    const bool ice = d.in_off[4] >= 0;
+    const int32_t n_vo = ice ? d.in_len[4] : 0;
+    const int32_t n_vb = d.in_off[5] >= 0 ? d.in_len[5] : 0;
+    const int32_t n_src = ice ? n_vo : n_vb;
+    const bool closed = d.flags & COVT_GEOM_CLOSED_IN_STREAM;
+    int32_t* geo_off = (int32_t*)(outb + d.out_off[0]);
+    int32_t* part_off = (int32_t*)(outb + d.out_off[1]);
+    int32_t* ring_off = (int32_t*)(outb + d.out_off[2]);
+    uint64_t* coords = (uint64_t*)(outb + d.out_off[3]);
+    int32_t* part_scr = (int32_t*)(outb + d.out_off[4]);
+    int32_t* ring_scr = (int32_t*)(outb + d.out_off[5]);
+    const uint32_t pcap = (uint32_t)d.part_cap, rcap = (uint32_t)d.ring_cap, ccap = (uint32_t)d.coord_cap;
+    int32_t nch[4];
+    split_chunks(d, nch);
+    const int32_t q0 = j * K;
+
+    if constexpr (PASS == 1) {
+        if (j == 0) {  // a failed source stream fails the column (assemble_column's first check)
+            for (int s = 0; s < 6; ++s) {
+                const int32_t ri = d.in_res[s];
+                const int32_t stt = ri >= 0 ? dres[ri].status : 0;
+                if (stt) {
+                    if (l == 0) split_fail(st, 0, 0, stt);
+                    break;
+                }
+            }
+        }
+        bool src_bad = false;
+        for (int s = 0; s < 6; ++s) src_bad |= d.in_res[s] >= 0 && dres[d.in_res[s]].status != 0;
+        if (src_bad) return;  // (uniform)
+        if (q0 >= n) {  // no features (n == 0, chunk 0): no parts
+            if (l == 0) geo_off[0] = 0;
+            return;
+        }
+        const int32_t fl = q0 + 4 * l;
+        const uint32_t tw = fl < n ? ((const g_u32*)types)[fl >> 2] : 0u;
+        uint32_t t[4], multi[4], gi[4], pf[4], ex[4], nm, tot;
+        bool bad_type = false, bad_cnt = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool valid = fl + q < n;
+            t[q] = valid ? (tw >> (8 * q)) & 0xffu : 0u;
+            bad_type |= t[q] > 5u;
+            multi[q] = (valid && t[q] >= 3u && t[q] <= 5u) ? 1u : 0u;
+            pf[q] = valid ? 1u : 0u;
+        }
+        excl_scan4(sm, buf, multi, gi, nm);
+        uint32_t own1[1] = {nm}, pre1[1];
+        split_gather<1>(sm, sc->rec[0], g0, j, own1, pre1);
+        const uint32_t go_base = pre1[0];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (multi[q]) {
+                const uint32_t i = add_sat(go_base, gi[q]);
+                if (i < (uint32_t)n_go) {
+                    const int32_t cc = ((const g_i32*)go)[i];
+                    bad_cnt |= cc < 0;
+                    pf[q] = min((uint32_t)max(cc, 0), pcap + 1u);
+                } else {
+                    bad_cnt = true;
+                }
+            }
+        }
+        excl_scan4(sm, buf, pf, ex, tot);
+        uint32_t own2[1] = {tot}, pre2[1];
+        split_gather<1>(sm, sc->rec[0] + 1, g0, j, own2, pre2);
+        const uint32_t P0 = pre2[0], P1 = add_sat(P0, tot);
+        const bool any_type = __syncthreads_or(bad_type), any_cnt = __syncthreads_or(bad_cnt);
+        if (any_type || any_cnt || P1 > pcap) {
+            if (l == 0) split_fail(st, 1, j, any_type ? COVT_ERR_BAD_HEADER : COVT_ERR_COUNT_MISMATCH);
+            return;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ex[q] += P0;
+        store4<NW>(geo_off, q0, n - q0, ex);
+        int2* base = sc->base[1] + sc->pre[1][k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (fl + q < n) split_bases(base, nch[1], fl + q, ex[q], pf[q]);
+        if (q0 + K >= n && l == 0) {  // the last chunk: the column's part count
+            geo_off[n] = (int32_t)P1;
+            st.P = P1;
+        }
+    } else if constexpr (PASS == 2) {
+        if (split_failed_before(st, 2)) return;
+        const uint32_t P = st.P;
+        if ((uint32_t)q0 >= P) {
+            if (j == 0 && l == 0) part_off[0] = 0;  // no parts: no rings
+            return;
+        }
+        const int32_t q1 = (int32_t)min((uint32_t)(q0 + K), P);
+        const int2 b0 = sc->base[1][sc->pre[1][k] + j];
+        // sweep A: the features of the chunk's parts -> the chunk's count of partOffsets-consuming parts
+        Expand<NW> x{geo_off, n, q1, b0.x, b0.y, q0};
+        const Expand<NW> x0 = x;
+        uint32_t usep_all = 0;
+        int32_t f[4], fs[4], fe[4], L = 0;
+        bool one_step = true;
+        uint32_t t[4], usep[4], pi[4], npo = 0;
+        while (x.q < q1) {
+            L = x.step(sm, buf, f, fs, fe);
+            one_step = one_step && x.q >= q1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool valid = 4 * l + q < L;
+                t[q] = valid ? (uint32_t)((const g_u8*)types)[f[q]] : 0u;
+                usep[q] = (valid && t[q] != 0u && t[q] != 3u) ? 1u : 0u;
+            }
+            uint32_t stot;
+            excl_scan4(sm, buf, usep, pi, stot);
+            usep_all = add_sat(usep_all, stot);
+        }
+        npo = usep_all;
+        uint32_t own1[1] = {npo}, pre1[1];
+        split_gather<1>(sm, sc->rec[1], g0, j, own1, pre1);
+        uint32_t po_base = pre1[0];
+        // sweep B: the ring counts (re-expanding only if the chunk took more than one step)
+        uint32_t R0 = 0, Rrun = 0;
+        bool bad_cnt = false;
+        int2* base = sc->base[2] + sc->pre[2][k];
+        // pass 2 has a second chained scan (rings before the chunk): gather it from the first sweep's ring
+        // totals is not possible (ring counts need po_base), so sweep B computes the totals, publishes,
+        // and stores after the gather (registers hold a single step; longer chunks redo the expansion)
+        uint32_t rp[4], scr[4], ex[4], tot = 0, rtot = 0;
+        auto ring_counts = [&](const uint32_t (&tt)[4], const uint32_t (&us)[4], const uint32_t (&pix)[4], int32_t LL,
+                               uint32_t pob) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool valid = 4 * l + q < LL;
+                uint32_t cc = 0;
+                if (us[q]) {
+                    const uint32_t i = add_sat(pob, pix[q]);
+                    if (i < (uint32_t)n_po) {
+                        const int32_t v = ((const g_i32*)po)[i];
+                        bad_cnt |= v < 0;
+                        cc = min((uint32_t)max(v, 0), rcap + 1u);
+                    } else {
+                        bad_cnt = true;
+                    }
+                }
+                const bool poly = tt[q] == 2u || tt[q] == 5u;
+                rp[q] = valid ? (poly ? cc : 1u) : 0u;
+                const uint32_t vcount = (tt[q] == 1u || tt[q] == 4u) ? cc : 1u;
+                scr[q] = poly ? 1u : (min(vcount, ccap + 1u) << 1);
+            }
+        };
+        if (one_step) {
+            ring_counts(t, usep, pi, L, po_base);
+            excl_scan4(sm, buf, rp, ex, tot);
+            uint32_t own2[1] = {tot}, pre2[1];
+            split_gather<1>(sm, sc->rec[1] + 1, g0, j, own2, pre2);
+            R0 = pre2[0];
+            Rrun = add_sat(R0, tot);
+            const bool any_cnt = __syncthreads_or(bad_cnt);
+            if (any_cnt || Rrun > rcap) {
+                if (l == 0) split_fail(st, 2, j, COVT_ERR_COUNT_MISMATCH);
+                return;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ex[q] += R0;
+            store4<NW>(part_off, q0, L, ex);
+            store4<NW>(part_scr, q0, L, scr);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (4 * l + q < L) split_bases(base, nch[2], q0 + 4 * l + q, ex[q], rp[q]);
+        } else {
+            // several steps: first their ring totals (no stores), then the gather, then the stores
+            x = x0;
+            uint32_t pob = po_base;
+            while (x.q < q1) {
+                L = x.step(sm, buf, f, fs, fe);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool valid = 4 * l + q < L;
+                    t[q] = valid ? (uint32_t)((const g_u8*)types)[f[q]] : 0u;
+                    usep[q] = (valid && t[q] != 0u && t[q] != 3u) ? 1u : 0u;
+                }
+                uint32_t stot;
+                excl_scan4(sm, buf, usep, pi, stot);
+                ring_counts(t, usep, pi, L, pob);
+                excl_scan4(sm, buf, rp, ex, tot);
+                rtot = add_sat(rtot, tot);
+                pob = add_sat(pob, stot);
+            }
+            uint32_t own2[1] = {rtot}, pre2[1];
+            split_gather<1>(sm, sc->rec[1] + 1, g0, j, own2, pre2);
+            R0 = pre2[0];
+            Rrun = add_sat(R0, rtot);
+            const bool any_cnt = __syncthreads_or(bad_cnt);
+            if (any_cnt || Rrun > rcap) {
+                if (l == 0) split_fail(st, 2, j, COVT_ERR_COUNT_MISMATCH);
+                return;
+            }
+            x = x0;
+            pob = po_base;
+            uint32_t R = R0;
+            while (x.q < q1) {
+                const int32_t p0 = x.q;
+                L = x.step(sm, buf, f, fs, fe);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool valid = 4 * l + q < L;
+                    t[q] = valid ? (uint32_t)((const g_u8*)types)[f[q]] : 0u;
+                    usep[q] = (valid && t[q] != 0u && t[q] != 3u) ? 1u : 0u;
+                }
+                uint32_t stot;
+                excl_scan4(sm, buf, usep, pi, stot);
+                ring_counts(t, usep, pi, L, pob);
+                excl_scan4(sm, buf, rp, ex, tot);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ex[q] += R;
+                store4<NW>(part_off, p0, L, ex);
+                store4<NW>(part_scr, p0, L, scr);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (4 * l + q < L) split_bases(base, nch[2], p0 + 4 * l + q, ex[q], rp[q]);
+                R = add_sat(R, tot);
+                pob = add_sat(pob, stot);
+            }
+        }
+        if (q1 == (int32_t)P && l == 0) {  // the last chunk: the column's ring count
+            part_off[P] = (int32_t)Rrun;
+            st.R = Rrun;
+        }
+    } else if constexpr (PASS == 3) {
+        if (split_failed_before(st, 3)) return;
+        const uint32_t P = st.P, R = st.R;
+        if ((uint32_t)q0 >= R) {
+            if (j == 0 && l == 0) ring_off[0] = 0;  // no rings: no coordinates
+            return;
+        }
+        const int32_t q1 = (int32_t)min((uint32_t)(q0 + K), R);
+        const int2 b0 = sc->base[2][sc->pre[2][k] + j];
+        Expand<NW> x{part_off, (int32_t)P, q1, b0.x, b0.y, q0};
+        const Expand<NW> x0 = x;
+        // sweep A: polygon rings of the chunk (the ringOffsets rank)
+        uint32_t npoly = 0;
+        int32_t p[4], ps[4], pe[4], L = 0;
+        uint32_t poly[4], ri[4], vs[4];
+        bool one_step = true;
+        while (x.q < q1) {
+            L = x.step(sm, buf, p, ps, pe);
+            one_step = one_step && x.q >= q1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool valid = 4 * l + q < L;
+                const int32_t sp = valid ? ((const g_i32*)part_scr)[p[q]] : 0;
+                poly[q] = (valid && (sp & 1)) ? 1u : 0u;
+                vs[q] = valid ? (uint32_t)sp >> 1 : 0u;
+            }
+            uint32_t stot;
+            excl_scan4(sm, buf, poly, ri, stot);
+            npoly = add_sat(npoly, stot);
+        }
+        uint32_t own1[1] = {npoly}, pre1[1];
+        split_gather<1>(sm, sc->rec[2], g0, j, own1, pre1);
+        const uint32_t ro_base = pre1[0];
+        bool bad_cnt = false;
+        uint32_t closing[4], vo_[4], ex[4], src[4], tv = 0, ts = 0;
+        auto vertex_counts = [&](uint32_t rob) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (poly[q]) {
+                    const uint32_t i = add_sat(rob, ri[q]);
+                    if (i < (uint32_t)n_ro) {
+                        const int32_t v = ((const g_i32*)ro)[i];
+                        bad_cnt |= v < 0;
+                        vs[q] = min((uint32_t)max(v, 0), ccap + 1u);
+                    } else {
+                        bad_cnt = true;
+                    }
+                }
+                closing[q] = (poly[q] && !closed && vs[q] > 0u) ? 1u : 0u;
+                vo_[q] = vs[q] + closing[q];
+            }
+        };
+        auto reload = [&](int32_t LL) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool valid = 4 * l + q < LL;
+                const int32_t sp = valid ? ((const g_i32*)part_scr)[p[q]] : 0;
+                poly[q] = (valid && (sp & 1)) ? 1u : 0u;
+                vs[q] = valid ? (uint32_t)sp >> 1 : 0u;
+            }
+        };
+        int2* base = sc->base[3] + sc->pre[3][k];
+        uint32_t V0, VS0, V1, VS1;
+        if (one_step) {
+            vertex_counts(ro_base);
+            excl_scan4(sm, buf, vo_, ex, tv);
+            excl_scan4(sm, buf, vs, src, ts);
+        } else {
+            x = x0;
+            uint32_t rob = ro_base;
+            while (x.q < q1) {
+                L = x.step(sm, buf, p, ps, pe);
+                reload(L);
+                uint32_t stot;
+                excl_scan4(sm, buf, poly, ri, stot);
+                vertex_counts(rob);
+                uint32_t a, b;
+                excl_scan4(sm, buf, vo_, ex, a);
+                excl_scan4(sm, buf, vs, src, b);
+                tv = add_sat(tv, a);
+                ts = add_sat(ts, b);
+                rob = add_sat(rob, stot);
+            }
+        }
+        uint32_t own2[2] = {tv, ts}, pre2[2];
+        split_gather<2>(sm, sc->rec[2] + 1, g0, j, own2, pre2);
+        V0 = pre2[0];
+        VS0 = pre2[1];
+        V1 = add_sat(V0, tv);
+        VS1 = add_sat(VS0, ts);
+        const bool any_cnt = __syncthreads_or(bad_cnt);
+        if (any_cnt || V1 > ccap || VS1 > (uint32_t)n_src) {
+            if (l == 0) split_fail(st, 3, j, COVT_ERR_COUNT_MISMATCH);
+            return;
+        }
+        auto store_rings = [&](int32_t r0, int32_t LL, uint32_t Vb, uint32_t VSb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                ex[q] += Vb;
+                src[q] = (VSb + src[q]) | (closing[q] << 31);
+            }
+            store4<NW>(ring_off, r0, LL, ex);
+            store4<NW>(ring_scr, r0, LL, src);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (4 * l + q < LL) split_bases(base, nch[3], r0 + 4 * l + q, ex[q], vo_[q]);
+        };
+        if (one_step) {
+            store_rings(q0, L, V0, VS0);
+        } else {
+            x = x0;
+            uint32_t rob = ro_base, Vb = V0, VSb = VS0;
+            while (x.q < q1) {
+                const int32_t r0 = x.q;
+                L = x.step(sm, buf, p, ps, pe);
+                reload(L);
+                uint32_t stot;
+                excl_scan4(sm, buf, poly, ri, stot);
+                vertex_counts(rob);
+                uint32_t a, b;
+                excl_scan4(sm, buf, vo_, ex, a);
+                excl_scan4(sm, buf, vs, src, b);
+                store_rings(r0, L, Vb, VSb);
+                Vb = add_sat(Vb, a);
+                VSb = add_sat(VSb, b);
+                rob = add_sat(rob, stot);
+            }
+        }
+        if (q1 == (int32_t)R && l == 0) {  // the last chunk: the column's coordinate counts
+            ring_off[R] = (int32_t)V1;
+            st.V = V1;
+            st.VS = VS1;
+        }
+    } else {  // PASS 4: coordinates
+        bool bad_idx = false;
+        if (!split_failed_before(st, 4)) {
+            const uint32_t R = st.R, V = st.V, VS = st.VS;
+            if ((uint32_t)q0 < V) {
+                const int32_t q1 = (int32_t)min((uint32_t)(q0 + K), V);
+                if (V == VS) {  // straight gather: coordinate v is source vertex v
+                    const int32_t i0 = q0 + 4 * l;
+                    int32_t idx[4];
+                    if (ice && i0 + 4 <= q1) {
+                        const i32x4 w = *(const g_i32x4*)(vo + i0);
+                        idx[0] = w.x; idx[1] = w.y; idx[2] = w.z; idx[3] = w.w;
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) idx[q] = i0 + q < q1 ? (ice ? ((const g_i32*)vo)[i0 + q] : i0 + q) : 0;
+                    }
+                    uint64_t xy[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const bool valid = i0 + q < q1;
+                        const bool inr = (uint32_t)idx[q] < (uint32_t)n_vb;
+                        bad_idx |= valid && !inr;
+                        xy[q] = (valid && inr) ? ((const g_u64*)vb)[idx[q]] : 0ull;
+                    }
+                    store4_xy<NW>(coords, q0, q1 - q0, xy);
+                } else {
+                    const int2 b0 = sc->base[3][sc->pre[3][k] + j];
+                    Expand<NW> x{ring_off, (int32_t)R, q1, b0.x, b0.y, q0};
+                    while (x.q < q1) {
+                        const int32_t v0 = x.q;
+                        int32_t r[4], rs[4], re[4];
+                        const int32_t L = x.step(sm, buf, r, rs, re);
+                        uint64_t xy[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const int32_t v = v0 + 4 * l + q;
+                            const bool valid = 4 * l + q < L;
+                            const uint32_t sr = valid ? (uint32_t)((const g_i32*)ring_scr)[r[q]] : 0u;
+                            const int32_t first = (int32_t)(sr & 0x7fffffffu);
+                            const int32_t s = ((sr >> 31) && v == re[q] - 1) ? first : first + (v - rs[q]);
+                            const int32_t idx = valid ? (ice ? ((const g_i32*)vo)[s] : s) : 0;
+                            const bool inr = (uint32_t)idx < (uint32_t)n_vb;
+                            bad_idx |= valid && !inr;
+                            xy[q] = (valid && inr) ? ((const g_u64*)vb)[idx] : 0ull;
+                        }
+                        store4_xy<NW>(coords, v0, L, xy);
+                    }
+                }
+            }
+        }
+        if (__syncthreads_or(bad_idx) && l == 0) split_fail(st, 4, j, COVT_ERR_TRUNCATED);
+        // the column's last pass-4 chunk to finish writes its result
+        __syncthreads();
+        if (l == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            const uint32_t done = atomicAdd(&st.done4, 1u) + 1u;
+            if (done == (uint32_t)nch[3]) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                const unsigned long long fk = ld_acq(&st.fail);
+                covt_geom_result r{COVT_OK, 0, 0, 0};
+                if (fk != ~0ull) {
+                    r.status = -(int32_t)(uint32_t)(fk & 0xffffffffu);
+                } else {
+                    r.num_parts = (int32_t)st.P;
+                    r.num_rings = (int32_t)st.R;
+                    r.num_coords = (int32_t)st.V;
+                }
+                gres[c] = r;
+            }
+        }
+    }
+}
+
+// pass PASS over every split column: workgroups take chunks by ticket (a chunk waits only on chunks of
+// its column with lower tickets, all already running) until the pass has none left
+template <int PASS>
+__global__ __launch_bounds__(64 * kCoopWaves) void split_pass_kernel(const uint8_t* __restrict__ dec,
+                                                                     const covt_stream_result* __restrict__ dres,
+                                                                     const covt_geom_desc* __restrict__ descs,
+                                                                     uint8_t* __restrict__ outb,
+                                                                     covt_geom_result* __restrict__ gres,
+                                                                     SplitScratch* __restrict__ sc) {
+    __shared__ AsmSmemT<kCoopWaves> smem;
+    __shared__ int32_t tk;
+    const int32_t ns = sc->n_split;
+    const int32_t total = sc->pre[PASS - 1][ns];
+    for (;;) {
+        if (threadIdx.x == 0) tk = (int32_t)atomicAdd(&sc->ticket[PASS - 1], 1u);
+        __syncthreads();
+        const int32_t g = tk;
+        __syncthreads();
+        if (g >= total) return;
+        // the split column holding chunk g: the last k with pre[k] <= g (binary search over ns + 1 prefixes)
+        int32_t lo = 0, hi = ns;  // pre[lo] <= g < pre[hi]
+        while (hi - lo > 1) {
+            const int32_t mid = (lo + hi) >> 1;
+            if (sc->pre[PASS - 1][mid] <= g) lo = mid;
+            else hi = mid;
+        }
+        const int32_t k = lo, j = g - sc->pre[PASS - 1][k], c = sc->col[k];
+        const covt_geom_desc d = descs[c];
+        split_chunk<PASS>(dec, dres, d, outb, sc, k, j, smem, gres, c);
+        __syncthreads();
+    }
+}
+
 }  // namespace covt
+
+namespace {
+// split-pass scratch, one per (device, stream): launches on one stream are ordered, so they can share it
+std::mutex g_split_mu;
+std::map<std::pair<int, hipStream_t>, void*> g_split_scratch;
+covt::SplitScratch* split_scratch(hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(g_split_mu);
+    void*& p = g_split_scratch[std::make_pair(dev, s)];
+    if (!p && hipMalloc(&p, sizeof(covt::SplitScratch)) != hipSuccess) p = nullptr;
+    return (covt::SplitScratch*)p;
+}
+}  // namespace
 
 extern "C" int covt_assemble_geometry_device(const uint8_t* d_decoded, const covt_stream_result* d_res,
                                              const covt_geom_desc* d_gdesc, int64_t n_columns, uint8_t* d_asm,
@@ -549,13 +1273,30 @@ extern "C" int covt_assemble_geometry_device(const uint8_t* d_decoded, const cov
     if (n_columns == 0) return COVT_OK;
     const int64_t blocks = (n_columns + covt::kAsmWaves - 1) / covt::kAsmWaves;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
-    // small batches: big columns by whole workgroups (launched first: they are the critical path)
+    hipStream_t s = (hipStream_t)hip_stream;
+    // small batches: big columns by many workgroups at once (the split passes), or -- past the split
+    // budget -- by one whole workgroup each; launched first: they are the critical path
     const bool coop = n_columns <= covt::kCoopMaxColumns;
     const int32_t coop_min = coop ? covt::kCoopMinItems : 0x7fffffff;
-    if (coop)
-        hipLaunchKernelGGL(covt::assemble_coop_kernel, dim3((unsigned)n_columns), dim3(64 * covt::kCoopWaves), 0,
-                           (hipStream_t)hip_stream, d_decoded, d_res, d_gdesc, n_columns, d_asm, d_gres, coop_min);
-    hipLaunchKernelGGL(covt::assemble_kernel, dim3((unsigned)blocks), dim3(64 * covt::kAsmWaves), 0,
-                       (hipStream_t)hip_stream, d_decoded, d_res, d_gdesc, n_columns, d_asm, d_gres, coop_min);
+    const int32_t* split_flag = nullptr;
+    if (coop) {
+        covt::SplitScratch* sc = split_scratch(s);
+        if (!sc) return COVT_ERR_DEVICE;
+        split_flag = sc->flag;
+        const dim3 wg(64 * covt::kCoopWaves);
+        hipLaunchKernelGGL(covt::split_prep, dim3(64), dim3(1024), 0, s, d_gdesc, n_columns, covt::kSplitMinItems, sc);
+        hipLaunchKernelGGL(covt::split_pass_kernel<1>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
+                           d_asm, d_gres, sc);
+        hipLaunchKernelGGL(covt::split_pass_kernel<2>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
+                           d_asm, d_gres, sc);
+        hipLaunchKernelGGL(covt::split_pass_kernel<3>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
+                           d_asm, d_gres, sc);
+        hipLaunchKernelGGL(covt::split_pass_kernel<4>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
+                           d_asm, d_gres, sc);
+        hipLaunchKernelGGL(covt::assemble_coop_kernel, dim3((unsigned)n_columns), wg, 0, s, d_decoded, d_res, d_gdesc,
+                           n_columns, d_asm, d_gres, coop_min, split_flag);
+    }
+    hipLaunchKernelGGL(covt::assemble_kernel, dim3((unsigned)blocks), dim3(64 * covt::kAsmWaves), 0, s, d_decoded,
+                       d_res, d_gdesc, n_columns, d_asm, d_gres, coop_min, split_flag);
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
 }

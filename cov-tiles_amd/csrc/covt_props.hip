@@ -13,6 +13,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "covt.h"
 #include "covt_internal.h"
 #include "covt_wave.h"
@@ -30,6 +34,9 @@ constexpr int kPropWaves = COVT_PROP_WAVES;  // independent waves (columns) per 
 constexpr int kPropCoopWaves = 16;
 constexpr int kPropCoopMaxColumns = 4096;
 constexpr int32_t kPropCoopMinFeatures = 8192;
+// ... and in such batches columns of at least this many features are cut into 4,096-feature chunks on
+// separate workgroups (prop_split_kernel below) while the chunk budget lasts
+constexpr int32_t kPropSplitMinFeatures = 1024;
 
 struct PropSmem {
     uint32_t red[2][kPropCoopWaves];  // per-wave partials (two buffers, alternating)
@@ -284,10 +291,12 @@ __global__ __launch_bounds__(64 * kPropWaves) void props_kernel(const uint8_t* _
                                                                 const covt_stream_result* __restrict__ dres,
                                                                 const covt_prop_desc* __restrict__ descs,
                                                                 int64_t n_cols, uint8_t* __restrict__ outb,
-                                                                covt_prop_result* __restrict__ pres, int32_t coop_min) {
+                                                                covt_prop_result* __restrict__ pres, int32_t coop_min,
+                                                                const int32_t* __restrict__ split_flag) {
     const int w = threadIdx.x >> 6;
     const int64_t c = uni64((int64_t)blockIdx.x * kPropWaves + w);
     if (c >= n_cols) return;
+    if (split_flag && split_flag[c]) return;  // materialized by prop_split_kernel
     const covt_prop_desc d = descs[c];
     if (uni(d.n_features) >= coop_min) return;
     covt_prop_result r;
@@ -303,10 +312,12 @@ __global__ __launch_bounds__(64 * kPropCoopWaves) void props_coop_kernel(const u
                                                                          const covt_prop_desc* __restrict__ descs,
                                                                          int64_t n_cols, uint8_t* __restrict__ outb,
                                                                          covt_prop_result* __restrict__ pres,
-                                                                         int32_t coop_min) {
+                                                                         int32_t coop_min,
+                                                                         const int32_t* __restrict__ split_flag) {
     __shared__ PropSmem smem;
     const int64_t c = blockIdx.x;
     if (c >= n_cols) return;
+    if (split_flag && split_flag[c]) return;  // materialized by prop_split_kernel
     const covt_prop_desc d = descs[c];
     if (d.n_features < coop_min) return;  // (uniform)
     covt_prop_result r;
@@ -314,7 +325,297 @@ __global__ __launch_bounds__(64 * kPropCoopWaves) void props_coop_kernel(const u
     if (threadIdx.x == 0) pres[c] = r;
 }
 
+// ---- multi-workgroup columns (small batches: one tile's latency, BASELINE config 1) -------------------
+// A whole workgroup still steps through a big column 4,096 features at a time, each step a chain of
+// dependent loads (validity nibbles -> scan -> gathers at the ranks).  The steps only share the count of
+// present features before them, so here every step is a chunk on a workgroup of its own: a chunk
+// publishes its present count and sums its predecessors' published counts (one load each, all in
+// flight; chunks take tickets in order, so a chunk only waits on chunks already running), then writes
+// its validity bits and values.  Chunk 0 also builds (or checks) the dictionary; the last chunk of a
+// column to finish writes the column's result in Java's status order.
+constexpr int kPropSplitK = 4 * 64 * kPropCoopWaves;  // features per chunk
+constexpr int kPropSplitMaxChunks = 16384;          // over all split columns (more: the coop path)
+constexpr int kPropSplitGrid = 256;                 // persistent workgroups (tickets)
+constexpr uint32_t kPropSplitMaxSpins = 1u << 22;   // look-back polls before a column is failed
+
+struct PropSplitCol {
+    int32_t dst;           // the dictionary's status (chunk 0)
+    uint32_t bad;          // any chunk saw an out-of-range rank / index
+    uint32_t done;         // chunks finished
+    uint32_t n_valid;      // present features (the last chunk)
+};
+struct PropSplitScratch {
+    uint32_t ticket;
+    int32_t n_split;
+    int32_t pad[2];
+    int32_t pre[kPropCoopMaxColumns + 1];  // chunks of split columns before column k
+    int32_t col[kPropCoopMaxColumns];      // split column k -> batch column
+    int32_t flag[kPropCoopMaxColumns];     // batch column c: split (1) or not (0)
+    PropSplitCol st[kPropCoopMaxColumns];
+    unsigned long long rec[kPropSplitMaxChunks];  // chunk: (1 << 32 | present count), 0 = not yet
+};
+
+__device__ __forceinline__ bool prop_split_wanted(const covt_prop_desc& d, int32_t split_min) {
+    return d.n_features >= split_min && !(d.flags & COVT_PROP_UNSUPPORTED);
+}
+
+// one workgroup: the split columns and their chunk prefixes (batch order while within the budget);
+// every workgroup: zeroes the records
+__global__ __launch_bounds__(1024) void prop_split_prep(const covt_prop_desc* __restrict__ descs, int64_t n_cols,
+                                                        int32_t split_min, PropSplitScratch* __restrict__ sc) {
+    for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < kPropSplitMaxChunks; i += (int64_t)gridDim.x * 1024)
+        sc->rec[i] = 0ull;
+    if (blockIdx.x != 0) return;
+    __shared__ int32_t a[1024], b[1024];
+    const int t = threadIdx.x;
+    int32_t ch[4] = {};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t c = 4 * t + k;
+        if (c < n_cols) {
+            const covt_prop_desc d = descs[c];
+            if (prop_split_wanted(d, split_min)) ch[k] = (d.n_features + kPropSplitK - 1) / kPropSplitK;
+        }
+    }
+    const int32_t s = ch[0] + ch[1] + ch[2] + ch[3];
+    a[t] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int32_t v = t >= off ? a[t - off] : 0;
+        __syncthreads();
+        a[t] += v;
+        __syncthreads();
+    }
+    const bool fits = a[t] <= kPropSplitMaxChunks;  // (the prefix only grows: the budget cuts a tail)
+    int32_t keep = 0, nk = 0;
+    for (int k = 0; k < 4; ++k) {
+        keep += fits ? ch[k] : 0;
+        nk += (fits && ch[k]) ? 1 : 0;
+    }
+    a[t] = keep;
+    b[t] = nk;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int32_t v = t >= off ? a[t - off] : 0, w = t >= off ? b[t - off] : 0;
+        __syncthreads();
+        a[t] += v;
+        b[t] += w;
+        __syncthreads();
+    }
+    int32_t run = a[t] - keep, idx = b[t] - nk;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t c = 4 * t + k;
+        if (c >= n_cols) continue;
+        const bool sp = fits && ch[k] > 0;
+        sc->flag[c] = sp ? 1 : 0;
+        if (!sp) continue;
+        sc->col[idx] = (int32_t)c;
+        sc->pre[idx] = run;
+        sc->st[idx] = PropSplitCol{COVT_OK, 0u, 0u, 0u};
+        run += ch[k];
+        ++idx;
+    }
+    if (t == 1023) {
+        sc->n_split = b[1023];
+        sc->pre[b[1023]] = a[1023];
+        sc->ticket = 0;
+    }
+}
+
+__device__ __forceinline__ unsigned long long pld_rlx(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// chunk j of split column k (batch column c)
+__device__ void prop_split_chunk(const uint8_t* in, const uint8_t* dec, const covt_stream_result* dres,
+                                 const covt_prop_desc& d, uint8_t* outb, covt_prop_result* pres, PropSplitScratch* sc,
+                                 int32_t k, int32_t j, int32_t c, PropSmem* smp) {
+    constexpr int NW = kPropCoopWaves;
+    const int l = (int)threadIdx.x, wv = (int)(threadIdx.x >> 6);
+    PropSplitCol& cs = sc->st[k];
+    const int32_t g0 = sc->pre[k], nch = sc->pre[k + 1] - g0;
+    int32_t st[3];
+    for (int q = 0; q < 3; ++q) st[q] = d.res[q] >= 0 ? ((const gp_i32*)dres)[2 * d.res[q]] : COVT_OK;
+    // the dictionary (chunk 0, wave 0): written by the owner whatever this sub-column's other streams hold
+    if (j == 0 && d.type == COVT_PROP_STRING && d.res[2] >= 0 && st[2] == COVT_OK) {
+        if (wv == 0) {
+            const int32_t x = dictionary(in, dec, d, outb, (d.flags & COVT_PROP_DICT_OWNER) != 0);
+            if (lane_id() == 0) cs.dst = x;
+        }
+    }
+    bool early = st[0] || st[1] || st[2] || (d.flags & (COVT_PROP_UNSUPPORTED_LATE | COVT_PROP_DATA_SHORT));
+    const int32_t n = d.n_features, dn = d.n_data;
+    const int32_t f0 = j * kPropSplitK;
+    bool bad = false;
+    uint32_t carry = 0, tot = 0;
+    if (!early) {
+        const uint8_t* prs = d.present_off >= 0 ? dec + d.present_off : nullptr;
+        uint8_t* vout = outb + d.out_off[0];
+        uint8_t* xout = outb + d.out_off[1];
+        const bool dense_bool = (d.flags & COVT_PROP_DENSE_BOOL) != 0;
+        const int32_t f = f0 + 4 * l;
+        const uint32_t vb = prs ? nibble(prs, f, n) : all_valid(f, n);
+        const uint32_t cnt = (uint32_t)__popc(vb);
+        const uint32_t inc = incl_scan(cnt);
+        uint32_t pre = inc - cnt;
+        if (lane_id() == 63) smp->red[0][wv] = inc;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const uint32_t t = smp->red[0][i];
+            pre += i < wv ? t : 0u;
+            tot += t;
+        }
+        // publish this chunk's count, sum the predecessors' (bounded wait: a lost record fails the column)
+        if (l == 0) __hip_atomic_store(&sc->rec[g0 + j], (1ull << 32) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t acc = 0;
+        bool lost = false;
+        for (int32_t i = l; i < j; i += 1024) {
+            unsigned long long v;
+            uint32_t spins = 0;
+            while (!((v = pld_rlx(&sc->rec[g0 + i])) >> 32) && ++spins < kPropSplitMaxSpins) __builtin_amdgcn_s_sleep(2);
+            lost |= !(v >> 32);
+            acc += (uint32_t)v;
+        }
+        const uint32_t wsum = lane_bcast(incl_scan(acc), 63);
+        __syncthreads();
+        if (lane_id() == 0) smp->red[1][wv] = wsum;
+        __syncthreads();
+        for (int i = 0; i < NW; ++i) carry += smp->red[1][i];
+        bad |= __syncthreads_or(lost);
+        uint32_t jr = carry + pre;  // rank of this thread's first present feature
+        const uint32_t vhi = lane_next(vb);
+        if (!(l & 1) && f < n) vout[f >> 3] = (uint8_t)(vb | (vhi << 4));
+        if (d.type == COVT_PROP_BOOLEAN) {
+            uint32_t xb;
+            if (dense_bool) {
+                xb = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool p = (vb >> q) & 1u;
+                    const bool ok = p && jr < (uint32_t)dn;
+                    bad |= p && !ok;
+                    if (ok) xb |= ((((const gp_u8*)(dec + d.data_off))[jr >> 3] >> (jr & 7u)) & 1u) << q;
+                    jr += p ? 1u : 0u;
+                }
+            } else {
+                xb = nibble(dec + d.data_off, f, n) & vb;
+            }
+            const uint32_t xhi = lane_next(xb);
+            if (!(l & 1) && f < n) xout[f >> 3] = (uint8_t)(xb | (xhi << 4));
+        } else if (d.type == COVT_PROP_INT64) {
+            int64_t v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool p = (vb >> q) & 1u;
+                const bool ok = p && jr < (uint32_t)dn;
+                bad |= p && !ok;
+                v[q] = ok ? ((const gp_i64*)(dec + d.data_off))[jr] : 0;
+                jr += p ? 1u : 0u;
+            }
+            int64_t* o = (int64_t*)xout + f;
+            if (f + 4 <= n) {
+                *(pi32x4*)o = pi32x4{(int32_t)v[0], (int32_t)(v[0] >> 32), (int32_t)v[1], (int32_t)(v[1] >> 32)};
+                *(pi32x4*)(o + 2) = pi32x4{(int32_t)v[2], (int32_t)(v[2] >> 32), (int32_t)v[3], (int32_t)(v[3] >> 32)};
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (f + q < n) o[q] = v[q];
+            }
+        } else {
+            const bool flt = d.type == COVT_PROP_FLOAT;
+            int32_t v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool p = (vb >> q) & 1u;
+                const bool ok = p && jr < (uint32_t)dn;
+                bad |= p && !ok;
+                int32_t x = 0;
+                if (ok) x = flt ? (int32_t)pld_le32(in + d.data_off + 4 * (int64_t)jr) : ((const gp_i32*)(dec + d.data_off))[jr];
+                bad |= ok && !flt && (uint32_t)x >= (uint32_t)d.n_dict;
+                v[q] = x;
+                jr += p ? 1u : 0u;
+            }
+            int32_t* o = (int32_t*)xout + f;
+            if (f + 4 <= n) {
+                *(pi32x4*)o = pi32x4{v[0], v[1], v[2], v[3]};
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (f + q < n) o[q] = v[q];
+            }
+        }
+        bad = __syncthreads_or(bad) != 0;
+    }
+    __syncthreads();
+    if (l == 0) {
+        if (bad) atomicOr(&cs.bad, 1u);
+        if (!early && f0 + kPropSplitK >= n) cs.n_valid = carry + tot;  // the last chunk: the column's count
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const uint32_t done = atomicAdd(&cs.done, 1u) + 1u;
+        if (done == (uint32_t)nch) {  // the column's last chunk to finish: its result, in Java's order
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            covt_prop_result r{COVT_OK, 0};
+            const int32_t dst = __hip_atomic_load(&cs.dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int q = 0; q < 3 && !r.status; ++q) {
+                if (st[q]) r.status = st[q];
+                else if (q == 0 && (d.flags & COVT_PROP_UNSUPPORTED_LATE)) r.status = COVT_ERR_UNSUPPORTED_ENCODING;
+            }
+            if (!r.status && (d.flags & COVT_PROP_DATA_SHORT)) r.status = COVT_ERR_TRUNCATED;
+            if (!r.status && dst) r.status = dst;
+            if (!r.status && __hip_atomic_load(&cs.bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                r.status = COVT_ERR_COUNT_MISMATCH;
+            if (!r.status) r.n_valid = (int32_t)__hip_atomic_load(&cs.n_valid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pres[c] = r;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64 * kPropCoopWaves) void prop_split_kernel(const uint8_t* __restrict__ in,
+                                                                         const uint8_t* __restrict__ dec,
+                                                                         const covt_stream_result* __restrict__ dres,
+                                                                         const covt_prop_desc* __restrict__ descs,
+                                                                         uint8_t* __restrict__ outb,
+                                                                         covt_prop_result* __restrict__ pres,
+                                                                         PropSplitScratch* __restrict__ sc) {
+    __shared__ PropSmem smem;
+    __shared__ int32_t tk;
+    const int32_t ns = sc->n_split, total = sc->pre[ns];
+    for (;;) {
+        if (threadIdx.x == 0) tk = (int32_t)atomicAdd(&sc->ticket, 1u);
+        __syncthreads();
+        const int32_t g = tk;
+        __syncthreads();
+        if (g >= total) return;
+        int32_t lo = 0, hi = ns;  // pre[lo] <= g < pre[hi]
+        while (hi - lo > 1) {
+            const int32_t mid = (lo + hi) >> 1;
+            if (sc->pre[mid] <= g) lo = mid;
+            else hi = mid;
+        }
+        const int32_t c = sc->col[lo];
+        const covt_prop_desc d = descs[c];
+        prop_split_chunk(in, dec, dres, d, outb, pres, sc, lo, g - sc->pre[lo], c, &smem);
+        __syncthreads();
+    }
+}
+
 }  // namespace covt
+
+namespace {
+// split scratch, one per (device, stream): launches on one stream are ordered, so they can share it
+std::mutex g_psplit_mu;
+std::map<std::pair<int, hipStream_t>, void*> g_psplit_scratch;
+covt::PropSplitScratch* prop_split_scratch(hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(g_psplit_mu);
+    void*& p = g_psplit_scratch[std::make_pair(dev, s)];
+    if (!p && hipMalloc(&p, sizeof(covt::PropSplitScratch)) != hipSuccess) p = nullptr;
+    return (covt::PropSplitScratch*)p;
+}
+}  // namespace
 
 extern "C" int covt_materialize_properties_device(const uint8_t* d_in, const uint8_t* d_decoded,
                                                   const covt_stream_result* d_res, const covt_prop_desc* d_pdesc,
@@ -325,14 +626,25 @@ extern "C" int covt_materialize_properties_device(const uint8_t* d_in, const uin
     if (n_columns == 0) return COVT_OK;
     const int64_t blocks = (n_columns + covt::kPropWaves - 1) / covt::kPropWaves;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
-    // small batches: big columns by whole workgroups (launched first: they are the critical path)
+    hipStream_t s = (hipStream_t)hip_stream;
+    // small batches: columns of kPropSplitMinFeatures or more by several workgroups each (prop_split_kernel),
+    // past the split budget those of kPropCoopMinFeatures or more by one whole workgroup; launched first:
+    // they are the critical path
     const bool coop = n_columns <= covt::kPropCoopMaxColumns;
     const int32_t coop_min = coop ? covt::kPropCoopMinFeatures : 0x7fffffff;
-    if (coop)
-        hipLaunchKernelGGL(covt::props_coop_kernel, dim3((unsigned)n_columns), dim3(64 * covt::kPropCoopWaves), 0,
-                           (hipStream_t)hip_stream, d_in, d_decoded, d_res, d_pdesc, n_columns, d_props, d_pres,
-                           coop_min);
-    hipLaunchKernelGGL(covt::props_kernel, dim3((unsigned)blocks), dim3(64 * covt::kPropWaves), 0,
-                       (hipStream_t)hip_stream, d_in, d_decoded, d_res, d_pdesc, n_columns, d_props, d_pres, coop_min);
+    const int32_t* split_flag = nullptr;
+    if (coop) {
+        covt::PropSplitScratch* sc = prop_split_scratch(s);
+        if (!sc) return COVT_ERR_DEVICE;
+        split_flag = sc->flag;
+        hipLaunchKernelGGL(covt::prop_split_prep, dim3(16), dim3(1024), 0, s, d_pdesc, n_columns,
+                           covt::kPropSplitMinFeatures, sc);
+        hipLaunchKernelGGL(covt::prop_split_kernel, dim3(covt::kPropSplitGrid), dim3(64 * covt::kPropCoopWaves), 0, s,
+                           d_in, d_decoded, d_res, d_pdesc, d_props, d_pres, sc);
+        hipLaunchKernelGGL(covt::props_coop_kernel, dim3((unsigned)n_columns), dim3(64 * covt::kPropCoopWaves), 0, s,
+                           d_in, d_decoded, d_res, d_pdesc, n_columns, d_props, d_pres, coop_min, split_flag);
+    }
+    hipLaunchKernelGGL(covt::props_kernel, dim3((unsigned)blocks), dim3(64 * covt::kPropWaves), 0, s, d_in, d_decoded,
+                       d_res, d_pdesc, n_columns, d_props, d_pres, coop_min, split_flag);
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
 }

@@ -175,6 +175,42 @@ def test_assembly_errors_cooperative(covt, oracle, gpu_available):
     _check_vs_oracle(oracle, cols, asm, gres, lay)
 
 
+def test_split_columns_multi_chunk(covt, oracle, gpu_available):
+    """Columns of many 4,096-item chunks in a small batch go through the split passes (several workgroups
+    per column, chunk-to-chunk scans by publish-and-gather, each pass seeding the next one's chunk starts):
+    bit-exact against the oracle, including chunks whose expansion takes several steps (runs of empty
+    multi-features / parts), ICE and plain, closed and open rings, and a failure in a late chunk."""
+    rng = np.random.default_rng(11)
+    cols = [A.synth_column(rng, 40000, True, False),
+            A.synth_column(rng, 30000, False, True),
+            A.synth_column(rng, 20000, False, False, probs=[0, 0, 1, 0, 0, 0]),
+            A.synth_column(rng, 25000, True, False, probs=[0, 0, 0, 0.2, 0.4, 0.4]),
+            A.synth_column(rng, 2, False, False, big=True, probs=[0, 0, 0, 0, 0, 1])]
+    # runs of empty multi-features: 20k MULTILINESTRINGs of which most claim zero parts
+    empt = A.synth_column(rng, 20000, False, False, probs=[0, 0, 0, 0, 1, 0])
+    go = empt["go"].copy()
+    go[rng.random(go.size) < 0.9] = 0
+    n = 20000
+    types = np.full(n, 4, np.uint8)
+    lines = int(go.sum())
+    po = rng.integers(2, 5, size=lines).astype(np.int32)
+    vb = rng.integers(-(1 << 20), 1 << 20, size=2 * int(po.sum()), dtype=np.int64).astype(np.int32)
+    cols.append({"types": types, "go": go.astype(np.int32), "po": po, "ro": np.zeros(0, np.int32), "vo": None,
+                 "vb": vb, "closed": False})
+    bad = A.synth_column(rng, 30000, False, False, probs=[0, 0, 1, 0, 0, 0])
+    bad = dict(bad, ro=bad["ro"].copy())
+    bad["ro"][-3] = -1  # a negative ring count in the last chunk of pass 3
+    cols.append(bad)
+    for c in cols:
+        c["caps"] = A.caps(c)
+        assert max(c["caps"]) <= covt.GEOM_MAX_CAP
+    asm, gres, lay = _run_kernel(covt, cols)
+    assert gres["status"].tolist()[:-1] == [0] * (len(cols) - 1)
+    assert int(gres["status"][-1]) == covt.ERR_COUNT_MISMATCH
+    _check_vs_oracle(oracle, cols, asm, gres, lay)
+    assert int(gres["num_coords"][0]) > 8 * 4096  # several chunks in every pass
+
+
 def _overflow_column(n_multi, parts_each, n_vertices):
     """n_multi MULTIPOINT features each claiming `parts_each` parts over a column of n_vertices point
     vertices: the part total is n_multi * parts_each (2^32 for the cases below), which a wrapping uint32

@@ -65,7 +65,7 @@ for s in "$@"; do
     mem_rle|mem_varint|mem_fastpfor|mem_lane) fam=${s#mem_}; step $s 600 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_TA_BUSY TA_DATA_STALLED_BY_TC_CYCLES TCP_PENDING_STALL_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     sq_rle|sq_varint|sq_fastpfor) fam=${s#sq_}; step $s 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     opinst) step opinst 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE -d gpurun_out/opinst -o run --output-format csv -- python tools/op_counters.py ;;
-    tests_changed) step pytest_changed 600 python -u -m pytest tests/test_gpu_assembly.py tests/test_gpu_split.py tests/test_gpu_rle_adversarial.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    tests_changed) step pytest_changed 600 python -u -m pytest tests/test_gpu_assembly.py tests/test_gpu_props.py tests/test_gpu_split.py tests/test_gpu_rle_adversarial.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     tests_dplan) step pytest_dplan 300 python -u -m pytest tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     dplan_geo) step dplan_geo 200 python tools/device_plan_prof.py 20 --sweep --geometry ;;
     dplan_ab) step dplan_ab 300 python tools/device_plan_ab.py 0 1 ;;

@@ -14,14 +14,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 import bench  # noqa: E402
 
 
-def launch_order_descs(plan, nbytes):
+def layout_descs(plan, nbytes, order, align):
+    """descriptors with every output slice re-assigned: slices in `order` (descriptor indices), each
+    starting on an `align`-byte boundary -> (descriptor bytes, new out_off per descriptor, buffer bytes)"""
     d = plan.descs.reshape(-1, 32).copy()
-    flags = d[:, 26:28].copy().view(np.uint16).ravel()
     assert plan.num_descs == plan.num_streams, "plan has split chunks"
-    sz = (nbytes + 15) // 16 * 16
-    oo = np.concatenate([[0], np.cumsum(sz)[:-1]]).astype(np.uint64)
+    sz = (nbytes[order] + align - 1) // align * align
+    oo = np.zeros(plan.num_streams, dtype=np.uint64)
+    oo[order] = np.concatenate([[0], np.cumsum(sz)[:-1]]).astype(np.uint64)
     d[:, 8:16] = oo.view(np.uint8).reshape(-1, 8)
-    return d.ravel().copy(), oo, flags
+    return d.ravel().copy(), oo, int(sz.sum())
 
 
 def main():
@@ -36,11 +38,22 @@ def main():
     s = plan.streams
     nbytes = np.zeros(plan.num_streams, dtype=np.int64)
     nbytes[s["desc_index"]] = (s["out_elems"] * s["elem_bytes"]).astype(np.int64)
-    ld, new_off, _ = launch_order_descs(plan, nbytes)
-    tile_desc = batch.d_desc
-    launch_desc = torch.from_numpy(ld).cuda()
-    old_off = plan.descs.reshape(-1, 32)[:, 8:16].copy().view(np.uint64).ravel()
-
+    tile_order = s["desc_index"].astype(np.int64)  # descriptor index of each stream, in tile order
+    launch_order = np.arange(plan.num_streams)
+    layouts = {}
+    for name, order, align in (("tile16", tile_order, 16), ("launch16", launch_order, 16),
+                               ("tile128", tile_order, 128), ("launch128", launch_order, 128),
+                               ("launch256", launch_order, 256)):
+        ld, off, total = layout_descs(plan, nbytes, order, align)
+        layouts[name] = (torch.from_numpy(ld).cuda(), off, total)
+    need = max(v[2] for v in layouts.values())
+    if need > batch.d_out.numel():
+        batch.d_out = torch.zeros(need + 16, dtype=torch.uint8, device="cuda")
+    tile_desc = layouts["tile16"][0]
+    launch_desc = layouts["launch16"][0]
+    new_off = layouts["launch16"][1]
+    old_off = layouts["tile16"][1]
+    assert np.array_equal(old_off, plan.descs.reshape(-1, 32)[:, 8:16].copy().view(np.uint64).ravel())
     # parity: the same bytes per stream in both layouts
     batch.d_desc = tile_desc
     batch.decode()
@@ -74,14 +87,14 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / per
 
-    ts = {"tile": [], "launch": []}
+    ts = {k: [] for k in layouts}
     for r in range(rounds):
-        ts["tile"].append(run(tile_desc))
-        ts["launch"].append(run(launch_desc))
+        for k, v in layouts.items():
+            ts[k].append(run(v[0]))
     alg = int(nbytes.sum()) + int(plan.descs.reshape(-1, 32)[:, 28:32].copy().view(np.int32).astype(np.int64).sum())
     for k, v in ts.items():
         m = float(np.median(v))
-        print("%-7s layout: median %.4f ms  (%s)  %.0f GB/s algorithmic, frac %.3f" % (
+        print("%-9s layout: median %.4f ms  (%s)  %.0f GB/s algorithmic, frac %.3f" % (
             k, m, " ".join("%.4f" % x for x in v), alg / m / 1e6, alg / m / 1e6 / 8000))
 
 
