@@ -1016,7 +1016,7 @@ void plan_property(PlanPart* p, int32_t t, int64_t tile_off, const PropRaw& q, i
         si.in_off = tile_off + q.s_off[role];
         si.out_elems = n;
         si.out_off = out_off;
-        out_off = align16(out_off + n * elem);
+        out_off = align_out(out_off + n * elem);
         p->in_bytes += q.s_bl[role];
         p->out_payload += n * elem;
         si.desc_index = (int32_t)n;  // temporarily: values to decode
@@ -1479,7 +1479,7 @@ int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, co
                     si.in_off = (int64_t)tile_offsets[t] + s.off;
                     si.out_elems = op == COVT_OP_NONE ? 0 : out_elems;
                     si.out_off = pp.out_off;
-                    pp.out_off = align16(pp.out_off + si.out_elems * elem);
+                    pp.out_off = align_out(pp.out_off + si.out_elems * elem);
                     pp.in_bytes += s.bl;
                     pp.out_payload += si.out_elems * elem;
                     if (s.kind == 1 && s.type == ST_VERTEX_BUFFER)

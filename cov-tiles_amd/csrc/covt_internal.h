@@ -35,6 +35,13 @@ constexpr int64_t kFusedMaxWaves = 4096;
 constexpr int kWavesPerBlock = COVT_WAVES_PER_BLOCK;
 constexpr int64_t kFusedLaneStreams = 64 * kWavesPerBlock;
 
+// Output slices of the decode launch (host and device plans): every stream's slice starts on a 128-byte
+// line.  A family's 1 KiB (or 2 KiB) wave stores then cover whole lines instead of straddling two partial
+// ones per store: the config-5 launch 1.602 -> 1.558 ms with the same kernels (tools/probe/layout_ab.py,
+// profiles/r04/layout_ab.txt; 16-byte slices, the round-3 layout, cost ~24 MB less buffer).
+constexpr int64_t kOutAlign = 128;
+__host__ __device__ inline int64_t align_out(int64_t x) { return (x + kOutAlign - 1) & ~(kOutAlign - 1); }
+
 // Plan rule for the lane-per-stream kernel: RLE streams of at most max_values values and max_bytes bytes
 // (a lane decodes serially; larger streams amortise a wave's window setup).  The two limits travel
 // packed as one int32 (values << 16 | bytes; < 0: no lane family), see lane_limits.

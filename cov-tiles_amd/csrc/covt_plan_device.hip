@@ -777,7 +777,7 @@ struct CountEmit {
         if (slots && writer && n < kSlots) slots[n] = s;
         ++n;
         const int64_t ob = (op == COVT_OP_NONE ? 0 : oe) * elem;
-        out = align16(out + ob);
+        out = align_out(out + ob);
         const int64_t c = (int64_t)s.bl + ob / 4;  // covt_plan_create's stream_cost
         cost += c;
         const int64_t sc = split_fpf_op(op) ? c + (fpf_w - 1) * (ob / 4) : c;
@@ -901,7 +901,7 @@ struct InfoEmit {
         si.in_off = tile_off + s.off;
         si.out_elems = op == COVT_OP_NONE ? 0 : oe;
         si.out_off = out;
-        out = align16(out + si.out_elems * elem);
+        out = align_out(out + si.out_elems * elem);
         in_bytes += s.bl;
         payload += si.out_elems * elem;
         if (s.kind == 1 && s.type == ST_VERTEX_BUFFER) verts += (s.ctype == CT_ICE || s.ctype == CT_ICE_MORTON) ? s.nv : s.nv / 2;
@@ -933,7 +933,7 @@ __global__ void walk_emit(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
 }
 
 // The records walk_count left in a tile's slots -> covt_stream_info, one lane per record: output slices
-// by a wave prefix sum of their aligned sizes (the walk's running align16 sum), totals by a wave
+// by a wave prefix sum of their aligned sizes (the walk's running align_out sum), totals by a wave
 // reduction.  Tiles with more than kSlots streams are left to walk_emit.
 __global__ void emit_slots(const uint64_t* __restrict__ offs, int32_t n_tiles, int32_t id_mode,
                            const int32_t* __restrict__ status, const int64_t* __restrict__ cnt,
@@ -959,7 +959,7 @@ __global__ void emit_slots(const uint64_t* __restrict__ offs, int32_t n_tiles, i
             choose_op(s, id_mode, op, nv, elem, oe);
         }
         const int64_t out_elems = op == COVT_OP_NONE ? 0 : oe;
-        const long long size = valid ? align16(out_elems * elem) : 0;
+        const long long size = valid ? align_out(out_elems * elem) : 0;
         long long incl = size;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {

@@ -198,7 +198,7 @@ void covt_plan_options_init(covt_plan_options* opts);
 /* One device-resident plan entry (32 bytes). */
 typedef struct covt_stream_desc {
     uint64_t in_off;     /* payload byte offset in the batch input buffer */
-    uint64_t out_off;    /* output byte offset in the batch output buffer (16-byte aligned) */
+    uint64_t out_off;    /* output byte offset in the batch output buffer (plans: 128-byte aligned) */
     int32_t avail;       /* readable payload bytes (byteLength for plans; buf_len-pos for stream calls) */
     int32_t num_values;  /* values (vertices for the Morton ops) to produce */
     uint8_t op;          /* enum covt_op */
@@ -466,7 +466,7 @@ int covt_plan_properties_host(const covt_plan* plan, const uint8_t* bytes, uint6
  * host memory).  d_bytes / n_bytes: the batch on the current device; d_tile_offsets / d_tile_sizes:
  * n_tiles uint64 each, on the device (a tile outside [0, n_bytes) gets COVT_ERR_INVALID_ARG as its
  * status).  The result is the host plan's layout exactly: streams in tile order with the same
- * covt_stream_info fields and 16-byte aligned output slices, descriptors in the same launch order
+ * covt_stream_info fields and 128-byte aligned output slices, descriptors in the same launch order
  * and families, including the split rule: with the same options, the long poles of a small batch are
  * cut into the same chunks (varint byte chunks, FastPFOR value chunks with their start states, ORC RLE
  * group chunks); geometry-column planning on request (covt_device_plan_geometry).  Property columns
