@@ -47,17 +47,14 @@ namespace covt {
 #define COVT_ASM_WAVES 4
 #endif
 constexpr int kAsmWaves = COVT_ASM_WAVES;  // independent waves (columns) per workgroup
-// Small batches (at most kCoopMaxColumns columns: one tile's latency, BASELINE config 1): columns with
-// at least kCoopMinItems features / parts / rings / coordinates are assembled by a whole workgroup of
-// kCoopWaves waves (4 x 64 x kCoopWaves items per step), the rest by single waves as in a batch.  A
-// column's passes are chains of dependent gathers, one step per 256 items on one wave (the config-1
-// tile's 35k-feature, 72k-coordinate line column: ~700 steps, 0.78 ms); sixteen waves take 16x fewer.
+// Small batches (at most kCoopMaxColumns columns: one tile's latency, BASELINE config 1): a column's
+// passes are chains of dependent gathers, one step per 256 items on one wave (the config-1 tile's
+// 35k-feature, 72k-coordinate line column: ~700 steps, 0.78 ms).  Columns of at least kSplitMinItems
+// features / parts / rings / coordinates are cut into chunks of one 4 x 64 x kCoopWaves-item step each,
+// run by as many workgroups at once (the split passes below); the rest by single waves as in a batch.
 constexpr int kCoopWaves = 16;
 constexpr int kCoopMaxColumns = 4096;
-constexpr int32_t kCoopMinItems = 8192;
-// ... and in such batches columns of at least this many items are cut into 4,096-item chunks on separate
-// workgroups (the split passes below) while the chunk budget lasts
-constexpr int32_t kSplitMinItems = 1024;
+constexpr int32_t kSplitMinItems = 512;
 
 typedef __attribute__((address_space(1))) const int32_t g_i32;
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
@@ -511,43 +508,20 @@ __device__ __forceinline__ int32_t column_items(const covt_geom_desc& d) {
     return max(max(n, d.part_cap), max(d.ring_cap, d.coord_cap));
 }
 
-// one wave per column; columns of at least `coop_min` items are left to assemble_coop_kernel
+// one wave per column (large batches: every wave has a column, the batch keeps the chip busy)
 __global__ __launch_bounds__(64 * kAsmWaves) void assemble_kernel(const uint8_t* __restrict__ dec,
                                                                   const covt_stream_result* __restrict__ dres,
                                                                   const covt_geom_desc* __restrict__ descs,
                                                                   int64_t n_cols, uint8_t* __restrict__ outb,
-                                                                  covt_geom_result* __restrict__ gres, int32_t coop_min,
-                                                                  const int32_t* __restrict__ split_flag) {
+                                                                  covt_geom_result* __restrict__ gres) {
     __shared__ AsmSmem smem[kAsmWaves];
     const int w = threadIdx.x >> 6;
     const int64_t c = uni64((int64_t)blockIdx.x * kAsmWaves + w);
     if (c >= n_cols) return;
-    if (split_flag && split_flag[c]) return;  // assembled by the split passes
     const covt_geom_desc d = descs[c];
-    if (uni(column_items(d)) >= coop_min && !((uint32_t)d.flags & COVT_GEOM_TOO_LARGE)) return;
     covt_geom_result r{COVT_OK, 0, 0, 0};
     assemble_column<1>(dec, dres, d, outb, r, smem[w]);
     if (lane_id() == 0) gres[c] = r;
-}
-
-// one workgroup of kCoopWaves waves per column of at least `coop_min` items (small batches only: the
-// grid is one workgroup per column, the others return at once)
-__global__ __launch_bounds__(64 * kCoopWaves) void assemble_coop_kernel(const uint8_t* __restrict__ dec,
-                                                                        const covt_stream_result* __restrict__ dres,
-                                                                        const covt_geom_desc* __restrict__ descs,
-                                                                        int64_t n_cols, uint8_t* __restrict__ outb,
-                                                                        covt_geom_result* __restrict__ gres,
-                                                                        int32_t coop_min,
-                                                                        const int32_t* __restrict__ split_flag) {
-    __shared__ AsmSmemT<kCoopWaves> smem;
-    const int64_t c = blockIdx.x;
-    if (c >= n_cols) return;
-    if (split_flag && split_flag[c]) return;  // assembled by the split passes
-    const covt_geom_desc d = descs[c];
-    if (column_items(d) < coop_min || ((uint32_t)d.flags & COVT_GEOM_TOO_LARGE)) return;  // (uniform)
-    covt_geom_result r{COVT_OK, 0, 0, 0};
-    assemble_column<kCoopWaves>(dec, dres, d, outb, r, smem);
-    if (threadIdx.x == 0) gres[c] = r;
 }
 
 // ---- multi-workgroup columns (small batches: one tile's latency, BASELINE config 1) -------------------
@@ -568,7 +542,7 @@ __global__ __launch_bounds__(64 * kCoopWaves) void assemble_coop_kernel(const ui
 //     marked column.
 // The last chunk of pass 4 to finish writes the column's result.
 constexpr int kSplitK = Coop<kCoopWaves>::K;  // items per chunk: one cooperative step
-constexpr int kSplitMaxChunks = 8192;          // per pass over all split columns (more: the coop path)
+constexpr int kSplitMaxChunks = 65536;         // per pass over all split columns (past it: single waves)
 constexpr int kSplitGrid = 256;                // persistent workgroups per pass kernel (tickets)
 constexpr uint32_t kSplitMaxSpins = 1u << 22;  // look-back polls (~seconds) before a column is failed
 
@@ -578,16 +552,18 @@ struct SplitCol {
     uint32_t done4;           // pass-4 chunks finished
     uint32_t pad;
 };
+// Per (device, stream) scratch of the split passes.  The look-back records carry the launch's epoch in
+// their high half (a record of an earlier launch reads as "not yet"), so nothing is cleared per launch.
 struct SplitScratch {
-    uint32_t ticket[4];                       // next chunk of pass p
-    int32_t n_split;                          // split columns
-    int32_t pad[3];
+    uint32_t ticket[4];                       // next ticket of pass p
+    int32_t n_split, n_small;                 // split columns; columns left to single waves
+    int32_t pad[2];
     int32_t pre[4][kCoopMaxColumns + 1];      // pass p: chunks of split columns before column k
     int32_t col[kCoopMaxColumns];             // split column k -> batch column
-    int32_t flag[kCoopMaxColumns];            // batch column c: split (1) or not (0)
+    int32_t small[kCoopMaxColumns];           // the other columns (single waves, pass 1's workgroups)
     SplitCol st[kCoopMaxColumns];
     int2 base[4][kSplitMaxChunks];            // pass p (1..3) chunk: (segment, segment start) of its first item
-    unsigned long long rec[4][3][kSplitMaxChunks];  // pass p, scan s, chunk: (1 << 32 | total), 0 = not yet
+    unsigned long long rec[4][3][kSplitMaxChunks];  // pass p, scan s, chunk: (epoch << 32 | total)
 };
 
 // chunks per pass of a column: ceil(capacity / kSplitK) (chunks past the pass's real item count exit)
@@ -599,99 +575,100 @@ __device__ __forceinline__ void split_chunks(const covt_geom_desc& d, int32_t (&
     c[3] = max(1, (d.coord_cap + kSplitK - 1) / kSplitK);
 }
 
-// one workgroup: the split columns (items >= coop_min, not too large, in batch order while every pass
-// keeps within kSplitMaxChunks) and their chunk prefixes; every workgroup: zeroes the look-back records
-__global__ __launch_bounds__(1024) void split_prep(const covt_geom_desc* __restrict__ descs, int64_t n_cols,
-                                                   int32_t coop_min, SplitScratch* __restrict__ sc) {
-    {  // the records (the largest part), by every workgroup
-        uint4* r = (uint4*)&sc->rec[0][0][0];
-        const int64_t n16 = (int64_t)sizeof(sc->rec) / 16;
-        for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 1024)
-            r[i] = make_uint4(0, 0, 0, 0);
+// exclusive prefix over a 1024-thread workgroup of NV int32 values per thread (DPP wave scans, the 16
+// wave totals through LDS); tot gets the workgroup totals
+template <int NV>
+__device__ __forceinline__ void wg_excl_scan(int32_t (&x)[NV], int32_t (&tot)[NV], int32_t (*lds)[16]) {
+    const int w = threadIdx.x >> 6;
+    uint32_t inc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        inc[v] = incl_scan((uint32_t)x[v]);
+        if (lane_id() == 63) lds[v][w] = (int32_t)inc[v];
     }
-    if (blockIdx.x != 0) return;
-    __shared__ int32_t part[4][1024];
-    // every thread takes 4 consecutive columns
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        int32_t pre = 0, all = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int32_t t = lds[v][i];
+            pre += i < w ? t : 0;
+            all += t;
+        }
+        x[v] = pre + (int32_t)inc[v] - x[v];
+        tot[v] = all;
+    }
+    __syncthreads();
+}
+
+// One workgroup: the columns of at least split_min items (not too large) become split columns, in batch
+// order while every pass keeps within kSplitMaxChunks; the others go to the small list (single waves)
+__global__ __launch_bounds__(1024) void split_prep(const covt_geom_desc* __restrict__ descs, int64_t n_cols,
+                                                   int32_t split_min, SplitScratch* __restrict__ sc) {
+    __shared__ int32_t lds[6][16];
     const int t = threadIdx.x;
-    int32_t ch[4][4] = {}, want[4] = {};
+    int32_t ch[4][4] = {};
+    bool want[4] = {}, live[4] = {};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t c = 4 * t + k;
-        if (c < n_cols) {
+        live[k] = c < n_cols;
+        if (live[k]) {
             const covt_geom_desc d = descs[c];
-            if (column_items(d) >= coop_min && !((uint32_t)d.flags & COVT_GEOM_TOO_LARGE)) {
+            if (column_items(d) >= split_min && !((uint32_t)d.flags & COVT_GEOM_TOO_LARGE)) {
                 split_chunks(d, ch[k]);
-                want[k] = 1;
+                want[k] = true;
             }
         }
     }
-    // inclusive per-thread sums of chunks per pass, then a workgroup scan (the budget: a column is split
-    // only while every pass's running total stays within kSplitMaxChunks; batch order decides)
-    int32_t s[4];
+    // the budget: a thread whose running chunk totals pass kSplitMaxChunks splits none of its columns
+    int32_t x[6], tot[6];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) s[p] = ch[0][p] + ch[1][p] + ch[2][p] + ch[3][p];
-    for (int p = 0; p < 4; ++p) part[p][t] = s[p];
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele scan (one-off, small)
-        int32_t v[4];
-        for (int p = 0; p < 4; ++p) v[p] = t >= off ? part[p][t - off] : 0;
-        __syncthreads();
-        for (int p = 0; p < 4; ++p) part[p][t] += v[p];
-        __syncthreads();
-    }
-    int32_t run[4];
-    for (int p = 0; p < 4; ++p) run[p] = part[p][t] - s[p];
+    for (int p = 0; p < 4; ++p) x[p] = ch[0][p] + ch[1][p] + ch[2][p] + ch[3][p];
+    x[4] = x[5] = 0;
+    int32_t own[4] = {x[0], x[1], x[2], x[3]};
+    wg_excl_scan<6>(x, tot, lds);
     bool fits = true;
-    for (int p = 0; p < 4; ++p) fits = fits && part[p][t] <= kSplitMaxChunks;
-    // a thread whose columns would pass the budget splits none of them (the budget is generous: config 1
-    // uses ~60 chunks of 8192; a batch past it keeps its big columns on the single-workgroup path)
-    int32_t nsplit = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) nsplit += (fits && want[k]) ? 1 : 0;
-    __shared__ int32_t cnt[1024];
-    cnt[t] = nsplit;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const int32_t v = t >= off ? cnt[t - off] : 0;
-        __syncthreads();
-        cnt[t] += v;
-        __syncthreads();
-    }
-    int32_t idx = cnt[t] - nsplit;
-    // prefixes over split columns only: recount chunks of the columns kept
-    int32_t keep[4][4] = {};
+    for (int p = 0; p < 4; ++p) fits = fits && x[p] + own[p] <= kSplitMaxChunks;
+    bool keep[4];
+    int32_t nsplit = 0, nsmall = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        for (int p = 0; p < 4; ++p) keep[k][p] = (fits && want[k]) ? ch[k][p] : 0;
-    for (int p = 0; p < 4; ++p) part[p][t] = keep[0][p] + keep[1][p] + keep[2][p] + keep[3][p];
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        int32_t v[4];
-        for (int p = 0; p < 4; ++p) v[p] = t >= off ? part[p][t - off] : 0;
-        __syncthreads();
-        for (int p = 0; p < 4; ++p) part[p][t] += v[p];
-        __syncthreads();
+    for (int k = 0; k < 4; ++k) {
+        keep[k] = fits && want[k];
+        nsplit += keep[k] ? 1 : 0;
+        nsmall += (live[k] && !keep[k]) ? 1 : 0;
     }
-    for (int p = 0; p < 4; ++p) run[p] = part[p][t] - (keep[0][p] + keep[1][p] + keep[2][p] + keep[3][p]);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) x[p] = keep[0] * ch[0][p] + keep[1] * ch[1][p] + keep[2] * ch[2][p] + keep[3] * ch[3][p];
+    x[4] = nsplit;
+    x[5] = nsmall;
+    wg_excl_scan<6>(x, tot, lds);
+    int32_t run[4] = {x[0], x[1], x[2], x[3]}, idx = x[4], sidx = x[5];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t c = 4 * t + k;
-        if (c >= n_cols) continue;
-        const bool sp = fits && want[k];
-        sc->flag[c] = sp ? 1 : 0;
-        if (!sp) continue;
+        if (!live[k]) continue;
+        if (!keep[k]) {
+            sc->small[sidx++] = (int32_t)c;
+            continue;
+        }
         sc->col[idx] = (int32_t)c;
+#pragma unroll
         for (int p = 0; p < 4; ++p) {
             sc->pre[p][idx] = run[p];
-            run[p] += keep[k][p];
+            run[p] += ch[k][p];
         }
         sc->st[idx] = SplitCol{~0ull, 0, 0, 0, 0, 0, 0};
         ++idx;
     }
-    if (t == 1023) {
-        sc->n_split = cnt[1023];
+    if (t == 0) {
+        sc->n_split = tot[4];
+        sc->n_small = tot[5];
+#pragma unroll
         for (int p = 0; p < 4; ++p) {
-            sc->pre[p][cnt[1023]] = part[p][1023];
+            sc->pre[p][tot[4]] = tot[p];
             sc->ticket[p] = 0;
         }
     }
@@ -708,9 +685,10 @@ __device__ __forceinline__ void st_rel(unsigned long long* p, unsigned long long
 // (saturating; every thread gets them).  Chunks of a column are consecutive record slots from `g0`.
 template <int NS>
 __device__ __forceinline__ void split_gather(AsmSmemT<kCoopWaves>& sm, unsigned long long (*rec)[kSplitMaxChunks],
-                                             int32_t g0, int32_t j, const uint32_t (&own)[NS], uint32_t (&pre)[NS]) {
+                                             int32_t g0, int32_t j, const uint32_t (&own)[NS], uint32_t (&pre)[NS],
+                                             uint32_t epoch) {
     if (threadIdx.x == 0)
-        for (int s = 0; s < NS; ++s) st_rel(&rec[s][g0 + j], (1ull << 32) | own[s]);
+        for (int s = 0; s < NS; ++s) st_rel(&rec[s][g0 + j], ((unsigned long long)epoch << 32) | own[s]);
     uint32_t acc[NS];
     for (int s = 0; s < NS; ++s) acc[s] = 0;
     bool lost = false;
@@ -720,8 +698,9 @@ __device__ __forceinline__ void split_gather(AsmSmemT<kCoopWaves>& sm, unsigned 
             // bounded wait: a predecessor that never publishes (a bug, not an input property) fails the
             // column instead of hanging the launch
             uint32_t spins = 0;
-            while (!((v = ld_acq(&rec[s][g0 + i])) >> 32) && ++spins < kSplitMaxSpins) __builtin_amdgcn_s_sleep(2);
-            lost |= !(v >> 32);
+            while ((uint32_t)((v = ld_acq(&rec[s][g0 + i])) >> 32) != epoch && ++spins < kSplitMaxSpins)
+                __builtin_amdgcn_s_sleep(2);
+            lost |= (uint32_t)(v >> 32) != epoch;
             acc[s] = add_sat(acc[s], (uint32_t)v);
         }
     }
@@ -770,7 +749,7 @@ template <int PASS>
 __device__ void split_chunk(const uint8_t* __restrict__ dec, const covt_stream_result* __restrict__ dres,
                             const covt_geom_desc& d, uint8_t* __restrict__ outb, SplitScratch* __restrict__ sc,
                             int32_t k, int32_t j, AsmSmemT<kCoopWaves>& sm, covt_geom_result* __restrict__ gres,
-                            int32_t c) {
+                            int32_t c, uint32_t epoch) {
     constexpr int NW = kCoopWaves, K = kSplitK;
     const int l = threadIdx.x;
     int buf = 0;
@@ -834,7 +813,7 @@ __device__ void split_chunk(const uint8_t* __restrict__ dec, const covt_stream_r
         }
         excl_scan4(sm, buf, multi, gi, nm);
         uint32_t own1[1] = {nm}, pre1[1];
-        split_gather<1>(sm, sc->rec[0], g0, j, own1, pre1);
+        split_gather<1>(sm, sc->rec[0], g0, j, own1, pre1, epoch);
         const uint32_t go_base = pre1[0];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -851,7 +830,7 @@ __device__ void split_chunk(const uint8_t* __restrict__ dec, const covt_stream_r
         }
         excl_scan4(sm, buf, pf, ex, tot);
         uint32_t own2[1] = {tot}, pre2[1];
-        split_gather<1>(sm, sc->rec[0] + 1, g0, j, own2, pre2);
+        split_gather<1>(sm, sc->rec[0] + 1, g0, j, own2, pre2, epoch);
         const uint32_t P0 = pre2[0], P1 = add_sat(P0, tot);
         const bool any_type = __syncthreads_or(bad_type), any_cnt = __syncthreads_or(bad_cnt);
         if (any_type || any_cnt || P1 > pcap) {
@@ -900,7 +879,7 @@ __device__ void split_chunk(const uint8_t* __restrict__ dec, const covt_stream_r
         }
         npo = usep_all;
         uint32_t own1[1] = {npo}, pre1[1];
-        split_gather<1>(sm, sc->rec[1], g0, j, own1, pre1);
+        split_gather<1>(sm, sc->rec[1], g0, j, own1, pre1, epoch);
         uint32_t po_base = pre1[0];
         // sweep B: the ring counts (re-expanding only if the chunk took more than one step)
         uint32_t R0 = 0, Rrun = 0;
@@ -936,7 +915,7 @@ __device__ void split_chunk(const uint8_t* __restrict__ dec, const covt_stream_r
             ring_counts(t, usep, pi, L, po_base);
             excl_scan4(sm, buf, rp, ex, tot);
             uint32_t own2[1] = {tot}, pre2[1];
-            split_gather<1>(sm, sc->rec[1] + 1, g0, j, own2, pre2);
+            split_gather<1>(sm, sc->rec[1] + 1, g0, j, own2, pre2, epoch);
             R0 = pre2[0];
             Rrun = add_sat(R0, tot);
             const bool any_cnt = __syncthreads_or(bad_cnt);
@@ -971,7 +950,7 @@ __device__ void split_chunk(const uint8_t* __restrict__ dec, const covt_stream_r
                 pob = add_sat(pob, stot);
             }
             uint32_t own2[1] = {rtot}, pre2[1];
-            split_gather<1>(sm, sc->rec[1] + 1, g0, j, own2, pre2);
+            split_gather<1>(sm, sc->rec[1] + 1, g0, j, own2, pre2, epoch);
             R0 = pre2[0];
             Rrun = add_sat(R0, rtot);
             const bool any_cnt = __syncthreads_or(bad_cnt);
@@ -1041,7 +1020,7 @@ __device__ void split_chunk(const uint8_t* __restrict__ dec, const covt_stream_r
             npoly = add_sat(npoly, stot);
         }
         uint32_t own1[1] = {npoly}, pre1[1];
-        split_gather<1>(sm, sc->rec[2], g0, j, own1, pre1);
+        split_gather<1>(sm, sc->rec[2], g0, j, own1, pre1, epoch);
         const uint32_t ro_base = pre1[0];
         bool bad_cnt = false;
         uint32_t closing[4], vo_[4], ex[4], src[4], tv = 0, ts = 0;
@@ -1095,7 +1074,7 @@ __device__ void split_chunk(const uint8_t* __restrict__ dec, const covt_stream_r
             }
         }
         uint32_t own2[2] = {tv, ts}, pre2[2];
-        split_gather<2>(sm, sc->rec[2] + 1, g0, j, own2, pre2);
+        split_gather<2>(sm, sc->rec[2] + 1, g0, j, own2, pre2, epoch);
         V0 = pre2[0];
         VS0 = pre2[1];
         V1 = add_sat(V0, tv);
@@ -1217,34 +1196,55 @@ __device__ void split_chunk(const uint8_t* __restrict__ dec, const covt_stream_r
 }
 
 // pass PASS over every split column: workgroups take chunks by ticket (a chunk waits only on chunks of
-// its column with lower tickets, all already running) until the pass has none left
+// its column with lower tickets, all already running) until the pass has none left; pass 1's workgroups
+// then take the small columns, sixteen per ticket, one wave each (their four passes on that wave)
 template <int PASS>
 __global__ __launch_bounds__(64 * kCoopWaves) void split_pass_kernel(const uint8_t* __restrict__ dec,
                                                                      const covt_stream_result* __restrict__ dres,
                                                                      const covt_geom_desc* __restrict__ descs,
                                                                      uint8_t* __restrict__ outb,
                                                                      covt_geom_result* __restrict__ gres,
-                                                                     SplitScratch* __restrict__ sc) {
-    __shared__ AsmSmemT<kCoopWaves> smem;
+                                                                     SplitScratch* __restrict__ sc, uint32_t epoch) {
+    __shared__ union U {
+        AsmSmemT<kCoopWaves> coop;
+        AsmSmem wave[kCoopWaves];
+    } smem;
+    __shared__ int32_t lpre[kCoopMaxColumns + 1];  // the pass's chunk prefixes (binary search in LDS)
     __shared__ int32_t tk;
     const int32_t ns = sc->n_split;
     const int32_t total = sc->pre[PASS - 1][ns];
+    const int32_t small_groups = PASS == 1 ? (sc->n_small + kCoopWaves - 1) / kCoopWaves : 0;
+    for (int32_t i = threadIdx.x; i <= ns; i += 64 * kCoopWaves) lpre[i] = sc->pre[PASS - 1][i];
+    __syncthreads();
     for (;;) {
         if (threadIdx.x == 0) tk = (int32_t)atomicAdd(&sc->ticket[PASS - 1], 1u);
         __syncthreads();
         const int32_t g = tk;
         __syncthreads();
-        if (g >= total) return;
-        // the split column holding chunk g: the last k with pre[k] <= g (binary search over ns + 1 prefixes)
-        int32_t lo = 0, hi = ns;  // pre[lo] <= g < pre[hi]
+        if (g >= total) {
+            if (PASS != 1 || g >= total + small_groups) return;
+            const int w = threadIdx.x >> 6;
+            const int32_t si = (g - total) * kCoopWaves + w;
+            if (si < sc->n_small) {  // (wave-uniform)
+                const int32_t c = uni(sc->small[si]);
+                const covt_geom_desc d = descs[c];
+                covt_geom_result r{COVT_OK, 0, 0, 0};
+                assemble_column<1>(dec, dres, d, outb, r, smem.wave[w]);
+                if (lane_id() == 0) gres[c] = r;
+            }
+            __syncthreads();
+            continue;
+        }
+        // the split column holding chunk g: the last k with lpre[k] <= g
+        int32_t lo = 0, hi = ns;  // lpre[lo] <= g < lpre[hi]
         while (hi - lo > 1) {
             const int32_t mid = (lo + hi) >> 1;
-            if (sc->pre[PASS - 1][mid] <= g) lo = mid;
+            if (lpre[mid] <= g) lo = mid;
             else hi = mid;
         }
-        const int32_t k = lo, j = g - sc->pre[PASS - 1][k], c = sc->col[k];
+        const int32_t k = lo, j = g - lpre[k], c = sc->col[k];
         const covt_geom_desc d = descs[c];
-        split_chunk<PASS>(dec, dres, d, outb, sc, k, j, smem, gres, c);
+        split_chunk<PASS>(dec, dres, d, outb, sc, k, j, smem.coop, gres, c, epoch);
         __syncthreads();
     }
 }
@@ -1252,16 +1252,26 @@ __global__ __launch_bounds__(64 * kCoopWaves) void split_pass_kernel(const uint8
 }  // namespace covt
 
 namespace {
-// split-pass scratch, one per (device, stream): launches on one stream are ordered, so they can share it
+// split-pass scratch, one per (device, stream): launches on one stream are ordered, so they can share it;
+// the epoch tags each launch's look-back records
+struct SplitSlot {
+    void* p = nullptr;
+    uint32_t epoch = 0;
+};
 std::mutex g_split_mu;
-std::map<std::pair<int, hipStream_t>, void*> g_split_scratch;
-covt::SplitScratch* split_scratch(hipStream_t s) {
+std::map<std::pair<int, hipStream_t>, SplitSlot> g_split_scratch;
+covt::SplitScratch* split_scratch(hipStream_t s, uint32_t& epoch) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> g(g_split_mu);
-    void*& p = g_split_scratch[std::make_pair(dev, s)];
-    if (!p && hipMalloc(&p, sizeof(covt::SplitScratch)) != hipSuccess) p = nullptr;
-    return (covt::SplitScratch*)p;
+    SplitSlot& q = g_split_scratch[std::make_pair(dev, s)];
+    if (!q.p) {
+        if (hipMalloc(&q.p, sizeof(covt::SplitScratch)) != hipSuccess) return (covt::SplitScratch*)(q.p = nullptr);
+        if (hipMemset(q.p, 0, sizeof(covt::SplitScratch)) != hipSuccess) return nullptr;  // epoch 0: never used
+    }
+    if (++q.epoch == 0) q.epoch = 1;
+    epoch = q.epoch;
+    return (covt::SplitScratch*)q.p;
 }
 }  // namespace
 
@@ -1274,29 +1284,27 @@ extern "C" int covt_assemble_geometry_device(const uint8_t* d_decoded, const cov
     const int64_t blocks = (n_columns + covt::kAsmWaves - 1) / covt::kAsmWaves;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
     hipStream_t s = (hipStream_t)hip_stream;
-    // small batches: big columns by many workgroups at once (the split passes), or -- past the split
-    // budget -- by one whole workgroup each; launched first: they are the critical path
+    // small batches (one tile's latency): big columns by many workgroups at once (the split passes);
+    // large batches: a wave per column
     const bool coop = n_columns <= covt::kCoopMaxColumns;
-    const int32_t coop_min = coop ? covt::kCoopMinItems : 0x7fffffff;
-    const int32_t* split_flag = nullptr;
     if (coop) {
-        covt::SplitScratch* sc = split_scratch(s);
+        // every column in the split passes' kernels: big ones chunked, the rest on single waves in pass 1
+        uint32_t epoch = 0;
+        covt::SplitScratch* sc = split_scratch(s, epoch);
         if (!sc) return COVT_ERR_DEVICE;
-        split_flag = sc->flag;
         const dim3 wg(64 * covt::kCoopWaves);
-        hipLaunchKernelGGL(covt::split_prep, dim3(64), dim3(1024), 0, s, d_gdesc, n_columns, covt::kSplitMinItems, sc);
+        hipLaunchKernelGGL(covt::split_prep, dim3(1), dim3(1024), 0, s, d_gdesc, n_columns, covt::kSplitMinItems, sc);
         hipLaunchKernelGGL(covt::split_pass_kernel<1>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
-                           d_asm, d_gres, sc);
+                           d_asm, d_gres, sc, epoch);
         hipLaunchKernelGGL(covt::split_pass_kernel<2>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
-                           d_asm, d_gres, sc);
+                           d_asm, d_gres, sc, epoch);
         hipLaunchKernelGGL(covt::split_pass_kernel<3>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
-                           d_asm, d_gres, sc);
+                           d_asm, d_gres, sc, epoch);
         hipLaunchKernelGGL(covt::split_pass_kernel<4>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
-                           d_asm, d_gres, sc);
-        hipLaunchKernelGGL(covt::assemble_coop_kernel, dim3((unsigned)n_columns), wg, 0, s, d_decoded, d_res, d_gdesc,
-                           n_columns, d_asm, d_gres, coop_min, split_flag);
+                           d_asm, d_gres, sc, epoch);
+    } else {
+        hipLaunchKernelGGL(covt::assemble_kernel, dim3((unsigned)blocks), dim3(64 * covt::kAsmWaves), 0, s, d_decoded,
+                           d_res, d_gdesc, n_columns, d_asm, d_gres);
     }
-    hipLaunchKernelGGL(covt::assemble_kernel, dim3((unsigned)blocks), dim3(64 * covt::kAsmWaves), 0, s, d_decoded,
-                       d_res, d_gdesc, n_columns, d_asm, d_gres, coop_min, split_flag);
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
 }

@@ -28,15 +28,12 @@ namespace covt {
 #endif
 constexpr int kPropWaves = COVT_PROP_WAVES;  // independent waves (columns) per workgroup
 // Small batches (at most kPropCoopMaxColumns columns, e.g. one tile: BASELINE config 1): columns of at
-// least kPropCoopMinFeatures features are materialized by a whole workgroup of kPropCoopWaves waves
-// (4 x 64 x kPropCoopWaves features per step; a step is a chain of dependent loads: the validity
-// nibbles, then the gathers at the scanned ranks), the rest by single waves.
+// least kPropSplitMinFeatures features are cut into chunks of 4 x 64 x kPropCoopWaves features (one step
+// of a whole workgroup; a step is a chain of dependent loads: the validity nibbles, then the gathers at
+// the scanned ranks) run by as many workgroups at once (prop_split_kernel below), the rest by single waves.
 constexpr int kPropCoopWaves = 16;
 constexpr int kPropCoopMaxColumns = 4096;
-constexpr int32_t kPropCoopMinFeatures = 8192;
-// ... and in such batches columns of at least this many features are cut into 4,096-feature chunks on
-// separate workgroups (prop_split_kernel below) while the chunk budget lasts
-constexpr int32_t kPropSplitMinFeatures = 1024;
+constexpr int32_t kPropSplitMinFeatures = 512;
 
 struct PropSmem {
     uint32_t red[2][kPropCoopWaves];  // per-wave partials (two buffers, alternating)
@@ -285,44 +282,20 @@ __device__ void materialize(const uint8_t* in, const uint8_t* dec, const covt_st
     res.n_valid = (int32_t)carry;
 }
 
-// one wave per column; columns of at least `coop_min` features are left to props_coop_kernel
+// one wave per column (large batches)
 __global__ __launch_bounds__(64 * kPropWaves) void props_kernel(const uint8_t* __restrict__ in,
                                                                 const uint8_t* __restrict__ dec,
                                                                 const covt_stream_result* __restrict__ dres,
                                                                 const covt_prop_desc* __restrict__ descs,
                                                                 int64_t n_cols, uint8_t* __restrict__ outb,
-                                                                covt_prop_result* __restrict__ pres, int32_t coop_min,
-                                                                const int32_t* __restrict__ split_flag) {
+                                                                covt_prop_result* __restrict__ pres) {
     const int w = threadIdx.x >> 6;
     const int64_t c = uni64((int64_t)blockIdx.x * kPropWaves + w);
     if (c >= n_cols) return;
-    if (split_flag && split_flag[c]) return;  // materialized by prop_split_kernel
     const covt_prop_desc d = descs[c];
-    if (uni(d.n_features) >= coop_min) return;
     covt_prop_result r;
     materialize<1>(in, dec, dres, d, outb, r, nullptr);
     if (lane_id() == 0) pres[c] = r;
-}
-
-// one workgroup of kPropCoopWaves waves per column of at least `coop_min` features (small batches only:
-// one workgroup per column, the others return at once)
-__global__ __launch_bounds__(64 * kPropCoopWaves) void props_coop_kernel(const uint8_t* __restrict__ in,
-                                                                         const uint8_t* __restrict__ dec,
-                                                                         const covt_stream_result* __restrict__ dres,
-                                                                         const covt_prop_desc* __restrict__ descs,
-                                                                         int64_t n_cols, uint8_t* __restrict__ outb,
-                                                                         covt_prop_result* __restrict__ pres,
-                                                                         int32_t coop_min,
-                                                                         const int32_t* __restrict__ split_flag) {
-    __shared__ PropSmem smem;
-    const int64_t c = blockIdx.x;
-    if (c >= n_cols) return;
-    if (split_flag && split_flag[c]) return;  // materialized by prop_split_kernel
-    const covt_prop_desc d = descs[c];
-    if (d.n_features < coop_min) return;  // (uniform)
-    covt_prop_result r;
-    materialize<kPropCoopWaves>(in, dec, dres, d, outb, r, &smem);
-    if (threadIdx.x == 0) pres[c] = r;
 }
 
 // ---- multi-workgroup columns (small batches: one tile's latency, BASELINE config 1) -------------------
@@ -334,7 +307,7 @@ __global__ __launch_bounds__(64 * kPropCoopWaves) void props_coop_kernel(const u
 // its validity bits and values.  Chunk 0 also builds (or checks) the dictionary; the last chunk of a
 // column to finish writes the column's result in Java's status order.
 constexpr int kPropSplitK = 4 * 64 * kPropCoopWaves;  // features per chunk
-constexpr int kPropSplitMaxChunks = 16384;          // over all split columns (more: the coop path)
+constexpr int kPropSplitMaxChunks = 65536;          // over all split columns (past it: single waves)
 constexpr int kPropSplitGrid = 256;                 // persistent workgroups (tickets)
 constexpr uint32_t kPropSplitMaxSpins = 1u << 22;   // look-back polls before a column is failed
 
@@ -344,81 +317,103 @@ struct PropSplitCol {
     uint32_t done;         // chunks finished
     uint32_t n_valid;      // present features (the last chunk)
 };
+// Per (device, stream) scratch; records carry the launch's epoch in their high half (nothing is cleared
+// per launch)
 struct PropSplitScratch {
     uint32_t ticket;
-    int32_t n_split;
-    int32_t pad[2];
+    int32_t n_split, n_small;
+    int32_t pad;
     int32_t pre[kPropCoopMaxColumns + 1];  // chunks of split columns before column k
     int32_t col[kPropCoopMaxColumns];      // split column k -> batch column
-    int32_t flag[kPropCoopMaxColumns];     // batch column c: split (1) or not (0)
+    int32_t small[kPropCoopMaxColumns];    // the other columns (single waves)
     PropSplitCol st[kPropCoopMaxColumns];
-    unsigned long long rec[kPropSplitMaxChunks];  // chunk: (1 << 32 | present count), 0 = not yet
+    unsigned long long rec[kPropSplitMaxChunks];  // chunk: (epoch << 32 | present count)
 };
 
 __device__ __forceinline__ bool prop_split_wanted(const covt_prop_desc& d, int32_t split_min) {
     return d.n_features >= split_min && !(d.flags & COVT_PROP_UNSUPPORTED);
 }
 
-// one workgroup: the split columns and their chunk prefixes (batch order while within the budget);
-// every workgroup: zeroes the records
+// exclusive prefix of NV int32 per thread over a 1024-thread workgroup (DPP wave scans + 16 wave totals)
+template <int NV>
+__device__ __forceinline__ void pwg_excl_scan(int32_t (&x)[NV], int32_t (&tot)[NV], int32_t (*lds)[16]) {
+    const int w = threadIdx.x >> 6;
+    uint32_t inc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        inc[v] = incl_scan((uint32_t)x[v]);
+        if (lane_id() == 63) lds[v][w] = (int32_t)inc[v];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        int32_t pre = 0, all = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int32_t t = lds[v][i];
+            pre += i < w ? t : 0;
+            all += t;
+        }
+        x[v] = pre + (int32_t)inc[v] - x[v];
+        tot[v] = all;
+    }
+    __syncthreads();
+}
+
+// one workgroup: the split columns and their chunk prefixes (batch order while within the budget), and
+// the small list (every other column)
 __global__ __launch_bounds__(1024) void prop_split_prep(const covt_prop_desc* __restrict__ descs, int64_t n_cols,
                                                         int32_t split_min, PropSplitScratch* __restrict__ sc) {
-    for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < kPropSplitMaxChunks; i += (int64_t)gridDim.x * 1024)
-        sc->rec[i] = 0ull;
-    if (blockIdx.x != 0) return;
-    __shared__ int32_t a[1024], b[1024];
+    __shared__ int32_t lds[3][16];
     const int t = threadIdx.x;
     int32_t ch[4] = {};
+    bool live[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t c = 4 * t + k;
-        if (c < n_cols) {
+        live[k] = c < n_cols;
+        if (live[k]) {
             const covt_prop_desc d = descs[c];
             if (prop_split_wanted(d, split_min)) ch[k] = (d.n_features + kPropSplitK - 1) / kPropSplitK;
         }
     }
-    const int32_t s = ch[0] + ch[1] + ch[2] + ch[3];
-    a[t] = s;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const int32_t v = t >= off ? a[t - off] : 0;
-        __syncthreads();
-        a[t] += v;
-        __syncthreads();
-    }
-    const bool fits = a[t] <= kPropSplitMaxChunks;  // (the prefix only grows: the budget cuts a tail)
-    int32_t keep = 0, nk = 0;
+    int32_t x[3], tot[3];
+    x[0] = ch[0] + ch[1] + ch[2] + ch[3];
+    x[1] = x[2] = 0;
+    const int32_t own = x[0];
+    pwg_excl_scan<3>(x, tot, lds);
+    const bool fits = x[0] + own <= kPropSplitMaxChunks;  // (the prefix only grows: the budget cuts a tail)
+    int32_t keep = 0, nk = 0, nsm = 0;
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
-        keep += fits ? ch[k] : 0;
-        nk += (fits && ch[k]) ? 1 : 0;
+        const bool sp = fits && ch[k] > 0;
+        keep += sp ? ch[k] : 0;
+        nk += sp ? 1 : 0;
+        nsm += (live[k] && !sp) ? 1 : 0;
     }
-    a[t] = keep;
-    b[t] = nk;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const int32_t v = t >= off ? a[t - off] : 0, w = t >= off ? b[t - off] : 0;
-        __syncthreads();
-        a[t] += v;
-        b[t] += w;
-        __syncthreads();
-    }
-    int32_t run = a[t] - keep, idx = b[t] - nk;
+    x[0] = keep;
+    x[1] = nk;
+    x[2] = nsm;
+    pwg_excl_scan<3>(x, tot, lds);
+    int32_t run = x[0], idx = x[1], sidx = x[2];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t c = 4 * t + k;
-        if (c >= n_cols) continue;
-        const bool sp = fits && ch[k] > 0;
-        sc->flag[c] = sp ? 1 : 0;
-        if (!sp) continue;
+        if (!live[k]) continue;
+        if (!(fits && ch[k] > 0)) {
+            sc->small[sidx++] = (int32_t)c;
+            continue;
+        }
         sc->col[idx] = (int32_t)c;
         sc->pre[idx] = run;
         sc->st[idx] = PropSplitCol{COVT_OK, 0u, 0u, 0u};
         run += ch[k];
         ++idx;
     }
-    if (t == 1023) {
-        sc->n_split = b[1023];
-        sc->pre[b[1023]] = a[1023];
+    if (t == 0) {
+        sc->n_split = tot[1];
+        sc->n_small = tot[2];
+        sc->pre[tot[1]] = tot[0];
         sc->ticket = 0;
     }
 }
@@ -430,7 +425,7 @@ __device__ __forceinline__ unsigned long long pld_rlx(const unsigned long long* 
 // chunk j of split column k (batch column c)
 __device__ void prop_split_chunk(const uint8_t* in, const uint8_t* dec, const covt_stream_result* dres,
                                  const covt_prop_desc& d, uint8_t* outb, covt_prop_result* pres, PropSplitScratch* sc,
-                                 int32_t k, int32_t j, int32_t c, PropSmem* smp) {
+                                 int32_t k, int32_t j, int32_t c, PropSmem* smp, uint32_t epoch) {
     constexpr int NW = kPropCoopWaves;
     const int l = (int)threadIdx.x, wv = (int)(threadIdx.x >> 6);
     PropSplitCol& cs = sc->st[k];
@@ -468,14 +463,17 @@ __device__ void prop_split_chunk(const uint8_t* in, const uint8_t* dec, const co
             tot += t;
         }
         // publish this chunk's count, sum the predecessors' (bounded wait: a lost record fails the column)
-        if (l == 0) __hip_atomic_store(&sc->rec[g0 + j], (1ull << 32) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (l == 0)
+            __hip_atomic_store(&sc->rec[g0 + j], ((unsigned long long)epoch << 32) | tot, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         uint32_t acc = 0;
         bool lost = false;
         for (int32_t i = l; i < j; i += 1024) {
             unsigned long long v;
             uint32_t spins = 0;
-            while (!((v = pld_rlx(&sc->rec[g0 + i])) >> 32) && ++spins < kPropSplitMaxSpins) __builtin_amdgcn_s_sleep(2);
-            lost |= !(v >> 32);
+            while ((uint32_t)((v = pld_rlx(&sc->rec[g0 + i])) >> 32) != epoch && ++spins < kPropSplitMaxSpins)
+                __builtin_amdgcn_s_sleep(2);
+            lost |= (uint32_t)(v >> 32) != epoch;
             acc += (uint32_t)v;
         }
         const uint32_t wsum = lane_bcast(incl_scan(acc), 63);
@@ -572,31 +570,49 @@ __device__ void prop_split_chunk(const uint8_t* in, const uint8_t* dec, const co
     }
 }
 
+// workgroups take chunks by ticket (a chunk waits only on chunks of its column already running) until
+// none are left, then the small columns, sixteen per ticket, one wave each
 __global__ __launch_bounds__(64 * kPropCoopWaves) void prop_split_kernel(const uint8_t* __restrict__ in,
                                                                          const uint8_t* __restrict__ dec,
                                                                          const covt_stream_result* __restrict__ dres,
                                                                          const covt_prop_desc* __restrict__ descs,
                                                                          uint8_t* __restrict__ outb,
                                                                          covt_prop_result* __restrict__ pres,
-                                                                         PropSplitScratch* __restrict__ sc) {
+                                                                         PropSplitScratch* __restrict__ sc, uint32_t epoch) {
     __shared__ PropSmem smem;
+    __shared__ int32_t lpre[kPropCoopMaxColumns + 1];
     __shared__ int32_t tk;
     const int32_t ns = sc->n_split, total = sc->pre[ns];
+    const int32_t small_groups = (sc->n_small + kPropCoopWaves - 1) / kPropCoopWaves;
+    for (int32_t i = threadIdx.x; i <= ns; i += 64 * kPropCoopWaves) lpre[i] = sc->pre[i];
+    __syncthreads();
     for (;;) {
         if (threadIdx.x == 0) tk = (int32_t)atomicAdd(&sc->ticket, 1u);
         __syncthreads();
         const int32_t g = tk;
         __syncthreads();
-        if (g >= total) return;
-        int32_t lo = 0, hi = ns;  // pre[lo] <= g < pre[hi]
+        if (g >= total) {
+            if (g >= total + small_groups) return;
+            const int32_t si = (g - total) * kPropCoopWaves + (int32_t)(threadIdx.x >> 6);
+            if (si < sc->n_small) {  // (wave-uniform)
+                const int32_t c = uni(sc->small[si]);
+                const covt_prop_desc d = descs[c];
+                covt_prop_result r;
+                materialize<1>(in, dec, dres, d, outb, r, nullptr);
+                if (lane_id() == 0) pres[c] = r;
+            }
+            __syncthreads();
+            continue;
+        }
+        int32_t lo = 0, hi = ns;  // lpre[lo] <= g < lpre[hi]
         while (hi - lo > 1) {
             const int32_t mid = (lo + hi) >> 1;
-            if (sc->pre[mid] <= g) lo = mid;
+            if (lpre[mid] <= g) lo = mid;
             else hi = mid;
         }
         const int32_t c = sc->col[lo];
         const covt_prop_desc d = descs[c];
-        prop_split_chunk(in, dec, dres, d, outb, pres, sc, lo, g - sc->pre[lo], c, &smem);
+        prop_split_chunk(in, dec, dres, d, outb, pres, sc, lo, g - lpre[lo], c, &smem, epoch);
         __syncthreads();
     }
 }
@@ -604,16 +620,26 @@ __global__ __launch_bounds__(64 * kPropCoopWaves) void prop_split_kernel(const u
 }  // namespace covt
 
 namespace {
-// split scratch, one per (device, stream): launches on one stream are ordered, so they can share it
+// split scratch, one per (device, stream): launches on one stream are ordered, so they can share it; the
+// epoch tags each launch's look-back records
+struct PropSplitSlot {
+    void* p = nullptr;
+    uint32_t epoch = 0;
+};
 std::mutex g_psplit_mu;
-std::map<std::pair<int, hipStream_t>, void*> g_psplit_scratch;
-covt::PropSplitScratch* prop_split_scratch(hipStream_t s) {
+std::map<std::pair<int, hipStream_t>, PropSplitSlot> g_psplit_scratch;
+covt::PropSplitScratch* prop_split_scratch(hipStream_t s, uint32_t& epoch) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> g(g_psplit_mu);
-    void*& p = g_psplit_scratch[std::make_pair(dev, s)];
-    if (!p && hipMalloc(&p, sizeof(covt::PropSplitScratch)) != hipSuccess) p = nullptr;
-    return (covt::PropSplitScratch*)p;
+    PropSplitSlot& q = g_psplit_scratch[std::make_pair(dev, s)];
+    if (!q.p) {
+        if (hipMalloc(&q.p, sizeof(covt::PropSplitScratch)) != hipSuccess) return (covt::PropSplitScratch*)(q.p = nullptr);
+        if (hipMemset(q.p, 0, sizeof(covt::PropSplitScratch)) != hipSuccess) return nullptr;  // epoch 0: never used
+    }
+    if (++q.epoch == 0) q.epoch = 1;
+    epoch = q.epoch;
+    return (covt::PropSplitScratch*)q.p;
 }
 }  // namespace
 
@@ -627,24 +653,19 @@ extern "C" int covt_materialize_properties_device(const uint8_t* d_in, const uin
     const int64_t blocks = (n_columns + covt::kPropWaves - 1) / covt::kPropWaves;
     if (blocks > 0x7fffffff) return COVT_ERR_INVALID_ARG;
     hipStream_t s = (hipStream_t)hip_stream;
-    // small batches: columns of kPropSplitMinFeatures or more by several workgroups each (prop_split_kernel),
-    // past the split budget those of kPropCoopMinFeatures or more by one whole workgroup; launched first:
-    // they are the critical path
-    const bool coop = n_columns <= covt::kPropCoopMaxColumns;
-    const int32_t coop_min = coop ? covt::kPropCoopMinFeatures : 0x7fffffff;
-    const int32_t* split_flag = nullptr;
-    if (coop) {
-        covt::PropSplitScratch* sc = prop_split_scratch(s);
+    if (n_columns <= covt::kPropCoopMaxColumns) {
+        // small batches: columns of kPropSplitMinFeatures or more in chunks on many workgroups, the rest
+        // on single waves of the same kernel
+        uint32_t epoch = 0;
+        covt::PropSplitScratch* sc = prop_split_scratch(s, epoch);
         if (!sc) return COVT_ERR_DEVICE;
-        split_flag = sc->flag;
-        hipLaunchKernelGGL(covt::prop_split_prep, dim3(16), dim3(1024), 0, s, d_pdesc, n_columns,
+        hipLaunchKernelGGL(covt::prop_split_prep, dim3(1), dim3(1024), 0, s, d_pdesc, n_columns,
                            covt::kPropSplitMinFeatures, sc);
         hipLaunchKernelGGL(covt::prop_split_kernel, dim3(covt::kPropSplitGrid), dim3(64 * covt::kPropCoopWaves), 0, s,
-                           d_in, d_decoded, d_res, d_pdesc, d_props, d_pres, sc);
-        hipLaunchKernelGGL(covt::props_coop_kernel, dim3((unsigned)n_columns), dim3(64 * covt::kPropCoopWaves), 0, s,
-                           d_in, d_decoded, d_res, d_pdesc, n_columns, d_props, d_pres, coop_min, split_flag);
+                           d_in, d_decoded, d_res, d_pdesc, d_props, d_pres, sc, epoch);
+    } else {
+        hipLaunchKernelGGL(covt::props_kernel, dim3((unsigned)blocks), dim3(64 * covt::kPropWaves), 0, s, d_in,
+                           d_decoded, d_res, d_pdesc, n_columns, d_props, d_pres);
     }
-    hipLaunchKernelGGL(covt::props_kernel, dim3((unsigned)blocks), dim3(64 * covt::kPropWaves), 0, s, d_in, d_decoded,
-                       d_res, d_pdesc, n_columns, d_props, d_pres, coop_min, split_flag);
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
 }
