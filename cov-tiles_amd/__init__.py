@@ -190,7 +190,8 @@ EXPORTED_SYMBOLS = (
     "covt_plan_options_init", "covt_plan_create_opts", "covt_device_plan_create_opts",
     "covt_device_plan_num_descs", "covt_device_plan_geometry", "covt_device_plan_num_geometry_columns",
     "covt_device_plan_assembly_bytes", "covt_device_plan_geometry_descs_device", "covt_device_plan_geometry_copy",
-    "covt_device_plan_assemble",
+    "covt_device_plan_assemble", "covt_device_plan_num_property_columns", "covt_device_plan_property_bytes",
+    "covt_device_plan_property_descs_device", "covt_device_plan_property_copy", "covt_device_plan_materialize",
 )
 
 
@@ -303,6 +304,14 @@ def lib() -> C.CDLL:
     L.covt_device_plan_geometry_descs_device.restype = vp
     L.covt_device_plan_geometry_copy.argtypes = [vp, vp, vp]
     L.covt_device_plan_assemble.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.covt_device_plan_num_property_columns.argtypes = [vp]
+    L.covt_device_plan_num_property_columns.restype = C.c_int64
+    L.covt_device_plan_property_bytes.argtypes = [vp]
+    L.covt_device_plan_property_bytes.restype = C.c_int64
+    L.covt_device_plan_property_descs_device.argtypes = [vp]
+    L.covt_device_plan_property_descs_device.restype = vp
+    L.covt_device_plan_property_copy.argtypes = [vp, vp, vp]
+    L.covt_device_plan_materialize.argtypes = [vp, vp, vp, vp, vp, vp, vp]
     L.covt_version.restype = C.c_char_p
     L.covt_device_count.argtypes = [i32p]
     _lib = L
@@ -843,6 +852,8 @@ class DevicePlan:
         a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
         L.covt_device_plan_totals(h, C.byref(a), C.byref(b), C.byref(c))
         self.in_bytes, self.out_payload, self.vertices = a.value, b.value, c.value
+        self.num_property_columns = L.covt_device_plan_num_property_columns(h)
+        self.property_bytes = L.covt_device_plan_property_bytes(h)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -863,6 +874,32 @@ class DevicePlan:
         _raise(lib().covt_device_plan_copy(self._h, info.ctypes.data, descs.ctypes.data, _ptr(st, C.c_int32)),
                "covt_device_plan_copy")
         return info, descs, st[:self.n_tiles]
+
+    def property_copy(self):
+        """(property records in tile order, property descriptors in materialization order) as host arrays
+        (plans made with PLAN_PROPERTIES in the options' flags; Plan.props / Plan.pdescs of the host plan)."""
+        n = self.num_property_columns
+        pinfo = np.zeros(n, dtype=PROP_INFO_DTYPE)
+        pdesc = np.zeros(n, dtype=PROP_DESC_DTYPE)
+        _raise(lib().covt_device_plan_property_copy(self._h, pinfo.ctypes.data, pdesc.ctypes.data),
+               "covt_device_plan_property_copy")
+        return pinfo, pdesc
+
+    def alloc_properties(self):
+        """(property buffer, property results) on the device, sized for this plan's property columns."""
+        import torch
+
+        return (torch.zeros(max(self.property_bytes, 16), dtype=torch.uint8, device=self.device),
+                torch.zeros(max(self.num_property_columns, 1) * 2, dtype=torch.int32, device=self.device))
+
+    def materialize(self, d_out, d_res, d_props, d_pres, stream=None):
+        """Enqueue the property materialization over this plan's property descriptors (after decode())."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _raise(lib().covt_device_plan_materialize(self._h, self.d_in.data_ptr(), d_out.data_ptr(), d_res.data_ptr(),
+                                                  d_props.data_ptr(), d_pres.data_ptr(), s.cuda_stream),
+               "covt_device_plan_materialize")
 
     def alloc(self):
         """(output buffer, result buffer) on the device, sized for this plan."""
@@ -1098,7 +1135,7 @@ def version() -> str:
 # the files whose sha256 (in this order) the Makefile compiles into covt_version() as "src:<16 hex>"
 _BUILD_SOURCES = ("csrc/covt_decode.hip", "csrc/covt_assemble.hip", "csrc/covt_props.hip", "csrc/covt_plan_device.hip",
                   "csrc/covt_host.cpp", "../include/covt.h", "csrc/covt_internal.h", "csrc/covt_wave.h",
-                  "csrc/covt_walk.h")
+                  "csrc/covt_walk.h", "csrc/covt_props_plan.h")
 
 
 def source_build_id() -> str:

@@ -194,7 +194,11 @@ __device__ __forceinline__ void st_out16(int32_t* p, int4 v) {
 #if defined(COVT_ABL_NOSTORE)  // ablation build: wide stores land on the first KiB of their 64 KiB
     p = (int32_t*)(((uintptr_t)p & ~(uintptr_t)65535) | ((uintptr_t)p & 1023));
 #endif
+#if defined(COVT_ST16_CACHED)  // experiment build: 16-byte output stores through L2 like the narrow ones
+    *(i32x4*)p = w;
+#else
     __builtin_nontemporal_store(w, (i32x4*)p);
+#endif
 }
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v) {

@@ -22,39 +22,14 @@
 #include "covt.h"
 #include "covt_internal.h"
 #include "covt_walk.h"
+#include "covt_props_plan.h"
 
 namespace {
 
-// One property (sub)column found by a walker (CovtParser.decodePropertyColumn, CovtParser.java:276-354).
-// Streams by role 0 present, 1 data, 2 length, 3 dictionary; offsets tile-relative (-1: absent).
-struct PropRaw {
-    int32_t layer, column, type, ctype, nf, lang, name_len, lang_len;
-    int64_t name_off, lang_off;  // tile-relative UTF-8 names (-1: none)
-    int64_t s_off[4];
-    int32_t s_nv[4], s_bl[4], s_enc[4];
-};
-PropRaw prop_init(int32_t layer, int32_t column, int32_t nf) {
-    PropRaw p{};
-    p.layer = layer;
-    p.column = column;
-    p.nf = nf;
-    p.lang = -1;
-    p.name_off = p.lang_off = -1;
-    for (int r = 0; r < 4; ++r) p.s_off[r] = -1;
-    return p;
-}
-void prop_stream(PropRaw& p, int role, int64_t off, int32_t nv, int32_t bl, int32_t enc) {
-    p.s_off[role] = off;
-    p.s_nv[role] = nv;
-    p.s_bl[role] = bl;
-    p.s_enc[role] = enc;
-}
 bool name_is(const uint8_t* t, int64_t off, int64_t len, const char* s) {
     return (size_t)len == std::strlen(s) && std::memcmp(t + off, s, (size_t)len) == 0;
 }
-// Gen C ColumnDataType (evaluation/file/ColumnDataType.java) / Gen D (converter/ColumnDataType.java)
-int genc_prop_type(int dt) { return dt == 0 ? COVT_PROP_STRING : dt == 1 ? COVT_PROP_FLOAT : dt == 3 ? COVT_PROP_INT64 : dt == 5 ? COVT_PROP_BOOLEAN : -1; }
-int gend_prop_type(int dt) { return dt == 0 ? COVT_PROP_BOOLEAN : dt == 3 ? COVT_PROP_INT64 : dt == 5 ? COVT_PROP_FLOAT : dt == 7 ? COVT_PROP_STRING : -1; }
+// PropRaw, the property walkers' record, and the planning rule: covt_props_plan.h (shared with the device plan)
 
 // LEB128 (metadata of Gen C is written with EncodingUtils.encodeVarints, i.e. 64-bit varints)
 bool rd_uv(const uint8_t* t, size_t len, size_t& o, uint64_t& v) {
@@ -943,65 +918,13 @@ struct PlanPart {
     int64_t out_off = 0, in_bytes = 0, out_payload = 0, vertices = 0;
 };
 void plan_property(PlanPart* p, int32_t t, int64_t tile_off, const PropRaw& q, int id_mode, int64_t& out_off) {
-    covt_prop_info pi{};
-    pi.tile = t;
-    pi.layer = q.layer;
-    pi.column = q.column;
-    pi.type = q.type;
-    pi.column_type = q.ctype;
-    pi.n_features = q.nf;
-    pi.n_data = q.s_nv[1];
-    pi.n_dict = q.s_off[3] >= 0 ? std::max(q.s_nv[3], 0) : 0;
-    pi.lang = q.lang;
-    pi.name_len = q.name_len;
-    pi.lang_len = q.lang_len;
-    pi.dict_bytes = q.s_off[3] >= 0 ? std::max(q.s_bl[3], 0) : 0;
-    pi.name_off = q.name_off >= 0 ? tile_off + q.name_off : -1;
-    pi.lang_off = q.lang_off >= 0 ? tile_off + q.lang_off : -1;
-    for (int k = 0; k < 3; ++k) pi.stream[k] = -1;
-    uint16_t fl = 0;
-    const int32_t nf = std::max(q.nf, 0), nb = (int32_t)(((int64_t)nf + 7) / 8);
-    const bool early_unsup = q.type < 0 || q.s_off[1] < 0 || (q.type != COVT_PROP_BOOLEAN && q.s_off[0] < 0) ||
-                             q.nf < 0 || q.s_nv[1] < 0;
-    int data_op = COVT_OP_NONE, data_elem = 0;
-    int64_t data_n = 0;
-    bool late_unsup = false;
-    if (!early_unsup) {
-        switch (q.type) {
-        case COVT_PROP_BOOLEAN:
-            if (q.s_off[0] >= 0) fl |= COVT_PROP_DENSE_BOOL;
-            data_op = COVT_OP_BYTE_RLE_RAW;
-            data_elem = 1;
-            data_n = (q.s_off[0] >= 0) ? ((int64_t)q.s_nv[1] + 7) / 8 : nb;
-            break;
-        case COVT_PROP_INT64:
-            data_elem = 8;
-            data_n = q.s_nv[1];
-            if (q.s_enc[1] == ENC_RLE) data_op = COVT_OP_RLE_S64;
-            else if (q.s_enc[1] == 2) data_op = id_mode == COVT_ID_JAVA ? COVT_OP_VARINT_ZZ_I32_AS_I64 : COVT_OP_VARINT_ZZ_S64;
-            else if (q.s_enc[1] == ENC_VARINT_DELTA_ZZ)
-                data_op = id_mode == COVT_ID_JAVA ? COVT_OP_VARINT_ZZ_DELTA_I64 : COVT_OP_VARINT_ZZ_DELTA_S64;
-            else late_unsup = true;
-            break;
-        case COVT_PROP_FLOAT:  // no decode: the kernel reads the little-endian words from the input
-            if ((int64_t)q.s_nv[1] * 4 > q.s_bl[1]) fl |= COVT_PROP_DATA_SHORT;
-            break;
-        default:  // STRING
-            if ((q.ctype != 1 && q.ctype != 2) || q.s_off[2] < 0 || q.s_off[3] < 0 || q.s_enc[1] != ENC_RLE ||
-                q.s_nv[3] < 0) {
-                late_unsup = true;
-            } else {
-                data_op = COVT_OP_RLE_I32;  // (int) data[dataCounter++]
-                data_elem = 4;
-                data_n = q.s_nv[1];
-                if (q.lang <= 0) fl |= COVT_PROP_DICT_OWNER;
-            }
-            break;
-        }
-    }
-    if (early_unsup) fl |= COVT_PROP_UNSUPPORTED;
-    if (late_unsup) fl |= COVT_PROP_UNSUPPORTED_LATE;
-    auto add = [&](int role, int op, int64_t n, int elem) {
+    covt_prop_info pi = prop_info_of(q, t, tile_off);
+    PropStreams ps;
+    prop_streams(q, id_mode, ps);  // covt_props_plan.h: the same rule as the device plan
+    for (int k = 0; k < ps.n; ++k) {
+        const int role = ps.role[k];
+        const int64_t n = ps.count[k];
+        const int elem = ps.elem[k];
         covt_stream_info si{};
         si.tile = t;
         si.layer = q.layer;
@@ -1011,29 +934,20 @@ void plan_property(PlanPart* p, int32_t t, int64_t tile_off, const PropRaw& q, i
         si.column_type = q.ctype;
         si.num_values = q.s_nv[role];
         si.byte_length = q.s_bl[role];
-        si.op = op;
+        si.op = ps.op[k];
         si.elem_bytes = elem;
         si.in_off = tile_off + q.s_off[role];
         si.out_elems = n;
         si.out_off = out_off;
         out_off = align_out(out_off + n * elem);
-        p->in_bytes += q.s_bl[role];
         p->out_payload += n * elem;
         si.desc_index = (int32_t)n;  // temporarily: values to decode
         pi.stream[role] = (int32_t)p->info.size();
         p->info.push_back(si);
-    };
-    if (!early_unsup) {
-        if (q.s_off[0] >= 0) add(0, COVT_OP_BYTE_RLE_RAW, nb, 1);  // decodeByteRle(numBytes), :296
-        if (!late_unsup && data_op != COVT_OP_NONE) add(1, data_op, data_n, data_elem);
-        if (!late_unsup && q.type == COVT_PROP_STRING) add(2, COVT_OP_RLE_I32, q.s_nv[3], 4);  // lengths: n_dict
     }
-    if (!early_unsup && q.type == COVT_PROP_FLOAT) p->in_bytes += q.s_bl[1];  // read in place
-    if (!early_unsup && (fl & COVT_PROP_DICT_OWNER)) p->in_bytes += q.s_bl[3];
-    if (q.type == COVT_PROP_FLOAT && q.s_off[1] >= 0) pi.out_off[1] = tile_off + q.s_off[1];  // temporarily
-    if (q.type == COVT_PROP_STRING && q.s_off[3] >= 0) pi.out_off[3] = tile_off + q.s_off[3];  // temporarily
+    p->in_bytes += ps.in_bytes;
     p->pinfo.push_back(pi);
-    p->pflags.push_back(fl);
+    p->pflags.push_back(ps.flags);
 }
 
 // Output slices of the property columns and the launch-ordered descriptors (after the decode
@@ -1047,18 +961,17 @@ void plan_property_layout(covt_plan* p) {
         covt_prop_info& pi = p->pinfo[k];
         in_float[k] = pi.out_off[1];
         in_dict[k] = pi.out_off[3];
-        const int64_t n = pi.n_features > 0 ? pi.n_features : 0, nb = (n + 7) / 8;
-        const int64_t vbytes = pi.type == COVT_PROP_BOOLEAN ? nb : pi.type == COVT_PROP_INT64 ? 8 * n : 4 * n;
+        const bool own = (p->pflags[k] & COVT_PROP_DICT_OWNER) != 0;
+        int64_t sz[4];
+        prop_layout_sizes(pi, own, sz);  // covt_props_plan.h
         pi.out_off[0] = off;
-        off = align16(off + nb);
-        pi.out_off[1] = off;
-        off = align16(off + vbytes);
-        if (pi.type == COVT_PROP_STRING && (p->pflags[k] & COVT_PROP_DICT_OWNER)) {
+        pi.out_off[1] = off + sz[0];
+        off += sz[0] + sz[1];
+        if (pi.type == COVT_PROP_STRING && own) {
             owner = k;
             pi.out_off[2] = off;
-            off = align16(off + 4 * ((int64_t)pi.n_dict + 1));
-            pi.out_off[3] = off;
-            off = align16(off + pi.dict_bytes);
+            pi.out_off[3] = off + sz[2];
+            off += sz[2] + sz[3];
         } else if (pi.type == COVT_PROP_STRING && pi.lang > 0 && owner < k && p->pinfo[owner].tile == pi.tile &&
                    p->pinfo[owner].layer == pi.layer && p->pinfo[owner].column == pi.column) {
             pi.out_off[2] = p->pinfo[owner].out_off[2];
@@ -1068,9 +981,9 @@ void plan_property_layout(covt_plan* p) {
         }
     }
     p->prop_bytes = off;
-    std::vector<SortKey> korder(np);  // largest (features + dictionary entries) first, ties in tile order
+std::vector<SortKey> korder(np);  // largest (features + dictionary entries) first, ties in tile order
     for (size_t k = 0; k < np; ++k)
-        korder[k] = SortKey{(1ull << 40) - (uint64_t)((int64_t)p->pinfo[k].n_features + p->pinfo[k].n_dict), (uint32_t)k};
+        korder[k] = SortKey{prop_order_key(p->pinfo[k]), (uint32_t)k};
     radix_sort(korder);
     std::vector<size_t> order(np);
     for (size_t k = 0; k < np; ++k) order[k] = korder[k].i;

@@ -28,6 +28,7 @@
 #include "covt.h"
 #include "covt_internal.h"
 #include "covt_walk.h"
+#include "covt_props_plan.h"
 
 struct covt_device_plan {
     int dev = 0;
@@ -42,6 +43,10 @@ struct covt_device_plan {
     int64_t n_geo = 0, asm_bytes = 0;
     covt_geom_info* d_ginfo = nullptr;
     covt_geom_desc* d_gdesc = nullptr;
+    void* prop_arena = nullptr;    // property columns (COVT_PLAN_PROPERTIES): records, infos, descriptors
+    int64_t n_props = 0, prop_bytes = 0;
+    covt_prop_info* d_pinfo = nullptr;
+    covt_prop_desc* d_pdesc = nullptr;
     int32_t* d_status = nullptr;
     covt_stream_info* d_info = nullptr;
     covt_stream_desc* d_desc = nullptr;
@@ -836,7 +841,7 @@ __global__ void walk_count(const uint8_t* __restrict__ bytes, uint64_t n_bytes, 
 // its largest stream split cost (covt_plan_create_ex step 3: nothing splits unless that passes the threshold)
 __global__ void __launch_bounds__(1024) plan_head(const int64_t* __restrict__ cb, const int64_t* __restrict__ obb,
                                                   const int64_t* __restrict__ tcost, int32_t n_tiles,
-                                                  int64_t* __restrict__ head) {
+                                                  int64_t* __restrict__ head, const unsigned long long* __restrict__ pacc) {
     __shared__ int64_t part[16][2];
     int64_t sum = 0, mx = 0;
     for (int32_t t = threadIdx.x; t < n_tiles; t += 1024) {
@@ -855,6 +860,10 @@ __global__ void __launch_bounds__(1024) plan_head(const int64_t* __restrict__ cb
     if (threadIdx.x == 0) {
         int64_t a = 0, b = 0;
         for (int i = 0; i < 16; ++i) a += part[i][0], b = part[i][1] > b ? part[i][1] : b;
+        if (pacc) {  // the property streams' split costs (prop_sizes)
+            a += (int64_t)pacc[2 + 1];
+            b = (int64_t)pacc[2 + 2] > b ? (int64_t)pacc[2 + 2] : b;
+        }
         head[0] = cb[n_tiles];
         head[1] = obb[n_tiles];
         head[2] = a;
@@ -1006,7 +1015,8 @@ __global__ void emit_slots(const uint64_t* __restrict__ offs, int32_t n_tiles, i
 // The per-tile sums (input bytes, payload, vertices, lane streams; zero for failed tiles) -> totals: one
 // workgroup (same-address atomics from every tile serialise in L2: ~0.5 ms for 10k tiles)
 __global__ void __launch_bounds__(1024) reduce_tiles(const long long* __restrict__ tsum, int32_t n_tiles,
-                                                     unsigned long long* __restrict__ totals) {
+                                                     unsigned long long* __restrict__ totals,
+                                                     const unsigned long long* __restrict__ pacc) {
     __shared__ long long part[16][4];
     long long a[4] = {0, 0, 0, 0};
     for (int32_t t = threadIdx.x; t < n_tiles; t += 1024) {
@@ -1024,6 +1034,10 @@ __global__ void __launch_bounds__(1024) reduce_tiles(const long long* __restrict
     if (threadIdx.x < 4) {
         long long x = 0;
         for (int i = 0; i < 16; ++i) x += part[i][threadIdx.x];
+        if (pacc) {  // + the property streams' (prop_sizes: bytes, payload, lane streams; no vertices)
+            const int k = threadIdx.x;
+            x += (long long)(k == 0 ? pacc[0] : k == 1 ? pacc[1] : k == 3 ? pacc[2] : 0ull);
+        }
         totals[T_IN + threadIdx.x] = (unsigned long long)x;  // T_IN, T_PAYLOAD, T_VERTS, T_LANE
     }
 }
@@ -1440,6 +1454,485 @@ __global__ void fpf_states_walk(const uint8_t* __restrict__ bytes, const covt_st
     }
 }
 
+// ---- Property columns (COVT_PLAN_PROPERTIES; covt_host.cpp walk_genc / walk_gend's property records,
+// plan_property and plan_property_layout).  The host plan puts a tile's property streams after its Id /
+// Geometry streams and gives them output slices in that order; here:
+//   prop_walk<false>  one wave per tile: the container walk again, counting property (sub)columns
+//   scan              -> each tile's first record; one D2H (the record count sizes the arrays)
+//   prop_walk<true>   the same walk writing the records (PropRaw, tile-relative offsets)
+//   prop_sizes        a thread per record: its decode streams (prop_streams, the host's rule), their count
+//                     and aligned output bytes; the records' byte / payload / lane / cost totals
+//   scans + tile_totals  each tile's streams and output bytes = Id / Geometry + property
+// and once the stream arrays exist, prop_fill writes the records' stream entries and covt_prop_info,
+// prop_layout / prop_layout_fill the property output slices, a stable radix sort the largest-first
+// materialization order and prop_desc_fill the covt_prop_desc table.
+struct PropSm {  // a property column's stream, as the Gen C walk reads it
+    int32_t noff, nlen, nv, bl, enc;
+    int32_t off;  // layer-data-relative
+};
+constexpr int kPropMaxStreams = 256;  // numStreams bound of the walk (walk_genc: > 256 is BAD_HEADER)
+constexpr size_t kPropWalkLds = 512 + kPropMaxStreams * sizeof(PropSm);  // Rd window + stream table
+
+// bytes [a, a + n) == bytes [b, b + n) of the tile (names; uniform)
+__device__ __forceinline__ bool names_equal(Rd<true>& r, int32_t a, int32_t b, int32_t n) {
+    for (int32_t i = 0; i < n; i += 8) {
+        const int32_t k = n - i < 8 ? n - i : 8;
+        const uint64_t m = k >= 8 ? ~0ull : ((1ull << (8 * k)) - 1);
+        if ((r.peek8(a + i) & m) != (r.peek8(b + i) & m)) return false;
+    }
+    return true;
+}
+
+// Gen C property records (walk_genc's props branch): a column's streams in metadata order, roles by
+// name; LOCALIZED_DICTIONARY strings as one sub-column per present_<lang> stream
+template <class PE>
+__device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
+    const int32_t len = (int32_t)r.len;
+    int32_t o = 0;
+    uint64_t version, nlayers;
+    if (!r.uv(o, version) || !r.uv(o, nlayers)) return COVT_ERR_TRUNCATED;
+    if (version != 1) return COVT_ERR_BAD_HEADER;
+    for (uint64_t L = 0; L < nlayers; ++L) {
+        uint64_t nlen, extent, nfeat, ncols;
+        if (!r.uv(o, nlen) || nlen > (uint64_t)(len - o)) return COVT_ERR_TRUNCATED;
+        o += (int32_t)nlen;
+        if (!r.uv(o, extent) || !r.uv(o, nfeat) || !r.uv(o, ncols)) return COVT_ERR_TRUNCATED;
+        if (ncols > 4096) return COVT_ERR_BAD_HEADER;
+        int64_t d = 0;
+        pe.layer_begin();
+        for (uint32_t c = 0; c < (uint32_t)ncols; ++c) {
+            uint64_t cn, ns, sn, nv, bl;
+            if (!r.uv(o, cn) || cn > (uint64_t)(len - o) || (uint64_t)(len - o) - cn < 2) return COVT_ERR_TRUNCATED;
+            const int32_t name = o;
+            o += (int32_t)cn;
+            const int dtype = r.at(o), ctype = r.at(o + 1);
+            o += 2;
+            if (!r.uv(o, ns)) return COVT_ERR_TRUNCATED;
+            if (ns > 256) return COVT_ERR_BAD_HEADER;
+            const int kind = COVT_IS(name, cn, "id") ? 0 : (COVT_IS(name, cn, "geometry") || dtype == 6) ? 1 : 2;
+            for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
+                if (!r.uv(o, sn) || sn > (uint64_t)(len - o)) return COVT_ERR_TRUNCATED;
+                const int32_t sname = o;
+                o += (int32_t)sn;
+                int enc;
+                if (!r.rec3(o, nv, bl, enc)) {
+                    if (!r.uv(o, nv) || !r.uv(o, bl) || o >= len) return COVT_ERR_TRUNCATED;
+                    enc = r.at(o++);
+                }
+                if (nv > 0x7fffffff || bl > 0x7fffffff) return COVT_ERR_BAD_HEADER;
+                if (kind == 2 && threadIdx.x == 0)
+                    tab[q] = PropSm{sname, (int32_t)sn, (int32_t)nv, (int32_t)bl, enc, (int32_t)d};
+                d += (int64_t)bl;
+            }
+            if (kind != 2) continue;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            PropRaw p = prop_init((int32_t)L, (int32_t)c, (int32_t)nfeat);
+            p.name_off = name;
+            p.name_len = (int32_t)cn;
+            p.type = genc_prop_type(dtype);
+            p.ctype = ctype;
+            if (p.type == COVT_PROP_STRING && ctype == 2) {
+                int ls = -1, ds = -1;
+                for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
+                    const PropSm sm = tab[q];
+                    if (COVT_IS(sm.noff, sm.nlen, "length")) ls = (int)q;
+                    else if (COVT_IS(sm.noff, sm.nlen, "dictionary")) ds = (int)q;
+                }
+                int32_t lang = 0;
+                for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
+                    const PropSm sm = tab[q];
+                    if (sm.nlen <= 8 || (r.peek8(sm.noff) != pk("present_", 0, 8))) continue;
+                    const int32_t ll = sm.nlen - 8;
+                    int dd = -1;
+                    for (uint32_t k = 0; k < (uint32_t)ns; ++k)
+                        if (tab[k].nlen == ll && names_equal(r, tab[k].noff, sm.noff + 8, ll)) dd = (int)k;
+                    PropRaw x = p;
+                    x.lang = lang++;
+                    x.lang_off = sm.noff + 8;
+                    x.lang_len = ll;
+                    prop_stream(x, 0, sm.off, sm.nv, sm.bl, sm.enc);
+                    if (dd >= 0) prop_stream(x, 1, tab[dd].off, tab[dd].nv, tab[dd].bl, tab[dd].enc);
+                    if (ls >= 0) prop_stream(x, 2, tab[ls].off, tab[ls].nv, tab[ls].bl, tab[ls].enc);
+                    if (ds >= 0) prop_stream(x, 3, tab[ds].off, tab[ds].nv, tab[ds].bl, tab[ds].enc);
+                    pe(x);
+                }
+            } else {
+                for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
+                    const PropSm sm = tab[q];
+                    if (COVT_IS(sm.noff, sm.nlen, "present")) prop_stream(p, 0, sm.off, sm.nv, sm.bl, sm.enc);
+                    if (COVT_IS(sm.noff, sm.nlen, "data")) prop_stream(p, 1, sm.off, sm.nv, sm.bl, sm.enc);
+                    if (COVT_IS(sm.noff, sm.nlen, "length")) prop_stream(p, 2, sm.off, sm.nv, sm.bl, sm.enc);
+                    if (COVT_IS(sm.noff, sm.nlen, "dictionary")) prop_stream(p, 3, sm.off, sm.nv, sm.bl, sm.enc);
+                }
+                pe(p);
+            }
+            __builtin_amdgcn_wave_barrier();  // the table is rewritten by the next column
+        }
+        if (d > (int64_t)(len - o)) return COVT_ERR_TRUNCATED;
+        pe.layer_end(o);  // the layer's data starts where its metadata ends
+        o += (int32_t)d;
+    }
+    return o == len ? COVT_OK : COVT_ERR_BAD_HEADER;
+}
+
+// Gen D property records (walk_gend's props branch): the implicit present stream, then data / length /
+// dictionary in TreeMap<StreamType> order (the last metadata entry of a type)
+template <class PE>
+__device__ int prop_walk_gend(Rd<true>& r, PE& pe) {
+    const int32_t len = (int32_t)r.len;
+    int32_t o = 0;
+    int32_t layer = 0;
+    while (o < len) {
+        const bool optimized = r.at(o++) & 1;
+        int32_t v, extent, nfeat, ncols;
+        if (!r.j4(o, v)) return COVT_ERR_TRUNCATED;
+        if (!optimized) {
+            if (v < 0 || v > len - o) return COVT_ERR_TRUNCATED;
+            o += v;
+        }
+        if (!r.j4(o, extent) || !r.j4(o, nfeat) || !r.j4(o, ncols)) return COVT_ERR_TRUNCATED;
+        if (ncols < 0 || ncols > 4096) return COVT_ERR_BAD_HEADER;
+        const int32_t meta = o;
+        for (int32_t ci = 0; ci < ncols; ++ci) {  // skip the metadata (checked by the Id / Geometry walk)
+            int32_t x;
+            if (optimized || ci == 0) {
+                if (!r.j4(o, x)) return COVT_ERR_TRUNCATED;
+            } else {
+                if (!r.j4(o, x) || x < 0 || x > len - o) return COVT_ERR_TRUNCATED;
+                o += x;
+            }
+            if (o >= len) return COVT_ERR_TRUNCATED;
+            const int desc = r.at(o++), dtype = (desc >> 3) & 0xF, ctype = desc & 0x7;
+            if (ctype > 4) return COVT_ERR_BAD_HEADER;
+            for (;;) {
+                if (o >= len) return COVT_ERR_TRUNCATED;
+                const int sd = r.at(o++), type = sd >> 4, enc = sd & 0xF;
+                if (type > ST_M || enc > 9) return COVT_ERR_BAD_HEADER;
+                int32_t nv, bl;
+                if (!r.j4(o, nv) || !r.j4(o, bl)) return COVT_ERR_TRUNCATED;
+                if ((dtype == 8 && type == ST_VERTEX_BUFFER) || (type == ST_DATA && ctype == CT_PLAIN) ||
+                    type == ST_DICTIONARY)
+                    break;
+            }
+        }
+        int32_t m = meta;
+        int64_t d = o;
+        pe.layer_begin();
+        for (int32_t ci = 0; ci < ncols; ++ci) {
+            int32_t x, kind;
+            int32_t name_off = -1, name_len = 0;
+            if (optimized || ci == 0) {
+                r.j4(m, x);
+                kind = x == 0 ? 0 : (x == 1 ? 1 : 2);
+            } else {
+                r.j4(m, x);
+                kind = COVT_IS(m, x, "id") ? 0 : COVT_IS(m, x, "geometry") ? 1 : 2;
+                name_off = m;
+                name_len = x;
+                m += x;
+            }
+            const int desc = r.at(m++), dtype = (desc >> 3) & 0xF, ctype = desc & 0x7;
+            const int32_t s0 = m;
+            uint32_t have = 0;
+            for (;;) {
+                const int sd = r.at(m++), type = sd >> 4;
+                int32_t nv, bl;
+                r.j4(m, nv);
+                r.j4(m, bl);
+                have |= 1u << type;
+                if ((dtype == 8 && type == ST_VERTEX_BUFFER) || (type == ST_DATA && ctype == CT_PLAIN) ||
+                    type == ST_DICTIONARY)
+                    break;
+            }
+            PropRaw p = prop_init(layer, ci, nfeat);
+            if (kind == 2 && dtype != 0) {  // the implicit present stream
+                const int32_t pl = r.byte_rle_length((int32_t)d, nfeat < 0 ? 0 : (int32_t)(((int64_t)nfeat + 7) / 8));
+                if (pl < 0) return COVT_ERR_TRUNCATED;
+                prop_stream(p, 0, d, nfeat, pl, 7);
+                d += pl;
+            }
+            for (int type = 0; type < 12; ++type) {
+                if (!(have >> type & 1) || (kind == 2 && type == ST_PRESENT)) continue;
+                int enc = 0;
+                int32_t nv = 0, bl = 0;
+                for (int32_t q = s0; q < m;) {  // the last entry of this type
+                    const int sd = r.at(q++);
+                    int32_t a, b;
+                    r.j4(q, a);
+                    r.j4(q, b);
+                    if ((sd >> 4) == type) enc = sd & 0xF, nv = a, bl = b;
+                }
+                if (bl < 0) return COVT_ERR_BAD_HEADER;
+                if (type > ST_PRESENT && type <= ST_DICTIONARY) prop_stream(p, type, d, nv, bl, enc);
+                d += bl;
+            }
+            if (d > len) return COVT_ERR_TRUNCATED;
+            if (kind == 2) {
+                p.name_off = name_off;
+                p.name_len = name_len;
+                p.type = gend_prop_type(dtype);
+                p.ctype = ctype;
+                pe(p);
+            }
+        }
+        pe.layer_end(0);
+        o = (int32_t)d;
+        ++layer;
+    }
+    return COVT_OK;
+}
+
+struct PropCountEmit {
+    int64_t n = 0;
+    __device__ void operator()(const PropRaw&) { ++n; }
+    __device__ void layer_begin() {}
+    __device__ void layer_end(int64_t) {}
+};
+struct PropRecEmit {
+    PropRaw* recs;    // this tile's first record
+    int32_t* rtile;
+    int32_t t;
+    int64_t n = 0, k0 = 0;
+    __device__ void operator()(const PropRaw& q) {
+        if (threadIdx.x == 0) {
+            recs[n] = q;
+            rtile[n] = t;
+        }
+        ++n;
+    }
+    __device__ void layer_begin() { k0 = n; }
+    __device__ void layer_end(int64_t data_start) {  // Gen C: data offsets relative to the layer's data start
+        if (!data_start) return;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        for (int64_t j = k0 + threadIdx.x; j < n; j += 64)
+            for (int q = 0; q < 4; ++q)
+                if (recs[j].s_off[q] >= 0) recs[j].s_off[q] += data_start;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+};
+
+// one wave per tile (tiles the Id / Geometry walk failed contribute nothing); EMIT: write the records
+template <bool EMIT>
+__global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
+                          const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format,
+                          const int32_t* __restrict__ status, int64_t* __restrict__ pcnt,
+                          const int64_t* __restrict__ pcb, PropRaw* __restrict__ recs, int32_t* __restrict__ rtile) {
+    const int32_t t = (int32_t)blockIdx.x;
+    if (t > n_tiles) return;
+    if (t == n_tiles || status[t]) {  // (t == n_tiles: the prefix sum's total slot)
+        if (!EMIT && threadIdx.x == 0) pcnt[t] = 0;
+        return;
+    }
+    Rd<true> r;
+    r.t = bytes + offs[t];
+    r.len = (int64_t)sizes[t];
+    r.wo = -(int64_t)0x40000000;
+    PropSm* tab = (PropSm*)((uint8_t*)covt_walk_win + 512);
+    if (EMIT) {
+        PropRecEmit e{recs + pcb[t], rtile + pcb[t], t};
+        (void)(format == COVT_FORMAT_GENC ? prop_walk_genc(r, e, tab) : prop_walk_gend(r, e));
+    } else {
+        PropCountEmit e;
+        const int st = format == COVT_FORMAT_GENC ? prop_walk_genc(r, e, tab) : prop_walk_gend(r, e);
+        if (threadIdx.x == 0) pcnt[t] = st ? 0 : e.n;  // (the Id / Geometry walk succeeded: so does this one)
+    }
+}
+
+enum { PA_IN = 0, PA_PAYLOAD = 1, PA_LANE = 2, PA_COST = 3, PA_CMAX = 4, PA_N = 8 };
+// a thread per record: its decode streams (prop_streams), their count and aligned output bytes, and the
+// records' totals (stream / in-place bytes, payload, lane-family streams, split cost and its maximum)
+__global__ void __launch_bounds__(256) prop_sizes(const PropRaw* __restrict__ recs, int64_t n_rec, int32_t id_mode,
+                                                  int32_t lane_max, int64_t* __restrict__ rs_cnt,
+                                                  int64_t* __restrict__ rs_ob, unsigned long long* __restrict__ acc) {
+    __shared__ unsigned long long part[4][5];
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    unsigned long long a[5] = {0, 0, 0, 0, 0};
+    if (r < n_rec) {
+        const PropRaw q = recs[r];
+        PropStreams ps;
+        prop_streams(q, id_mode, ps);
+        int64_t ob = 0;
+        for (int k = 0; k < ps.n; ++k) {
+            const int64_t bytes = ps.count[k] * ps.elem[k];
+            ob = align_out(ob + bytes);
+            a[PA_PAYLOAD] += (unsigned long long)bytes;
+            a[PA_LANE] += lane_stream(ps.op[k], (int32_t)ps.count[k], q.s_bl[ps.role[k]], lane_max) ? 1ull : 0ull;
+            const unsigned long long c = (unsigned long long)((int64_t)q.s_bl[ps.role[k]] + bytes / 4);
+            a[PA_COST] += c;
+            a[PA_CMAX] = c > a[PA_CMAX] ? c : a[PA_CMAX];
+        }
+        a[PA_IN] = (unsigned long long)ps.in_bytes;
+        rs_cnt[r] = ps.n;
+        rs_ob[r] = ob;
+    } else if (r == n_rec) {
+        rs_cnt[r] = 0;
+        rs_ob[r] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const unsigned long long x = __shfl_xor(a[k], d, 64);
+            a[k] = k == PA_CMAX ? (x > a[k] ? x : a[k]) : a[k] + x;
+        }
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 5; ++k) part[threadIdx.x >> 6][k] = a[k];
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        unsigned long long x = 0;
+        for (int w = 0; w < 4; ++w) {
+            const unsigned long long y = part[w][threadIdx.x];
+            x = threadIdx.x == PA_CMAX ? (y > x ? y : x) : x + y;
+        }
+        if (threadIdx.x == PA_CMAX) atomicMax(&acc[PA_CMAX], x);
+        else if (x) atomicAdd(&acc[threadIdx.x], x);
+    }
+}
+
+// each tile's streams and output bytes: its Id / Geometry ones + its records' (slot n_tiles: 0)
+__global__ void tile_totals(const int64_t* __restrict__ cnt, const int64_t* __restrict__ ob, const int64_t* __restrict__ pcb,
+                            const int64_t* __restrict__ rsb, const int64_t* __restrict__ rob, int32_t n_tiles,
+                            int64_t* __restrict__ tc, int64_t* __restrict__ to) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > n_tiles) return;
+    if (t == n_tiles) {
+        tc[t] = to[t] = 0;
+        return;
+    }
+    const int64_t r0 = pcb[t], r1 = pcb[t + 1];
+    tc[t] = cnt[t] + (rsb[r1] - rsb[r0]);
+    to[t] = ob[t] + (rob[r1] - rob[r0]);
+}
+
+// a thread per record: its stream entries (after the tile's Id / Geometry streams, output slices after
+// theirs, as plan_property appends them) and its covt_prop_info / flags
+__global__ void prop_fill(const PropRaw* __restrict__ recs, const int32_t* __restrict__ rtile, int64_t n_rec,
+                          int32_t id_mode, const uint64_t* __restrict__ offs, const int64_t* __restrict__ cnt,
+                          const int64_t* __restrict__ ob, const int64_t* __restrict__ cb, const int64_t* __restrict__ obb,
+                          const int64_t* __restrict__ pcb, const int64_t* __restrict__ rsb, const int64_t* __restrict__ rob,
+                          covt_stream_info* __restrict__ info, int32_t* __restrict__ nvals, covt_prop_info* __restrict__ pinfo,
+                          uint16_t* __restrict__ pflags, int64_t* __restrict__ pin) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rec) return;
+    const int32_t t = rtile[r];
+    const PropRaw q = recs[r];
+    PropStreams ps;
+    prop_streams(q, id_mode, ps);
+    const int64_t r0 = pcb[t];
+    int64_t si_k = cb[t] + cnt[t] + (rsb[r] - rsb[r0]);
+    int64_t out = obb[t] + ob[t] + (rob[r] - rob[r0]);
+    const int64_t tile_off = (int64_t)offs[t];
+    covt_prop_info pi = prop_info_of(q, t, tile_off);
+    for (int k = 0; k < ps.n; ++k, ++si_k) {
+        const int role = ps.role[k];
+        covt_stream_info si;
+        si.tile = t;
+        si.layer = q.layer;
+        si.column_kind = 2;
+        si.stream_type = role;
+        si.encoding = q.s_enc[role];
+        si.column_type = q.ctype;
+        si.num_values = q.s_nv[role];
+        si.byte_length = q.s_bl[role];
+        si.num_bits = 0;
+        si.op = ps.op[k];
+        si.elem_bytes = ps.elem[k];
+        si.desc_index = -1;
+        si.in_off = tile_off + q.s_off[role];
+        si.out_elems = ps.count[k];
+        si.out_off = out;
+        out = align_out(out + ps.count[k] * ps.elem[k]);
+        info[si_k] = si;
+        nvals[si_k] = (int32_t)ps.count[k];
+        pi.stream[role] = (int32_t)si_k;
+    }
+    pin[2 * r] = pi.out_off[1];  // the FLOAT data / STRING dictionary input offsets (plan_property_layout's
+    pin[2 * r + 1] = pi.out_off[3];  // in_float / in_dict)
+    pinfo[r] = pi;
+    pflags[r] = ps.flags;
+}
+
+// property output layout (plan_property_layout): bytes per record, then their offsets
+__global__ void prop_layout(const covt_prop_info* __restrict__ pinfo, const uint16_t* __restrict__ pflags, int64_t n_rec,
+                            int64_t* __restrict__ psz) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r > n_rec) return;
+    if (r == n_rec) {
+        psz[r] = 0;
+        return;
+    }
+    const covt_prop_info pi = pinfo[r];
+    const bool own = (pflags[r] & COVT_PROP_DICT_OWNER) != 0;
+    int64_t sz[4];
+    prop_layout_sizes(pi, own, sz);
+    psz[r] = sz[0] + sz[1] + (pi.type == COVT_PROP_STRING && own ? sz[2] + sz[3] : 0);
+}
+__global__ void prop_layout_fill(covt_prop_info* __restrict__ pinfo, const uint16_t* __restrict__ pflags, int64_t n_rec,
+                                 const int64_t* __restrict__ poff) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rec) return;
+    covt_prop_info& pi = pinfo[r];
+    const bool own = (pflags[r] & COVT_PROP_DICT_OWNER) != 0;
+    int64_t sz[4];
+    prop_layout_sizes(pi, own, sz);
+    const int64_t off = poff[r];
+    pi.out_off[0] = off;
+    pi.out_off[1] = off + sz[0];
+    if (pi.type == COVT_PROP_STRING && own) {
+        pi.out_off[2] = off + sz[0] + sz[1];
+        pi.out_off[3] = off + sz[0] + sz[1] + sz[2];
+        return;
+    }
+    pi.out_off[2] = pi.out_off[3] = -1;
+    if (pi.type != COVT_PROP_STRING || pi.lang <= 0 || r - pi.lang < 0) return;
+    // a localized sub-column shares its column's dictionary: the owner is language 0, lang rows back
+    const int64_t w = r - pi.lang;
+    const covt_prop_info& po = pinfo[w];
+    if (!(pflags[w] & COVT_PROP_DICT_OWNER) || po.tile != pi.tile || po.layer != pi.layer || po.column != pi.column)
+        return;
+    int64_t so[4];
+    prop_layout_sizes(po, true, so);
+    pi.out_off[2] = poff[w] + so[0] + so[1];
+    pi.out_off[3] = poff[w] + so[0] + so[1] + so[2];
+}
+__global__ void prop_order_keys(const covt_prop_info* __restrict__ pinfo, int64_t n_rec, uint64_t* __restrict__ keys,
+                                uint32_t* __restrict__ vals) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rec) return;
+    keys[r] = prop_order_key(pinfo[r]);
+    vals[r] = (uint32_t)r;
+}
+__global__ void prop_desc_fill(covt_prop_info* __restrict__ pinfo, const uint16_t* __restrict__ pflags,
+                               const int64_t* __restrict__ pin, const uint32_t* __restrict__ order, int64_t n_rec,
+                               const covt_stream_info* __restrict__ info, covt_prop_desc* __restrict__ pdesc) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_rec) return;
+    const uint32_t r = order[k];
+    covt_prop_info& pi = pinfo[r];
+    auto s_out = [&](int role) -> int64_t { return pi.stream[role] >= 0 ? info[pi.stream[role]].out_off : -1; };
+    covt_prop_desc d;
+    d.present_off = s_out(0);
+    d.data_off = pi.type == COVT_PROP_FLOAT ? pin[2 * r] : s_out(1);
+    d.length_off = s_out(2);
+    d.dict_in_off = pi.type == COVT_PROP_STRING ? pin[2 * r + 1] : -1;
+    for (int m = 0; m < 4; ++m) d.out_off[m] = pi.out_off[m];
+    for (int m = 0; m < 3; ++m) d.res[m] = pi.stream[m] >= 0 ? info[pi.stream[m]].desc_index : -1;
+    d.n_features = pi.n_features;
+    d.n_data = pi.n_data;
+    d.n_dict = pi.n_dict;
+    d.dict_bytes = pi.dict_bytes;
+    d.type = (int16_t)pi.type;
+    d.flags = (int16_t)pflags[r];
+    pi.desc_index = (int32_t)k;
+    pdesc[k] = d;
+}
+
 // ---- Geometry columns (covt_device_plan_geometry; covt_host.cpp plan_geometry): a column is a run of
 // adjacent geometry streams of one (tile, layer); its record holds the source streams, the assembly
 // capacities and its six 16-byte aligned output slices; descriptors go largest (coordinates +
@@ -1543,7 +2036,8 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
                                  const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                                  const covt_plan_options* opts, void* hip_stream, covt_device_plan** out) {
     covt_plan_options o;
-    if (!covt_resolve_options(opts, o) || o.flags) return COVT_ERR_INVALID_ARG;
+    if (!covt_resolve_options(opts, o) || (o.flags & ~COVT_PLAN_PROPERTIES)) return COVT_ERR_INVALID_ARG;
+    const bool props = (o.flags & COVT_PLAN_PROPERTIES) != 0;
     if (!out || n_tiles < 0 || (n_tiles && (!d_bytes || !d_tile_offsets || !d_tile_sizes))) return COVT_ERR_INVALID_ARG;
     if (format != COVT_FORMAT_GENC && format != COVT_FORMAT_GEND) return COVT_ERR_INVALID_ARG;
     if (id_mode != COVT_ID_FORMAT && id_mode != COVT_ID_JAVA) return COVT_ERR_INVALID_ARG;
@@ -1567,10 +2061,13 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     // scan scratch | slots
     size_t scan_tmp = 0;
     DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)nt1, s));
+    // [+ properties: per-tile record counts | their prefix | streams and output bytes per tile | totals]
     const size_t o_cnt = up256(nt1 * 4), o_ob = o_cnt + up256(nt1 * 8), o_cb = o_ob + up256(nt1 * 8),
                  o_obb = o_cb + up256(nt1 * 8), o_tot = o_obb + up256(nt1 * 8), o_head = o_tot + up256(T_N * 8),
                  o_ts = o_head + 256, o_tc = o_ts + up256(nt1 * 32), o_tmp = o_tc + up256(nt1 * 16),
-                 o_slots = o_tmp + up256(scan_tmp);
+                 o_pc = o_tmp + up256(scan_tmp), o_pcb = o_pc + (props ? up256(nt1 * 8) : 0),
+                 o_ttc = o_pcb + (props ? up256(nt1 * 8) : 0), o_tto = o_ttc + (props ? up256(nt1 * 8) : 0),
+                 o_pacc = o_tto + (props ? up256(nt1 * 8) : 0), o_slots = o_pacc + (props ? 256 : 0);
     // device_walk 0: a wave per tile with per-tile slots; 1: the same walk twice; k >= 2: k lanes per workgroup
     const int wl = o.device_walk >= 2 ? o.device_walk : 0;
     const bool use_slots = o.device_walk == 0;
@@ -1595,9 +2092,85 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
             d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cnt, ob, nullptr,
             fpf_w, tcost);
     DCHK(hipGetLastError());
-    DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, cnt, cb, (int)nt1, s));
-    DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, ob, obb, (int)nt1, s));
-    plan_head<<<1, 1024, 0, s>>>(cb, obb, tcost, n_tiles, head);
+    // property columns: their records (a count walk, one D2H for the record count, the emitting walk), each
+    // record's streams and output bytes, and each tile's totals = Id / Geometry + property
+    int64_t *pcnt = nullptr, *pcb = nullptr, *rs_cnt = nullptr, *rs_ob = nullptr, *rsb = nullptr, *rob = nullptr;
+    unsigned long long* pacc = nullptr;
+    PropRaw* recs = nullptr;
+    int32_t* rtile = nullptr;
+    int64_t n_rec = 0;
+    size_t pscan_tmp = 0, psort_tmp = 0;
+    size_t po_rt = 0, po_rc = 0, po_ro = 0, po_rsb = 0, po_rob = 0, po_pi = 0, po_pf = 0, po_pin = 0, po_psz = 0,
+           po_poff = 0, po_k0 = 0, po_k1 = 0, po_v0 = 0, po_v1 = 0, po_pd = 0, po_st = 0, po_sc = 0, prop_total = 0;
+    const int64_t* scan_cnt = cnt;
+    const int64_t* scan_ob = ob;
+    if (props) {
+        pcnt = (int64_t*)(ta + o_pc);
+        pcb = (int64_t*)(ta + o_pcb);
+        pacc = (unsigned long long*)(ta + o_pacc);
+        DCHK(hipMemsetAsync(pacc, 0, 256, s));
+        prop_walk<false><<<(int)nt1, 64, kPropWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
+                                                           p->d_status, pcnt, nullptr, nullptr, nullptr);
+        DCHK(hipGetLastError());
+        DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, pcnt, pcb, (int)nt1, s));
+        DCHK(hipMemcpyAsync(&n_rec, pcb + n_tiles, 8, hipMemcpyDeviceToHost, s));
+        DCHK(hipStreamSynchronize(s));
+        if (n_rec > 0x7fffffff) return fail(COVT_ERR_INVALID_ARG);
+        const size_t nr = (size_t)(n_rec > 0 ? n_rec : 1), nr1 = nr + 1;
+        DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, pscan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)nr1, s));
+        DCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, psort_tmp, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                (uint32_t*)nullptr, (uint32_t*)nullptr, (int)nr, 0, 41, s));
+        // property arena: records | their tiles | stream counts | output bytes | both prefixes | infos | flags |
+        // in-place input offsets | layout sizes | layout offsets | order keys / values in, out | descriptors |
+        // sort scratch | scan scratch
+        po_rt = up256(nr * sizeof(PropRaw));
+        po_rc = po_rt + up256(nr * 4);
+        po_ro = po_rc + up256(nr1 * 8);
+        po_rsb = po_ro + up256(nr1 * 8);
+        po_rob = po_rsb + up256(nr1 * 8);
+        po_pi = po_rob + up256(nr1 * 8);
+        po_pf = po_pi + up256(nr * sizeof(covt_prop_info));
+        po_pin = po_pf + up256(nr * 2);
+        po_psz = po_pin + up256(nr * 16);
+        po_poff = po_psz + up256(nr1 * 8);
+        po_k0 = po_poff + up256(nr1 * 8);
+        po_k1 = po_k0 + up256(nr * 8);
+        po_v0 = po_k1 + up256(nr * 8);
+        po_v1 = po_v0 + up256(nr * 4);
+        po_pd = po_v1 + up256(nr * 4);
+        po_st = po_pd + up256(nr * sizeof(covt_prop_desc));
+        po_sc = po_st + up256(psort_tmp);
+        prop_total = po_sc + up256(pscan_tmp);
+        DCHK(hipMalloc(&p->prop_arena, prop_total));
+        uint8_t* pa = (uint8_t*)p->prop_arena;
+        recs = (PropRaw*)pa;
+        rtile = (int32_t*)(pa + po_rt);
+        rs_cnt = (int64_t*)(pa + po_rc);
+        rs_ob = (int64_t*)(pa + po_ro);
+        rsb = (int64_t*)(pa + po_rsb);
+        rob = (int64_t*)(pa + po_rob);
+        p->n_props = n_rec;
+        p->d_pinfo = (covt_prop_info*)(pa + po_pi);
+        p->d_pdesc = (covt_prop_desc*)(pa + po_pd);
+        if (n_rec > 0) {
+            prop_walk<true><<<n_tiles, 64, kPropWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
+                                                             format, p->d_status, nullptr, pcb, recs, rtile);
+            DCHK(hipGetLastError());
+        }
+        const int32_t lane_max0 = lane_limits(o.lane_max_bytes, o.lane_max_values);
+        prop_sizes<<<(int)((nr1 + 255) / 256), 256, 0, s>>>(recs, n_rec, id_mode, lane_max0, rs_cnt, rs_ob, pacc);
+        DCHK(hipGetLastError());
+        DCHK(hipcub::DeviceScan::ExclusiveSum(pa + po_sc, pscan_tmp, rs_cnt, rsb, (int)(n_rec + 1), s));
+        DCHK(hipcub::DeviceScan::ExclusiveSum(pa + po_sc, pscan_tmp, rs_ob, rob, (int)(n_rec + 1), s));
+        int64_t *tcn = (int64_t*)(ta + o_ttc), *ton = (int64_t*)(ta + o_tto);
+        tile_totals<<<(int)((nt1 + 255) / 256), 256, 0, s>>>(cnt, ob, pcb, rsb, rob, n_tiles, tcn, ton);
+        DCHK(hipGetLastError());
+        scan_cnt = tcn;
+        scan_ob = ton;
+    }
+    DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, scan_cnt, cb, (int)nt1, s));
+    DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, scan_ob, obb, (int)nt1, s));
+    plan_head<<<1, 1024, 0, s>>>(cb, obb, tcost, n_tiles, head, pacc);
     DCHK(hipGetLastError());
     int64_t hd[4];
     DCHK(hipMemcpyAsync(hd, head, sizeof(hd), hipMemcpyDeviceToHost, s));
@@ -1664,8 +2237,15 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
                 d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cb, obb,
                 lane_max, p->d_info, nvals, tsum, nullptr);
         DCHK(hipGetLastError());
-        reduce_tiles<<<1, 1024, 0, s>>>(tsum, n_tiles, totals);
+        reduce_tiles<<<1, 1024, 0, s>>>(tsum, n_tiles, totals, pacc);
         DCHK(hipGetLastError());
+        if (props && n_rec > 0) {  // the property streams after each tile's Id / Geometry ones
+            uint8_t* pa = (uint8_t*)p->prop_arena;
+            prop_fill<<<(int)((n_rec + 255) / 256), 256, 0, s>>>(recs, rtile, n_rec, id_mode, d_tile_offsets, cnt, ob, cb,
+                                                                 obb, pcb, rsb, rob, p->d_info, nvals, p->d_pinfo,
+                                                                 (uint16_t*)(pa + po_pf), (int64_t*)(pa + po_pin));
+            DCHK(hipGetLastError());
+        }
     }
     const int blocks_s = (int)((ns + 255) / 256);
     if (ns > 0 && !splitting) {
@@ -1724,6 +2304,27 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         fpf_states_walk<<<walkers, 64, kStreamRdLds, s>>>(d_bytes, p->d_info, nvals, totals, fpf_list, o.split_values, p->d_desc);
         DCHK(hipGetLastError());
     }
+    if (props) {  // property output layout and the largest-first descriptor order (after the stream descriptors)
+        uint8_t* pa = (uint8_t*)p->prop_arena;
+        auto* pflags = (uint16_t*)(pa + po_pf);
+        auto *psz = (int64_t*)(pa + po_psz), *poff = (int64_t*)(pa + po_poff);
+        const int pb = (int)((n_rec + 256) / 256);
+        prop_layout<<<pb, 256, 0, s>>>(p->d_pinfo, pflags, n_rec, psz);
+        DCHK(hipGetLastError());
+        DCHK(hipcub::DeviceScan::ExclusiveSum(pa + po_sc, pscan_tmp, psz, poff, (int)(n_rec + 1), s));
+        DCHK(hipMemcpyAsync(&p->prop_bytes, poff + n_rec, 8, hipMemcpyDeviceToHost, s));
+        if (n_rec > 0) {
+            prop_layout_fill<<<pb, 256, 0, s>>>(p->d_pinfo, pflags, n_rec, poff);
+            auto *pk0 = (uint64_t*)(pa + po_k0), *pk1 = (uint64_t*)(pa + po_k1);
+            auto *pv0 = (uint32_t*)(pa + po_v0), *pv1 = (uint32_t*)(pa + po_v1);
+            prop_order_keys<<<pb, 256, 0, s>>>(p->d_pinfo, n_rec, pk0, pv0);
+            DCHK(hipGetLastError());
+            DCHK(hipcub::DeviceRadixSort::SortPairs(pa + po_st, psort_tmp, pk0, pk1, pv0, pv1, (int)n_rec, 0, 41, s));
+            prop_desc_fill<<<pb, 256, 0, s>>>(p->d_pinfo, pflags, (const int64_t*)(pa + po_pin), pv1, n_rec, p->d_info,
+                                              p->d_pdesc);
+            DCHK(hipGetLastError());
+        }
+    }
     unsigned long long tot[T_N];
     DCHK(hipMemcpyAsync(tot, totals, sizeof(tot), hipMemcpyDeviceToHost, s));
     DCHK(hipStreamSynchronize(s));
@@ -1744,6 +2345,7 @@ void covt_device_plan_destroy(covt_device_plan* p) {
     if (p->stream_arena) (void)hipFree(p->stream_arena);
     if (p->desc_arena) (void)hipFree(p->desc_arena);
     if (p->geo_arena) (void)hipFree(p->geo_arena);
+    if (p->prop_arena) (void)hipFree(p->prop_arena);
     if (sw) (void)hipSetDevice(cur);
     delete p;
 }
@@ -1863,6 +2465,25 @@ int covt_device_plan_geometry(covt_device_plan* p, void* hip_stream) {
     p->asm_bytes = asm_bytes;
     p->geo_built = true;
     return COVT_OK;
+}
+
+int64_t covt_device_plan_num_property_columns(const covt_device_plan* p) { return p ? p->n_props : 0; }
+int64_t covt_device_plan_property_bytes(const covt_device_plan* p) { return p ? p->prop_bytes : 0; }
+const covt_prop_desc* covt_device_plan_property_descs_device(const covt_device_plan* p) { return p ? p->d_pdesc : nullptr; }
+int covt_device_plan_property_copy(const covt_device_plan* p, covt_prop_info* infos, covt_prop_desc* descs) {
+    if (!p) return COVT_ERR_INVALID_ARG;
+    if (p->n_props == 0) return COVT_OK;
+    if (infos && hipMemcpy(infos, p->d_pinfo, (size_t)p->n_props * sizeof(covt_prop_info), hipMemcpyDeviceToHost) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    if (descs && hipMemcpy(descs, p->d_pdesc, (size_t)p->n_props * sizeof(covt_prop_desc), hipMemcpyDeviceToHost) != hipSuccess)
+        return COVT_ERR_DEVICE;
+    return COVT_OK;
+}
+int covt_device_plan_materialize(const covt_device_plan* p, const uint8_t* d_in, const uint8_t* d_decoded,
+                                 const covt_stream_result* d_res, uint8_t* d_props, covt_prop_result* d_pres,
+                                 void* hip_stream) {
+    if (!p) return COVT_ERR_INVALID_ARG;
+    return covt_materialize_properties_device(d_in, d_decoded, d_res, p->d_pdesc, p->n_props, d_props, d_pres, hip_stream);
 }
 
 int64_t covt_device_plan_num_geometry_columns(const covt_device_plan* p) { return p && p->geo_built ? p->n_geo : 0; }

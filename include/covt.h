@@ -469,8 +469,8 @@ int covt_plan_properties_host(const covt_plan* plan, const uint8_t* bytes, uint6
  * covt_stream_info fields and 128-byte aligned output slices, descriptors in the same launch order
  * and families, including the split rule: with the same options, the long poles of a small batch are
  * cut into the same chunks (varint byte chunks, FastPFOR value chunks with their start states, ORC RLE
- * group chunks); geometry-column planning on request (covt_device_plan_geometry).  Property columns
- * and multi-GPU shards stay with the host plan.
+ * group chunks); geometry-column planning on request (covt_device_plan_geometry); property columns
+ * with COVT_PLAN_PROPERTIES in opts->flags.  Multi-GPU shards stay with the host plan.
  * Runs on `hip_stream` and synchronises it twice (three times when it splits: the stream count and
  * the descriptor count size the arrays).
  * Limits and memory: a tile of 0x7ff00000 bytes or more gets COVT_ERR_INVALID_ARG as its status
@@ -481,7 +481,7 @@ typedef struct covt_device_plan covt_device_plan;
 int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_tile_offsets,
                             const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                             void* hip_stream, covt_device_plan** out);
-/* the same with explicit options (NULL: the defaults; flags must be 0) */
+/* the same with explicit options (NULL: the defaults; flags: 0 or COVT_PLAN_PROPERTIES) */
 int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_tile_offsets,
                                  const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                                  const covt_plan_options* opts, void* hip_stream, covt_device_plan** out);
@@ -515,6 +515,19 @@ int covt_device_plan_geometry_copy(const covt_device_plan* plan, covt_geom_info*
  * result per column in launch order (column c's at its covt_geom_info.desc_index). */
 int covt_device_plan_assemble(covt_device_plan* plan, const uint8_t* d_decoded, const covt_stream_result* d_res,
                               uint8_t* d_asm, covt_geom_result* d_gres, void* hip_stream);
+/* Property columns from a device plan made with COVT_PLAN_PROPERTIES in opts->flags: the records,
+ * output layout and largest-first descriptors of covt_plan_property_columns / covt_plan_property_descs,
+ * built on the device with the plan (the host plan's exactly); a plan without the flag has none. */
+int64_t covt_device_plan_num_property_columns(const covt_device_plan* plan);
+int64_t covt_device_plan_property_bytes(const covt_device_plan* plan);
+const covt_prop_desc* covt_device_plan_property_descs_device(const covt_device_plan* plan);
+int covt_device_plan_property_copy(const covt_device_plan* plan, covt_prop_info* infos, covt_prop_desc* descs);
+/* covt_materialize_properties_device over the plan's property descriptors, after covt_device_plan_decode
+ * on the same stream: d_props covt_device_plan_property_bytes bytes, d_pres one result per (sub)column in
+ * descriptor order (column c's at its covt_prop_info.desc_index). */
+int covt_device_plan_materialize(const covt_device_plan* plan, const uint8_t* d_in, const uint8_t* d_decoded,
+                                 const covt_stream_result* d_res, uint8_t* d_props, covt_prop_result* d_pres,
+                                 void* hip_stream);
 /* the grouped decode launch over the plan's descriptors (covt_decode_streams_device_grouped):
  * d_out covt_device_plan_output_bytes bytes, d_res num_descs results (stream i's at its desc_index).
  * Asynchronous. */

@@ -341,3 +341,82 @@ def test_split_malformed_streams(covt, gpu_available, decodable_tiles):
     _assert_same_plan(hp, dp)
     _assert_same_decode(covt, hp, dp)
     _assert_same_assembly(covt, hp, dp)
+
+
+# ---- property columns (COVT_PLAN_PROPERTIES on the device: covt_plan_device.hip prop_walk ... prop_desc_fill)
+def _assert_same_properties(hp, dp):
+    """The device plan's property records (covt_prop_info: streams, names, layout) and largest-first
+    descriptors equal the host plan's byte for byte."""
+    assert dp.num_property_columns == hp.num_property_columns > 0
+    assert dp.property_bytes == hp.property_bytes
+    pinfo, pdesc = dp.property_copy()
+    assert pinfo.tobytes() == hp.props.tobytes()
+    assert pdesc.tobytes() == hp.pdescs.tobytes()
+
+
+def _assert_same_materialization(covt, hp, dp):
+    """Decode + materialization through the device plan equal the host path's (covt_plan_properties_host),
+    column by column, statuses included."""
+    import torch
+
+    d_out, d_res = dp.alloc()
+    d_props, d_pres = dp.alloc_properties()
+    dp.decode(d_out, d_res)
+    dp.materialize(d_out, d_res, d_props, d_pres)
+    torch.cuda.synchronize()
+    buf_d = d_props.cpu().numpy()[:dp.property_bytes]
+    pres_d = d_pres.cpu().numpy().view(covt.PROP_RESULT_DTYPE)[:dp.num_property_columns][hp.props["desc_index"]]
+    buf_h, pres_h = hp.properties_host()
+    assert np.array_equal(pres_d, pres_h)
+    n_ok = 0
+    for c in range(hp.num_property_columns):
+        if int(pres_h["status"][c]) != 0:
+            continue
+        x, y = hp.property_column(buf_h, pres_h, c), hp.property_column(buf_d, pres_d, c)
+        assert np.array_equal(x.validity, y.validity) and np.array_equal(x.values, y.values), c
+        assert (x.dict_offsets is None) == (y.dict_offsets is None), c
+        if x.dict_offsets is not None:
+            assert np.array_equal(x.dict_offsets, y.dict_offsets) and np.array_equal(x.dict_bytes, y.dict_bytes), c
+        n_ok += 1
+    return n_ok
+
+
+@pytest.mark.parametrize("id_mode", [0, 1], ids=["id_format", "id_java"])
+def test_properties_genc(covt, gpu_available, id_mode):
+    """Every fixture tile with COVT_PLAN_PROPERTIES: Gen C property walk (roles by stream name, localized
+    present_<lang> sub-columns sharing their column's dictionary), the property streams after each tile's
+    Id / Geometry streams, the same launch order, layout and descriptors as the host plan."""
+    tiles = [open(p, "rb").read() for p in tile_paths()]
+    hp = _host_plan(covt, tiles, covt.FORMAT_GENC, id_mode, flags=covt.PLAN_PROPERTIES)
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, id_mode)
+    _assert_same_plan(hp, dp)
+    _assert_same_properties(hp, dp)
+    assert _assert_same_materialization(covt, hp, dp) > 10000
+    _assert_same_decode(covt, hp, dp)
+
+
+@pytest.mark.parametrize("optimized", [False, True], ids=["named", "optimized"])
+def test_properties_gend(covt, gpu_available, decodable_tiles, optimized):
+    """Gen D conversions with property columns: the implicit present stream's byte-RLE length walked on the
+    device, TreeMap stream order; plan, layout, descriptors and materialization as the host's."""
+    tiles = [RT.genc_to_gend(t, optimized=optimized)[0] for _, t in decodable_tiles[::3]]
+    hp = _host_plan(covt, tiles, covt.FORMAT_GEND, 0, flags=covt.PLAN_PROPERTIES)
+    dp = _device_plan(covt, hp, covt.FORMAT_GEND, 0)
+    assert (hp.tile_status == 0).all()
+    _assert_same_plan(hp, dp)
+    _assert_same_properties(hp, dp)
+    _assert_same_materialization(covt, hp, dp)
+
+
+def test_properties_split(covt, gpu_available, decodable_tiles, golden_streams):
+    """Property plans with the split rule forced (long property RLE streams cut into group chunks too):
+    the same plan, and the Id / Geometry streams still match the golden digests."""
+    picks = decodable_tiles[::4][:24]
+    keys, tiles = [k for k, _ in picks], [t for _, t in picks]
+    hp = _host_plan(covt, tiles, covt.FORMAT_GENC, 0, split=True, split_min=0, split_ratio=0, split_chunk=128,
+                    split_values=256, flags=covt.PLAN_PROPERTIES)
+    assert (hp.family_counts[covt.FAMILY_SPLIT:] > 0).all(), hp.family_counts
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
+    _assert_same_plan(hp, dp)
+    _assert_same_properties(hp, dp)
+    _assert_same_materialization(covt, hp, dp)
