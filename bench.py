@@ -314,10 +314,45 @@ def device_plan_leg(plan, batch, torch, dev, covt, args, t_plan):
         e_.record(stream)
     torch.cuda.synchronize(dev)
     _, res = batch.results()
-    return {"ms_median": round(float(np.median(times)) * 1e3, 3), "ms_min": round(min(times) * 1e3, 3),
-            "host_plan_ms": round(t_plan * 1e3, 1), "streams": dp.num_streams,
-            "descs_equal_host_plan": same, "decode_ms": round(float(np.mean([a.elapsed_time(b) for a, b in ev])), 4),
-            "decode_errors": int((res[:, 0] != 0).sum()), "reps": args.device_plan_reps}
+    out = {"ms_median": round(float(np.median(times)) * 1e3, 3), "ms_min": round(min(times) * 1e3, 3),
+           "host_plan_ms": round(t_plan * 1e3, 1), "streams": dp.num_streams,
+           "descs_equal_host_plan": same, "decode_ms": round(float(np.mean([a.elapsed_time(b) for a, b in ev])), 4),
+           "decode_errors": int((res[:, 0] != 0).sum()), "reps": args.device_plan_reps}
+    dp.close()
+    try:
+        out["properties"] = device_plan_props(plan, batch, torch, dev, covt, args, offs, sizes)
+    except Exception as e:  # noqa: BLE001 -- reported on the line, never fatal to the headline
+        out["properties"] = {"error": repr(e)}
+    return out
+
+
+def device_plan_props(plan, batch, torch, dev, covt, args, offs, sizes):
+    """The same batch planned with its property columns (COVT_PLAN_PROPERTIES): the whole decodeCovt plan on
+    the GPU, checked against the host plan's records and descriptors."""
+    popts = covt.PlanOptions(flags=covt.PLAN_PROPERTIES)
+    t0 = time.perf_counter()
+    hp = covt.Plan(plan.blob, plan.offsets, plan.sizes, covt.FORMAT_GENC, args.id_mode, options=popts)
+    t_hp = time.perf_counter() - t0
+    ptimes = []
+    for k in range(args.device_plan_reps):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        pdp = covt.DevicePlan(batch.d_in, offs, sizes, covt.FORMAT_GENC, args.id_mode, options=popts)
+        ptimes.append(time.perf_counter() - t0)
+        if k < args.device_plan_reps - 1:
+            pdp.close()
+    info, descs, _ = pdp.host_copy()
+    pinfo, pdesc = pdp.property_copy()
+    psame = bool(info.tobytes() == hp.streams.tobytes() and descs.tobytes() == hp.descs.tobytes() and
+                 pinfo.tobytes() == hp.props.tobytes() and pdesc.tobytes() == hp.pdescs.tobytes())
+    res = {"ms_median": round(float(np.median(ptimes)) * 1e3, 3), "ms_min": round(min(ptimes) * 1e3, 3),
+           "host_plan_ms": round(t_hp * 1e3, 1), "streams": pdp.num_streams,
+           "property_columns": pdp.num_property_columns, "equal_host_plan": psame,
+           "note": "covt_device_plan_create_opts with COVT_PLAN_PROPERTIES: Id / Geometry / property "
+                   "streams, property records, layout and descriptors on the GPU (wall clock per "
+                   "creation, 3 syncs)"}
+    pdp.close()
+    return res
 
 
 def assembly_leg(batch, plan, stream, args, dist, torch, dev):
