@@ -3,7 +3,8 @@
 creation printed (run under rocprofv3 --kernel-trace --stats [--hip-trace] for the per-kernel / per-call
 breakdown).  usage: device_plan_prof.py [reps] [--sweep | --small | --n256] [--nosplit] [--sorted] [--geometry]
 --sweep: also batches of 1 tile (the library's largest), 256, 2048 and 4096 tiles (latency vs. occupancy).
---geometry: also time covt_device_plan_geometry (the geometry-column planning) after each creation."""
+--geometry: also time covt_device_plan_geometry (the geometry-column planning) after each creation.
+--props: plans with COVT_PLAN_PROPERTIES (property columns planned on the device too)."""
 import os
 import sys
 import time
@@ -49,7 +50,12 @@ def run(covt, tiles, reps, label):
     for _ in range(reps + 2):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        dp = covt.DevicePlan(d_blob, d_off, d_size, options=covt.PlanOptions(split_min=-1) if "--nosplit" in sys.argv else None)
+        kw = {}
+        if "--nosplit" in sys.argv:
+            kw["split_min"] = -1
+        if "--props" in sys.argv:
+            kw["flags"] = covt.PLAN_PROPERTIES
+        dp = covt.DevicePlan(d_blob, d_off, d_size, options=covt.PlanOptions(**kw) if kw else None)
         ts.append(time.perf_counter() - t0)
         if "--geometry" in sys.argv:
             t0 = time.perf_counter()

@@ -87,6 +87,8 @@ for s in "$@"; do
     config1_passes) for v in libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so; do
             COVT_LIB_VARIANT=$v step config1_$v 300 rocprofv3 --kernel-trace --stats -d gpurun_out/config1_$v -o run --output-format csv -- python tools/config1_prof.py 20
         done ;;
+    dplan_props) step dplan_props 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_props -o run --output-format csv -- python tools/device_plan_prof.py 5 --props ;;
+    launch_modes) step launch_modes 300 python tools/launch_mode_ab.py ;;
     dplan_prof) step dplan_prof 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_prof -o run --output-format csv -- python tools/device_plan_prof.py 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
