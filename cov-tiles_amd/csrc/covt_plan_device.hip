@@ -1467,9 +1467,12 @@ __global__ void fpf_states_walk(const uint8_t* __restrict__ bytes, const covt_st
 // prop_layout / prop_layout_fill the property output slices, a stable radix sort the largest-first
 // materialization order and prop_desc_fill the covt_prop_desc table.
 struct PropSm {  // a property column's stream, as the Gen C walk reads it
-    int32_t noff, nlen, nv, bl, enc;
-    int32_t off;  // layer-data-relative
+    uint64_t h0, h8;  // localized string columns: hashes of the name and of its bytes from 8 on (names_hash)
+    int32_t noff, nlen, nv, bl;
+    int32_t off;      // layer-data-relative
+    uint16_t enc, role;  // role: PR_* bits of the name, classified while the window holds it
 };
+enum { PR_PRESENT = 1, PR_DATA = 2, PR_LENGTH = 4, PR_DICTIONARY = 8, PR_PRESENT_LANG = 16 };
 constexpr int kPropMaxStreams = 256;  // numStreams bound of the walk (walk_genc: > 256 is BAD_HEADER)
 constexpr size_t kPropWalkLds = 512 + kPropMaxStreams * sizeof(PropSm);  // Rd window + stream table
 
@@ -1481,6 +1484,20 @@ __device__ __forceinline__ bool names_equal(Rd<true>& r, int32_t a, int32_t b, i
         if ((r.peek8(a + i) & m) != (r.peek8(b + i) & m)) return false;
     }
     return true;
+}
+// a hash of bytes [a, a + n) (equal bytes, equal hashes): read while the walk's window holds the name, so
+// the localized columns' name matching below compares hashes and confirms a match with names_equal --
+// one window refill per match instead of a refill per byte compared (two names of a long column lie
+// further apart than the window, and the all-pairs compare ping-ponged between them: ~9 ms per walk)
+__device__ __forceinline__ uint64_t names_hash(Rd<true>& r, int32_t a, int32_t n) {
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)(uint32_t)n;
+    for (int32_t i = 0; i < n; i += 8) {
+        const int32_t k = n - i < 8 ? n - i : 8;
+        const uint64_t m = k >= 8 ? ~0ull : ((1ull << (8 * k)) - 1);
+        h = (h ^ (r.peek8(a + i) & m)) * 0xff51afd7ed558ccdull;
+        h ^= h >> 29;
+    }
+    return h;
 }
 
 // Gen C property records (walk_genc's props branch): a column's streams in metadata order, roles by
@@ -1510,6 +1527,7 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
             if (!r.uv(o, ns)) return COVT_ERR_TRUNCATED;
             if (ns > 256) return COVT_ERR_BAD_HEADER;
             const int kind = COVT_IS(name, cn, "id") ? 0 : (COVT_IS(name, cn, "geometry") || dtype == 6) ? 1 : 2;
+            const bool localized = kind == 2 && genc_prop_type(dtype) == COVT_PROP_STRING && ctype == 2;
             for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
                 if (!r.uv(o, sn) || sn > (uint64_t)(len - o)) return COVT_ERR_TRUNCATED;
                 const int32_t sname = o;
@@ -1520,8 +1538,24 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
                     enc = r.at(o++);
                 }
                 if (nv > 0x7fffffff || bl > 0x7fffffff) return COVT_ERR_BAD_HEADER;
-                if (kind == 2 && threadIdx.x == 0)
-                    tab[q] = PropSm{sname, (int32_t)sn, (int32_t)nv, (int32_t)bl, enc, (int32_t)d};
+                if (kind == 2) {  // the name's role (and, localized, its hashes) while the window holds it
+                    uint32_t role = 0;
+                    if (COVT_IS(sname, sn, "present")) role |= PR_PRESENT;
+                    if (COVT_IS(sname, sn, "data")) role |= PR_DATA;
+                    if (COVT_IS(sname, sn, "length")) role |= PR_LENGTH;
+                    if (COVT_IS(sname, sn, "dictionary")) role |= PR_DICTIONARY;
+                    uint64_t h0 = 0, h8 = 0;
+                    if (localized) {
+                        if (sn > 8 && r.peek8(sname) == pk("present_", 0, 8)) {
+                            role |= PR_PRESENT_LANG;
+                            h8 = names_hash(r, sname + 8, (int32_t)sn - 8);
+                        }
+                        h0 = names_hash(r, sname, (int32_t)sn);
+                    }
+                    if (threadIdx.x == 0)
+                        tab[q] = PropSm{h0, h8, sname, (int32_t)sn, (int32_t)nv, (int32_t)bl, (int32_t)d, (uint16_t)enc,
+                                        (uint16_t)role};
+                }
                 d += (int64_t)bl;
             }
             if (kind != 2) continue;
@@ -1533,21 +1567,32 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
             p.name_len = (int32_t)cn;
             p.type = genc_prop_type(dtype);
             p.ctype = ctype;
-            if (p.type == COVT_PROP_STRING && ctype == 2) {
+            if (localized) {
                 int ls = -1, ds = -1;
                 for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
-                    const PropSm sm = tab[q];
-                    if (COVT_IS(sm.noff, sm.nlen, "length")) ls = (int)q;
-                    else if (COVT_IS(sm.noff, sm.nlen, "dictionary")) ds = (int)q;
+                    const uint32_t role = tab[q].role;
+                    if (role & PR_LENGTH) ls = (int)q;
+                    else if (role & PR_DICTIONARY) ds = (int)q;
                 }
                 int32_t lang = 0;
                 for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
                     const PropSm sm = tab[q];
-                    if (sm.nlen <= 8 || (r.peek8(sm.noff) != pk("present_", 0, 8))) continue;
+                    if (!(sm.role & PR_PRESENT_LANG)) continue;
                     const int32_t ll = sm.nlen - 8;
+                    // the last stream named <lang>: 64 candidates per step, hash matches confirmed from the
+                    // highest down (a serial all-pairs scan was ~ns^2 dependent LDS reads: ms per tile)
                     int dd = -1;
-                    for (uint32_t k = 0; k < (uint32_t)ns; ++k)
-                        if (tab[k].nlen == ll && names_equal(r, tab[k].noff, sm.noff + 8, ll)) dd = (int)k;
+                    for (int32_t k0 = ((int32_t)ns - 1) & ~63; k0 >= 0 && dd < 0; k0 -= 64) {
+                        const int32_t k = k0 + (int32_t)threadIdx.x;
+                        const bool m = k < (int32_t)ns && tab[k].nlen == ll && tab[k].h0 == sm.h8;
+                        uint64_t bal = __ballot(m);
+                        while (bal && dd < 0) {
+                            const int hi = 63 - __builtin_clzll(bal);
+                            const int32_t kk = k0 + hi;
+                            if (names_equal(r, tab[kk].noff, sm.noff + 8, ll)) dd = kk;
+                            bal &= ~(1ull << hi);
+                        }
+                    }
                     PropRaw x = p;
                     x.lang = lang++;
                     x.lang_off = sm.noff + 8;
@@ -1561,10 +1606,10 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
             } else {
                 for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
                     const PropSm sm = tab[q];
-                    if (COVT_IS(sm.noff, sm.nlen, "present")) prop_stream(p, 0, sm.off, sm.nv, sm.bl, sm.enc);
-                    if (COVT_IS(sm.noff, sm.nlen, "data")) prop_stream(p, 1, sm.off, sm.nv, sm.bl, sm.enc);
-                    if (COVT_IS(sm.noff, sm.nlen, "length")) prop_stream(p, 2, sm.off, sm.nv, sm.bl, sm.enc);
-                    if (COVT_IS(sm.noff, sm.nlen, "dictionary")) prop_stream(p, 3, sm.off, sm.nv, sm.bl, sm.enc);
+                    if (sm.role & PR_PRESENT) prop_stream(p, 0, sm.off, sm.nv, sm.bl, sm.enc);
+                    if (sm.role & PR_DATA) prop_stream(p, 1, sm.off, sm.nv, sm.bl, sm.enc);
+                    if (sm.role & PR_LENGTH) prop_stream(p, 2, sm.off, sm.nv, sm.bl, sm.enc);
+                    if (sm.role & PR_DICTIONARY) prop_stream(p, 3, sm.off, sm.nv, sm.bl, sm.enc);
                 }
                 pe(p);
             }

@@ -68,11 +68,16 @@ for s in "$@"; do
     tests_changed) step pytest_changed 600 python -u -m pytest tests/test_gpu_assembly.py tests/test_gpu_props.py tests/test_gpu_split.py tests/test_gpu_rle_adversarial.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     tests_dplan) step pytest_dplan 300 python -u -m pytest tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     dplan_geo) step dplan_geo 200 python tools/device_plan_prof.py 20 --sweep --geometry ;;
+    dplan_sweep) step dplan_sweep 300 python tools/device_plan_prof.py 10 --sweep ;;
+    dplan_props_sweep) step dplan_props_sweep 300 python tools/device_plan_prof.py 10 --sweep --props ;;
     dplan_ab) step dplan_ab 300 python tools/device_plan_ab.py 0 1 ;;
     dplan_var) for v in ${AB_VARIANTS:-libcovt.so}; do
             COVT_LIB_VARIANT=$v timeout -k 10 200 python tools/device_plan_prof.py 20 --sweep 2>&1 | grep -v amdgpu.ids || fatal dplan_var $?
         done ;;
     dplan_prof_small) step dplan_prof_small 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_prof_small -o run --output-format csv -- python tools/device_plan_prof.py 5 --small ;;
+    dplan_props_small) step dplan_props_small 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_props_small -o run --output-format csv -- python tools/device_plan_prof.py 5 --small --props ;;
+    dplan_sq1) step dplan_sq1 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/dplan_sq1 -o run --output-format csv -- python tools/device_plan_prof.py 2 --props ;;
+    dplan_sq2) step dplan_sq2 300 rocprofv3 --pmc SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_BRANCH GRBM_GUI_ACTIVE -d gpurun_out/dplan_sq2 -o run --output-format csv -- python tools/device_plan_prof.py 2 --props ;;
     dplan_prof_256) step dplan_prof_256 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_prof_256 -o run --output-format csv -- python tools/device_plan_prof.py 5 --n256 ;;
     dplan_api_small) step dplan_api_small 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_api_small -o run --output-format csv -- python tools/device_plan_prof.py 20 --small --nosplit ;;
     dplan_sq_small) step dplan_sq_small 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_BRANCH -d gpurun_out/dplan_sq_small -o run --output-format csv -- python tools/device_plan_prof.py 3 --small --nosplit ;;

@@ -95,10 +95,10 @@ def main():
     print("torch fill_ of the output bytes: %.3f ms  %5.0f GB/s" % (t, w_total / t / 1e6))
 
     # 2. the batch's own regions in three output layouts
-    def layout(order):
+    def layout(order, align=16):
         d = descs.copy()
         oo = np.zeros(plan.num_streams, dtype=np.uint64)
-        sz = (nbytes[order] + 15) // 16 * 16
+        sz = (nbytes[order] + align - 1) // align * align
         oo[order] = np.concatenate([[0], np.cumsum(sz)[:-1]]).astype(np.uint64)
         d[:, 8:16] = oo.view(np.uint8).reshape(-1, 8)
         return torch.from_numpy(d.ravel().copy()).cuda()
@@ -124,6 +124,15 @@ def main():
                                                     hi - lo, out.data_ptr(), 1, sink.data_ptr(), stream))
             tb = int(ib[lo:hi].sum() + nbytes[lo:hi].sum())
             print("   %-8s read+write %-12s: %.3f ms  %5.0f GB/s" % (fname, name, t, tb / t / 1e6))
+    # 2b. several consecutive descriptors per wave (a longer contiguous write run in launch order)
+    wp.probe_copy_regions_multi.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int,
+                                            C.c_void_p, C.c_void_p]
+    for name, dd in (("tile order", tile_d), ("launch order", launch_d)):
+        for K in (1, 2, 4, 8, 16):
+            t = timed(lambda: wp.probe_copy_regions_multi(inb.data_ptr(), dd.data_ptr(), d_nb.data_ptr(),
+                                                          plan.num_streams, out.data_ptr(), K, sink.data_ptr(), stream))
+            print("regions read+write %-12s %2d descriptors per wave: %.3f ms  %5.0f GB/s" % (
+                name, K, t, (w_total + r_total) / t / 1e6))
     # 3. the real decode launch for reference, same process
     t = timed(lambda: batch.decode(), reps=10)
     print("decode launch (tile-order layout): %.3f ms  %5.0f GB/s algorithmic" % (t, (w_total + r_total) / t / 1e6))
