@@ -307,6 +307,13 @@ struct SortKey {
     uint64_t k;
     uint32_t i;
 };
+inline int key_family(uint64_t k) {
+#ifdef COVT_EXACT_ORDER
+    return (int)(k >> 60);
+#else
+    return (int)(k >> kLaunchFamShift);
+#endif
+}
 void radix_sort(std::vector<SortKey>& a) {
     const size_t n = a.size();
     if (n < 2) return;
@@ -1444,7 +1451,7 @@ int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, co
         });
     }
     // 3. launch order: grouped by family (the lane family also by op, for op-uniform waves), largest
-    // streams first inside a family so the long poles start early (static wave->stream map); one
+    // streams first inside a family so the long poles start early (launch_key, covt_internal.h); one
     // precomputed key per stream, ties in tile order
     const size_t ns = p->info.size();
     std::vector<SortKey> keys(ns);
@@ -1511,9 +1518,13 @@ int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, co
                                                     : rsplit           ? COVT_FAMILY_SPLIT_RLE
                                                                        : COVT_FAMILY_SPLIT)
                                  : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family_of(s.op);
+#ifdef COVT_EXACT_ORDER  // (A/B: the exact cost-descending order of rounds 1-4)
             const uint64_t cost = std::min<uint64_t>((uint64_t)stream_cost(s), (1ull << 48) - 1);
             keys[i] = SortKey{(fam << 60) | ((lane ? (uint64_t)s.op : 0ull) << 52) | ((1ull << 48) - 1 - cost),
                               (uint32_t)i};
+#else
+            keys[i] = SortKey{launch_key((uint32_t)fam, fam == COVT_FAMILY_LANE, s.op, stream_cost(s)), (uint32_t)i};
+#endif
             int64_t nd = 1;
             if (rsplit) {
                 nd = (int64_t)rs->second.first.size() * COVT_SPLIT_SLOTS;
@@ -1531,7 +1542,7 @@ int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, co
     dpos[0] = 0;
     for (size_t k = 0; k < ns; ++k) {
         dpos[k + 1] = dpos[k] + ndesc[keys[k].i];
-        p->fam_counts[keys[k].k >> 60] += ndesc[keys[k].i];
+        p->fam_counts[key_family(keys[k].k)] += ndesc[keys[k].i];
     }
     p->descs.resize((size_t)dpos[ns]);
     p->desc_stream.resize((size_t)dpos[ns]);
@@ -1540,7 +1551,7 @@ int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, co
             const size_t k = (size_t)kk;
             const size_t i = keys[k].i;
             covt_stream_info& si = p->info[i];
-            const int fam = (int)(keys[k].k >> 60);
+            const int fam = key_family(keys[k].k);
             size_t o = (size_t)dpos[k];
             covt_stream_desc d{};
             d.in_off = (uint64_t)si.in_off;

@@ -42,6 +42,35 @@ constexpr int64_t kFusedLaneStreams = 64 * kWavesPerBlock;
 constexpr int64_t kOutAlign = 128;
 __host__ __device__ inline int64_t align_out(int64_t x) { return (x + kOutAlign - 1) & ~(kOutAlign - 1); }
 
+// Launch order (covt_plan_create step 3; the device plan's stream_keys): a 16-bit key, family-major
+// (3 bits), then -- for the lane family -- the op and the exact cost (bytes + output bytes / 4 <= 1023 for
+// a lane stream), largest first, so each 64-stream wave gets streams of one op and near-equal length;
+// for every other family the cost in 1/128 octaves, largest first, so the long poles start early.  A
+// stable sort keeps tile order inside a key.  (The rounds 1-4 key was a 60-bit exact cost: a 40-bit
+// radix sort on the device, ~18 launches, 0.16 ms of the 10k-tile plan; this one is two 8-bit
+// counting-sort passes.)
+constexpr int kLaunchFamShift = 13;
+__host__ __device__ inline uint32_t lane_op_index(int32_t op) {  // the lane ops in op order
+    return op == COVT_OP_BYTE_RLE_U8 ? 0u : op == COVT_OP_RLE_U64 ? 1u : op == COVT_OP_RLE_I32 ? 2u
+         : op == COVT_OP_RLE_S64 ? 3u : 4u;
+}
+__host__ __device__ inline uint32_t launch_key(uint32_t fam, bool lane, int32_t op, int64_t cost) {
+    const uint64_t c = cost > 0 ? (uint64_t)cost : 0;
+    uint32_t sub;
+    if (lane) {
+        sub = (lane_op_index(op) << 10) | (1023u - (uint32_t)(c < 1023 ? c : 1023));
+    } else {
+        uint32_t h = 0;  // 0: no cost; else 1 + e * 128 + the 7 bits below the top one, e = floor(log2 c)
+        if (c) {
+            const int e = 63 - __builtin_clzll(c);
+            const uint32_t mant = e >= 7 ? (uint32_t)(c >> (e - 7)) & 127u : (uint32_t)(c << (7 - e)) & 127u;
+            h = ((uint32_t)e << 7) + mant + 1u;
+        }
+        sub = 8191u - (h < 8191u ? h : 8191u);
+    }
+    return (fam << kLaunchFamShift) | sub;
+}
+
 // Plan rule for the lane-per-stream kernel: RLE streams of at most max_values values and max_bytes bytes
 // (a lane decodes serially; larger streams amortise a wave's window setup).  The two limits travel
 // packed as one int32 (values << 16 | bytes; < 0: no lane family), see lane_limits.

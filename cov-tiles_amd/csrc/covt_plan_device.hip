@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <mutex>
 
 #include "covt.h"
 #include "covt_internal.h"
@@ -54,6 +55,34 @@ struct covt_device_plan {
 };
 
 namespace {
+
+// The plan's arenas come from a per-device stream-ordered pool that keeps freed memory (up to
+// kPoolKeep bytes) for the next plan: a plain hipMalloc of the ~100 MB stream arena between the plan's
+// two host syncs cost ~0.15 ms of the 10k-tile plan (profiles/r04, kernel trace gap).
+constexpr uint64_t kPoolKeep = 8ull << 30;
+hipMemPool_t plan_pool(int dev) {
+    static std::mutex mu;
+    static hipMemPool_t pools[64] = {};
+    if (dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    if (!pools[dev]) {
+        hipMemPoolProps pp{};
+        pp.allocType = hipMemAllocationTypePinned;
+        pp.location.type = hipMemLocationTypeDevice;
+        pp.location.id = dev;
+        hipMemPool_t mp = nullptr;
+        if (hipMemPoolCreate(&mp, &pp) != hipSuccess) return nullptr;
+        uint64_t keep = kPoolKeep;
+        (void)hipMemPoolSetAttribute(mp, hipMemPoolAttrReleaseThreshold, &keep);
+        pools[dev] = mp;
+    }
+    return pools[dev];
+}
+hipError_t plan_malloc(void** q, size_t n, int dev, hipStream_t s) {
+    hipMemPool_t mp = plan_pool(dev);
+    if (!mp) return hipErrorOutOfMemory;
+    return hipMallocFromPoolAsync(q, n, mp, s);
+}
 
 // device totals (int64 slots)
 enum { T_STREAMS = 0, T_OUT = 1, T_IN = 2, T_PAYLOAD = 3, T_VERTS = 4, T_LANE = 5, T_FAM = 8,
@@ -1049,34 +1078,164 @@ __global__ void __launch_bounds__(1024) reduce_tiles(const long long* __restrict
 // way), in 32-bit keys and cb + 8 sort bits when they fit (the bench batch: 26 bits, 4 radix passes
 // instead of 8 over 64-bit keys)
 static_assert(COVT_OP_COUNT <= 32, "the lane op takes 5 key bits");
-template <class K>
 __global__ void stream_keys(const covt_stream_info* info, const int32_t* nvals, int64_t n, int32_t lane_max,
-                            int64_t lane_min, unsigned long long* totals, K* keys, uint32_t* vals,
-                            const uint8_t* sfam, const int64_t* sndesc, int cb) {
+                            int64_t lane_min, unsigned long long* totals, uint32_t* keys, const uint8_t* sfam,
+                            const int64_t* sndesc) {
     __shared__ unsigned long long fam_n[COVT_NUM_FAMILIES];
     if (threadIdx.x < COVT_NUM_FAMILIES) fam_n[threadIdx.x] = 0;
     __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t fam = 0xffu;
     if (i < n) {
         const covt_stream_info& s = info[i];
         const int32_t lm = (int64_t)totals[T_LANE] < lane_min ? -1 : lane_max;
         const bool lane = lane_stream(s.op, nvals[i], s.byte_length, lm);
-        const uint64_t fam = sfam ? (uint64_t)sfam[i] : lane ? (uint64_t)COVT_FAMILY_LANE : (uint64_t)covt_op_family(s.op);
-        const uint64_t cmax = (1ull << cb) - 1;
+        fam = sfam ? (uint32_t)sfam[i] : lane ? (uint32_t)COVT_FAMILY_LANE : (uint32_t)covt_op_family(s.op);
         const int64_t c = (int64_t)s.byte_length + s.out_elems * s.elem_bytes / 4;
-        const uint64_t cost = (uint64_t)c < cmax ? (uint64_t)c : cmax;
-        keys[i] = (K)((fam << (cb + 5)) | ((lane ? (uint64_t)s.op : 0ull) << cb) | (cmax - cost));
-        vals[i] = (uint32_t)i;
-        atomicAdd(&fam_n[fam], sndesc ? (unsigned long long)sndesc[i] : 1ull);
+        keys[i] = launch_key(fam, fam == COVT_FAMILY_LANE, s.op, c);
+        if (sndesc) atomicAdd(&fam_n[fam], (unsigned long long)sndesc[i]);
+    }
+    if (!sndesc) {  // one descriptor per stream: a ballot per family (same-address LDS atomics serialized)
+#pragma unroll
+        for (int f = 0; f < COVT_NUM_FAMILIES; ++f) {
+            const uint64_t b = __ballot(fam == (uint32_t)f);
+            if (b && (threadIdx.x & 63) == 0) atomicAdd(&fam_n[f], (unsigned long long)__popcll(b));
+        }
     }
     __syncthreads();
     if (threadIdx.x < COVT_NUM_FAMILIES && fam_n[threadIdx.x])
         atomicAdd(&totals[T_FAM + threadIdx.x], fam_n[threadIdx.x]);
 }
 
-template <class K>
-__global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const K* keys, const uint32_t* order,
-                           int64_t n, int cb, covt_stream_desc* desc) {
+// ---- launch order: a stable LSD radix sort of the streams' 16-bit launch keys, two 8-bit passes of
+// three launches each: per-chunk digit counts, one workgroup's scan of them (digit-major, so chunk order
+// inside a digit), and the scatter, each wave ranking its 64 keys among equal digits with eight ballots
+constexpr int kSortBuckets = 256;
+constexpr int kSortChunk = 4096;  // keys per workgroup (4 rounds of 1024)
+
+__global__ void __launch_bounds__(256) order_hist(const uint32_t* __restrict__ keys, int64_t n, int32_t nb, int shift,
+                                                  uint32_t* __restrict__ ghist) {
+    __shared__ uint32_t h[kSortBuckets];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kSortChunk;
+    for (int j = threadIdx.x; j < kSortChunk; j += 256)
+        if (base + j < n) atomicAdd(&h[(keys[base + j] >> shift) & 255u], 1u);
+    __syncthreads();
+    ghist[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+}
+
+// exclusive scan of m counts in one workgroup (segments of ceil(m / 1024) per thread)
+__global__ void __launch_bounds__(1024) order_scan(uint32_t* __restrict__ a, int64_t m) {
+    __shared__ uint32_t part[1024];
+    const int64_t seg = (m + 1023) / 1024, lo = threadIdx.x * seg, hi = lo + seg < m ? lo + seg : m;
+    uint32_t sum = 0;
+#pragma unroll 16
+    for (int64_t k = lo; k < hi; ++k) sum += a[k];  // (independent loads: 16 in flight per thread)
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele over the 1024 segment sums
+        const uint32_t x = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+#pragma unroll 16
+    for (int64_t k = lo; k < hi; ++k) {
+        const uint32_t c = a[k];
+        a[k] = run;
+        run += c;
+    }
+}
+
+// vals null: the identity (the first pass).  scanned: gpos holds order_scan's offsets; else gpos holds
+// order_hist's counts and each workgroup sums the ones before it (nb <= kSortFuseChunks: one launch less)
+constexpr int kSortFuseChunks = 512;
+__global__ void __launch_bounds__(1024) order_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                      int64_t n, int32_t nb, int shift, const uint32_t* __restrict__ gpos,
+                                                      int scanned, uint32_t* __restrict__ okeys, uint32_t* __restrict__ ovals) {
+    __shared__ uint32_t run[kSortBuckets];
+    __shared__ uint32_t wc[16][kSortBuckets];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (scanned) {
+        if (threadIdx.x < kSortBuckets) run[threadIdx.x] = gpos[(size_t)threadIdx.x * nb + blockIdx.x];
+    } else {
+        // digit totals and the counts of the chunks before this one (4 threads per digit)
+        const int dg = threadIdx.x >> 2, part = threadIdx.x & 3;
+        const uint32_t* row = gpos + (size_t)dg * nb;
+        uint32_t tot = 0, pre = 0;
+#pragma unroll 8
+        for (int c = part; c < nb; c += 4) {
+            const uint32_t v = row[c];
+            tot += v;
+            pre += c < (int)blockIdx.x ? v : 0u;
+        }
+        tot += __shfl_xor(tot, 1, 64);
+        tot += __shfl_xor(tot, 2, 64);
+        pre += __shfl_xor(pre, 1, 64);
+        pre += __shfl_xor(pre, 2, 64);
+        uint32_t* ts = &wc[0][0];  // (scratch before the rounds)
+        if (part == 0) ts[dg] = tot;
+        __syncthreads();
+        if (threadIdx.x < 64) {  // exclusive scan of the 256 digit totals: 4 per lane, then the lanes
+            const uint32_t a0 = ts[4 * l], a1 = ts[4 * l + 1], a2 = ts[4 * l + 2], a3 = ts[4 * l + 3];
+            const uint32_t sl = a0 + a1 + a2 + a3;
+            uint32_t x = sl;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d, 64);
+                if (l >= d) x += y;
+            }
+            x -= sl;
+            ts[kSortBuckets + 4 * l] = x;
+            ts[kSortBuckets + 4 * l + 1] = x + a0;
+            ts[kSortBuckets + 4 * l + 2] = x + a0 + a1;
+            ts[kSortBuckets + 4 * l + 3] = x + a0 + a1 + a2;
+        }
+        __syncthreads();
+        if (part == 0) run[dg] = ts[kSortBuckets + dg] + pre;
+        __syncthreads();
+    }
+    const int64_t base = (int64_t)blockIdx.x * kSortChunk;
+    for (int r = 0; r < kSortChunk / 1024; ++r) {
+        for (int k = threadIdx.x; k < 16 * kSortBuckets; k += 1024) (&wc[0][0])[k] = 0;
+        __syncthreads();
+        const int64_t e = base + r * 1024 + threadIdx.x;
+        const bool valid = e < n;
+        const uint32_t key = valid ? keys[e] : 0u, dg = (key >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            const bool b = (dg >> bit) & 1u;
+            const uint64_t bb = __ballot(b);
+            peers &= b ? bb : ~bb;
+        }
+        const uint64_t below = peers & ((1ull << l) - 1ull);
+        const uint32_t rank = (uint32_t)__popcll(below);
+        if (valid && below == 0) wc[w][dg] = (uint32_t)__popcll(peers);  // the lowest lane of each digit
+        __syncthreads();
+        if (threadIdx.x < kSortBuckets) {  // waves in order, after the chunk's earlier keys
+            uint32_t x = run[threadIdx.x];
+            for (int q = 0; q < 16; ++q) {
+                const uint32_t c = wc[q][threadIdx.x];
+                wc[q][threadIdx.x] = x;
+                x += c;
+            }
+            run[threadIdx.x] = x;
+        }
+        __syncthreads();
+        if (valid) {
+            const uint32_t pos = wc[w][dg] + rank;
+            okeys[pos] = key;
+            ovals[pos] = vals ? vals[e] : (uint32_t)e;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const uint32_t* keys, const uint32_t* order,
+                           int64_t n, covt_stream_desc* desc) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const uint32_t i = order[k];
@@ -1088,7 +1247,7 @@ __global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const K
     d.num_values = nvals[i];
     d.op = (uint8_t)si.op;
     d.num_bits = (uint8_t)si.num_bits;
-    d.flags = ((uint64_t)keys[k] >> (cb + 5)) == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
+    d.flags = (keys[k] >> kLaunchFamShift) == COVT_FAMILY_LANE ? COVT_DESC_LANE : 0;
     d.byte_length = si.byte_length;
     desc[k] = d;
     si.desc_index = (int32_t)k;
@@ -1467,14 +1626,16 @@ __global__ void fpf_states_walk(const uint8_t* __restrict__ bytes, const covt_st
 // prop_layout / prop_layout_fill the property output slices, a stable radix sort the largest-first
 // materialization order and prop_desc_fill the covt_prop_desc table.
 struct PropSm {  // a property column's stream, as the Gen C walk reads it
-    uint64_t h0, h8;  // localized string columns: hashes of the name and of its bytes from 8 on (names_hash)
+    uint32_t h0, h8;  // localized string columns: hashes of the name and of its bytes from 8 on (names_hash)
     int32_t noff, nlen, nv, bl;
     int32_t off;      // layer-data-relative
     uint16_t enc, role;  // role: PR_* bits of the name, classified while the window holds it
 };
 enum { PR_PRESENT = 1, PR_DATA = 2, PR_LENGTH = 4, PR_DICTIONARY = 8, PR_PRESENT_LANG = 16 };
 constexpr int kPropMaxStreams = 256;  // numStreams bound of the walk (walk_genc: > 256 is BAD_HEADER)
-constexpr size_t kPropWalkLds = 512 + kPropMaxStreams * sizeof(PropSm);  // Rd window + stream table
+// LDS: Rd<true>'s window, the fast walk's window and tables (walk_count's layout), then the stream table
+constexpr size_t kPropTabOffset = (kFastSmemOffset + sizeof(FastSmem) + 15) & ~(size_t)15;
+constexpr size_t kPropWalkLds = kPropTabOffset + kPropMaxStreams * sizeof(PropSm);
 
 // bytes [a, a + n) == bytes [b, b + n) of the tile (names; uniform)
 __device__ __forceinline__ bool names_equal(Rd<true>& r, int32_t a, int32_t b, int32_t n) {
@@ -1489,7 +1650,7 @@ __device__ __forceinline__ bool names_equal(Rd<true>& r, int32_t a, int32_t b, i
 // the localized columns' name matching below compares hashes and confirms a match with names_equal --
 // one window refill per match instead of a refill per byte compared (two names of a long column lie
 // further apart than the window, and the all-pairs compare ping-ponged between them: ~9 ms per walk)
-__device__ __forceinline__ uint64_t names_hash(Rd<true>& r, int32_t a, int32_t n) {
+__device__ __forceinline__ uint32_t names_hash(Rd<true>& r, int32_t a, int32_t n) {
     uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)(uint32_t)n;
     for (int32_t i = 0; i < n; i += 8) {
         const int32_t k = n - i < 8 ? n - i : 8;
@@ -1497,7 +1658,7 @@ __device__ __forceinline__ uint64_t names_hash(Rd<true>& r, int32_t a, int32_t n
         h = (h ^ (r.peek8(a + i) & m)) * 0xff51afd7ed558ccdull;
         h ^= h >> 29;
     }
-    return h;
+    return (uint32_t)(h ^ (h >> 32));
 }
 
 // Gen C property records (walk_genc's props branch): a column's streams in metadata order, roles by
@@ -1544,7 +1705,7 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
                     if (COVT_IS(sname, sn, "data")) role |= PR_DATA;
                     if (COVT_IS(sname, sn, "length")) role |= PR_LENGTH;
                     if (COVT_IS(sname, sn, "dictionary")) role |= PR_DICTIONARY;
-                    uint64_t h0 = 0, h8 = 0;
+                    uint32_t h0 = 0, h8 = 0;
                     if (localized) {
                         if (sn > 8 && r.peek8(sname) == pk("present_", 0, 8)) {
                             role |= PR_PRESENT_LANG;
@@ -1568,41 +1729,7 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
             p.type = genc_prop_type(dtype);
             p.ctype = ctype;
             if (localized) {
-                int ls = -1, ds = -1;
-                for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
-                    const uint32_t role = tab[q].role;
-                    if (role & PR_LENGTH) ls = (int)q;
-                    else if (role & PR_DICTIONARY) ds = (int)q;
-                }
-                int32_t lang = 0;
-                for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
-                    const PropSm sm = tab[q];
-                    if (!(sm.role & PR_PRESENT_LANG)) continue;
-                    const int32_t ll = sm.nlen - 8;
-                    // the last stream named <lang>: 64 candidates per step, hash matches confirmed from the
-                    // highest down (a serial all-pairs scan was ~ns^2 dependent LDS reads: ms per tile)
-                    int dd = -1;
-                    for (int32_t k0 = ((int32_t)ns - 1) & ~63; k0 >= 0 && dd < 0; k0 -= 64) {
-                        const int32_t k = k0 + (int32_t)threadIdx.x;
-                        const bool m = k < (int32_t)ns && tab[k].nlen == ll && tab[k].h0 == sm.h8;
-                        uint64_t bal = __ballot(m);
-                        while (bal && dd < 0) {
-                            const int hi = 63 - __builtin_clzll(bal);
-                            const int32_t kk = k0 + hi;
-                            if (names_equal(r, tab[kk].noff, sm.noff + 8, ll)) dd = kk;
-                            bal &= ~(1ull << hi);
-                        }
-                    }
-                    PropRaw x = p;
-                    x.lang = lang++;
-                    x.lang_off = sm.noff + 8;
-                    x.lang_len = ll;
-                    prop_stream(x, 0, sm.off, sm.nv, sm.bl, sm.enc);
-                    if (dd >= 0) prop_stream(x, 1, tab[dd].off, tab[dd].nv, tab[dd].bl, tab[dd].enc);
-                    if (ls >= 0) prop_stream(x, 2, tab[ls].off, tab[ls].nv, tab[ls].bl, tab[ls].enc);
-                    if (ds >= 0) prop_stream(x, 3, tab[ds].off, tab[ds].nv, tab[ds].bl, tab[ds].enc);
-                    pe(x);
-                }
+                prop_localized(r, pe, tab, ns, p);
             } else {
                 for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
                     const PropSm sm = tab[q];
@@ -1620,6 +1747,145 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
         o += (int32_t)d;
     }
     return o == len ? COVT_OK : COVT_ERR_BAD_HEADER;
+}
+
+// names_hash over window bytes (the fast walk's copy of the tile; q + n within the look-ahead)
+__device__ __forceinline__ uint32_t names_hash_win(const FastGenc& f, int32_t q, int32_t n) {
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)(uint32_t)n;
+    for (int32_t i = 0; i < n; i += 8) {
+        const int32_t k = n - i < 8 ? n - i : 8;
+        const uint64_t m = k >= 8 ? ~0ull : ((1ull << (8 * k)) - 1);
+        h = (h ^ (f.upeek8(q + i) & m)) * 0xff51afd7ed558ccdull;
+        h ^= h >> 29;
+    }
+    return (uint32_t)(h ^ (h >> 32));
+}
+
+// The localized sub-columns of a Gen C string column from its stream table (prop_walk_genc's rule): one
+// per present_<lang> stream, with the last stream named <lang> as data and the last length / dictionary
+template <class PE>
+__device__ __forceinline__ void prop_localized(Rd<true>& r, PE& pe, const PropSm* tab, uint32_t ns, const PropRaw& p) {
+    int ls = -1, ds = -1;
+    for (uint32_t q = 0; q < ns; ++q) {
+        const uint32_t role = tab[q].role;
+        if (role & PR_LENGTH) ls = (int)q;
+        else if (role & PR_DICTIONARY) ds = (int)q;
+    }
+    int32_t lang = 0;
+    for (uint32_t q = 0; q < ns; ++q) {
+        const PropSm sm = tab[q];
+        if (!(sm.role & PR_PRESENT_LANG)) continue;
+        const int32_t ll = sm.nlen - 8;
+        // the last stream named <lang>: 64 candidates per step, hash matches confirmed from the highest
+        // down (a serial all-pairs scan was ~ns^2 dependent LDS reads: ms per tile)
+        int dd = -1;
+        for (int32_t k0 = ((int32_t)ns - 1) & ~63; k0 >= 0 && dd < 0; k0 -= 64) {
+            const int32_t k = k0 + (int32_t)threadIdx.x;
+            const bool m = k < (int32_t)ns && tab[k].nlen == ll && tab[k].h0 == sm.h8;
+            uint64_t bal = __ballot(m);
+            while (bal && dd < 0) {
+                const int hi = 63 - __builtin_clzll(bal);
+                const int32_t kk = k0 + hi;
+                if (names_equal(r, tab[kk].noff, sm.noff + 8, ll)) dd = kk;
+                bal &= ~(1ull << hi);
+            }
+        }
+        PropRaw x = p;
+        x.lang = lang++;
+        x.lang_off = sm.noff + 8;
+        x.lang_len = ll;
+        prop_stream(x, 0, sm.off, sm.nv, sm.bl, sm.enc);
+        if (dd >= 0) prop_stream(x, 1, tab[dd].off, tab[dd].nv, tab[dd].bl, tab[dd].enc);
+        if (ls >= 0) prop_stream(x, 2, tab[ls].off, tab[ls].nv, tab[ls].bl, tab[ls].enc);
+        if (ds >= 0) prop_stream(x, 3, tab[ds].off, tab[ds].nv, tab[ds].bl, tab[ds].enc);
+        pe(x);
+    }
+}
+
+// prop_walk_genc on walk_count's speculative tables (FastGenc): a column header and a stream record are
+// one LDS read each, and a stream's name, numValues and encoding are parsed only in property columns.
+// kFastFallback when the tile leaves the fast grammar (the caller walks it with prop_walk_genc); a
+// successful fast walk emits the same records.
+template <class PE>
+__device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropSm* tab) {
+    const int32_t len = f.len;
+    int32_t o = 0;
+    uint32_t version, nlayers;
+    if (!f.uv4(o, version) || !f.uv4(o, nlayers) || version != 1) return kFastFallback;
+    for (uint32_t L = 0; L < nlayers; ++L) {
+        uint32_t nlen, extent, nfeat, ncols;
+        if (!f.uv4(o, nlen) || nlen > (uint32_t)(len - o)) return kFastFallback;
+        o += (int32_t)nlen;
+        if (!f.uv4(o, extent) || !f.uv4(o, nfeat) || !f.uv4(o, ncols) || ncols > 4096) return kFastFallback;
+        int64_t d = 0;
+        pe.layer_begin();
+        for (uint32_t c = 0; c < ncols; ++c) {
+            const int32_t qc = f.at(o);
+            const uint32_t ce = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->ctab[qc]);
+            if (!ce) return kFastFallback;
+            const uint32_t ns = (ce >> 8) & 0x1ffu, kind = (ce >> 17) & 3u;
+            if (kind != 2) {  // Id / Geometry: only their data bytes
+                o += (int32_t)(ce & 0xffu);
+                for (uint32_t s = 0; s < ns; ++s) {
+                    const uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[f.at(o)]);
+                    if (!se) return kFastFallback;
+                    d += (int32_t)(se >> 8);
+                    o += (int32_t)(se & 0xffu);
+                }
+                continue;
+            }
+            const uint64_t hw = f.upeek8(qc);
+            const int32_t n = (int32_t)(hw & 0xffu);  // the name's length (one LEB128 byte)
+            const int dtype = (int)(f.upeek8(qc + 1 + n) & 0xffu);
+            const int ctype = (int)(ce >> 19) & 0xff;
+            PropRaw p = prop_init((int32_t)L, (int32_t)c, (int32_t)nfeat);
+            p.name_off = o + 1;
+            p.name_len = n;
+            p.type = genc_prop_type(dtype);
+            p.ctype = ctype;
+            const bool localized = p.type == COVT_PROP_STRING && ctype == 2;
+            o += (int32_t)(ce & 0xffu);
+            for (uint32_t s = 0; s < ns; ++s) {
+                const int32_t q = f.at(o);
+                const uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[q]);
+                if (!se) return kFastFallback;
+                int type, enc;
+                int32_t nv;
+                f.rec(q, se, type, nv, enc);
+                const int32_t bl = (int32_t)(se >> 8);
+                const uint32_t role = type >= ST_PRESENT && type <= ST_DICTIONARY ? 1u << type : 0u;
+                if (localized) {
+                    const int32_t sn = (int32_t)(f.upeek8(q) & 0xffu);
+                    uint32_t rl = role;
+                    uint32_t h8 = 0;
+                    if (sn > 8 && f.upeek8(q + 1) == pk("present_", 0, 8)) {
+                        rl |= PR_PRESENT_LANG;
+                        h8 = names_hash_win(f, q + 9, sn - 8);
+                    }
+                    const uint32_t h0 = names_hash_win(f, q + 1, sn);
+                    if (threadIdx.x == 0)
+                        tab[s] = PropSm{h0, h8, o + 1, sn, nv, bl, (int32_t)d, (uint16_t)enc, (uint16_t)rl};
+                } else {  // the roles applied in metadata order (the last stream of a role wins)
+                    if (role) prop_stream(p, type, d, nv, bl, enc);
+                }
+                d += bl;
+                o += (int32_t)(se & 0xffu);
+            }
+            if (localized) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                prop_localized(r, pe, tab, ns, p);
+                __builtin_amdgcn_wave_barrier();  // the table is rewritten by the next column
+            } else {
+                pe(p);
+            }
+        }
+        if (d > (int64_t)(len - o)) return kFastFallback;
+        pe.layer_end(o);
+        o += (int32_t)d;
+    }
+    return o == len ? COVT_OK : kFastFallback;
 }
 
 // Gen D property records (walk_gend's props branch): the implicit present stream, then data / length /
@@ -1762,6 +2028,23 @@ struct PropRecEmit {
     }
 };
 
+// a tile's property records: Gen C through the fast walk first (the serial walk on a fallback)
+template <class PE>
+__device__ __forceinline__ int prop_walk_tile(Rd<true>& r, PE& e, PropSm* tab, int32_t format) {
+    if (format != COVT_FORMAT_GENC) return prop_walk_gend(r, e);
+    FastGenc f;
+    f.t = r.t;
+    f.len = (int32_t)r.len;
+    f.wb = -(int32_t)0x40000000;
+    f.segs = 0;
+    f.fs = (FastSmem*)((uint8_t*)covt_walk_win + kFastSmemOffset);
+    const PE fresh = e;
+    const int st = prop_walk_genc_fast(f, r, e, tab);
+    if (st != kFastFallback) return st;
+    e = fresh;
+    return prop_walk_genc(r, e, tab);
+}
+
 // one wave per tile (tiles the Id / Geometry walk failed contribute nothing); EMIT: write the records
 template <bool EMIT>
 __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
@@ -1778,13 +2061,13 @@ __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
     r.t = bytes + offs[t];
     r.len = (int64_t)sizes[t];
     r.wo = -(int64_t)0x40000000;
-    PropSm* tab = (PropSm*)((uint8_t*)covt_walk_win + 512);
+    PropSm* tab = (PropSm*)((uint8_t*)covt_walk_win + kPropTabOffset);
     if (EMIT) {
         PropRecEmit e{recs + pcb[t], rtile + pcb[t], t};
-        (void)(format == COVT_FORMAT_GENC ? prop_walk_genc(r, e, tab) : prop_walk_gend(r, e));
+        (void)prop_walk_tile(r, e, tab, format);
     } else {
         PropCountEmit e;
-        const int st = format == COVT_FORMAT_GENC ? prop_walk_genc(r, e, tab) : prop_walk_gend(r, e);
+        const int st = prop_walk_tile(r, e, tab, format);
         if (threadIdx.x == 0) pcnt[t] = st ? 0 : e.n;  // (the Id / Geometry walk succeeded: so does this one)
     }
 }
@@ -2117,7 +2400,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     const int wl = o.device_walk >= 2 ? o.device_walk : 0;
     const bool use_slots = o.device_walk == 0;
     const size_t tile_bytes = o_slots + (use_slots ? up256((size_t)n_tiles * kSlots * sizeof(RawStream)) : 0);
-    DCHK(hipMalloc(&p->tile_arena, tile_bytes));
+    DCHK(plan_malloc(&p->tile_arena, tile_bytes, p->dev, s));
     uint8_t* ta = (uint8_t*)p->tile_arena;
     p->d_status = (int32_t*)ta;
     int64_t *cnt = (int64_t*)(ta + o_cnt), *ob = (int64_t*)(ta + o_ob), *cb = (int64_t*)(ta + o_cb),
@@ -2186,7 +2469,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         po_st = po_pd + up256(nr * sizeof(covt_prop_desc));
         po_sc = po_st + up256(psort_tmp);
         prop_total = po_sc + up256(pscan_tmp);
-        DCHK(hipMalloc(&p->prop_arena, prop_total));
+        DCHK(plan_malloc(&p->prop_arena, prop_total, p->dev, s));
         uint8_t* pa = (uint8_t*)p->prop_arena;
         recs = (PropRaw*)pa;
         rtile = (int32_t*)(pa + po_rt);
@@ -2229,42 +2512,43 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     int64_t smin = o.split_min;
     if (smin >= 0 && o.split_ratio > 0) smin = std::max<int64_t>(smin, hd[2] / o.split_ratio);
     const bool splitting = smin >= 0 && ns > 0 && hd[3] > smin;
-    // stream arena: info | nvals | keys in/out | vals in/out | descs | sort scratch [| split: family | desc
-    // counts | offsets | RLE list | FastPFOR list | scan scratch]
-    // sort keys: cost bits kcb (every stream's cost <= the largest split cost hd[3] < 2^kcb; 48 as the
-    // host plan's key at most), 32-bit keys when cb + 8 bits fit
-    int kcb = 1;
-    while (kcb < 48 && (hd[3] >> kcb) != 0) ++kcb;
-    const bool k32 = kcb + 8 <= 32;
-    const int kbits = kcb + 8;
-    size_t sort_tmp = 0, dscan_tmp = 0;
-    if (k32)
-        DCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ns, 0, kbits, s));
-    else
-        DCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint64_t*)nullptr, (uint64_t*)nullptr,
-                                                (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ns, 0, kbits, s));
+    // stream arena: info | nvals | launch buckets | sorted buckets | launch order | bucket counts | descs [|
+    // split: family | desc counts | offsets | RLE list | FastPFOR list | scan scratch]
+    size_t dscan_tmp = 0;
     if (splitting)
         DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, dscan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)(ns + 1), s));
     const size_t n = (size_t)(ns > 0 ? ns : 1);
+    const int32_t nb = (int32_t)((n + kSortChunk - 1) / kSortChunk);  // counting-sort chunks
     // RLE chunk records: every candidate reserves (its cost / split_chunk + 2) <= the batch's
     const int64_t chunk_cap = splitting ? hd[2] / o.split_chunk + 2 * ns + 2 : 0;
-    const size_t o_nv = up256(n * sizeof(covt_stream_info)), o_k0 = o_nv + up256(n * 4), o_k1 = o_k0 + up256(n * 8),
-                 o_v0 = o_k1 + up256(n * 8), o_v1 = o_v0 + up256(n * 4), o_d = o_v1 + up256(n * 4),
-                 o_st = o_d + up256(n * sizeof(covt_stream_desc)), o_sf = o_st + up256(sort_tmp),
+    const size_t o_nv = up256(n * sizeof(covt_stream_info)), o_k0 = o_nv + up256(n * 4), o_k1 = o_k0 + up256(n * 4),
+                 o_v0 = o_k1 + up256(n * 4), o_v1 = o_v0 + up256(n * 4), o_h = o_v1 + up256(n * 4),
+                 o_d = o_h + up256((size_t)kSortBuckets * nb * 4),
+                 o_sf = o_d + up256(n * sizeof(covt_stream_desc)),
                  o_sn = o_sf + up256(n), o_dn = o_sn + up256(n * 8), o_dp = o_dn + up256((n + 1) * 8),
                  o_rl = o_dp + up256((n + 1) * 8), o_fl = o_rl + up256(n * 4), o_rb = o_fl + up256(n * 4),
                  o_rc = o_rb + up256(n * 8), o_ch = o_rc + up256(n * 4), o_ds = o_ch + up256((size_t)chunk_cap * 16),
                  stream_bytes = splitting ? o_ds + up256(dscan_tmp) : o_sf;
-    DCHK(hipMalloc(&p->stream_arena, stream_bytes));
+    DCHK(plan_malloc(&p->stream_arena, stream_bytes, p->dev, s));
     uint8_t* sa = (uint8_t*)p->stream_arena;
     p->d_info = (covt_stream_info*)sa;
     int32_t* nvals = (int32_t*)(sa + o_nv);
-    uint64_t *k0 = (uint64_t*)(sa + o_k0), *k1 = (uint64_t*)(sa + o_k1);
-    uint32_t *q0 = (uint32_t*)k0, *q1 = (uint32_t*)k1;  // (32-bit keys)
-    uint32_t *v0 = (uint32_t*)(sa + o_v0), *v1 = (uint32_t*)(sa + o_v1);
+    uint32_t *q0 = (uint32_t*)(sa + o_k0), *q1 = (uint32_t*)(sa + o_k1), *v0 = (uint32_t*)(sa + o_v0),
+             *v1 = (uint32_t*)(sa + o_v1);
+    uint32_t* bhist = (uint32_t*)(sa + o_h);
     p->d_order = v1;
     p->d_desc = (covt_stream_desc*)(sa + o_d);
+    // launch order: the stable radix sort of the launch keys q0 (low byte: -> q1, v0; high byte: -> q0, v1)
+    auto launch_order = [&]() {
+        const int scanned = nb > kSortFuseChunks;
+        for (int pass = 0; pass < 2; ++pass) {
+            order_hist<<<nb, 256, 0, s>>>(pass ? q1 : q0, ns, nb, 8 * pass, bhist);
+            if (scanned) order_scan<<<1, 1024, 0, s>>>(bhist, (int64_t)kSortBuckets * nb);
+            if (pass == 0) order_scatter<<<nb, 1024, 0, s>>>(q0, nullptr, ns, nb, 0, bhist, scanned, q1, v0);
+            else order_scatter<<<nb, 1024, 0, s>>>(q1, v0, ns, nb, 8, bhist, scanned, q0, v1);
+        }
+        return hipGetLastError();
+    };
     const int32_t lane_max = lane_limits(o.lane_max_bytes, o.lane_max_values);
     const int64_t lane_min = o.lane_min_streams;
     if (n_tiles) {
@@ -2294,19 +2578,10 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     }
     const int blocks_s = (int)((ns + 255) / 256);
     if (ns > 0 && !splitting) {
-        if (k32) {
-            stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, q0, v0, nullptr,
-                                                 nullptr, kcb);
-            DCHK(hipGetLastError());
-            DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, q0, q1, v0, v1, (int)ns, 0, kbits, s));
-            fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, q1, v1, ns, kcb, p->d_desc);
-        } else {
-            stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, k0, v0, nullptr,
-                                                 nullptr, kcb);
-            DCHK(hipGetLastError());
-            DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, k0, k1, v0, v1, (int)ns, 0, kbits, s));
-            fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, k1, v1, ns, kcb, p->d_desc);
-        }
+        stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, q0, nullptr, nullptr);
+        DCHK(hipGetLastError());
+        DCHK(launch_order());
+        fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, q0, v1, ns, p->d_desc);
         DCHK(hipGetLastError());
     } else if (splitting) {
         auto* sfam = (uint8_t*)(sa + o_sf);
@@ -2322,15 +2597,9 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         rle_chunks_walk<<<walkers, 64, kStreamRdLds, s>>>(d_bytes, p->d_info, nvals, totals, rle_list, o.split_chunk, sfam,
                                                  sndesc, chunks, chunk_cap, rle_base, rle_cons);
         DCHK(hipGetLastError());
-        if (k32) {
-            stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, q0, v0, sfam, sndesc, kcb);
-            DCHK(hipGetLastError());
-            DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, q0, q1, v0, v1, (int)ns, 0, kbits, s));
-        } else {
-            stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, k0, v0, sfam, sndesc, kcb);
-            DCHK(hipGetLastError());
-            DCHK(hipcub::DeviceRadixSort::SortPairs(sa + o_st, sort_tmp, k0, k1, v0, v1, (int)ns, 0, kbits, s));
-        }
+        stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, q0, sfam, sndesc);
+        DCHK(hipGetLastError());
+        DCHK(launch_order());
         gather_ndesc<<<(int)((ns + 256) / 256), 256, 0, s>>>(v1, sndesc, ns, dn);
         DCHK(hipGetLastError());
         DCHK(hipcub::DeviceScan::ExclusiveSum(sa + o_ds, dscan_tmp, dn, dpos, (int)(ns + 1), s));
@@ -2338,7 +2607,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         DCHK(hipMemcpyAsync(&nd, dpos + ns, 8, hipMemcpyDeviceToHost, s));
         DCHK(hipStreamSynchronize(s));
         // descriptor arena: descriptors | the stream of each
-        DCHK(hipMalloc(&p->desc_arena, up256((size_t)nd * sizeof(covt_stream_desc)) + up256((size_t)nd * 4)));
+        DCHK(plan_malloc(&p->desc_arena, up256((size_t)nd * sizeof(covt_stream_desc)) + up256((size_t)nd * 4), p->dev, s));
         p->n_descs = nd;
         p->d_desc = (covt_stream_desc*)p->desc_arena;
         p->d_order = (uint32_t*)((uint8_t*)p->desc_arena + up256((size_t)nd * sizeof(covt_stream_desc)));
@@ -2386,11 +2655,11 @@ void covt_device_plan_destroy(covt_device_plan* p) {
     if (!p) return;
     int cur = 0;
     const bool sw = hipGetDevice(&cur) == hipSuccess && cur != p->dev && hipSetDevice(p->dev) == hipSuccess;
-    if (p->tile_arena) (void)hipFree(p->tile_arena);
-    if (p->stream_arena) (void)hipFree(p->stream_arena);
-    if (p->desc_arena) (void)hipFree(p->desc_arena);
-    if (p->geo_arena) (void)hipFree(p->geo_arena);
-    if (p->prop_arena) (void)hipFree(p->prop_arena);
+    // (hipFree's implicit device synchronization, then the arenas back to the pool)
+    (void)hipDeviceSynchronize();
+    for (void* q : {p->tile_arena, p->stream_arena, p->desc_arena, p->geo_arena, p->prop_arena})
+        if (q) (void)hipFreeAsync(q, nullptr);
+    (void)hipStreamSynchronize(nullptr);
     if (sw) (void)hipSetDevice(cur);
     delete p;
 }
@@ -2450,11 +2719,12 @@ int covt_device_plan_geometry(covt_device_plan* p, void* hip_stream) {
     // stage 1 arena: column starts | their indices | scan scratch
     void* tmp = nullptr;
     const size_t o_gp = up256(n1 * 8), o_t = o_gp + up256(n1 * 8);
-    if (hipMalloc(&tmp, o_t + up256(scan_tmp)) != hipSuccess) return COVT_ERR_DEVICE;
-    struct Free {
+    if (plan_malloc(&tmp, o_t + up256(scan_tmp), p->dev, s) != hipSuccess) return COVT_ERR_DEVICE;
+    struct Free {  // stream-ordered: after the work on s that uses it
         void* q;
-        ~Free() { if (q) (void)hipFree(q); }
-    } free_tmp{tmp};
+        hipStream_t s;
+        ~Free() { if (q) (void)hipFreeAsync(q, s); }
+    } free_tmp{tmp, s};
     int64_t *gst = (int64_t*)tmp, *gpos = (int64_t*)((uint8_t*)tmp + o_gp);
     const int blocks = (int)((n1 + 255) / 256);
     geom_mark<<<blocks, 256, 0, s>>>(p->d_info, ns, gst);
@@ -2477,8 +2747,8 @@ int covt_device_plan_geometry(covt_device_plan* p, void* hip_stream) {
                  o_cs = o_st + up256(sort_tmp), total = o_cs + up256(cscan_tmp);
     // the arena is the plan's only on success: a failed build frees it (a retry allocates afresh)
     void* arena = nullptr;
-    if (hipMalloc(&arena, total) != hipSuccess) return COVT_ERR_DEVICE;
-    Free free_arena{arena};
+    if (plan_malloc(&arena, total, p->dev, s) != hipSuccess) return COVT_ERR_DEVICE;
+    Free free_arena{arena, s};
     uint8_t* g = (uint8_t*)arena;
     p->d_ginfo = (covt_geom_info*)g;
     p->d_gdesc = (covt_geom_desc*)(g + o_gd);
@@ -2503,7 +2773,7 @@ int covt_device_plan_geometry(covt_device_plan* p, void* hip_stream) {
             hipStreamSynchronize(s) != hipSuccess)
             return COVT_ERR_DEVICE;
     }
-    if (p->geo_arena) (void)hipFree(p->geo_arena);
+    if (p->geo_arena) (void)hipFreeAsync(p->geo_arena, s);
     p->geo_arena = arena;
     free_arena.q = nullptr;
     p->n_geo = nc;

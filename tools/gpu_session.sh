@@ -78,6 +78,7 @@ for s in "$@"; do
     dplan_props_small) step dplan_props_small 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_props_small -o run --output-format csv -- python tools/device_plan_prof.py 5 --small --props ;;
     dplan_sq1) step dplan_sq1 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/dplan_sq1 -o run --output-format csv -- python tools/device_plan_prof.py 2 --props ;;
     dplan_sq2) step dplan_sq2 300 rocprofv3 --pmc SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_BRANCH GRBM_GUI_ACTIVE -d gpurun_out/dplan_sq2 -o run --output-format csv -- python tools/device_plan_prof.py 2 --props ;;
+    dplan_api) step dplan_api 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_api -o run --output-format csv -- python tools/device_plan_prof.py 5 ;;
     dplan_prof_256) step dplan_prof_256 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_prof_256 -o run --output-format csv -- python tools/device_plan_prof.py 5 --n256 ;;
     dplan_api_small) step dplan_api_small 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_api_small -o run --output-format csv -- python tools/device_plan_prof.py 20 --small --nosplit ;;
     dplan_sq_small) step dplan_sq_small 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_BRANCH -d gpurun_out/dplan_sq_small -o run --output-format csv -- python tools/device_plan_prof.py 3 --small --nosplit ;;
