@@ -518,6 +518,16 @@ __device__ __forceinline__ int walk_gend_dev(Rd<kWave>& r, E& emit) {
 
 __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
+// a stream's launch key (launch_key, covt_internal.h) as its entry is written; lm: the batch's lane limits
+// (lane_limits, or -1 when the batch has fewer lane streams than lane_min: totals[T_LANE] is known before
+// the entries are written -- walk_count counts them)
+__device__ __forceinline__ uint32_t entry_key(int32_t op, int32_t nv, int32_t bl, int64_t out_elems, int32_t elem,
+                                              int32_t lm) {
+    const bool lane = lane_stream(op, nv, bl, lm);
+    const uint32_t fam = lane ? (uint32_t)COVT_FAMILY_LANE : (uint32_t)covt_op_family(op);
+    return launch_key(fam, lane, op, (int64_t)bl + out_elems * elem / 4);
+}
+
 // ---- speculative Gen C walk (one wave per tile) -------------------------------------------------------
 // The serial walk spends ~90 scalar instructions per metadata varint (~75k per tile: 2.2 ms for the 10k-
 // tile bench batch, profiles/r02).  Most of a Gen C tile's metadata is a chain of records of two shapes:
@@ -804,6 +814,7 @@ struct CountEmit {
     bool writer = true, wave = false;
     int64_t n = 0, out = 0, k0 = 0;
     int64_t fpf_w = 1, cost = 0, cmax = 0;  // the split rule's cost: sum, and the largest split cost
+
     __device__ void operator()(const RawStream& s) {
         int op, elem;
         int64_t nvals, oe;
@@ -906,7 +917,8 @@ struct InfoEmit {
     covt_stream_info* info;
     int32_t* nvals;
     int64_t k, out, in_bytes = 0, payload = 0, verts = 0, lane = 0, k0 = 0;
-    int32_t lane_max;
+    int32_t lane_max, lm = -1;
+    uint32_t* keys = nullptr;
     bool writer, wave;
     __device__ void layer_begin() { k0 = k; }
     __device__ void layer_end(int64_t data_start) {  // rebase the layer's data offsets (this lane's own stores)
@@ -947,6 +959,7 @@ struct InfoEmit {
         if (writer) {
             info[k] = si;
             nvals[k] = (int32_t)nv;
+            if (keys) keys[k] = entry_key(op, (int32_t)nv, s.bl, si.out_elems, elem, lm);
         }
         ++k;
     }
@@ -958,12 +971,14 @@ __global__ void walk_emit(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
                           const int32_t* __restrict__ status, const int64_t* __restrict__ cnt_base,
                           const int64_t* __restrict__ ob_base, int32_t lane_max, covt_stream_info* __restrict__ info,
                           int32_t* __restrict__ nvals, long long* __restrict__ tsum,
-                          const int64_t* __restrict__ cnt) {
+                          const int64_t* __restrict__ cnt, uint32_t* __restrict__ keys, int32_t lm) {
     const int32_t t = kWave ? (int32_t)blockIdx.x : (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t >= n_tiles || status[t]) return;
     if (cnt && cnt[t] <= kSlots) return;  // emit_slots has this tile's records
     InfoEmit e{t, id_mode, (int64_t)offs[t], info, nvals, cnt_base[t], ob_base[t]};
     e.lane_max = lane_max;
+    e.lm = lm;
+    e.keys = keys;
     e.writer = !kWave || threadIdx.x == 0;
     e.wave = kWave;
     walk_tile<kWave>(bytes, n_bytes, offs[t], sizes[t], format, e);
@@ -977,7 +992,8 @@ __global__ void emit_slots(const uint64_t* __restrict__ offs, int32_t n_tiles, i
                            const int32_t* __restrict__ status, const int64_t* __restrict__ cnt,
                            const int64_t* __restrict__ cnt_base, const int64_t* __restrict__ ob_base,
                            const RawStream* __restrict__ slots, int32_t lane_max, covt_stream_info* __restrict__ info,
-                           int32_t* __restrict__ nvals, long long* __restrict__ tsum) {
+                           int32_t* __restrict__ nvals, long long* __restrict__ tsum, uint32_t* __restrict__ keys,
+                           int32_t lm) {
     const int32_t t = blockIdx.x;
     if (t >= n_tiles || status[t]) return;
     const int64_t n = cnt[t];
@@ -1023,6 +1039,7 @@ __global__ void emit_slots(const uint64_t* __restrict__ offs, int32_t n_tiles, i
             si.out_off = out + (incl - size);
             info[base + j] = si;
             nvals[base + j] = (int32_t)nv;
+            if (keys) keys[base + j] = entry_key(op, (int32_t)nv, s.bl, out_elems, elem, lm);
             in_bytes += s.bl;
             payload += out_elems * elem;
             if (s.kind == 1 && s.type == ST_VERTEX_BUFFER)
@@ -1071,13 +1088,10 @@ __global__ void __launch_bounds__(1024) reduce_tiles(const long long* __restrict
     }
 }
 
-// launch-order key of covt_plan_create_ex step 3: family, lane op, cost descending
-// (split plans: the family and descriptor count of each stream from split_mark / rle_chunks_walk).
-// Packed into cb + 8 bits (family << (cb + 5) | lane op << cb | 2^cb - 1 - cost) where every stream's
-// cost is below 2^cb: the host plan's order exactly (its 64-bit key orders the same fields the same
-// way), in 32-bit keys and cb + 8 sort bits when they fit (the bench batch: 26 bits, 4 radix passes
-// instead of 8 over 64-bit keys)
-static_assert(COVT_OP_COUNT <= 32, "the lane op takes 5 key bits");
+// Launch keys of a split plan (covt_plan_create_ex step 3): the family and descriptor count of each stream
+// from split_mark / rle_chunks_walk.  (Unsplit plans write the keys with the stream entries and count the
+// families in the sort.)
+static_assert(COVT_NUM_FAMILIES <= 8 && kLaunchFamShift == 13, "launch keys: 16 bits, two radix passes");
 __global__ void stream_keys(const covt_stream_info* info, const int32_t* nvals, int64_t n, int32_t lane_max,
                             int64_t lane_min, unsigned long long* totals, uint32_t* keys, const uint8_t* sfam,
                             const int64_t* sndesc) {
@@ -1105,6 +1119,18 @@ __global__ void stream_keys(const covt_stream_info* info, const int32_t* nvals, 
     __syncthreads();
     if (threadIdx.x < COVT_NUM_FAMILIES && fam_n[threadIdx.x])
         atomicAdd(&totals[T_FAM + threadIdx.x], fam_n[threadIdx.x]);
+}
+
+// An unsplit plan whose batch has fewer lane streams than lane_min: its keys again without the lane family
+// (the entries were keyed with it; nothing to do otherwise -- every workgroup returns at once)
+__global__ void __launch_bounds__(256) lane_keys(const covt_stream_info* __restrict__ info, const int32_t* __restrict__ nvals,
+                                                 int64_t n, int64_t lane_min, const unsigned long long* __restrict__ totals,
+                                                 uint32_t* __restrict__ keys) {
+    if ((int64_t)totals[T_LANE] >= lane_min) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const covt_stream_info& si = info[i];
+        keys[i] = entry_key(si.op, nvals[i], si.byte_length, si.out_elems, si.elem_bytes, -1);
+    }
 }
 
 // ---- launch order: a stable LSD radix sort of the streams' 16-bit launch keys, two 8-bit passes of
@@ -1154,12 +1180,21 @@ __global__ void __launch_bounds__(1024) order_scan(uint32_t* __restrict__ a, int
 constexpr int kSortFuseChunks = 512;
 __global__ void __launch_bounds__(1024) order_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                       int64_t n, int32_t nb, int shift, const uint32_t* __restrict__ gpos,
-                                                      int scanned, uint32_t* __restrict__ okeys, uint32_t* __restrict__ ovals) {
+                                                      int scanned, uint32_t* __restrict__ okeys, uint32_t* __restrict__ ovals,
+                                                      unsigned long long* __restrict__ ftot) {
     __shared__ uint32_t run[kSortBuckets];
     __shared__ uint32_t wc[16][kSortBuckets];
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    // ftot (the high-byte pass of the launch keys): workgroup 0 writes the streams per family (a family is
+    // 2^(kLaunchFamShift - 8) consecutive digits)
+    constexpr int kFamDigits = 1 << (kLaunchFamShift - 8);
     if (scanned) {
         if (threadIdx.x < kSortBuckets) run[threadIdx.x] = gpos[(size_t)threadIdx.x * nb + blockIdx.x];
+        if (ftot && blockIdx.x == 0 && threadIdx.x < COVT_NUM_FAMILIES) {
+            const int d0 = threadIdx.x * kFamDigits, d1 = d0 + kFamDigits;
+            const uint32_t end = d1 < kSortBuckets ? gpos[(size_t)d1 * nb] : (uint32_t)n;
+            ftot[threadIdx.x] = end - gpos[(size_t)d0 * nb];
+        }
     } else {
         // digit totals and the counts of the chunks before this one (4 threads per digit)
         const int dg = threadIdx.x >> 2, part = threadIdx.x & 3;
@@ -1195,6 +1230,11 @@ __global__ void __launch_bounds__(1024) order_scatter(const uint32_t* __restrict
         }
         __syncthreads();
         if (part == 0) run[dg] = ts[kSortBuckets + dg] + pre;
+        if (ftot && blockIdx.x == 0 && threadIdx.x < COVT_NUM_FAMILIES) {
+            unsigned long long f = 0;
+            for (int q = 0; q < kFamDigits; ++q) f += ts[threadIdx.x * kFamDigits + q];
+            ftot[threadIdx.x] = f;
+        }
         __syncthreads();
     }
     const int64_t base = (int64_t)blockIdx.x * kSortChunk;
@@ -2145,7 +2185,8 @@ __global__ void prop_fill(const PropRaw* __restrict__ recs, const int32_t* __res
                           const int64_t* __restrict__ ob, const int64_t* __restrict__ cb, const int64_t* __restrict__ obb,
                           const int64_t* __restrict__ pcb, const int64_t* __restrict__ rsb, const int64_t* __restrict__ rob,
                           covt_stream_info* __restrict__ info, int32_t* __restrict__ nvals, covt_prop_info* __restrict__ pinfo,
-                          uint16_t* __restrict__ pflags, int64_t* __restrict__ pin) {
+                          uint16_t* __restrict__ pflags, int64_t* __restrict__ pin, uint32_t* __restrict__ keys,
+                          int32_t lm) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_rec) return;
     const int32_t t = rtile[r];
@@ -2178,6 +2219,7 @@ __global__ void prop_fill(const PropRaw* __restrict__ recs, const int32_t* __res
         out = align_out(out + ps.count[k] * ps.elem[k]);
         info[si_k] = si;
         nvals[si_k] = (int32_t)ps.count[k];
+        if (keys) keys[si_k] = entry_key(si.op, (int32_t)ps.count[k], si.byte_length, si.out_elems, si.elem_bytes, lm);
         pi.stream[role] = (int32_t)si_k;
     }
     pin[2 * r] = pi.out_off[1];  // the FLOAT data / STRING dictionary input offsets (plan_property_layout's
@@ -2410,6 +2452,8 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     DCHK(hipMemsetAsync(totals, 0, T_N * 8, s));
     DCHK(hipMemsetAsync(tsum, 0, nt1 * 32, s));  // failed tiles leave zeros
     const int64_t fpf_w = o.fpf_split_weight;
+    const int32_t lane_max = lane_limits(o.lane_max_bytes, o.lane_max_values);
+    const int64_t lane_min = o.lane_min_streams;
     // 0: a wave per tile, its lanes in lockstep; k > 0: k lanes per workgroup, a lane per tile
     RawStream* slots = use_slots ? (RawStream*)(ta + o_slots) : nullptr;
     if (wl == 0)
@@ -2539,32 +2583,36 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     p->d_order = v1;
     p->d_desc = (covt_stream_desc*)(sa + o_d);
     // launch order: the stable radix sort of the launch keys q0 (low byte: -> q1, v0; high byte: -> q0, v1)
+    unsigned long long* fam_tot = splitting ? nullptr : totals + T_FAM;  // (split plans: stream_keys counts)
     auto launch_order = [&]() {
         const int scanned = nb > kSortFuseChunks;
         for (int pass = 0; pass < 2; ++pass) {
             order_hist<<<nb, 256, 0, s>>>(pass ? q1 : q0, ns, nb, 8 * pass, bhist);
             if (scanned) order_scan<<<1, 1024, 0, s>>>(bhist, (int64_t)kSortBuckets * nb);
-            if (pass == 0) order_scatter<<<nb, 1024, 0, s>>>(q0, nullptr, ns, nb, 0, bhist, scanned, q1, v0);
-            else order_scatter<<<nb, 1024, 0, s>>>(q1, v0, ns, nb, 8, bhist, scanned, q0, v1);
+            if (pass == 0) order_scatter<<<nb, 1024, 0, s>>>(q0, nullptr, ns, nb, 0, bhist, scanned, q1, v0, nullptr);
+            else order_scatter<<<nb, 1024, 0, s>>>(q1, v0, ns, nb, 8, bhist, scanned, q0, v1, fam_tot);
         }
         return hipGetLastError();
     };
-    const int32_t lane_max = lane_limits(o.lane_max_bytes, o.lane_max_values);
-    const int64_t lane_min = o.lane_min_streams;
+    // unsplit plans: the launch keys written with the stream entries, taking every small RLE stream to the
+    // lane family (lane_keys redoes them when the batch has fewer such streams than lane_min: the count
+    // is known once the entries are written); split plans: stream_keys after split_mark
+    uint32_t* ekeys = splitting ? nullptr : q0;
+    const int32_t lm = lane_max;
     if (n_tiles) {
         if (slots) {
             emit_slots<<<n_tiles, 64, 0, s>>>(d_tile_offsets, n_tiles, id_mode, p->d_status, cnt, cb, obb, slots,
-                                              lane_max, p->d_info, nvals, tsum);
+                                              lane_max, p->d_info, nvals, tsum, ekeys, lm);
             DCHK(hipGetLastError());
         }
         if (wl == 0)  // (with slots: only tiles with more than kSlots streams walk again)
             walk_emit<true><<<n_tiles, 64, kWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
                                                           id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, tsum,
-                                                          slots ? cnt : nullptr);
+                                                          slots ? cnt : nullptr, ekeys, lm);
         else
             walk_emit<false><<<(n_tiles + wl - 1) / wl, wl, (size_t)wl * 64 + 16, s>>>(
                 d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cb, obb,
-                lane_max, p->d_info, nvals, tsum, nullptr);
+                lane_max, p->d_info, nvals, tsum, nullptr, ekeys, lm);
         DCHK(hipGetLastError());
         reduce_tiles<<<1, 1024, 0, s>>>(tsum, n_tiles, totals, pacc);
         DCHK(hipGetLastError());
@@ -2572,13 +2620,14 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
             uint8_t* pa = (uint8_t*)p->prop_arena;
             prop_fill<<<(int)((n_rec + 255) / 256), 256, 0, s>>>(recs, rtile, n_rec, id_mode, d_tile_offsets, cnt, ob, cb,
                                                                  obb, pcb, rsb, rob, p->d_info, nvals, p->d_pinfo,
-                                                                 (uint16_t*)(pa + po_pf), (int64_t*)(pa + po_pin));
+                                                                 (uint16_t*)(pa + po_pf), (int64_t*)(pa + po_pin), ekeys,
+                                                                 lm);
             DCHK(hipGetLastError());
         }
     }
     const int blocks_s = (int)((ns + 255) / 256);
     if (ns > 0 && !splitting) {
-        stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, q0, nullptr, nullptr);
+        lane_keys<<<256, 256, 0, s>>>(p->d_info, nvals, ns, lane_min, totals, q0);
         DCHK(hipGetLastError());
         DCHK(launch_order());
         fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, q0, v1, ns, p->d_desc);
