@@ -63,20 +63,30 @@ typedef __attribute__((address_space(1))) const uint64_t g_u64;
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const i32x4 g_i32x4;
 
-template <int NW>
+template <int NW, int IPL = 4>
 struct __attribute__((aligned(16))) AsmSmemT {
-    int32_t slot[4 * 64 * NW];  // expansion: segment-end marks of the current step
-    int32_t ends[4 * 64 * NW];  // expansion: the step's segment ends
-    uint32_t red[2][NW];        // cooperative scans / reductions: per-wave totals (two buffers)
+    int32_t slot[IPL * 64 * NW];  // expansion: segment-end marks of the current step
+    int32_t ends[IPL * 64 * NW];  // expansion: the step's segment ends
+    uint32_t red[2][NW];          // cooperative scans / reductions: per-wave totals (two buffers)
 };
-typedef AsmSmemT<1> AsmSmem;
+// Items of a step per thread.  A single wave holds its items LANE-MAJOR (item k of lane l is step item
+// 64 k + l): every load and store instruction of the passes then covers 64 consecutive items (256 bytes
+// of int32), where four consecutive items per lane spread each instruction over 1 KiB -- the batch
+// assembly is bound by the texture address unit's per-line work (TA busy 87 % of the kernel, issue
+// stalls 31 % of wave time; 8 consecutive items per lane: 2 KiB per instruction, 3.82 -> 5.35 ms).
+// A cooperative group (NW > 1, the split passes) keeps IPL consecutive items per thread.
+#ifndef COVT_ASM_IPL
+#define COVT_ASM_IPL 4
+#endif
+constexpr int kAsmIpl = COVT_ASM_IPL;
+typedef AsmSmemT<1, kAsmIpl> AsmSmem;
 
 // The threads assembling one column: a wave (NW = 1: lane_id, wave primitives, no barrier) or a whole
 // workgroup of NW waves (thread index, per-wave partials through LDS and workgroup barriers).  Items
-// of a step: 4 consecutive per thread, K = 256 NW per step.
-template <int NW>
+// of a step: IPL consecutive per thread, K = 64 IPL NW per step.
+template <int NW, int IPL = 4>
 struct Coop {
-    static constexpr int K = 4 * 64 * NW;
+    static constexpr int K = IPL * 64 * NW;
     __device__ __forceinline__ static int tid() { return NW == 1 ? lane_id() : (int)threadIdx.x; }
     __device__ __forceinline__ static int wid() { return NW == 1 ? 0 : (int)(threadIdx.x >> 6); }
     __device__ __forceinline__ static void sync() {
@@ -88,7 +98,8 @@ struct Coop {
     // group total.  Sums saturate at 0xffffffff: every count is checked against a capacity below 2^31, so
     // a saturated total fails the check, where a wrapped one could pass it (a 4096-item cooperative step
     // of clamped counts can reach 2^32).  A saturated prefix is only ever stored for a failing column.
-    __device__ __forceinline__ static uint32_t group_prefix(AsmSmemT<NW>& sm, uint32_t inc, uint32_t own,
+    template <int I>
+    __device__ __forceinline__ static uint32_t group_prefix(AsmSmemT<NW, I>& sm, uint32_t inc, uint32_t own,
                                                            uint32_t& tot, int buf) {
         if (NW == 1) {
             tot = lane_bcast(inc, 63);
@@ -112,123 +123,216 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {  // lane l - 1's val
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
 }
 
-// exclusive scan of the step's items held 4 per thread (items 4t .. 4t+3); `tot` gets the uniform total.
-// Cooperative groups alternate the two partial buffers (each buffer is rewritten only after a barrier
-// that follows every read of its previous contents).
-template <int NW>
-__device__ __forceinline__ void excl_scan4(AsmSmemT<NW>& sm, int& buf, const uint32_t x[4], uint32_t ex[4], uint32_t& tot) {
-    const uint32_t s = add_sat(add_sat(x[0], x[1]), add_sat(x[2], x[3]));  // saturating: see group_prefix
+// exclusive scan of the step's items held IPL per thread (items IPL t .. IPL t + IPL - 1); `tot` gets the
+// uniform total.  Cooperative groups alternate the two partial buffers (each buffer is rewritten only after
+// a barrier that follows every read of its previous contents).
+template <int NW, int IPL>
+__device__ __forceinline__ void excl_scan4(AsmSmemT<NW, IPL>& sm, int& buf, const uint32_t (&x)[IPL], uint32_t (&ex)[IPL],
+                                           uint32_t& tot) {
+    if (NW == 1) {  // lane-major items: a wave scan per row of 64, rows carried in order
+        uint32_t carry = 0;
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {
+            const uint32_t inc = incl_scan_sat(x[k]);
+            ex[k] = add_sat(carry, inc - x[k]);
+            carry = add_sat(carry, lane_bcast(inc, 63));
+        }
+        tot = carry;
+        buf ^= 1;
+        return;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) s = add_sat(s, x[k]);  // saturating: see group_prefix
     const uint32_t inc = incl_scan_sat(s);
-    uint32_t run = Coop<NW>::group_prefix(sm, inc, s, tot, buf);
+    uint32_t run = Coop<NW, IPL>::group_prefix(sm, inc, s, tot, buf);
     buf ^= 1;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < IPL; ++k) {
         ex[k] = run;
         run = add_sat(run, x[k]);
     }
 }
 
-// items q + 4l + k (k < 4) of a step of L: one 16-byte store when the lane's four are valid and
+// items q + IPL l + k (k < IPL) of a step of L: 16-byte stores when the lane's items are valid and
 // aligned (arrays are 16-byte aligned; aligned when q % 4 == 0), else element stores
-template <int NW>
-__device__ __forceinline__ void store4(int32_t* a, int32_t q, int32_t L, const uint32_t v[4]) {
-    const int32_t i0 = 4 * Coop<NW>::tid();
-    if ((q & 3) == 0 && i0 + 4 <= L) {
-        *(i32x4*)(a + q + i0) = i32x4{(int32_t)v[0], (int32_t)v[1], (int32_t)v[2], (int32_t)v[3]};
+template <int NW, int IPL>
+__device__ __forceinline__ void store4(int32_t* a, int32_t q, int32_t L, const uint32_t (&v)[IPL]) {
+    if (NW == 1) {  // lane-major: each store 64 consecutive items
+#pragma unroll
+        for (int k = 0; k < IPL; ++k)
+            if (64 * k + lane_id() < L) a[q + 64 * k + lane_id()] = (int32_t)v[k];
+        return;
+    }
+    const int32_t i0 = IPL * Coop<NW, IPL>::tid();
+    if ((q & 3) == 0 && i0 + IPL <= L) {
+#pragma unroll
+        for (int k = 0; k < IPL; k += 4)
+            *(i32x4*)(a + q + i0 + k) = i32x4{(int32_t)v[k], (int32_t)v[k + 1], (int32_t)v[k + 2], (int32_t)v[k + 3]};
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < IPL; ++k)
             if (i0 + k < L) a[q + i0 + k] = (int32_t)v[k];
     }
 }
-// coordinates (8 bytes each): two 16-byte nontemporal stores for four aligned valid items
-template <int NW>
-__device__ __forceinline__ void store4_xy(uint64_t* a, int32_t q, int32_t L, const uint64_t v[4]) {
-    const int32_t i0 = 4 * Coop<NW>::tid();
-    if ((q & 3) == 0 && i0 + 4 <= L) {
+// coordinates (8 bytes each): 16-byte nontemporal stores for aligned valid items
+template <int NW, int IPL>
+__device__ __forceinline__ void store4_xy(uint64_t* a, int32_t q, int32_t L, const uint64_t (&v)[IPL]) {
+    if (NW == 1) {  // lane-major: each store 64 consecutive coordinates (512 bytes)
+#pragma unroll
+        for (int k = 0; k < IPL; ++k)
+            if (64 * k + lane_id() < L) __builtin_nontemporal_store(v[k], a + q + 64 * k + lane_id());
+        return;
+    }
+    const int32_t i0 = IPL * Coop<NW, IPL>::tid();
+    if ((q & 3) == 0 && i0 + IPL <= L) {
         i32x4* p = (i32x4*)(a + q + i0);
-        __builtin_nontemporal_store(i32x4{(int32_t)v[0], (int32_t)(v[0] >> 32), (int32_t)v[1], (int32_t)(v[1] >> 32)}, p);
-        __builtin_nontemporal_store(i32x4{(int32_t)v[2], (int32_t)(v[2] >> 32), (int32_t)v[3], (int32_t)(v[3] >> 32)},
-                                    p + 1);
+#pragma unroll
+        for (int k = 0; k < IPL; k += 2)
+            __builtin_nontemporal_store(
+                i32x4{(int32_t)v[k], (int32_t)(v[k] >> 32), (int32_t)v[k + 1], (int32_t)(v[k + 1] >> 32)}, p + k / 2);
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < IPL; ++k)
             if (i0 + k < L) a[q + i0 + k] = v[k];
     }
 }
 
 // Segmented expansion cursor over O[0..S] (nondecreasing, O[0] = 0, O[S] = total), uniform over the
-// group.  A step covers up to K items, thread t the four items q + 4t + k.
-template <int NW>
+// group.  A step covers up to K items, thread t the IPL items q + IPL t + k.
+template <int NW, int IPL = 4>
 struct Expand {
-    static constexpr int K = Coop<NW>::K;
+    static constexpr int K = Coop<NW, IPL>::K;
     const int32_t* O;
     int32_t S, total;
     int32_t base;   // segment index with O[base] <= q
     int32_t obase;  // O[base]
     int32_t q;      // first item of the next step
 
-    // one step: L items (uniform); item k of the thread (valid if 4t + k < L) gets its segment, the
+    // one step: L items (uniform); item k of the thread (valid if IPL t + k < L) gets its segment, the
     // segment's start and end
-    __device__ __forceinline__ int32_t step(AsmSmemT<NW>& sm, int& buf, int32_t seg[4], int32_t start[4],
-                                            int32_t end[4]) {
-        const int t = Coop<NW>::tid();
-        int32_t e[4];
+    __device__ __forceinline__ int32_t step(AsmSmemT<NW, IPL>& sm, int& buf, int32_t (&seg)[IPL], int32_t (&start)[IPL],
+                                            int32_t (&end)[IPL]) {
+        if (NW == 1) return step_lm(sm, seg, start, end);
+        const int t = Coop<NW, IPL>::tid();
+        int32_t e[IPL];
+        const int32_t j0 = base + 1 + IPL * t;  // ends of segments base + 1 + IPL t + k
+        if (j0 + IPL - 1 <= S) {  // 16-byte loads (4-byte aligned)
+            typedef int32_t i32x4u __attribute__((ext_vector_type(4), aligned(4)));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {  // end of segment base + 1 + 4t + k
-            const int32_t j = base + 1 + 4 * t + k;
-            e[k] = j <= S ? ((const g_i32*)O)[j] : 0x7fffffff;
+            for (int k = 0; k < IPL; k += 4) {
+                const i32x4u w = *(const __attribute__((address_space(1))) i32x4u*)(O + j0 + k);
+                e[k] = w.x, e[k + 1] = w.y, e[k + 2] = w.z, e[k + 3] = w.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) e[k] = j0 + k <= S ? ((const g_i32*)O)[j0 + k] : 0x7fffffff;
         }
-        *(i32x4*)&sm.ends[4 * t] = i32x4{e[0], e[1], e[2], e[3]};
-        *(i32x4*)&sm.slot[4 * t] = i32x4{0, 0, 0, 0};
-        Coop<NW>::sync();
-        int32_t r[5];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) r[k] = max(e[k] - q, 0);  // item offset where segment base+2+4t+k starts
-        if (NW == 1) r[4] = (int32_t)lane_next((uint32_t)r[0], 0x7fffffffu);
-        else r[4] = 4 * t + 4 < K ? max(sm.ends[4 * t + 4] - q, 0) : 0x7fffffff;
+        for (int k = 0; k < IPL; k += 4) {
+            *(i32x4*)&sm.ends[IPL * t + k] = i32x4{e[k], e[k + 1], e[k + 2], e[k + 3]};
+            *(i32x4*)&sm.slot[IPL * t + k] = i32x4{0, 0, 0, 0};
+        }
+        Coop<NW, IPL>::sync();
+        int32_t r[IPL + 1];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (r[k] < K && r[k + 1] != r[k]) sm.slot[r[k]] = 4 * t + k + 1;  // the last of equal ends wins
-        Coop<NW>::sync();
-        const i32x4 sl = *(const i32x4*)&sm.slot[4 * t];
-        uint32_t m[4];
-        m[0] = (uint32_t)sl.x;
-        m[1] = max(m[0], (uint32_t)sl.y);
-        m[2] = max(m[1], (uint32_t)sl.z);
-        m[3] = max(m[2], (uint32_t)sl.w);
-        const uint32_t wincl = incl_max_scan(m[3]);
+        for (int k = 0; k < IPL; ++k) r[k] = max(e[k] - q, 0);  // item offset where segment base+2+IPL t+k starts
+        if (NW == 1) r[IPL] = (int32_t)lane_next((uint32_t)r[0], 0x7fffffffu);
+        else r[IPL] = IPL * t + IPL < K ? max(sm.ends[IPL * t + IPL] - q, 0) : 0x7fffffff;
+#pragma unroll
+        for (int k = 0; k < IPL; ++k)
+            if (r[k] < K && r[k + 1] != r[k]) sm.slot[r[k]] = IPL * t + k + 1;  // the last of equal ends wins
+        Coop<NW, IPL>::sync();
+        uint32_t m[IPL];
+#pragma unroll
+        for (int k = 0; k < IPL; k += 4) {
+            const i32x4 sl = *(const i32x4*)&sm.slot[IPL * t + k];
+            m[k] = k ? max(m[k - 1], (uint32_t)sl.x) : (uint32_t)sl.x;
+            m[k + 1] = max(m[k], (uint32_t)sl.y);
+            m[k + 2] = max(m[k + 1], (uint32_t)sl.z);
+            m[k + 3] = max(m[k + 2], (uint32_t)sl.w);
+        }
+        const uint32_t wincl = incl_max_scan(m[IPL - 1]);
         uint32_t prev = wave_shr1(wincl);
         if (NW > 1) {  // the maximum over the lower waves' marks
-            if (lane_id() == 63) sm.red[buf][Coop<NW>::wid()] = wincl;
+            if (lane_id() == 63) sm.red[buf][Coop<NW, IPL>::wid()] = wincl;
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < NW; ++i)
-                if (i < Coop<NW>::wid()) prev = max(prev, sm.red[buf][i]);
+                if (i < Coop<NW, IPL>::wid()) prev = max(prev, sm.red[buf][i]);
             buf ^= 1;
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int32_t cnt = (int32_t)max(prev, m[k]);  // segment ends <= q + 4t + k
+        for (int k = 0; k < IPL; ++k) {
+            const int32_t cnt = (int32_t)max(prev, m[k]);  // segment ends <= q + IPL t + k
             start[k] = cnt == 0 ? obase : sm.ends[cnt - 1];
             end[k] = sm.ends[min(cnt, K - 1)];
             seg[k] = base + cnt;
         }
         // items this step: at most K, the rest of the column, and what the K loaded ends cover
         int32_t L = min(K, total - q);
-        if (base + K < S) L = min(L, (NW == 1 ? (int32_t)lane_bcast((uint32_t)e[3], 63) : sm.ends[K - 1]) - q);
+        if (base + K < S) L = min(L, (NW == 1 ? (int32_t)lane_bcast((uint32_t)e[IPL - 1], 63) : sm.ends[K - 1]) - q);
         L = max(L, 0);
         int adv = 0;  // segments ending at or before the next q
 #pragma unroll
-        for (int k = 0; k < 4; ++k) adv += __popcll(__ballot(e[k] <= q + L));
+        for (int k = 0; k < IPL; ++k) adv += __popcll(__ballot(e[k] <= q + L));
         if (NW > 1) {
             uint32_t tot;
-            (void)Coop<NW>::group_prefix(sm, lane_id() == 63 ? (uint32_t)adv : 0u, 0u, tot, buf);
+            (void)Coop<NW, IPL>::group_prefix(sm, lane_id() == 63 ? (uint32_t)adv : 0u, 0u, tot, buf);
             buf ^= 1;
             adv = (int)tot;
         }
         const int32_t nob = adv > 0 ? uni(sm.ends[adv - 1]) : obase;
-        Coop<NW>::sync();
+        Coop<NW, IPL>::sync();
+        obase = nob;
+        base += adv;
+        q += L;
+        return L;
+    }
+
+    // the single-wave step, items lane-major (item k of lane l: step item 64 k + l; segment base + 1 + 64 k + l
+    // ends at ends[64 k + l])
+    __device__ __forceinline__ int32_t step_lm(AsmSmemT<NW, IPL>& sm, int32_t (&seg)[IPL], int32_t (&start)[IPL],
+                                               int32_t (&end)[IPL]) {
+        const int l = lane_id();
+        int32_t e[IPL], r[IPL];
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {
+            const int32_t j = base + 1 + 64 * k + l;
+            e[k] = j <= S ? ((const g_i32*)O)[j] : 0x7fffffff;
+        }
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {
+            sm.ends[64 * k + l] = e[k];
+            sm.slot[64 * k + l] = 0;
+            r[k] = max(e[k] - q, 0);  // item offset where segment base + 2 + 64 k + l starts
+        }
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {  // the last of equal ends marks (the next segment's end: lane l + 1)
+            const uint32_t tail = k + 1 < IPL ? lane_bcast((uint32_t)r[k + 1 < IPL ? k + 1 : k], 0) : 0x7fffffffu;
+            const int32_t rn = (int32_t)lane_next((uint32_t)r[k], tail);
+            if (r[k] < K && rn != r[k]) sm.slot[r[k]] = 64 * k + l + 1;
+        }
+        wave_sync();
+        uint32_t carry = 0;
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {
+            const uint32_t m = max(incl_max_scan((uint32_t)sm.slot[64 * k + l]), carry);  // segment ends <= item
+            carry = lane_bcast(m, 63);
+            const int32_t cnt = (int32_t)m;
+            start[k] = cnt == 0 ? obase : sm.ends[cnt - 1];
+            end[k] = sm.ends[min(cnt, K - 1)];
+            seg[k] = base + cnt;
+        }
+        int32_t L = min(K, total - q);
+        if (base + K < S) L = min(L, (int32_t)lane_bcast((uint32_t)e[IPL - 1], 63) - q);
+        L = max(L, 0);
+        int adv = 0;
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) adv += __popcll(__ballot(e[k] <= q + L));
+        const int32_t nob = adv > 0 ? uni(sm.ends[adv - 1]) : obase;
+        wave_sync();
         obase = nob;
         base += adv;
         q += L;
@@ -243,12 +347,14 @@ __device__ __forceinline__ void mem_publish() {  // the group's global stores vi
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-template <int NW>
+template <int NW, int IPL = 4>
 __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stream_result* __restrict__ dres,
                                 const covt_geom_desc& d, uint8_t* __restrict__ outb, covt_geom_result& res,
-                                AsmSmemT<NW>& sm) {
-    constexpr int K = Coop<NW>::K;
-    const int l = Coop<NW>::tid();
+                                AsmSmemT<NW, IPL>& sm) {
+    constexpr int K = Coop<NW, IPL>::K;
+    const int l = Coop<NW, IPL>::tid();
+    // step item of this thread's k-th item: lane-major for a wave, IPL consecutive per thread for a group
+    auto ioff = [&](int k) { return NW == 1 ? 64 * k + l : IPL * l + k; };
     int buf = 0;  // cooperative partials buffer (see excl_scan4)
     res.num_parts = res.num_rings = res.num_coords = 0;
     if ((uint32_t)d.flags & COVT_GEOM_TOO_LARGE) { res.status = COVT_ERR_INVALID_ARG; return; }
@@ -286,20 +392,31 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     // ---- pass 1: features -> parts (items: features) ----
     uint32_t go_base = 0, P = 0;
     for (int32_t f0 = 0; f0 < n; f0 += K) {
-        const int32_t fl = f0 + 4 * l;  // this lane's first feature; types are 16-byte aligned
-        const uint32_t tw = fl < n ? ((const g_u32*)types)[fl >> 2] : 0u;
-        uint32_t t[4], multi[4], gi[4], pf[4], ex[4], nm, tot;
+        uint32_t t[IPL], multi[IPL], gi[IPL], pf[IPL], ex[IPL], nm, tot;
+        if (NW == 1) {  // lane-major: one byte per item
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool valid = fl + k < n;
-            t[k] = valid ? (tw >> (8 * k)) & 0xffu : 0u;
-            bad_type |= t[k] > 5u;
-            multi[k] = (valid && t[k] >= 3u && t[k] <= 5u) ? 1u : 0u;
-            pf[k] = valid ? 1u : 0u;
+            for (int k = 0; k < IPL; ++k) {
+                const bool valid = f0 + ioff(k) < n;
+                t[k] = valid ? (uint32_t)((const g_u8*)types)[f0 + ioff(k)] : 0u;
+                bad_type |= t[k] > 5u;
+                multi[k] = (valid && t[k] >= 3u && t[k] <= 5u) ? 1u : 0u;
+                pf[k] = valid ? 1u : 0u;
+            }
+        } else {
+            const int32_t fl = f0 + IPL * l;  // this thread's first feature; types are 16-byte aligned
+            const uint32_t tw = fl < n ? ((const g_u32*)types)[fl >> 2] : 0u;
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) {
+                const bool valid = fl + k < n;
+                t[k] = valid ? (tw >> (8 * k)) & 0xffu : 0u;
+                bad_type |= t[k] > 5u;
+                multi[k] = (valid && t[k] >= 3u && t[k] <= 5u) ? 1u : 0u;
+                pf[k] = valid ? 1u : 0u;
+            }
         }
         excl_scan4(sm, buf, multi, gi, nm);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < IPL; ++k) {
             if (multi[k]) {
                 const uint32_t i = go_base + gi[k];
                 if (i < (uint32_t)n_go) {
@@ -313,7 +430,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
         }
         excl_scan4(sm, buf, pf, ex, tot);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ex[k] += P;
+        for (int k = 0; k < IPL; ++k) ex[k] += P;
         store4<NW>(geo_off, f0, n - f0, ex);
         go_base += nm;
         P = add_sat(P, tot);
@@ -331,22 +448,22 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     // ---- pass 2: parts -> rings (items: parts, segments: features) ----
     uint32_t po_base = 0, R = 0;
     {
-        Expand<NW> x{geo_off, n, (int32_t)P, 0, 0, 0};
+        Expand<NW, IPL> x{geo_off, n, (int32_t)P, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t p0 = x.q;
-            int32_t f[4], fs[4], fe[4];
+            int32_t f[IPL], fs[IPL], fe[IPL];
             const int32_t L = x.step(sm, buf, f, fs, fe);
-            uint32_t t[4], usep[4], pi[4], rp[4], scr[4], ex[4], npo, tot;
+            uint32_t t[IPL], usep[IPL], pi[IPL], rp[IPL], scr[IPL], ex[IPL], npo, tot;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool valid = 4 * l + k < L;
+            for (int k = 0; k < IPL; ++k) {
+                const bool valid = ioff(k) < L;
                 t[k] = valid ? (uint32_t)((const g_u8*)types)[f[k]] : 0u;
                 usep[k] = (valid && t[k] != 0u && t[k] != 3u) ? 1u : 0u;  // line and polygon parts
             }
             excl_scan4(sm, buf, usep, pi, npo);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool valid = 4 * l + k < L;
+            for (int k = 0; k < IPL; ++k) {
+                const bool valid = ioff(k) < L;
                 uint32_t c = 0;
                 if (usep[k]) {
                     const uint32_t i = po_base + pi[k];
@@ -365,7 +482,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
             }
             excl_scan4(sm, buf, rp, ex, tot);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) ex[k] += R;
+            for (int k = 0; k < IPL; ++k) ex[k] += R;
             store4<NW>(part_off, p0, L, ex);
             store4<NW>(part_scr, p0, L, scr);
             po_base += npo;
@@ -384,23 +501,23 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     // ---- pass 3: rings -> coordinates (items: rings, segments: parts) ----
     uint32_t ro_base = 0, V = 0, VS = 0;
     {
-        Expand<NW> x{part_off, (int32_t)P, (int32_t)R, 0, 0, 0};
+        Expand<NW, IPL> x{part_off, (int32_t)P, (int32_t)R, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t r0 = x.q;
-            int32_t p[4], ps[4], pe[4];
+            int32_t p[IPL], ps[IPL], pe[IPL];
             const int32_t L = x.step(sm, buf, p, ps, pe);
-            uint32_t poly[4], ri[4], vs[4], vo_[4], ex[4], src[4], nr, tv, ts;
+            uint32_t poly[IPL], ri[IPL], vs[IPL], vo_[IPL], ex[IPL], src[IPL], nr, tv, ts;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool valid = 4 * l + k < L;
+            for (int k = 0; k < IPL; ++k) {
+                const bool valid = ioff(k) < L;
                 const int32_t sp = valid ? ((const g_i32*)part_scr)[p[k]] : 0;
                 poly[k] = (valid && (sp & 1)) ? 1u : 0u;
                 vs[k] = valid ? (uint32_t)sp >> 1 : 0u;
             }
             excl_scan4(sm, buf, poly, ri, nr);
-            uint32_t closing[4];
+            uint32_t closing[IPL];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < IPL; ++k) {
                 if (poly[k]) {
                     const uint32_t i = ro_base + ri[k];
                     if (i < (uint32_t)n_ro) {
@@ -417,7 +534,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
             excl_scan4(sm, buf, vo_, ex, tv);
             excl_scan4(sm, buf, vs, src, ts);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < IPL; ++k) {
                 ex[k] += V;
                 src[k] = (VS + src[k]) | (closing[k] << 31);
             }
@@ -443,47 +560,72 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
         // no closing vertex to insert: coordinate v is source vertex v (a straight copy / gather).  Two
         // steps per iteration, their index loads and gathers issued before any store (stores may alias
         // the loads as far as the compiler knows, so a one-step loop waits out every chain in turn)
-        auto idx4 = [&](int32_t i0, int32_t (&idx)[4]) {
-            if (ice && i0 + 4 <= (int32_t)V) {  // vertexOffsets are 16-byte aligned, i0 % 4 == 0
-                const i32x4 w = *(const g_i32x4*)(vo + i0);
-                idx[0] = w.x; idx[1] = w.y; idx[2] = w.z; idx[3] = w.w;
+        auto idx4 = [&](int32_t i0, int32_t (&idx)[IPL]) {
+            if (ice && i0 + IPL <= (int32_t)V) {  // vertexOffsets are 16-byte aligned, i0 % 4 == 0
+#pragma unroll
+                for (int k = 0; k < IPL; k += 4) {
+                    const i32x4 w = *(const g_i32x4*)(vo + i0 + k);
+                    idx[k] = w.x; idx[k + 1] = w.y; idx[k + 2] = w.z; idx[k + 3] = w.w;
+                }
             } else {
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
+                for (int k = 0; k < IPL; ++k)
                     idx[k] = i0 + k < (int32_t)V ? (ice ? ((const g_i32*)vo)[i0 + k] : i0 + k) : 0;
             }
         };
-        auto gather4 = [&](int32_t i0, const int32_t (&idx)[4], uint64_t (&xy)[4]) {
+        auto gather4 = [&](int32_t i0, const int32_t (&idx)[IPL], uint64_t (&xy)[IPL]) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < IPL; ++k) {
                 const bool valid = i0 + k < (int32_t)V;
                 const bool inr = (uint32_t)idx[k] < (uint32_t)n_vb;
                 bad_idx |= valid && !inr;
                 xy[k] = (valid && inr) ? ((const g_u64*)vb)[idx[k]] : 0ull;
             }
         };
-        for (int32_t v0 = 0; v0 < (int32_t)V; v0 += 2 * K) {
-            const int32_t i0 = v0 + 4 * l, i1 = i0 + K;
-            int32_t ia[4], ib[4];
-            idx4(i0, ia);
-            idx4(i1, ib);
-            uint64_t xa[4], xb[4];
-            gather4(i0, ia, xa);
-            gather4(i1, ib, xb);
-            store4_xy<NW>(coords, v0, (int32_t)V - v0, xa);
-            if (v0 + K < (int32_t)V) store4_xy<NW>(coords, v0 + K, (int32_t)V - v0 - K, xb);
+        if (NW == 1) {  // lane-major: two steps per iteration, every instruction 64 consecutive coordinates
+            for (int32_t v0 = 0; v0 < (int32_t)V; v0 += 2 * K) {
+                int32_t ia[2 * IPL];
+#pragma unroll
+                for (int k = 0; k < 2 * IPL; ++k) {
+                    const int32_t i = v0 + 64 * k + l;
+                    ia[k] = i < (int32_t)V ? (ice ? ((const g_i32*)vo)[i] : i) : 0;
+                }
+                uint64_t xa[2 * IPL];
+#pragma unroll
+                for (int k = 0; k < 2 * IPL; ++k) {
+                    const bool valid = v0 + 64 * k + l < (int32_t)V;
+                    const bool inr = (uint32_t)ia[k] < (uint32_t)n_vb;
+                    bad_idx |= valid && !inr;
+                    xa[k] = (valid && inr) ? ((const g_u64*)vb)[ia[k]] : 0ull;
+                }
+#pragma unroll
+                for (int k = 0; k < 2 * IPL; ++k)
+                    if (v0 + 64 * k + l < (int32_t)V) __builtin_nontemporal_store(xa[k], coords + v0 + 64 * k + l);
+            }
+        } else {
+            for (int32_t v0 = 0; v0 < (int32_t)V; v0 += 2 * K) {
+                const int32_t i0 = v0 + IPL * l, i1 = i0 + K;
+                int32_t ia[IPL], ib[IPL];
+                idx4(i0, ia);
+                idx4(i1, ib);
+                uint64_t xa[IPL], xb[IPL];
+                gather4(i0, ia, xa);
+                gather4(i1, ib, xb);
+                store4_xy<NW>(coords, v0, (int32_t)V - v0, xa);
+                if (v0 + K < (int32_t)V) store4_xy<NW>(coords, v0 + K, (int32_t)V - v0 - K, xb);
+            }
         }
     } else {
-        Expand<NW> x{ring_off, (int32_t)R, (int32_t)V, 0, 0, 0};
+        Expand<NW, IPL> x{ring_off, (int32_t)R, (int32_t)V, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t v0 = x.q;
-            int32_t r[4], rs[4], re[4];
+            int32_t r[IPL], rs[IPL], re[IPL];
             const int32_t L = x.step(sm, buf, r, rs, re);
-            uint64_t xy[4];
+            uint64_t xy[IPL];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int32_t v = v0 + 4 * l + k;
-                const bool valid = 4 * l + k < L;
+            for (int k = 0; k < IPL; ++k) {
+                const int32_t v = v0 + ioff(k);
+                const bool valid = ioff(k) < L;
                 const uint32_t sr = valid ? (uint32_t)((const g_i32*)ring_scr)[r[k]] : 0u;
                 const int32_t first = (int32_t)(sr & 0x7fffffffu);
                 const int32_t src = ((sr >> 31) && v == re[k] - 1) ? first : first + (v - rs[k]);
@@ -520,7 +662,7 @@ __global__ __launch_bounds__(64 * kAsmWaves) void assemble_kernel(const uint8_t*
     if (c >= n_cols) return;
     const covt_geom_desc d = descs[c];
     covt_geom_result r{COVT_OK, 0, 0, 0};
-    assemble_column<1>(dec, dres, d, outb, r, smem[w]);
+    assemble_column<1, kAsmIpl>(dec, dres, d, outb, r, smem[w]);
     if (lane_id() == 0) gres[c] = r;
 }
 

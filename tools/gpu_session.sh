@@ -22,7 +22,7 @@ for s in "$@"; do
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     abfpf) step ab_fpf 900 python tools/ab.py ${AB_VARIANTS:-libcovt_base.so libcovt.so} ;;
     tests_asm) step pytest_gpu_asm 600 python -m pytest tests/test_gpu_assembly.py -m gpu -q -p no:cacheprovider --durations=5 ;;
-    asm_ab) for v in libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so; do
+    asm_ab) for v in ${AB_VARIANTS:-libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so}; do
             COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/asm_run.py 20 2>&1 | grep -v amdgpu.ids || fatal asm_ab $?
         done ;;
     pmc_asm) step pmc_asm_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_asm_fetch -o run --output-format csv -- python tools/asm_run.py 3 && \
@@ -30,6 +30,7 @@ for s in "$@"; do
     sq_asm) step sq_asm 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/sq_asm -o run --output-format csv -- python tools/asm_run.py 3 && \
             step mem_asm 300 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_TA_BUSY TA_DATA_STALLED_BY_TC_CYCLES TCP_PENDING_STALL_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU -d gpurun_out/mem_asm -o run --output-format csv -- python tools/asm_run.py 3 ;;
     asm_longpole) step asm_longpole 300 python tools/asm_longpole.py 10 ;;
+    asm_debug) step asm_debug 300 python tools/asm_debug.py 1 ;;
     tests_all) step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
