@@ -76,7 +76,7 @@ struct __attribute__((aligned(16))) AsmSmemT {
 // stalls 31 % of wave time; 8 consecutive items per lane: 2 KiB per instruction, 3.82 -> 5.35 ms).
 // A cooperative group (NW > 1, the split passes) keeps IPL consecutive items per thread.
 #ifndef COVT_ASM_IPL
-#define COVT_ASM_IPL 4
+#define COVT_ASM_IPL 8
 #endif
 constexpr int kAsmIpl = COVT_ASM_IPL;
 typedef AsmSmemT<1, kAsmIpl> AsmSmem;
