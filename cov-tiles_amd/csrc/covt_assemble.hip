@@ -78,6 +78,12 @@ struct __attribute__((aligned(16))) AsmSmemT {
 #ifndef COVT_ASM_IPL
 #define COVT_ASM_IPL 8
 #endif
+// single waves: the step's count window (the next K PartOffsets / RingOffsets entries from the rank
+// base) loaded with the step's own loads and picked from LDS by rank, instead of a load that waits on
+// the rank scan
+#ifndef COVT_ASM_WIN
+#define COVT_ASM_WIN 1
+#endif
 constexpr int kAsmIpl = COVT_ASM_IPL;
 typedef AsmSmemT<1, kAsmIpl> AsmSmem;
 
@@ -391,6 +397,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
 
     // ---- pass 1: features -> parts (items: features) ----
     uint32_t go_base = 0, P = 0;
+    bool multi_n = false;  // some feature's part count is not 1
     for (int32_t f0 = 0; f0 < n; f0 += K) {
         uint32_t t[IPL], multi[IPL], gi[IPL], pf[IPL], ex[IPL], nm, tot;
         if (NW == 1) {  // lane-major: one byte per item
@@ -430,7 +437,10 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
         }
         excl_scan4(sm, buf, pf, ex, tot);
 #pragma unroll
-        for (int k = 0; k < IPL; ++k) ex[k] += P;
+        for (int k = 0; k < IPL; ++k) {
+            ex[k] += P;
+            multi_n |= multi[k] && pf[k] != 1u;
+        }
         store4<NW>(geo_off, f0, n - f0, ex);
         go_base += nm;
         P = add_sat(P, tot);
@@ -445,14 +455,34 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     res.status = COVT_OK;
     return;
 #endif
+    // a pass whose segments all hold one item: item i is segment i
+    auto ident_step = [&](Expand<NW, IPL>& x, int32_t (&sg)[IPL]) {
+        const int32_t L = min(K, x.total - x.q);
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) sg[k] = x.q + ioff(k);
+        x.q += L;
+        return L;
+    };
+    const bool ident2 = !Coop<NW>::any(multi_n);
     // ---- pass 2: parts -> rings (items: parts, segments: features) ----
     uint32_t po_base = 0, R = 0;
+    bool poly_n = false;  // some part's ring count is not 1
     {
         Expand<NW, IPL> x{geo_off, n, (int32_t)P, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t p0 = x.q;
-            int32_t f[IPL], fs[IPL], fe[IPL];
-            const int32_t L = x.step(sm, buf, f, fs, fe);
+            int32_t f[IPL], fs[IPL], fe[IPL], pw[IPL];
+            constexpr bool kWin = NW == 1 && COVT_ASM_WIN;
+            if (kWin) {
+#pragma unroll
+                for (int k = 0; k < IPL; ++k) {
+                    const uint32_t i = po_base + (uint32_t)ioff(k);
+                    pw[k] = i < (uint32_t)n_po ? ((const g_i32*)po)[i] : 0;
+                }
+            }
+            // one part per feature (no multi-geometry with a count other than 1): part p is feature p, no
+            // expansion (most columns; the step's loads, marks and scans are half of the pass)
+            const int32_t L = ident2 ? ident_step(x, f) : x.step(sm, buf, f, fs, fe);
             uint32_t t[IPL], usep[IPL], pi[IPL], rp[IPL], scr[IPL], ex[IPL], npo, tot;
 #pragma unroll
             for (int k = 0; k < IPL; ++k) {
@@ -461,6 +491,12 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 usep[k] = (valid && t[k] != 0u && t[k] != 3u) ? 1u : 0u;  // line and polygon parts
             }
             excl_scan4(sm, buf, usep, pi, npo);
+            if (kWin) {  // (the step's expansion is done with the LDS tables)
+                wave_sync();
+#pragma unroll
+                for (int k = 0; k < IPL; ++k) sm.slot[ioff(k)] = pw[k];
+                wave_sync();
+            }
 #pragma unroll
             for (int k = 0; k < IPL; ++k) {
                 const bool valid = ioff(k) < L;
@@ -468,7 +504,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 if (usep[k]) {
                     const uint32_t i = po_base + pi[k];
                     if (i < (uint32_t)n_po) {
-                        const int32_t v = ((const g_i32*)po)[i];
+                        const int32_t v = kWin ? sm.slot[pi[k]] : ((const g_i32*)po)[i];
                         bad_cnt |= v < 0;
                         c = min((uint32_t)max(v, 0), rcap + 1u);
                     } else {
@@ -482,7 +518,10 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
             }
             excl_scan4(sm, buf, rp, ex, tot);
 #pragma unroll
-            for (int k = 0; k < IPL; ++k) ex[k] += R;
+            for (int k = 0; k < IPL; ++k) {
+                ex[k] += R;
+                poly_n |= ioff(k) < L && rp[k] != 1u;
+            }
             store4<NW>(part_off, p0, L, ex);
             store4<NW>(part_scr, p0, L, scr);
             po_base += npo;
@@ -498,14 +537,23 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
     res.status = COVT_OK;
     return;
 #endif
+    const bool ident3 = !Coop<NW>::any(poly_n);
     // ---- pass 3: rings -> coordinates (items: rings, segments: parts) ----
     uint32_t ro_base = 0, V = 0, VS = 0;
     {
         Expand<NW, IPL> x{part_off, (int32_t)P, (int32_t)R, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t r0 = x.q;
-            int32_t p[IPL], ps[IPL], pe[IPL];
-            const int32_t L = x.step(sm, buf, p, ps, pe);
+            int32_t p[IPL], ps[IPL], pe[IPL], rw[IPL];
+            constexpr bool kWin = NW == 1 && COVT_ASM_WIN;
+            if (kWin) {
+#pragma unroll
+                for (int k = 0; k < IPL; ++k) {
+                    const uint32_t i = ro_base + (uint32_t)ioff(k);
+                    rw[k] = i < (uint32_t)n_ro ? ((const g_i32*)ro)[i] : 0;
+                }
+            }
+            const int32_t L = ident3 ? ident_step(x, p) : x.step(sm, buf, p, ps, pe);  // (one ring per part)
             uint32_t poly[IPL], ri[IPL], vs[IPL], vo_[IPL], ex[IPL], src[IPL], nr, tv, ts;
 #pragma unroll
             for (int k = 0; k < IPL; ++k) {
@@ -515,13 +563,19 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 vs[k] = valid ? (uint32_t)sp >> 1 : 0u;
             }
             excl_scan4(sm, buf, poly, ri, nr);
+            if (kWin) {
+                wave_sync();
+#pragma unroll
+                for (int k = 0; k < IPL; ++k) sm.slot[ioff(k)] = rw[k];
+                wave_sync();
+            }
             uint32_t closing[IPL];
 #pragma unroll
             for (int k = 0; k < IPL; ++k) {
                 if (poly[k]) {
                     const uint32_t i = ro_base + ri[k];
                     if (i < (uint32_t)n_ro) {
-                        const int32_t v = ((const g_i32*)ro)[i];
+                        const int32_t v = kWin ? sm.slot[ri[k]] : ((const g_i32*)ro)[i];
                         bad_cnt |= v < 0;
                         vs[k] = min((uint32_t)max(v, 0), ccap + 1u);
                     } else {

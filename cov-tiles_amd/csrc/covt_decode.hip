@@ -557,10 +557,17 @@ __device__ __forceinline__ void win_value(const WaveSmem& sm, int32_t sj, int32_
 // (VariableByte tail) the region is decoded to its end, a trailing partial value is dropped and
 // more than `want` values is an error.  VAL_U64_STRICT with `first_bad`: the index (from this call's
 // first value) of the first over-long value is stored there when one stops the call.
+// `line` (values per 128-byte output line, a power of two; 0: off): a window's values end on an output
+// line unless they are the call's last -- the tail of a line is decoded from the next window, which
+// starts at it -- so no output line is written in two parts by consecutive windows (varint WRITE_SIZE
+// was 1.10x the output bytes, profiles/r03/pmc_traffic.txt)
+#ifndef COVT_VARINT_LINES
+#define COVT_VARINT_LINES 1
+#endif
 template <int MODE, int VAL, int K = 1, class Emit>
 __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t& pos, int32_t end, int32_t want,
                                bool until_end, int32_t& err, Emit&& emit, int32_t out0 = 0,
-                               int32_t* first_bad = nullptr) {
+                               int32_t* first_bad = nullptr, int32_t line = 0) {
     const int l = lane_id();
     int32_t got = 0;
     while (until_end ? (pos < end) : (got < want)) {
@@ -587,6 +594,18 @@ __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t&
             take = want - got;
         }
         if (take <= 0) break;
+        if (COVT_VARINT_LINES && MODE == MODE_RAW && line && !until_end && got + take < want) {
+            const int32_t cut = (out0 + got + take) & (line - 1);  // values past the window's last whole line
+            if (cut < take) {
+                take -= cut;
+            } else {
+                const int32_t aligned = (int32_t)(((uintptr_t)(sb + pos) & ~(uintptr_t)15) - (uintptr_t)sb);
+                if (w.woff != aligned) {  // only a line's tail left here: restart the window at it
+                    win_load<MODE, VAL>(sm, sb, w, pos, end);
+                    continue;
+                }
+            }
+        }
         bool lerr = false;
         int32_t fb = INT32_MAX;  // first over-long value (VAL_U64_STRICT, first_bad)
         const int32_t s0 = pos - w.woff;
@@ -707,6 +726,9 @@ __device__ __forceinline__ void sink_u64(const uint32_t (&lo)[4], const uint32_t
 
 template <int OP>
 __device__ __forceinline__ void run_varint_stream(Ctx& c) {
+    // values per 128-byte output line: 8-byte outputs (ids as int64, Morton x,y pairs) 16, else 32
+    constexpr int32_t kLine = (OP == COVT_OP_VARINT_I32_AS_I64 || OP == COVT_OP_VARINT_ZZ_I32_AS_I64 ||
+                               OP == COVT_OP_VARINT_ZZ_DELTA_I64 || OP == COVT_OP_VARINT_DELTA_MORTON) ? 16 : 32;
     int32_t pos = 0;
     Carry cr{0, 0};
     Win w;
@@ -720,14 +742,16 @@ __device__ __forceinline__ void run_varint_stream(Ctx& c) {
             *c.sm, c.sb, w, pos, c.avail, c.n, false, c.err,
             [&](const uint32_t (&lo)[4], const uint32_t (&hi)[4], int32_t base, int32_t first, int32_t count) {
                 sink_u64<OP>(lo, hi, base, first, count, (int64_t*)c.out, acc);
-            });
+            },
+            0, nullptr, 16);
     } else {
         if ((OP == COVT_OP_VARINT_ZZ_DELTA_XY) && (c.n & 1)) {
             // Java decodes the x,y pair and then overruns values[] (ArrayIndexOutOfBounds)
-            varint_take<MODE_RAW, VAL_J4, 4>(*c.sm, c.sb, w, pos, c.avail, c.n - 1, false, c.err, sink4);
+            varint_take<MODE_RAW, VAL_J4, 4>(*c.sm, c.sb, w, pos, c.avail, c.n - 1, false, c.err, sink4, 0, nullptr,
+                                             kLine);
             if (!c.err) c.err = COVT_ERR_COUNT_MISMATCH;
         } else {
-            varint_take<MODE_RAW, VAL_J4, 4>(*c.sm, c.sb, w, pos, c.avail, c.n, false, c.err, sink4);
+            varint_take<MODE_RAW, VAL_J4, 4>(*c.sm, c.sb, w, pos, c.avail, c.n, false, c.err, sink4, 0, nullptr, kLine);
         }
     }
     c.consumed = pos;
