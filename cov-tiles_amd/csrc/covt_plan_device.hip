@@ -7,16 +7,18 @@
 // with one wave per tile, so a caller whose tiles are already in HBM gets a decodable descriptor table
 // without a round trip through the host:
 //   1. walk_count   one wave per tile: the container walk, counting the tile's streams and output bytes
+//                   and leaving up to 128 stream records per tile in slots
 //   2. prefix sums  (hipcub) of the per-tile counts and output bytes -> each tile's first stream and
-//                   output offset; one 16-byte D2H of the totals to size the stream arrays
-//   3. walk_emit    the same walk again, writing each stream's covt_stream_info (output slices
-//                   16-byte aligned, in tile order: the host plan's layout, byte for byte)
-//   4. stream_keys  launch-order key per stream (family, lane op, cost descending), as the host plan
-//   5. radix sort   (hipcub, stable: ties in tile order) -> launch order
-//   6. fill_descs   descriptor k from the k-th stream in launch order; family counts
-// Streams are never split into chunks here (the host plan splits only streams longer than 1/3000 of a
-// batch's cost, i.e. long poles of small batches; a batch big enough to be worth a device plan splits
-// nothing, so the descriptor tables are identical -- tests/test_gpu_device_plan.py).
+//                   output offset; one 32-byte D2H of the totals to size the stream arrays
+//   3. emit_slots   each stream's covt_stream_info from the slots (output slices 128-byte aligned, in tile
+//                   order: the host plan's layout, byte for byte) and its 16-bit launch key (launch_key,
+//                   covt_internal.h); walk_emit walks the tiles with more streams again
+//   4. radix sort   two 8-bit stable passes of the launch keys (ties in tile order) -> launch order; the
+//                   high-byte pass counts the families
+//   5. fill_descs   descriptor k from the k-th stream in launch order (writing it in the sort's last
+//                   scatter instead measured slower: the scatter's rounds expose the gather's latency)
+// The split rule is the host plan's (split plans: split_mark .. fpf_states_walk below); property columns
+// (COVT_PLAN_PROPERTIES) add a property walk per tile and their stream entries after the tile's own.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
