@@ -397,7 +397,8 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
 
     // ---- pass 1: features -> parts (items: features) ----
     uint32_t go_base = 0, P = 0;
-    bool multi_n = false;  // some feature's part count is not 1
+    bool multi_n = false;   // some feature's part count is not 1
+    bool has_poly = false;  // some feature is a polygon or multi-polygon
     for (int32_t f0 = 0; f0 < n; f0 += K) {
         uint32_t t[IPL], multi[IPL], gi[IPL], pf[IPL], ex[IPL], nm, tot;
         if (NW == 1) {  // lane-major: one byte per item
@@ -406,6 +407,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 const bool valid = f0 + ioff(k) < n;
                 t[k] = valid ? (uint32_t)((const g_u8*)types)[f0 + ioff(k)] : 0u;
                 bad_type |= t[k] > 5u;
+                has_poly |= t[k] == 2u || t[k] == 5u;
                 multi[k] = (valid && t[k] >= 3u && t[k] <= 5u) ? 1u : 0u;
                 pf[k] = valid ? 1u : 0u;
             }
@@ -417,6 +419,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 const bool valid = fl + k < n;
                 t[k] = valid ? (tw >> (8 * k)) & 0xffu : 0u;
                 bad_type |= t[k] > 5u;
+                has_poly |= t[k] == 2u || t[k] == 5u;
                 multi[k] = (valid && t[k] >= 3u && t[k] <= 5u) ? 1u : 0u;
                 pf[k] = valid ? 1u : 0u;
             }
@@ -464,6 +467,10 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
         return L;
     };
     const bool ident2 = !Coop<NW>::any(multi_n);
+    // no polygon: every part is one ring (rings = parts), so pass 2 also writes the ring offsets (the
+    // exclusive scan of the parts' vertex counts) and pass 3, with both scratch arrays, is skipped
+    const bool nopoly = !Coop<NW>::any(has_poly);
+    uint32_t V = 0, VS = 0;
     // ---- pass 2: parts -> rings (items: parts, segments: features) ----
     uint32_t po_base = 0, R = 0;
     bool poly_n = false;  // some part's ring count is not 1
@@ -523,10 +530,21 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 poly_n |= ioff(k) < L && rp[k] != 1u;
             }
             store4<NW>(part_off, p0, L, ex);
-            store4<NW>(part_scr, p0, L, scr);
+            if (nopoly) {  // ring p = part p: its coordinates start at the scan of the vertex counts
+                uint32_t vc[IPL], vex[IPL], vt;
+#pragma unroll
+                for (int k = 0; k < IPL; ++k) vc[k] = ioff(k) < L ? scr[k] >> 1 : 0u;
+                excl_scan4(sm, buf, vc, vex, vt);
+#pragma unroll
+                for (int k = 0; k < IPL; ++k) vex[k] += V;
+                store4<NW>(ring_off, p0, L, vex);
+                V = add_sat(V, vt);
+            } else {
+                store4<NW>(part_scr, p0, L, scr);
+            }
             po_base += npo;
             R = add_sat(R, tot);
-            if (Coop<NW>::any(bad_cnt) || R > rcap) break;
+            if (Coop<NW>::any(bad_cnt) || R > rcap || (nopoly && V > ccap)) break;
         }
     }
     if (Coop<NW>::any(bad_cnt) || R > rcap) { res.status = COVT_ERR_COUNT_MISMATCH; return; }
@@ -539,8 +557,10 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
 #endif
     const bool ident3 = !Coop<NW>::any(poly_n);
     // ---- pass 3: rings -> coordinates (items: rings, segments: parts) ----
-    uint32_t ro_base = 0, V = 0, VS = 0;
-    {
+    uint32_t ro_base = 0;
+    if (nopoly) {
+        VS = V;  // (no closing vertex; the checks of pass 3's end)
+    } else {
         Expand<NW, IPL> x{part_off, (int32_t)P, (int32_t)R, 0, 0, 0};
         while (x.q < x.total) {
             const int32_t r0 = x.q;
@@ -593,7 +613,7 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                 src[k] = (VS + src[k]) | (closing[k] << 31);
             }
             store4<NW>(ring_off, r0, L, ex);
-            store4<NW>(ring_scr, r0, L, src);
+            if (!closed) store4<NW>(ring_scr, r0, L, src);  // (read by pass 4 only when rings get a closing vertex)
             ro_base += nr;
             V = add_sat(V, tv);
             VS = add_sat(VS, ts);
