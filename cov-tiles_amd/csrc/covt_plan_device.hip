@@ -1123,32 +1123,34 @@ __global__ void stream_keys(const covt_stream_info* info, const int32_t* nvals, 
         atomicAdd(&totals[T_FAM + threadIdx.x], fam_n[threadIdx.x]);
 }
 
-// An unsplit plan whose batch has fewer lane streams than lane_min: its keys again without the lane family
-// (the entries were keyed with it; nothing to do otherwise -- every workgroup returns at once)
-__global__ void __launch_bounds__(256) lane_keys(const covt_stream_info* __restrict__ info, const int32_t* __restrict__ nvals,
-                                                 int64_t n, int64_t lane_min, const unsigned long long* __restrict__ totals,
-                                                 uint32_t* __restrict__ keys) {
-    if ((int64_t)totals[T_LANE] >= lane_min) return;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const covt_stream_info& si = info[i];
-        keys[i] = entry_key(si.op, nvals[i], si.byte_length, si.out_elems, si.elem_bytes, -1);
-    }
-}
-
 // ---- launch order: a stable LSD radix sort of the streams' 16-bit launch keys, two 8-bit passes of
 // three launches each: per-chunk digit counts, one workgroup's scan of them (digit-major, so chunk order
 // inside a digit), and the scatter, each wave ranking its 64 keys among equal digits with eight ballots
 constexpr int kSortBuckets = 256;
 constexpr int kSortChunk = 4096;  // keys per workgroup (4 rounds of 1024)
 
-__global__ void __launch_bounds__(256) order_hist(const uint32_t* __restrict__ keys, int64_t n, int32_t nb, int shift,
-                                                  uint32_t* __restrict__ ghist) {
+// info non-null (the first pass of an unsplit plan): a batch with fewer lane streams than lane_min gets
+// its keys again without the lane family first (the entries were keyed with it)
+__global__ void __launch_bounds__(256) order_hist(uint32_t* __restrict__ keys, int64_t n, int32_t nb, int shift,
+                                                  uint32_t* __restrict__ ghist, const covt_stream_info* __restrict__ info,
+                                                  const int32_t* __restrict__ nvals, int64_t lane_min,
+                                                  const unsigned long long* __restrict__ totals) {
     __shared__ uint32_t h[kSortBuckets];
     h[threadIdx.x] = 0;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * kSortChunk;
-    for (int j = threadIdx.x; j < kSortChunk; j += 256)
-        if (base + j < n) atomicAdd(&h[(keys[base + j] >> shift) & 255u], 1u);
+    const bool rekey = info && (int64_t)totals[T_LANE] < lane_min;
+    for (int j = threadIdx.x; j < kSortChunk; j += 256) {
+        const int64_t i = base + j;
+        if (i >= n) continue;
+        uint32_t key = keys[i];
+        if (rekey) {
+            const covt_stream_info& si = info[i];
+            key = entry_key(si.op, nvals[i], si.byte_length, si.out_elems, si.elem_bytes, -1);
+            keys[i] = key;
+        }
+        atomicAdd(&h[(key >> shift) & 255u], 1u);
+    }
     __syncthreads();
     ghist[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
@@ -2589,7 +2591,8 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     auto launch_order = [&]() {
         const int scanned = nb > kSortFuseChunks;
         for (int pass = 0; pass < 2; ++pass) {
-            order_hist<<<nb, 256, 0, s>>>(pass ? q1 : q0, ns, nb, 8 * pass, bhist);
+            order_hist<<<nb, 256, 0, s>>>(pass ? q1 : q0, ns, nb, 8 * pass, bhist,
+                                          pass == 0 && !splitting ? p->d_info : nullptr, nvals, lane_min, totals);
             if (scanned) order_scan<<<1, 1024, 0, s>>>(bhist, (int64_t)kSortBuckets * nb);
             if (pass == 0) order_scatter<<<nb, 1024, 0, s>>>(q0, nullptr, ns, nb, 0, bhist, scanned, q1, v0, nullptr);
             else order_scatter<<<nb, 1024, 0, s>>>(q1, v0, ns, nb, 8, bhist, scanned, q0, v1, fam_tot);
@@ -2597,8 +2600,8 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         return hipGetLastError();
     };
     // unsplit plans: the launch keys written with the stream entries, taking every small RLE stream to the
-    // lane family (lane_keys redoes them when the batch has fewer such streams than lane_min: the count
-    // is known once the entries are written); split plans: stream_keys after split_mark
+    // lane family (the sort's first pass redoes them when the batch has fewer such streams than lane_min:
+    // the count is known once the entries are written); split plans: stream_keys after split_mark
     uint32_t* ekeys = splitting ? nullptr : q0;
     const int32_t lm = lane_max;
     if (n_tiles) {
@@ -2629,8 +2632,6 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     }
     const int blocks_s = (int)((ns + 255) / 256);
     if (ns > 0 && !splitting) {
-        lane_keys<<<256, 256, 0, s>>>(p->d_info, nvals, ns, lane_min, totals, q0);
-        DCHK(hipGetLastError());
         DCHK(launch_order());
         fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, q0, v1, ns, p->d_desc);
         DCHK(hipGetLastError());
