@@ -736,6 +736,15 @@ __device__ int walk_genc_fast(FastGenc& f, E& emit) {
             const int ctype = (int)(ce >> 19) & 0xff;
             if (kind == 1 && ns > (uint32_t)kFwGeo) return kFastFallback;
             o += (int32_t)(ce & 0xffu);
+            if (kind == 2) {  // a property column (most records): only its data bytes, in a loop of its own
+                for (uint32_t s = 0; s < ns; ++s) {
+                    const uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[f.at(o)]);
+                    if (!se) return kFastFallback;
+                    d += (int32_t)(se >> 8);
+                    o += (int32_t)(se & 0xffu);
+                }
+                continue;
+            }
             uint32_t present = 0;
             for (uint32_t s = 0; s < ns; ++s) {
                 const int32_t q = f.at(o);
