@@ -2283,6 +2283,14 @@ struct LaneBytes {  // the lane's stream through a window in its LDS slot; one-d
         for (int k = 0; k < kLaneSlot; ++k) slot[k * 256] = st[k];
         cq = -1;
     }
+    // bytes [p, p + 4) little-endian (two slot dwords and a byte align)
+    __device__ __forceinline__ uint32_t at4(int32_t p) {
+        if (p + 4 - w0 > 4 * kLaneSlot) load(p);
+        const int32_t a = p - w0, q = a >> 2;
+        const uint32_t d0 = slot[q * 256], d1 = (a & 3) ? slot[(q + 1) * 256] : 0u;
+        cq = -1;
+        return __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)(a & 3));
+    }
     __device__ __forceinline__ uint32_t at(int32_t p) {
         if (p - w0 >= 4 * kLaneSlot) load(p);  // slides forward (reads are sequential)
         const int32_t a = p - w0, q = a >> 2;
@@ -2392,6 +2400,33 @@ struct Pack16 {
             if ((nb & 15u) == 0) flush();
         }
     }
+    // four bytes (little-endian in v) at any byte position of the packet
+    __device__ __forceinline__ void put4(uint32_t v) {
+        const uint32_t sh = 8u * (nb & 3u), k = (nb >> 2) & 3u;
+        const uint32_t lo = v << sh, hi = sh ? v >> (32u - sh) : 0u;
+        const uint32_t mlo = 0xffffffffu << sh;
+        uint32_t w[4] = {w0, w1, w2, w3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((uint32_t)j == k) w[j] = (w[j] & ~mlo) | lo;
+        w0 = w[0];
+        w1 = w[1];
+        w2 = w[2];
+        w3 = w[3];
+        nb += 4;
+        if ((nb & 15u) < 4u) {  // crossed into the next packet: flush, carry the high bytes
+            flush();
+            w0 = hi;
+        } else if (sh) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((uint32_t)j == k + 1u) w[j] = hi;
+            w0 = w[0];
+            w1 = w[1];
+            w2 = w[2];
+            w3 = w[3];
+        }
+    }
     __device__ __forceinline__ void finish() {
         if (nb & 15u) flush();
     }
@@ -2449,14 +2484,18 @@ __device__ void lane_rle_byte(LaneBytes& in, int32_t n, uint8_t* out, bool check
         } else {
             const int32_t cnt = 0x100 - (int32_t)control;
             if (o + cnt > in.avail) { err = COVT_ERR_TRUNCATED; return; }
-            for (int32_t i = 0; i < cnt; ++i) {
-                const uint32_t b = in.at(o++);
-                if (done < n) {
-                    bad |= b > 5u;
-                    pk.put8(b);
-                    ++done;
-                }
+            const int32_t take = cnt < n - done ? cnt : n - done;  // literals past n are skipped
+            int32_t i = 0;
+            if (!check) {  // (no value check) four bytes per step
+                for (; i + 4 <= take; i += 4, o += 4) pk.put4(in.at4(o));
             }
+            for (; i < take; ++i) {
+                const uint32_t b = in.at(o++);
+                bad |= b > 5u;
+                pk.put8(b);
+            }
+            done += take;
+            o += cnt - take;
         }
     }
     pk.finish();
