@@ -47,6 +47,7 @@ struct covt_device_plan {
     covt_geom_info* d_ginfo = nullptr;
     covt_geom_desc* d_gdesc = nullptr;
     void* prop_arena = nullptr;    // property columns (COVT_PLAN_PROPERTIES): records, infos, descriptors
+    void* scratch = nullptr;       // creation-time scratch (the property walk's record slots), freed on the way
     int64_t n_props = 0, prop_bytes = 0;
     covt_prop_info* d_pinfo = nullptr;
     covt_prop_desc* d_pdesc = nullptr;
@@ -1164,31 +1165,7 @@ __global__ void __launch_bounds__(256) order_hist(uint32_t* __restrict__ keys, i
     ghist[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
 
-// exclusive scan of m counts in one workgroup (segments of ceil(m / 1024) per thread)
-__global__ void __launch_bounds__(1024) order_scan(uint32_t* __restrict__ a, int64_t m) {
-    __shared__ uint32_t part[1024];
-    const int64_t seg = (m + 1023) / 1024, lo = threadIdx.x * seg, hi = lo + seg < m ? lo + seg : m;
-    uint32_t sum = 0;
-#pragma unroll 16
-    for (int64_t k = lo; k < hi; ++k) sum += a[k];  // (independent loads: 16 in flight per thread)
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele over the 1024 segment sums
-        const uint32_t x = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += x;
-        __syncthreads();
-    }
-    uint32_t run = part[threadIdx.x] - sum;
-#pragma unroll 16
-    for (int64_t k = lo; k < hi; ++k) {
-        const uint32_t c = a[k];
-        a[k] = run;
-        run += c;
-    }
-}
-
-// vals null: the identity (the first pass).  scanned: gpos holds order_scan's offsets; else gpos holds
+// vals null: the identity (the first pass).  scanned: gpos holds the scanned offsets; else gpos holds
 // order_hist's counts and each workgroup sums the ones before it (nb <= kSortFuseChunks: one launch less)
 constexpr int kSortFuseChunks = 512;
 __global__ void __launch_bounds__(1024) order_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
@@ -2056,13 +2033,14 @@ struct PropCountEmit {
 };
 struct PropRecEmit {
     PropRaw* recs;    // this tile's first record
-    int32_t* rtile;
+    int32_t* rtile;   // (null: the tile's slots, no tile column)
     int32_t t;
     int64_t n = 0, k0 = 0;
+    int64_t cap = INT64_MAX;  // records kept (slots: kPropSlots; the rest are only counted)
     __device__ void operator()(const PropRaw& q) {
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == 0 && n < cap) {
             recs[n] = q;
-            rtile[n] = t;
+            if (rtile) rtile[n] = t;
         }
         ++n;
     }
@@ -2072,7 +2050,8 @@ struct PropRecEmit {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         __builtin_amdgcn_wave_barrier();
-        for (int64_t j = k0 + threadIdx.x; j < n; j += 64)
+        const int64_t e = n < cap ? n : cap;
+        for (int64_t j = k0 + threadIdx.x; j < e; j += 64)
             for (int q = 0; q < 4; ++q)
                 if (recs[j].s_off[q] >= 0) recs[j].s_off[q] += data_start;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -2098,7 +2077,12 @@ __device__ __forceinline__ int prop_walk_tile(Rd<true>& r, PE& e, PropSm* tab, i
     return prop_walk_genc(r, e, tab);
 }
 
-// one wave per tile (tiles the Id / Geometry walk failed contribute nothing); EMIT: write the records
+// one wave per tile (tiles the Id / Geometry walk failed contribute nothing).  EMIT false: count the
+// records, keeping the first kPropSlots of each tile in its slots (`recs` = the slot array, null: count
+// only); EMIT true: write them at pcb[t] -- only for the tiles with more records than slots when `pcnt` is
+// given (the others are copied from their slots by prop_compact)
+constexpr int kPropSlots = 256;
+constexpr size_t kPropSlotBytes = (size_t)2 << 30;  // slot memory a plan may take (10k tiles: 328 MB)
 template <bool EMIT>
 __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
                           const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format,
@@ -2110,6 +2094,7 @@ __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
         if (!EMIT && threadIdx.x == 0) pcnt[t] = 0;
         return;
     }
+    if (EMIT && pcnt && pcnt[t] <= kPropSlots) return;  // (in its slots)
     Rd<true> r;
     r.t = bytes + offs[t];
     r.len = (int64_t)sizes[t];
@@ -2118,11 +2103,32 @@ __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
     if (EMIT) {
         PropRecEmit e{recs + pcb[t], rtile + pcb[t], t};
         (void)prop_walk_tile(r, e, tab, format);
+    } else if (recs) {
+        PropRecEmit e{recs + (size_t)t * kPropSlots, nullptr, t};
+        e.cap = kPropSlots;
+        const int st = prop_walk_tile(r, e, tab, format);
+        if (threadIdx.x == 0) pcnt[t] = st ? 0 : e.n;  // (the Id / Geometry walk succeeded: so does this one)
     } else {
         PropCountEmit e;
         const int st = prop_walk_tile(r, e, tab, format);
-        if (threadIdx.x == 0) pcnt[t] = st ? 0 : e.n;  // (the Id / Geometry walk succeeded: so does this one)
+        if (threadIdx.x == 0) pcnt[t] = st ? 0 : e.n;
     }
+}
+
+// the records of the tiles whose records fit their slots -> their place at pcb[t] (a wave per tile)
+__global__ void __launch_bounds__(64) prop_compact(const PropRaw* __restrict__ slots, const int64_t* __restrict__ pcnt,
+                                                   const int64_t* __restrict__ pcb, int32_t n_tiles,
+                                                   PropRaw* __restrict__ recs, int32_t* __restrict__ rtile) {
+    const int32_t t = (int32_t)blockIdx.x;
+    if (t >= n_tiles) return;
+    const int64_t n = pcnt[t];
+    if (n <= 0 || n > kPropSlots) return;
+    static_assert(sizeof(PropRaw) % 16 == 0, "records copy as 16-byte words");
+    constexpr int kW = (int)(sizeof(PropRaw) / 16);
+    const uint4* src = (const uint4*)(slots + (size_t)t * kPropSlots);
+    uint4* dst = (uint4*)(recs + pcb[t]);
+    for (int64_t i = threadIdx.x; i < n * kW; i += 64) dst[i] = src[i];
+    for (int64_t i = threadIdx.x; i < n; i += 64) rtile[pcb[t] + i] = t;
 }
 
 enum { PA_IN = 0, PA_PAYLOAD = 1, PA_LANE = 2, PA_COST = 3, PA_CMAX = 4, PA_N = 8 };
@@ -2482,6 +2488,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     int64_t *pcnt = nullptr, *pcb = nullptr, *rs_cnt = nullptr, *rs_ob = nullptr, *rsb = nullptr, *rob = nullptr;
     unsigned long long* pacc = nullptr;
     PropRaw* recs = nullptr;
+    PropRaw* prop_slots = nullptr;  // the property walk's per-tile record slots (freed once copied)
     int32_t* rtile = nullptr;
     int64_t n_rec = 0;
     size_t pscan_tmp = 0, psort_tmp = 0;
@@ -2494,8 +2501,15 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         pcb = (int64_t*)(ta + o_pcb);
         pacc = (unsigned long long*)(ta + o_pacc);
         DCHK(hipMemsetAsync(pacc, 0, 256, s));
+        // one walk counting the records and keeping up to kPropSlots per tile (batches whose slots would
+        // take more than kPropSlotBytes walk twice: count, then emit)
+        void* pslots = nullptr;
+        const size_t slot_bytes = (size_t)n_tiles * kPropSlots * sizeof(PropRaw);
+        if (slot_bytes <= kPropSlotBytes && n_tiles > 0) DCHK(plan_malloc(&pslots, slot_bytes, p->dev, s));
+        prop_slots = (PropRaw*)pslots;
+        p->scratch = pslots;  // (a failure on the way frees it with the plan)
         prop_walk<false><<<(int)nt1, 64, kPropWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
-                                                           p->d_status, pcnt, nullptr, nullptr, nullptr);
+                                                           p->d_status, pcnt, nullptr, prop_slots, nullptr);
         DCHK(hipGetLastError());
         DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, pcnt, pcb, (int)nt1, s));
         DCHK(hipMemcpyAsync(&n_rec, pcb + n_tiles, 8, hipMemcpyDeviceToHost, s));
@@ -2538,9 +2552,19 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         p->d_pinfo = (covt_prop_info*)(pa + po_pi);
         p->d_pdesc = (covt_prop_desc*)(pa + po_pd);
         if (n_rec > 0) {
+            if (prop_slots) {  // from the slots; the tiles with more records walk again
+                prop_compact<<<n_tiles, 64, 0, s>>>(prop_slots, pcnt, pcb, n_tiles, recs, rtile);
+                DCHK(hipGetLastError());
+            }
             prop_walk<true><<<n_tiles, 64, kPropWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
-                                                             format, p->d_status, nullptr, pcb, recs, rtile);
+                                                             format, p->d_status, prop_slots ? pcnt : nullptr, pcb, recs,
+                                                             rtile);
             DCHK(hipGetLastError());
+        }
+        if (prop_slots) {
+            p->scratch = nullptr;
+            DCHK(hipFreeAsync(prop_slots, s));  // (stream-ordered: after the copy)
+            prop_slots = nullptr;
         }
         const int32_t lane_max0 = lane_limits(o.lane_max_bytes, o.lane_max_values);
         prop_sizes<<<(int)((nr1 + 255) / 256), 256, 0, s>>>(recs, n_rec, id_mode, lane_max0, rs_cnt, rs_ob, pacc);
@@ -2576,11 +2600,18 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, dscan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)(ns + 1), s));
     const size_t n = (size_t)(ns > 0 ? ns : 1);
     const int32_t nb = (int32_t)((n + kSortChunk - 1) / kSortChunk);  // counting-sort chunks
+    // more chunks than one scatter workgroup sums itself: their counts scanned by hipcub into bscan
+    const bool scanned = nb > kSortFuseChunks;
+    const size_t mh = (size_t)kSortBuckets * nb;
+    size_t hscan_tmp = 0;
+    if (scanned)
+        DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, hscan_tmp, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)mh, s));
     // RLE chunk records: every candidate reserves (its cost / split_chunk + 2) <= the batch's
     const int64_t chunk_cap = splitting ? hd[2] / o.split_chunk + 2 * ns + 2 : 0;
     const size_t o_nv = up256(n * sizeof(covt_stream_info)), o_k0 = o_nv + up256(n * 4), o_k1 = o_k0 + up256(n * 4),
                  o_v0 = o_k1 + up256(n * 4), o_v1 = o_v0 + up256(n * 4), o_h = o_v1 + up256(n * 4),
-                 o_d = o_h + up256((size_t)kSortBuckets * nb * 4),
+                 o_hs = o_h + up256(mh * 4), o_ht = o_hs + (scanned ? up256(mh * 4) : 0),
+                 o_d = o_ht + (scanned ? up256(hscan_tmp) : 0),
                  o_sf = o_d + up256(n * sizeof(covt_stream_desc)),
                  o_sn = o_sf + up256(n), o_dn = o_sn + up256(n * 8), o_dp = o_dn + up256((n + 1) * 8),
                  o_rl = o_dp + up256((n + 1) * 8), o_fl = o_rl + up256(n * 4), o_rb = o_fl + up256(n * 4),
@@ -2593,18 +2624,21 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     uint32_t *q0 = (uint32_t*)(sa + o_k0), *q1 = (uint32_t*)(sa + o_k1), *v0 = (uint32_t*)(sa + o_v0),
              *v1 = (uint32_t*)(sa + o_v1);
     uint32_t* bhist = (uint32_t*)(sa + o_h);
+    uint32_t* bscan = scanned ? (uint32_t*)(sa + o_hs) : bhist;
     p->d_order = v1;
     p->d_desc = (covt_stream_desc*)(sa + o_d);
     // launch order: the stable radix sort of the launch keys q0 (low byte: -> q1, v0; high byte: -> q0, v1)
     unsigned long long* fam_tot = splitting ? nullptr : totals + T_FAM;  // (split plans: stream_keys counts)
     auto launch_order = [&]() {
-        const int scanned = nb > kSortFuseChunks;
         for (int pass = 0; pass < 2; ++pass) {
             order_hist<<<nb, 256, 0, s>>>(pass ? q1 : q0, ns, nb, 8 * pass, bhist,
                                           pass == 0 && !splitting ? p->d_info : nullptr, nvals, lane_min, totals);
-            if (scanned) order_scan<<<1, 1024, 0, s>>>(bhist, (int64_t)kSortBuckets * nb);
-            if (pass == 0) order_scatter<<<nb, 1024, 0, s>>>(q0, nullptr, ns, nb, 0, bhist, scanned, q1, v0, nullptr);
-            else order_scatter<<<nb, 1024, 0, s>>>(q1, v0, ns, nb, 8, bhist, scanned, q0, v1, fam_tot);
+            if (scanned) {
+                const hipError_t e = hipcub::DeviceScan::ExclusiveSum(sa + o_ht, hscan_tmp, bhist, bscan, (int)mh, s);
+                if (e != hipSuccess) return e;
+            }
+            if (pass == 0) order_scatter<<<nb, 1024, 0, s>>>(q0, nullptr, ns, nb, 0, bscan, scanned, q1, v0, nullptr);
+            else order_scatter<<<nb, 1024, 0, s>>>(q1, v0, ns, nb, 8, bscan, scanned, q0, v1, fam_tot);
         }
         return hipGetLastError();
     };
@@ -2718,7 +2752,7 @@ void covt_device_plan_destroy(covt_device_plan* p) {
     const bool sw = hipGetDevice(&cur) == hipSuccess && cur != p->dev && hipSetDevice(p->dev) == hipSuccess;
     // (hipFree's implicit device synchronization, then the arenas back to the pool)
     (void)hipDeviceSynchronize();
-    for (void* q : {p->tile_arena, p->stream_arena, p->desc_arena, p->geo_arena, p->prop_arena})
+    for (void* q : {p->tile_arena, p->stream_arena, p->desc_arena, p->geo_arena, p->prop_arena, p->scratch})
         if (q) (void)hipFreeAsync(q, nullptr);
     (void)hipStreamSynchronize(nullptr);
     if (sw) (void)hipSetDevice(cur);
