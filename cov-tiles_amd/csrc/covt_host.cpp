@@ -928,10 +928,10 @@ void plan_property(PlanPart* p, int32_t t, int64_t tile_off, const PropRaw& q, i
     covt_prop_info pi = prop_info_of(q, t, tile_off);
     PropStreams ps;
     prop_streams(q, id_mode, ps);  // covt_props_plan.h: the same rule as the device plan
-    for (int k = 0; k < ps.n; ++k) {
-        const int role = ps.role[k];
-        const int64_t n = ps.count[k];
-        const int elem = ps.elem[k];
+    for (int role = 0; role < 3; ++role) {
+        if (!(ps.has >> role & 1u)) continue;
+        const int64_t n = ps.count[role];
+        const int elem = ps.elem[role];
         covt_stream_info si{};
         si.tile = t;
         si.layer = q.layer;
@@ -941,7 +941,7 @@ void plan_property(PlanPart* p, int32_t t, int64_t tile_off, const PropRaw& q, i
         si.column_type = q.ctype;
         si.num_values = q.s_nv[role];
         si.byte_length = q.s_bl[role];
-        si.op = ps.op[k];
+        si.op = ps.op[role];
         si.elem_bytes = elem;
         si.in_off = tile_off + q.s_off[role];
         si.out_elems = n;

@@ -553,7 +553,13 @@ constexpr int kFastFallback = 1;
 struct FastSmem {
     uint32_t win[kFwBytes / 4 + 4];
     uint32_t stab[kFwSpan];  // stream record at j: length | byteLength << 8 (0: not fast)
-    uint32_t ctab[kFwSpan];  // column header at j: length | numStreams << 8 | kind << 17 | columnType << 19 (0: not fast)
+    uint32_t ctab[kFwSpan];  // column header at j: length | numStreams << 8 | kind << 17 | columnType << 19 |
+                             // min(dataType, 31) << 27 (0: not fast)
+};
+// the property walk's extra tables (after FastSmem; the Id walk neither builds nor allocates them)
+struct FastSmemRec {
+    uint32_t rtab[kFwSpan];  // stream record at j: numValues | (StreamType of its name + 1) << 28
+    uint8_t etab[kFwSpan];   // its encoding
 };
 // LDS: Rd<true>'s 512-byte window, then the geometry table (kFwGeo entries for the fast walk, 256 for the
 // serial one, which overlaps the fast walk's tables: it only runs once they are abandoned).  Small
@@ -562,12 +568,37 @@ constexpr size_t kFastSmemOffset = 512 + kFwGeo * 16;
 constexpr size_t kWalkLds = kFastSmemOffset + sizeof(FastSmem) > 512 + 256 * 16 ? kFastSmemOffset + sizeof(FastSmem)
                                                                                   : 512 + 256 * 16;
 
+// StreamType of a stream name of n bytes (lo: bytes 0-7, hi: 8-15, masked to n; -1: none)
+__device__ __forceinline__ int fast_name_type(uint32_t n, uint64_t lo, uint64_t hi) {
+    int type = -1;
+    if (n >= 4 && n <= 16) {
+#define COVT_FNAME(str, v)                                                              \
+    {                                                                                   \
+        constexpr uint64_t n_ = cstrlen(str), l_ = pk(str, 0, n_), h_ = pk(str, 8, n_); \
+        if (n == n_ && lo == l_ && hi == h_) type = v;                                  \
+    }
+        COVT_FNAME("data", ST_DATA)
+        COVT_FNAME("length", ST_LENGTH)
+        COVT_FNAME("present", ST_PRESENT)
+        COVT_FNAME("dictionary", ST_DICTIONARY)
+        COVT_FNAME("geometry_types", ST_GEOMETRY_TYPES)
+        COVT_FNAME("geometry_offsets", ST_GEOMETRY_OFFSETS)
+        COVT_FNAME("part_offsets", ST_PART_OFFSETS)
+        COVT_FNAME("ring_offsets", ST_RING_OFFSETS)
+        COVT_FNAME("vertex_offsets", ST_VERTEX_OFFSETS)
+        COVT_FNAME("vertex_buffer", ST_VERTEX_BUFFER)
+#undef COVT_FNAME
+    }
+    return type;
+}
+
 struct FastGenc {
     const uint8_t* t;
     int32_t len;
     int32_t wb;  // tile offset of window byte 0 (16-byte aligned address; may be < 0 at the tile start)
     uint32_t segs;  // window positions [256 k, 256 k + 256) whose record tables are built: bit k
     FastSmem* fs;
+    FastSmemRec* fr = nullptr;  // the property walk's tables (null: not built)
     // bytes [q, q + 8) of the window, q per lane (q <= kFwBytes - 8)
     __device__ __forceinline__ uint64_t peek8(int32_t q) const {
         const uint32_t* w = fs->win;
@@ -603,10 +634,11 @@ struct FastGenc {
     __device__ void build(int sg) {
         const int l = threadIdx.x;
         constexpr uint64_t kId = pk("id", 0, 2), kGeo = pk("geometry", 0, 8);
-#pragma unroll
+#pragma unroll 1
         for (int i = 0; i < 4; ++i) {
             const int32_t q = 256 * sg + l + 64 * i, j = wb + q;
-            uint32_t se = 0, ce = 0;
+            uint32_t se = 0, ce = 0, re = 0;
+            uint8_t ee = 0;
             const uint64_t nm = peek8(q + 1);              // name bytes (a stream / column name)
             const uint32_t n = fs->win[q >> 2] >> (8 * (q & 3)) & 0xffu;  // its length (one LEB128 byte)
             if (j >= 0 && n < 0x80u) {
@@ -625,6 +657,20 @@ struct FastGenc {
                     const uint32_t bl = (x & 0x3fffu) | ((x & 0x3fff0000u) >> 2);
                     const int32_t slen = 1 + (int32_t)n + e2 + 2;
                     if (bl < (1u << 24) && j + slen <= len) se = (uint32_t)slen | (bl << 8);
+                    if (fr && se) {  // the property walk's fields: name's StreamType, numValues, encoding
+                        uint32_t v = (uint32_t)w;
+                        v = (e1 >= 3 ? v : v & ((1u << (8 * (e1 + 1))) - 1u)) & 0x7f7f7f7fu;
+                        v = (v & 0x007f007fu) | ((v & 0x7f007f00u) >> 1);
+                        const uint32_t nv = (v & 0x3fffu) | ((v & 0x3fff0000u) >> 2);
+                        const uint64_t lo = n >= 8 ? nm : nm & ((1ull << (8 * n)) - 1);
+                        uint64_t hi = 0;
+                        if (n > 8) {
+                            hi = peek8(q + 9);
+                            if (n < 16) hi &= (1ull << (8 * (n - 8))) - 1;
+                        }
+                        re = nv | ((uint32_t)(fast_name_type(n, lo, hi) + 1) << 28);
+                        ee = (uint8_t)(w >> (8 * (e2 + 1)));
+                    }
                 }
                 // column header: dataType, columnType, numStreams (1-2 byte LEB128, <= 256)
                 const uint32_t b2 = (uint32_t)(w >> 16) & 0xffu, b3 = (uint32_t)(w >> 24) & 0xffu;
@@ -636,11 +682,15 @@ struct FastGenc {
                     const bool id = n == 2 && (nm & 0xffffull) == kId;
                     const bool geo = (n == 8 && nm == kGeo) || dtype == 6;
                     const uint32_t kind = id ? 0u : geo ? 1u : 2u;
-                    ce = (uint32_t)clen | (ns << 8) | (kind << 17) | (ctype << 19);
+                    ce = (uint32_t)clen | (ns << 8) | (kind << 17) | (ctype << 19) | ((dtype < 31u ? dtype : 31u) << 27);
                 }
             }
             fs->stab[q] = se;
             fs->ctab[q] = ce;
+            if (fr) {
+                fr->rtab[q] = re;
+                fr->etab[q] = ee;
+            }
         }
         segs |= 1u << sg;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -683,25 +733,7 @@ struct FastGenc {
             hi = upeek8(q + 9);
             if (n < 16) hi &= (1ull << (8 * (n - 8))) - 1;
         }
-        type = -1;
-        if (n >= 4 && n <= 16) {
-#define COVT_FNAME(str, v)                                                              \
-    {                                                                                   \
-        constexpr uint64_t n_ = cstrlen(str), l_ = pk(str, 0, n_), h_ = pk(str, 8, n_); \
-        if (n == n_ && lo == l_ && hi == h_) type = v;                                  \
-    }
-            COVT_FNAME("data", ST_DATA)
-            COVT_FNAME("length", ST_LENGTH)
-            COVT_FNAME("present", ST_PRESENT)
-            COVT_FNAME("dictionary", ST_DICTIONARY)
-            COVT_FNAME("geometry_types", ST_GEOMETRY_TYPES)
-            COVT_FNAME("geometry_offsets", ST_GEOMETRY_OFFSETS)
-            COVT_FNAME("part_offsets", ST_PART_OFFSETS)
-            COVT_FNAME("ring_offsets", ST_RING_OFFSETS)
-            COVT_FNAME("vertex_offsets", ST_VERTEX_OFFSETS)
-            COVT_FNAME("vertex_buffer", ST_VERTEX_BUFFER)
-#undef COVT_FNAME
-        }
+        type = fast_name_type(n, lo, hi);
         const uint64_t w = upeek8(q + 1 + (int32_t)n);
         const uint64_t stop = ~w & 0x8080808080808080ull;  // (the table checked: numValues <= 4 bytes)
         const int e1 = __builtin_ctzll(stop) >> 3;
@@ -1663,9 +1695,65 @@ struct PropSm {  // a property column's stream, as the Gen C walk reads it
 };
 enum { PR_PRESENT = 1, PR_DATA = 2, PR_LENGTH = 4, PR_DICTIONARY = 8, PR_PRESENT_LANG = 16 };
 constexpr int kPropMaxStreams = 256;  // numStreams bound of the walk (walk_genc: > 256 is BAD_HEADER)
-// LDS: Rd<true>'s window, the fast walk's window and tables (walk_count's layout), then the stream table
-constexpr size_t kPropTabOffset = (kFastSmemOffset + sizeof(FastSmem) + 15) & ~(size_t)15;
-constexpr size_t kPropWalkLds = kPropTabOffset + kPropMaxStreams * sizeof(PropSm);
+// LDS: Rd<true>'s window, the fast walk's window and tables (walk_count's layout)
+constexpr size_t kPropRecOffset = (kFastSmemOffset + sizeof(FastSmem) + 15) & ~(size_t)15;
+constexpr size_t kPropWalkLds = kPropRecOffset + sizeof(FastSmemRec) > kWalkLds ? kPropRecOffset + sizeof(FastSmemRec) : kWalkLds;
+
+// A property column's stream table in registers: entry s in lane s % 64, slot s / 64 (32 VGPRs).  It
+// was 7 KB of LDS per wave, which halved the walk's resident waves against the Id walk's -- and the walk
+// is a latency-bound chain, so resident tiles set its rate.
+struct PropTab {
+    uint32_t h0[4], h8[4];
+    int32_t noff[4], nlen[4], nv[4], bl[4], off[4];
+    uint32_t er[4];  // enc | role << 16
+    template <class T>
+    static __device__ __forceinline__ T pick(const T (&a)[4], uint32_t j) {  // a[j], j uniform
+        return j == 0 ? a[0] : j == 1 ? a[1] : j == 2 ? a[2] : a[3];
+    }
+    __device__ __forceinline__ void set(uint32_t s, const PropSm& v) {  // (s, v uniform)
+        // selects, not conditional stores: those were merged into one store at a computed index (scratch)
+        const bool me = threadIdx.x == (s & 63u);
+        const uint32_t j = s >> 6, e = (uint32_t)v.enc | ((uint32_t)v.role << 16);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const bool w = me && k == j;
+            h0[k] = w ? v.h0 : h0[k];
+            h8[k] = w ? v.h8 : h8[k];
+            noff[k] = w ? v.noff : noff[k];
+            nlen[k] = w ? v.nlen : nlen[k];
+            nv[k] = w ? v.nv : nv[k];
+            bl[k] = w ? v.bl : bl[k];
+            off[k] = w ? v.off : off[k];
+            er[k] = w ? e : er[k];
+        }
+    }
+    static __device__ __forceinline__ int32_t rl(int32_t x, uint32_t ln) { return __builtin_amdgcn_readlane(x, (int)ln); }
+    __device__ __forceinline__ PropSm get(uint32_t s) const {  // entry s (uniform), on every lane
+        const uint32_t j = s >> 6, ln = s & 63u;
+        PropSm v;
+        v.h0 = (uint32_t)rl((int32_t)pick(h0, j), ln);
+        v.h8 = (uint32_t)rl((int32_t)pick(h8, j), ln);
+        v.noff = rl(pick(noff, j), ln);
+        v.nlen = rl(pick(nlen, j), ln);
+        v.nv = rl(pick(nv, j), ln);
+        v.bl = rl(pick(bl, j), ln);
+        v.off = rl(pick(off, j), ln);
+        const uint32_t e = (uint32_t)rl((int32_t)pick(er, j), ln);
+        v.enc = (uint16_t)(e & 0xffffu);
+        v.role = (uint16_t)(e >> 16);
+        return v;
+    }
+    // the highest entry below ns whose role has any of `bits` (-1: none)
+    __device__ __forceinline__ int32_t last_role(uint32_t ns, uint32_t bits, uint32_t notbits) const {
+        for (int32_t j = 3; j >= 0; --j) {
+            const uint32_t k = 64u * (uint32_t)j + threadIdx.x;
+            const uint32_t role = pick(er, (uint32_t)j) >> 16;
+            const uint64_t b = __ballot(k < ns && (role & bits) && !(role & notbits));
+            if (b) return 64 * j + 63 - __builtin_clzll(b);
+        }
+        return -1;
+    }
+};
 
 // bytes [a, a + n) == bytes [b, b + n) of the tile (names; uniform)
 __device__ __forceinline__ bool names_equal(Rd<true>& r, int32_t a, int32_t b, int32_t n) {
@@ -1694,7 +1782,7 @@ __device__ __forceinline__ uint32_t names_hash(Rd<true>& r, int32_t a, int32_t n
 // Gen C property records (walk_genc's props branch): a column's streams in metadata order, roles by
 // name; LOCALIZED_DICTIONARY strings as one sub-column per present_<lang> stream
 template <class PE>
-__device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
+__device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropTab& tab) {
     const int32_t len = (int32_t)r.len;
     int32_t o = 0;
     uint64_t version, nlayers;
@@ -1743,16 +1831,12 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
                         }
                         h0 = names_hash(r, sname, (int32_t)sn);
                     }
-                    if (threadIdx.x == 0)
-                        tab[q] = PropSm{h0, h8, sname, (int32_t)sn, (int32_t)nv, (int32_t)bl, (int32_t)d, (uint16_t)enc,
-                                        (uint16_t)role};
+                    tab.set(q, PropSm{h0, h8, sname, (int32_t)sn, (int32_t)nv, (int32_t)bl, (int32_t)d, (uint16_t)enc,
+                                      (uint16_t)role});
                 }
                 d += (int64_t)bl;
             }
             if (kind != 2) continue;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
             PropRaw p = prop_init((int32_t)L, (int32_t)c, (int32_t)nfeat);
             p.name_off = name;
             p.name_len = (int32_t)cn;
@@ -1762,7 +1846,7 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
                 prop_localized(r, pe, tab, ns, p);
             } else {
                 for (uint32_t q = 0; q < (uint32_t)ns; ++q) {
-                    const PropSm sm = tab[q];
+                    const PropSm sm = tab.get(q);
                     if (sm.role & PR_PRESENT) prop_stream(p, 0, sm.off, sm.nv, sm.bl, sm.enc);
                     if (sm.role & PR_DATA) prop_stream(p, 1, sm.off, sm.nv, sm.bl, sm.enc);
                     if (sm.role & PR_LENGTH) prop_stream(p, 2, sm.off, sm.nv, sm.bl, sm.enc);
@@ -1770,7 +1854,6 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropSm* tab) {
                 }
                 pe(p);
             }
-            __builtin_amdgcn_wave_barrier();  // the table is rewritten by the next column
         }
         if (d > (int64_t)(len - o)) return COVT_ERR_TRUNCATED;
         pe.layer_end(o);  // the layer's data starts where its metadata ends
@@ -1794,41 +1877,44 @@ __device__ __forceinline__ uint32_t names_hash_win(const FastGenc& f, int32_t q,
 // The localized sub-columns of a Gen C string column from its stream table (prop_walk_genc's rule): one
 // per present_<lang> stream, with the last stream named <lang> as data and the last length / dictionary
 template <class PE>
-__device__ __forceinline__ void prop_localized(Rd<true>& r, PE& pe, const PropSm* tab, uint32_t ns, const PropRaw& p) {
-    int ls = -1, ds = -1;
-    for (uint32_t q = 0; q < ns; ++q) {
-        const uint32_t role = tab[q].role;
-        if (role & PR_LENGTH) ls = (int)q;
-        else if (role & PR_DICTIONARY) ds = (int)q;
-    }
+__device__ __forceinline__ void prop_localized(Rd<true>& r, PE& pe, const PropTab& tab, uint32_t ns, const PropRaw& p) {
+    const int32_t ls = tab.last_role(ns, PR_LENGTH, 0), ds = tab.last_role(ns, PR_DICTIONARY, PR_LENGTH);
+    const PropSm lsm = tab.get(ls >= 0 ? (uint32_t)ls : 0u), dsm = tab.get(ds >= 0 ? (uint32_t)ds : 0u);
     int32_t lang = 0;
-    for (uint32_t q = 0; q < ns; ++q) {
-        const PropSm sm = tab[q];
-        if (!(sm.role & PR_PRESENT_LANG)) continue;
-        const int32_t ll = sm.nlen - 8;
-        // the last stream named <lang>: 64 candidates per step, hash matches confirmed from the highest
-        // down (a serial all-pairs scan was ~ns^2 dependent LDS reads: ms per tile)
-        int dd = -1;
-        for (int32_t k0 = ((int32_t)ns - 1) & ~63; k0 >= 0 && dd < 0; k0 -= 64) {
-            const int32_t k = k0 + (int32_t)threadIdx.x;
-            const bool m = k < (int32_t)ns && tab[k].nlen == ll && tab[k].h0 == sm.h8;
-            uint64_t bal = __ballot(m);
-            while (bal && dd < 0) {
-                const int hi = 63 - __builtin_clzll(bal);
-                const int32_t kk = k0 + hi;
-                if (names_equal(r, tab[kk].noff, sm.noff + 8, ll)) dd = kk;
-                bal &= ~(1ull << hi);
+    for (uint32_t j = 0; 64 * j < ns; ++j) {  // the present_<lang> streams in order
+        uint64_t pm = __ballot(64 * j + threadIdx.x < ns && ((PropTab::pick(tab.er, j) >> 16) & PR_PRESENT_LANG));
+        while (pm) {
+            const uint32_t q = 64 * j + (uint32_t)__builtin_ctzll(pm);
+            pm &= pm - 1;
+            const PropSm sm = tab.get(q);
+            const int32_t ll = sm.nlen - 8;
+            // the last stream named <lang>: 64 candidates per step, hash matches confirmed from the highest
+            // down (a serial all-pairs scan was ~ns^2 dependent LDS reads: ms per tile)
+            int dd = -1;
+            for (int32_t k0 = ((int32_t)ns - 1) & ~63; k0 >= 0 && dd < 0; k0 -= 64) {
+                const uint32_t jj = (uint32_t)k0 >> 6;
+                const int32_t k = k0 + (int32_t)threadIdx.x;
+                const bool m = k < (int32_t)ns && PropTab::pick(tab.nlen, jj) == ll && PropTab::pick(tab.h0, jj) == sm.h8;
+                uint64_t bal = __ballot(m);
+                while (bal && dd < 0) {
+                    const int hi = 63 - __builtin_clzll(bal);
+                    if (names_equal(r, PropTab::rl(PropTab::pick(tab.noff, jj), (uint32_t)hi), sm.noff + 8, ll)) dd = k0 + hi;
+                    bal &= ~(1ull << hi);
+                }
             }
+            PropRaw x = p;
+            x.lang = lang++;
+            x.lang_off = sm.noff + 8;
+            x.lang_len = ll;
+            prop_stream(x, 0, sm.off, sm.nv, sm.bl, sm.enc);
+            if (dd >= 0) {
+                const PropSm dm = tab.get((uint32_t)dd);
+                prop_stream(x, 1, dm.off, dm.nv, dm.bl, dm.enc);
+            }
+            if (ls >= 0) prop_stream(x, 2, lsm.off, lsm.nv, lsm.bl, lsm.enc);
+            if (ds >= 0) prop_stream(x, 3, dsm.off, dsm.nv, dsm.bl, dsm.enc);
+            pe(x);
         }
-        PropRaw x = p;
-        x.lang = lang++;
-        x.lang_off = sm.noff + 8;
-        x.lang_len = ll;
-        prop_stream(x, 0, sm.off, sm.nv, sm.bl, sm.enc);
-        if (dd >= 0) prop_stream(x, 1, tab[dd].off, tab[dd].nv, tab[dd].bl, tab[dd].enc);
-        if (ls >= 0) prop_stream(x, 2, tab[ls].off, tab[ls].nv, tab[ls].bl, tab[ls].enc);
-        if (ds >= 0) prop_stream(x, 3, tab[ds].off, tab[ds].nv, tab[ds].bl, tab[ds].enc);
-        pe(x);
     }
 }
 
@@ -1837,7 +1923,7 @@ __device__ __forceinline__ void prop_localized(Rd<true>& r, PE& pe, const PropSm
 // kFastFallback when the tile leaves the fast grammar (the caller walks it with prop_walk_genc); a
 // successful fast walk emits the same records.
 template <class PE>
-__device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropSm* tab) {
+__device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropTab& tab) {
     const int32_t len = f.len;
     int32_t o = 0;
     uint32_t version, nlayers;
@@ -1864,9 +1950,8 @@ __device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropSm* tab
                 }
                 continue;
             }
-            const uint64_t hw = f.upeek8(qc);
-            const int32_t n = (int32_t)(hw & 0xffu);  // the name's length (one LEB128 byte)
-            const int dtype = (int)(f.upeek8(qc + 1 + n) & 0xffu);
+            const int32_t n = (int32_t)(f.upeek8(qc) & 0xffu);  // the name's length (one LEB128 byte)
+            const int dtype = (int)(ce >> 27);  // (min(dataType, 31): the same property type)
             const int ctype = (int)(ce >> 19) & 0xff;
             PropRaw p = prop_init((int32_t)L, (int32_t)c, (int32_t)nfeat);
             p.name_off = o + 1;
@@ -1874,14 +1959,16 @@ __device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropSm* tab
             p.type = genc_prop_type(dtype);
             p.ctype = ctype;
             const bool localized = p.type == COVT_PROP_STRING && ctype == 2;
+            if (localized && ns > (uint32_t)kPropMaxStreams) return kFastFallback;  // (the table's bound)
             o += (int32_t)(ce & 0xffu);
             for (uint32_t s = 0; s < ns; ++s) {
                 const int32_t q = f.at(o);
                 const uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[q]);
+                const uint32_t re = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fr->rtab[q]);
+                const int enc = __builtin_amdgcn_readfirstlane((int)f.fr->etab[q]);
                 if (!se) return kFastFallback;
-                int type, enc;
-                int32_t nv;
-                f.rec(q, se, type, nv, enc);
+                const int type = (int)(re >> 28) - 1;
+                const int32_t nv = (int32_t)(re & 0x0fffffffu);
                 const int32_t bl = (int32_t)(se >> 8);
                 const uint32_t role = type >= ST_PRESENT && type <= ST_DICTIONARY ? 1u << type : 0u;
                 if (localized) {
@@ -1893,8 +1980,7 @@ __device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropSm* tab
                         h8 = names_hash_win(f, q + 9, sn - 8);
                     }
                     const uint32_t h0 = names_hash_win(f, q + 1, sn);
-                    if (threadIdx.x == 0)
-                        tab[s] = PropSm{h0, h8, o + 1, sn, nv, bl, (int32_t)d, (uint16_t)enc, (uint16_t)rl};
+                    tab.set(s, PropSm{h0, h8, o + 1, sn, nv, bl, (int32_t)d, (uint16_t)enc, (uint16_t)rl});
                 } else {  // the roles applied in metadata order (the last stream of a role wins)
                     if (role) prop_stream(p, type, d, nv, bl, enc);
                 }
@@ -1902,11 +1988,7 @@ __device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropSm* tab
                 o += (int32_t)(se & 0xffu);
             }
             if (localized) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                __builtin_amdgcn_wave_barrier();
                 prop_localized(r, pe, tab, ns, p);
-                __builtin_amdgcn_wave_barrier();  // the table is rewritten by the next column
             } else {
                 pe(p);
             }
@@ -2046,6 +2128,9 @@ struct PropRecEmit {
     }
     __device__ void layer_begin() { k0 = n; }
     __device__ void layer_end(int64_t data_start) {  // Gen C: data offsets relative to the layer's data start
+#ifdef COVT_PROPX_NOLAYERFIX
+        return;
+#endif
         if (!data_start) return;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -2062,7 +2147,7 @@ struct PropRecEmit {
 
 // a tile's property records: Gen C through the fast walk first (the serial walk on a fallback)
 template <class PE>
-__device__ __forceinline__ int prop_walk_tile(Rd<true>& r, PE& e, PropSm* tab, int32_t format) {
+__device__ __forceinline__ int prop_walk_tile(Rd<true>& r, PE& e, PropTab& tab, int32_t format) {
     if (format != COVT_FORMAT_GENC) return prop_walk_gend(r, e);
     FastGenc f;
     f.t = r.t;
@@ -2070,6 +2155,7 @@ __device__ __forceinline__ int prop_walk_tile(Rd<true>& r, PE& e, PropSm* tab, i
     f.wb = -(int32_t)0x40000000;
     f.segs = 0;
     f.fs = (FastSmem*)((uint8_t*)covt_walk_win + kFastSmemOffset);
+    f.fr = (FastSmemRec*)((uint8_t*)covt_walk_win + kPropRecOffset);
     const PE fresh = e;
     const int st = prop_walk_genc_fast(f, r, e, tab);
     if (st != kFastFallback) return st;
@@ -2099,11 +2185,15 @@ __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
     r.t = bytes + offs[t];
     r.len = (int64_t)sizes[t];
     r.wo = -(int64_t)0x40000000;
-    PropSm* tab = (PropSm*)((uint8_t*)covt_walk_win + kPropTabOffset);
+    PropTab tab;
     if (EMIT) {
         PropRecEmit e{recs + pcb[t], rtile + pcb[t], t};
         (void)prop_walk_tile(r, e, tab, format);
+#ifdef COVT_PROPX_COUNTONLY
+    } else if (false) {
+#else
     } else if (recs) {
+#endif
         PropRecEmit e{recs + (size_t)t * kPropSlots, nullptr, t};
         e.cap = kPropSlots;
         const int st = prop_walk_tile(r, e, tab, format);
@@ -2145,12 +2235,15 @@ __global__ void __launch_bounds__(256) prop_sizes(const PropRaw* __restrict__ re
         PropStreams ps;
         prop_streams(q, id_mode, ps);
         int64_t ob = 0;
-        for (int k = 0; k < ps.n; ++k) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {  // (k: the role)
+            if (!(ps.has >> k & 1u)) continue;
             const int64_t bytes = ps.count[k] * ps.elem[k];
+            const int32_t bl = q.s_bl[k];
             ob = align_out(ob + bytes);
             a[PA_PAYLOAD] += (unsigned long long)bytes;
-            a[PA_LANE] += lane_stream(ps.op[k], (int32_t)ps.count[k], q.s_bl[ps.role[k]], lane_max) ? 1ull : 0ull;
-            const unsigned long long c = (unsigned long long)((int64_t)q.s_bl[ps.role[k]] + bytes / 4);
+            a[PA_LANE] += lane_stream(ps.op[k], (int32_t)ps.count[k], bl, lane_max) ? 1ull : 0ull;
+            const unsigned long long c = (unsigned long long)((int64_t)bl + bytes / 4);
             a[PA_COST] += c;
             a[PA_CMAX] = c > a[PA_CMAX] ? c : a[PA_CMAX];
         }
@@ -2217,29 +2310,33 @@ __global__ void prop_fill(const PropRaw* __restrict__ recs, const int32_t* __res
     int64_t out = obb[t] + ob[t] + (rob[r] - rob[r0]);
     const int64_t tile_off = (int64_t)offs[t];
     covt_prop_info pi = prop_info_of(q, t, tile_off);
-    for (int k = 0; k < ps.n; ++k, ++si_k) {
-        const int role = ps.role[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {  // (k: the role)
+        if (!(ps.has >> k & 1u)) continue;
+        const int role = k;
+        const int32_t cnt_k = (int32_t)ps.count[k];
         covt_stream_info si;
         si.tile = t;
         si.layer = q.layer;
         si.column_kind = 2;
         si.stream_type = role;
-        si.encoding = q.s_enc[role];
+        si.encoding = q.s_enc[k];
         si.column_type = q.ctype;
-        si.num_values = q.s_nv[role];
-        si.byte_length = q.s_bl[role];
+        si.num_values = q.s_nv[k];
+        si.byte_length = q.s_bl[k];
         si.num_bits = 0;
         si.op = ps.op[k];
         si.elem_bytes = ps.elem[k];
         si.desc_index = -1;
-        si.in_off = tile_off + q.s_off[role];
+        si.in_off = tile_off + q.s_off[k];
         si.out_elems = ps.count[k];
         si.out_off = out;
         out = align_out(out + ps.count[k] * ps.elem[k]);
         info[si_k] = si;
-        nvals[si_k] = (int32_t)ps.count[k];
-        if (keys) keys[si_k] = entry_key(si.op, (int32_t)ps.count[k], si.byte_length, si.out_elems, si.elem_bytes, lm);
-        pi.stream[role] = (int32_t)si_k;
+        nvals[si_k] = cnt_k;
+        if (keys) keys[si_k] = entry_key(si.op, cnt_k, si.byte_length, si.out_elems, si.elem_bytes, lm);
+        pi.stream[k] = (int32_t)si_k;
+        ++si_k;
     }
     pin[2 * r] = pi.out_off[1];  // the FLOAT data / STRING dictionary input offsets (plan_property_layout's
     pin[2 * r + 1] = pi.out_off[3];  // in_float / in_dict)
@@ -2350,8 +2447,12 @@ __global__ void geom_columns(const covt_stream_info* __restrict__ info, int64_t 
         const covt_stream_info& s = info[j];
         const int k = s.stream_type - ST_GEOMETRY_TYPES;
         if (k < 0 || k > 5) continue;
-        g.stream[k] = (int32_t)j;
-        len[k] = k == 5 ? s.out_elems / 2 : s.out_elems;  // vertexBuffer: x,y pairs
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {  // (constant indices: g and len stay in registers, not scratch)
+            if (m != k) continue;
+            g.stream[m] = (int32_t)j;
+            len[m] = m == 5 ? s.out_elems / 2 : s.out_elems;  // vertexBuffer: x,y pairs
+        }
         if (k == 5) g.column_type = s.column_type;
     }
     g.n_features = (int32_t)len[0];

@@ -28,11 +28,17 @@ __host__ __device__ inline PropRaw prop_init(int32_t layer, int32_t column, int3
     for (int r = 0; r < 4; ++r) p.s_off[r] = -1;
     return p;
 }
+// (constant indices only: a record indexed by a run-time role lives in scratch on the GPU, where the
+// property walk kept its record -- 144 bytes per lane of private memory)
 __host__ __device__ inline void prop_stream(PropRaw& p, int role, int64_t off, int32_t nv, int32_t bl, int32_t enc) {
-    p.s_off[role] = off;
-    p.s_nv[role] = nv;
-    p.s_bl[role] = bl;
-    p.s_enc[role] = enc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        if (r != role) continue;
+        p.s_off[r] = off;
+        p.s_nv[r] = nv;
+        p.s_bl[r] = bl;
+        p.s_enc[r] = enc;
+    }
 }
 // Gen C ColumnDataType (evaluation/file/ColumnDataType.java) / Gen D (converter/ColumnDataType.java)
 __host__ __device__ inline int genc_prop_type(int dt) {
@@ -47,8 +53,9 @@ __host__ __device__ inline int gend_prop_type(int dt) {
 // stream was decoded (data encodings, non-dictionary strings).
 struct PropStreams {
     uint16_t flags;
-    int32_t n;                            // streams, in role order
-    int32_t role[3], op[3], elem[3];
+    int32_t n;                            // streams
+    uint32_t has;                         // bit r: a stream of role r (0 present, 1 data, 2 length)
+    int32_t op[3], elem[3];               // by role; the streams go in role order
     int64_t count[3];                     // output elements of each
     int64_t in_bytes;                     // stream bytes + bytes read in place (floats, the owner's dictionary)
 };
@@ -98,11 +105,13 @@ __host__ __device__ inline void prop_streams(const PropRaw& q, int id_mode, Prop
     ps.flags = fl;
     ps.n = 0;
     ps.in_bytes = 0;
+    ps.has = 0;
+    // (indexed by the role, a constant at every call: a slot index would put the arrays in scratch)
     auto add = [&](int role, int op, int64_t n, int elem) {
-        ps.role[ps.n] = role;
-        ps.op[ps.n] = op;
-        ps.count[ps.n] = n;
-        ps.elem[ps.n] = elem;
+        ps.has |= 1u << role;
+        ps.op[role] = op;
+        ps.count[role] = n;
+        ps.elem[role] = elem;
         ps.in_bytes += q.s_bl[role];
         ++ps.n;
     };
@@ -135,9 +144,10 @@ __host__ __device__ inline covt_prop_info prop_info_of(const PropRaw& q, int32_t
     pi.lang_off = q.lang_off >= 0 ? tile_off + q.lang_off : -1;
     for (int k = 0; k < 3; ++k) pi.stream[k] = -1;
     pi.desc_index = 0;
-    for (int k = 0; k < 4; ++k) pi.out_off[k] = 0;
-    if (q.type == COVT_PROP_FLOAT && q.s_off[1] >= 0) pi.out_off[1] = tile_off + q.s_off[1];  // temporarily
-    if (q.type == COVT_PROP_STRING && q.s_off[3] >= 0) pi.out_off[3] = tile_off + q.s_off[3];  // temporarily
+    // temporarily (as values: two conditional stores were merged into one at a computed index, in scratch)
+    pi.out_off[0] = pi.out_off[2] = 0;
+    pi.out_off[1] = (q.type == COVT_PROP_FLOAT && q.s_off[1] >= 0) ? tile_off + q.s_off[1] : 0;
+    pi.out_off[3] = (q.type == COVT_PROP_STRING && q.s_off[3] >= 0) ? tile_off + q.s_off[3] : 0;
     return pi;
 }
 

@@ -78,6 +78,9 @@ for s in "$@"; do
     dplan_var) for v in ${AB_VARIANTS:-libcovt.so}; do
             COVT_LIB_VARIANT=$v timeout -k 10 200 python tools/device_plan_prof.py 20 --sweep 2>&1 | grep -v amdgpu.ids || fatal dplan_var $?
         done ;;
+    dplan_props_var) for v in ${AB_VARIANTS:-libcovt.so}; do
+            COVT_LIB_VARIANT=$v timeout -k 10 200 python tools/device_plan_prof.py 20 --sweep --props 2>&1 | grep -v amdgpu.ids || fatal dplan_props_var $?
+        done ;;
     dplan_prof_small) step dplan_prof_small 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_prof_small -o run --output-format csv -- python tools/device_plan_prof.py 5 --small ;;
     dplan_props_small) step dplan_props_small 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_props_small -o run --output-format csv -- python tools/device_plan_prof.py 5 --small --props ;;
     dplan_sq1) step dplan_sq1 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/dplan_sq1 -o run --output-format csv -- python tools/device_plan_prof.py 2 --props ;;
