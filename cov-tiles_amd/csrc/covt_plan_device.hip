@@ -2128,9 +2128,6 @@ struct PropRecEmit {
     }
     __device__ void layer_begin() { k0 = n; }
     __device__ void layer_end(int64_t data_start) {  // Gen C: data offsets relative to the layer's data start
-#ifdef COVT_PROPX_NOLAYERFIX
-        return;
-#endif
         if (!data_start) return;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -2189,11 +2186,7 @@ __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
     if (EMIT) {
         PropRecEmit e{recs + pcb[t], rtile + pcb[t], t};
         (void)prop_walk_tile(r, e, tab, format);
-#ifdef COVT_PROPX_COUNTONLY
-    } else if (false) {
-#else
     } else if (recs) {
-#endif
         PropRecEmit e{recs + (size_t)t * kPropSlots, nullptr, t};
         e.cap = kPropSlots;
         const int st = prop_walk_tile(r, e, tab, format);
