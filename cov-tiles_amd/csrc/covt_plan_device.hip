@@ -848,6 +848,14 @@ __device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes,
     return format == COVT_FORMAT_GENC ? walk_genc_dev(r, emit) : walk_gend_dev(r, emit);
 }
 
+// the walks' tile order in a property plan: largest first (the batch's few 442 KB tiles were the property
+// walk's tail when they started late: 10k-tile plan 3.16-3.21 -> 2.95-2.99 ms; an Id / Geometry plan
+// gains nothing from it and would pay the sort, ~0.04 ms)
+__global__ void tile_iota(uint32_t* __restrict__ v, int32_t n) {
+    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < n) v[i] = (uint32_t)i;
+}
+
 // Records a tile's walk leaves for emit_slots: up to kSlots per tile (the fixture library's busiest
 // tile has 67 Id / Geometry streams); a tile with more is walked again by walk_emit
 constexpr int kSlots = 128;
@@ -899,9 +907,11 @@ template <bool kWave>
 __global__ void walk_count(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
                            const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                            int32_t* __restrict__ status, int64_t* __restrict__ cnt, int64_t* __restrict__ ob,
-                           RawStream* __restrict__ slots, int64_t fpf_w, int64_t* __restrict__ tcost) {
-    const int32_t t = kWave ? (int32_t)blockIdx.x : (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+                           RawStream* __restrict__ slots, int64_t fpf_w, int64_t* __restrict__ tcost,
+                           const uint32_t* __restrict__ order) {
+    int32_t t = kWave ? (int32_t)blockIdx.x : (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t > n_tiles) return;
+    if (order && t < n_tiles) t = (int32_t)order[t];  // (largest tiles first)
     if (t == n_tiles) {  // the prefix sums' total slot
         if (!kWave || threadIdx.x == 0) cnt[t] = 0, ob[t] = 0;
         return;
@@ -2170,9 +2180,11 @@ template <bool EMIT>
 __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
                           const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format,
                           const int32_t* __restrict__ status, int64_t* __restrict__ pcnt,
-                          const int64_t* __restrict__ pcb, PropRaw* __restrict__ recs, int32_t* __restrict__ rtile) {
-    const int32_t t = (int32_t)blockIdx.x;
+                          const int64_t* __restrict__ pcb, PropRaw* __restrict__ recs, int32_t* __restrict__ rtile,
+                          const uint32_t* __restrict__ order) {
+    int32_t t = (int32_t)blockIdx.x;
     if (t > n_tiles) return;
+    if (order && t < n_tiles) t = (int32_t)order[t];  // (largest tiles first)
     if (t == n_tiles || status[t]) {  // (t == n_tiles: the prefix sum's total slot)
         if (!EMIT && threadIdx.x == 0) pcnt[t] = 0;
         return;
@@ -2569,13 +2581,41 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     const int64_t lane_min = o.lane_min_streams;
     // 0: a wave per tile, its lanes in lockstep; k > 0: k lanes per workgroup, a lane per tile
     RawStream* slots = use_slots ? (RawStream*)(ta + o_slots) : nullptr;
+    // property plans of more than 256 tiles: both walks largest tiles first (a stable descending sort of
+    // the sizes)
+    uint32_t* order = nullptr;
+    void* order_mem = nullptr;
+    if (props && n_tiles > 256) {
+        size_t otmp = 0;
+        DCHK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, otmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                          (const uint32_t*)nullptr, (uint32_t*)nullptr, n_tiles, 0, 40, s));
+        const size_t nt = (size_t)n_tiles;
+        DCHK(plan_malloc(&order_mem, up256(nt * 8) + 2 * up256(nt * 4) + up256(otmp), p->dev, s));
+        uint8_t* om = (uint8_t*)order_mem;
+        uint32_t* iota = (uint32_t*)(om + up256(nt * 8));
+        order = (uint32_t*)(om + up256(nt * 8) + up256(nt * 4));
+        tile_iota<<<(n_tiles + 255) / 256, 256, 0, s>>>(iota, n_tiles);
+        const hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(
+            om + up256(nt * 8) + 2 * up256(nt * 4), otmp, d_tile_sizes, (uint64_t*)om, iota, order, n_tiles, 0, 40, s);
+        if (e != hipSuccess) {
+            (void)hipFreeAsync(order_mem, s);
+            return fail(COVT_ERR_DEVICE);
+        }
+    }
+    struct OrderFree {  // (stream-ordered: after the walks that read it)
+        void* m;
+        hipStream_t q;
+        ~OrderFree() { if (m) (void)hipFreeAsync(m, q); }
+    } order_free{order_mem, s};
+    const uint32_t* id_order = order;
+    const uint32_t* prop_order = order;
     if (wl == 0)
         walk_count<true><<<(int)nt1, 64, kWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
-                                                        id_mode, p->d_status, cnt, ob, slots, fpf_w, tcost);
+                                                        id_mode, p->d_status, cnt, ob, slots, fpf_w, tcost, id_order);
     else
         walk_count<false><<<(int)((nt1 + wl - 1) / wl), wl, (size_t)wl * 64 + 16, s>>>(
             d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cnt, ob, nullptr,
-            fpf_w, tcost);
+            fpf_w, tcost, id_order);
     DCHK(hipGetLastError());
     // property columns: their records (a count walk, one D2H for the record count, the emitting walk), each
     // record's streams and output bytes, and each tile's totals = Id / Geometry + property
@@ -2603,7 +2643,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         prop_slots = (PropRaw*)pslots;
         p->scratch = pslots;  // (a failure on the way frees it with the plan)
         prop_walk<false><<<(int)nt1, 64, kPropWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
-                                                           p->d_status, pcnt, nullptr, prop_slots, nullptr);
+                                                           p->d_status, pcnt, nullptr, prop_slots, nullptr, prop_order);
         DCHK(hipGetLastError());
         DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, pcnt, pcb, (int)nt1, s));
         DCHK(hipMemcpyAsync(&n_rec, pcb + n_tiles, 8, hipMemcpyDeviceToHost, s));
@@ -2652,7 +2692,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
             }
             prop_walk<true><<<n_tiles, 64, kPropWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
                                                              format, p->d_status, prop_slots ? pcnt : nullptr, pcb, recs,
-                                                             rtile);
+                                                             rtile, nullptr);
             DCHK(hipGetLastError());
         }
         if (prop_slots) {

@@ -420,3 +420,16 @@ def test_properties_split(covt, gpu_available, decodable_tiles, golden_streams):
     _assert_same_plan(hp, dp)
     _assert_same_properties(hp, dp)
     _assert_same_materialization(covt, hp, dp)
+
+
+def test_properties_full_batch(covt, gpu_available):
+    """The bench's 10k-tile batch with COVT_PLAN_PROPERTIES: more than 256 tiles, so both device walks take
+    the tiles largest first (a device sort of the sizes) while every record keeps its tile-order place;
+    plan, property records and descriptors equal the host plan's."""
+    import bench
+
+    picks = bench.sample_batch(bench.tile_library(), 10000, bench.SEED)
+    hp = _host_plan(covt, [t for _, t in picks], covt.FORMAT_GENC, 0, split=True, flags=covt.PLAN_PROPERTIES)
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
+    _assert_same_plan(hp, dp)
+    _assert_same_properties(hp, dp)
