@@ -2399,12 +2399,18 @@ __global__ void prop_order_keys(const covt_prop_info* __restrict__ pinfo, int64_
     keys[r] = prop_order_key(pinfo[r]);
     vals[r] = (uint32_t)r;
 }
-__global__ void prop_desc_fill(covt_prop_info* __restrict__ pinfo, const uint16_t* __restrict__ pflags,
-                               const int64_t* __restrict__ pin, const uint32_t* __restrict__ order, int64_t n_rec,
-                               const covt_stream_info* __restrict__ info, covt_prop_desc* __restrict__ pdesc) {
+// the sort's order -> each record's row (so prop_desc_fill reads the records in order and scatters only
+// its descriptor writes: gathering a record, its streams and flags per row was 182 us on the 10k batch)
+__global__ void prop_rank(const uint32_t* __restrict__ order, int64_t n_rec, uint32_t* __restrict__ rank) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_rec) return;
-    const uint32_t r = order[k];
+    if (k < n_rec) rank[order[k]] = (uint32_t)k;
+}
+__global__ void prop_desc_fill(covt_prop_info* __restrict__ pinfo, const uint16_t* __restrict__ pflags,
+                               const int64_t* __restrict__ pin, const uint32_t* __restrict__ rank, int64_t n_rec,
+                               const covt_stream_info* __restrict__ info, covt_prop_desc* __restrict__ pdesc) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rec) return;
+    const uint32_t k = rank[r];
     covt_prop_info& pi = pinfo[r];
     auto s_out = [&](int role) -> int64_t { return pi.stream[role] >= 0 ? info[pi.stream[role]].out_off : -1; };
     covt_prop_desc d;
@@ -2863,7 +2869,8 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
             prop_order_keys<<<pb, 256, 0, s>>>(p->d_pinfo, n_rec, pk0, pv0);
             DCHK(hipGetLastError());
             DCHK(hipcub::DeviceRadixSort::SortPairs(pa + po_st, psort_tmp, pk0, pk1, pv0, pv1, (int)n_rec, 0, 41, s));
-            prop_desc_fill<<<pb, 256, 0, s>>>(p->d_pinfo, pflags, (const int64_t*)(pa + po_pin), pv1, n_rec, p->d_info,
+            prop_rank<<<pb, 256, 0, s>>>(pv1, n_rec, pv0);  // (pv0, the sort's input values, is free)
+            prop_desc_fill<<<pb, 256, 0, s>>>(p->d_pinfo, pflags, (const int64_t*)(pa + po_pin), pv0, n_rec, p->d_info,
                                               p->d_pdesc);
             DCHK(hipGetLastError());
         }
