@@ -1688,9 +1688,11 @@ __global__ void fpf_states_walk(const uint8_t* __restrict__ bytes, const covt_st
 // ---- Property columns (COVT_PLAN_PROPERTIES; covt_host.cpp walk_genc / walk_gend's property records,
 // plan_property and plan_property_layout).  The host plan puts a tile's property streams after its Id /
 // Geometry streams and gives them output slices in that order; here:
-//   prop_walk<false>  one wave per tile: the container walk again, counting property (sub)columns
+//   prop_walk<false>  one wave per tile (largest tiles first): the container walk again, counting property
+//                     (sub)columns and keeping each tile's first kPropSlots records in its slots
 //   scan              -> each tile's first record; one D2H (the record count sizes the arrays)
-//   prop_walk<true>   the same walk writing the records (PropRaw, tile-relative offsets)
+//   prop_compact      the slots -> the records' places (PropRaw, tile-relative offsets); prop_walk<true>
+//                     walks again only the tiles with more records than slots
 //   prop_sizes        a thread per record: its decode streams (prop_streams, the host's rule), their count
 //                     and aligned output bytes; the records' byte / payload / lane / cost totals
 //   scans + tile_totals  each tile's streams and output bytes = Id / Geometry + property
