@@ -11,12 +11,15 @@ tile, inputs (tile bytes + descriptor table) already resident in HBM, outputs wr
 
 N>1: one process per GPU -- either started by torch.distributed.run (WORLD_SIZE/RANK/LOCAL_RANK in the
 environment) or, without a launcher, spawned here (one child per GPU, started before anything touches
-the GPU; fails if fewer than N GPUs are visible).  Scaling is weak by default: each rank decodes its own
-10k-tile batch (seed 20250117 + rank).  Tiles are independent, so there is no collective on the data
-path and no RCCL: a gloo group carries the timing barriers and gathers the per-rank numbers.
---scaling strong shards one 10k-tile batch over the ranks with the greedy byte-balanced split of
-SURVEY §8(e).  Besides `value` (config 5) the line carries BASELINE configs 2-4 (`configs`), the
-PCIe-inclusive and C-ABI host timings, assembly and property legs, and the CPU baseline.
+the GPU; fails if fewer than N GPUs are visible).  Scaling is strong by default, as BASELINE config 5
+states it ("10k-tile batch ... sharded across 8xMI355X"): one 10k-tile batch split over the ranks by the
+greedy longest-processing-time byte balance of SURVEY §8(e).  At N > 1 the line also carries `weak`: every
+rank then decodes a whole 10k-tile batch of its own (seed 20250117 + rank), the per-GPU-work-fixed figure;
+`--scaling weak` makes that the headline instead.  Tiles are independent, so there is no collective on
+the data path and no RCCL: a gloo group carries the timing barriers and gathers the per-rank numbers.
+Besides `value` (config 5) the line carries BASELINE configs 2-4 (`configs`), the PCIe-inclusive and
+C-ABI host timings, the device plan (+ decode: `device_plan.plan_plus_decode`), assembly and property legs,
+and the CPU baseline.
 """
 from __future__ import annotations
 
@@ -593,6 +596,24 @@ def free_port():
         return s.getsockname()[1]
 
 
+def timed_steps(batch, stream, steps, torch, dev, barrier):
+    """`steps` decode launches bracketed by a barrier + synchronize on both sides -> (wall s, mean HIP-event
+    ms of one launch on the launch stream)."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        batch.decode(stream)
+        e.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier()
+    wall = time.perf_counter() - t0
+    return wall, float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+
 def launch_ranks(args):
     """`bench.py --gpus N` without a launcher: one child process per GPU (RANK/LOCAL_RANK/WORLD_SIZE set
     before the child touches the GPU), rank 0 prints the line.  This parent never initialises HIP."""
@@ -632,7 +653,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--tiles", type=int, default=10000)
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="strong (default): one --tiles batch sharded over the ranks (BASELINE config 5); "
+                         "weak: a whole --tiles batch per rank")
+    ap.add_argument("--no-weak", action="store_true", help="N > 1 strong runs: skip the extra weak-scaling field")
     ap.add_argument("--cpu-iters", type=int, default=20, help="timed CPU-baseline iterations (after 3 warm-ups)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (default: all usable CPUs)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -716,22 +740,29 @@ def main():
         if (res[:, 0] != 0).any():
             raise RuntimeError("decode reported errors on %d streams" % int((res[:, 0] != 0).sum()))
 
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
-        torch.cuda.synchronize(dev)
-        barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for s, e in ev:
-            s.record(stream)
-            batch.decode(stream)
-            e.record(stream)
-        torch.cuda.synchronize(dev)
-        barrier()
-        wall = time.perf_counter() - t0
-        kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+        wall, kern_ms = timed_steps(batch, stream, args.steps, torch, dev, barrier)
 
     legs = {}
+    weak = None
+    if world > 1 and args.scaling == "strong" and not args.no_weak:
+        # the per-GPU-work-fixed figure beside the strong headline: a whole batch per rank
+        wpicks = sample_batch(lib, args.tiles, SEED + rank)
+        wplan = covt.Plan.from_tiles([t for _, t in wpicks], covt.FORMAT_GENC, args.id_mode)
+        if args.dry_run:
+            barrier()
+            t0 = time.perf_counter()
+            barrier()
+            wwall = time.perf_counter() - t0
+            wms = wwall * 1e3 / max(args.steps, 1)
+        else:
+            wbatch = covt.DeviceBatch(wplan, dev)
+            for _ in range(args.warmup):
+                wbatch.decode(stream)
+            wwall, wms = timed_steps(wbatch, stream, args.steps, torch, dev, barrier)
+            del wbatch
+        weak = {"tiles": len(wpicks), "stream_bytes": int(wplan.in_bytes), "wall_s": wwall, "kernel_ms": wms,
+                "seed": SEED + rank}
+        del wplan
     if not args.dry_run:
         if args.e2e_reps > 0:
             legs["end_to_end"] = end_to_end(plan, batch, stream, torch, dev, args.e2e_reps)
@@ -748,7 +779,7 @@ def main():
 
     mine = {"rank": rank, "device": dev_name, "local_rank": local_rank, "seed": seed, "tiles": len(picks),
             "streams": int(plan.num_streams), "stream_bytes": int(plan.in_bytes), "output_bytes": int(plan.out_bytes),
-            "vertices": int(plan.vertices), "wall_s": wall, "kernel_ms": kern_ms}
+            "vertices": int(plan.vertices), "wall_s": wall, "kernel_ms": kern_ms, "weak": weak}
     if dist is not None:
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
@@ -779,7 +810,7 @@ def main():
             try:
                 with open(pmc) as f:
                     pm = json.load(f)
-                if pm.get("tiles") != args.tiles or pm.get("scaling") != args.scaling:
+                if pm.get("tiles") != args.tiles or len(ranks) > 1:
                     traffic_note = "profiles/pmc_traffic.json measured on another workload"
                 elif pm.get("kernel_sources_sha256") != kernel_sources_sha256():
                     traffic_note = "stale: profiles/pmc_traffic.json measured on other decode / plan sources"
@@ -802,8 +833,9 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "fixture-sampled: seeded sample of the reference's committed OMT+Bing COVT tiles",
-            "config": {"workload": "config5: %d-tile mixed-zoom z2-z14 batch per GPU (%s scaling), "
-                                   "all Id+Geometry streams" % (len(picks), args.scaling),
+            "config": {"workload": ("config5: %d-tile mixed-zoom z2-z14 batch, all Id+Geometry streams" % args.tiles)
+                       + (" sharded over %d GPUs (strong scaling, LPT byte balance)" % world if world > 1 and
+                          args.scaling == "strong" else " per GPU (weak scaling)" if world > 1 else ", one GPU"),
                        "tiles_per_gpu": len(picks), "streams_per_gpu": plan.num_streams,
                        "stream_bytes_per_gpu": plan.in_bytes, "output_bytes_per_gpu": plan.out_bytes,
                        "vertices_per_gpu": plan.vertices,
@@ -840,6 +872,16 @@ def main():
                           "gbps": round(r["stream_bytes"] * args.steps / r["wall_s"] / 1e9, 3)
                           if r["wall_s"] > 0 else None} for r in ranks],
         }
+        if ranks[0]["weak"] is not None:
+            ww = max(r["weak"]["wall_s"] for r in ranks)
+            wb = float(sum(r["weak"]["stream_bytes"] for r in ranks))
+            line["weak"] = {"value": round(wb * args.steps / ww / 1e9, 3), "unit": "GB/s",
+                            "ms_per_step": round(ww * 1e3 / args.steps, 4),
+                            "kernel_ms": round(max(r["weak"]["kernel_ms"] for r in ranks), 4),
+                            "tiles_per_gpu": ranks[0]["weak"]["tiles"], "tiles_total": sum(r["weak"]["tiles"] for r in ranks),
+                            "stream_bytes_total": int(wb), "seeds": [r["weak"]["seed"] for r in ranks],
+                            "note": "weak scaling: every rank decodes its own whole %d-tile batch (seed %d + rank); "
+                                    "same step timing as `value`" % (args.tiles, SEED)}
         line.update(legs)
         line["host_plan_ms"] = round(t_plan * 1e3, 1)  # covt_plan_create: metadata walk, descriptors, host
         line["host_pack_ms"] = round(t_pack * 1e3, 1)  # pack_tiles: copying the tiles into one buffer

@@ -192,7 +192,22 @@ EXPORTED_SYMBOLS = (
     "covt_device_plan_assembly_bytes", "covt_device_plan_geometry_descs_device", "covt_device_plan_geometry_copy",
     "covt_device_plan_assemble", "covt_device_plan_num_property_columns", "covt_device_plan_property_bytes",
     "covt_device_plan_property_descs_device", "covt_device_plan_property_copy", "covt_device_plan_materialize",
+    "covt_release_scratch", "covt_scratch_blocks", "covt_device_plan_pool_trim",
 )
+
+
+def release_scratch(stream=None, all: bool = False) -> int:
+    """covt_release_scratch: free the small-batch assembly / property scratch of (current device, `stream`),
+    or every block with all=True; returns the number of blocks freed."""
+    import torch
+
+    s = stream if stream is not None else (torch.cuda.current_stream() if not all else None)
+    return lib().covt_release_scratch(C.c_void_p(s.cuda_stream if s is not None else 0), 1 if all else 0)
+
+
+def scratch_blocks() -> int:
+    """Scratch blocks held by the small-batch paths (covt_scratch_blocks)."""
+    return int(lib().covt_scratch_blocks())
 
 
 def build(force: bool = False) -> str:
@@ -263,6 +278,9 @@ def lib() -> C.CDLL:
     L.covt_plan_geometry_columns.argtypes = [vp, vp]
     L.covt_plan_geometry_descs.argtypes = [vp, vp]
     L.covt_assemble_geometry_device.argtypes = [vp, vp, vp, C.c_int64, vp, vp, vp]
+    L.covt_release_scratch.argtypes = [vp, C.c_int]
+    L.covt_scratch_blocks.restype = C.c_int64
+    L.covt_device_plan_pool_trim.argtypes = [C.c_int, C.c_uint64]
     L.covt_plan_assemble_host.argtypes = [vp, u8p, C.c_uint64, vp, vp]
     L.covt_plan_create_ex.argtypes = [u8p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
                                       C.c_int32, C.c_uint32, C.POINTER(vp)]
@@ -1135,7 +1153,7 @@ def version() -> str:
 # the files whose sha256 (in this order) the Makefile compiles into covt_version() as "src:<16 hex>"
 _BUILD_SOURCES = ("csrc/covt_decode.hip", "csrc/covt_assemble.hip", "csrc/covt_props.hip", "csrc/covt_plan_device.hip",
                   "csrc/covt_host.cpp", "../include/covt.h", "csrc/covt_internal.h", "csrc/covt_wave.h",
-                  "csrc/covt_walk.h", "csrc/covt_props_plan.h")
+                  "csrc/covt_walk.h", "csrc/covt_props_plan.h", "csrc/covt_scratch.h")
 
 
 def source_build_id() -> str:

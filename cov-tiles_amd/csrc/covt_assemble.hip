@@ -33,12 +33,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <map>
-#include <mutex>
-#include <utility>
-
 #include "covt.h"
 #include "covt_internal.h"
+#include "covt_scratch.h"
 #include "covt_wave.h"
 
 namespace covt {
@@ -773,7 +770,8 @@ struct SplitCol {
 struct SplitScratch {
     uint32_t ticket[4];                       // next ticket of pass p
     int32_t n_split, n_small;                 // split columns; columns left to single waves
-    int32_t pad[2];
+    uint32_t epoch;                           // this launch's record tag, advanced by split_prep (never 0)
+    int32_t pad;
     int32_t pre[4][kCoopMaxColumns + 1];      // pass p: chunks of split columns before column k
     int32_t col[kCoopMaxColumns];             // split column k -> batch column
     int32_t small[kCoopMaxColumns];           // the other columns (single waves, pass 1's workgroups)
@@ -882,6 +880,10 @@ __global__ __launch_bounds__(1024) void split_prep(const covt_geom_desc* __restr
     if (t == 0) {
         sc->n_split = tot[4];
         sc->n_small = tot[5];
+        // a new tag for this launch's look-back records, kept in device memory so that a captured graph
+        // replays with a fresh one (epoch 0, the zeroed scratch's, is never used)
+        const uint32_t e = sc->epoch + 1u;
+        sc->epoch = e ? e : 1u;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             sc->pre[p][tot[4]] = tot[p];
@@ -1420,7 +1422,7 @@ __global__ __launch_bounds__(64 * kCoopWaves) void split_pass_kernel(const uint8
                                                                      const covt_geom_desc* __restrict__ descs,
                                                                      uint8_t* __restrict__ outb,
                                                                      covt_geom_result* __restrict__ gres,
-                                                                     SplitScratch* __restrict__ sc, uint32_t epoch) {
+                                                                     SplitScratch* __restrict__ sc) {
     __shared__ union U {
         AsmSmemT<kCoopWaves> coop;
         AsmSmem wave[kCoopWaves];
@@ -1429,6 +1431,7 @@ __global__ __launch_bounds__(64 * kCoopWaves) void split_pass_kernel(const uint8
     __shared__ int32_t tk;
     const int32_t ns = sc->n_split;
     const int32_t total = sc->pre[PASS - 1][ns];
+    const uint32_t epoch = sc->epoch;  // (split_prep, earlier on this stream)
     const int32_t small_groups = PASS == 1 ? (sc->n_small + kCoopWaves - 1) / kCoopWaves : 0;
     for (int32_t i = threadIdx.x; i <= ns; i += 64 * kCoopWaves) lpre[i] = sc->pre[PASS - 1][i];
     __syncthreads();
@@ -1467,29 +1470,13 @@ __global__ __launch_bounds__(64 * kCoopWaves) void split_pass_kernel(const uint8
 
 }  // namespace covt
 
-namespace {
-// split-pass scratch, one per (device, stream): launches on one stream are ordered, so they can share it;
-// the epoch tags each launch's look-back records
-struct SplitSlot {
-    void* p = nullptr;
-    uint32_t epoch = 0;
-};
-std::mutex g_split_mu;
-std::map<std::pair<int, hipStream_t>, SplitSlot> g_split_scratch;
-covt::SplitScratch* split_scratch(hipStream_t s, uint32_t& epoch) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> g(g_split_mu);
-    SplitSlot& q = g_split_scratch[std::make_pair(dev, s)];
-    if (!q.p) {
-        if (hipMalloc(&q.p, sizeof(covt::SplitScratch)) != hipSuccess) return (covt::SplitScratch*)(q.p = nullptr);
-        if (hipMemset(q.p, 0, sizeof(covt::SplitScratch)) != hipSuccess) return nullptr;  // epoch 0: never used
-    }
-    if (++q.epoch == 0) q.epoch = 1;
-    epoch = q.epoch;
-    return (covt::SplitScratch*)q.p;
+namespace covt {
+// split-pass scratch, one per (device, stream) (covt_scratch.h)
+StreamScratch& assembly_scratch() {
+    static StreamScratch m(sizeof(SplitScratch));
+    return m;
 }
-}  // namespace
+}  // namespace covt
 
 extern "C" int covt_assemble_geometry_device(const uint8_t* d_decoded, const covt_stream_result* d_res,
                                              const covt_geom_desc* d_gdesc, int64_t n_columns, uint8_t* d_asm,
@@ -1505,19 +1492,18 @@ extern "C" int covt_assemble_geometry_device(const uint8_t* d_decoded, const cov
     const bool coop = n_columns <= covt::kCoopMaxColumns;
     if (coop) {
         // every column in the split passes' kernels: big ones chunked, the rest on single waves in pass 1
-        uint32_t epoch = 0;
-        covt::SplitScratch* sc = split_scratch(s, epoch);
+        covt::SplitScratch* sc = (covt::SplitScratch*)covt::assembly_scratch().get(s);
         if (!sc) return COVT_ERR_DEVICE;
         const dim3 wg(64 * covt::kCoopWaves);
         hipLaunchKernelGGL(covt::split_prep, dim3(1), dim3(1024), 0, s, d_gdesc, n_columns, covt::kSplitMinItems, sc);
         hipLaunchKernelGGL(covt::split_pass_kernel<1>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
-                           d_asm, d_gres, sc, epoch);
+                           d_asm, d_gres, sc);
         hipLaunchKernelGGL(covt::split_pass_kernel<2>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
-                           d_asm, d_gres, sc, epoch);
+                           d_asm, d_gres, sc);
         hipLaunchKernelGGL(covt::split_pass_kernel<3>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
-                           d_asm, d_gres, sc, epoch);
+                           d_asm, d_gres, sc);
         hipLaunchKernelGGL(covt::split_pass_kernel<4>, dim3(covt::kSplitGrid), wg, 0, s, d_decoded, d_res, d_gdesc,
-                           d_asm, d_gres, sc, epoch);
+                           d_asm, d_gres, sc);
     } else {
         hipLaunchKernelGGL(covt::assemble_kernel, dim3((unsigned)blocks), dim3(64 * covt::kAsmWaves), 0, s, d_decoded,
                            d_res, d_gdesc, n_columns, d_asm, d_gres);

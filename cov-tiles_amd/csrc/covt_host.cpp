@@ -988,7 +988,7 @@ void plan_property_layout(covt_plan* p) {
         }
     }
     p->prop_bytes = off;
-std::vector<SortKey> korder(np);  // largest (features + dictionary entries) first, ties in tile order
+    std::vector<SortKey> korder(np);  // largest (features + dictionary entries) first, ties in tile order
     for (size_t k = 0; k < np; ++k)
         korder[k] = SortKey{prop_order_key(p->pinfo[k]), (uint32_t)k};
     radix_sort(korder);

@@ -61,8 +61,10 @@ namespace {
 
 // The plan's arenas come from a per-device stream-ordered pool that keeps freed memory (up to
 // kPoolKeep bytes) for the next plan: a plain hipMalloc of the ~100 MB stream arena between the plan's
-// two host syncs cost ~0.15 ms of the 10k-tile plan (profiles/r04, kernel trace gap).
-constexpr uint64_t kPoolKeep = 8ull << 30;
+// two host syncs cost ~0.15 ms of the 10k-tile plan (profiles/r04, kernel trace gap).  The retained memory
+// is invisible to other allocators (PyTorch's cache): 1 GiB covers a 10k-tile property plan's arenas, and
+// covt_device_plan_pool_trim hands it back on request.
+constexpr uint64_t kPoolKeep = 1ull << 30;
 hipMemPool_t plan_pool(int dev) {
     static std::mutex mu;
     static hipMemPool_t pools[64] = {};
@@ -2178,12 +2180,17 @@ __device__ __forceinline__ int prop_walk_tile(Rd<true>& r, PE& e, PropTab& tab, 
 // given (the others are copied from their slots by prop_compact)
 constexpr int kPropSlots = 256;
 constexpr size_t kPropSlotBytes = (size_t)2 << 30;  // slot memory a plan may take (10k tiles: 328 MB)
+// The two walks read the same metadata as the Id / Geometry walk, which accepted the tile, so they cannot
+// fail on it; if one does anyway (a divergence between the walkers) the count walk raises `diverged` and
+// the plan fails with COVT_ERR_BAD_HEADER instead of dropping the tile's property columns, and the emit
+// walk never writes past the records its count walk found (pcb[t + 1] - pcb[t]).
 template <bool EMIT>
 __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
                           const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format,
                           const int32_t* __restrict__ status, int64_t* __restrict__ pcnt,
                           const int64_t* __restrict__ pcb, PropRaw* __restrict__ recs, int32_t* __restrict__ rtile,
-                          const uint32_t* __restrict__ order) {
+                          const uint32_t* __restrict__ order, unsigned long long* __restrict__ diverged,
+                          bool slotted) {
     int32_t t = (int32_t)blockIdx.x;
     if (t > n_tiles) return;
     if (order && t < n_tiles) t = (int32_t)order[t];  // (largest tiles first)
@@ -2191,7 +2198,7 @@ __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
         if (!EMIT && threadIdx.x == 0) pcnt[t] = 0;
         return;
     }
-    if (EMIT && pcnt && pcnt[t] <= kPropSlots) return;  // (in its slots)
+    if (EMIT && pcnt[t] <= kPropSlots && slotted) return;  // (in its slots)
     Rd<true> r;
     r.t = bytes + offs[t];
     r.len = (int64_t)sizes[t];
@@ -2199,16 +2206,23 @@ __global__ void prop_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
     PropTab tab;
     if (EMIT) {
         PropRecEmit e{recs + pcb[t], rtile + pcb[t], t};
+        e.cap = pcb[t + 1] - pcb[t];
         (void)prop_walk_tile(r, e, tab, format);
     } else if (recs) {
         PropRecEmit e{recs + (size_t)t * kPropSlots, nullptr, t};
         e.cap = kPropSlots;
         const int st = prop_walk_tile(r, e, tab, format);
-        if (threadIdx.x == 0) pcnt[t] = st ? 0 : e.n;  // (the Id / Geometry walk succeeded: so does this one)
+        if (threadIdx.x == 0) {
+            pcnt[t] = st ? 0 : e.n;
+            if (st) atomicOr(diverged, 1ull);
+        }
     } else {
         PropCountEmit e;
         const int st = prop_walk_tile(r, e, tab, format);
-        if (threadIdx.x == 0) pcnt[t] = st ? 0 : e.n;
+        if (threadIdx.x == 0) {
+            pcnt[t] = st ? 0 : e.n;
+            if (st) atomicOr(diverged, 1ull);
+        }
     }
 }
 
@@ -2228,7 +2242,7 @@ __global__ void __launch_bounds__(64) prop_compact(const PropRaw* __restrict__ s
     for (int64_t i = threadIdx.x; i < n; i += 64) rtile[pcb[t] + i] = t;
 }
 
-enum { PA_IN = 0, PA_PAYLOAD = 1, PA_LANE = 2, PA_COST = 3, PA_CMAX = 4, PA_N = 8 };
+enum { PA_IN = 0, PA_PAYLOAD = 1, PA_LANE = 2, PA_COST = 3, PA_CMAX = 4, PA_DIVERGED = 7, PA_N = 8 };
 // a thread per record: its decode streams (prop_streams), their count and aligned output bytes, and the
 // records' totals (stream / in-place bytes, payload, lane-family streams, split cost and its maximum)
 __global__ void __launch_bounds__(256) prop_sizes(const PropRaw* __restrict__ recs, int64_t n_rec, int32_t id_mode,
@@ -2651,11 +2665,16 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         prop_slots = (PropRaw*)pslots;
         p->scratch = pslots;  // (a failure on the way frees it with the plan)
         prop_walk<false><<<(int)nt1, 64, kPropWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
-                                                           p->d_status, pcnt, nullptr, prop_slots, nullptr, prop_order);
+                                                           p->d_status, pcnt, nullptr, prop_slots, nullptr, prop_order,
+                                                           pacc + PA_DIVERGED, prop_slots != nullptr);
         DCHK(hipGetLastError());
         DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, pcnt, pcb, (int)nt1, s));
-        DCHK(hipMemcpyAsync(&n_rec, pcb + n_tiles, 8, hipMemcpyDeviceToHost, s));
+        unsigned long long head[2] = {0, 0};  // record count, walk divergence
+        DCHK(hipMemcpyAsync(&head[0], pcb + n_tiles, 8, hipMemcpyDeviceToHost, s));
+        DCHK(hipMemcpyAsync(&head[1], pacc + PA_DIVERGED, 8, hipMemcpyDeviceToHost, s));
         DCHK(hipStreamSynchronize(s));
+        n_rec = (int64_t)head[0];
+        if (head[1]) return fail(COVT_ERR_BAD_HEADER);  // the property walk failed a tile the Id walk accepted
         if (n_rec > 0x7fffffff) return fail(COVT_ERR_INVALID_ARG);
         const size_t nr = (size_t)(n_rec > 0 ? n_rec : 1), nr1 = nr + 1;
         DCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, pscan_tmp, (int64_t*)nullptr, (int64_t*)nullptr, (int)nr1, s));
@@ -2699,8 +2718,8 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
                 DCHK(hipGetLastError());
             }
             prop_walk<true><<<n_tiles, 64, kPropWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles,
-                                                             format, p->d_status, prop_slots ? pcnt : nullptr, pcb, recs,
-                                                             rtile, nullptr);
+                                                             format, p->d_status, pcnt, pcb, recs, rtile, nullptr,
+                                                             pacc + PA_DIVERGED, prop_slots != nullptr);
             DCHK(hipGetLastError());
         }
         if (prop_slots) {
@@ -2887,6 +2906,19 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     for (int f = 0; f < COVT_NUM_FAMILIES; ++f) p->fam_counts[f] = (int64_t)tot[T_FAM + f];
     *out = p;
     return COVT_OK;
+}
+
+int covt_device_plan_pool_trim(int device, uint64_t keep_bytes) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return COVT_ERR_INVALID_ARG;
+    hipMemPool_t mp = plan_pool(device);
+    if (!mp) return COVT_ERR_DEVICE;
+    int cur = 0;
+    const bool sw = hipGetDevice(&cur) == hipSuccess && cur != device && hipSetDevice(device) == hipSuccess;
+    (void)hipDeviceSynchronize();  // (freed arenas return to the pool in stream order)
+    const hipError_t e = hipMemPoolTrimTo(mp, (size_t)keep_bytes);
+    if (sw) (void)hipSetDevice(cur);
+    return e == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
 }
 
 void covt_device_plan_destroy(covt_device_plan* p) {

@@ -13,12 +13,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <map>
-#include <mutex>
-#include <utility>
-
 #include "covt.h"
 #include "covt_internal.h"
+#include "covt_scratch.h"
 #include "covt_wave.h"
 
 namespace covt {
@@ -322,7 +319,7 @@ struct PropSplitCol {
 struct PropSplitScratch {
     uint32_t ticket;
     int32_t n_split, n_small;
-    int32_t pad;
+    uint32_t epoch;  // this launch's record tag, advanced by prop_split_prep (never 0)
     int32_t pre[kPropCoopMaxColumns + 1];  // chunks of split columns before column k
     int32_t col[kPropCoopMaxColumns];      // split column k -> batch column
     int32_t small[kPropCoopMaxColumns];    // the other columns (single waves)
@@ -415,6 +412,10 @@ __global__ __launch_bounds__(1024) void prop_split_prep(const covt_prop_desc* __
         sc->n_small = tot[2];
         sc->pre[tot[1]] = tot[0];
         sc->ticket = 0;
+        // a new tag for this launch's look-back records, kept in device memory so that a captured graph
+        // replays with a fresh one (epoch 0, the zeroed scratch's, is never used)
+        const uint32_t e = sc->epoch + 1u;
+        sc->epoch = e ? e : 1u;
     }
 }
 
@@ -432,13 +433,6 @@ __device__ void prop_split_chunk(const uint8_t* in, const uint8_t* dec, const co
     const int32_t g0 = sc->pre[k], nch = sc->pre[k + 1] - g0;
     int32_t st[3];
     for (int q = 0; q < 3; ++q) st[q] = d.res[q] >= 0 ? ((const gp_i32*)dres)[2 * d.res[q]] : COVT_OK;
-    // the dictionary (chunk 0, wave 0): written by the owner whatever this sub-column's other streams hold
-    if (j == 0 && d.type == COVT_PROP_STRING && d.res[2] >= 0 && st[2] == COVT_OK) {
-        if (wv == 0) {
-            const int32_t x = dictionary(in, dec, d, outb, (d.flags & COVT_PROP_DICT_OWNER) != 0);
-            if (lane_id() == 0) cs.dst = x;
-        }
-    }
     bool early = st[0] || st[1] || st[2] || (d.flags & (COVT_PROP_UNSUPPORTED_LATE | COVT_PROP_DATA_SHORT));
     const int32_t n = d.n_features, dn = d.n_data;
     const int32_t f0 = j * kPropSplitK;
@@ -546,6 +540,15 @@ __device__ void prop_split_chunk(const uint8_t* in, const uint8_t* dec, const co
         }
         bad = __syncthreads_or(bad) != 0;
     }
+    // the dictionary (chunk 0, wave 0): written by the owner whatever this sub-column's other streams hold.
+    // Built after the chunk has published its present count, so the column's later chunks never wait in
+    // their look-back for a long dictionary (cs.dst is read only by the column's last chunk to finish)
+    if (j == 0 && d.type == COVT_PROP_STRING && d.res[2] >= 0 && st[2] == COVT_OK) {
+        if (wv == 0) {
+            const int32_t x = dictionary(in, dec, d, outb, (d.flags & COVT_PROP_DICT_OWNER) != 0);
+            if (lane_id() == 0) cs.dst = x;
+        }
+    }
     __syncthreads();
     if (l == 0) {
         if (bad) atomicOr(&cs.bad, 1u);
@@ -578,11 +581,12 @@ __global__ __launch_bounds__(64 * kPropCoopWaves) void prop_split_kernel(const u
                                                                          const covt_prop_desc* __restrict__ descs,
                                                                          uint8_t* __restrict__ outb,
                                                                          covt_prop_result* __restrict__ pres,
-                                                                         PropSplitScratch* __restrict__ sc, uint32_t epoch) {
+                                                                         PropSplitScratch* __restrict__ sc) {
     __shared__ PropSmem smem;
     __shared__ int32_t lpre[kPropCoopMaxColumns + 1];
     __shared__ int32_t tk;
     const int32_t ns = sc->n_split, total = sc->pre[ns];
+    const uint32_t epoch = sc->epoch;  // (prop_split_prep, earlier on this stream)
     const int32_t small_groups = (sc->n_small + kPropCoopWaves - 1) / kPropCoopWaves;
     for (int32_t i = threadIdx.x; i <= ns; i += 64 * kPropCoopWaves) lpre[i] = sc->pre[i];
     __syncthreads();
@@ -619,29 +623,13 @@ __global__ __launch_bounds__(64 * kPropCoopWaves) void prop_split_kernel(const u
 
 }  // namespace covt
 
-namespace {
-// split scratch, one per (device, stream): launches on one stream are ordered, so they can share it; the
-// epoch tags each launch's look-back records
-struct PropSplitSlot {
-    void* p = nullptr;
-    uint32_t epoch = 0;
-};
-std::mutex g_psplit_mu;
-std::map<std::pair<int, hipStream_t>, PropSplitSlot> g_psplit_scratch;
-covt::PropSplitScratch* prop_split_scratch(hipStream_t s, uint32_t& epoch) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> g(g_psplit_mu);
-    PropSplitSlot& q = g_psplit_scratch[std::make_pair(dev, s)];
-    if (!q.p) {
-        if (hipMalloc(&q.p, sizeof(covt::PropSplitScratch)) != hipSuccess) return (covt::PropSplitScratch*)(q.p = nullptr);
-        if (hipMemset(q.p, 0, sizeof(covt::PropSplitScratch)) != hipSuccess) return nullptr;  // epoch 0: never used
-    }
-    if (++q.epoch == 0) q.epoch = 1;
-    epoch = q.epoch;
-    return (covt::PropSplitScratch*)q.p;
+namespace covt {
+// split scratch, one per (device, stream) (covt_scratch.h)
+StreamScratch& property_scratch() {
+    static StreamScratch m(sizeof(PropSplitScratch));
+    return m;
 }
-}  // namespace
+}  // namespace covt
 
 extern "C" int covt_materialize_properties_device(const uint8_t* d_in, const uint8_t* d_decoded,
                                                   const covt_stream_result* d_res, const covt_prop_desc* d_pdesc,
@@ -656,16 +644,24 @@ extern "C" int covt_materialize_properties_device(const uint8_t* d_in, const uin
     if (n_columns <= covt::kPropCoopMaxColumns) {
         // small batches: columns of kPropSplitMinFeatures or more in chunks on many workgroups, the rest
         // on single waves of the same kernel
-        uint32_t epoch = 0;
-        covt::PropSplitScratch* sc = prop_split_scratch(s, epoch);
+        covt::PropSplitScratch* sc = (covt::PropSplitScratch*)covt::property_scratch().get(s);
         if (!sc) return COVT_ERR_DEVICE;
         hipLaunchKernelGGL(covt::prop_split_prep, dim3(1), dim3(1024), 0, s, d_pdesc, n_columns,
                            covt::kPropSplitMinFeatures, sc);
         hipLaunchKernelGGL(covt::prop_split_kernel, dim3(covt::kPropSplitGrid), dim3(64 * covt::kPropCoopWaves), 0, s,
-                           d_in, d_decoded, d_res, d_pdesc, d_props, d_pres, sc, epoch);
+                           d_in, d_decoded, d_res, d_pdesc, d_props, d_pres, sc);
     } else {
         hipLaunchKernelGGL(covt::props_kernel, dim3((unsigned)blocks), dim3(64 * covt::kPropWaves), 0, s, d_in,
                            d_decoded, d_res, d_pdesc, n_columns, d_props, d_pres);
     }
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
+}
+
+extern "C" int covt_release_scratch(void* hip_stream, int all) {
+    const hipStream_t s = (hipStream_t)hip_stream;
+    return covt::assembly_scratch().release(s, all != 0) + covt::property_scratch().release(s, all != 0);
+}
+
+extern "C" int64_t covt_scratch_blocks(void) {
+    return (int64_t)(covt::assembly_scratch().size() + covt::property_scratch().size());
 }

@@ -455,6 +455,19 @@ int covt_materialize_properties_device(const uint8_t* d_in, const uint8_t* d_dec
                                        const covt_prop_desc* d_pdesc, int64_t n_columns, uint8_t* d_props,
                                        covt_prop_result* d_pres, void* hip_stream);
 
+/* Scratch of the small-batch paths.  For batches of at most 4,096 columns covt_assemble_geometry_device
+ * and covt_materialize_properties_device keep one device scratch block per (device, HIP stream) (about
+ * 8.4 MB for assembly, 0.6 MB for properties), allocated and zeroed on the stream's first use and reused
+ * by every later launch on it.  Each launch tags its look-back records with an epoch its own first kernel
+ * advances in device memory, so launches captured in a HIP graph replay correctly.  At most 16 blocks of
+ * each kind are kept; beyond that the least recently used one is freed.  covt_release_scratch frees the
+ * blocks of (current device, hip_stream), or every block when `all` is non-zero, and returns how many it
+ * freed.  hipFree waits for the device, so no launch still in flight uses a freed block; a caller that
+ * creates a stream per batch should release its blocks before destroying the stream. */
+int covt_release_scratch(void* hip_stream, int all);
+/* blocks currently held (assembly + properties) */
+int64_t covt_scratch_blocks(void);
+
 /* Convenience: H2D + decode + property materialization + D2H of the whole plan on the current device.
  * host_props: covt_plan_property_bytes bytes; host_pres: one result per (sub)column in tile order. */
 int covt_plan_properties_host(const covt_plan* plan, const uint8_t* bytes, uint64_t n_bytes, uint8_t* host_props,
@@ -472,11 +485,15 @@ int covt_plan_properties_host(const covt_plan* plan, const uint8_t* bytes, uint6
  * group chunks); geometry-column planning on request (covt_device_plan_geometry); property columns
  * with COVT_PLAN_PROPERTIES in opts->flags.  Multi-GPU shards stay with the host plan.
  * Runs on `hip_stream` and synchronises it twice (three times when it splits: the stream count and
- * the descriptor count size the arrays).
+ * the descriptor count size the arrays); COVT_PLAN_PROPERTIES adds one more (the property record
+ * count).  COVT_ERR_BAD_HEADER if the property walk fails a tile the Id / Geometry walk accepted (the
+ * walkers diverged: never on well-formed or corrupted input that the host plan rejects the same way).
  * Limits and memory: a tile of 0x7ff00000 bytes or more gets COVT_ERR_INVALID_ARG as its status
  * (32-bit cursors; the host plan walks such tiles); besides the stream arrays the plan holds ~5 KiB
  * of per-tile walk slots on the device (128 stream records of 40 bytes per tile: ~0.5 GB at 100k
- * tiles) unless opts->device_walk != 0. */
+ * tiles) unless opts->device_walk != 0.  The arenas come from a per-device stream-ordered memory pool
+ * that keeps up to 1 GiB of freed plan memory for the next plan (PyTorch's allocator does not see it);
+ * covt_device_plan_pool_trim(device, keep_bytes) releases all but keep_bytes of it. */
 typedef struct covt_device_plan covt_device_plan;
 int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_tile_offsets,
                             const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
@@ -486,6 +503,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
                                  const uint64_t* d_tile_sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
                                  const covt_plan_options* opts, void* hip_stream, covt_device_plan** out);
 void covt_device_plan_destroy(covt_device_plan* plan);
+int covt_device_plan_pool_trim(int device, uint64_t keep_bytes);
 int64_t covt_device_plan_num_streams(const covt_device_plan* plan);
 int64_t covt_device_plan_num_descs(const covt_device_plan* plan); /* = num_streams unless it splits */
 int64_t covt_device_plan_output_bytes(const covt_device_plan* plan);

@@ -8,8 +8,13 @@
 //   varint P N | zigzag P N | zzdelta P N | coords P N | morton P NV NB
 //   rle N P SIGNED | byterle N P BL | byterle3 N P | fpf N BL P | fpfcoords N BL P | fpfmorton NV BL P NB
 //   batch                 (GpuCovtBatch: one tile, create + decode; prints "ok <n streams> <statuses>")
+//   batch2 S1 S2 ...      (GpuCovtBatch over the tiles of sizes S1, S2, ... packed back to back in one direct
+//                          buffer: decode twice into the SAME direct output buffer, poisoned between the
+//                          calls -- the reuse contract of INTEGRATION.md section 3; prints
+//                          "ok <n streams> <statuses> <output hex> <ms first call> <ms second call>")
 #include <jni.h>
 
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -213,6 +218,43 @@ int main() {
                 if (r) {  // statuses, then the output bytes after them
                     const jlong ns = BFN(numStreams)(env, nullptr, h);
                     std::cout << "ok " << ns << " " << hex(O(r)->data) << " " << hex(out->data) << "\n";
+                    BFN(destroy)(env, nullptr, h);
+                    continue;
+                }
+                BFN(destroy)(env, nullptr, h);
+            }
+        } else if (m == "batch2") {  // several tiles, two decodes into one reused direct output buffer
+            Obj* tiles = make(Obj::DIRECT);
+            const size_t nt = a.size();
+            Obj* offs = new_array((jsize)nt, 8);
+            Obj* sizes = new_array((jsize)nt, 8);
+            // pack: tile k's bytes (consecutive in the hex input) at a 16-byte aligned offset of the buffer
+            size_t src = 0;
+            for (size_t k = 0; k < nt; ++k) {
+                tiles->data.resize((tiles->data.size() + 15) & ~(size_t)15, 0);
+                const int64_t o = (int64_t)tiles->data.size(), sz = (int64_t)a[k];
+                std::memcpy(offs->data.data() + 8 * k, &o, 8);
+                std::memcpy(sizes->data.data() + 8 * k, &sz, 8);
+                tiles->data.insert(tiles->data.end(), buf->data.begin() + (std::ptrdiff_t)src,
+                                   buf->data.begin() + (std::ptrdiff_t)(src + (size_t)a[k]));
+                src += (size_t)a[k];
+            }
+            tiles->data.resize(tiles->data.size() + 4096, 0);  // COVT_INPUT_PADDING
+            const jlong h = BFN(create)(env, nullptr, J<jobject>(tiles), J<jlongArray>(offs), J<jlongArray>(sizes), 0, 0, 0);
+            if (g_exc.empty()) {
+                Obj* out = make(Obj::DIRECT);
+                out->data.assign((size_t)BFN(outputBytes)(env, nullptr, h), 0);
+                double ms[2] = {0, 0};
+                for (int call = 0; call < 2 && g_exc.empty(); ++call) {
+                    if (call) std::memset(out->data.data(), 0xA5, out->data.size());  // the second call rewrites it all
+                    const auto t0 = std::chrono::steady_clock::now();
+                    r = BFN(decode)(env, nullptr, h, J<jobject>(tiles), J<jobject>(out));
+                    ms[call] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                }
+                if (r && g_exc.empty()) {
+                    const jlong ns = BFN(numStreams)(env, nullptr, h);
+                    std::cout << "ok " << ns << " " << hex(O(r)->data) << " " << hex(out->data) << " " << ms[0] << " "
+                              << ms[1] << "\n";
                     BFN(destroy)(env, nullptr, h);
                     continue;
                 }

@@ -20,16 +20,18 @@ def _run(args, timeout=240):
 
 
 def test_gpus2_dry_run_spawns_two_ranks():
-    p, lines = _run(["--gpus", "2", "--dry-run", "--tiles", "40", "--steps", "2", "--warmup", "1", "--cpu-iters", "2"])
+    p, lines = _run(["--gpus", "2", "--dry-run", "--tiles", "40", "--steps", "2", "--warmup", "1", "--cpu-iters", "2",
+                     "--scaling", "weak"])
     assert p.returncode == 0, p.stderr[-2000:]
     assert len(lines) == 1, p.stdout  # rank 0 only
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["dry_run"]
+    assert line["n_gpus"] == 2 and line["dry_run"] and line["scaling"] == "weak"
     pr = line["per_rank"]
     assert [r["rank"] for r in pr] == [0, 1]
     assert len({r["seed"] for r in pr}) == 2  # weak scaling: distinct per-rank batches
     assert all(r["tiles"] == 40 for r in pr)
     assert line["config"]["parallelism"].startswith("dp2")
+    assert "weak" not in line  # the weak figure is the headline here
     cb = line["cpu_baseline"]  # rank 0's batch, at every N (north_star: "next to the Java CPU decoder ... in the same run")
     assert cb is not None and cb["value"] > 0 and cb["kind"] == "port"
     # N > 1 field semantics: byte totals are sums over ranks, each rank's own beside them;
@@ -51,12 +53,35 @@ def test_gpus2_dry_run_spawns_two_ranks():
     assert line["build"]["match"] and line["build"]["library"] == line["build"]["sources"]
 
 
-def test_gpus2_strong_dry_run_shards_one_batch():
-    p, lines = _run(["--gpus", "2", "--dry-run", "--tiles", "41", "--steps", "1", "--warmup", "0",
-                     "--scaling", "strong"])
+def test_gpus2_default_is_strong_scaling():
+    """BASELINE config 5 ("10k-tile batch ... sharded across 8xMI355X"): at N > 1
+    the default shards ONE batch over the ranks by LPT byte balance; the weak figure rides beside it."""
+    import bench
+
+    p, lines = _run(["--gpus", "2", "--dry-run", "--tiles", "41", "--steps", "1", "--warmup", "0", "--no-cpu"])
     assert p.returncode == 0, p.stderr[-2000:]
-    pr = json.loads(lines[0])["per_rank"]
+    line = json.loads(lines[0])
+    assert line["scaling"] == "strong" and "sharded over 2 GPUs" in line["config"]["workload"]
+    pr = line["per_rank"]
     assert sum(r["tiles"] for r in pr) == 41 and len({r["seed"] for r in pr}) == 1
+    assert line["config"]["tiles_total"] == 41
+    # the shards are the LPT split of the one batch: their bytes add up to the whole batch's
+    covt = bench.load_covt()
+    allp = bench.sample_batch(bench.tile_library(), 41, bench.SEED)
+    whole = covt.Plan.from_tiles([t for _, t in allp])
+    assert line["config"]["stream_bytes_total"] == whole.in_bytes
+    sh = bench.lpt_shards([len(t) for _, t in allp], 2)
+    assert sorted(len(s) for s in sh) == sorted(r["tiles"] for r in pr)
+    w = line["weak"]
+    assert w["tiles_per_gpu"] == 41 and w["tiles_total"] == 82 and len(set(w["seeds"])) == 2
+    assert w["value"] > 0
+
+
+def test_gpus1_default_is_the_whole_batch():
+    p, lines = _run(["--dry-run", "--tiles", "25", "--steps", "1", "--warmup", "0", "--no-cpu"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and line["per_rank"][0]["tiles"] == 25 and "weak" not in line
 
 
 @pytest.mark.skipif(__import__("torch").cuda.device_count() >= 2, reason="host has >= 2 GPUs")

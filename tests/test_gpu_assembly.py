@@ -266,3 +266,77 @@ def test_batch_assembly_properties(covt, oracle, gpu_available):
         d = _digest(col.geometry_offsets, col.part_offsets, col.ring_offsets, col.coords)
         assert ref[key][int(g["layer"][c])] == (0, d), (key, int(g["layer"][c]))
     assert int(gres["num_coords"].sum()) >= plan.vertices  # + closing vertices of PLAIN polygon rings
+
+
+def _split_cols():
+    rng = np.random.default_rng(12)
+    cols = [A.synth_column(rng, 30000, True, False), A.synth_column(rng, 20000, False, True),
+            A.synth_column(rng, 300, False, False)]
+    for c in cols:
+        c["caps"] = A.caps(c)
+    return cols
+
+
+def test_split_passes_replay_in_a_hip_graph(covt, oracle, gpu_available):
+    """the split passes' look-back records are tagged with an epoch that the launch's
+    own prep kernel advances in device memory, so a captured graph replays with a fresh epoch each time
+    (a host-side epoch would be frozen into the graph and a replay would accept the previous replay's
+    records).  Three replays, output poisoned before each, bit-exact against the oracle."""
+    import torch
+
+    cols = _split_cols()
+    dec, desc, asm_bytes, lay = A.pack_columns(covt, cols, None, None)
+    dev = torch.device("cuda:0")
+    d_dec = torch.from_numpy(dec).to(dev)
+    d_desc = torch.from_numpy(desc).to(dev)
+    d_asm = torch.full((asm_bytes,), 0x5A, dtype=torch.uint8, device=dev)
+    d_gres = torch.zeros(4 * len(cols), dtype=torch.int32, device=dev)
+    d_res = torch.zeros(2, dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream(dev)
+
+    def launch():
+        assert covt.lib().covt_assemble_geometry_device(d_dec.data_ptr(), d_res.data_ptr(), d_desc.data_ptr(),
+                                                        len(cols), d_asm.data_ptr(), d_gres.data_ptr(),
+                                                        s.cuda_stream) == 0
+
+    with torch.cuda.stream(s):
+        launch()  # the stream's scratch exists before capture (allocation cannot be captured)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        launch()
+    for _ in range(3):
+        d_asm.fill_(0x5A)
+        d_gres.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        gres = d_gres.cpu().numpy().view(covt.GEOM_RESULT_DTYPE)
+        assert (gres["status"] == 0).all()
+        _check_vs_oracle(oracle, cols, d_asm.cpu().numpy(), gres, lay)
+    del g
+    torch.cuda.synchronize()
+    assert covt.release_scratch(s) >= 1
+
+
+def test_scratch_blocks_bounded_and_released(covt, oracle, gpu_available):
+    """one scratch block per (device, stream), at most 16 kept (least recently used
+    freed), all freed by covt_release_scratch(all); results stay exact on every stream."""
+    import torch
+
+    covt.release_scratch(all=True)
+    assert covt.scratch_blocks() == 0
+    cols = _split_cols()
+    dev = torch.device("cuda:0")
+    streams = [torch.cuda.Stream(dev) for _ in range(20)]
+    for i, s in enumerate(streams):
+        with torch.cuda.stream(s):
+            asm, gres, lay = _run_kernel(covt, cols)
+        if i % 7 == 0:
+            _check_vs_oracle(oracle, cols, asm, gres, lay)
+        assert covt.scratch_blocks() <= 16
+    assert covt.scratch_blocks() == 16
+    assert covt.release_scratch(streams[-1]) == 1  # the most recent one is still held
+    assert covt.release_scratch(all=True) == 15 and covt.scratch_blocks() == 0
+    asm, gres, lay = _run_kernel(covt, cols)  # and a fresh block works
+    _check_vs_oracle(oracle, cols, asm, gres, lay)

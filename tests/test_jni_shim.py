@@ -136,3 +136,39 @@ def test_gpu_covt_batch_through_jni(shim, covt, gpu_available):
         s = plan.streams[i]
         o, n = int(s["out_off"]), int(s["out_elems"]) * int(s["elem_bytes"])
         assert np.array_equal(jout[o:o + n], out[o:o + n]), i
+
+
+@pytest.mark.gpu
+def test_gpu_covt_batch_reused_direct_buffers(shim, covt, gpu_available, golden_streams):
+    """INTEGRATION.md section 3, the reuse contract: a Java caller keeps one direct
+    output ByteBuffer and decodes into it call after call (GpuCovtBatch.decode; the caller shape of
+    CovtParserTest.java:44-60 run per batch).  The second decode into the same buffer, poisoned in
+    between, must rewrite every stream: each stream's SHA-256, status and consumed bytes equal the
+    oracle's golden digest of its source tile (tests/golden/oracle_streams.json)."""
+    import hashlib
+
+    keys = ["omt/5_16_20", "omt/14_8298_10748", "bing/4-8-5", "omt/9_265_341", "omt/2_2_2"]
+    tiles = [open(os.path.join(ROOT, "tests", "golden", "tiles", k + ".covt"), "rb").read() for k in keys]
+    case = "batch2 " + " ".join(str(len(t)) for t in tiles) + " | " + b"".join(tiles).hex()
+    (got,) = run(shim, [case])
+    kind, ns, st_hex, out_hex, ms1, ms2 = got.split()
+    assert kind == "ok"
+    plan = covt.Plan.from_tiles(tiles)
+    assert int(ns) == plan.num_streams
+    status = np.frombuffer(bytes.fromhex(st_hex), "<i4")
+    out = np.frombuffer(bytes.fromhex(out_hex), np.uint8)
+    col = golden_streams["columns"]
+    ish, ist = col.index("fmt_sha256"), col.index("fmt_status")
+    st = plan.streams
+    bounds = np.searchsorted(st["tile"], np.arange(len(tiles) + 1))
+    n = 0
+    for t, key in enumerate(keys):
+        rows = golden_streams["tiles"][key]["streams"]
+        assert bounds[t + 1] - bounds[t] == len(rows), key
+        for i, row in zip(range(int(bounds[t]), int(bounds[t + 1])), rows):
+            assert int(status[i]) == row[ist], (key, i)
+            if row[ist] == 0:
+                assert hashlib.sha256(plan.stream_array(out, i).tobytes()).hexdigest() == row[ish], (key, i)
+                n += 1
+    assert n >= 100
+    print("GpuCovtBatch.decode into a fresh direct buffer %s ms, reused %s ms" % (ms1, ms2))

@@ -18,6 +18,9 @@ step() {  # step NAME LIMIT cmd...
     case $rc in 0|1|5) ;; *) fatal "$name" "$rc";; esac
 }
 for s in "$@"; do
+    # STEP+props: the same step on the property plan (OPB_PROPS=1), logs suffixed _props
+    unset OPB_PROPS; sfx=
+    case $s in *+props) export OPB_PROPS=1; sfx=_props; s=${s%+props};; esac
     case $s in
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     abfpf) step ab_fpf 900 python tools/ab.py ${AB_VARIANTS:-libcovt_base.so libcovt.so} ;;
@@ -62,12 +65,12 @@ for s in "$@"; do
     sq_fpf) step sq_fpf 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/sq_fpf -o run --output-format csv -- python tools/family_run.py fastpfor 2 ;;
     sq_fpf2) step sq_fpf2 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE -d gpurun_out/sq_fpf2 -o run --output-format csv -- python tools/family_run.py fastpfor 2 ;;
     util_rle_props) OPB_PROPS=1 step $s 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_VALU -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py rle 2 ;;
-    util_rle|util_varint|util_fastpfor|util_lane|util_all) fam=${s#util_}; step $s 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_VALU -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
-    sqi_rle|sqi_varint|sqi_fastpfor|sqi_lane|sqi_all) fam=${s#sqi_}; step $s 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
-    sqc_rle|sqc_varint|sqc_fastpfor|sqc_lane|sqc_all) fam=${s#sqc_}; step $s 600 rocprofv3 --pmc SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_BRANCH GRBM_GUI_ACTIVE -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
-    icache_rle|icache_varint|icache_fastpfor|icache_lane|icache_all) fam=${s#icache_}; step $s 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH GRBM_GUI_ACTIVE -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
-    mem_rle|mem_varint|mem_fastpfor|mem_lane) fam=${s#mem_}; step $s 600 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_TA_BUSY TA_DATA_STALLED_BY_TC_CYCLES TCP_PENDING_STALL_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
-    sq_rle|sq_varint|sq_fastpfor) fam=${s#sq_}; step $s 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
+    util_rle|util_varint|util_fastpfor|util_lane|util_all) fam=${s#util_}; step $s$sfx 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_VALU -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
+    sqi_rle|sqi_varint|sqi_fastpfor|sqi_lane|sqi_all) fam=${s#sqi_}; step $s$sfx 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
+    sqc_rle|sqc_varint|sqc_fastpfor|sqc_lane|sqc_all) fam=${s#sqc_}; step $s$sfx 600 rocprofv3 --pmc SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_BRANCH GRBM_GUI_ACTIVE -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
+    icache_rle|icache_varint|icache_fastpfor|icache_lane|icache_all) fam=${s#icache_}; step $s 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH GRBM_GUI_ACTIVE -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
+    mem_rle|mem_varint|mem_fastpfor|mem_lane) fam=${s#mem_}; step $s$sfx 600 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_TA_BUSY TA_DATA_STALLED_BY_TC_CYCLES TCP_PENDING_STALL_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
+    sq_rle|sq_varint|sq_fastpfor|sq_lane) fam=${s#sq_}; step $s$sfx 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     opinst) step opinst 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE -d gpurun_out/opinst -o run --output-format csv -- python tools/op_counters.py ;;
     tests_changed) step pytest_changed 600 python -u -m pytest tests/test_gpu_assembly.py tests/test_gpu_props.py tests/test_gpu_split.py tests/test_gpu_rle_adversarial.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     tests_dplan) step pytest_dplan 300 python -u -m pytest tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
@@ -90,11 +93,12 @@ for s in "$@"; do
     dplan_api_small) step dplan_api_small 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_api_small -o run --output-format csv -- python tools/device_plan_prof.py 20 --small --nosplit ;;
     dplan_sq_small) step dplan_sq_small 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_BRANCH -d gpurun_out/dplan_sq_small -o run --output-format csv -- python tools/device_plan_prof.py 3 --small --nosplit ;;
     dplan_sorted) step dplan_sorted 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_sorted -o run --output-format csv -- python tools/device_plan_prof.py 10 --sorted ;;
+    shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
     ops_props) OPB_PROPS=1 step ops_props 600 python tools/op_breakdown.py ;;
     props_time) step props_time 300 python tools/props_run.py ;;
-    fetch_rle|fetch_lane|fetch_rle_props|fetch_lane_props) fam=${s#fetch_}; fam=${fam%_props}
+    fetch_fastpfor|fetch_varint|fetch_rle|fetch_lane|fetch_rle_props|fetch_lane_props) fam=${s#fetch_}; fam=${fam%_props}
         if [ "${s%_props}" != "$s" ]; then export OPB_PROPS=1; else unset OPB_PROPS; fi
-        step $s 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
+        step $s$sfx 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     sq_rle_props) OPB_PROPS=1 step $s 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_WAVES -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py rle 2 ;;
     config1_prof) step config1_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/config1_prof -o run --output-format csv -- python tools/config1_prof.py 20 ;;
     config1_passes) for v in libcovt_asm1.so libcovt_asm2.so libcovt_asm3.so libcovt.so; do

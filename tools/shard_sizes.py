@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Strong-scaling shard sizes of BASELINE config 5 timed on ONE GPU.
+
+The 10k-tile bench batch is split over N = 1, 2, 4, 8 ranks exactly as `bench.py --gpus N` (default strong
+scaling) splits it (LPT byte balance, bench.lpt_shards); every shard of each split is planned and its
+decode launch timed alone on this GPU (HIP events, mean of --steps after --warmup).  An N-GPU run takes as
+long as its slowest shard, so `projected_gbps` = the whole batch's stream bytes / the slowest shard's
+launch: what the strong-scaling line would report with no host-side effects.  `frac` is each shard's own
+algorithmic bytes over its launch time against the 8 TB/s peak; `vs_full` its GB/s against the full batch's.
+usage: shard_sizes.py [steps] [--ns 1,2,4,8]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    import torch
+
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    steps = int(args[0]) if args else 30
+    ns = [1, 2, 4, 8]
+    for a in sys.argv[1:]:
+        if a.startswith("--ns="):
+            ns = [int(x) for x in a[5:].split(",")]
+    covt = bench.load_covt()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    allp = bench.sample_batch(bench.tile_library(), 10000, bench.SEED)
+    full_bytes = None
+    full_gbps = None
+    print("%3s %5s %6s %10s %10s %9s %8s %8s %7s" % ("N", "shard", "tiles", "in MB", "out MB", "ms", "GB/s",
+                                                    "frac", "vs_full"))
+    for n in ns:
+        shards = bench.lpt_shards([len(t) for _, t in allp], n)
+        worst = 0.0
+        for k, sh in enumerate(shards):
+            plan = covt.Plan.from_tiles([allp[i][1] for i in sh])
+            batch = covt.DeviceBatch(plan, dev)
+            for _ in range(5):
+                batch.decode(stream)
+            torch.cuda.synchronize(dev)
+            _, res = batch.results()
+            assert (res[:, 0] == 0).all()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+            for s, e in ev:
+                s.record(stream)
+                batch.decode(stream)
+                e.record(stream)
+            torch.cuda.synchronize(dev)
+            ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+            gbps = plan.in_bytes / (ms * 1e-3) / 1e9
+            frac = (plan.in_bytes + plan.out_bytes) / (ms * 1e-3) / 8e12
+            if n == 1:
+                full_bytes, full_gbps = plan.in_bytes, gbps
+            worst = max(worst, ms)
+            print("%3d %5d %6d %10.1f %10.1f %9.4f %8.1f %8.4f %7.3f" % (
+                n, k, len(sh), plan.in_bytes / 1e6, plan.out_bytes / 1e6, ms, gbps, frac,
+                gbps / full_gbps if full_gbps else float("nan")), flush=True)
+            del batch, plan
+        if full_bytes:
+            print("    N=%d: slowest shard %.4f ms -> projected strong-scaling value %.1f GB/s (%.2fx of N=1, "
+                  "efficiency %.3f)" % (n, worst, full_bytes / (worst * 1e-3) / 1e9,
+                                         full_bytes / (worst * 1e-3) / 1e9 / full_gbps,
+                                         full_bytes / (worst * 1e-3) / 1e9 / full_gbps / n), flush=True)
+
+
+if __name__ == "__main__":
+    main()
