@@ -408,8 +408,12 @@ struct Win {
     uint32_t cpre, cmsk; // this lane's chunk: terminators before it, terminator mask
 };
 
+// lsrc (MODE_WORDREV only): the stream words already staged in LDS, lsrc[i] = W(lw0 + i) for the words the
+// window needs (those before `end`), so the window costs no HBM round trip (FastPFOR's VariableByte tail
+// inside the page's meta window).  lsrc must not overlap the window or its index (win, list).
 template <int MODE, int VAL>
-__device__ void win_load(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t p, int32_t end) {
+__device__ void win_load(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t p, int32_t end, const uint32_t* lsrc = nullptr,
+                         int32_t lw0 = 0) {
     const int l = lane_id();
     uint4 d;
     int32_t woff;
@@ -424,11 +428,17 @@ __device__ void win_load(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t p, int
         const uint8_t* q = sb + woff + 16 * l;
         d = make_uint4(0, 0, 0, 0);
         if (woff + 16 * l < end) {
-            d.x = ld_be32(q);
-            d.y = ld_be32(q + 4);
-            d.z = ld_be32(q + 8);
-            d.w = ld_be32(q + 12);
+            if (lsrc) {
+                const uint32_t* ws = lsrc + ((woff + 16 * l) >> 2) - lw0;
+                d = make_uint4(ws[0], ws[1], ws[2], ws[3]);
+            } else {
+                d.x = ld_be32(q);
+                d.y = ld_be32(q + 4);
+                d.z = ld_be32(q + 8);
+                d.w = ld_be32(q + 12);
+            }
         }
+        wave_sync();  // (every lane's LDS reads before the window's writes)
     }
     ((uint4*)sm.u.v.win)[l] = d;
     if (VAL == VAL_NONE) {  // byte-oriented readers: no terminator index
@@ -567,12 +577,15 @@ __device__ __forceinline__ void win_value(const WaveSmem& sm, int32_t sj, int32_
 template <int MODE, int VAL, int K = 1, class Emit>
 __device__ int32_t varint_take(WaveSmem& sm, const uint8_t* sb, Win& w, int32_t& pos, int32_t end, int32_t want,
                                bool until_end, int32_t& err, Emit&& emit, int32_t out0 = 0,
-                               int32_t* first_bad = nullptr, int32_t line = 0) {
+                               int32_t* first_bad = nullptr, int32_t line = 0, const uint32_t* lsrc = nullptr,
+                               int32_t lw0 = 0) {
     const int l = lane_id();
     int32_t got = 0;
     while (until_end ? (pos < end) : (got < want)) {
-        if (!w.valid || pos < w.woff || pos >= w.woff + kWin || (w.serial && pos != w.p0))
-            win_load<MODE, VAL>(sm, sb, w, pos, end);
+        if (!w.valid || pos < w.woff || pos >= w.woff + kWin || (w.serial && pos != w.p0)) {
+            win_load<MODE, VAL>(sm, sb, w, pos, end, lsrc, lw0);
+            lsrc = nullptr;  // (the first window's index overwrites the staged words)
+        }
         const int32_t r = w.serial ? 0 : win_rank(sm, w, pos);
         const int32_t have = w.K - r;
         if (have <= 0) {
@@ -1376,37 +1389,58 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
     int32_t L = 0;
     int64_t p = 1;
     int xs_v = 0, xz_v = -1, xc_v = 0;  // lane k: dataTobePacked[k] start word, size, values consumed
+    FpfPre pre;                          // the first block's prefetch (its packed words: at the page start)
+    int64_t mw0 = 0;                     // stream word of cbuf[0] (the meta window)
+    bool xin = false;                    // the page's metadata fits the meta window
     if (c.byte_length > c.avail) { c.err = COVT_ERR_TRUNCATED; }
     if (!c.err && nw > 0) {
-        L = (int32_t)W.uniform(0);
+        // W[0] (L) and W[1] (the first page's whereMeta) share one scalar-cache line: one round trip
+        const uint32_t head0 = W.uniform(0), head1 = W.uniform(1);  // (the input is padded past every stream)
+        L = (int32_t)head0;
         if (L < 0) c.err = COVT_ERR_BAD_HEADER;
         L -= L % kFpfBlock;
         if (!c.err && L > c.n) c.err = COVT_ERR_COUNT_MISMATCH;
         int32_t done = 0;
         // 1 KiB of stream words from word w on the 16-byte grid, byte-swapped into dst[]:
-        // dst[m] = W(base + m) for m < 255, base = w - (0..3) returned.  One 16-byte load per lane, by the
+        // dst[m] = W(base + m) for m < 255, base = w - (0..3) returned; words at or past the stream's end
+        // (nw) read as 0, as JavaFastPFOR's reads past its int[] do.  One 16-byte load per lane, by the
         // lanes whose 16 bytes start before the stream's last word ends (like win_load: a short stream's
-        // directory or container window would otherwise fetch up to 1 KiB past it; words past the stream
-        // are never used)
+        // window would otherwise fetch up to 1 KiB past it).  Issued and finished separately, so other
+        // loads can be in flight between.
         const uintptr_t s_end = (uintptr_t)(c.sb + 4 * nw);
-        auto load_words = [&](uint32_t* dst, int64_t w) -> int64_t {
+        struct WordsRaw {
+            uint4 r;
+            int64_t base;
+            uint32_t sh;
+        };
+        auto words_issue = [&](int64_t w) -> WordsRaw {
             const uintptr_t addr = (uintptr_t)(c.sb + 4 * w);
             const uintptr_t a16 = addr & ~(uintptr_t)15;
-            const uint32_t o = (uint32_t)(addr & 15u), sh = o & 3u;
-            const uintptr_t al = a16 + 16 * (uintptr_t)l;
-            const uint4 r = al < s_end ? ld128(al) : make_uint4(0, 0, 0, 0);
-            const uint32_t nx = lane_next(r.x);
+            const uint32_t o = (uint32_t)(addr & 15u);
+            // lanes past the stream repeat the last granule (their words are zeroed by words_store): an
+            // unmasked load, so the compiler's vmcnt waits stay partial (a masked one drains every load)
+            const uint32_t lmax = s_end > a16 ? (uint32_t)((s_end - 1 - a16) >> 4) : 0u;
+            WordsRaw q;
+            q.r = ld128_off((const g_u8*)a16, 16u * min((uint32_t)l, lmax));
+            q.base = uni64(w - (int64_t)(o >> 2));
+            q.sh = o & 3u;
+            return q;
+        };
+        auto words_store = [&](uint32_t* dst, const WordsRaw& q) -> int64_t {
+            const uint32_t nx = lane_next(q.r.x);
+            const uint32_t sel = be_sel(q.sh);
+            const int64_t wl = q.base + 4 * l;  // stream word of dst[4 l]
             uint4 wv;
-            const uint32_t sel = be_sel(sh);
-            wv.x = be_word(r.y, r.x, sel);
-            wv.y = be_word(r.z, r.y, sel);
-            wv.z = be_word(r.w, r.z, sel);
-            wv.w = be_word(nx, r.w, sel);
+            wv.x = wl < nw ? be_word(q.r.y, q.r.x, sel) : 0u;
+            wv.y = wl + 1 < nw ? be_word(q.r.z, q.r.y, sel) : 0u;
+            wv.z = wl + 2 < nw ? be_word(q.r.w, q.r.z, sel) : 0u;
+            wv.w = wl + 3 < nw ? be_word(nx, q.r.w, sel) : 0u;
             wave_sync();
             ((uint4*)dst)[l] = wv;
             wave_sync();
-            return uni64(w - (int64_t)(o >> 2));
+            return q.base;
         };
+        auto load_words = [&](uint32_t* dst, int64_t w) -> int64_t { return words_store(dst, words_issue(w)); };
         while (!c.err && done < L) {
             done = uni(done);
             const bool cached = skip && skip->pdone >= 0;
@@ -1418,31 +1452,42 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
             const int32_t thissize = uni((L - done) < kFpfPage ? (L - done) : kFpfPage);
             const int64_t p0 = uni64(p);
             if (p0 >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
-            int64_t ie;
-            int32_t bytesize;
-            xc_v = 0;
-            if (cached && done == skip->pdone) {
-                bytesize = skip->bytesize;
-                ie = p0 + (int32_t)W.uniform(p0) + 1;  // the byte container
-                xs_v = skip->xs;
-                xz_v = skip->xz;
-            } else {
-                ie = p0 + (int32_t)W.uniform(p0);
-                if (ie < 0 || ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
-                bytesize = (int32_t)W.uniform(ie++);
-                if (bytesize < 0 || bytesize > kFpfBcCap) { c.err = COVT_ERR_BAD_HEADER; break; }
+            int64_t ie = p0 + (int32_t)(p0 == 1 ? head1 : W.uniform(p0));  // the page's bytesize word
+            if (ie < 0 || ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+            // One round trip for the page's metadata and its first block: the 1 KiB meta window from the
+            // bytesize word (bytesize, the byte container, and for a small page the exception directory and
+            // arrays too: 74 % of the bench batch's pages have <= 1 KiB of metadata) is staged in cbuf, and
+            // a page decoded from its first block gets that block's packed words (word p0 + 1, bit width not
+            // yet known: every lane up to the stream's end) in flight beside it.
+            // (issued for every page, also one decoded from a later block (a split chunk's first page, which
+            // requests its first block again): a load under a branch makes the compiler drain every load)
+            const WordsRaw mq = words_issue(ie);
+            const bool spec = v0 <= done && v1 > done;  // the range starts at this page's first block
+            {
+                const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)(p0 + 1)) & ~(uintptr_t)15;
+                const uint32_t lmax = s_end > a16 ? (uint32_t)((s_end - 1 - a16) >> 4) : 0u;
+                pre.raw = ld128_off((const g_u8*)a16, 16u * min((uint32_t)l, lmax));
             }
+            mw0 = words_store(sm.u.f.cbuf, mq);
+            auto mword = [&](int64_t w) -> uint32_t { return uniu(sm.u.f.cbuf[w - mw0]); };
+            const int32_t bytesize = (int32_t)mword(ie++);  // (ie - mw0 <= 3)
+            if (bytesize < 0 || bytesize > kFpfBcCap) { c.err = COVT_ERR_BAD_HEADER; break; }
+            xc_v = 0;
             const int64_t bcw = (bytesize + 3) / 4;
             const int64_t bc = ie;
             if (bc + bcw >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
             ie += bcw;
             if (cached && done == skip->pdone) {
                 ie = skip->ie_end;
+                xs_v = skip->xs;
+                xz_v = skip->xz;
             } else {
-                // exception-array directory (bitmap, then size + packed words per set bit), parsed from a
-                // 1 KiB LDS window of words; the arrays' start/size/cursor live in lanes 2..32 of VGPRs
-                int64_t dbase = load_words(sm.u.f.stage, ie);
+                // exception-array directory (bitmap, then size + packed words per set bit): from the meta
+                // window, or -- past it -- from 1 KiB LDS windows of words in stage; the arrays'
+                // start/size/cursor live in lanes 2..32 of VGPRs
+                int64_t dbase = INT64_MIN / 2;
                 auto dword = [&](int64_t w) -> uint32_t {
+                    if (w >= mw0 && w < mw0 + 255) return mword(w);
                     if (w < dbase || w >= dbase + 255) dbase = load_words(sm.u.f.stage, w);
                     return uniu(sm.u.f.stage[w - dbase]);
                 };
@@ -1471,6 +1516,12 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                     skip->xz = xz_v;
                 }
             }
+            // the whole metadata section (container, directory, exception arrays) inside the meta window:
+            // the container walk never reloads it and exception values are read from it (no global loads)
+            xin = ie - mw0 <= 255;
+            // lane 0 stands for "no exception array" in the header walk: an unbounded size (its cursor counts
+            // the other blocks' exceptions, never read as one)
+            xz_v = l == 0 ? INT32_MAX : xz_v;
             COVT_PHASE(c, 0);
             const int32_t nblocks_page = uni(thissize / kFpfBlock);
             // blocks of this page holding values of [v0, v1)
@@ -1479,7 +1530,7 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
             const int32_t nw32 = (int32_t)nw;
             const int32_t bclen = uni((int32_t)(bcw * 4));
             const uint8_t* cb8 = (const uint8_t*)sm.u.f.cbuf;
-            int32_t cbase = INT32_MIN / 2;
+            int32_t cbase = (int32_t)(4 * (mw0 - bc));  // (the meta window holds the container's start)
             auto chunk_load = [&](int32_t at) {  // container bytes [cbase, cbase + 1020), cbase in (at - 16, at]
                 cbase = (int32_t)(4 * (load_words(sm.u.f.cbuf, bc + (at >> 2)) - bc));
             };
@@ -1488,29 +1539,31 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
             auto walk = [&](int32_t cur, FpfHdr& h) -> int32_t {
                 cur = uni(cur);
                 cbase = uni(cbase);
-                if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 260)) chunk_load(cur);
+                if (!xin && (uint32_t)(cur - cbase) > (uint32_t)(1020 - 260)) chunk_load(cur);
                 const int32_t j = cur - cbase;
                 const uint32_t hw =
                     uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(j >> 2) + 1], sm.u.f.cbuf[j >> 2], (uint32_t)j & 3u));
                 const int32_t b = (int32_t)(int8_t)(hw & 0xffu);
                 const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
-                const int32_t idx = (int32_t)(int8_t)((hw >> 16) & 0xffu) - b;
-                const bool hasx = ce > 0;
-                const bool arr = hasx && idx >= 2 && idx <= 32;  // exceptions from dataTobePacked[idx]
-                const int32_t k = arr ? idx : 0;
+                const int32_t hasx = ce > 0 ? 1 : 0;
+                // exceptions: index maxbits - b; 1 = the implicit 1 << b, 2..32 = dataTobePacked[idx] (a block
+                // without exceptions gets 1, a valid index its exception code never reads)
+                const int32_t idx = hasx ? (int32_t)(int8_t)((hw >> 16) & 0xffu) - b : 1;
+                const int32_t k = (uint32_t)(idx - 2) <= 30u ? idx : 0;  // lane 0: no array
                 const int32_t xsz = __builtin_amdgcn_readlane(xz_v, k);
                 const int32_t xc = __builtin_amdgcn_readlane(xc_v, k);
-                bool bad = (uint32_t)b > 32u || cur + 2 > bclen;
-                bad |= hasx && (cur + 3 + ce > bclen || (idx != 1 && !arr));
-                bad |= arr && (xsz < 0 || xc + ce > xsz);
                 h.b = b;
                 h.ce = ce;
-                h.idx = hasx ? idx : 0;
-                h.xcur = arr ? (uint32_t)xc : 0u;
-                h.bcoff = cur + (hasx ? 3 : 2);
+                h.idx = idx;
+                h.xcur = (uint32_t)xc;  // (read only for idx >= 2)
+                h.bcoff = cur + 2 + hasx;
                 h.next = h.bcoff + ce;
-                xc_v += (l == (arr ? idx : 64)) ? ce : 0;
-                return bad ? COVT_ERR_BAD_HEADER : COVT_OK;
+                xc_v += l == k ? ce : 0;
+                // every check at once as the largest of differences that must not be positive (all operands
+                // far below 2^30): the bit width in [0, 32], the header and its exception positions inside
+                // the container, the index in [1, 32], the array holding ce more values
+                const int32_t worst = max(max(max(b - 32, -b), h.next - bclen), max(max(idx - 32, 1 - idx), xc + ce - xsz));
+                return worst > 0 ? COVT_ERR_BAD_HEADER : COVT_OK;
             };
             // (32-bit: a stream holds < 2^29 words)
             auto xword = [&](int32_t k, uint32_t xs, uint32_t i, uint32_t& xbit) -> int32_t {
@@ -1519,7 +1572,7 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                 xbit = bit & 31u;
                 return (int32_t)(xs + __umul24(i >> 5, (uint32_t)k) + (bit >> 5));
             };
-            auto prefetch = [&](const FpfHdr& hv, int32_t pkv, FpfPre& pr, int slot) {
+            auto prefetch = [&](const FpfHdr& hv, int32_t pkv, FpfPre& pr, int slot, bool raw = true) {
                 FpfHdr h;
                 h.idx = uni(hv.idx);
                 h.ce = uni(hv.ce);
@@ -1534,19 +1587,27 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                 // 2b + 2 whose 16 bytes the unpack reads repeat the last one's address, lanes without an
                 // exception read word 0.  A masked load or a select of its address under a branch made
                 // the compiler drain every outstanding load (vmcnt(0)) right after issuing the prefetch.
-                const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pk) & ~(uintptr_t)15;
-                const uint32_t lraw = min((uint32_t)l, 2u * (uint32_t)uni(hv.b) + 1u);
-                pr.raw = ld128_off((const g_u8*)a16, 16u * lraw);
+                if (raw) {  // (a page's first block: its words were requested with the meta window)
+                    const uintptr_t a16 = ((uintptr_t)c.sb + 4u * (uint32_t)pk) & ~(uintptr_t)15;
+                    const uint32_t lraw = min((uint32_t)l, 2u * (uint32_t)uni(hv.b) + 1u);
+                    pr.raw = ld128_off((const g_u8*)a16, 16u * lraw);
+                }
                 const int32_t k = h.idx;
                 const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
                 uint32_t xb;
                 const int32_t wx = xword(k >= 2 ? k : 2, xs, h.xcur + (uint32_t)l, xb);
                 const uint32_t xon = (uint32_t)(k >= 2) & (uint32_t)(l < h.ce) & (uint32_t)(wx < nw32);
-                const uint32_t wi = (uint32_t)wx & (0u - xon);
-                const u32x3 xv = *(const g_v3*)((const g_u8*)(((uintptr_t)c.sb) & ~(uintptr_t)3) + 4u * wi);
-                pr.x0 = xv.x;
-                pr.x1 = xv.y;
-                pr.x2 = xv.z;
+                // (a page whose metadata fits the meta window reads its exception words from LDS when the
+                // block is patched: no load here.  Reading them here into pr.x* would make the compiler drain
+                // every outstanding load first -- those registers are a global load's destination on the
+                // other path)
+                if (!xin) {
+                    const uint32_t wi = (uint32_t)wx & (0u - xon);
+                    const u32x3 xv = *(const g_v3*)((const g_u8*)(((uintptr_t)c.sb) & ~(uintptr_t)3) + 4u * wi);
+                    pr.x0 = xv.x;
+                    pr.x1 = xv.y;
+                    pr.x2 = xv.z;
+                }
                 const int32_t pb = h.bcoff - cbase;  // positions of exception e at cbuf byte pb + e
                 pr.pos = cb8[min(pb + l, 4 * 260 - 1)];
                 if (h.ce > 64) {  // rare: keep positions 64.. in LDS (the chunk may move on)
@@ -1556,7 +1617,6 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                 }
             };
             FpfHdr h;
-            FpfPre pre;
             int32_t pk = (int32_t)p0 + 1;
             int32_t cur0 = 0;
             // headers of the page's blocks before the range: only their offsets, packed words and exception
@@ -1570,7 +1630,7 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                 } else {
                     int32_t cur = 0, pkk = pk;
                     for (int32_t j = 0; j < jb0; ++j) {
-                        if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 8)) chunk_load(cur);
+                        if (!xin && (uint32_t)(cur - cbase) > (uint32_t)(1020 - 8)) chunk_load(cur);
                         const int32_t jj = cur - cbase;
                         const uint32_t hw = uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(jj >> 2) + 1],
                                                                             sm.u.f.cbuf[jj >> 2], (uint32_t)jj & 3u));
@@ -1671,12 +1731,18 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                     if (k != 1) {  // uniform
                         uint32_t xbit;
                         const int32_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
-                        uint64_t lo = be_word(pc.x1, pc.x0, bsel);
-                        uint64_t hi = be_word(pc.x2, pc.x1, bsel);
-                        lo = wi < nw32 ? lo : 0ull;  // words past the stream read as 0
-                        hi = (wi + 1 < nw32 && xbit + (uint32_t)k > 32u) ? hi : 0ull;
-                        const uint64_t m = k == 32 ? 0xffffffffull : ((1ull << k) - 1ull);
-                        ex = (uint32_t)(((lo | (hi << 32)) >> xbit) & m);
+                        uint32_t lo, hi;
+                        if (xin) {  // meta window: words already swapped, 0 past the stream
+                            const int32_t m = el ? wi - (int32_t)mw0 : 0;
+                            lo = sm.u.f.cbuf[m];
+                            hi = sm.u.f.cbuf[m + 1];
+                        } else {
+                            lo = wi < nw32 ? be_word(pc.x1, pc.x0, bsel) : 0u;  // words past the stream read as 0
+                            hi = wi + 1 < nw32 ? be_word(pc.x2, pc.x1, bsel) : 0u;
+                        }
+                        // bits [xbit, xbit + k) of hi:lo (xbit < 32, k <= 32)
+                        const uint32_t m = k == 32 ? 0xffffffffu : ((1u << k) - 1u);
+                        ex = __builtin_amdgcn_alignbit(hi, lo, xbit) & m;
                     }
                     // lanes without an exception OR 0 into their own slot: no branch, no conflict
                     atomicOr(&sm.u.f.patch[el ? pc.pos : (uint32_t)(4 * l)], el ? ex << (b & 31) : 0u);
@@ -1713,7 +1779,7 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
                 c.err = walk(cur0, h);
                 if (!c.err && pk + 8 * h.b > nw32) c.err = COVT_ERR_TRUNCATED;
                 if (!c.err) {
-                    prefetch(h, pk, pre, 0);
+                    prefetch(h, pk, pre, 0, !spec);
                     // (the loop is entered only from here, so its header sees these stores on every path)
                     if (!sum_only) fpf_prime_stores<OP>(c.out, (int64_t)done + (int64_t)jb0 * kFpfBlock);
                     int32_t j = jb0;
@@ -1729,18 +1795,22 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
             if (done >= v1) break;  // the range ends in this page
         }
         decoded = L;
-        // VariableByte tail over words [p, nw)
+        // VariableByte tail over words [p, nw): from the last page's meta window when the window holds it
+        // (words (4 vpos & ~15) / 4 .. nw - 1 staged in cbuf; cbuf lies past the varint window and most of
+        // its terminator list, so the window's first load reads it before anything is overwritten)
         if (!c.err && has_end && p < nw) {
             int32_t vpos = (int32_t)(4 * p);
             const int32_t base = L;
             Win w;
             w.valid = false;
+            const bool tail_in = L > 0 && ((int64_t)(vpos & ~15) >> 2) >= mw0 && nw - mw0 <= 255;
             const int32_t got = varint_take<MODE_WORDREV, VAL_VB>(
                 sm, c.sb, w, vpos, (int32_t)(4 * nw), c.n - L, true, c.err,
                 [&](const uint32_t (&lo)[1], const uint32_t (&hi)[1], int32_t vb, int32_t, int32_t count) {
                     if (sum_only) sum_values<OP, 1>(lo, (int64_t)base + vb, count, ax, ay);
                     else sink_values<OP, 1>(lo, (int64_t)base + vb, 0, count, c.nb, c.out, cr);
-                });
+                },
+                0, nullptr, 0, tail_in ? sm.u.f.cbuf : nullptr, (int32_t)mw0);
             decoded = L + got;
         }
     }

@@ -599,6 +599,7 @@ struct FastGenc {
     int32_t len;
     int32_t wb;  // tile offset of window byte 0 (16-byte aligned address; may be < 0 at the tile start)
     uint32_t segs;  // window positions [256 k, 256 k + 256) whose record tables are built: bit k
+    uint32_t lim;   // window positions [0, lim) all have their tables built
     FastSmem* fs;
     FastSmemRec* fr = nullptr;  // the property walk's tables (null: not built)
     // bytes [q, q + 8) of the window, q per lane (q <= kFwBytes - 8)
@@ -623,6 +624,7 @@ struct FastGenc {
         wb = (int32_t)(int64_t)(b - lo);
         wb = __builtin_amdgcn_readfirstlane(wb);
         segs = 0;
+        lim = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 #pragma unroll
         for (int i = 0; i < kFwBytes / 16; i += 64)
@@ -695,6 +697,8 @@ struct FastGenc {
             }
         }
         segs |= 1u << sg;
+        lim = (segs & 1u) ? ((segs & 2u) ? 512u : 256u) : 0u;
+        static_assert(kFwSpan == 512, "lim: two table segments");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         __builtin_amdgcn_wave_barrier();
@@ -704,6 +708,13 @@ struct FastGenc {
         const int32_t q = o - wb;
         if (!((segs >> (q >> 8)) & 1u)) build(q >> 8);
         return q;
+    }
+    // the same with one compare when the tables already cover o (the Id walk's property-record loop, whose
+    // scalar instructions bound the walk)
+    __device__ __forceinline__ int32_t at_run(int32_t o) {
+        const int32_t q = o - wb;
+        if ((uint32_t)q < lim) return q;
+        return at(o);
     }
     // window offset of tile offset o for plain byte reads (no tables needed)
     __device__ __forceinline__ int32_t at_bytes(int32_t o) {
@@ -772,12 +783,17 @@ __device__ int walk_genc_fast(FastGenc& f, E& emit) {
             if (kind == 1 && ns > (uint32_t)kFwGeo) return kFastFallback;
             o += (int32_t)(ce & 0xffu);
             if (kind == 2) {  // a property column (most records): only its data bytes, in a loop of its own
+                // (no per-record check: a position with no fast record there (entry 0) counts as 2^24 data
+                // bytes and 255 bytes of metadata, so the layer's data overruns the tile and the check after
+                // the layer falls back; the walk emits nothing in between.  32-bit sums: < 2^9 * 2^24 per column)
+                uint32_t dd = 0;
                 for (uint32_t s = 0; s < ns; ++s) {
-                    const uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[f.at(o)]);
-                    if (!se) return kFastFallback;
-                    d += (int32_t)(se >> 8);
+                    uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[f.at_run(o)]);
+                    se = se ? se : 0xffffffffu;
+                    dd += se >> 8;
                     o += (int32_t)(se & 0xffu);
                 }
+                d += dd;
                 continue;
             }
             uint32_t present = 0;
@@ -841,6 +857,7 @@ __device__ __forceinline__ int walk_tile(const uint8_t* bytes, uint64_t n_bytes,
         f.len = (int32_t)size;
         f.wb = -(int32_t)0x40000000;
         f.segs = 0;
+        f.lim = 0;
         f.fs = (FastSmem*)((uint8_t*)covt_walk_win + kFastSmemOffset);
         const E fresh = emit;
         const int st = walk_genc_fast(f, emit);
@@ -2165,6 +2182,7 @@ __device__ __forceinline__ int prop_walk_tile(Rd<true>& r, PE& e, PropTab& tab, 
     f.len = (int32_t)r.len;
     f.wb = -(int32_t)0x40000000;
     f.segs = 0;
+    f.lim = 0;
     f.fs = (FastSmem*)((uint8_t*)covt_walk_win + kFastSmemOffset);
     f.fr = (FastSmemRec*)((uint8_t*)covt_walk_win + kPropRecOffset);
     const PE fresh = e;

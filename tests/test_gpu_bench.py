@@ -1,6 +1,6 @@
 """The real (non-dry-run) N-rank bench path on the one-GPU test box: `bench.py --gpus 2 --share-device`
-spawns two ranks before anything touches the GPU, both decode their own batch on cuda:0 (gloo barriers,
-max-over-ranks timing), and rank 0 prints one line with both ranks' kernel times and the CPU baseline
+spawns two ranks before anything touches the GPU, both decode their shard of one batch on cuda:0 (gloo
+barriers, max-over-ranks timing; then each its own whole batch for the weak figure), and rank 0 prints one line with both ranks' kernel times and the CPU baseline
 (north_star: every 1/2/4/8 figure next to the CPU decoder in the same run)."""
 import json
 import os
@@ -26,8 +26,12 @@ def test_two_ranks_share_device(gpu_available):
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["shared_device"] and "dry_run" not in line
     pr = line["per_rank"]
-    assert [r["rank"] for r in pr] == [0, 1] and len({r["seed"] for r in pr}) == 2
-    assert all(r["kernel_ms"] > 0 and r["tiles"] == 500 for r in pr)
+    # strong scaling (the default, BASELINE config 5): the ranks share ONE 500-tile batch by LPT shards
+    assert [r["rank"] for r in pr] == [0, 1] and len({r["seed"] for r in pr}) == 1
+    assert all(r["kernel_ms"] > 0 for r in pr) and sum(r["tiles"] for r in pr) == 500
+    assert line["scaling"] == "strong" and line["config"]["tiles_total"] == 500
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
+    w = line["weak"]  # the weak figure beside it: each rank its own 500-tile batch
+    assert w["tiles_per_gpu"] == 500 and w["tiles_total"] == 1000 and len(set(w["seeds"])) == 2 and w["value"] > 0
     cb = line["cpu_baseline"]
     assert cb is not None and cb["value"] > 0 and cb["cores"] >= 1

@@ -73,6 +73,7 @@ for s in "$@"; do
     sq_rle|sq_varint|sq_fastpfor|sq_lane) fam=${s#sq_}; step $s$sfx 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     opinst) step opinst 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE -d gpurun_out/opinst -o run --output-format csv -- python tools/op_counters.py ;;
     tests_changed) step pytest_changed 600 python -u -m pytest tests/test_gpu_assembly.py tests/test_gpu_props.py tests/test_gpu_split.py tests/test_gpu_rle_adversarial.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    tests_r05) step pytest_r05 600 python -u -m pytest tests/test_gpu_assembly.py tests/test_gpu_props.py tests/test_jni_shim.py tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -s ;;
     tests_dplan) step pytest_dplan 300 python -u -m pytest tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     dplan_geo) step dplan_geo 200 python tools/device_plan_prof.py 20 --sweep --geometry ;;
     dplan_sweep) step dplan_sweep 300 python tools/device_plan_prof.py 10 --sweep ;;
