@@ -250,6 +250,44 @@ __device__ __forceinline__ void store_run(uint8_t* arr, int32_t o, int32_t n, in
     }
 }
 
+// The same for four runs at once, one per 16-lane quarter of the wave (o, n, base, delta uniform within a
+// quarter; a quarter with n <= 0 stores nothing).  The long runs of an ORC RLE batch went through store_run
+// one at a time, each iteration a chain of lane broadcasts and one store (RLE_U64 streams of long runs --
+// 6 KB of bytes, 31.5k values -- were the longest single waves of small batches).
+template <int E>
+__device__ __forceinline__ void store_run_q(uint8_t* arr, int32_t o, int32_t n, int64_t base, int32_t delta) {
+    constexpr int K = 16 / E;
+    static_assert(2 * (K - 1) <= 16, "head and tail elements fit a quarter");
+    const int q = lane_id() & 15;
+    auto val = [&](int32_t i) -> int64_t { return (int64_t)((uint64_t)base + (uint64_t)(int64_t)(int32_t)(i * delta)); };
+    const int32_t a0 = (o + K - 1) & ~(K - 1);
+    const int32_t head = n > 0 ? min(a0 - o, n) : 0;
+    const int32_t nch = n > 0 ? (n - head) / K : 0;
+    const int32_t body_end = head + nch * K;
+    const int32_t tailn = n > 0 ? n - body_end : 0;
+    if (q < head + tailn) {  // head and tail: one element per lane
+        const int32_t ti = q < head ? q : body_end + (q - head);
+        const int64_t v = val(ti);
+        if (E == 8) st_out((int64_t*)arr + o + ti, v);
+        else st_out((int32_t*)arr + o + ti, (int32_t)v);
+    }
+    const int32_t steps = (int32_t)wave_max((uint32_t)((nch + 15) >> 4));
+    for (int32_t c0 = 0; c0 < 16 * steps; c0 += 16) {
+        const int32_t ch = c0 + q;
+        if (ch < nch) {
+            const int32_t i = head + K * ch;
+            int4 w;
+            if (E == 8) {
+                const int64_t v0 = val(i), v1 = val(i + 1);
+                w = make_int4((int)v0, (int)(v0 >> 32), (int)v1, (int)(v1 >> 32));
+            } else {
+                w = make_int4((int)val(i), (int)val(i + 1), (int)val(i + 2), (int)val(i + 3));
+            }
+            st_out16((int32_t*)(arr + (int64_t)(o + i) * E), w);
+        }
+    }
+}
+
 // Per-op output transform, specialised at compile time.  Lane l holds slots base + K l .. + K - 1;
 // slots [first, first + count) of the group are values (uniform; `first` < K skips leading slots so
 // that `base` can stay a multiple of K and 16-byte stores stay aligned).  A full group takes the
@@ -979,16 +1017,30 @@ __device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
                         st_out((int64_t*)c.out + goff + i, v);
                     }
                 }
-                uint64_t bigm = __ballot(rv && take > 8);
-                while (bigm) {  // wave-uniform loop over the long runs of this batch
-                    const int src = __ffsll((long long)bigm) - 1;
-                    bigm &= bigm - 1;
-                    const int32_t o2 = (int32_t)lane_bcast((uint32_t)goff, src);
-                    const int32_t t2 = (int32_t)lane_bcast((uint32_t)take, src);
-                    const int32_t d2 = (int32_t)lane_bcast((uint32_t)delta, src);
-                    const int64_t bb = (int64_t)lane_bcast64((uint64_t)b64, src);
-                    if (to_i32) store_run<4>(c.out, o2, t2, bb, d2);  // literals[0] + used * delta
-                    else store_run<8>(c.out, o2, t2, bb, d2);
+                const bool big = rv && take > 8;
+                const uint64_t bigm = __ballot(big);
+                if (bigm) {  // the batch's long runs, compacted to lanes 0..nbig-1, four at a time
+                    const int32_t nbig = __popcll(bigm);
+                    const uint64_t below = (1ull << l) - 1ull;
+                    const int32_t dst = big ? __popcll(bigm & below) : nbig + __popcll(~bigm & below);
+                    const int32_t co = __builtin_amdgcn_ds_permute(dst << 2, goff);
+                    const int32_t ct = __builtin_amdgcn_ds_permute(dst << 2, big ? take : 0);
+                    const int32_t cd = __builtin_amdgcn_ds_permute(dst << 2, delta);
+                    const int32_t cbl = __builtin_amdgcn_ds_permute(dst << 2, (int32_t)(uint32_t)b64);
+                    const int32_t cbh = __builtin_amdgcn_ds_permute(dst << 2, (int32_t)(uint32_t)((uint64_t)b64 >> 32));
+                    for (int32_t r0 = 0; r0 < nbig; r0 += 4) {
+                        const int32_t src = r0 + (l >> 4);  // this quarter's run
+                        // (every lane_get with the whole wave active: a bpermute under a select can become a
+                        // branch, and a source lane off in EXEC reads 0)
+                        const int32_t o2 = lane_get(co, src & 63);
+                        const int32_t tk = lane_get(ct, src & 63);
+                        const int32_t t2 = src < nbig ? tk : 0;
+                        const int32_t d2 = lane_get(cd, src & 63);
+                        const int64_t bb = (int64_t)(((uint64_t)(uint32_t)lane_get(cbh, src & 63) << 32) |
+                                                     (uint32_t)lane_get(cbl, src & 63));
+                        if (to_i32) store_run_q<4>(c.out, o2, t2, bb, d2);  // literals[0] + used * delta
+                        else store_run_q<8>(c.out, o2, t2, bb, d2);
+                    }
                 }
                 COVT_PHASE(c, 3);
                 // literals: every literal value of the batch, 64 per step whatever the group sizes.
@@ -1375,7 +1427,8 @@ struct FpfSkip {
 };
 template <int OP>
 __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 = INT32_MAX, Carry cr0 = Carry{0, 0},
-                             bool sum_only = false, Carry* sums = nullptr, FpfSkip* skip = nullptr) {
+                             bool sum_only = false, Carry* sums = nullptr, FpfSkip* skip = nullptr,
+                             Carry* fin = nullptr) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
     const Words W{c.sb, c.byte_length / 4};
@@ -1828,6 +1881,28 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
         sums->x = lane_bcast(incl_scan(ax), 63);
         sums->y = lane_bcast(incl_scan(ay), 63);
     }
+    if (fin) *fin = cr;  // the running sums after the range (from cr0)
+}
+
+// A FastPFOR chunk's values were stored with the running sums from 0 at its first value: add the sums of
+// the values before it (x / y alternate by value index for the coordinate op; v0 is a multiple of 256), in
+// place, 16 bytes per lane.  (Morton codes are not linear in the sum: that op decodes twice instead.)
+template <int OP>
+__device__ __forceinline__ void fpf_add_carry(uint8_t* out, int32_t v0, int32_t v1, Carry cr) {
+    const uint32_t cx = cr.x, cy = OP == COVT_OP_FPF_ZZ_DELTA_XY ? cr.y : cr.x;
+    if ((cx | cy) == 0u) return;  // (uniform)
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's own stores of the range have completed
+    int32_t* o = (int32_t*)out;
+    for (int32_t i = v0 + 4 * lane_id(); i < v1; i += 256) {
+        if (i + 4 <= v1) {
+            typedef __attribute__((address_space(1))) i32x4 g_i4;
+            const i32x4 v = *(const g_i4*)(o + i);
+            st_out16(o + i, make_int4((int32_t)((uint32_t)v.x + cx), (int32_t)((uint32_t)v.y + cy),
+                                      (int32_t)((uint32_t)v.z + cx), (int32_t)((uint32_t)v.w + cy)));
+        } else {
+            for (int32_t k = i; k < v1; ++k) o[k] = (int32_t)((uint32_t)o[k] + (((k - v0) & 1) ? cy : cx));
+        }
+    }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -2068,11 +2143,16 @@ __device__ __forceinline__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v
             skip.xc = l <= 32 ? *slot(4 + l) : 0;
         }
     }
+    // The delta ops are linear in the carry: one decode stores the chunk's values with its own running
+    // sums (from 0), publishes them, and after the look-back adds the predecessors' sums in place (an
+    // 8 KiB read-modify-write for a 2048-value chunk instead of a second decode).  Morton decodes twice:
+    // a pass of sums only, then the decode with the carry.
+    constexpr bool kOnce = OP != COVT_OP_FPF_DELTA_MORTON;
 #pragma nounroll
     for (int pass = 0; pass < 2; ++pass) {  // one inlined copy of the decoder for both passes
         Carry sums{0u, 0u};
         c.err = 0;
-        run_fastpfor<OP>(c, v0, v1, carry, pass == 0, &sums, &skip);
+        run_fastpfor<OP>(c, v0, v1, carry, pass == 0 && !kOnce, &sums, &skip, kOnce ? &sums : nullptr);
         if (pass == 1) {
             err = c.err;
             break;
@@ -2092,6 +2172,10 @@ __device__ __forceinline__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v
         if (!err) err = own_err;
         if (err) break;
         carry = Carry{excl.sx, excl.sy};
+        if (kOnce) {  // the values are stored: add the carry (chunk 0: none)
+            fpf_add_carry<OP>(c.out, v0, v1 < c.n ? v1 : c.n, carry);
+            break;
+        }
     }
     if (lane_id() == 0 && (v1 >= c.n || err)) {  // the last chunk (or an error) sets the stream's result
         covt_stream_result r;

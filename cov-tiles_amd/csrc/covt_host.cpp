@@ -1277,7 +1277,7 @@ bool covt_resolve_options(const covt_plan_options* in, covt_plan_options& o) {
     if (o.lane_max_bytes == 0) o.lane_max_bytes = props ? COVT_LANE_MAX_BYTES_PROPS : COVT_LANE_MAX_BYTES;
     if (o.lane_max_values == 0) o.lane_max_values = props ? COVT_LANE_MAX_VALUES_PROPS : COVT_LANE_MAX_VALUES;
     return o.lane_max_bytes <= 65535 && o.lane_max_values > 0 && o.lane_max_values <= 32767 && o.split_ratio >= 0 && o.split_chunk >= 64 && o.split_values >= 256 && o.split_values % 256 == 0 &&
-           o.fpf_split_weight >= 1 && o.lane_min_streams >= 0 && o.plan_threads >= 0 && o.prefault_threads >= 1 &&
+           o.fpf_split_weight >= 1 && o.lane_min_streams >= 0 && o.split_max_streams >= 0 && o.plan_threads >= 0 && o.prefault_threads >= 1 &&
            o.device_walk >= 0 && o.device_walk <= 256 && (o.host_prefault == 0 || o.host_prefault == 1);
 }
 
@@ -1300,6 +1300,7 @@ void covt_plan_options_init(covt_plan_options* o) {
     o->host_prefault = 1;
     o->prefault_threads = 8;
     o->device_walk = 0;
+    o->split_max_streams = COVT_SPLIT_MAX_STREAMS;
 }
 
 int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
@@ -1484,6 +1485,7 @@ int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, co
         });
         const int64_t total = tot_cost.load(), n_lane = tot_lane.load();
         if (split_min >= 0 && split_ratio > 0) split_min = std::max<int64_t>(split_min, total / split_ratio);
+        if (o.split_max_streams > 0 && (int64_t)ns > o.split_max_streams) split_min = -1;
         if (n_lane < o.lane_min_streams) lane_max = -1;
     }
     const int64_t split_chunk = o.split_chunk;

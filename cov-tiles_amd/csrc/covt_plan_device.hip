@@ -2771,7 +2771,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     // the split threshold (covt_plan_create_ex step 3): nothing splits unless the largest cost passes it
     int64_t smin = o.split_min;
     if (smin >= 0 && o.split_ratio > 0) smin = std::max<int64_t>(smin, hd[2] / o.split_ratio);
-    const bool splitting = smin >= 0 && ns > 0 && hd[3] > smin;
+    const bool splitting = smin >= 0 && ns > 0 && hd[3] > smin && (o.split_max_streams <= 0 || ns <= o.split_max_streams);
     // stream arena: info | nvals | launch buckets | sorted buckets | launch order | bucket counts | descs [|
     // split: family | desc counts | offsets | RLE list | FastPFOR list | scan scratch]
     size_t dscan_tmp = 0;

@@ -43,8 +43,9 @@ class StreamScratch {
         }
         void* p = nullptr;
         if (hipMalloc(&p, bytes_) != hipSuccess) return nullptr;
-        // zero: epoch 0 is never a launch's, so no record reads as current before it is written
-        if (hipMemset(p, 0, bytes_) != hipSuccess) {
+        // zero: epoch 0 is never a launch's, so no record reads as current before it is written.  On `s`
+        // itself: a non-blocking stream (PyTorch's) is not ordered after the null stream's hipMemset
+        if (hipMemsetAsync(p, 0, bytes_, s) != hipSuccess) {
             (void)hipFree(p);
             return nullptr;
         }

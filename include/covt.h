@@ -165,7 +165,8 @@ enum covt_op {
 #define COVT_LANE_MAX_BYTES_PROPS 512 /* ... plans with COVT_PLAN_PROPERTIES */
 #define COVT_LANE_MAX_VALUES 256    /* covt_plan_options.lane_max_values 0 (auto): Id / Geometry plans */
 #define COVT_LANE_MAX_VALUES_PROPS 512 /* ... plans with COVT_PLAN_PROPERTIES */
-#define COVT_LANE_MIN_STREAMS 16384 /* default covt_plan_options.lane_min_streams */
+#define COVT_LANE_MIN_STREAMS 65536 /* default covt_plan_options.lane_min_streams */
+#define COVT_SPLIT_MAX_STREAMS 32768 /* default covt_plan_options.split_max_streams */
 
 /* Plan-layout options.  Every plan property that used to be steered by the environment is a field
  * here: a library inside a JVM or tile server plans the same way whatever its process inherited.
@@ -192,6 +193,9 @@ typedef struct covt_plan_options {
                                   1 = the same walk twice (no slots), k >= 2: k tiles per workgroup, a lane each */
     int32_t lane_max_values;   /* the lane family's value limit (<= 32767; 0: auto, COVT_LANE_MAX_VALUES or _PROPS with
                                   property columns, whose many small dictionary-index streams favour longer lanes) */
+    int64_t split_max_streams; /* plans of more streams than this split nothing (0: no bound).  Enough streams keep
+                                  every wave slot busy, and there the chunks' header re-walks and look-back cost
+                                  more than the long poles they shorten */
 } covt_plan_options;
 void covt_plan_options_init(covt_plan_options* opts);
 

@@ -95,6 +95,8 @@ for s in "$@"; do
     dplan_sq_small) step dplan_sq_small 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_BRANCH -d gpurun_out/dplan_sq_small -o run --output-format csv -- python tools/device_plan_prof.py 3 --small --nosplit ;;
     dplan_sorted) step dplan_sorted 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_sorted -o run --output-format csv -- python tools/device_plan_prof.py 10 --sorted ;;
     shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
+    shards_policy) step shards_policy 600 python tools/shard_sizes.py 20 --ns=1,2,4,8,16 --opts= \
+            --opts=lane_min_streams=16384,split_max_streams=0 --opts=split_max_streams=16384 --opts=split_max_streams=0 ;;
     ops_props) OPB_PROPS=1 step ops_props 600 python tools/op_breakdown.py ;;
     props_time) step props_time 300 python tools/props_run.py ;;
     fetch_fastpfor|fetch_varint|fetch_rle|fetch_lane|fetch_rle_props|fetch_lane_props) fam=${s#fetch_}; fam=${fam%_props}

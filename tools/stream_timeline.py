@@ -36,11 +36,22 @@ def main():
         tile_bytes = [lib[i % len(lib)] for i in range(tiles)]
     else:
         tile_bytes = [t for _, t in bench.sample_batch(bench.tile_library(), tiles, bench.SEED)]
+    for a in sys.argv[1:]:  # --shard=N/k: shard k of the N-way LPT split (bench.py's strong scaling)
+        if a.startswith("--shard="):
+            n, k = (int(x) for x in a[8:].split("/"))
+            sh = bench.lpt_shards([len(t) for t in tile_bytes], n)[k]
+            tile_bytes = [tile_bytes[i] for i in sh]
+            print("shard %d of %d: %d tiles" % (k, n, len(tile_bytes)))
     # --props: the plan also decodes every property column's streams (COVT_PLAN_PROPERTIES)
-    plan = covt.Plan.from_tiles(tile_bytes, flags=covt.PLAN_PROPERTIES if "--props" in sys.argv else 0)
+    opts = {}
+    for a in sys.argv[1:]:  # --opts=k=v,k=v: plan options (covt.PlanOptions)
+        if a.startswith("--opts="):
+            opts = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a[7:].split(",") if kv}
+    plan = covt.Plan.from_tiles(tile_bytes, flags=covt.PLAN_PROPERTIES if "--props" in sys.argv else 0,
+                                options=covt.PlanOptions(**opts))
     batch = covt.DeviceBatch(plan, "cuda")
     L = covt.lib()
-    phase = torch.zeros(plan.num_streams * 8, dtype=torch.int32, device="cuda")
+    phase = torch.zeros(max(plan.num_streams, plan.descs.size // 32) * 8, dtype=torch.int32, device="cuda")  # (a row per descriptor)
     L.covt_debug_set_phase_buffer(ctypes.c_void_p(phase.data_ptr()), ctypes.c_void_p(batch.d_desc.data_ptr()))
     for _ in range(3):
         batch.decode()
@@ -111,6 +122,8 @@ def main():
             mm = m & (b >= lo) & (b < hi)
             cells.append("%7.1f/%-8d" % (d_t[mm].sum() * TICK_US / 1e3, int(mm.sum())))
         print("%-12s" % NAMES.get(op, op) + "".join("%16s" % c for c in cells))
+    if len(ph_launch) < int(di.max()) + 1:  # (a split plan's descriptors outnumber its streams)
+        return
     ph = ph_launch[di]  # tile order
     print("shader clocks by phase (G = 1e9 clocks; RLE: 0 window 1 next[] 2 walk 3 small-groups 4 big-groups "
           "5 long-literal 7 loop; FPF: 0 page-dir 1 stage 2 walk+prefetch 3 unpack 4 exceptions 5 sink 6 tail)")
