@@ -149,7 +149,8 @@ class PlanOptions(C.Structure):
                 ("split_chunk", C.c_int64), ("split_values", C.c_int64), ("fpf_split_weight", C.c_int32),
                 ("lane_max_bytes", C.c_int32), ("lane_min_streams", C.c_int64), ("plan_threads", C.c_int32),
                 ("host_prefault", C.c_int32), ("prefault_threads", C.c_int32), ("device_walk", C.c_int32),
-                ("lane_max_values", C.c_int32), ("split_max_streams", C.c_int64)]
+                ("lane_max_values", C.c_int32), ("split_max_streams", C.c_int64),
+                ("split_grow", C.c_int32)]
 
     def __init__(self, **kw):
         super().__init__()

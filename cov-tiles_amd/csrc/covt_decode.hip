@@ -36,7 +36,16 @@ constexpr int kFpfBlock = 256;
 constexpr int kFpfPage = 65536;
 constexpr int kFpfBcCap = 3 * kFpfPage / kFpfBlock + kFpfPage;  // JavaFastPFOR byteContainer size
 
-constexpr int kLongStream = 16384;  // bytes or values: raised wave priority
+#ifndef COVT_LONG_STREAM
+#define COVT_LONG_STREAM 16384
+#endif
+#ifndef COVT_LONG_PRIO
+#define COVT_LONG_PRIO 2
+#endif
+#ifndef COVT_CHUNK_PRIO
+#define COVT_CHUNK_PRIO 2
+#endif
+constexpr int kLongStream = COVT_LONG_STREAM;  // bytes or values: raised wave priority
 #ifdef COVT_TIMING
 constexpr int kPhases = 8;            // profiling build: per-stream phase clocks
 __device__ uint32_t* covt_phase_buf;  // [n_streams][kPhases], set by covt_debug_set_phase_buffer
@@ -2219,6 +2228,8 @@ __device__ __forceinline__ int64_t decode_split_chunk(WaveSmem* sm, const uint8_
     if (lane_id() == 0) tk = atomicAdd(ctr, 1u);
     const int64_t t = (int64_t)lane_bcast(tk, 0);
     if (t >= n_chunks) return -1;
+    // chunks are pieces of the launch's longest streams: the same raised priority as a long stream's wave
+    __builtin_amdgcn_s_setprio(COVT_CHUNK_PRIO);
     const covt_stream_desc d = descs[kSplitSlots * t];
     const covt_stream_desc rg = descs[kSplitSlots * t + 1];  // the chunk's byte range
     Ctx c;
@@ -2313,7 +2324,7 @@ __device__ __forceinline__ void decode_family_wave(uint8_t* smem, const uint8_t*
     const covt_stream_desc d = descs[sid];
     if ((d.flags & (COVT_DESC_LANE | COVT_DESC_SPLIT | COVT_DESC_SPLIT_PAD)) || op_family(d.op) != FAM) return;
     // long streams are the kernel's critical path: let their waves win instruction arbitration
-    if (d.byte_length > kLongStream || d.num_values > kLongStream) __builtin_amdgcn_s_setprio(2);
+    if (d.byte_length > kLongStream || d.num_values > kLongStream) __builtin_amdgcn_s_setprio(COVT_LONG_PRIO);
 #ifdef COVT_TIMING  // profiling build (libcovt_timing.so): result = (duration, start) in 100 MHz ticks
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif

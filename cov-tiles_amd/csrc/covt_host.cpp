@@ -605,7 +605,25 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
         if (mode == COVT_LAUNCH_FUSED || (mode == COVT_LAUNCH_AUTO && waves <= kFusedMaxWaves))
             return covt_launch_fused(d_in, d_desc, counts, d_out, d_res, s);
     }
-    if (splits) {
+#ifndef COVT_SPLIT_LAYOUT
+#define COVT_SPLIT_LAYOUT 0
+#endif
+    if (splits && COVT_SPLIT_LAYOUT == 1) {
+        add(COVT_FAMILY_VARINT, kSplitV, kSplitR);
+        add(COVT_FAMILY_FASTPFOR, -1, -1);
+        add(COVT_FAMILY_RLE, COVT_FAMILY_LANE, -1);
+        add(kSplitF, -1, -1);
+    } else if (splits && COVT_SPLIT_LAYOUT == 2) {
+        add(COVT_FAMILY_VARINT, kSplitV, -1);
+        add(COVT_FAMILY_FASTPFOR, kSplitF, -1);
+        add(COVT_FAMILY_RLE, kSplitR, -1);
+        add(COVT_FAMILY_LANE, -1, -1);
+    } else if (splits && COVT_SPLIT_LAYOUT == 3) {
+        add(kSplitF, kSplitV, kSplitR);
+        add(COVT_FAMILY_FASTPFOR, -1, -1);
+        add(COVT_FAMILY_VARINT, -1, -1);
+        add(COVT_FAMILY_RLE, COVT_FAMILY_LANE, -1);
+    } else if (splits) {
         // RLE chunks behind the varint queue (round 2 A/B: with the RLE family, config 3 0.132 -> 0.150 ms)
         add(kSplitV, COVT_FAMILY_VARINT, kSplitR);
         add(COVT_FAMILY_FASTPFOR, -1, -1);
@@ -1277,7 +1295,7 @@ bool covt_resolve_options(const covt_plan_options* in, covt_plan_options& o) {
     if (o.lane_max_bytes == 0) o.lane_max_bytes = props ? COVT_LANE_MAX_BYTES_PROPS : COVT_LANE_MAX_BYTES;
     if (o.lane_max_values == 0) o.lane_max_values = props ? COVT_LANE_MAX_VALUES_PROPS : COVT_LANE_MAX_VALUES;
     return o.lane_max_bytes <= 65535 && o.lane_max_values > 0 && o.lane_max_values <= 32767 && o.split_ratio >= 0 && o.split_chunk >= 64 && o.split_values >= 256 && o.split_values % 256 == 0 &&
-           o.fpf_split_weight >= 1 && o.lane_min_streams >= 0 && o.split_max_streams >= 0 && o.plan_threads >= 0 && o.prefault_threads >= 1 &&
+           o.fpf_split_weight >= 1 && o.lane_min_streams >= 0 && o.split_max_streams >= 0 && (o.split_grow == 0 || o.split_grow == 1) && o.plan_threads >= 0 && o.prefault_threads >= 1 &&
            o.device_walk >= 0 && o.device_walk <= 256 && (o.host_prefault == 0 || o.host_prefault == 1);
 }
 
@@ -1301,6 +1319,7 @@ void covt_plan_options_init(covt_plan_options* o) {
     o->prefault_threads = 8;
     o->device_walk = 0;
     o->split_max_streams = COVT_SPLIT_MAX_STREAMS;
+    o->split_grow = 1;
 }
 
 int covt_plan_create_ex(const uint8_t* bytes, const uint64_t* tile_offsets, const uint64_t* tile_sizes,
@@ -1468,6 +1487,7 @@ int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, co
     int64_t split_min = o.split_min;
     const int64_t split_ratio = o.split_ratio;
     int32_t lane_max = lane_limits(o.lane_max_bytes, o.lane_max_values);
+    int64_t grow = 1;
     {
         // batch totals: cost (split threshold) and the streams the lane kernel would take (it decodes 64
         // streams per wave, each serially: a wave of 100-250-value streams takes ~80-110 us, worth it only
@@ -1487,9 +1507,10 @@ int covt_plan_create_opts(const uint8_t* bytes, const uint64_t* tile_offsets, co
         if (split_min >= 0 && split_ratio > 0) split_min = std::max<int64_t>(split_min, total / split_ratio);
         if (o.split_max_streams > 0 && (int64_t)ns > o.split_max_streams) split_min = -1;
         if (n_lane < o.lane_min_streams) lane_max = -1;
+        grow = split_grow_factor(total, o.split_grow);
     }
-    const int64_t split_chunk = o.split_chunk;
-    const int64_t split_values = o.split_values;  // FastPFOR: whole blocks
+    const int64_t split_chunk = o.split_chunk * grow;
+    const int64_t split_values = o.split_values * grow;  // FastPFOR: whole blocks
     // long RLE streams: chunk boundaries from the host walk (stream index -> chunks, consumed)
     std::unordered_map<size_t, std::pair<std::vector<RleChunk>, int32_t>> rle_split;
     if (split_min >= 0) {

@@ -119,6 +119,15 @@ __host__ __device__ inline bool split_stream(int op, int32_t num_values, int64_t
     return split_op(op) && !(op == COVT_OP_VARINT_ZZ_DELTA_XY && (num_values & 1));
 }
 
+// covt_plan_options.split_grow: chunks (split_chunk bytes, split_values values) doubled for plans of >= 4 MiB of
+// cost and quadrupled from 48 MiB.  In a plan whose streams fill the chip a chunk wave shares its SIMD with
+// the crowd, and its fixed costs (start state, look-back) weigh more than a longer body
+// (profiles/r05/shard_sizes.txt: 2 KiB chunks best for one tile, 4 KiB for 8-30 MiB plans, 8 KiB above)
+__host__ __device__ inline int64_t split_grow_factor(int64_t total_cost, int32_t grow) {
+    if (!grow) return 1;
+    return total_cost >= (48ll << 20) ? 4 : total_cost >= (4ll << 20) ? 2 : 1;
+}
+
 // FastPFOR split chunks: the host-walked start state in pads [2..7] of the chunk (covt_host.cpp
 // fpf_chunk_states): seven int32 slots per pad, every field but op / num_bits / flags
 constexpr int kFpfStateSlots = 42;

@@ -2772,6 +2772,8 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     int64_t smin = o.split_min;
     if (smin >= 0 && o.split_ratio > 0) smin = std::max<int64_t>(smin, hd[2] / o.split_ratio);
     const bool splitting = smin >= 0 && ns > 0 && hd[3] > smin && (o.split_max_streams <= 0 || ns <= o.split_max_streams);
+    const int64_t grow = split_grow_factor(hd[2], o.split_grow);
+    const int64_t schunk = o.split_chunk * grow, svalues = o.split_values * grow;
     // stream arena: info | nvals | launch buckets | sorted buckets | launch order | bucket counts | descs [|
     // split: family | desc counts | offsets | RLE list | FastPFOR list | scan scratch]
     size_t dscan_tmp = 0;
@@ -2862,13 +2864,13 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         auto *sndesc = (int64_t*)(sa + o_sn), *dn = (int64_t*)(sa + o_dn), *dpos = (int64_t*)(sa + o_dp);
         auto *rle_list = (uint32_t*)(sa + o_rl), *fpf_list = (uint32_t*)(sa + o_fl);
         const int walkers = (int)std::min<int64_t>(ns, 1024);
-        split_mark<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, smin, o.split_chunk,
-                                            o.split_values, fpf_w, totals, sfam, sndesc, rle_list, fpf_list);
+        split_mark<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, smin, schunk,
+                                            svalues, fpf_w, totals, sfam, sndesc, rle_list, fpf_list);
         DCHK(hipGetLastError());
         auto* chunks = (int4*)(sa + o_ch);
         auto* rle_base = (int64_t*)(sa + o_rb);
         auto* rle_cons = (int32_t*)(sa + o_rc);
-        rle_chunks_walk<<<walkers, 64, kStreamRdLds, s>>>(d_bytes, p->d_info, nvals, totals, rle_list, o.split_chunk, sfam,
+        rle_chunks_walk<<<walkers, 64, kStreamRdLds, s>>>(d_bytes, p->d_info, nvals, totals, rle_list, schunk, sfam,
                                                  sndesc, chunks, chunk_cap, rle_base, rle_cons);
         DCHK(hipGetLastError());
         stream_keys<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, ns, lane_max, lane_min, totals, q0, sfam, sndesc);
@@ -2885,11 +2887,11 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         p->n_descs = nd;
         p->d_desc = (covt_stream_desc*)p->desc_arena;
         p->d_order = (uint32_t*)((uint8_t*)p->desc_arena + up256((size_t)nd * sizeof(covt_stream_desc)));
-        fill_split_descs<<<(int)((nd + 255) / 256), 256, 0, s>>>(p->d_info, nvals, v1, dpos, ns, nd, sfam, o.split_chunk,
-                                                                 o.split_values, chunks, rle_base, rle_cons, p->d_desc,
+        fill_split_descs<<<(int)((nd + 255) / 256), 256, 0, s>>>(p->d_info, nvals, v1, dpos, ns, nd, sfam, schunk,
+                                                                 svalues, chunks, rle_base, rle_cons, p->d_desc,
                                                                  p->d_order);
         DCHK(hipGetLastError());
-        fpf_states_walk<<<walkers, 64, kStreamRdLds, s>>>(d_bytes, p->d_info, nvals, totals, fpf_list, o.split_values, p->d_desc);
+        fpf_states_walk<<<walkers, 64, kStreamRdLds, s>>>(d_bytes, p->d_info, nvals, totals, fpf_list, svalues, p->d_desc);
         DCHK(hipGetLastError());
     }
     if (props) {  // property output layout and the largest-first descriptor order (after the stream descriptors)

@@ -166,7 +166,7 @@ enum covt_op {
 #define COVT_LANE_MAX_VALUES 256    /* covt_plan_options.lane_max_values 0 (auto): Id / Geometry plans */
 #define COVT_LANE_MAX_VALUES_PROPS 512 /* ... plans with COVT_PLAN_PROPERTIES */
 #define COVT_LANE_MIN_STREAMS 65536 /* default covt_plan_options.lane_min_streams */
-#define COVT_SPLIT_MAX_STREAMS 32768 /* default covt_plan_options.split_max_streams */
+#define COVT_SPLIT_MAX_STREAMS 65536 /* default covt_plan_options.split_max_streams */
 
 /* Plan-layout options.  Every plan property that used to be steered by the environment is a field
  * here: a library inside a JVM or tile server plans the same way whatever its process inherited.
@@ -196,6 +196,8 @@ typedef struct covt_plan_options {
     int64_t split_max_streams; /* plans of more streams than this split nothing (0: no bound).  Enough streams keep
                                   every wave slot busy, and there the chunks' header re-walks and look-back cost
                                   more than the long poles they shorten */
+    int32_t split_grow;        /* 1 (default): split_chunk / split_values doubled for plans of >= 4 MiB of cost and
+                                  quadrupled from 48 MiB (covt_internal.h split_grow_factor); 0: fixed */
 } covt_plan_options;
 void covt_plan_options_init(covt_plan_options* opts);
 

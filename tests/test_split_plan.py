@@ -268,12 +268,12 @@ def test_options_validated(covt):
     """Out-of-range options are COVT_ERR_INVALID_ARG (IllegalArgumentException), not silently clamped."""
     for kw in ({"split_chunk": 63}, {"split_values": 300}, {"split_values": 0}, {"fpf_split_weight": 0},
                {"split_ratio": -1}, {"plan_threads": -2}, {"prefault_threads": 0}, {"host_prefault": 2},
-               {"device_walk": 257}, {"flags": 0x80}, {"split_max_streams": -1}):
+               {"device_walk": 257}, {"flags": 0x80}, {"split_max_streams": -1}, {"split_grow": 2}):
         with pytest.raises(covt.IllegalArgumentException):
             covt.Plan.from_tiles([_tile()], options=covt.PlanOptions(**kw))
     o = covt.PlanOptions()
     assert (o.split_min, o.split_ratio, o.split_chunk, o.split_values, o.lane_max_bytes, o.lane_min_streams,
-            o.lane_max_values, o.split_max_streams) == (8192, 3000, 2048, 2048, 0, 65536, 0, 32768)  # lane limits 0: auto
+            o.lane_max_values, o.split_max_streams, o.split_grow) == (8192, 3000, 2048, 2048, 0, 65536, 0, 65536, 1)
     for kw in ({"lane_max_bytes": 65536}, {"lane_max_values": 32768}, {"lane_max_values": -1}):
         with pytest.raises(covt.IllegalArgumentException):
             covt.Plan.from_tiles([_tile()], options=covt.PlanOptions(**kw))

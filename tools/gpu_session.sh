@@ -94,6 +94,35 @@ for s in "$@"; do
     dplan_api_small) step dplan_api_small 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_api_small -o run --output-format csv -- python tools/device_plan_prof.py 20 --small --nosplit ;;
     dplan_sq_small) step dplan_sq_small 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_BRANCH -d gpurun_out/dplan_sq_small -o run --output-format csv -- python tools/device_plan_prof.py 3 --small --nosplit ;;
     dplan_sorted) step dplan_sorted 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_sorted -o run --output-format csv -- python tools/device_plan_prof.py 10 --sorted ;;
+    timeline_shard8) step timeline_shard8 300 python tools/stream_timeline.py --shard=8/0 ;;
+    shards_ratio) step shards_ratio 600 python tools/shard_sizes.py 20 --ns=4,8 --opts= \
+            --opts=split_max_streams=0,split_ratio=200 --opts=split_max_streams=0,split_ratio=500 \
+            --opts=split_max_streams=0,split_ratio=1000 --opts=split_max_streams=0,split_ratio=500,split_chunk=8192,split_values=8192 ;;
+    shards_big) step shards_big 600 python tools/shard_sizes.py 20 --ns=1,4,8 --opts= \
+            --opts=split_max_streams=0,split_ratio=1500,split_chunk=8192,split_values=8192 \
+            --opts=split_max_streams=0,split_ratio=1500,split_chunk=16384,split_values=16384 \
+            --opts=split_max_streams=0,split_ratio=2500,split_chunk=8192,split_values=8192 \
+            --opts=split_max_streams=0,split_ratio=2500,split_chunk=4096,split_values=4096 ;;
+    timeline_shard8s) step timeline_shard8s 300 python tools/stream_timeline.py --shard=8/0 --opts=split_max_streams=0 && \
+        step timeline_shard4s 300 python tools/stream_timeline.py --shard=4/0 --opts=split_max_streams=0,split_ratio=2500,split_chunk=8192,split_values=8192 && \
+        step timeline_shard4 300 python tools/stream_timeline.py --shard=4/0 ;;
+    shards_layout) for v in ${AB_VARIANTS:-libcovt.so libcovt_sl1.so libcovt_sl2.so libcovt_sl3.so}; do
+            echo "== layout $v"; COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/shard_sizes.py 20 --ns=4,8 \
+            --opts=split_max_streams=0 --opts=split_max_streams=0,split_ratio=2500,split_chunk=8192,split_values=8192 \
+            --opts=split_max_streams=0,split_ratio=6000,split_chunk=4096,split_values=4096 2>&1 | grep -A4 "slowest shard ms per N" || fatal shards_layout $?
+        done ;;
+    long_poles) step long_poles4 300 python tools/long_poles.py 20 --shard=4/0 && step long_poles8 300 python tools/long_poles.py 20 --shard=8/0 ;;
+    shards_prio) for v in ${AB_VARIANTS:-libcovt.so libcovt_p0.so libcovt_L64.so libcovt_p3L64.so}; do
+            echo "== prio $v"; COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/shard_sizes.py 20 --ns=1,4,8 --opts= --opts= 2>&1 | grep -A3 "slowest shard ms per N" || fatal shards_prio $?
+        done ;;
+    shards_cprio) for v in ${AB_VARIANTS:-libcovt.so libcovt_cp0.so libcovt_sl1.so}; do
+            echo "== chunk prio $v"; COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/shard_sizes.py 20 --ns=1,4,8,16 --opts= --opts=split_max_streams=0 \
+            --opts=split_max_streams=0,split_chunk=8192,split_values=8192 --opts=split_max_streams=0,split_ratio=2000,split_chunk=8192,split_values=8192 2>&1 | grep -A5 "slowest shard ms per N" || fatal shards_cprio $?
+        done ;;
+    shards_chunk) step shards_chunk 900 python tools/shard_sizes.py 20 --ns=8,16,32,64 --configs --opts= --opts=split_max_streams=0 \
+            --opts=split_max_streams=0,split_chunk=4096,split_values=4096 --opts=split_max_streams=0,split_chunk=8192,split_values=8192 \
+            --opts=split_max_streams=0,split_chunk=16384,split_values=16384 ;;
+    shards_grow) step shards_grow 900 python tools/shard_sizes.py 20 --ns=1,2,4,8,16,32,64 --configs --opts= --opts=split_grow=0,split_max_streams=32768 ;;
     shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
     shards_policy) step shards_policy 600 python tools/shard_sizes.py 20 --ns=1,2,4,8,16 --opts= \
             --opts=lane_min_streams=16384,split_max_streams=0 --opts=split_max_streams=16384 --opts=split_max_streams=0 ;;

@@ -7,7 +7,7 @@ decode launch timed alone on this GPU (HIP events, mean of --steps after --warmu
 long as its slowest shard, so `projected_gbps` = the whole batch's stream bytes / the slowest shard's
 launch: what the strong-scaling line would report with no host-side effects.  `frac` is each shard's own
 algorithmic bytes over its launch time against the 8 TB/s peak; `vs_full` its GB/s against the full batch's.
-usage: shard_sizes.py [steps] [--ns=1,2,4,8] [--opts=split_ratio=12000,split_min=4096 ...] (several --opts: each a
+usage: shard_sizes.py [steps] [--ns=1,2,4,8] [--configs] [--opts=split_ratio=12000,split_min=4096 ...] (several --opts: each a
 variant, the slowest shard per N of each printed at the end)"""
 import os
 import sys
@@ -38,7 +38,7 @@ def main():
     if len(variants) > 1:
         print("slowest shard ms per N:", flush=True)
         for opts, worst in summary:
-            print("  %-40s %s" % (opts or "defaults", "  ".join("N=%d %.4f" % (n, w) for n, w in worst)), flush=True)
+            print("  %-40s %s" % (opts or "defaults", "  ".join(w for _, w in worst)), flush=True)
 
 
 def run(ns, steps, opts):
@@ -85,7 +85,7 @@ def run(ns, steps, opts):
                 n, k, len(sh), plan.in_bytes / 1e6, plan.out_bytes / 1e6, ms, gbps, frac,
                 gbps / full_gbps if full_gbps else float("nan")), flush=True)
             del batch, plan
-        worsts.append((n, worst))
+        worsts.append((n, "N=%d %.4f" % (n, worst)))
         if full_bytes:
             print("    N=%d: slowest shard %.4f ms -> projected strong-scaling value %.1f GB/s (%.2fx of N=1, "
                   "efficiency %.3f)" % (n, worst, full_bytes / (worst * 1e-3) / 1e9,
@@ -93,7 +93,26 @@ def run(ns, steps, opts):
                                          full_bytes / (worst * 1e-3) / 1e9 / full_gbps / n), flush=True)
 
 
-
+    if "--configs" in sys.argv:  # BASELINE configs 2-4: the config leg's subset launch under these options
+        lib = bench.tile_library()
+        for name in ("config2", "config3", "config4"):
+            picks = bench.config_tiles(lib, name)
+            plan = covt.Plan.from_tiles([t for _, t in picks], covt.FORMAT_GENC, 0, options=popts)
+            batch = covt.DeviceBatch(plan, dev)
+            sub = batch.subset(bench.config_mask(plan, name))
+            for _ in range(5):
+                sub.decode(stream)
+            torch.cuda.synchronize(dev)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+            for s_, e_ in ev:
+                s_.record(stream)
+                sub.decode(stream)
+                e_.record(stream)
+            torch.cuda.synchronize(dev)
+            ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+            print("%s: %.4f ms" % (name, ms), flush=True)
+            worsts.append((name, "%s %.4f" % (name, ms)))
+            del sub, batch, plan
     return worsts
 
 

@@ -70,6 +70,25 @@ def main():
     op_t[:] = ops[di] + 100 * lane[di]  # lane-kernel streams: op + 100
     d_t = dur  # results are in tile order
     st_t = start
+    fl = plan.descs.reshape(-1, 32)[:, 26]
+    heads = np.nonzero(((fl & covt.DESC_SPLIT) != 0) & ((fl & covt.DESC_SPLIT_PAD) == 0))[0]
+    if heads.size:  # split streams: (duration, start) of each chunk in its head descriptor's phase row
+        hs = plan.desc_streams[heads]
+        c_st = ph_launch[heads, 1]
+        c_en = c_st + ph_launch[heads, 0]
+        sst = np.full(len(s), np.iinfo(np.int64).max)
+        sen = np.zeros(len(s), dtype=np.int64)
+        np.minimum.at(sst, hs, c_st)
+        np.maximum.at(sen, hs, c_en)
+        sp = np.unique(hs)
+        st_t = st_t.copy()
+        d_t = d_t.copy()
+        st_t[sp] = sst[sp]
+        d_t[sp] = sen[sp] - sst[sp]
+        op_t[sp] += 200  # split streams: op + 200 (first chunk start -> last chunk end)
+        print("split: %d streams in %d chunks, chunk wave-time %.1f us, p50 chunk %.1f us, max chunk %.1f us" % (
+            sp.size, heads.size, ph_launch[heads, 0].sum() * TICK_US, np.percentile(ph_launch[heads, 0], 50) * TICK_US,
+            ph_launch[heads, 0].max() * TICK_US))
     t0 = st_t.min()
     end_t = st_t - t0 + d_t
     print("launch span %.1f us (first start -> last end); %d streams" % (end_t.max() * TICK_US, len(s)))
@@ -92,9 +111,13 @@ def main():
         print("   %-12s %8d %8d  start %7.1f  dur %7.1f" % (NAMES.get(int(op_t[i]), op_t[i]), s["byte_length"][i],
                                                           s["num_values"][i], (st_t[i] - t0) * TICK_US,
                                                           d_t[i] * TICK_US))
+    for o, n in list(NAMES.items()):
+        if o < 100:
+            NAMES[o + 200] = "S_" + n
     fam_of = {1: 0, 2: 0, 3: 0, 4: 0, 16: 0}
     for fam, name in enumerate(("RLE", "VARINT", "FASTPFOR", "LANE")):
-        m = np.array([(3 if o >= 100 else fam_of.get(int(o), 2 if o in (10, 11, 12) else 1)) == fam for o in op_t])
+        m = np.array([(3 if 100 <= o < 200 else fam_of.get(int(o) % 200, 2 if o % 200 in (10, 11, 12) else 1)) == fam
+                      for o in op_t])
         if m.any():
             print("  family %-8s first start %7.1f us  last start %7.1f us  last end %7.1f us  wave-time %9.1f us"
                   % (name, (st_t[m].min() - t0) * TICK_US, (st_t[m].max() - t0) * TICK_US, end_t[m].max() * TICK_US,
