@@ -605,25 +605,7 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
         if (mode == COVT_LAUNCH_FUSED || (mode == COVT_LAUNCH_AUTO && waves <= kFusedMaxWaves))
             return covt_launch_fused(d_in, d_desc, counts, d_out, d_res, s);
     }
-#ifndef COVT_SPLIT_LAYOUT
-#define COVT_SPLIT_LAYOUT 0
-#endif
-    if (splits && COVT_SPLIT_LAYOUT == 1) {
-        add(COVT_FAMILY_VARINT, kSplitV, kSplitR);
-        add(COVT_FAMILY_FASTPFOR, -1, -1);
-        add(COVT_FAMILY_RLE, COVT_FAMILY_LANE, -1);
-        add(kSplitF, -1, -1);
-    } else if (splits && COVT_SPLIT_LAYOUT == 2) {
-        add(COVT_FAMILY_VARINT, kSplitV, -1);
-        add(COVT_FAMILY_FASTPFOR, kSplitF, -1);
-        add(COVT_FAMILY_RLE, kSplitR, -1);
-        add(COVT_FAMILY_LANE, -1, -1);
-    } else if (splits && COVT_SPLIT_LAYOUT == 3) {
-        add(kSplitF, kSplitV, kSplitR);
-        add(COVT_FAMILY_FASTPFOR, -1, -1);
-        add(COVT_FAMILY_VARINT, -1, -1);
-        add(COVT_FAMILY_RLE, COVT_FAMILY_LANE, -1);
-    } else if (splits) {
+    if (splits) {
         // RLE chunks behind the varint queue (round 2 A/B: with the RLE family, config 3 0.132 -> 0.150 ms)
         add(kSplitV, COVT_FAMILY_VARINT, kSplitR);
         add(COVT_FAMILY_FASTPFOR, -1, -1);

@@ -123,6 +123,13 @@ for s in "$@"; do
             --opts=split_max_streams=0,split_chunk=4096,split_values=4096 --opts=split_max_streams=0,split_chunk=8192,split_values=8192 \
             --opts=split_max_streams=0,split_chunk=16384,split_values=16384 ;;
     shards_grow) step shards_grow 900 python tools/shard_sizes.py 20 --ns=1,2,4,8,16,32,64 --configs --opts= --opts=split_grow=0,split_max_streams=32768 ;;
+    n4) step timeline_n4s 300 python tools/stream_timeline.py --shard=4/0 --opts=split_max_streams=0 && \
+        step shards_n4 600 python tools/shard_sizes.py 20 --ns=4,8 --opts= --opts=split_max_streams=0 --opts=split_max_streams=0,fpf_split_weight=2 \
+            --opts=split_max_streams=0,split_ratio=6000 --opts=split_max_streams=0,split_ratio=1500 ;;
+    shards_w) for v in ${AB_VARIANTS:-libcovt.so libcovt_sl1.so}; do
+            echo "== $v"; COVT_LIB_VARIANT=$v timeout -k 10 400 python tools/shard_sizes.py 20 --ns=2,4,8,16,32 --configs --opts= --opts=split_max_streams=0 \
+            --opts=fpf_split_weight=2 --opts=split_max_streams=0,fpf_split_weight=2 2>&1 | grep -A5 "slowest shard ms per N" || fatal shards_w $?
+        done ;;
     shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
     shards_policy) step shards_policy 600 python tools/shard_sizes.py 20 --ns=1,2,4,8,16 --opts= \
             --opts=lane_min_streams=16384,split_max_streams=0 --opts=split_max_streams=16384 --opts=split_max_streams=0 ;;
