@@ -130,6 +130,9 @@ for s in "$@"; do
             echo "== $v"; COVT_LIB_VARIANT=$v timeout -k 10 400 python tools/shard_sizes.py 20 --ns=2,4,8,16,32 --configs --opts= --opts=split_max_streams=0 \
             --opts=fpf_split_weight=2 --opts=split_max_streams=0,fpf_split_weight=2 2>&1 | grep -A5 "slowest shard ms per N" || fatal shards_w $?
         done ;;
+    fetch_fpf_ab) for v in ${AB_VARIANTS:-libcovt_prev.so libcovt.so libcovt_s8.so}; do
+            COVT_LIB_VARIANT=$v step fetch_fpf_$v 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/fetch_fpf_$v -o run --output-format csv -- python tools/family_run.py fastpfor 2
+        done ;;
     shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
     shards_policy) step shards_policy 600 python tools/shard_sizes.py 20 --ns=1,2,4,8,16 --opts= \
             --opts=lane_min_streams=16384,split_max_streams=0 --opts=split_max_streams=16384 --opts=split_max_streams=0 ;;

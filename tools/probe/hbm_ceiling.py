@@ -84,12 +84,23 @@ def main():
             tb = units * 1024 * (1 + R)
             print("copy1:%d nt=%d blocks=%6d: %.3f ms  %5.0f GB/s (r %d MB + w %d MB)" % (
                 R, nt, blocks, t, tb / t / 1e6, units * 1024 // 1000000, units * 1024 * R // 1000000))
+    hc.probe_copy_depth.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    for depth in (2, 4):  # D loads in flight per lane (k_copy_d)
+        for blocks in (1024, 2048, 4096, 8192, 16384):
+            t = timed(lambda: hc.probe_copy_depth(inb.data_ptr(), units, R, out.data_ptr(), depth, blocks, stream))
+            tb = units * 1024 * (1 + R)
+            print("copy1:%d depth=%d blocks=%6d: %.3f ms  %5.0f GB/s" % (R, depth, blocks, t, tb / t / 1e6))
     # copy 1:1 (the guide's float4 copy shape)
     half = min(r16, n16 // 2) // 64
     for blocks in (4096, 8192, 16384):
         t = timed(lambda: hc.probe_copy(out.data_ptr(), half, 1, out.data_ptr() + half * 1024, 1, blocks, stream))
         print("copy1:1 nt=1 blocks=%6d: %.3f ms  %5.0f GB/s (r+w %d MB)" % (blocks, t, 2 * half * 1024 / t / 1e6,
                                                                            2 * half * 1024 // 1000000))
+    for depth in (2, 4):
+        for blocks in (2048, 4096, 8192, 16384):
+            t = timed(lambda: hc.probe_copy_depth(out.data_ptr(), half, 1, out.data_ptr() + half * 1024, depth, blocks,
+                                                  stream))
+            print("copy1:1 depth=%d blocks=%6d: %.3f ms  %5.0f GB/s" % (depth, blocks, t, 2 * half * 1024 / t / 1e6))
     x = out[: 4 * (w_total // 4)].view(torch.int32)
     t = timed(lambda: x.fill_(3))
     print("torch fill_ of the output bytes: %.3f ms  %5.0f GB/s" % (t, w_total / t / 1e6))
