@@ -133,6 +133,11 @@ for s in "$@"; do
     fetch_fpf_ab) for v in ${AB_VARIANTS:-libcovt_prev.so libcovt.so libcovt_s8.so}; do
             COVT_LIB_VARIANT=$v step fetch_fpf_$v 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/fetch_fpf_$v -o run --output-format csv -- python tools/family_run.py fastpfor 2
         done ;;
+    dplan_lib) rm -f gpurun_out/dplan_lib.log; for v in ${AB_VARIANTS:-libcovt_r0.so libcovt.so libcovt_r0.so libcovt.so}; do
+            echo "== $v" >> gpurun_out/dplan_lib.log
+            COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/device_plan_prof.py 20 >> gpurun_out/dplan_lib.log 2>&1 || fatal dplan_lib $?
+        done ;;
+    tests_dplan) step pytest_dplan 600 python -u -m pytest tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
     shards_policy) step shards_policy 600 python tools/shard_sizes.py 20 --ns=1,2,4,8,16 --opts= \
             --opts=lane_min_streams=16384,split_max_streams=0 --opts=split_max_streams=16384 --opts=split_max_streams=0 ;;
