@@ -195,7 +195,7 @@ typedef struct covt_plan_options {
                                   property columns, whose many small dictionary-index streams favour longer lanes) */
     int64_t split_max_streams; /* plans of more streams than this split nothing (0: no bound).  Enough streams keep
                                   every wave slot busy, and there the chunks' header re-walks and look-back cost
-                                  more than the long poles they shorten (DESIGN.md section 10.2) */
+                                  more than the long poles they shorten (DESIGN.md section 7) */
     int32_t split_grow;        /* 1 (default): split_chunk / split_values doubled for plans of >= 4 MiB of cost and
                                   quadrupled from 48 MiB (covt_internal.h split_grow_factor); 0: fixed */
 } covt_plan_options;
