@@ -300,3 +300,47 @@ def test_lane_limits_auto_by_plan_flags(covt):
                                            options=covt.PlanOptions(lane_min_streams=0, lane_max_bytes=64,
                                                                     lane_max_values=100)))
     assert ls["avail"].max() <= 64 and ls["num_values"].max() <= 100
+
+
+def _chunk_units(covt, plan):
+    """(varint chunk bytes, FastPFOR chunk values) seen in a plan's split descriptors (None: no such chunk)"""
+    d = plan.descs.view(DESC)
+    fam0 = int(plan.family_counts[:covt.FAMILY_SPLIT].sum())
+    sp = d[fam0:]
+    units = {"varint": set(), "fpf": set()}
+    for k in range(0, sp.size, covt.SPLIT_SLOTS):
+        cd, rg = sp[k], sp[k + 1]
+        if cd["flags"] & covt.DESC_SPLIT_RLE or int(cd["avail"]) != 0:
+            continue
+        kind = "fpf" if cd["flags"] & covt.DESC_SPLIT_FPF else "varint"
+        nxt = k + covt.SPLIT_SLOTS
+        if nxt < sp.size and int(sp[nxt]["avail"]) == 1:  # a first chunk with a successor: a full chunk
+            units[kind].add(int(rg["out_off"]) - int(rg["in_off"]))
+    return units
+
+
+def test_split_grow_and_max_streams(covt):
+    """covt_plan_options.split_grow: chunks double for plans of >= 4 MiB of cost and quadruple from 48 MiB
+    (covt_internal.h split_grow_factor, the same in the device plan); split_max_streams: a plan of more streams
+    splits nothing."""
+    import glob
+
+    names = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "tiles", "omt", "*.covt")))
+    tiles = [open(n, "rb").read() for n in names]
+    base = dict(split_min=256, split_ratio=0, split_chunk=1000, split_values=512, split_max_streams=0)
+    fixed = covt.Plan.from_tiles(tiles, options=covt.PlanOptions(split_grow=0, **base))
+    st = fixed.streams
+    cost = int((st["byte_length"].astype(np.int64) + st["out_elems"].astype(np.int64) * st["elem_bytes"] // 4).sum())
+    grow = 4 if cost >= 48 << 20 else 2 if cost >= 4 << 20 else 1
+    assert grow > 1, cost  # (the fixture library is a plan of several MiB of cost)
+    grown = covt.Plan.from_tiles(tiles, options=covt.PlanOptions(split_grow=1, **base))
+    uf, ug = _chunk_units(covt, fixed), _chunk_units(covt, grown)
+    assert uf["varint"] == {1000} and ug["varint"] == {1000 * grow}
+    assert uf["fpf"] == {512} and ug["fpf"] == {512 * grow}
+    assert grown.num_descs < fixed.num_descs
+    # split_max_streams: the bound is inclusive
+    n = fixed.num_streams
+    at = covt.Plan.from_tiles(tiles, options=covt.PlanOptions(**dict(base, split_max_streams=n)))
+    over = covt.Plan.from_tiles(tiles, options=covt.PlanOptions(**dict(base, split_max_streams=n - 1)))
+    assert at.family_counts[covt.FAMILY_SPLIT:].sum() > 0
+    assert over.family_counts[covt.FAMILY_SPLIT:].sum() == 0 and over.num_descs == n

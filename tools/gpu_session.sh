@@ -138,6 +138,14 @@ for s in "$@"; do
             COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/device_plan_prof.py 20 >> gpurun_out/dplan_lib.log 2>&1 || fatal dplan_lib $?
         done ;;
     tests_dplan) step pytest_dplan 600 python -u -m pytest tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    tests_fpf) step pytest_fpf 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_split.py tests/test_gpu_configs.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    deep_shards) rm -f gpurun_out/deep_shards.log; for v in ${AB_VARIANTS:-libcovt_d0.so libcovt.so libcovt_deep6.so}; do
+            echo "== $v" >> gpurun_out/deep_shards.log
+            COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/shard_sizes.py 20 --ns=4,8,16 --opts= --opts= >> gpurun_out/deep_shards.log 2>&1 || fatal deep_shards $?
+            COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/long_poles.py 20 --shard=8/0 >> gpurun_out/deep_shards.log 2>&1 || fatal deep_shards $?
+        done ;;
+    shards_n4r) step shards_n4r 600 python tools/shard_sizes.py 20 --ns=2,4,8 --opts= --opts=split_max_streams=0 --opts=split_max_streams=0,split_ratio=6000 \
+            --opts=split_max_streams=0,split_ratio=12000 --opts=split_ratio=6000 ;;
     shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
     shards_policy) step shards_policy 600 python tools/shard_sizes.py 20 --ns=1,2,4,8,16 --opts= \
             --opts=lane_min_streams=16384,split_max_streams=0 --opts=split_max_streams=16384 --opts=split_max_streams=0 ;;
