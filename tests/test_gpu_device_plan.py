@@ -285,6 +285,20 @@ def test_split_default_options(covt, gpu_available, decodable_tiles, golden_stre
     _assert_same_assembly(covt, hp, dp)  # split descriptors feed the assembly's stream results
 
 
+@pytest.mark.parametrize("grow", [0, 1])
+def test_split_grow_library(covt, gpu_available, decodable_tiles, golden_streams, grow):
+    """The whole fixture library (several MiB of plan cost) split with covt_plan_options.split_grow on and
+    off: the device plan grows its chunks by the same factor of the plan's cost (split_grow_factor) and
+    cuts the same chunks (FastPFOR start states, RLE group boundaries); decoded to the golden digests."""
+    keys, tiles = [k for k, _ in decodable_tiles], [t for _, t in decodable_tiles]
+    hp = _host_plan(covt, tiles, covt.FORMAT_GENC, 0, split=True, split_min=256, split_ratio=0, split_chunk=1000,
+                    split_values=512, split_max_streams=0, split_grow=grow)
+    assert (hp.family_counts[covt.FAMILY_SPLIT:] > 0).all(), hp.family_counts
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
+    _assert_same_plan(hp, dp)
+    _assert_golden(covt, hp, dp, keys, golden_streams)
+
+
 @pytest.mark.parametrize("kw", [dict(split_min=0, split_ratio=0, split_chunk=64, split_values=256),
                                 dict(split_min=512, split_ratio=0, split_chunk=300, split_values=512,
                                      fpf_split_weight=3),
