@@ -594,6 +594,41 @@ __device__ __forceinline__ int fast_name_type(uint32_t n, uint64_t lo, uint64_t 
     return type;
 }
 
+// The same for a uniform name (the walk's scalar path): the candidate picked by length (and by the first
+// byte where two names share one), then one compare.  The ten compare chains above cost the scalar unit
+// ~60 instructions per Id / Geometry record, and the walk is bound by scalar issue.
+__device__ __forceinline__ int fast_name_type_u(uint32_t n, uint64_t lo, uint64_t hi) {
+    const uint32_t c0 = (uint32_t)lo & 0xffu;
+    int t = -1;
+    uint64_t el = 0, eh = 0;
+#define COVT_FNAME_U(str, v)                                                      \
+    {                                                                             \
+        constexpr uint64_t n_ = cstrlen(str), l_ = pk(str, 0, n_), h_ = pk(str, 8, n_); \
+        t = v;                                                                    \
+        el = l_;                                                                  \
+        eh = h_;                                                                  \
+    }
+    switch (n) {
+    case 4: COVT_FNAME_U("data", ST_DATA) break;
+    case 6: COVT_FNAME_U("length", ST_LENGTH) break;
+    case 7: COVT_FNAME_U("present", ST_PRESENT) break;
+    case 10: COVT_FNAME_U("dictionary", ST_DICTIONARY) break;
+    case 12:
+        if (c0 == 'p') COVT_FNAME_U("part_offsets", ST_PART_OFFSETS)
+        else COVT_FNAME_U("ring_offsets", ST_RING_OFFSETS)
+        break;
+    case 13: COVT_FNAME_U("vertex_buffer", ST_VERTEX_BUFFER) break;
+    case 14:
+        if (c0 == 'g') COVT_FNAME_U("geometry_types", ST_GEOMETRY_TYPES)
+        else COVT_FNAME_U("vertex_offsets", ST_VERTEX_OFFSETS)
+        break;
+    case 16: COVT_FNAME_U("geometry_offsets", ST_GEOMETRY_OFFSETS) break;
+    default: return -1;
+    }
+#undef COVT_FNAME_U
+    return lo == el && hi == eh ? t : -1;
+}
+
 struct FastGenc {
     const uint8_t* t;
     int32_t len;
@@ -746,7 +781,7 @@ struct FastGenc {
             hi = upeek8(q + 9);
             if (n < 16) hi &= (1ull << (8 * (n - 8))) - 1;
         }
-        type = fast_name_type(n, lo, hi);
+        type = fast_name_type_u(n, lo, hi);
         const uint64_t w = upeek8(q + 1 + (int32_t)n);
         const uint64_t stop = ~w & 0x8080808080808080ull;  // (the table checked: numValues <= 4 bytes)
         const int e1 = __builtin_ctzll(stop) >> 3;
@@ -820,19 +855,29 @@ __device__ int walk_genc_fast(FastGenc& f, E& emit) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 __builtin_amdgcn_wave_barrier();
+                // stream s in lane s (ns <= kFwGeo <= 64); each type's streams by one ballot, emitted in
+                // lane order (a scan of the table per type cost six dependent LDS reads per stream)
+                const uint32_t ls = threadIdx.x;
+                const uint4 g = ls < ns ? geo[ls] : make_uint4(0xffu, 0u, 0u, 0u);
+                const uint32_t gt = g.x & 0xffu;
                 for (int want = ST_GEOMETRY_TYPES; want <= ST_VERTEX_BUFFER; ++want) {
                     if (!(present >> want & 1)) continue;
-                    for (uint32_t s = 0; s < ns; ++s) {
-                        const uint4 g = geo[s];
-                        if ((int)(g.x & 0xff) != want) continue;
-                        emit(RawStream{(int32_t)L, 1, want, (int)(g.x >> 8), ctype, (int32_t)g.y, (int32_t)g.z, nb, d});
-                        d += (int64_t)g.z;
+                    uint64_t m = __ballot(ls < ns && gt == (uint32_t)want);
+                    while (m) {
+                        const int sl = __builtin_ctzll(m);
+                        m &= m - 1;
+                        const uint32_t gx = (uint32_t)__builtin_amdgcn_readlane((int)g.x, sl);
+                        const int32_t gy = __builtin_amdgcn_readlane((int)g.y, sl);
+                        const int32_t gz = __builtin_amdgcn_readlane((int)g.z, sl);
+                        emit(RawStream{(int32_t)L, 1, want, (int)(gx >> 8), ctype, gy, gz, nb, d});
+                        d += (int64_t)gz;
                     }
                 }
-                for (uint32_t s = 0; s < ns; ++s) {
-                    const uint4 g = geo[s];
-                    const int type = (int)(int8_t)(g.x & 0xff);
-                    if (type < ST_GEOMETRY_TYPES || type > ST_VERTEX_BUFFER) d += (int64_t)g.z;
+                uint64_t mo = __ballot(ls < ns && (gt < (uint32_t)ST_GEOMETRY_TYPES || gt > (uint32_t)ST_VERTEX_BUFFER));
+                while (mo) {  // the rest: only their data bytes
+                    const int sl = __builtin_ctzll(mo);
+                    mo &= mo - 1;
+                    d += (int64_t)__builtin_amdgcn_readlane((int)g.z, sl);
                 }
             }
         }

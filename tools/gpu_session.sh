@@ -146,6 +146,9 @@ for s in "$@"; do
         done ;;
     shards_n4r) step shards_n4r 600 python tools/shard_sizes.py 20 --ns=2,4,8 --opts= --opts=split_max_streams=0 --opts=split_max_streams=0,split_ratio=6000 \
             --opts=split_max_streams=0,split_ratio=12000 --opts=split_ratio=6000 ;;
+    sq_rle_abl) for v in libcovt.so libcovt_abl_ABL_RLE_NOLIT.so libcovt_abl_ABL_RLE_NORUN.so; do
+            OPB_PROPS=1 COVT_LIB_VARIANT=$v step sq_rle_abl_$v 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/sq_rle_abl_$v -o run --output-format csv -- python tools/family_run.py rle 2
+        done ;;
     shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
     shards_policy) step shards_policy 600 python tools/shard_sizes.py 20 --ns=1,2,4,8,16 --opts= \
             --opts=lane_min_streams=16384,split_max_streams=0 --opts=split_max_streams=16384 --opts=split_max_streams=0 ;;
