@@ -1938,16 +1938,46 @@ __device__ int prop_walk_genc(Rd<true>& r, PE& pe, PropTab& tab) {
     return o == len ? COVT_OK : COVT_ERR_BAD_HEADER;
 }
 
-// names_hash over window bytes (the fast walk's copy of the tile; q + n within the look-ahead)
-__device__ __forceinline__ uint32_t names_hash_win(const FastGenc& f, int32_t q, int32_t n) {
+// names_hash of every stream name of a localized column at once, a lane per stream (name bytes read from
+// the tile): on the scalar unit, the walk's bound, two hashes cost ~60 instructions per stream.  h8 (the
+// bytes after "present_") for the present_<lang> streams.
+__device__ __forceinline__ uint64_t tile_bytes8(const uint8_t* t, int32_t len, int32_t off) {
+    const uintptr_t lo = (uintptr_t)t, hi = lo + (uintptr_t)(uint32_t)len, a = lo + (uintptr_t)(uint32_t)off;
+    const uintptr_t a4 = a & ~(uintptr_t)3;
+    auto ld4 = [&](uintptr_t x) -> uint32_t {  // dwords overlapping the tile lie inside its allocation
+        return (x + 4 > lo && x < hi) ? *(const __attribute__((address_space(1))) uint32_t*)x : 0u;
+    };
+    const uint32_t d0 = ld4(a4), d1 = ld4(a4 + 4), d2 = ld4(a4 + 8), sh = (uint32_t)(a & 3u);
+    return ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32) | __builtin_amdgcn_alignbyte(d1, d0, sh);
+}
+__device__ __forceinline__ uint32_t names_hash_lane(const uint8_t* t, int32_t len, int32_t a, int32_t n, int32_t nmax) {
     uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)(uint32_t)n;
-    for (int32_t i = 0; i < n; i += 8) {
+    for (int32_t i = 0; i < nmax; i += 8) {  // (the wave's longest name sets the trip count)
         const int32_t k = n - i < 8 ? n - i : 8;
-        const uint64_t m = k >= 8 ? ~0ull : ((1ull << (8 * k)) - 1);
-        h = (h ^ (f.upeek8(q + i) & m)) * 0xff51afd7ed558ccdull;
-        h ^= h >> 29;
+        const uint64_t m = k >= 8 ? ~0ull : ((1ull << (8 * (k > 0 ? k : 0))) - 1);
+        uint64_t hn = (h ^ (tile_bytes8(t, len, a + i) & m)) * 0xff51afd7ed558ccdull;
+        hn ^= hn >> 29;
+        h = i < n ? hn : h;
     }
     return (uint32_t)(h ^ (h >> 32));
+}
+__device__ __forceinline__ void names_hash_lanes(const uint8_t* t, int32_t len, PropTab& tab, uint32_t ns) {
+    for (uint32_t j = 0; 64 * j < ns; ++j) {
+        const bool v = 64 * j + threadIdx.x < ns;
+        const int32_t noff = PropTab::pick(tab.noff, j), nlen = v ? PropTab::pick(tab.nlen, j) : 0;
+        const bool lang = v && ((PropTab::pick(tab.er, j) >> 16) & PR_PRESENT_LANG);
+        int32_t nmax = nlen;
+#pragma unroll
+        for (int sh = 1; sh < 64; sh <<= 1) nmax = max(nmax, __shfl_xor(nmax, sh));
+        nmax = __builtin_amdgcn_readfirstlane(nmax);
+        const uint32_t h0 = v ? names_hash_lane(t, len, noff, nlen, nmax) : 0u;
+        const uint32_t h8 = lang ? names_hash_lane(t, len, noff + 8, nlen - 8, nmax) : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            tab.h0[k] = k == j ? h0 : tab.h0[k];
+            tab.h8[k] = k == j ? h8 : tab.h8[k];
+        }
+    }
 }
 
 // The localized sub-columns of a Gen C string column from its stream table (prop_walk_genc's rule): one
@@ -2019,7 +2049,7 @@ __device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropTab& ta
             if (kind != 2) {  // Id / Geometry: only their data bytes
                 o += (int32_t)(ce & 0xffu);
                 for (uint32_t s = 0; s < ns; ++s) {
-                    const uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[f.at(o)]);
+                    const uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[f.at_run(o)]);
                     if (!se) return kFastFallback;
                     d += (int32_t)(se >> 8);
                     o += (int32_t)(se & 0xffu);
@@ -2037,8 +2067,13 @@ __device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropTab& ta
             const bool localized = p.type == COVT_PROP_STRING && ctype == 2;
             if (localized && ns > (uint32_t)kPropMaxStreams) return kFastFallback;  // (the table's bound)
             o += (int32_t)(ce & 0xffu);
+            // the column's role streams in lanes 0..3 (lane = StreamType, the last stream of a role wins): a
+            // select per field, where prop_stream on the record in scalar registers cost ~24 scalar
+            // instructions per stream (the walk is bound by scalar issue)
+            int64_t v_off = -1;
+            int32_t v_nv = 0, v_bl = 0, v_enc = 0;
             for (uint32_t s = 0; s < ns; ++s) {
-                const int32_t q = f.at(o);
+                const int32_t q = f.at_run(o);
                 const uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[q]);
                 const uint32_t re = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fr->rtab[q]);
                 const int enc = __builtin_amdgcn_readfirstlane((int)f.fr->etab[q]);
@@ -2047,25 +2082,33 @@ __device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropTab& ta
                 const int32_t nv = (int32_t)(re & 0x0fffffffu);
                 const int32_t bl = (int32_t)(se >> 8);
                 const uint32_t role = type >= ST_PRESENT && type <= ST_DICTIONARY ? 1u << type : 0u;
-                if (localized) {
+                if (localized) {  // (the names' hashes: after the column, a lane per stream)
                     const int32_t sn = (int32_t)(f.upeek8(q) & 0xffu);
                     uint32_t rl = role;
-                    uint32_t h8 = 0;
-                    if (sn > 8 && f.upeek8(q + 1) == pk("present_", 0, 8)) {
-                        rl |= PR_PRESENT_LANG;
-                        h8 = names_hash_win(f, q + 9, sn - 8);
-                    }
-                    const uint32_t h0 = names_hash_win(f, q + 1, sn);
-                    tab.set(s, PropSm{h0, h8, o + 1, sn, nv, bl, (int32_t)d, (uint16_t)enc, (uint16_t)rl});
-                } else {  // the roles applied in metadata order (the last stream of a role wins)
-                    if (role) prop_stream(p, type, d, nv, bl, enc);
+                    if (sn > 8 && f.upeek8(q + 1) == pk("present_", 0, 8)) rl |= PR_PRESENT_LANG;
+                    tab.set(s, PropSm{0u, 0u, o + 1, sn, nv, bl, (int32_t)d, (uint16_t)enc, (uint16_t)rl});
+                } else if (role) {  // the roles applied in metadata order (the last stream of a role wins)
+                    const bool me = threadIdx.x == (uint32_t)type;
+                    v_off = me ? d : v_off;
+                    v_nv = me ? nv : v_nv;
+                    v_bl = me ? bl : v_bl;
+                    v_enc = me ? enc : v_enc;
                 }
                 d += bl;
                 o += (int32_t)(se & 0xffu);
             }
             if (localized) {
+                names_hash_lanes(f.t, f.len, tab, ns);
                 prop_localized(r, pe, tab, ns, p);
             } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    p.s_off[q] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v_off >> 32), q) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readlane((int)v_off, q));
+                    p.s_nv[q] = __builtin_amdgcn_readlane(v_nv, q);
+                    p.s_bl[q] = __builtin_amdgcn_readlane(v_bl, q);
+                    p.s_enc[q] = __builtin_amdgcn_readlane(v_enc, q);
+                }
                 pe(p);
             }
         }

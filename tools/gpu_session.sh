@@ -149,6 +149,12 @@ for s in "$@"; do
     sq_rle_abl) for v in libcovt.so libcovt_abl_ABL_RLE_NOLIT.so libcovt_abl_ABL_RLE_NORUN.so; do
             OPB_PROPS=1 COVT_LIB_VARIANT=$v step sq_rle_abl_$v 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/sq_rle_abl_$v -o run --output-format csv -- python tools/family_run.py rle 2
         done ;;
+    sq_dplan) step sq_dplan 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/sq_dplan -o run --output-format csv -- python tools/device_plan_prof.py 3 ;;
+    sq_dplan_props) step sq_dplan_props 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY SQ_WAVE_CYCLES -d gpurun_out/sq_dplan_props -o run --output-format csv -- python tools/device_plan_prof.py 3 --props ;;
+    dplan_lib_props) rm -f gpurun_out/dplan_lib_props.log; for v in ${AB_VARIANTS:-libcovt_dp0.so libcovt.so libcovt_dp0.so libcovt.so}; do
+            echo "== $v" >> gpurun_out/dplan_lib_props.log
+            COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/device_plan_prof.py 10 --props >> gpurun_out/dplan_lib_props.log 2>&1 || fatal dplan_lib_props $?
+        done ;;
     shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
     shards_policy) step shards_policy 600 python tools/shard_sizes.py 20 --ns=1,2,4,8,16 --opts= \
             --opts=lane_min_streams=16384,split_max_streams=0 --opts=split_max_streams=16384 --opts=split_max_streams=0 ;;
