@@ -811,7 +811,7 @@ __device__ int walk_genc_fast(FastGenc& f, E& emit) {
         int64_t d = 0;
         emit.layer_begin();
         for (uint32_t c = 0; c < ncols; ++c) {
-            const uint32_t ce = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->ctab[f.at(o)]);
+            const uint32_t ce = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->ctab[f.at_run(o)]);
             if (!ce) return kFastFallback;
             const uint32_t ns = (ce >> 8) & 0x1ffu, kind = (ce >> 17) & 3u;
             const int ctype = (int)(ce >> 19) & 0xff;
@@ -2042,7 +2042,7 @@ __device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropTab& ta
         int64_t d = 0;
         pe.layer_begin();
         for (uint32_t c = 0; c < ncols; ++c) {
-            const int32_t qc = f.at(o);
+            const int32_t qc = f.at_run(o);
             const uint32_t ce = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->ctab[qc]);
             if (!ce) return kFastFallback;
             const uint32_t ns = (ce >> 8) & 0x1ffu, kind = (ce >> 17) & 3u;
@@ -2056,7 +2056,8 @@ __device__ int prop_walk_genc_fast(FastGenc& f, Rd<true>& r, PE& pe, PropTab& ta
                 }
                 continue;
             }
-            const int32_t n = (int32_t)(f.upeek8(qc) & 0xffu);  // the name's length (one LEB128 byte)
+            const int32_t n = (int32_t)((__builtin_amdgcn_readfirstlane((int)f.fs->win[qc >> 2]) >> (8 * (qc & 3))) &
+                                        0xff);  // the name's length (one LEB128 byte)
             const int dtype = (int)(ce >> 27);  // (min(dataType, 31): the same property type)
             const int ctype = (int)(ce >> 19) & 0xff;
             PropRaw p = prop_init((int32_t)L, (int32_t)c, (int32_t)nfeat);
