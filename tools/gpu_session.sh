@@ -159,6 +159,9 @@ for s in "$@"; do
             COVT_LIB_VARIANT=$v step sqa_$v 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/sqa_$v -o run --output-format csv -- python tools/asm_run.py 2 && \
             COVT_LIB_VARIANT=$v step mema_$v 300 rocprofv3 --pmc TA_TA_BUSY TA_DATA_STALLED_BY_TC_CYCLES TCP_PENDING_STALL_CYCLES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY -d gpurun_out/mema_$v -o run --output-format csv -- python tools/asm_run.py 2
         done ;;
+    sq_dplan_var) for v in ${AB_VARIANTS:-libcovt.so libcovt_pl2.so}; do
+            COVT_LIB_VARIANT=$v step sqd_$v 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/sqd_$v -o run --output-format csv -- python tools/device_plan_prof.py 2
+        done ;;
     shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
     shards_policy) step shards_policy 600 python tools/shard_sizes.py 20 --ns=1,2,4,8,16 --opts= \
             --opts=lane_min_streams=16384,split_max_streams=0 --opts=split_max_streams=16384 --opts=split_max_streams=0 ;;
