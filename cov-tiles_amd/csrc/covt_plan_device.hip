@@ -821,13 +821,18 @@ __device__ int walk_genc_fast(FastGenc& f, E& emit) {
                 // (no per-record check: a position with no fast record there (entry 0) counts as 2^24 data
                 // bytes and 255 bytes of metadata, so the layer's data overruns the tile and the check after
                 // the layer falls back; the walk emits nothing in between.  32-bit sums: < 2^9 * 2^24 per column)
+                // (the window offset carried instead of the tile offset, a count-down loop: fewer scalar
+                // instructions per record, the walk's bound)
                 uint32_t dd = 0;
-                for (uint32_t s = 0; s < ns; ++s) {
-                    uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[f.at_run(o)]);
+                int32_t q = o - f.wb;
+                for (uint32_t left = ns; left != 0; --left) {
+                    if ((uint32_t)q >= f.lim) q = f.at(q + f.wb);  // (a window reload moves wb)
+                    uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[q]);
                     se = se ? se : 0xffffffffu;
                     dd += se >> 8;
-                    o += (int32_t)(se & 0xffu);
+                    q += (int32_t)(se & 0xffu);
                 }
+                o = q + f.wb;
                 d += dd;
                 continue;
             }
