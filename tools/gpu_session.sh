@@ -162,6 +162,8 @@ for s in "$@"; do
     sq_dplan_var) for v in ${AB_VARIANTS:-libcovt.so libcovt_pl2.so}; do
             COVT_LIB_VARIANT=$v step sqd_$v 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/sqd_$v -o run --output-format csv -- python tools/device_plan_prof.py 2
         done ;;
+    shards_n4b) step shards_n4b 600 python tools/shard_sizes.py 20 --ns=4 --opts= --opts=split_max_streams=0,split_ratio=1600 \
+            --opts=split_max_streams=0,split_ratio=1800 --opts=split_max_streams=0,split_ratio=2000 --opts=split_max_streams=0,split_ratio=2400 ;;
     shards) step shard_sizes 300 python tools/shard_sizes.py 30 ;;
     shards_policy) step shards_policy 600 python tools/shard_sizes.py 20 --ns=1,2,4,8,16 --opts= \
             --opts=lane_min_streams=16384,split_max_streams=0 --opts=split_max_streams=16384 --opts=split_max_streams=0 ;;
