@@ -928,6 +928,9 @@ __global__ void tile_iota(uint32_t* __restrict__ v, int32_t n) {
 // Records a tile's walk leaves for emit_slots: up to kSlots per tile (the fixture library's busiest
 // tile has 67 Id / Geometry streams); a tile with more is walked again by walk_emit
 constexpr int kSlots = 128;
+#ifndef COVT_DEFER_SUMS
+#define COVT_DEFER_SUMS 1
+#endif
 
 struct CountEmit {
     int32_t id_mode;
@@ -935,8 +938,17 @@ struct CountEmit {
     bool writer = true, wave = false;
     int64_t n = 0, out = 0, k0 = 0;
     int64_t fpf_w = 1, cost = 0, cmax = 0;  // the split rule's cost: sum, and the largest split cost
+    // a wave walk with slots: a slotted record is only written here, its op, output bytes and costs are
+    // summed by the whole wave after the walk (slot_sums): 17.0k -> 15.3k scalar instructions per tile of the
+    // bench batch (the walk is bound by scalar issue; plan 0.64 -> 0.63 ms, paired)
+    bool defer = false;
 
     __device__ void operator()(const RawStream& s) {
+        if (defer && n < kSlots) {
+            if (writer) slots[n] = s;
+            ++n;
+            return;
+        }
         int op, elem;
         int64_t nvals, oe;
         choose_op(s, id_mode, op, nvals, elem, oe);
@@ -948,6 +960,37 @@ struct CountEmit {
         cost += c;
         const int64_t sc = split_fpf_op(op) ? c + (fpf_w - 1) * (ob / 4) : c;
         cmax = sc > cmax ? sc : cmax;
+    }
+    // the slotted records' sums (defer), one lane per record: output bytes (each stream's slice aligned, so
+    // the walk's running align_out sum is the sum of the aligned sizes), split cost sum and maximum
+    __device__ void slot_sums() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        const int64_t m = n < kSlots ? n : kSlots;
+        int64_t so = 0, sc = 0, sm = 0;
+        for (int64_t j = threadIdx.x; j < m; j += 64) {
+            int op, elem;
+            int64_t nvals, oe;
+            const RawStream r = slots[j];
+            choose_op(r, id_mode, op, nvals, elem, oe);
+            const int64_t ob = (op == COVT_OP_NONE ? 0 : oe) * elem;
+            so += align_out(ob);
+            const int64_t c = (int64_t)r.bl + ob / 4;
+            sc += c;
+            const int64_t x = split_fpf_op(op) ? c + (fpf_w - 1) * (ob / 4) : c;
+            sm = x > sm ? x : sm;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            so += __shfl_xor(so, d, 64);
+            sc += __shfl_xor(sc, d, 64);
+            const int64_t x = __shfl_xor(sm, d, 64);
+            sm = x > sm ? x : sm;
+        }
+        out += so;
+        cost += sc;
+        cmax = sm > cmax ? sm : cmax;
     }
     __device__ void layer_begin() { k0 = n; }
     __device__ void layer_end(int64_t data_start) {  // rebase the layer's recorded data offsets
@@ -972,6 +1015,9 @@ struct CountEmit {
 // Both take ~0.7 ms for one tile alone and ~3.6 ms per walk kernel for the 10k-tile batch
 // (profiles/r02/device_plan_ab.txt); the walk is a serial chain per tile whose step time neither the
 // scalar nor the lane layout changes.
+#ifdef COVT_PLAN_TIMING  // profiling build (tools/walk_timeline.py): each tile's walk (start, end), 100 MHz ticks
+__device__ uint64_t* covt_walk_clock;
+#endif
 template <bool kWave>
 __global__ void walk_count(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const uint64_t* __restrict__ offs,
                            const uint64_t* __restrict__ sizes, int32_t n_tiles, int32_t format, int32_t id_mode,
@@ -990,7 +1036,19 @@ __global__ void walk_count(const uint8_t* __restrict__ bytes, uint64_t n_bytes, 
     e.writer = !kWave || threadIdx.x == 0;
     e.wave = kWave;
     e.fpf_w = fpf_w;
+    e.defer = kWave && COVT_DEFER_SUMS && e.slots;
+#ifdef COVT_PLAN_TIMING
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const int st = walk_tile<kWave>(bytes, n_bytes, offs[t], sizes[t], format, e);
+    if (kWave && e.defer && st == COVT_OK) e.slot_sums();
+#ifdef COVT_PLAN_TIMING
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    if (kWave && threadIdx.x == 0 && covt_walk_clock) {
+        covt_walk_clock[2 * (size_t)t] = t_start;
+        covt_walk_clock[2 * (size_t)t + 1] = t_end;
+    }
+#endif
     if (!kWave || threadIdx.x == 0) {
         status[t] = st;
         cnt[t] = st ? 0 : e.n;  // a failed tile contributes nothing
@@ -2652,6 +2710,11 @@ size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
+#ifdef COVT_PLAN_TIMING
+extern "C" int covt_debug_walk_clock(void* p) {  // 2 x n_tiles uint64 on the device (null: off)
+    return hipMemcpyToSymbol(HIP_SYMBOL(covt_walk_clock), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
 extern "C" {
 
 int covt_device_plan_create(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_tile_offsets,

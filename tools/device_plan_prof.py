@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Profiling target: covt_device_plan_create on the bench batch (BASELINE config 5) N times, wall-clock per
 creation printed (run under rocprofv3 --kernel-trace --stats [--hip-trace] for the per-kernel / per-call
-breakdown).  usage: device_plan_prof.py [reps] [--sweep | --small | --n256] [--nosplit] [--sorted] [--geometry]
+breakdown).  usage: device_plan_prof.py [reps] [--sweep | --small | --n256] [--nosplit] [--sorted] [--geometry] [--drop=K,...]
 --sweep: also batches of 1 tile (the library's largest), 256, 2048 and 4096 tiles (latency vs. occupancy).
 --geometry: also time covt_device_plan_geometry (the geometry-column planning) after each creation.
---props: plans with COVT_PLAN_PROPERTIES (property columns planned on the device too)."""
+--props: plans with COVT_PLAN_PROPERTIES (property columns planned on the device too).
+--drop=K,...: also the batch without its K largest tiles (is the walk bound by its longest tiles?)."""
 import os
 import sys
 import time
@@ -35,6 +36,15 @@ def main():
         return
     picks = bench.sample_batch(lib, 10000, bench.SEED)
     run(covt, [t for _, t in picks], reps, "10000 tiles")
+    for a in sys.argv[1:]:
+        if a.startswith("--drop="):
+            tl = [t for _, t in picks]
+            by = np.argsort([-len(t) for t in tl], kind="stable")
+            for k in (int(x) for x in a[7:].split(",")):
+                keep = sorted(by[k:])
+                sub = [tl[i] for i in keep]
+                run(covt, sub, reps, "%5d tiles (%d largest dropped, %.1f %% of the bytes)"
+                    % (len(sub), k, 100.0 * sum(len(t) for t in sub) / sum(len(t) for t in tl)))
     if "--sorted" in sys.argv:  # the same batch, largest tiles first (walk launch order experiment)
         run(covt, sorted((t for _, t in picks), key=len, reverse=True), reps, "10000 tiles, largest first")
 

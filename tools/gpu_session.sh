@@ -76,6 +76,9 @@ for s in "$@"; do
     tests_r05) step pytest_r05 600 python -u -m pytest tests/test_gpu_assembly.py tests/test_gpu_props.py tests/test_jni_shim.py tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -s ;;
     tests_dplan) step pytest_dplan 300 python -u -m pytest tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     dplan_geo) step dplan_geo 200 python tools/device_plan_prof.py 20 --sweep --geometry ;;
+    dplan_drop) step dplan_drop 300 python tools/device_plan_prof.py 20 --drop=16,64,256,1024,4096 ;;
+    walk_timeline) step walk_timeline 300 python tools/walk_timeline.py 5 ;;
+    dplan_prof_props) step dplan_prof_props 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_prof_props -o run --output-format csv -- python tools/device_plan_prof.py 5 --props ;;
     dplan_sweep) step dplan_sweep 300 python tools/device_plan_prof.py 10 --sweep ;;
     dplan_props_sweep) step dplan_props_sweep 300 python tools/device_plan_prof.py 10 --sweep --props ;;
     dplan_ab) step dplan_ab 300 python tools/device_plan_ab.py 0 1 ;;
