@@ -87,10 +87,43 @@ def main():
         print("family %-8s alone: %.3f ms (%d streams)" % (name, e0.elapsed_time(e1) / 5, n))
     if quick:
         return
+    # each descriptor's family (launch order groups the plan's descriptors by family, so an op's subset is
+    # contiguous per family too)
+    fl = descs[:, 26:28].copy().view(np.uint16).ravel()
+    fam_of = np.zeros(len(descs), dtype=np.int64)
+    for f in range(covt.NUM_FAMILIES):
+        n = int(plan.family_counts[f])
+        lo = int(plan.family_counts[:f].sum())
+        fam_of[lo:lo + n] = f
+    res_g = torch.zeros(2 * plan.num_streams, dtype=torch.int32, device="cuda")
+
+    def run_grouped(sub, cnt, reps=5):
+        def go():
+            L.covt_decode_streams_device_grouped(batch.d_in.data_ptr(), sub.data_ptr(),
+                                                 cnt.ctypes.data_as(C.POINTER(C.c_int64)), batch.d_out.data_ptr(),
+                                                 res_g.data_ptr(), stream.cuda_stream)
+        go(); go()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            go()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    print("per op: t = every family kernel over the op's descriptors back to back (covt_decode_streams_device: "
+          "each kernel skips the other families' descriptors, so empty waves are dispatched); tg = the grouped "
+          "launch the decode uses (covt_decode_streams_device_grouped: the op's own families, concurrent)")
     for op in sorted(set(ops.tolist())):
         m = ops == op
         sub = torch.from_numpy(np.ascontiguousarray(descs[m]).reshape(-1)).cuda()
         t = run(sub, int(m.sum()))
+        cnt_op = np.bincount(fam_of[m], minlength=covt.NUM_FAMILIES).astype(np.int64)
+        if (fl[m] & 0x1e).any():  # split chunks: their pads are descriptors of other ops
+            tg = float("nan")
+        else:
+            tg = run_grouped(sub, cnt_op)
         ib = int(s_launch["byte_length"][m].sum())
         ob = int((s_launch["out_elems"][m] * s_launch["elem_bytes"][m]).sum())
         nv = int(s_launch["num_values"][m].sum())
@@ -100,9 +133,10 @@ def main():
         rest = torch.from_numpy(np.ascontiguousarray(descs[idx[64:]]).reshape(-1)).cuda()
         tr = run(rest, max(len(idx) - 64, 0)) if len(idx) > 64 else 0.0
         print("%-12s streams=%7d values=%11d in=%6.1fMB out=%7.1fMB  t=%7.3f ms  alg=%7.1f GB/s  %.2f Gval/s"
-              "  | largest stream (%d B, %d vals) %.3f ms | all but top-64 %.3f ms"
+              "  | largest stream (%d B, %d vals) %.3f ms | all but top-64 %.3f ms | tg=%7.3f ms  alg=%7.1f GB/s"
               % (NAMES.get(op, op), int(m.sum()), nv, ib / 1e6, ob / 1e6, t, (ib + ob) / t / 1e6, nv / t / 1e6,
-                 int(s_launch["byte_length"][idx[0]]), int(s_launch["num_values"][idx[0]]), t1, tr))
+                 int(s_launch["byte_length"][idx[0]]), int(s_launch["num_values"][idx[0]]), t1, tr, tg,
+                 (ib + ob) / tg / 1e6))
 
 
 if __name__ == "__main__":
