@@ -37,6 +37,7 @@ struct covt_device_plan {
     int dev = 0;
     int32_t n_tiles = 0, format = 0, id_mode = 0;
     int64_t n_streams = 0, n_descs = 0, out_bytes = 0, in_bytes = 0, out_payload = 0, vertices = 0;
+    int32_t spec_redo = 0;  // the stream part ran again with counted sizes (a bound-sized plan that missed)
     int64_t fam_counts[COVT_NUM_FAMILIES] = {};
     void* tile_arena = nullptr;    // status, per-tile counts and prefix sums, totals, scan scratch
     void* stream_arena = nullptr;  // infos, values, keys, launch order, descriptors, sort scratch
@@ -931,6 +932,12 @@ constexpr int kSlots = 128;
 #ifndef COVT_DEFER_SUMS
 #define COVT_DEFER_SUMS 1
 #endif
+#ifndef COVT_PLAN_SPEC
+#define COVT_PLAN_SPEC 1
+#endif
+// a plan is built without the mid-plan synchronisation when its tiles at this many streams each would exceed
+// the split bound (split_max_streams): such a plan splits nothing, so the guess is rarely wrong
+constexpr int64_t kSpecStreamsPerTile = 32;
 
 struct CountEmit {
     int32_t id_mode;
@@ -1100,16 +1107,17 @@ struct InfoEmit {
     int64_t k, out, in_bytes = 0, payload = 0, verts = 0, lane = 0, k0 = 0;
     int32_t lane_max, lm = -1;
     uint32_t* keys = nullptr;
+    int64_t cap = INT64_MAX;  // entries the arena holds (a plan sized to a bound)
     bool writer, wave;
     __device__ void layer_begin() { k0 = k; }
     __device__ void layer_end(int64_t data_start) {  // rebase the layer's data offsets (this lane's own stores)
         if (!data_start) return;
         if (wave) {  // the layer's records, one lane each (lane 0 wrote them: a barrier-free wave is in order)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            for (int64_t j = k0 + threadIdx.x; j < k; j += 64) info[j].in_off += data_start;
+            for (int64_t j = k0 + threadIdx.x; j < k && j < cap; j += 64) info[j].in_off += data_start;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         } else {
-            for (int64_t j = k0; j < k; ++j) info[j].in_off += data_start;
+            for (int64_t j = k0; j < k && j < cap; ++j) info[j].in_off += data_start;
         }
     }
     __device__ void operator()(const RawStream& s) {
@@ -1137,7 +1145,7 @@ struct InfoEmit {
         payload += si.out_elems * elem;
         if (s.kind == 1 && s.type == ST_VERTEX_BUFFER) verts += (s.ctype == CT_ICE || s.ctype == CT_ICE_MORTON) ? s.nv : s.nv / 2;
         lane += lane_stream(op, (int32_t)nv, s.bl, lane_max);
-        if (writer) {
+        if (writer && k < cap) {
             info[k] = si;
             nvals[k] = (int32_t)nv;
             if (keys) keys[k] = entry_key(op, (int32_t)nv, s.bl, si.out_elems, elem, lm);
@@ -1152,7 +1160,7 @@ __global__ void walk_emit(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
                           const int32_t* __restrict__ status, const int64_t* __restrict__ cnt_base,
                           const int64_t* __restrict__ ob_base, int32_t lane_max, covt_stream_info* __restrict__ info,
                           int32_t* __restrict__ nvals, long long* __restrict__ tsum,
-                          const int64_t* __restrict__ cnt, uint32_t* __restrict__ keys, int32_t lm) {
+                          const int64_t* __restrict__ cnt, uint32_t* __restrict__ keys, int32_t lm, int64_t cap) {
     const int32_t t = kWave ? (int32_t)blockIdx.x : (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t >= n_tiles || status[t]) return;
     if (cnt && cnt[t] <= kSlots) return;  // emit_slots has this tile's records
@@ -1160,6 +1168,7 @@ __global__ void walk_emit(const uint8_t* __restrict__ bytes, uint64_t n_bytes, c
     e.lane_max = lane_max;
     e.lm = lm;
     e.keys = keys;
+    e.cap = cap;
     e.writer = !kWave || threadIdx.x == 0;
     e.wave = kWave;
     walk_tile<kWave>(bytes, n_bytes, offs[t], sizes[t], format, e);
@@ -1174,7 +1183,7 @@ __global__ void emit_slots(const uint64_t* __restrict__ offs, int32_t n_tiles, i
                            const int64_t* __restrict__ cnt_base, const int64_t* __restrict__ ob_base,
                            const RawStream* __restrict__ slots, int32_t lane_max, covt_stream_info* __restrict__ info,
                            int32_t* __restrict__ nvals, long long* __restrict__ tsum, uint32_t* __restrict__ keys,
-                           int32_t lm) {
+                           int32_t lm, int64_t cap) {
     const int32_t t = blockIdx.x;
     if (t >= n_tiles || status[t]) return;
     const int64_t n = cnt[t];
@@ -1201,7 +1210,7 @@ __global__ void emit_slots(const uint64_t* __restrict__ offs, int32_t n_tiles, i
             const long long u = __shfl_up(incl, d, 64);
             if (lane >= d) incl += u;
         }
-        if (valid) {
+        if (valid && base + j < cap) {  // (cap: a plan sized to a bound; the overflow is caught on the host)
             covt_stream_info si;
             si.tile = t;
             si.layer = s.layer;
@@ -1313,7 +1322,10 @@ constexpr int kSortChunk = 4096;  // keys per workgroup (4 rounds of 1024)
 __global__ void __launch_bounds__(256) order_hist(uint32_t* __restrict__ keys, int64_t n, int32_t nb, int shift,
                                                   uint32_t* __restrict__ ghist, const covt_stream_info* __restrict__ info,
                                                   const int32_t* __restrict__ nvals, int64_t lane_min,
-                                                  const unsigned long long* __restrict__ totals) {
+                                                  const unsigned long long* __restrict__ totals,
+                                                  const int64_t* __restrict__ dn) {
+    if (dn) n = min(n, *dn);  // (a plan sized to a bound: the counted streams, from the device)
+    if (dn && (int64_t)blockIdx.x * kSortChunk >= n && blockIdx.x > 0) return;  // (chunks past them: never read)
     __shared__ uint32_t h[kSortBuckets];
     h[threadIdx.x] = 0;
     __syncthreads();
@@ -1340,7 +1352,13 @@ constexpr int kSortFuseChunks = 512;
 __global__ void __launch_bounds__(1024) order_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                       int64_t n, int32_t nb, int shift, const uint32_t* __restrict__ gpos,
                                                       int scanned, uint32_t* __restrict__ okeys, uint32_t* __restrict__ ovals,
-                                                      unsigned long long* __restrict__ ftot) {
+                                                      unsigned long long* __restrict__ ftot, const int64_t* __restrict__ dn) {
+    const int32_t stride = nb;  // (ghist rows: one count per launched chunk)
+    if (dn) {  // a plan sized to a bound: the counted streams and their chunks only
+        n = min(n, *dn);
+        nb = max(1, (int32_t)((n + kSortChunk - 1) / kSortChunk));
+        if ((int32_t)blockIdx.x >= nb) return;
+    }
     __shared__ uint32_t run[kSortBuckets];
     __shared__ uint32_t wc[16][kSortBuckets];
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -1348,16 +1366,16 @@ __global__ void __launch_bounds__(1024) order_scatter(const uint32_t* __restrict
     // 2^(kLaunchFamShift - 8) consecutive digits)
     constexpr int kFamDigits = 1 << (kLaunchFamShift - 8);
     if (scanned) {
-        if (threadIdx.x < kSortBuckets) run[threadIdx.x] = gpos[(size_t)threadIdx.x * nb + blockIdx.x];
+        if (threadIdx.x < kSortBuckets) run[threadIdx.x] = gpos[(size_t)threadIdx.x * stride + blockIdx.x];
         if (ftot && blockIdx.x == 0 && threadIdx.x < COVT_NUM_FAMILIES) {
             const int d0 = threadIdx.x * kFamDigits, d1 = d0 + kFamDigits;
-            const uint32_t end = d1 < kSortBuckets ? gpos[(size_t)d1 * nb] : (uint32_t)n;
-            ftot[threadIdx.x] = end - gpos[(size_t)d0 * nb];
+            const uint32_t end = d1 < kSortBuckets ? gpos[(size_t)d1 * stride] : (uint32_t)n;
+            ftot[threadIdx.x] = end - gpos[(size_t)d0 * stride];
         }
     } else {
         // digit totals and the counts of the chunks before this one (4 threads per digit)
         const int dg = threadIdx.x >> 2, part = threadIdx.x & 3;
-        const uint32_t* row = gpos + (size_t)dg * nb;
+        const uint32_t* row = gpos + (size_t)dg * stride;
         uint32_t tot = 0, pre = 0;
 #pragma unroll 8
         for (int c = part; c < nb; c += 4) {
@@ -1433,10 +1451,8 @@ __global__ void __launch_bounds__(1024) order_scatter(const uint32_t* __restrict
     }
 }
 
-__global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const uint32_t* keys, const uint32_t* order,
-                           int64_t n, covt_stream_desc* desc) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
+__device__ __forceinline__ void fill_desc(covt_stream_info* info, const int32_t* nvals, const uint32_t* keys,
+                                          const uint32_t* order, int64_t k, covt_stream_desc* desc) {
     const uint32_t i = order[k];
     covt_stream_info& si = info[i];
     covt_stream_desc d;
@@ -1450,6 +1466,13 @@ __global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const u
     d.byte_length = si.byte_length;
     desc[k] = d;
     si.desc_index = (int32_t)k;
+}
+// dn: a plan sized to a bound (the counted streams from the device, a grid-stride loop over them)
+__global__ void fill_descs(covt_stream_info* info, const int32_t* nvals, const uint32_t* keys, const uint32_t* order,
+                           int64_t n, covt_stream_desc* desc, const int64_t* __restrict__ dn) {
+    if (dn) n = min(n, *dn);
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        fill_desc(info, nvals, keys, order, k, desc);
 }
 
 // ---- Split plans (covt_plan_create_ex step 3 on the device; only when some stream's split cost passes
@@ -2917,18 +2940,38 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     DCHK(hipcub::DeviceScan::ExclusiveSum(ta + o_tmp, scan_tmp, scan_ob, obb, (int)nt1, s));
     plan_head<<<1, 1024, 0, s>>>(cb, obb, tcost, n_tiles, head, pacc);
     DCHK(hipGetLastError());
-    int64_t hd[4];
-    DCHK(hipMemcpyAsync(hd, head, sizeof(hd), hipMemcpyDeviceToHost, s));
-    DCHK(hipStreamSynchronize(s));
-    const int64_t ns = hd[0];
-    p->n_streams = ns;
-    p->n_descs = ns;
-    p->out_bytes = hd[1];
+    // Id / Geometry plans of many tiles skip the host synchronisation between the walk and the stream entries
+    // (~57 us of the 10k-tile plan's 0.62 ms, profiles/r05): the stream arena is sized to a bound, the kernels
+    // take the stream count from the device (head[0]), and the count and the split decision are checked at the
+    // plan's final synchronisation -- a plan past the bound, or one that splits, runs this part again with the
+    // counted sizes.  (Property plans synchronise for their record count anyway.)
+    int64_t hd[4] = {0, 0, 0, 0};
+    const int64_t spec_cap = std::min<int64_t>((int64_t)kSortFuseChunks * kSortChunk, (int64_t)n_tiles * kSlots);
+    const bool spec = COVT_PLAN_SPEC && !props && wl == 0 && slots && o.split_max_streams > 0 &&
+                      (int64_t)n_tiles * kSpecStreamsPerTile > o.split_max_streams;
+    if (!spec) {
+        DCHK(hipMemcpyAsync(hd, head, sizeof(hd), hipMemcpyDeviceToHost, s));
+        DCHK(hipStreamSynchronize(s));
+    }
+    auto splits = [&](int64_t ns, int64_t& smin) {  // the split threshold (covt_plan_create_ex step 3)
+        smin = o.split_min;
+        if (smin >= 0 && o.split_ratio > 0) smin = std::max<int64_t>(smin, hd[2] / o.split_ratio);
+        return smin >= 0 && ns > 0 && hd[3] > smin && (o.split_max_streams <= 0 || ns <= o.split_max_streams);
+    };
+    // the stream entries, their launch order and descriptors; sp: sized to spec_cap, nothing split
+    auto stream_part = [&](bool sp) -> int {
+    const int64_t ns = sp ? spec_cap : hd[0];
+    const int64_t* dns = sp ? head : nullptr;
+    const int64_t ecap = sp ? spec_cap : INT64_MAX;
+    if (!sp) {
+        p->n_streams = ns;
+        p->n_descs = ns;
+        p->out_bytes = hd[1];
+    }
     if (ns > 0x7fffffff) return fail(COVT_ERR_INVALID_ARG);
-    // the split threshold (covt_plan_create_ex step 3): nothing splits unless the largest cost passes it
-    int64_t smin = o.split_min;
-    if (smin >= 0 && o.split_ratio > 0) smin = std::max<int64_t>(smin, hd[2] / o.split_ratio);
-    const bool splitting = smin >= 0 && ns > 0 && hd[3] > smin && (o.split_max_streams <= 0 || ns <= o.split_max_streams);
+    // nothing splits unless the largest cost passes the threshold
+    int64_t smin = 0;
+    const bool splitting = !sp && splits(ns, smin);
     const int64_t grow = split_grow_factor(hd[2], o.split_grow);
     const int64_t schunk = o.split_chunk * grow, svalues = o.split_values * grow;
     // stream arena: info | nvals | launch buckets | sorted buckets | launch order | bucket counts | descs [|
@@ -2970,13 +3013,13 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     auto launch_order = [&]() {
         for (int pass = 0; pass < 2; ++pass) {
             order_hist<<<nb, 256, 0, s>>>(pass ? q1 : q0, ns, nb, 8 * pass, bhist,
-                                          pass == 0 && !splitting ? p->d_info : nullptr, nvals, lane_min, totals);
+                                          pass == 0 && !splitting ? p->d_info : nullptr, nvals, lane_min, totals, dns);
             if (scanned) {
                 const hipError_t e = hipcub::DeviceScan::ExclusiveSum(sa + o_ht, hscan_tmp, bhist, bscan, (int)mh, s);
                 if (e != hipSuccess) return e;
             }
-            if (pass == 0) order_scatter<<<nb, 1024, 0, s>>>(q0, nullptr, ns, nb, 0, bscan, scanned, q1, v0, nullptr);
-            else order_scatter<<<nb, 1024, 0, s>>>(q1, v0, ns, nb, 8, bscan, scanned, q0, v1, fam_tot);
+            if (pass == 0) order_scatter<<<nb, 1024, 0, s>>>(q0, nullptr, ns, nb, 0, bscan, scanned, q1, v0, nullptr, dns);
+            else order_scatter<<<nb, 1024, 0, s>>>(q1, v0, ns, nb, 8, bscan, scanned, q0, v1, fam_tot, dns);
         }
         return hipGetLastError();
     };
@@ -2988,17 +3031,17 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     if (n_tiles) {
         if (slots) {
             emit_slots<<<n_tiles, 64, 0, s>>>(d_tile_offsets, n_tiles, id_mode, p->d_status, cnt, cb, obb, slots,
-                                              lane_max, p->d_info, nvals, tsum, ekeys, lm);
+                                              lane_max, p->d_info, nvals, tsum, ekeys, lm, ecap);
             DCHK(hipGetLastError());
         }
         if (wl == 0)  // (with slots: only tiles with more than kSlots streams walk again)
             walk_emit<true><<<n_tiles, 64, kWalkLds, s>>>(d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format,
                                                           id_mode, p->d_status, cb, obb, lane_max, p->d_info, nvals, tsum,
-                                                          slots ? cnt : nullptr, ekeys, lm);
+                                                          slots ? cnt : nullptr, ekeys, lm, ecap);
         else
             walk_emit<false><<<(n_tiles + wl - 1) / wl, wl, (size_t)wl * 64 + 16, s>>>(
                 d_bytes, n_bytes, d_tile_offsets, d_tile_sizes, n_tiles, format, id_mode, p->d_status, cb, obb,
-                lane_max, p->d_info, nvals, tsum, nullptr, ekeys, lm);
+                lane_max, p->d_info, nvals, tsum, nullptr, ekeys, lm, ecap);
         DCHK(hipGetLastError());
         reduce_tiles<<<1, 1024, 0, s>>>(tsum, n_tiles, totals, pacc);
         DCHK(hipGetLastError());
@@ -3014,7 +3057,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     const int blocks_s = (int)((ns + 255) / 256);
     if (ns > 0 && !splitting) {
         DCHK(launch_order());
-        fill_descs<<<blocks_s, 256, 0, s>>>(p->d_info, nvals, q0, v1, ns, p->d_desc);
+        fill_descs<<<sp ? std::min(blocks_s, 2048) : blocks_s, 256, 0, s>>>(p->d_info, nvals, q0, v1, ns, p->d_desc, dns);
         DCHK(hipGetLastError());
     } else if (splitting) {
         auto* sfam = (uint8_t*)(sa + o_sf);
@@ -3051,6 +3094,13 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
         fpf_states_walk<<<walkers, 64, kStreamRdLds, s>>>(d_bytes, p->d_info, nvals, totals, fpf_list, svalues, p->d_desc);
         DCHK(hipGetLastError());
     }
+    return COVT_OK;
+    };
+    {
+        const int st = stream_part(spec);
+        if (st) return st;  // (fail() has destroyed the plan)
+    }
+
     if (props) {  // property output layout and the largest-first descriptor order (after the stream descriptors)
         uint8_t* pa = (uint8_t*)p->prop_arena;
         auto* pflags = (uint16_t*)(pa + po_pf);
@@ -3075,7 +3125,25 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     }
     unsigned long long tot[T_N];
     DCHK(hipMemcpyAsync(tot, totals, sizeof(tot), hipMemcpyDeviceToHost, s));
+    if (spec) DCHK(hipMemcpyAsync(hd, head, sizeof(hd), hipMemcpyDeviceToHost, s));
     DCHK(hipStreamSynchronize(s));
+    if (spec) {
+        int64_t smin = 0;
+        if (hd[0] > spec_cap || splits(hd[0], smin)) {  // past the bound, or a split plan: with the counted sizes
+            ++p->spec_redo;
+            DCHK(hipFreeAsync(p->stream_arena, s));
+            p->stream_arena = nullptr;
+            DCHK(hipMemsetAsync(totals + T_FAM, 0, COVT_NUM_FAMILIES * 8, s));
+            const int st = stream_part(false);
+            if (st) return st;
+            DCHK(hipMemcpyAsync(tot, totals, sizeof(tot), hipMemcpyDeviceToHost, s));
+            DCHK(hipStreamSynchronize(s));
+        } else {
+            p->n_streams = hd[0];
+            p->n_descs = hd[0];
+            p->out_bytes = hd[1];
+        }
+    }
 #undef DCHK
     p->in_bytes = (int64_t)tot[T_IN];
     p->out_payload = (int64_t)tot[T_PAYLOAD];

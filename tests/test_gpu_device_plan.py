@@ -242,6 +242,40 @@ def test_tiles_past_slot_capacity(covt, gpu_available, decodable_tiles, walk, fm
     _assert_same_geometry(hp, dp)
 
 
+def test_bound_sized_plan_past_its_bound(covt, gpu_available, decodable_tiles):
+    """A plan of more than 2,048 tiles is built without the mid-plan synchronisation, its stream arena sized
+    to 128 streams per tile (covt_plan_device.hip, stream_part).  Tiles of merged small fixtures hold more than
+    that each, so the bound-sized pass overflows (its writes are clipped) and the plan is redone with the
+    counted sizes: it must still equal the host plan and decode to the same outputs."""
+    omt = sorted((t for k, t in decodable_tiles if k.startswith("omt/")), key=len)
+    merged, i = [], 0
+    while True:  # the smallest fixtures merged until the tile holds more than 128 Id / Geometry streams
+        merged.append(omt[i])
+        i += 1
+        hp1 = _host_plan(covt, [_merge_genc(merged)], covt.FORMAT_GENC, 0)
+        if hp1.num_streams > 160:
+            break
+    big = _merge_genc(merged)
+    tiles = [big] * 2100
+    hp = _host_plan(covt, tiles, covt.FORMAT_GENC, 0, split=True)
+    assert hp.num_streams > 128 * len(tiles) and hp.num_descs == hp.num_streams
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
+    _assert_same_plan(hp, dp)  # (descriptors byte-equal: the decode through them is the host plan's)
+
+
+def test_bound_sized_plan_that_splits(covt, gpu_available, decodable_tiles):
+    """A bound-sized plan (more than 2,048 tiles) whose streams stay under split_max_streams and whose largest
+    stream passes the split threshold: the split decision, known only at the final synchronisation, redoes the
+    stream part as a split plan; it must equal the host plan's (chunks and all) and decode to its outputs."""
+    lib = dict(decodable_tiles)
+    tiles = [lib["bing/5-8-12"]] * 2100 + [lib["omt/14_8298_10748"]]  # 31 streams each, then the largest tile
+    hp = _host_plan(covt, tiles, covt.FORMAT_GENC, 0, split=True)
+    assert hp.num_streams <= 65536 and hp.num_descs > hp.num_streams
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
+    _assert_same_plan(hp, dp)
+    _assert_same_decode(covt, hp, dp)
+
+
 def _assert_golden(covt, hp, dp, keys, golden_streams):
     """Decode through the device plan; every stream's status, consumed bytes and output SHA-256 equal
     the oracle's digests of its tile (tests/golden/oracle_streams.json)."""
