@@ -733,8 +733,8 @@ struct FastGenc {
             }
         }
         segs |= 1u << sg;
-        lim = (segs & 1u) ? ((segs & 2u) ? 512u : 256u) : 0u;
-        static_assert(kFwSpan == 512, "lim: two table segments");
+        lim = (segs & 1u) ? ((kFwSpan > 256 && (segs & 2u)) ? 512u : 256u) : 0u;
+        static_assert(kFwSpan == 512 || kFwSpan == 256, "lim: one or two table segments");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         __builtin_amdgcn_wave_barrier();
