@@ -81,6 +81,9 @@ struct __attribute__((aligned(16))) AsmSmemT {
 #ifndef COVT_ASM_WIN
 #define COVT_ASM_WIN 1
 #endif
+#ifndef COVT_ASM_NT  // pass 4: single-use loads (vertexOffsets, a plain column's vertices) nontemporal
+#define COVT_ASM_NT 1
+#endif
 constexpr int kAsmIpl = COVT_ASM_IPL;
 typedef AsmSmemT<1, kAsmIpl> AsmSmem;
 
@@ -659,7 +662,8 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
 #pragma unroll
                 for (int k = 0; k < 2 * IPL; ++k) {
                     const int32_t i = v0 + 64 * k + l;
-                    ia[k] = i < (int32_t)V ? (ice ? ((const g_i32*)vo)[i] : i) : 0;
+                    // (vertexOffsets are read once: streamed past L2, which keeps the dictionary the gathers reuse)
+                    ia[k] = i < (int32_t)V ? (ice ? (COVT_ASM_NT ? __builtin_nontemporal_load(vo + i) : ((const g_i32*)vo)[i]) : i) : 0;
                 }
                 uint64_t xa[2 * IPL];
 #pragma unroll
@@ -667,7 +671,9 @@ __device__ void assemble_column(const uint8_t* __restrict__ dec, const covt_stre
                     const bool valid = v0 + 64 * k + l < (int32_t)V;
                     const bool inr = (uint32_t)ia[k] < (uint32_t)n_vb;
                     bad_idx |= valid && !inr;
-                    xa[k] = (valid && inr) ? ((const g_u64*)vb)[ia[k]] : 0ull;
+                    // (a plain column's vertices are copied once: streamed too; an ICE dictionary is gathered ~2.7
+                    // times per vertex and stays cached)
+                    xa[k] = (valid && inr) ? ((COVT_ASM_NT && !ice) ? __builtin_nontemporal_load(vb + ia[k]) : ((const g_u64*)vb)[ia[k]]) : 0ull;
                 }
 #pragma unroll
                 for (int k = 0; k < 2 * IPL; ++k)
