@@ -41,7 +41,7 @@
 namespace covt {
 
 #ifndef COVT_ASM_WAVES
-#define COVT_ASM_WAVES 4
+#define COVT_ASM_WAVES 1
 #endif
 constexpr int kAsmWaves = COVT_ASM_WAVES;  // independent waves (columns) per workgroup
 // Small batches (at most kCoopMaxColumns columns: one tile's latency, BASELINE config 1): a column's
