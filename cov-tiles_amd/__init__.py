@@ -51,6 +51,7 @@ LAUNCH_AUTO, LAUNCH_FUSED, LAUNCH_FORKED = 0, 1, 2
 
 # property columns (include/covt.h "Property columns")
 PLAN_PROPERTIES = 0x1
+RELEASE_PINNED = 0x2  # covt_release_scratch flag: also free blocks pinned by a graph capture
 PROP_BOOLEAN, PROP_INT64, PROP_FLOAT, PROP_STRING = 0, 1, 2, 3
 PROP_DICT_OWNER, PROP_DENSE_BOOL, PROP_UNSUPPORTED, PROP_DATA_SHORT, PROP_UNSUPPORTED_LATE = 0x1, 0x2, 0x4, 0x8, 0x10
 
@@ -197,13 +198,15 @@ EXPORTED_SYMBOLS = (
 )
 
 
-def release_scratch(stream=None, all: bool = False) -> int:
+def release_scratch(stream=None, all: bool = False, pinned: bool = False) -> int:
     """covt_release_scratch: free the small-batch assembly / property scratch of (current device, `stream`),
-    or every block with all=True; returns the number of blocks freed."""
+    or every block with all=True; blocks pinned by a graph capture only with pinned=True (no graph captured
+    on them may replay afterwards); returns the number of blocks freed."""
     import torch
 
     s = stream if stream is not None else (torch.cuda.current_stream() if not all else None)
-    return lib().covt_release_scratch(C.c_void_p(s.cuda_stream if s is not None else 0), 1 if all else 0)
+    flags = (1 if all else 0) | (RELEASE_PINNED if pinned else 0)
+    return lib().covt_release_scratch(C.c_void_p(s.cuda_stream if s is not None else 0), flags)
 
 
 def scratch_blocks() -> int:

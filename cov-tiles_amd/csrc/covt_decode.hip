@@ -2157,6 +2157,13 @@ __device__ __forceinline__ void run_fastpfor_chunk(Ctx& c, int32_t v0, int32_t v
     // 8 KiB read-modify-write for a 2048-value chunk instead of a second decode).  Morton decodes twice:
     // a pass of sums only, then the decode with the carry.
     constexpr bool kOnce = OP != COVT_OP_FPF_DELTA_MORTON;
+    // fpf_add_carry adds the carry in place: right only for int32 outputs indexed by value whose values are
+    // linear in the running sum (x / y by value parity for XY, whose chunks start at even values -- v0 is a
+    // multiple of 256).  Any other op listed in split_fpf_op (covt_internal.h) must decode twice.
+    static_assert(OP == COVT_OP_FPF_ZZ_DELTA_I32 || OP == COVT_OP_FPF_ZZ_DELTA_XY || OP == COVT_OP_FPF_DELTA_MORTON,
+                  "split FastPFOR op without a carry rule");
+    static_assert(!kOnce || OP == COVT_OP_FPF_ZZ_DELTA_I32 || OP == COVT_OP_FPF_ZZ_DELTA_XY,
+                  "in-place carry only for the linear int32 ops");
 #pragma nounroll
     for (int pass = 0; pass < 2; ++pass) {  // one inlined copy of the decoder for both passes
         Carry sums{0u, 0u};

@@ -103,6 +103,9 @@ __host__ __device__ inline bool split_op(int op) {
            op == COVT_OP_VARINT_ZZ_I32_AS_I64 || op == COVT_OP_VARINT_ZZ_DELTA_I64 || op == COVT_OP_VARINT_U64 ||
            op == COVT_OP_VARINT_ZZ_S64;
 }
+// FastPFOR ops whose long streams split into value chunks.  The chunk kernel (covt_decode.hip
+// run_fastpfor_chunk) adds a chunk's carry in place for the linear int32 ops (ZZ_DELTA_I32, ZZ_DELTA_XY) and
+// decodes Morton twice; an op added here needs a carry rule there (static_asserts guard it).
 __host__ __device__ inline bool split_fpf_op(int op) {
     return op == COVT_OP_FPF_ZZ_DELTA_I32 || op == COVT_OP_FPF_ZZ_DELTA_XY || op == COVT_OP_FPF_DELTA_MORTON;
 }

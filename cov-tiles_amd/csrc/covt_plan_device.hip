@@ -819,20 +819,22 @@ __device__ int walk_genc_fast(FastGenc& f, E& emit) {
             if (kind == 1 && ns > (uint32_t)kFwGeo) return kFastFallback;
             o += (int32_t)(ce & 0xffu);
             if (kind == 2) {  // a property column (most records): only its data bytes, in a loop of its own
-                // (no per-record check: a position with no fast record there (entry 0) counts as 2^24 data
-                // bytes and 255 bytes of metadata, so the layer's data overruns the tile and the check after
-                // the layer falls back; the walk emits nothing in between.  32-bit sums: < 2^9 * 2^24 per column)
+                // (a position with no fast record there (entry 0) is remembered in `miss` -- one scalar OR
+                // per record -- and the walk falls back after the column; meanwhile it steps 255 bytes and
+                // counts 2^24 - 1 data bytes, and emits nothing.  32-bit sums: < 2^9 * 2^24 per column)
                 // (the window offset carried instead of the tile offset, a count-down loop: fewer scalar
                 // instructions per record, the walk's bound)
-                uint32_t dd = 0;
+                uint32_t dd = 0, miss = 0;
                 int32_t q = o - f.wb;
                 for (uint32_t left = ns; left != 0; --left) {
                     if ((uint32_t)q >= f.lim) q = f.at(q + f.wb);  // (a window reload moves wb)
                     uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)f.fs->stab[q]);
+                    miss |= se == 0u;
                     se = se ? se : 0xffffffffu;
                     dd += se >> 8;
                     q += (int32_t)(se & 0xffu);
                 }
+                if (miss) return kFastFallback;  // (a tile over 16 MiB could otherwise pass the overrun check)
                 o = q + f.wb;
                 d += dd;
                 continue;
@@ -938,6 +940,9 @@ constexpr int kSlots = 128;
 // a plan is built without the mid-plan synchronisation when its tiles at this many streams each would exceed
 // the split bound (split_max_streams): such a plan splits nothing, so the guess is rarely wrong
 constexpr int64_t kSpecStreamsPerTile = 32;
+// ... and its stream arena is sized to this many streams per tile (the bench batch averages 43, the fixture
+// library's busiest tile has 67): a batch averaging more is redone with its counted size (a third sync)
+constexpr int64_t kSpecCapPerTile = 64;
 
 struct CountEmit {
     int32_t id_mode;
@@ -2946,7 +2951,7 @@ int covt_device_plan_create_opts(const uint8_t* d_bytes, uint64_t n_bytes, const
     // plan's final synchronisation -- a plan past the bound, or one that splits, runs this part again with the
     // counted sizes.  (Property plans synchronise for their record count anyway.)
     int64_t hd[4] = {0, 0, 0, 0};
-    const int64_t spec_cap = std::min<int64_t>((int64_t)kSortFuseChunks * kSortChunk, (int64_t)n_tiles * kSlots);
+    const int64_t spec_cap = std::min<int64_t>((int64_t)kSortFuseChunks * kSortChunk, (int64_t)n_tiles * kSpecCapPerTile);
     const bool spec = COVT_PLAN_SPEC && !props && wl == 0 && slots && o.split_max_streams > 0 &&
                       (int64_t)n_tiles * kSpecStreamsPerTile > o.split_max_streams;
     if (!spec) {

@@ -659,7 +659,8 @@ extern "C" int covt_materialize_properties_device(const uint8_t* d_in, const uin
 
 extern "C" int covt_release_scratch(void* hip_stream, int all) {
     const hipStream_t s = (hipStream_t)hip_stream;
-    return covt::assembly_scratch().release(s, all != 0) + covt::property_scratch().release(s, all != 0);
+    const bool every = (all & 1) != 0, pinned = (all & COVT_RELEASE_PINNED) != 0;
+    return covt::assembly_scratch().release(s, every, pinned) + covt::property_scratch().release(s, every, pinned);
 }
 
 extern "C" int64_t covt_scratch_blocks(void) {

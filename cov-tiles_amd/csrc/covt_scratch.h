@@ -6,6 +6,11 @@
 // with a fresh epoch every time).  A block is allocated and zeroed on a stream's first use; at most
 // kMaxSlots blocks are kept per kind, the least recently used one is freed beyond that (hipFree waits for
 // the device), and covt_release_scratch (include/covt.h) frees them on request.
+// A block handed out while its stream is capturing a HIP graph is pinned: the graph holds its address, so
+// the block is never evicted and covt_release_scratch frees it only when asked to with
+// COVT_RELEASE_PINNED (the caller then promises that no graph captured on that stream replays again).
+// A block cannot be allocated during a capture (hipMemsetAsync would be captured and re-zero the epoch
+// records on every replay): the stream must have run one launch before its capture.
 #ifndef COVT_SCRATCH_H
 #define COVT_SCRATCH_H
 
@@ -27,19 +32,26 @@ class StreamScratch {
     void* get(hipStream_t s) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+        hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cst) != hipSuccess) return nullptr;
+        const bool capturing = cst != hipStreamCaptureStatusNone;
         std::lock_guard<std::mutex> g(mu_);
         const auto key = std::make_pair(dev, s);
         auto it = slots_.find(key);
         if (it != slots_.end()) {
             it->second.used = ++clock_;
+            it->second.pinned |= capturing;  // a captured graph now points at this block
             return it->second.p;
         }
-        if (slots_.size() >= kMaxSlots) {  // evict the least recently used block
-            auto lru = slots_.begin();
+        if (capturing) return nullptr;  // (see the header comment)
+        if (slots_.size() >= kMaxSlots) {  // evict the least recently used unpinned block (if any)
+            auto lru = slots_.end();
             for (auto j = slots_.begin(); j != slots_.end(); ++j)
-                if (j->second.used < lru->second.used) lru = j;
-            free_slot(lru->first.first, lru->second.p);
-            slots_.erase(lru);
+                if (!j->second.pinned && (lru == slots_.end() || j->second.used < lru->second.used)) lru = j;
+            if (lru != slots_.end()) {
+                free_slot(lru->first.first, lru->second.p);
+                slots_.erase(lru);
+            }
         }
         void* p = nullptr;
         if (hipMalloc(&p, bytes_) != hipSuccess) return nullptr;
@@ -49,18 +61,19 @@ class StreamScratch {
             (void)hipFree(p);
             return nullptr;
         }
-        slots_[key] = Slot{p, ++clock_};
+        slots_[key] = Slot{p, ++clock_, false};
         return p;
     }
 
-    // frees the block of (current device, s), or every block when `all`; returns the number freed
-    int release(hipStream_t s, bool all) {
+    // frees the block of (current device, s), or every block when `all`; pinned blocks only with
+    // `pinned_too`; returns the number freed
+    int release(hipStream_t s, bool all, bool pinned_too) {
         int dev = 0;
         if (!all && hipGetDevice(&dev) != hipSuccess) return 0;
         std::lock_guard<std::mutex> g(mu_);
         int n = 0;
         for (auto it = slots_.begin(); it != slots_.end();) {
-            if (all || it->first == std::make_pair(dev, s)) {
+            if ((all || it->first == std::make_pair(dev, s)) && (pinned_too || !it->second.pinned)) {
                 free_slot(it->first.first, it->second.p);
                 it = slots_.erase(it);
                 ++n;
@@ -80,6 +93,7 @@ class StreamScratch {
     struct Slot {
         void* p;
         uint64_t used;
+        bool pinned;  // first used or reused under a graph capture
     };
     static void free_slot(int dev, void* p) {
         int cur = 0;

@@ -465,11 +465,19 @@ int covt_materialize_properties_device(const uint8_t* d_in, const uint8_t* d_dec
  * and covt_materialize_properties_device keep one device scratch block per (device, HIP stream) (about
  * 8.4 MB for assembly, 0.6 MB for properties), allocated and zeroed on the stream's first use and reused
  * by every later launch on it.  Each launch tags its look-back records with an epoch its own first kernel
- * advances in device memory, so launches captured in a HIP graph replay correctly.  At most 16 blocks of
- * each kind are kept; beyond that the least recently used one is freed.  covt_release_scratch frees the
- * blocks of (current device, hip_stream), or every block when `all` is non-zero, and returns how many it
- * freed.  hipFree waits for the device, so no launch still in flight uses a freed block; a caller that
- * creates a stream per batch should release its blocks before destroying the stream. */
+ * advances in device memory, so launches captured in a HIP graph replay correctly -- under two rules: a
+ * graph is replayed on its capture stream (or on streams ordered with it: replays of graphs that share a
+ * capture stream must not overlap, they share one block's tickets and epoch), and the stream has run one
+ * such launch before the capture (a block cannot be allocated while capturing: the launch then fails with
+ * COVT_ERR_DEVICE).  A block used under a capture is pinned for the graph: it is never evicted and
+ * covt_release_scratch frees it only with COVT_RELEASE_PINNED.  At most 16 unpinned blocks of each kind
+ * are kept; beyond that the least recently used unpinned one is freed.  covt_release_scratch frees the
+ * unpinned block of (current device, hip_stream), or every unpinned block when bit 0 of `all` is set, plus
+ * the pinned ones matched the same way with COVT_RELEASE_PINNED (the caller promises that no graph
+ * captured on them replays again), and returns how many it freed.  hipFree waits for the device, so no
+ * launch still in flight uses a freed block; a caller that creates a stream per batch should release its
+ * blocks before destroying the stream. */
+#define COVT_RELEASE_PINNED 0x2
 int covt_release_scratch(void* hip_stream, int all);
 /* blocks currently held (assembly + properties) */
 int64_t covt_scratch_blocks(void);
@@ -490,9 +498,11 @@ int covt_plan_properties_host(const covt_plan* plan, const uint8_t* bytes, uint6
  * cut into the same chunks (varint byte chunks, FastPFOR value chunks with their start states, ORC RLE
  * group chunks); geometry-column planning on request (covt_device_plan_geometry); property columns
  * with COVT_PLAN_PROPERTIES in opts->flags.  Multi-GPU shards stay with the host plan.
- * Runs on `hip_stream` and synchronises it twice (three times when it splits: the stream count and
- * the descriptor count size the arrays); COVT_PLAN_PROPERTIES adds one more (the property record
- * count).  COVT_ERR_BAD_HEADER if the property walk fails a tile the Id / Geometry walk accepted (the
+ * Runs on `hip_stream` and synchronises it: once for an Id / Geometry plan of more than
+ * split_max_streams / 32 tiles (nothing splits there; the stream arrays are sized to 64 streams per tile
+ * and the count is checked at the end -- a batch averaging more is redone with its counted size: three
+ * syncs), otherwise twice (three times when it splits: the stream count and the descriptor count size the
+ * arrays); COVT_PLAN_PROPERTIES adds one more (the property record count).  COVT_ERR_BAD_HEADER if the property walk fails a tile the Id / Geometry walk accepted (the
  * walkers diverged: never on well-formed or corrupted input that the host plan rejects the same way).
  * Limits and memory: a tile of 0x7ff00000 bytes or more gets COVT_ERR_INVALID_ARG as its status
  * (32-bit cursors; the host plan walks such tiles); besides the stream arrays the plan holds ~5 KiB

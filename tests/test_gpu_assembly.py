@@ -316,7 +316,58 @@ def test_split_passes_replay_in_a_hip_graph(covt, oracle, gpu_available):
         _check_vs_oracle(oracle, cols, d_asm.cpu().numpy(), gres, lay)
     del g
     torch.cuda.synchronize()
-    assert covt.release_scratch(s) >= 1
+    assert covt.release_scratch(s) == 0  # pinned by the capture: kept unless asked
+    assert covt.release_scratch(s, pinned=True) >= 1
+
+
+def test_captured_graph_survives_scratch_eviction(covt, oracle, gpu_available):
+    """a block used under a graph capture is pinned -- launches on 20 other streams
+    after the capture (more than the 16 blocks kept) evict only unpinned blocks, and covt_release_scratch
+    without COVT_RELEASE_PINNED keeps it -- so the graph replays into live memory, bit-exact."""
+    import torch
+
+    covt.release_scratch(all=True, pinned=True)
+    cols = _split_cols()
+    dec, desc, asm_bytes, lay = A.pack_columns(covt, cols, None, None)
+    dev = torch.device("cuda:0")
+    d_dec = torch.from_numpy(dec).to(dev)
+    d_desc = torch.from_numpy(desc).to(dev)
+    d_asm = torch.full((asm_bytes,), 0x5A, dtype=torch.uint8, device=dev)
+    d_gres = torch.zeros(4 * len(cols), dtype=torch.int32, device=dev)
+    d_res = torch.zeros(2, dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream(dev)
+
+    def launch():
+        assert covt.lib().covt_assemble_geometry_device(d_dec.data_ptr(), d_res.data_ptr(), d_desc.data_ptr(),
+                                                        len(cols), d_asm.data_ptr(), d_gres.data_ptr(),
+                                                        s.cuda_stream) == 0
+
+    with torch.cuda.stream(s):
+        launch()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        launch()
+    streams = [torch.cuda.Stream(dev) for _ in range(20)]
+    for o in streams:
+        with torch.cuda.stream(o):
+            _run_kernel(covt, cols)
+        assert covt.scratch_blocks() <= 16
+    torch.cuda.synchronize()
+    assert covt.release_scratch(all=True) >= 1  # every unpinned block ...
+    assert covt.scratch_blocks() == 1           # ... but the graph's
+    for _ in range(2):
+        d_asm.fill_(0x5A)
+        d_gres.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        gres = d_gres.cpu().numpy().view(covt.GEOM_RESULT_DTYPE)
+        assert (gres["status"] == 0).all()
+        _check_vs_oracle(oracle, cols, d_asm.cpu().numpy(), gres, lay)
+    del g
+    torch.cuda.synchronize()
+    assert covt.release_scratch(all=True, pinned=True) == 1 and covt.scratch_blocks() == 0
 
 
 def test_scratch_blocks_bounded_and_released(covt, oracle, gpu_available):
@@ -324,7 +375,7 @@ def test_scratch_blocks_bounded_and_released(covt, oracle, gpu_available):
     freed), all freed by covt_release_scratch(all); results stay exact on every stream."""
     import torch
 
-    covt.release_scratch(all=True)
+    covt.release_scratch(all=True, pinned=True)
     assert covt.scratch_blocks() == 0
     cols = _split_cols()
     dev = torch.device("cuda:0")

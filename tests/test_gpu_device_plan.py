@@ -481,3 +481,24 @@ def test_properties_full_batch(covt, gpu_available):
     dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
     _assert_same_plan(hp, dp)
     _assert_same_properties(hp, dp)
+
+
+def test_bound_sized_plan_redo(covt, gpu_available, decodable_tiles):
+    """an Id / Geometry plan of more than split_max_streams / 32 tiles sizes its stream
+    arrays to 64 streams per tile before the count is known; a batch of the busiest tiles (more than 64
+    streams each) overruns that bound and is redone with the counted size -- still the host plan exactly,
+    and it decodes the same."""
+    counted = []
+    for _, t in decodable_tiles:
+        hp1 = _host_plan(covt, [t], covt.FORMAT_GENC, 0)
+        counted.append((hp1.num_streams, t))
+    counted.sort(key=lambda x: -x[0])
+    busy = [t for n, t in counted if n > 64][:1]
+    if not busy:
+        pytest.skip("no fixture tile with more than 64 Id / Geometry streams")
+    tiles = busy * 6
+    hp = _host_plan(covt, tiles, covt.FORMAT_GENC, 0, split=True, split_max_streams=64)
+    assert hp.num_streams > 64 * len(tiles)
+    dp = _device_plan(covt, hp, covt.FORMAT_GENC, 0)
+    _assert_same_plan(hp, dp)
+    _assert_same_decode(covt, hp, dp)

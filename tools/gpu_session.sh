@@ -68,13 +68,12 @@ for s in "$@"; do
     util_rle|util_varint|util_fastpfor|util_lane|util_all) fam=${s#util_}; step $s$sfx 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_VALU -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     sqi_rle|sqi_varint|sqi_fastpfor|sqi_lane|sqi_all) fam=${s#sqi_}; step $s$sfx 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     sqc_rle|sqc_varint|sqc_fastpfor|sqc_lane|sqc_all) fam=${s#sqc_}; step $s$sfx 600 rocprofv3 --pmc SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_BRANCH GRBM_GUI_ACTIVE -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
-    icache_rle|icache_varint|icache_fastpfor|icache_lane|icache_all) fam=${s#icache_}; step $s 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH GRBM_GUI_ACTIVE -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
+    icache_rle|icache_varint|icache_fastpfor|icache_lane|icache_all) fam=${s#icache_}; step $s$sfx 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH GRBM_GUI_ACTIVE -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     mem_rle|mem_varint|mem_fastpfor|mem_lane) fam=${s#mem_}; step $s$sfx 600 rocprofv3 --pmc GRBM_GUI_ACTIVE TA_TA_BUSY TA_DATA_STALLED_BY_TC_CYCLES TCP_PENDING_STALL_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     sq_rle|sq_varint|sq_fastpfor|sq_lane) fam=${s#sq_}; step $s$sfx 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR -d gpurun_out/$s$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 ;;
     opinst) step opinst 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE -d gpurun_out/opinst -o run --output-format csv -- python tools/op_counters.py ;;
     tests_changed) step pytest_changed 600 python -u -m pytest tests/test_gpu_assembly.py tests/test_gpu_props.py tests/test_gpu_split.py tests/test_gpu_rle_adversarial.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     tests_r05) step pytest_r05 600 python -u -m pytest tests/test_gpu_assembly.py tests/test_gpu_props.py tests/test_jni_shim.py tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -s ;;
-    tests_dplan) step pytest_dplan 300 python -u -m pytest tests/test_gpu_device_plan.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     dplan_geo) step dplan_geo 200 python tools/device_plan_prof.py 20 --sweep --geometry ;;
     dplan_drop) step dplan_drop 300 python tools/device_plan_prof.py 20 --drop=16,64,256,1024,4096 ;;
     walk_timeline) step walk_timeline 300 python tools/walk_timeline.py 5 ;;

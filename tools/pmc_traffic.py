@@ -32,7 +32,7 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
 
-    res = {"tiles": 10000, "scaling": "weak", "kernel_sources_sha256": bench.kernel_sources_sha256(),
+    res = {"tiles": 10000, "n_gpus": 1, "kernel_sources_sha256": bench.kernel_sources_sha256(),
            "fetch_kib_raw": fetch, "write_kib_raw": write,
            "read_bytes_corrected": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
            "note": "FETCH_SIZE x2 (gfx950 wide-read correction), WRITE_SIZE as is; KiB -> bytes"}
