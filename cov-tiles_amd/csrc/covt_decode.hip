@@ -42,6 +42,9 @@ constexpr int kFpfBcCap = 3 * kFpfPage / kFpfBlock + kFpfPage;  // JavaFastPFOR 
 #ifndef COVT_LONG_PRIO
 #define COVT_LONG_PRIO 2
 #endif
+#ifndef COVT_FPF_STREAM  // 1: whole FastPFOR streams through run_fastpfor_stream (0: run_fastpfor, A/B)
+#define COVT_FPF_STREAM 1
+#endif
 #ifndef COVT_CHUNK_PRIO
 #define COVT_CHUNK_PRIO 2
 #endif
@@ -69,7 +72,10 @@ struct __attribute__((aligned(16))) WaveSmem {
             uint16_t grec[64];             // RLE: the chain walk's successor of each step (int RLE)
         } v;
         struct {
-            uint32_t stage[324];  // packed words of one FastPFOR block (<= 1024 + 15 B)
+            union {
+                uint32_t stage[324];  // split chunks: packed words of one FastPFOR block (<= 1024 + 15 B)
+                uint32_t ring[512];   // whole streams: two 1 KiB windows of the page's packed words
+            };
             uint32_t patch[256];  // exception patches of one block
             uint32_t cbuf[260];   // 1 KiB chunk of the page's byte container
             uint8_t posx[2][192]; // positions of exceptions 64..255 of the next two blocks
@@ -79,8 +85,8 @@ struct __attribute__((aligned(16))) WaveSmem {
 constexpr int kSmemHdr = 272;  // offsetof(WaveSmem, u), checked below
 constexpr int kFamSmemRle = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2 + (kWin + 8) * 2 + 64 * 2;
 constexpr int kFamSmemVarint = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2;
-constexpr int kFamSmemFpf = kSmemHdr + (324 + 256 + 260) * 4 + 384 > kFamSmemVarint
-                                ? kSmemHdr + (324 + 256 + 260) * 4 + 384
+constexpr int kFamSmemFpf = kSmemHdr + (512 + 256 + 260) * 4 + 384 > kFamSmemVarint
+                                ? kSmemHdr + (512 + 256 + 260) * 4 + 384
                                 : kFamSmemVarint;
 static_assert(kFamSmemFpf >= kSmemHdr + (int)sizeof(((WaveSmem*)nullptr)->u.f), "FastPFOR scratch stride");
 static_assert(kFamSmemVarint >= kSmemHdr + (int)sizeof(((WaveSmem*)nullptr)->u.v.win) +
@@ -1893,6 +1899,416 @@ __device__ __forceinline__ void run_fastpfor(Ctx& c, int32_t v0 = 0, int32_t v1 
     if (fin) *fin = cr;  // the running sums after the range (from cr0)
 }
 
+// FastPFOR + VariableByte over a whole stream (the family kernels' path; split chunks keep run_fastpfor
+// above).  Same page framing, directory and checks as run_fastpfor; what differs is how the blocks get
+// their words and headers:
+//  * packed words stream through LDS: a page's packed words are one contiguous run of stream words from
+//    p0 + 1 (block j's 8 b words follow block j - 1's), so they are read in 1 KiB windows from the 128-byte
+//    line holding word p0 + 1 -- one 16-byte load per lane, each window requested as soon as the previous
+//    one is staged -- and staged byte-swapped into a 512-word ring (two windows).  A block waits only when
+//    its words pass the staged end, on a load issued a window (about five blocks) earlier; no load address
+//    depends on a block header.  Lane 63's last word needs the next window's first bytes: it is written
+//    when that window is staged (the staged end lags by one word).
+//  * block headers in batches of up to 64 (one serial walk of the header chain, one LDS read per header,
+//    then lane-parallel: packed-word offsets and exception cursors by prefix sums, every check at once by
+//    ballot); each block reads its state from those lanes.
+// Blocks before a failing one are decoded and stored; the failing block's status is the stream's.
+template <int OP>
+__device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
+    WaveSmem& sm = *c.sm;
+    const int l = lane_id();
+    const Words W{c.sb, c.byte_length / 4};
+    const int64_t nw = W.nw;
+    const int32_t nw32 = (int32_t)nw;
+    const uint32_t bsel = be_sel((uint32_t)((uintptr_t)c.sb & 3u));  // a stream word from the 4-byte grid
+    Carry cr{0u, 0u};
+    int32_t decoded = 0;
+    int32_t L = 0;
+    int64_t p = 1;
+    int xs_v = 0, xz_v = -1, xc_v = 0;  // lane k: dataTobePacked[k] start word, size, values consumed
+    int64_t mw0 = 0;                     // stream word of cbuf[0] (the meta window)
+    if (c.byte_length > c.avail) { c.err = COVT_ERR_TRUNCATED; }
+    if (!c.err && nw > 0) {
+        const uint32_t head0 = W.uniform(0), head1 = W.uniform(1);
+        L = (int32_t)head0;
+        if (L < 0) c.err = COVT_ERR_BAD_HEADER;
+        L -= L % kFpfBlock;
+        if (!c.err && L > c.n) c.err = COVT_ERR_COUNT_MISMATCH;
+        int32_t done = 0;
+        const uintptr_t s_end = (uintptr_t)(c.sb + 4 * nw);
+        struct WordsRaw {
+            uint4 r;
+            int64_t base;
+            uint32_t sh;
+        };
+        auto words_issue = [&](int64_t w) -> WordsRaw {
+            const uintptr_t addr = (uintptr_t)(c.sb + 4 * w);
+            const uintptr_t a16 = addr & ~(uintptr_t)15;
+            const uint32_t o = (uint32_t)(addr & 15u);
+            const uint32_t lmax = s_end > a16 ? (uint32_t)((s_end - 1 - a16) >> 4) : 0u;
+            WordsRaw q;
+            q.r = ld128_off((const g_u8*)a16, 16u * min((uint32_t)l, lmax));
+            q.base = uni64(w - (int64_t)(o >> 2));
+            q.sh = o & 3u;
+            return q;
+        };
+        auto words_store = [&](uint32_t* dst, const WordsRaw& q) -> int64_t {
+            const uint32_t nx = lane_next(q.r.x);
+            const uint32_t sel = be_sel(q.sh);
+            const int64_t wl = q.base + 4 * l;
+            uint4 wv;
+            wv.x = wl < nw ? be_word(q.r.y, q.r.x, sel) : 0u;
+            wv.y = wl + 1 < nw ? be_word(q.r.z, q.r.y, sel) : 0u;
+            wv.z = wl + 2 < nw ? be_word(q.r.w, q.r.z, sel) : 0u;
+            wv.w = wl + 3 < nw ? be_word(nx, q.r.w, sel) : 0u;
+            wave_sync();
+            ((uint4*)dst)[l] = wv;
+            wave_sync();
+            return q.base;
+        };
+        auto load_words = [&](uint32_t* dst, int64_t w) -> int64_t { return words_store(dst, words_issue(w)); };
+        while (!c.err && done < L) {
+            done = uni(done);
+            const int32_t thissize = uni((L - done) < kFpfPage ? (L - done) : kFpfPage);
+            const int64_t p0 = uni64(p);
+            if (p0 >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+            int64_t ie = p0 + (int32_t)(p0 == 1 ? head1 : W.uniform(p0));  // the page's bytesize word
+            if (ie < 0 || ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+            // one round trip: the meta window (bytesize, byte container, small pages' directory and exception
+            // arrays) and the first window of packed words, requested together (meta first: its wait does not
+            // wait for the packed words)
+            const WordsRaw mq = words_issue(ie);
+            const uintptr_t pa = (uintptr_t)c.sb + 4u * (uint32_t)(p0 + 1);
+            const uintptr_t A0 = pa & ~(uintptr_t)127;
+            // last 16-byte granule of the stream relative to A0: lanes past it repeat it (unmasked loads)
+            const uint32_t glast = s_end > A0 ? (uint32_t)((s_end - 1 - A0) & ~(uintptr_t)15) : 0u;
+            // ring word m (window k, lane l, word i: m = 256 k + 4 l + i) holds stream word wbase + m
+            const int32_t wbase = uni((int32_t)(p0 + 1) - (int32_t)((pa - A0) >> 2));
+            uint4 R = ld128_off((const g_u8*)A0, min(16u * (uint32_t)l, glast));
+            int32_t kst = 0;       // windows staged
+            int32_t vend = wbase;  // stream words below vend are staged
+            uint32_t prev63 = 0u;  // lane 63's last raw dword of the last staged window
+            mw0 = words_store(sm.u.f.cbuf, mq);
+            auto mword = [&](int64_t w) -> uint32_t { return uniu(sm.u.f.cbuf[w - mw0]); };
+            const int32_t bytesize = (int32_t)mword(ie++);
+            if (bytesize < 0 || bytesize > kFpfBcCap) { c.err = COVT_ERR_BAD_HEADER; break; }
+            xc_v = 0;
+            const int64_t bcw = (bytesize + 3) / 4;
+            const int64_t bc = ie;
+            if (bc + bcw >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+            ie += bcw;
+            {
+                int64_t dbase = INT64_MIN / 2;
+                auto dword = [&](int64_t w) -> uint32_t {
+                    if (w >= mw0 && w < mw0 + 255) return mword(w);
+                    // (the ring is free until the first window is staged)
+                    if (w < dbase || w >= dbase + 255) dbase = load_words(sm.u.f.ring, w);
+                    return uniu(sm.u.f.ring[w - dbase]);
+                };
+                uint32_t bm = dword(ie++) & ~1u;
+                xs_v = 0;
+                xz_v = -1;
+                while (bm) {
+                    const int32_t k = __builtin_ctz(bm) + 1;
+                    bm &= bm - 1;
+                    if (ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+                    const int32_t size = (int32_t)dword(ie++);
+                    if (size < 0) { c.err = COVT_ERR_BAD_HEADER; break; }
+                    const int64_t groups = ((int64_t)size + 31) / 32;
+                    xs_v = l == k ? (int)(uint32_t)ie : xs_v;
+                    xz_v = l == k ? size : xz_v;
+                    ie += groups * k;
+                    ie -= ((groups * 32 - size) * k) / 32;
+                }
+                if (c.err) break;
+            }
+            const bool xin = ie - mw0 <= 255;  // the page's whole metadata sits in the meta window
+            COVT_PHASE(c, 0);
+            const int32_t nblocks = uni(thissize / kFpfBlock);
+            const int32_t bclen = uni((int32_t)(bcw * 4));
+            const uint8_t* cb8 = (const uint8_t*)sm.u.f.cbuf;
+            const g_u8* cbyte = (const g_u8*)(c.sb + 4 * bc);  // container byte q: cbyte[q ^ 3]
+            int32_t cbase = (int32_t)(4 * (mw0 - bc));
+            auto chunk_load = [&](int32_t at) {  // container bytes [cbase, cbase + 1020), cbase in (at - 16, at]
+                cbase = (int32_t)(4 * (load_words(sm.u.f.cbuf, bc + (at >> 2)) - bc));
+            };
+            auto xword = [&](int32_t k, uint32_t xs, uint32_t i, uint32_t& xbit) -> int32_t {
+                const uint32_t bit = __umul24(i & 31u, (uint32_t)k);
+                xbit = bit & 31u;
+                return (int32_t)(xs + __umul24(i >> 5, (uint32_t)k) + (bit >> 5));
+            };
+            // the next window of packed words: staged into the ring, the one after it requested
+            auto stage = [&]() {
+                const int32_t k = uni(kst);
+                const uint32_t nx = lane_next(R.x, 0u);
+                const int32_t w0 = wbase + 256 * k + 4 * l;
+                uint4 wv;
+                wv.x = w0 < nw32 ? be_word(R.y, R.x, bsel) : 0u;
+                wv.y = w0 + 1 < nw32 ? be_word(R.z, R.y, bsel) : 0u;
+                wv.z = w0 + 2 < nw32 ? be_word(R.w, R.z, bsel) : 0u;
+                wv.w = w0 + 3 < nw32 ? be_word(nx, R.w, bsel) : 0u;  // (lane 63: incomplete, not stored)
+                const int32_t fw = wbase + 256 * k - 1;  // the previous window's last word
+                const uint32_t fix = fw < nw32 ? be_word(lane_bcast(R.x, 0), prev63, bsel) : 0u;
+                prev63 = lane_bcast(R.w, 63);
+                const uint32_t ri = (uint32_t)(256 * k + 4 * l) & 511u;
+                wave_sync();
+                if (l < 63) {
+                    *(uint4*)&sm.u.f.ring[ri] = wv;
+                } else {
+                    sm.u.f.ring[ri] = wv.x;
+                    sm.u.f.ring[ri + 1] = wv.y;
+                    sm.u.f.ring[ri + 2] = wv.z;
+                }
+                if (l == 0 && k > 0) sm.u.f.ring[(uint32_t)(256 * k - 1) & 511u] = fix;
+                wave_sync();
+                kst = k + 1;
+                vend = wbase + 256 * (k + 1) - 1;
+                R = ld128_off((const g_u8*)A0, min(1024u * (uint32_t)(k + 1) + 16u * (uint32_t)l, glast));
+                wave_sync();  // (the request stays ahead of the stores that follow: see the block's wait)
+            };
+            // the page's first window (requested with the meta window): vend >= p0 + 1 from here on
+            // (unconditional: a page holds >= 1 block -- L is a multiple of 256 -- and a path around it would
+            // reach the first block's wait right after the page's request)
+            stage();
+            int32_t cur = 0, pk = (int32_t)p0 + 1;
+            for (int32_t jbat = 0; jbat < nblocks && !c.err; jbat += 64) {
+                jbat = uni(jbat);
+                const int32_t nbat = uni(min(64, nblocks - jbat));
+                // (1) the header chain: block jbat + g's header bytes and container offset to lane g
+                uint32_t hw_v = 0u;
+                int32_t cur_v = bclen + 1;  // (past the container: no header)
+                for (int32_t g = 0; g < nbat; ++g) {
+                    cur = uni(cur);
+                    cbase = uni(cbase);
+                    if (cur > bclen) break;  // the chain has left the container
+                    if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 8)) chunk_load(cur);
+                    const int32_t q = cur - cbase;
+                    const uint32_t hw =
+                        uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(q >> 2) + 1], sm.u.f.cbuf[q >> 2], (uint32_t)q & 3u));
+                    hw_v = l == g ? hw : hw_v;
+                    cur_v = l == g ? cur : cur_v;
+                    const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
+                    cur += ce > 0 ? 3 + ce : 2;
+                }
+                COVT_PHASE(c, 1);
+                // (2) lane-parallel: fields, exception cursors (a prefix sum per exception width present),
+                // packed-word offsets, checks
+                const bool in = l < nbat;
+                const int32_t b_v = (int32_t)(int8_t)(hw_v & 0xffu);
+                const int32_t ce_v = (int32_t)((hw_v >> 8) & 0xffu);
+                const bool hasx = ce_v > 0;
+                const int32_t idx_v = hasx ? (int32_t)(int8_t)((hw_v >> 16) & 0xffu) - b_v : 1;
+                const bool arr_k = hasx && idx_v >= 2 && idx_v <= 32;  // exceptions from dataTobePacked[idx]
+                const bool arr = in && arr_k;
+                int32_t xcur_v = 0;
+                for (uint64_t todo = __ballot(arr); todo;) {
+                    const int32_t kk = __builtin_amdgcn_readlane(idx_v, (int32_t)__builtin_ctzll(todo));
+                    const bool mine = arr && idx_v == kk;
+                    const uint32_t v = mine ? (uint32_t)ce_v : 0u;
+                    const uint32_t s = incl_scan(v);
+                    const int32_t base = __builtin_amdgcn_readlane(xc_v, kk);
+                    xcur_v = mine ? base + (int32_t)(s - v) : xcur_v;
+                    xc_v += l == kk ? (int32_t)lane_bcast(s, 63) : 0;
+                    todo &= ~__ballot(mine);
+                }
+                const uint32_t w8 = in ? 8u * (uint32_t)(b_v & 63) : 0u;
+                const uint32_t pinc = incl_scan(w8);
+                const int32_t pk_v = pk + (int32_t)(pinc - w8);
+                pk += (int32_t)lane_bcast(pinc, 63);
+                int32_t nok = nbat;  // blocks of the batch before the first failing one
+                int32_t ferr = 0;
+                {
+                    const int32_t xsz = lane_get(xz_v, arr_k ? idx_v : 0);
+                    bool bad = (uint32_t)b_v > 32u || cur_v + 2 > bclen;
+                    bad |= hasx && (cur_v + 3 + ce_v > bclen || (idx_v != 1 && !arr_k));
+                    bad |= arr_k && (xsz < 0 || xcur_v + ce_v > xsz);
+                    const bool trunc = pk_v + 8 * b_v > nw32;
+                    const uint64_t fail = __ballot(in && (bad || trunc));
+                    if (fail) {
+                        nok = (int32_t)__builtin_ctzll(fail);
+                        ferr = __builtin_amdgcn_readlane(bad ? COVT_ERR_BAD_HEADER : COVT_ERR_TRUNCATED, nok);
+                    }
+                }
+                COVT_PHASE(c, 2);
+                // (3) the blocks, exception loads one block ahead (pages whose metadata is past the meta window)
+                struct Hdr {
+                    int32_t b, ce, idx, pk, bcoff;
+                    uint32_t xcur;
+                };
+                auto rec = [&](int32_t g, Hdr& h) {
+                    const uint32_t hw = (uint32_t)__builtin_amdgcn_readlane((int32_t)hw_v, g);
+                    h.b = (int32_t)(int8_t)(hw & 0xffu);
+                    h.ce = (int32_t)((hw >> 8) & 0xffu);
+                    h.idx = h.ce > 0 ? (int32_t)(int8_t)((hw >> 16) & 0xffu) - h.b : 1;
+                    h.xcur = (uint32_t)__builtin_amdgcn_readlane(xcur_v, g);
+                    h.bcoff = __builtin_amdgcn_readlane(cur_v, g) + (h.ce > 0 ? 3 : 2);
+                    h.pk = __builtin_amdgcn_readlane(pk_v, g);
+                };
+                // the container window holding block h's exception positions (the first 64 are read from it)
+                auto pos_window = [&](const Hdr& h) {
+                    cbase = uni(cbase);
+                    if (!xin && h.ce > 0 && (uint32_t)(h.bcoff - cbase) > (uint32_t)(1020 - 64)) chunk_load(h.bcoff);
+                };
+                auto prefetch = [&](const Hdr& h, FpfPre& pr) {
+                    const int32_t k = h.idx;
+                    const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
+                    uint32_t xb;
+                    const int32_t wx = xword(k >= 2 ? k : 2, xs, h.xcur + (uint32_t)l, xb);
+                    const uint32_t xon = (uint32_t)(k >= 2) & (uint32_t)(l < h.ce) & (uint32_t)(wx < nw32);
+                    if (!xin) {  // (xin: the values are read from the meta window when the block is patched)
+                        const uint32_t wi = (uint32_t)wx & (0u - xon);
+                        const u32x3 xv = *(const g_v3*)((const g_u8*)(((uintptr_t)c.sb) & ~(uintptr_t)3) + 4u * wi);
+                        pr.x0 = xv.x;
+                        pr.x1 = xv.y;
+                        pr.x2 = xv.z;
+                    }
+                    const int32_t pb = h.bcoff - cbase;
+                    pr.pos = cb8[min(max(pb + l, 0), 4 * 260 - 1)];
+                };
+                Hdr h{0, 0, 1, pk, 0, 0u};  // (a batch failing at its first block: a harmless prefetch)
+                FpfPre pre, preB;
+                if (nok > 0) {
+                    rec(0, h);
+                    pos_window(h);
+                }
+                prefetch(h, pre);
+                // as many zero stores to the batch's first block as a block's sink issues (overwritten by its
+                // values): every path from a window request or this prefetch to its wait then passes a store
+                // -- also when the first block needs the next window at once -- so the compiler's vmcnt waits
+                // stay partial instead of vmcnt(0) (which would also wait for the stores just issued)
+                fpf_prime_stores<OP>(c.out, (int64_t)done + (int64_t)jbat * kFpfBlock);
+                auto block = [&](int32_t g, const FpfPre& pc, FpfPre& pn) {
+                    Hdr hc;
+                    hc.b = uni(h.b);
+                    hc.ce = uni(h.ce);
+                    hc.idx = uni(h.idx);
+                    hc.xcur = uniu(h.xcur);
+                    hc.bcoff = uni(h.bcoff);
+                    hc.pk = uni(h.pk);
+                    const int32_t b = hc.b;
+                    // this block's words staged.  One window is always enough (vend >= pk: the previous block
+                    // needed up to pk; a block needs <= 256 words), and never two stages back to back: every
+                    // path from a window's request to its wait then passes a block's output stores, so the
+                    // compiler's vmcnt wait there stays partial (a loop here, or a second stage, made it
+                    // vmcnt(0) on every block: the stores and exception loads just issued waited for too)
+                    if (uni(vend) < hc.pk + 8 * b) stage();
+                    if (hc.ce > 0) ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
+                    COVT_PHASE(c, 3);
+                    // the next block's exception loads in flight (issued on every path; the batch's last
+                    // block re-reads its own)
+                    if (g + 1 < nok) {
+                        rec(g + 1, h);
+                        pos_window(h);
+                    }
+                    prefetch(h, pn);
+                    // unpack: lane l -> values 4l..4l+3 of miniblock l/8, words from the ring
+                    uint32_t v[4];
+                    {
+                        const uint32_t mask = b == 32 ? 0xffffffffu : ((1u << b) - 1u);
+                        uint32_t bit = __umul24((uint32_t)(l & 7) * 4u, (uint32_t)b);
+                        const int32_t r0 = (hc.pk - wbase) & 511;
+                        const int32_t wb = (int32_t)__umul24((uint32_t)(l >> 3), (uint32_t)b) + r0;
+                        if (r0 + 8 * b <= 511) {
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const int32_t wi = wb + (int32_t)(bit >> 5);
+                                const uint32_t lo = sm.u.f.ring[wi], hi = sm.u.f.ring[wi + 1];
+                                v[k] = __builtin_amdgcn_alignbit(hi, lo, bit & 31u) & mask;
+                                bit += (uint32_t)b;
+                            }
+                        } else {  // the block wraps around the ring's end
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const int32_t wi = wb + (int32_t)(bit >> 5);
+                                const uint32_t lo = sm.u.f.ring[wi & 511], hi = sm.u.f.ring[(wi + 1) & 511];
+                                v[k] = __builtin_amdgcn_alignbit(hi, lo, bit & 31u) & mask;
+                                bit += (uint32_t)b;
+                            }
+                        }
+                    }
+                    COVT_PHASE(c, 4);
+                    if (hc.ce > 0) {  // out[pos] |= (index == 1 ? 1 : exceptvalue) << b
+                        const int32_t k = hc.idx;
+                        const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
+                        const bool el = l < hc.ce;
+                        uint32_t ex = 1u;
+                        if (k != 1) {  // uniform
+                            uint32_t xbit;
+                            const int32_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
+                            uint32_t lo, hi;
+                            if (xin) {  // meta window: words already swapped, 0 past the stream
+                                const int32_t m = el ? wi - (int32_t)mw0 : 0;
+                                lo = sm.u.f.cbuf[m];
+                                hi = sm.u.f.cbuf[m + 1];
+                            } else {
+                                lo = wi < nw32 ? be_word(pc.x1, pc.x0, bsel) : 0u;
+                                hi = wi + 1 < nw32 ? be_word(pc.x2, pc.x1, bsel) : 0u;
+                            }
+                            const uint32_t m = k == 32 ? 0xffffffffu : ((1u << k) - 1u);
+                            ex = __builtin_amdgcn_alignbit(hi, lo, xbit) & m;
+                        }
+                        atomicOr(&sm.u.f.patch[el ? pc.pos : (uint32_t)(4 * l)], el ? ex << (b & 31) : 0u);
+                        if (hc.ce > 64) {  // rare: more than 64 exceptions in the block (positions from memory)
+                            for (int q = 1; q < 4; ++q) {
+                                const int32_t e = l + 64 * q;
+                                if (e < hc.ce) {
+                                    const uint32_t ex2 = k == 1 ? 1u : xget(W, xs, k, hc.xcur + (uint32_t)e);
+                                    const uint32_t ps = cbyte[(hc.bcoff + e) ^ 3];
+                                    atomicOr(&sm.u.f.patch[ps], ex2 << (b & 31));
+                                }
+                            }
+                        }
+                        wave_sync();
+                        const uint4 pt = ((const uint4*)sm.u.f.patch)[l];
+                        v[0] |= pt.x;
+                        v[1] |= pt.y;
+                        v[2] |= pt.z;
+                        v[3] |= pt.w;
+                    }
+                    COVT_PHASE(c, 5);
+                    sink_values<OP, 4>(v, (int64_t)done + (int64_t)(jbat + g) * kFpfBlock, 0, kFpfBlock, c.nb, c.out, cr);
+                    wave_sync();
+                    COVT_PHASE(c, 6);
+                };
+                for (int32_t g = 0; g < nok; g += 2) {
+                    g = uni(g);
+                    block(g, pre, preB);
+                    if (g + 1 < nok) block(g + 1, preB, pre);
+                }
+                if (ferr) c.err = ferr;
+            }
+            done += thissize;
+            p = ie;
+        }
+        decoded = L;
+        // VariableByte tail over words [p, nw): from the last page's meta window when it holds them
+        if (!c.err && p < nw) {
+            int32_t vpos = (int32_t)(4 * p);
+            const int32_t base = L;
+            Win w;
+            w.valid = false;
+            const bool tail_in = L > 0 && ((int64_t)(vpos & ~15) >> 2) >= mw0 && nw - mw0 <= 255;
+            const int32_t got = varint_take<MODE_WORDREV, VAL_VB>(
+                sm, c.sb, w, vpos, (int32_t)(4 * nw), c.n - L, true, c.err,
+                [&](const uint32_t (&lo)[1], const uint32_t (&hi)[1], int32_t vb, int32_t, int32_t count) {
+                    sink_values<OP, 1>(lo, (int64_t)base + vb, 0, count, c.nb, c.out, cr);
+                },
+                0, nullptr, 0, tail_in ? sm.u.f.cbuf : nullptr, (int32_t)mw0);
+            decoded = L + got;
+        }
+    }
+    // values the codec did not produce stay 0 in Java's decompressedValues[]: transform them too
+    if (!c.err) {
+        for (int32_t b = decoded; b < c.n; b += 64) {
+            uint32_t vv[1] = {0};
+            sink_values<OP, 1>(vv, b, 0, c.n - b < 64 ? c.n - b : 64, c.nb, c.out, cr);
+        }
+        if (OP == COVT_OP_FPF_ZZ_DELTA_XY && (c.n & 1)) c.err = COVT_ERR_COUNT_MISMATCH;
+    }
+    COVT_PHASE(c, 7);
+    c.consumed = c.byte_length;
+}
+
 // A FastPFOR chunk's values were stored with the running sums from 0 at its first value: add the sums of
 // the values before it (x / y alternate by value index for the coordinate op; v0 is a multiple of 256), in
 // place, 16 bytes per lane.  (Morton codes are not linear in the sum: that op decodes twice instead.)
@@ -2379,9 +2795,15 @@ __device__ __forceinline__ void decode_family_wave(uint8_t* smem, const uint8_t*
         }
     } else {
         switch (c.op) {
+#if COVT_FPF_STREAM
+        case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor_stream<COVT_OP_FPF_ZZ_DELTA_I32>(c); break;
+        case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor_stream<COVT_OP_FPF_ZZ_DELTA_XY>(c); break;
+        default: run_fastpfor_stream<COVT_OP_FPF_DELTA_MORTON>(c); break;
+#else
         case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_I32>(c); break;
         case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_XY>(c); break;
         default: run_fastpfor<COVT_OP_FPF_DELTA_MORTON>(c); break;
+#endif
         }
     }
     if (lane_id() == 0) {

@@ -182,6 +182,13 @@ for s in "$@"; do
     dplan_props) step dplan_props 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dplan_props -o run --output-format csv -- python tools/device_plan_prof.py 5 --props ;;
     launch_modes) step launch_modes 300 python tools/launch_mode_ab.py ;;
     dplan_prof) step dplan_prof 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d gpurun_out/dplan_prof -o run --output-format csv -- python tools/device_plan_prof.py 10 ;;
+    sqi_fpf_var) for v in ${AB_VARIANTS:-libcovt_base.so libcovt.so}; do
+            COVT_LIB_VARIANT=$v step sqi_fpf_$v 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/sqi_fpf_$v -o run --output-format csv -- python tools/family_run.py fastpfor 2 && \
+            COVT_LIB_VARIANT=$v step sqw_fpf_$v 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU -d gpurun_out/sqw_fpf_$v -o run --output-format csv -- python tools/family_run.py fastpfor 2 || exit $?
+        done ;;
+    fpf_probe) for v in ${AB_VARIANTS:-libcovt_base.so libcovt.so libcovt_base.so libcovt.so}; do
+            COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/fpf_probe.py 20 2>&1 | grep -v amdgpu.ids || fatal fpf_probe $?
+        done ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
 done
