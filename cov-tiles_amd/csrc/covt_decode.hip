@@ -1918,62 +1918,62 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
     WaveSmem& sm = *c.sm;
     const int l = lane_id();
     const Words W{c.sb, c.byte_length / 4};
-    const int64_t nw = W.nw;
-    const int32_t nw32 = (int32_t)nw;
+    const int32_t nw32 = W.nw;  // (32-bit word indices: a stream holds < 2^29 words)
     const uint32_t bsel = be_sel((uint32_t)((uintptr_t)c.sb & 3u));  // a stream word from the 4-byte grid
     Carry cr{0u, 0u};
     int32_t decoded = 0;
     int32_t L = 0;
-    int64_t p = 1;
+    int32_t p = 1;
     int xs_v = 0, xz_v = -1, xc_v = 0;  // lane k: dataTobePacked[k] start word, size, values consumed
-    int64_t mw0 = 0;                     // stream word of cbuf[0] (the meta window)
+    int32_t mw0 = 0;                     // stream word of cbuf[0] (the meta window)
     if (c.byte_length > c.avail) { c.err = COVT_ERR_TRUNCATED; }
-    if (!c.err && nw > 0) {
+    if (!c.err && nw32 > 0) {
         const uint32_t head0 = W.uniform(0), head1 = W.uniform(1);
         L = (int32_t)head0;
         if (L < 0) c.err = COVT_ERR_BAD_HEADER;
         L -= L % kFpfBlock;
         if (!c.err && L > c.n) c.err = COVT_ERR_COUNT_MISMATCH;
         int32_t done = 0;
-        const uintptr_t s_end = (uintptr_t)(c.sb + 4 * nw);
+        const uintptr_t s_end = (uintptr_t)c.sb + 4u * (uint32_t)nw32;
         struct WordsRaw {
             uint4 r;
-            int64_t base;
+            int32_t base;
             uint32_t sh;
         };
-        auto words_issue = [&](int64_t w) -> WordsRaw {
-            const uintptr_t addr = (uintptr_t)(c.sb + 4 * w);
+        auto words_issue = [&](int32_t w) -> WordsRaw {
+            const uintptr_t addr = (uintptr_t)c.sb + 4u * (uint32_t)w;
             const uintptr_t a16 = addr & ~(uintptr_t)15;
             const uint32_t o = (uint32_t)(addr & 15u);
             const uint32_t lmax = s_end > a16 ? (uint32_t)((s_end - 1 - a16) >> 4) : 0u;
             WordsRaw q;
             q.r = ld128_off((const g_u8*)a16, 16u * min((uint32_t)l, lmax));
-            q.base = uni64(w - (int64_t)(o >> 2));
+            q.base = uni(w - (int32_t)(o >> 2));
             q.sh = o & 3u;
             return q;
         };
-        auto words_store = [&](uint32_t* dst, const WordsRaw& q) -> int64_t {
+        auto words_store = [&](uint32_t* dst, const WordsRaw& q) -> int32_t {
             const uint32_t nx = lane_next(q.r.x);
             const uint32_t sel = be_sel(q.sh);
-            const int64_t wl = q.base + 4 * l;
+            const int32_t wl = q.base + 4 * l;
             uint4 wv;
-            wv.x = wl < nw ? be_word(q.r.y, q.r.x, sel) : 0u;
-            wv.y = wl + 1 < nw ? be_word(q.r.z, q.r.y, sel) : 0u;
-            wv.z = wl + 2 < nw ? be_word(q.r.w, q.r.z, sel) : 0u;
-            wv.w = wl + 3 < nw ? be_word(nx, q.r.w, sel) : 0u;
+            wv.x = wl < nw32 ? be_word(q.r.y, q.r.x, sel) : 0u;
+            wv.y = wl + 1 < nw32 ? be_word(q.r.z, q.r.y, sel) : 0u;
+            wv.z = wl + 2 < nw32 ? be_word(q.r.w, q.r.z, sel) : 0u;
+            wv.w = wl + 3 < nw32 ? be_word(nx, q.r.w, sel) : 0u;
             wave_sync();
             ((uint4*)dst)[l] = wv;
             wave_sync();
             return q.base;
         };
-        auto load_words = [&](uint32_t* dst, int64_t w) -> int64_t { return words_store(dst, words_issue(w)); };
+        auto load_words = [&](uint32_t* dst, int32_t w) -> int32_t { return words_store(dst, words_issue(w)); };
         while (!c.err && done < L) {
             done = uni(done);
             const int32_t thissize = uni((L - done) < kFpfPage ? (L - done) : kFpfPage);
-            const int64_t p0 = uni64(p);
-            if (p0 >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
-            int64_t ie = p0 + (int32_t)(p0 == 1 ? head1 : W.uniform(p0));  // the page's bytesize word
-            if (ie < 0 || ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+            const int32_t p0 = uni(p);
+            if (p0 >= nw32) { c.err = COVT_ERR_TRUNCATED; break; }
+            const int64_t ie0 = (int64_t)p0 + (int32_t)(p0 == 1 ? head1 : W.uniform(p0));  // the page's bytesize word
+            if (ie0 < 0 || ie0 >= nw32) { c.err = COVT_ERR_TRUNCATED; break; }
+            int32_t ie = (int32_t)ie0;
             // one round trip: the meta window (bytesize, byte container, small pages' directory and exception
             // arrays) and the first window of packed words, requested together (meta first: its wait does not
             // wait for the packed words)
@@ -1989,45 +1989,49 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
             int32_t vend = wbase;  // stream words below vend are staged
             uint32_t prev63 = 0u;  // lane 63's last raw dword of the last staged window
             mw0 = words_store(sm.u.f.cbuf, mq);
-            auto mword = [&](int64_t w) -> uint32_t { return uniu(sm.u.f.cbuf[w - mw0]); };
+            auto mword = [&](int32_t w) -> uint32_t { return uniu(sm.u.f.cbuf[w - mw0]); };
             const int32_t bytesize = (int32_t)mword(ie++);
             if (bytesize < 0 || bytesize > kFpfBcCap) { c.err = COVT_ERR_BAD_HEADER; break; }
             xc_v = 0;
-            const int64_t bcw = (bytesize + 3) / 4;
-            const int64_t bc = ie;
-            if (bc + bcw >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
+            const int32_t bcw = (bytesize + 3) / 4;
+            const int32_t bc = ie;
+            if (bc + bcw >= nw32) { c.err = COVT_ERR_TRUNCATED; break; }
             ie += bcw;
+            // the directory in 64-bit arithmetic (array sizes up to 2^31 - 1 move the cursor far past the
+            // stream: caught by the next read's bound, or by the next page's), its end clamped to nw after
+            int64_t ie64 = ie;
             {
-                int64_t dbase = INT64_MIN / 2;
-                auto dword = [&](int64_t w) -> uint32_t {
+                int32_t dbase = INT32_MIN / 2;
+                auto dword = [&](int32_t w) -> uint32_t {
                     if (w >= mw0 && w < mw0 + 255) return mword(w);
                     // (the ring is free until the first window is staged)
                     if (w < dbase || w >= dbase + 255) dbase = load_words(sm.u.f.ring, w);
                     return uniu(sm.u.f.ring[w - dbase]);
                 };
-                uint32_t bm = dword(ie++) & ~1u;
+                uint32_t bm = dword((int32_t)ie64++) & ~1u;
                 xs_v = 0;
                 xz_v = -1;
                 while (bm) {
                     const int32_t k = __builtin_ctz(bm) + 1;
                     bm &= bm - 1;
-                    if (ie >= nw) { c.err = COVT_ERR_TRUNCATED; break; }
-                    const int32_t size = (int32_t)dword(ie++);
+                    if (ie64 >= nw32) { c.err = COVT_ERR_TRUNCATED; break; }
+                    const int32_t size = (int32_t)dword((int32_t)ie64++);
                     if (size < 0) { c.err = COVT_ERR_BAD_HEADER; break; }
                     const int64_t groups = ((int64_t)size + 31) / 32;
-                    xs_v = l == k ? (int)(uint32_t)ie : xs_v;
+                    xs_v = l == k ? (int)(uint32_t)ie64 : xs_v;
                     xz_v = l == k ? size : xz_v;
-                    ie += groups * k;
-                    ie -= ((groups * 32 - size) * k) / 32;
+                    ie64 += groups * k;
+                    ie64 -= ((groups * 32 - size) * k) / 32;
                 }
                 if (c.err) break;
             }
-            const bool xin = ie - mw0 <= 255;  // the page's whole metadata sits in the meta window
+            const bool xin = ie64 - mw0 <= 255;  // the page's whole metadata sits in the meta window
+            ie = (int32_t)(ie64 < nw32 ? ie64 : (int64_t)nw32);  // (>= nw: the next page, or the tail, stops)
             COVT_PHASE(c, 0);
             const int32_t nblocks = uni(thissize / kFpfBlock);
             const int32_t bclen = uni((int32_t)(bcw * 4));
             const uint8_t* cb8 = (const uint8_t*)sm.u.f.cbuf;
-            const g_u8* cbyte = (const g_u8*)(c.sb + 4 * bc);  // container byte q: cbyte[q ^ 3]
+            const g_u8* cbyte = (const g_u8*)(c.sb + 4u * (uint32_t)bc);  // container byte q: cbyte[q ^ 3]
             int32_t cbase = (int32_t)(4 * (mw0 - bc));
             auto chunk_load = [&](int32_t at) {  // container bytes [cbase, cbase + 1020), cbase in (at - 16, at]
                 cbase = (int32_t)(4 * (load_words(sm.u.f.cbuf, bc + (at >> 2)) - bc));
@@ -2150,6 +2154,7 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                     if (!xin && h.ce > 0 && (uint32_t)(h.bcoff - cbase) > (uint32_t)(1020 - 64)) chunk_load(h.bcoff);
                 };
                 auto prefetch = [&](const Hdr& h, FpfPre& pr) {
+                    if (h.ce == 0) return;  // (uniform; the block reads neither)
                     const int32_t k = h.idx;
                     const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
                     uint32_t xb;
@@ -2282,14 +2287,14 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
         }
         decoded = L;
         // VariableByte tail over words [p, nw): from the last page's meta window when it holds them
-        if (!c.err && p < nw) {
+        if (!c.err && p < nw32) {
             int32_t vpos = (int32_t)(4 * p);
             const int32_t base = L;
             Win w;
             w.valid = false;
-            const bool tail_in = L > 0 && ((int64_t)(vpos & ~15) >> 2) >= mw0 && nw - mw0 <= 255;
+            const bool tail_in = L > 0 && ((vpos & ~15) >> 2) >= mw0 && nw32 - mw0 <= 255;
             const int32_t got = varint_take<MODE_WORDREV, VAL_VB>(
-                sm, c.sb, w, vpos, (int32_t)(4 * nw), c.n - L, true, c.err,
+                sm, c.sb, w, vpos, 4 * nw32, c.n - L, true, c.err,
                 [&](const uint32_t (&lo)[1], const uint32_t (&hi)[1], int32_t vb, int32_t, int32_t count) {
                     sink_values<OP, 1>(lo, (int64_t)base + vb, 0, count, c.nb, c.out, cr);
                 },
@@ -2822,7 +2827,7 @@ __device__ __forceinline__ void decode_family_wave(uint8_t* smem, const uint8_t*
 }
 
 #ifndef COVT_FPF_WAVES
-#define COVT_FPF_WAVES 7  // A/B: waves per SIMD the FastPFOR family kernel is register-budgeted for
+#define COVT_FPF_WAVES 8  // A/B: waves per SIMD the FastPFOR family kernel is register-budgeted for (7: round 5)
 #endif
 template <int FAM>
 __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(FAM == COVT_FAMILY_FASTPFOR ? COVT_FPF_WAVES : 7))) void decode_family_kernel(const uint8_t* __restrict__ in,

@@ -189,6 +189,8 @@ for s in "$@"; do
     fpf_probe) for v in ${AB_VARIANTS:-libcovt_base.so libcovt.so libcovt_base.so libcovt.so}; do
             COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/fpf_probe.py 20 2>&1 | grep -v amdgpu.ids || fatal fpf_probe $?
         done ;;
+    timeline_ab) step timeline_old 300 env TIMING_LIB=libcovt_timing_old.so python tools/stream_timeline.py && \
+        step timeline_new 300 python tools/stream_timeline.py ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
 done

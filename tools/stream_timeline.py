@@ -9,7 +9,7 @@ import ctypes
 import os
 import sys
 
-os.environ["COVT_LIB_VARIANT"] = "libcovt_timing.so"
+os.environ["COVT_LIB_VARIANT"] = os.environ.get("TIMING_LIB", "libcovt_timing.so")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 
