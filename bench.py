@@ -608,6 +608,49 @@ def config_legs(lib, args, torch, dev, covt, stream):
     return out
 
 
+def strong_shards_leg(allp, kern_ms_full, args, torch, dev, covt, stream, ns=(2, 4, 8)):
+    """BASELINE config 5 "sharded across 8xMI355X", re-measured on this one GPU at every N = 1 run: the same
+    10k-tile batch split over N ranks exactly as `bench.py --gpus N` splits it (LPT byte balance), every
+    shard planned with the default options and its decode launch timed alone (HIP events, mean of --steps
+    after --warmup).  An N-GPU strong-scaling step lasts as long as its slowest shard, so `projected_value`
+    = the batch's stream bytes / that shard's launch and `efficiency` = projected_value / (N x the full
+    batch's rate).  A projection (one GPU, no host effects), not the N-GPU run the driver measures."""
+    total_in = None
+    out = {"note": "per-shard decode launches timed alone on one GPU; an N-GPU step = its slowest shard",
+           "full_kernel_ms": round(kern_ms_full, 5)}
+    for n in ns:
+        shards = lpt_shards([len(t) for _, t in allp], n)
+        ms = []
+        ins = []
+        for sh in shards:
+            plan = covt.Plan.from_tiles([allp[i][1] for i in sh], covt.FORMAT_GENC, args.id_mode)
+            b = covt.DeviceBatch(plan, dev)
+            with torch.cuda.stream(stream):
+                for _ in range(max(args.warmup, 2)):
+                    b.decode(stream)
+                torch.cuda.synchronize(dev)
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                      for _ in range(max(args.steps // 2, 5))]
+                for a, e in ev:
+                    a.record(stream)
+                    b.decode(stream)
+                    e.record(stream)
+                torch.cuda.synchronize(dev)
+            _, res = b.results()
+            if (res[:, 0] != 0).any():
+                raise RuntimeError("strong shard decode reported errors")
+            ms.append(float(np.mean([a.elapsed_time(e) for a, e in ev])))
+            ins.append(int(plan.in_bytes))
+            del b, plan
+        total_in = sum(ins)
+        worst = max(ms)
+        proj = total_in / (worst * 1e-3) / 1e9
+        full = total_in / (kern_ms_full * 1e-3) / 1e9
+        out["n%d" % n] = {"shard_ms": [round(x, 4) for x in ms], "slowest_ms": round(worst, 4),
+                          "projected_value": round(proj, 2), "efficiency": round(proj / (n * full), 3)}
+    return out
+
+
 def free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -686,6 +729,8 @@ def main():
     ap.add_argument("--device-plan-reps", type=int, default=5, help="device-side plan creations timed; 0 skips")
     ap.add_argument("--abi-host-reps", type=int, default=2,
                     help="reps of the C-ABI host entry covt_plan_decode_host (pageable in/out); 0 skips")
+    ap.add_argument("--no-strong-shards", action="store_true",
+                    help="N = 1: skip the strong-scaling shard projection (per-shard launches for N = 2, 4, 8)")
     ap.add_argument("--share-device", action="store_true",
                     help="every rank on cuda:0 (runs the real N-rank path on a one-GPU box; not a scaling figure)")
     ap.add_argument("--dry-run", action="store_true",
@@ -794,6 +839,8 @@ def main():
             legs["properties"] = properties_leg(picks, args, dist, torch, dev, covt, stream)
         if not args.no_configs and rank == 0 and world == 1:
             legs["configs"] = config_legs(lib, args, torch, dev, covt, stream)
+        if not args.no_strong_shards and world == 1 and args.scaling == "strong":
+            legs["strong_shards"] = strong_shards_leg(allp, kern_ms, args, torch, dev, covt, stream)
 
     mine = {"rank": rank, "device": dev_name, "local_rank": local_rank, "seed": seed, "tiles": len(picks),
             "streams": int(plan.num_streams), "stream_bytes": int(plan.in_bytes), "output_bytes": int(plan.out_bytes),

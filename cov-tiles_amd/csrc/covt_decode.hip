@@ -2139,14 +2139,22 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                     int32_t b, ce, idx, pk, bcoff;
                     uint32_t xcur;
                 };
+                // block g's fields, packed lane-side (b | ce << 8 | idx << 16; the positions' container offset)
+                // so that a block reads four lanes and decodes three bit fields
+                const uint32_t f_v = (uint32_t)(b_v & 0xff) | ((uint32_t)ce_v << 8) | ((uint32_t)(idx_v & 0xff) << 16);
+                const int32_t bo_v = cur_v + (hasx ? 3 : 2);
                 auto rec = [&](int32_t g, Hdr& h) {
-                    const uint32_t hw = (uint32_t)__builtin_amdgcn_readlane((int32_t)hw_v, g);
-                    h.b = (int32_t)(int8_t)(hw & 0xffu);
-                    h.ce = (int32_t)((hw >> 8) & 0xffu);
-                    h.idx = h.ce > 0 ? (int32_t)(int8_t)((hw >> 16) & 0xffu) - h.b : 1;
-                    h.xcur = (uint32_t)__builtin_amdgcn_readlane(xcur_v, g);
-                    h.bcoff = __builtin_amdgcn_readlane(cur_v, g) + (h.ce > 0 ? 3 : 2);
-                    h.pk = __builtin_amdgcn_readlane(pk_v, g);
+                    const uint32_t f = uniu((uint32_t)__builtin_amdgcn_readlane((int32_t)f_v, g));
+                    h.b = (int32_t)(f & 0xffu);
+                    h.ce = (int32_t)((f >> 8) & 0xffu);
+                    h.idx = (int32_t)(int8_t)((f >> 16) & 0xffu);
+                    h.xcur = uniu((uint32_t)__builtin_amdgcn_readlane(xcur_v, g));
+                    h.bcoff = uni(__builtin_amdgcn_readlane(bo_v, g));
+                    h.pk = uni(__builtin_amdgcn_readlane(pk_v, g));
+                };
+                // (the next block's exception count alone: its other fields are read only if it has exceptions)
+                auto next_ce = [&](int32_t g) -> int32_t {
+                    return (int32_t)((uniu((uint32_t)__builtin_amdgcn_readlane((int32_t)f_v, g)) >> 8) & 0xffu);
                 };
                 // the container window holding block h's exception positions (the first 64 are read from it)
                 auto pos_window = [&](const Hdr& h) {
@@ -2170,13 +2178,15 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                     const int32_t pb = h.bcoff - cbase;
                     pr.pos = cb8[min(max(pb + l, 0), 4 * 260 - 1)];
                 };
-                Hdr h{0, 0, 1, pk, 0, 0u};  // (a batch failing at its first block: a harmless prefetch)
                 FpfPre pre, preB;
-                if (nok > 0) {
-                    rec(0, h);
-                    pos_window(h);
+                {
+                    Hdr h0{0, 0, 1, pk, 0, 0u};  // (a batch failing at its first block: a harmless prefetch)
+                    if (nok > 0) {
+                        rec(0, h0);
+                        pos_window(h0);
+                    }
+                    prefetch(h0, pre);
                 }
-                prefetch(h, pre);
                 // as many zero stores to the batch's first block as a block's sink issues (overwritten by its
                 // values): every path from a window request or this prefetch to its wait then passes a store
                 // -- also when the first block needs the next window at once -- so the compiler's vmcnt waits
@@ -2184,12 +2194,8 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                 fpf_prime_stores<OP>(c.out, (int64_t)done + (int64_t)jbat * kFpfBlock);
                 auto block = [&](int32_t g, const FpfPre& pc, FpfPre& pn) {
                     Hdr hc;
-                    hc.b = uni(h.b);
-                    hc.ce = uni(h.ce);
-                    hc.idx = uni(h.idx);
-                    hc.xcur = uniu(h.xcur);
-                    hc.bcoff = uni(h.bcoff);
-                    hc.pk = uni(h.pk);
+                    rec(g, hc);  // (read again here rather than carried from the previous block: no loop-carried
+                                 // copies of the fields)
                     const int32_t b = hc.b;
                     // this block's words staged.  One window is always enough (vend >= pk: the previous block
                     // needed up to pk; a block needs <= 256 words), and never two stages back to back: every
@@ -2199,13 +2205,13 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                     if (uni(vend) < hc.pk + 8 * b) stage();
                     if (hc.ce > 0) ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
                     COVT_PHASE(c, 3);
-                    // the next block's exception loads in flight (issued on every path; the batch's last
-                    // block re-reads its own)
-                    if (g + 1 < nok) {
-                        rec(g + 1, h);
-                        pos_window(h);
+                    // the next block's exception loads in flight (blocks with exceptions only)
+                    if (g + 1 < nok && next_ce(g + 1) > 0) {
+                        Hdr hn;
+                        rec(g + 1, hn);
+                        pos_window(hn);
+                        prefetch(hn, pn);
                     }
-                    prefetch(h, pn);
                     // unpack: lane l -> values 4l..4l+3 of miniblock l/8, words from the ring
                     uint32_t v[4];
                     {
