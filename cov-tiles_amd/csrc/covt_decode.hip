@@ -45,6 +45,9 @@ constexpr int kFpfBcCap = 3 * kFpfPage / kFpfBlock + kFpfPage;  // JavaFastPFOR 
 #ifndef COVT_FPF_STREAM  // 1: whole FastPFOR streams through run_fastpfor_stream (0: run_fastpfor, A/B)
 #define COVT_FPF_STREAM 1
 #endif
+#ifndef COVT_RLE_SHORT_SPAN  // int RLE windows with at most this many live bytes build next[] position-major
+#define COVT_RLE_SHORT_SPAN 448
+#endif
 #ifndef COVT_CHUNK_PRIO
 #define COVT_CHUNK_PRIO 2
 #endif
@@ -78,16 +81,20 @@ struct __attribute__((aligned(16))) WaveSmem {
             };
             uint32_t patch[256];  // exception patches of one block
             uint32_t cbuf[260];   // 1 KiB chunk of the page's byte container
-            uint8_t posx[2][192]; // positions of exceptions 64..255 of the next two blocks
+            union {
+                uint8_t posx[2][192];  // split chunks: positions of exceptions 64..255 of the next two blocks
+                uint32_t xw[224];      // whole streams: a block batch's exception words (kFpfXw)
+            };
         } f;
     } u;
 };
 constexpr int kSmemHdr = 272;  // offsetof(WaveSmem, u), checked below
 constexpr int kFamSmemRle = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2 + (kWin + 8) * 2 + 64 * 2;
 constexpr int kFamSmemVarint = kSmemHdr + (kWin / 4 + 4) * 4 + kWin * 2;
-constexpr int kFamSmemFpf = kSmemHdr + (512 + 256 + 260) * 4 + 384 > kFamSmemVarint
-                                ? kSmemHdr + (512 + 256 + 260) * 4 + 384
+constexpr int kFamSmemFpf = kSmemHdr + (512 + 256 + 260 + 224) * 4 > kFamSmemVarint
+                                ? kSmemHdr + (512 + 256 + 260 + 224) * 4
                                 : kFamSmemVarint;
+constexpr int kFpfXw = 224;  // LDS words of a FastPFOR block batch's gathered exception words
 static_assert(kFamSmemFpf >= kSmemHdr + (int)sizeof(((WaveSmem*)nullptr)->u.f), "FastPFOR scratch stride");
 static_assert(kFamSmemVarint >= kSmemHdr + (int)sizeof(((WaveSmem*)nullptr)->u.v.win) +
                                     (int)sizeof(((WaveSmem*)nullptr)->u.v.list), "varint scratch stride");
@@ -889,7 +896,34 @@ __device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
         // no arithmetic); "no group completes here" is the sentinel next[kWin], which points at itself.
         const uint32_t nb = (uint32_t)(uintptr_t)(lds_cu16*)&sm.u.v.next[0];
         const uint32_t sent = nb + 2u * (uint32_t)kWin;
-        {
+        // live positions: [jlo, vlen) (the walk starts at jlo; a group ends at most at vlen)
+        const int32_t vlen = min(kWin, c.avail - woff);
+        if (vlen - jlo <= COVT_RLE_SHORT_SPAN) {
+            // a short window (a stream's last, or a short stream): position-major, one position per lane and
+            // step -- ceil(live / 64) steps instead of every lane's 16 positions; each position's terminator
+            // rank from the window index (cpre / cmask).  Positions outside [jlo, vlen] are never visited.
+            if (l == 0) {
+                if (vlen < kWin) sm.u.v.next[vlen] = (uint16_t)sent;
+                sm.u.v.next[kWin] = (uint16_t)sent;
+            }
+            const int32_t its = uni((vlen - jlo + 63) >> 6);
+            for (int32_t i = 0; i < its; ++i) {
+                const int32_t j = jlo + 64 * i + l;
+                uint32_t nx = sent;
+                if (j < vlen) {
+                    const uint32_t cb = win_byte(sm, j);
+                    const int32_t x = j + (cb < 0x80u ? 2 : 1);  // run: rank of j + 2; literal: of j + 1
+                    uint32_t rk = (uint32_t)K;
+                    if (x < kWin) {
+                        const int32_t ch = x >> 4;
+                        rk = (uint32_t)sm.cpre[ch] + __popc((uint32_t)sm.cmask[ch] & ((1u << (x & 15)) - 1u));
+                    }
+                    const uint32_t ridx = cb < 0x80u ? rk : rk + (0xffu - cb);
+                    if (ridx < (uint32_t)K) nx = nb + 2u * ((uint32_t)sm.u.v.list[ridx] + 1u);
+                }
+                if (j < kWin) sm.u.v.next[j] = (uint16_t)nx;
+            }
+        } else {
             const uint32_t ncmsk = lane_next(w.cmsk);
             uint32_t R[18];
             R[0] = w.cpre;
@@ -1378,9 +1412,11 @@ struct FpfPre {
     uint32_t x0, x1, x2; // exception e = lane: 12 bytes (4-B aligned) covering its packed word(s)
 };
 
-// 12 bytes from a 4-byte aligned global address
+// 12 / 8 bytes from a 4-byte aligned global address
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 typedef __attribute__((address_space(1))) const u32x3 g_v3;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const u32x2 g_v2;
 
 // FastPFOR (256-value blocks, 65536-value pages) + VariableByte, JavaFastPFOR 0.1.12 as called by
 // DecodingUtils.java:316-444.  Per page the exception-array directory is read and the byte
@@ -2036,11 +2072,6 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
             auto chunk_load = [&](int32_t at) {  // container bytes [cbase, cbase + 1020), cbase in (at - 16, at]
                 cbase = (int32_t)(4 * (load_words(sm.u.f.cbuf, bc + (at >> 2)) - bc));
             };
-            auto xword = [&](int32_t k, uint32_t xs, uint32_t i, uint32_t& xbit) -> int32_t {
-                const uint32_t bit = __umul24(i & 31u, (uint32_t)k);
-                xbit = bit & 31u;
-                return (int32_t)(xs + __umul24(i >> 5, (uint32_t)k) + (bit >> 5));
-            };
             // the next window of packed words: staged into the ring, the one after it requested
             auto stage = [&]() {
                 const int32_t k = uni(kst);
@@ -2075,24 +2106,44 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
             // reach the first block's wait right after the page's request)
             stage();
             int32_t cur = 0, pk = (int32_t)p0 + 1;
-            for (int32_t jbat = 0; jbat < nblocks && !c.err; jbat += 64) {
+            for (int32_t jbat = 0, nbat = 0; jbat < nblocks && !c.err; jbat += nbat) {
                 jbat = uni(jbat);
-                const int32_t nbat = uni(min(64, nblocks - jbat));
-                // (1) the header chain: block jbat + g's header bytes and container offset to lane g
+                nbat = uni(min(64, nblocks - jbat));
+                // (1) the header chain: block jbat + g's header bytes and container offset to lane g.  A page
+                // whose container is past the meta window reads it through 1 KiB chunks; a batch then holds
+                // only blocks whose header and exception positions lie in the chunk loaded at its start, so the
+                // chunk moves forward once per KiB of container and a block's positions never reload it (a
+                // reload is a synchronous load: it waits for every request in flight)
                 uint32_t hw_v = 0u;
                 int32_t cur_v = bclen + 1;  // (past the container: no header)
+                cur = uni(cur);
+                cbase = uni(cbase);
+                if (!xin && cur <= bclen && (uint32_t)(cur - cbase) > (uint32_t)(1020 - 258)) chunk_load(cur);
                 for (int32_t g = 0; g < nbat; ++g) {
                     cur = uni(cur);
                     cbase = uni(cbase);
                     if (cur > bclen) break;  // the chain has left the container
-                    if ((uint32_t)(cur - cbase) > (uint32_t)(1020 - 8)) chunk_load(cur);
+                    if (!xin && cur - cbase > 1020 - 8) {  // the next header is past the chunk: a new batch
+                        nbat = g;
+                        break;
+                    }
                     const int32_t q = cur - cbase;
                     const uint32_t hw =
                         uniu(__builtin_amdgcn_alignbyte(sm.u.f.cbuf[(q >> 2) + 1], sm.u.f.cbuf[q >> 2], (uint32_t)q & 3u));
+                    const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
+                    const int32_t nx = cur + (ce > 0 ? 3 + ce : 2);
+                    if (!xin && g > 0 && nx - cbase > 1020) {  // its positions are past the chunk: a new batch
+                        nbat = g;
+                        break;
+                    }
                     hw_v = l == g ? hw : hw_v;
                     cur_v = l == g ? cur : cur_v;
-                    const int32_t ce = (int32_t)((hw >> 8) & 0xffu);
-                    cur += ce > 0 ? 3 + ce : 2;
+                    cur = nx;
+                }
+                nbat = uni(nbat);
+                if (nbat == 0) {  // (cannot happen: the chunk was loaded at the batch's first header)
+                    c.err = COVT_ERR_BAD_HEADER;
+                    break;
                 }
                 COVT_PHASE(c, 1);
                 // (2) lane-parallel: fields, exception cursors (a prefix sum per exception width present),
@@ -2134,84 +2185,87 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                     }
                 }
                 COVT_PHASE(c, 2);
-                // (3) the blocks, exception loads one block ahead (pages whose metadata is past the meta window)
+                // (3) the blocks.  Block g's fields, packed lane-side (b | ce << 8 | idx << 16 | xo << 24; the
+                // positions' container offset), so that a block reads four lanes: xo = where its exception words sit
+                // in xw (255: read from memory -- pages whose metadata the meta window holds read them from there)
                 struct Hdr {
-                    int32_t b, ce, idx, pk, bcoff;
+                    int32_t b, ce, idx, pk, bcoff, xo;
                     uint32_t xcur;
                 };
-                // block g's fields, packed lane-side (b | ce << 8 | idx << 16; the positions' container offset)
-                // so that a block reads four lanes and decodes three bit fields
-                const uint32_t f_v = (uint32_t)(b_v & 0xff) | ((uint32_t)ce_v << 8) | ((uint32_t)(idx_v & 0xff) << 16);
+                int32_t xo_v = 255;
+                if (!xin) {
+                    // The batch's exception words, gathered into xw by four requests at once: per block with an
+                    // exception array, the words holding its values (one more for the straddling read).  One wait
+                    // per batch instead of a dependent load per block: 97 % of the bench batch's blocks carry
+                    // exceptions, and 79 % sit on pages whose metadata is past the meta window.  (Words past xw:
+                    // those blocks read memory.)
+                    const bool ab = arr && l < nok;
+                    const int32_t k = ab ? idx_v : 2;
+                    const uint32_t xs = (uint32_t)lane_get(xs_v, k);
+                    const uint32_t b0 = __umul24((uint32_t)xcur_v, (uint32_t)k);
+                    const uint32_t b1 = __umul24((uint32_t)(xcur_v + ce_v), (uint32_t)k);
+                    const int32_t wlo = (int32_t)(xs + (b0 >> 5));
+                    const int32_t wn = ab ? (int32_t)((b1 + 31u) >> 5) - (int32_t)(b0 >> 5) + 1 : 0;
+                    const uint32_t winc = incl_scan((uint32_t)wn);
+                    const int32_t wo = (int32_t)(winc - (uint32_t)wn);
+                    const int32_t wend = (int32_t)winc;  // non-decreasing over the lanes
+                    xo_v = ab && wend <= kFpfXw ? wo : 255;
+                    const int32_t tot = uni(min((int32_t)lane_bcast(winc, 63), kFpfXw));
+                    const g_u8* sb4 = (const g_u8*)(((uintptr_t)c.sb) & ~(uintptr_t)3);
+                    u32x2 d[4];
+                    bool okw[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {  // word t of xw: block g = the first whose words end past t
+                        const int32_t t = 64 * r + l;
+                        int32_t lo = 0, hi = 64;  // (65 outcomes: 7 halvings)
+#pragma unroll
+                        for (int s2 = 0; s2 < 7; ++s2) {
+                            const int32_t mid = (lo + hi) >> 1;
+                            const bool le = lane_get(wend, mid & 63) <= t;
+                            const bool act = lo < hi;
+                            lo = act && le ? mid + 1 : lo;
+                            hi = act && !le ? mid : hi;
+                        }
+                        const int32_t g = min(lo, 63);
+                        const int32_t w = lane_get(wlo, g) + (t - lane_get(wo, g));
+                        okw[r] = t < tot && w < nw32;
+                        d[r] = *(const g_v2*)(sb4 + 4u * (okw[r] ? (uint32_t)w : 0u));  // (unmasked: no drain)
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (64 * r + l < kFpfXw) sm.u.f.xw[64 * r + l] = okw[r] ? be_word(d[r].y, d[r].x, bsel) : 0u;
+                    wave_sync();
+                }
+                const uint32_t f_v = (uint32_t)(b_v & 0xff) | ((uint32_t)ce_v << 8) | ((uint32_t)(idx_v & 0xff) << 16) |
+                                     ((uint32_t)xo_v << 24);
                 const int32_t bo_v = cur_v + (hasx ? 3 : 2);
                 auto rec = [&](int32_t g, Hdr& h) {
                     const uint32_t f = uniu((uint32_t)__builtin_amdgcn_readlane((int32_t)f_v, g));
                     h.b = (int32_t)(f & 0xffu);
                     h.ce = (int32_t)((f >> 8) & 0xffu);
                     h.idx = (int32_t)(int8_t)((f >> 16) & 0xffu);
+                    h.xo = (int32_t)(f >> 24);
                     h.xcur = uniu((uint32_t)__builtin_amdgcn_readlane(xcur_v, g));
                     h.bcoff = uni(__builtin_amdgcn_readlane(bo_v, g));
                     h.pk = uni(__builtin_amdgcn_readlane(pk_v, g));
                 };
-                // (the next block's exception count alone: its other fields are read only if it has exceptions)
-                auto next_ce = [&](int32_t g) -> int32_t {
-                    return (int32_t)((uniu((uint32_t)__builtin_amdgcn_readlane((int32_t)f_v, g)) >> 8) & 0xffu);
-                };
-                // the container window holding block h's exception positions (the first 64 are read from it)
-                auto pos_window = [&](const Hdr& h) {
-                    cbase = uni(cbase);
-                    if (!xin && h.ce > 0 && (uint32_t)(h.bcoff - cbase) > (uint32_t)(1020 - 64)) chunk_load(h.bcoff);
-                };
-                auto prefetch = [&](const Hdr& h, FpfPre& pr) {
-                    if (h.ce == 0) return;  // (uniform; the block reads neither)
-                    const int32_t k = h.idx;
-                    const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
-                    uint32_t xb;
-                    const int32_t wx = xword(k >= 2 ? k : 2, xs, h.xcur + (uint32_t)l, xb);
-                    const uint32_t xon = (uint32_t)(k >= 2) & (uint32_t)(l < h.ce) & (uint32_t)(wx < nw32);
-                    if (!xin) {  // (xin: the values are read from the meta window when the block is patched)
-                        const uint32_t wi = (uint32_t)wx & (0u - xon);
-                        const u32x3 xv = *(const g_v3*)((const g_u8*)(((uintptr_t)c.sb) & ~(uintptr_t)3) + 4u * wi);
-                        pr.x0 = xv.x;
-                        pr.x1 = xv.y;
-                        pr.x2 = xv.z;
-                    }
-                    const int32_t pb = h.bcoff - cbase;
-                    pr.pos = cb8[min(max(pb + l, 0), 4 * 260 - 1)];
-                };
-                FpfPre pre, preB;
-                {
-                    Hdr h0{0, 0, 1, pk, 0, 0u};  // (a batch failing at its first block: a harmless prefetch)
-                    if (nok > 0) {
-                        rec(0, h0);
-                        pos_window(h0);
-                    }
-                    prefetch(h0, pre);
-                }
                 // as many zero stores to the batch's first block as a block's sink issues (overwritten by its
-                // values): every path from a window request or this prefetch to its wait then passes a store
-                // -- also when the first block needs the next window at once -- so the compiler's vmcnt waits
-                // stay partial instead of vmcnt(0) (which would also wait for the stores just issued)
+                // values): every path from a window request to its wait then passes a store -- also when the
+                // first block needs the next window at once -- so the compiler's vmcnt waits stay partial instead
+                // of vmcnt(0) (which would also wait for the stores just issued)
                 fpf_prime_stores<OP>(c.out, (int64_t)done + (int64_t)jbat * kFpfBlock);
-                auto block = [&](int32_t g, const FpfPre& pc, FpfPre& pn) {
+                auto block = [&](int32_t g) {
                     Hdr hc;
-                    rec(g, hc);  // (read again here rather than carried from the previous block: no loop-carried
-                                 // copies of the fields)
+                    rec(g, hc);
                     const int32_t b = hc.b;
                     // this block's words staged.  One window is always enough (vend >= pk: the previous block
                     // needed up to pk; a block needs <= 256 words), and never two stages back to back: every
                     // path from a window's request to its wait then passes a block's output stores, so the
                     // compiler's vmcnt wait there stays partial (a loop here, or a second stage, made it
-                    // vmcnt(0) on every block: the stores and exception loads just issued waited for too)
+                    // vmcnt(0) on every block: the stores just issued waited for too)
                     if (uni(vend) < hc.pk + 8 * b) stage();
                     if (hc.ce > 0) ((uint4*)sm.u.f.patch)[l] = make_uint4(0, 0, 0, 0);
                     COVT_PHASE(c, 3);
-                    // the next block's exception loads in flight (blocks with exceptions only)
-                    if (g + 1 < nok && next_ce(g + 1) > 0) {
-                        Hdr hn;
-                        rec(g + 1, hn);
-                        pos_window(hn);
-                        prefetch(hn, pn);
-                    }
                     // unpack: lane l -> values 4l..4l+3 of miniblock l/8, words from the ring
                     uint32_t v[4];
                     {
@@ -2240,26 +2294,35 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                     COVT_PHASE(c, 4);
                     if (hc.ce > 0) {  // out[pos] |= (index == 1 ? 1 : exceptvalue) << b
                         const int32_t k = hc.idx;
-                        const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
                         const bool el = l < hc.ce;
+                        // exception e = lane: its position (container byte bcoff + e, inside the chunk: batch rule)
+                        const uint32_t pos = cb8[min(max(hc.bcoff - cbase + l, 0), 4 * 260 - 1)];
                         uint32_t ex = 1u;
-                        if (k != 1) {  // uniform
-                            uint32_t xbit;
-                            const int32_t wi = xword(k, xs, hc.xcur + (uint32_t)l, xbit);
+                        if (k != 1) {  // uniform; k in [2, 32] (checked)
+                            const uint32_t xs = (uint32_t)__builtin_amdgcn_readlane(xs_v, k);
+                            // value i = xcur + e of dataTobePacked[k]: bits [i k, i k + k) of its words
+                            const uint32_t bb = __umul24(hc.xcur + (uint32_t)l, (uint32_t)k);
+                            const uint32_t xbit = bb & 31u;
                             uint32_t lo, hi;
                             if (xin) {  // meta window: words already swapped, 0 past the stream
-                                const int32_t m = el ? wi - (int32_t)mw0 : 0;
+                                const int32_t m = el ? (int32_t)(xs + (bb >> 5)) - mw0 : 0;
                                 lo = sm.u.f.cbuf[m];
                                 hi = sm.u.f.cbuf[m + 1];
-                            } else {
-                                lo = wi < nw32 ? be_word(pc.x1, pc.x0, bsel) : 0u;
-                                hi = wi + 1 < nw32 ? be_word(pc.x2, pc.x1, bsel) : 0u;
+                            } else if (hc.xo != 255) {  // the batch's gathered words
+                                const int32_t m = el ? hc.xo + (int32_t)(bb >> 5) - (int32_t)(__umul24(hc.xcur, (uint32_t)k) >> 5) : 0;
+                                lo = sm.u.f.xw[m];
+                                hi = sm.u.f.xw[m + 1];
+                            } else {  // (past xw: from memory)
+                                const int32_t wi = (int32_t)(xs + (bb >> 5));
+                                lo = el && wi < nw32 ? W(wi) : 0u;
+                                hi = el && wi + 1 < nw32 ? W(wi + 1) : 0u;
                             }
                             const uint32_t m = k == 32 ? 0xffffffffu : ((1u << k) - 1u);
                             ex = __builtin_amdgcn_alignbit(hi, lo, xbit) & m;
                         }
-                        atomicOr(&sm.u.f.patch[el ? pc.pos : (uint32_t)(4 * l)], el ? ex << (b & 31) : 0u);
+                        atomicOr(&sm.u.f.patch[el ? pos : (uint32_t)(4 * l)], el ? ex << (b & 31) : 0u);
                         if (hc.ce > 64) {  // rare: more than 64 exceptions in the block (positions from memory)
+                            const uint32_t xs = k >= 2 ? (uint32_t)__builtin_amdgcn_readlane(xs_v, k) : 0u;
                             for (int q = 1; q < 4; ++q) {
                                 const int32_t e = l + 64 * q;
                                 if (e < hc.ce) {
@@ -2281,10 +2344,9 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                     wave_sync();
                     COVT_PHASE(c, 6);
                 };
-                for (int32_t g = 0; g < nok; g += 2) {
+                for (int32_t g = 0; g < nok; ++g) {
                     g = uni(g);
-                    block(g, pre, preB);
-                    if (g + 1 < nok) block(g + 1, preB, pre);
+                    block(g);
                 }
                 if (ferr) c.err = ferr;
             }

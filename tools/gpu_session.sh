@@ -191,6 +191,11 @@ for s in "$@"; do
         done ;;
     timeline_ab) step timeline_old 300 env TIMING_LIB=libcovt_timing_old.so python tools/stream_timeline.py && \
         step timeline_new 300 python tools/stream_timeline.py ;;
+    abprops) step ab_props 900 env AB_PROPS=1 python tools/ab.py ${AB_VARIANTS:-libcovt_base.so libcovt.so} ;;
+    tcc_families) for fam in fastpfor varint rle lane; do
+            step tcc_$fam$sfx 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE -d gpurun_out/tcc_$fam$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 && \
+            step fetch_$fam$sfx 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/fetch_$fam$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 || exit $?
+        done ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
 done
