@@ -60,8 +60,8 @@ for s in "$@"; do
     mvt_gpu) step mvt_gpu 300 python tools/mvt_vs_covt.py --gpu 9000 ;;
     fpfsize) step fpfsize 300 python -c "import sys; sys.path.insert(0, 'tools'); import op_breakdown; op_breakdown.fpf_scaling()" ;;
     prof) step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu ;;
-    pmc_fetch) step rocprof_pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --no-props --no-assemble ;;
-    pmc_write) step rocprof_pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --no-props --no-assemble ;;
+    pmc_fetch) step rocprof_pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --no-props --no-assemble --no-strong-shards ;;
+    pmc_write) step rocprof_pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --no-props --no-assemble --no-strong-shards ;;
     sq_fpf) step sq_fpf 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/sq_fpf -o run --output-format csv -- python tools/family_run.py fastpfor 2 ;;
     sq_fpf2) step sq_fpf2 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE -d gpurun_out/sq_fpf2 -o run --output-format csv -- python tools/family_run.py fastpfor 2 ;;
     util_rle_props) OPB_PROPS=1 step $s 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_VALU -d gpurun_out/$s -o run --output-format csv -- python tools/family_run.py rle 2 ;;
@@ -195,6 +195,10 @@ for s in "$@"; do
     tcc_families) for fam in fastpfor varint rle lane; do
             step tcc_$fam$sfx 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE -d gpurun_out/tcc_$fam$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 && \
             step fetch_$fam$sfx 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/fetch_$fam$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 || exit $?
+        done ;;
+    shards_ab) for v in ${AB_VARIANTS:-libcovt_r5.so libcovt.so libcovt_r5.so libcovt.so}; do
+            echo "== $v" >> gpurun_out/shards_ab.log
+            COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/shard_sizes.py 15 --ns=1,2,4,8 >> gpurun_out/shards_ab.log 2>&1 || fatal shards_ab $?
         done ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 R=${1:-r03}
 mkdir -p gpurun_out "gpurun_out/$R"
-LEAN="--no-cpu --no-props --no-assemble --no-configs --e2e-reps 0 --abi-host-reps 0 --device-plan-reps 0"
+LEAN="--no-cpu --no-props --no-assemble --no-configs --no-strong-shards --e2e-reps 0 --abi-host-reps 0 --device-plan-reps 0"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
     python bench.py --steps 20 --warmup 3 $LEAN > "gpurun_out/$R/prof_bench.json" 2> "gpurun_out/$R/prof_bench.err"
 python tools/launch_span.py gpurun_out/prof/run_kernel_trace.csv > "gpurun_out/$R/rocprof_launch_spans.txt"
