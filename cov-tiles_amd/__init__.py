@@ -43,6 +43,7 @@ DESC_SPLIT_RLE = 0x10
 SPLIT_SLOTS = 8
 ID_FORMAT, ID_JAVA = 0, 1
 LAUNCH_AUTO, LAUNCH_FUSED, LAUNCH_FORKED = 0, 1, 2
+LAUNCH_FPF_STREAM, LAUNCH_FPF_CLASSIC = 0x4, 0x8  # or-ed in: the FastPFOR family kernel variant (include/covt.h)
 
 (OP_NONE, OP_BYTE_RLE_U8, OP_RLE_U64, OP_RLE_I32, OP_RLE_S64, OP_VARINT_I32, OP_VARINT_ZZ_I32,
  OP_VARINT_ZZ_DELTA_I32, OP_VARINT_ZZ_DELTA_XY, OP_VARINT_DELTA_MORTON, OP_FPF_ZZ_DELTA_I32, OP_FPF_ZZ_DELTA_XY,
@@ -754,7 +755,8 @@ class DeviceBatch:
         g.replay()
 
     def decode(self, stream=None, launch: int = 0):
-        """launch: LAUNCH_AUTO (0), LAUNCH_FUSED or LAUNCH_FORKED (covt_decode_streams_device_grouped_mode)."""
+        """launch: LAUNCH_AUTO (0), LAUNCH_FUSED or LAUNCH_FORKED, optionally | LAUNCH_FPF_STREAM or LAUNCH_FPF_CLASSIC
+        (covt_decode_streams_device_grouped_mode)."""
         import torch
 
         s = stream if stream is not None else torch.cuda.current_stream(self.device)

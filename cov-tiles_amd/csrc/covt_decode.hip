@@ -42,9 +42,6 @@ constexpr int kFpfBcCap = 3 * kFpfPage / kFpfBlock + kFpfPage;  // JavaFastPFOR 
 #ifndef COVT_LONG_PRIO
 #define COVT_LONG_PRIO 2
 #endif
-#ifndef COVT_FPF_STREAM  // 1: whole FastPFOR streams through run_fastpfor_stream (0: run_fastpfor, A/B)
-#define COVT_FPF_STREAM 1
-#endif
 #ifndef COVT_RLE_SHORT_SPAN  // int RLE windows with at most this many live bytes build next[] position-major
 #define COVT_RLE_SHORT_SPAN 448
 #endif
@@ -2073,6 +2070,8 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                 cbase = (int32_t)(4 * (load_words(sm.u.f.cbuf, bc + (at >> 2)) - bc));
             };
             // the next window of packed words: staged into the ring, the one after it requested
+            bool fin = false;           // the current batch is the page's last (or fails)
+            int32_t bneed = INT32_MAX;  // ... and its blocks need the words below this
             auto stage = [&]() {
                 const int32_t k = uni(kst);
                 const uint32_t nx = lane_next(R.x, 0u);
@@ -2098,13 +2097,12 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                 wave_sync();
                 kst = k + 1;
                 vend = wbase + 256 * (k + 1) - 1;
-                R = ld128_off((const g_u8*)A0, min(1024u * (uint32_t)(k + 1) + 16u * (uint32_t)l, glast));
+                // the next window, unless the page's last batch is staged far enough (a window requested past
+                // a page's last needed word was up to 1 KiB of extra reads per page)
+                if (!fin || vend < bneed)
+                    R = ld128_off((const g_u8*)A0, min(1024u * (uint32_t)(k + 1) + 16u * (uint32_t)l, glast));
                 wave_sync();  // (the request stays ahead of the stores that follow: see the block's wait)
             };
-            // the page's first window (requested with the meta window): vend >= p0 + 1 from here on
-            // (unconditional: a page holds >= 1 block -- L is a multiple of 256 -- and a path around it would
-            // reach the first block's wait right after the page's request)
-            stage();
             int32_t cur = 0, pk = (int32_t)p0 + 1;
             for (int32_t jbat = 0, nbat = 0; jbat < nblocks && !c.err; jbat += nbat) {
                 jbat = uni(jbat);
@@ -2185,6 +2183,11 @@ __device__ __forceinline__ void run_fastpfor_stream(Ctx& c) {
                     }
                 }
                 COVT_PHASE(c, 2);
+                fin = jbat + nbat >= nblocks || ferr != 0;
+                bneed = nok > 0 ? uni(__builtin_amdgcn_readlane(pk_v + 8 * b_v, nok - 1)) : 0;
+                // the page's first window (requested with the meta window): vend >= p0 + 1 from here on.  (Before the
+                // batch's first block on every path: the prime stores below then separate it from every wait.)
+                if (jbat == 0) stage();
                 // (3) the blocks.  Block g's fields, packed lane-side (b | ce << 8 | idx << 16 | xo << 24; the
                 // positions' container offset), so that a block reads four lanes: xo = where its exception words sit
                 // in xw (255: read from memory -- pages whose metadata the meta window holds read them from there)
@@ -2813,7 +2816,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void decode_split_kernel(const
 }
 
 // One stream of family FAM on this wave (descriptor sid; `smem`: the wave's scratch).
-template <int FAM>
+// FS (FastPFOR only): whole streams through run_fastpfor_stream (the ring / batched-header path) instead of
+// run_fastpfor; the launch picks it for batches of many FastPFOR streams (covt_launch_family_split)
+template <int FAM, bool FS = false>
 __device__ __forceinline__ void decode_family_wave(uint8_t* smem, const uint8_t* __restrict__ in,
                                                    const covt_stream_desc* __restrict__ descs, int64_t sid,
                                                    uint8_t* __restrict__ out, covt_stream_result* __restrict__ res) {
@@ -2867,16 +2872,18 @@ __device__ __forceinline__ void decode_family_wave(uint8_t* smem, const uint8_t*
         default: run_varint_stream<COVT_OP_VARINT_ZZ_DELTA_I64>(c); break;
         }
     } else {
-        switch (c.op) {
-#if COVT_FPF_STREAM
-        case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor_stream<COVT_OP_FPF_ZZ_DELTA_I32>(c); break;
-        case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor_stream<COVT_OP_FPF_ZZ_DELTA_XY>(c); break;
-        default: run_fastpfor_stream<COVT_OP_FPF_DELTA_MORTON>(c); break;
-#else
-        case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_I32>(c); break;
-        case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_XY>(c); break;
-        default: run_fastpfor<COVT_OP_FPF_DELTA_MORTON>(c); break;
-#endif
+        if constexpr (FS) {
+            switch (c.op) {
+            case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor_stream<COVT_OP_FPF_ZZ_DELTA_I32>(c); break;
+            case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor_stream<COVT_OP_FPF_ZZ_DELTA_XY>(c); break;
+            default: run_fastpfor_stream<COVT_OP_FPF_DELTA_MORTON>(c); break;
+            }
+        } else {
+            switch (c.op) {
+            case COVT_OP_FPF_ZZ_DELTA_I32: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_I32>(c); break;
+            case COVT_OP_FPF_ZZ_DELTA_XY: run_fastpfor<COVT_OP_FPF_ZZ_DELTA_XY>(c); break;
+            default: run_fastpfor<COVT_OP_FPF_DELTA_MORTON>(c); break;
+            }
         }
     }
     if (lane_id() == 0) {
@@ -2895,10 +2902,13 @@ __device__ __forceinline__ void decode_family_wave(uint8_t* smem, const uint8_t*
 }
 
 #ifndef COVT_FPF_WAVES
-#define COVT_FPF_WAVES 8  // A/B: waves per SIMD the FastPFOR family kernel is register-budgeted for (7: round 5)
+#define COVT_FPF_WAVES 7  // A/B: waves per SIMD the FastPFOR family kernel (run_fastpfor) is register-budgeted for
 #endif
-template <int FAM>
-__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(FAM == COVT_FAMILY_FASTPFOR ? COVT_FPF_WAVES : 7))) void decode_family_kernel(const uint8_t* __restrict__ in,
+#ifndef COVT_FPF_STREAM_WAVES
+#define COVT_FPF_STREAM_WAVES 8  // ... and its run_fastpfor_stream variant (7 -> 8: launch 1.504 -> 1.495 ms)
+#endif
+template <int FAM, bool FS = false>
+__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(FAM == COVT_FAMILY_FASTPFOR ? (FS ? COVT_FPF_STREAM_WAVES : COVT_FPF_WAVES) : 7))) void decode_family_kernel(const uint8_t* __restrict__ in,
                                                             const covt_stream_desc* __restrict__ descs,
                                                             int64_t n_streams, uint8_t* __restrict__ out,
                                                             covt_stream_result* __restrict__ res) {
@@ -2908,7 +2918,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
     const int wv = uni((int)(threadIdx.x >> 6));
     const int64_t sid = (int64_t)blockIdx.x * kWavesPerBlock + wv;
     if (sid >= n_streams) return;
-    decode_family_wave<FAM>(smem + wv * kStride, in, descs, sid, out, res);
+    decode_family_wave<FAM, FS>(smem + wv * kStride, in, descs, sid, out, res);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -3318,10 +3328,12 @@ extern "C" int covt_launch_fused(const uint8_t* d_in, const covt_stream_desc* d_
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
 }
 
-extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc,
-                                        int64_t n_streams, uint8_t* d_out, covt_stream_result* d_res,
-                                        const covt_stream_desc* d_split, int64_t n_split, covt_stream_result* d_split_res,
-                                        hipStream_t stream) {
+extern "C" int covt_launch_family_split_mode(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc,
+                                             int64_t n_streams, uint8_t* d_out, covt_stream_result* d_res,
+                                             const covt_stream_desc* d_split, int64_t n_split,
+                                             covt_stream_result* d_split_res, hipStream_t stream, int fpf_mode) {
+    if (fpf_mode != 0 && fpf_mode != COVT_LAUNCH_FPF_STREAM && fpf_mode != COVT_LAUNCH_FPF_CLASSIC)
+        return COVT_ERR_INVALID_ARG;
     if (n_split < 0 || n_split % covt::kSplitSlots) return COVT_ERR_INVALID_ARG;
     if (n_split && fam != COVT_FAMILY_VARINT && fam != COVT_FAMILY_FASTPFOR && fam != COVT_FAMILY_RLE)
         return COVT_ERR_INVALID_ARG;
@@ -3364,12 +3376,27 @@ extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt
                            n_streams, d_out, d_res);
         break;
     case COVT_FAMILY_FASTPFOR:
-        hipLaunchKernelGGL(covt::decode_family_kernel<COVT_FAMILY_FASTPFOR>, grid, block, 0, stream, d_in, d_desc,
-                           n_streams, d_out, d_res);
+        // the ring / batched-header variant for batches of many FastPFOR streams: there it takes the launch 1.525 ->
+        // 1.474 ms, while in smaller batches -- a strong-scaling shard -- the per-block pipeline of run_fastpfor
+        // keeps the family shorter (N = 2 shard 0.962 -> 0.883 ms)
+        if (fpf_mode == COVT_LAUNCH_FPF_STREAM || (fpf_mode == 0 && n_streams >= kFpfStreamMinStreams))
+            hipLaunchKernelGGL((covt::decode_family_kernel<COVT_FAMILY_FASTPFOR, true>), grid, block, 0, stream, d_in,
+                               d_desc, n_streams, d_out, d_res);
+        else
+            hipLaunchKernelGGL((covt::decode_family_kernel<COVT_FAMILY_FASTPFOR, false>), grid, block, 0, stream, d_in,
+                               d_desc, n_streams, d_out, d_res);
         break;
     default: return COVT_ERR_INVALID_ARG;
     }
     return hipGetLastError() == hipSuccess ? COVT_OK : COVT_ERR_DEVICE;
+}
+
+extern "C" int covt_launch_family_split(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc,
+                                        int64_t n_streams, uint8_t* d_out, covt_stream_result* d_res,
+                                        const covt_stream_desc* d_split, int64_t n_split, covt_stream_result* d_split_res,
+                                        hipStream_t stream) {
+    return covt_launch_family_split_mode(fam, d_in, d_desc, n_streams, d_out, d_res, d_split, n_split, d_split_res,
+                                         stream, 0);
 }
 
 extern "C" int covt_launch_family(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,

@@ -556,6 +556,9 @@ void fork_release(ForkCtx* f) {
 
 int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const int64_t counts[COVT_NUM_FAMILIES],
                    uint8_t* d_out, covt_stream_result* d_res, hipStream_t s, int mode = COVT_LAUNCH_AUTO) {
+    const int fpf_mode = mode & (COVT_LAUNCH_FPF_STREAM | COVT_LAUNCH_FPF_CLASSIC);
+    mode &= ~(COVT_LAUNCH_FPF_STREAM | COVT_LAUNCH_FPF_CLASSIC);
+    if (fpf_mode == (COVT_LAUNCH_FPF_STREAM | COVT_LAUNCH_FPF_CLASSIC)) return COVT_ERR_INVALID_ARG;
     if (mode != COVT_LAUNCH_AUTO && mode != COVT_LAUNCH_FUSED && mode != COVT_LAUNCH_FORKED) return COVT_ERR_INVALID_ARG;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return COVT_ERR_DEVICE;
@@ -629,7 +632,8 @@ int launch_grouped(const uint8_t* d_in, const covt_stream_desc* d_desc, const in
             const int fam = qs[i].fam[k];
             if (fam < 0) continue;
             if (fam != kSplitV && fam != kSplitF && fam != kSplitR) {
-                st = covt_launch_family(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam], q);
+                st = covt_launch_family_split_mode(fam, d_in, d_desc + off[fam], counts[fam], d_out, d_res + off[fam],
+                                                   nullptr, 0, nullptr, q, fpf_mode);
                 continue;
             }
             const int kind = fam == kSplitV ? COVT_FAMILY_VARINT : fam == kSplitR ? COVT_FAMILY_RLE : COVT_FAMILY_FASTPFOR;

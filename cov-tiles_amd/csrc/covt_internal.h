@@ -18,12 +18,20 @@ int covt_launch_family(int fam, const uint8_t* d_in, const covt_stream_desc* d_d
 int covt_launch_family_split(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
                              uint8_t* d_out, covt_stream_result* d_res, const covt_stream_desc* d_split,
                              int64_t n_split, covt_stream_result* d_split_res, hipStream_t stream);
+// The same with the FastPFOR family's variant chosen by the caller: 0 auto (run_fastpfor_stream for at least
+// kFpfStreamMinStreams descriptors, run_fastpfor below), COVT_LAUNCH_FPF_STREAM or COVT_LAUNCH_FPF_CLASSIC.
+int covt_launch_family_split_mode(int fam, const uint8_t* d_in, const covt_stream_desc* d_desc, int64_t n_streams,
+                                  uint8_t* d_out, covt_stream_result* d_res, const covt_stream_desc* d_split,
+                                  int64_t n_split, covt_stream_result* d_split_res, hipStream_t stream, int fpf_mode);
 int covt_op_family_of(int op);
 // Every family of a grouped descriptor table (family f at offset sum(counts[0..f))) in ONE kernel launch
 // on `stream` (small batches; split regions' records zeroed beforehand).
 int covt_launch_fused(const uint8_t* d_in, const covt_stream_desc* d_desc, const int64_t counts[COVT_NUM_FAMILIES],
                       uint8_t* d_out, covt_stream_result* d_res, hipStream_t stream);
 }
+// A FastPFOR family launch of at least this many streams takes run_fastpfor_stream (8 times the chip's 8,192
+// wave slots: the bench batch's 77k; a strong-scaling shard of it, 9.7k-39k, keeps run_fastpfor)
+constexpr int64_t kFpfStreamMinStreams = 65536;
 // Batches of at most this many waves (split chunks + wave-per-stream descriptors + lane streams /
 // kFusedLaneStreams) decode in one fused launch instead of the forked per-family launches
 constexpr int64_t kFusedMaxWaves = 4096;

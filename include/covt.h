@@ -269,6 +269,12 @@ int covt_decode_streams_device_grouped(const uint8_t* d_in, const covt_stream_de
 #define COVT_LAUNCH_AUTO 0
 #define COVT_LAUNCH_FUSED 1
 #define COVT_LAUNCH_FORKED 2
+/* or-ed into launch_mode: the FastPFOR family's kernel variant in a forked launch.  By default (neither) a
+ * family of at least 65,536 streams takes the streamed variant (packed words through an LDS ring, block
+ * headers 64 at a time, a batch's exception words gathered at once: the shorter launch for large batches) and
+ * smaller ones the per-block pipeline (shorter for strong-scaling shards); both give identical results. */
+#define COVT_LAUNCH_FPF_STREAM 0x4
+#define COVT_LAUNCH_FPF_CLASSIC 0x8
 int covt_decode_streams_device_grouped_mode(const uint8_t* d_in, const covt_stream_desc* d_desc,
                                             const int64_t family_counts[COVT_NUM_FAMILIES], uint8_t* d_out,
                                             covt_stream_result* d_res, void* hip_stream, int32_t launch_mode);

@@ -198,7 +198,7 @@ for s in "$@"; do
         done ;;
     shards_ab) for v in ${AB_VARIANTS:-libcovt_r5.so libcovt.so libcovt_r5.so libcovt.so}; do
             echo "== $v" >> gpurun_out/shards_ab.log
-            COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/shard_sizes.py 15 --ns=1,2,4,8 >> gpurun_out/shards_ab.log 2>&1 || fatal shards_ab $?
+            COVT_LIB_VARIANT=$v timeout -k 10 300 python tools/shard_sizes.py 15 --ns=${SHARD_NS:-1,2,4,8} >> gpurun_out/shards_ab.log 2>&1 || fatal shards_ab $?
         done ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
