@@ -443,7 +443,7 @@ enum { VAL_J4 = 0, VAL_VB = 1, VAL_U64 = 2, VAL_U64_STRICT = 3, VAL_NONE = 4 }; 
 // WORDREV: window byte j = logical byte woff + j of the VariableByte sequence, i.e. the LE bytes of
 // the big-endian words W[i] (DecodingUtils.java:319-327); woff is a multiple of 16.
 __device__ __forceinline__ uint32_t win_byte(const WaveSmem& sm, int32_t j) {
-    return (sm.u.v.win[j >> 2] >> (8 * (j & 3))) & 0xffu;
+    return ((const uint8_t*)sm.u.v.win)[j];  // ds_read_u8 (a dword read needed a shift and a mask)
 }
 // bytes [j, j+12) of the window as three little-endian dwords
 __device__ __forceinline__ void win_bytes12(const WaveSmem& sm, int32_t j, uint32_t& x0, uint32_t& x1,
@@ -1120,12 +1120,12 @@ __device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
                         const int32_t gb = __popcll(__ballot(cust <= u0)) - 1;  // group holding value u0
                         // the groups starting inside the step mark their first value's lane (ds_permute: a lane
                         // no one writes to reads 0, the instruction's defined result; groups without a start
-                        // inside send 0 to lane 0, which no start inside the step reaches), then a running
-                        // max gives each value its group (was: a 64-bit OR reduction and two popcounts;
-                        // property decode 4.44 -> 4.35 ms)
+                        // inside send 0 to lane 0, which no start inside the step reaches); a value's group is
+                        // gb + the marks at or below its lane: one ballot and a v_mbcnt (was: a DPP running
+                        // max over the marking lanes, before that a 64-bit OR reduction)
                         const bool in = s > 0 && s < 64;
-                        const int32_t mk = __builtin_amdgcn_ds_permute(in ? s << 2 : 0, in ? l + 1 : 0);
-                        const int32_t gk = max(gb, (int32_t)incl_max_scan((uint32_t)mk) - 1);
+                        const int32_t mk = __builtin_amdgcn_ds_permute(in ? s << 2 : 0, in ? 1 : 0);
+                        const int32_t gk = gb + bits_below(__ballot(mk != 0)) + mk;
                         const uint32_t info = (uint32_t)lane_get((int32_t)cpk, gk);
                         const int32_t u = u0 + l;
                         if (u < U) {
@@ -1146,9 +1146,12 @@ __device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
                     const uint32_t cpk = (uint32_t)__builtin_amdgcn_ds_permute(dst << 2, (int32_t)pk);
                     for (int32_t u0 = 0; u0 < U; u0 += 64) {
                         const int32_t s = cust - u0;
-                        const uint64_t mask = wave_or64(s >= 0 && s < 64 ? 1ull << s : 0ull);
                         const int32_t gb = __popcll(__ballot(cust <= u0)) - 1;  // group holding value u0
-                        const int32_t gk = gb + __popcll(mask & ((2ull << l) - 1ull) & ~1ull);
+                        // marks and groups as in the one-byte path; a group starting at u0 itself is gb
+                        const bool in = s > 0 && s < 64;
+                        const int32_t mk = __builtin_amdgcn_ds_permute(in ? s << 2 : 0, in ? 1 : 0);
+                        const int32_t gk = gb + bits_below(__ballot(mk != 0)) + mk;
+                        const bool gfirst = mk != 0 || (l == 0 && __builtin_amdgcn_readlane(cust, gb) == u0);
                         const uint32_t info = (uint32_t)lane_get((int32_t)cpk, gk);
                         const int32_t u = u0 + l;
                         if (u < U) {
@@ -1158,7 +1161,7 @@ __device__ __forceinline__ void run_rle_int(Ctx& c, int32_t o0 = 0) {
                             const int32_t pv = rank > 0 ? (int32_t)sm.u.v.list[rank - 1] : -2;
                             // a group's first varint starts after its header (the byte after the previous
                             // group's last terminator; at the window's first group, after jlo)
-                            const int32_t sj = ((mask >> l) & 1ull) ? max(pv + 2, jlo + 1) : pv + 1;
+                            const int32_t sj = gfirst ? max(pv + 2, jlo + 1) : pv + 1;
                             if (to_i32) st_out((int32_t*)c.out + o, (int32_t)win_vulong_lo32(sm, sj, ej));
                             else store(o, win_vulong(sm, sj, ej));
                         }

@@ -120,6 +120,10 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
 __device__ __forceinline__ uint32_t lane_next(uint32_t x, uint32_t tail = 0) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)tail, (int)x, 0x130, 0xf, 0xf, false);
 }
+// set bits of the 64-bit lane mask m below this lane (v_mbcnt_lo / _hi: two VALU, no 64-bit shifts)
+__device__ __forceinline__ int32_t bits_below(uint64_t m) {
+    return (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 // value of lane `src` (any lane index 0..63 per lane): ds_bpermute, no LDS allocation
 __device__ __forceinline__ int32_t lane_get(int32_t x, int32_t src) {
     return __builtin_amdgcn_ds_bpermute(src << 2, x);
