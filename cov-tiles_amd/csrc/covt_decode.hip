@@ -2397,16 +2397,28 @@ __device__ __forceinline__ void fpf_add_carry(uint8_t* out, int32_t v0, int32_t 
     if ((cx | cy) == 0u) return;  // (uniform)
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's own stores of the range have completed
     int32_t* o = (int32_t*)out;
-    for (int32_t i = v0 + 4 * lane_id(); i < v1; i += 256) {
-        if (i + 4 <= v1) {
-            typedef __attribute__((address_space(1))) i32x4 g_i4;
-            const i32x4 v = *(const g_i4*)(o + i);
-            st_out16(o + i, make_int4((int32_t)((uint32_t)v.x + cx), (int32_t)((uint32_t)v.y + cy),
-                                      (int32_t)((uint32_t)v.z + cx), (int32_t)((uint32_t)v.w + cy)));
-        } else {
-            for (int32_t k = i; k < v1; ++k) o[k] = (int32_t)((uint32_t)o[k] + (((k - v0) & 1) ? cy : cx));
+    typedef __attribute__((address_space(1))) i32x4 g_i4;
+    // Eight 1 KiB loads in flight per round trip (a load -> add -> store loop waited out one HBM round trip
+    // per KiB: the values were just written past L2; an 8192-value chunk spent most of its time here).  The
+    // loads are unmasked (a lane past the range re-reads the range's last whole 16 bytes, not stored), the
+    // stores masked; the range's last 0-3 values (a stream's end) element by element.
+    const int32_t nq = (v1 - v0) >> 2;  // whole 16-byte quads
+    const int32_t last = v0 + 4 * (nq > 0 ? nq - 1 : 0);
+    constexpr int kDeep = 8;
+    for (int32_t q0 = 0; q0 < nq; q0 += 64 * kDeep) {
+        i32x4 v[kDeep];
+#pragma unroll
+        for (int k = 0; k < kDeep; ++k) v[k] = *(const g_i4*)(o + min(v0 + 4 * (q0 + 64 * k + lane_id()), last));
+#pragma unroll
+        for (int k = 0; k < kDeep; ++k) {
+            const int32_t q = q0 + 64 * k + lane_id();
+            if (q < nq)
+                st_out16(o + v0 + 4 * q, make_int4((int32_t)((uint32_t)v[k].x + cx), (int32_t)((uint32_t)v[k].y + cy),
+                                                   (int32_t)((uint32_t)v[k].z + cx), (int32_t)((uint32_t)v[k].w + cy)));
         }
     }
+    const int32_t i = v0 + 4 * nq + lane_id();  // (v0 even: value i is an x value when i - v0 is even)
+    if (i < v1) o[i] = (int32_t)((uint32_t)o[i] + (((i - v0) & 1) ? cy : cx));
 }
 
 // --------------------------------------------------------------------------------------------

@@ -192,6 +192,11 @@ for s in "$@"; do
     timeline_ab) step timeline_old 300 env TIMING_LIB=libcovt_timing_old.so python tools/stream_timeline.py && \
         step timeline_new 300 python tools/stream_timeline.py ;;
     abprops) step ab_props 900 env AB_PROPS=1 python tools/ab.py ${AB_VARIANTS:-libcovt_base.so libcovt.so} ;;
+    sq_families) for fam in fastpfor varint rle lane; do  # -> tools/pmc_families.py
+            step sqi_$fam$sfx 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/sqi_$fam$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 && \
+            step sqw_$fam$sfx 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE -d gpurun_out/sqw_$fam$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 || exit $?
+        done
+        python tools/pmc_families.py gpurun_out $sfx > gpurun_out/pmc_families$sfx.txt ;;
     tcc_families) for fam in fastpfor varint rle lane; do
             step tcc_$fam$sfx 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE -d gpurun_out/tcc_$fam$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 && \
             step fetch_$fam$sfx 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/fetch_$fam$sfx -o run --output-format csv -- python tools/family_run.py $fam 2 || exit $?
