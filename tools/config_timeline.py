@@ -74,6 +74,11 @@ def main():
                 k = np.nonzero(m)[0][np.argmax(cdur[m])]
                 row = sd[chunk_rows[k]]
                 op, nv, bl = int(row[24]), int(row[20:24].view(np.int32)[0]), int(row[28:32].view(np.int32)[0])
+                if not cst[m].any():  # the fused kernel (small launches) records no chunk (duration, start)
+                    print("   family %-9s chunks=%4d (in the fused kernel: chunk start / duration not recorded) of %s %d B "
+                          "%d vals, phase kclk %s" % (fname, int(m.sum()), NAMES.get(op, op), bl, nv,
+                                                      " ".join("%d" % (x // 1000) for x in allph[chunk_rows[k], 2:])))
+                    continue
                 print("   family %-9s chunks=%4d first start %6.1f last start %6.1f last end %6.1f us; longest chunk "
                       "%.1f us (start %.1f) of %s %d B %d vals, phase kclk %s" % (
                           fname, int(m.sum()), (cst[m].min() - t0) * TICK_US, (cst[m].max() - t0) * TICK_US,

@@ -12,7 +12,7 @@ import collections
 import csv
 import sys
 
-DECODE = ("decode_family_kernel<0>", "decode_family_kernel<1>", "decode_family_kernel<2>", "decode_lane_kernel")
+DECODE = ("decode_family_kernel<0", "decode_family_kernel<1", "decode_family_kernel<2", "decode_lane_kernel")  # (<FAM, FS>)
 
 
 def main():

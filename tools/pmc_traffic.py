@@ -18,7 +18,7 @@ def last_launch(path, counter):
     by = {}
     for r in rows:
         k = r["Kernel_Name"]
-        fam = k.split("<")[1].split(">")[0] if "decode_family" in k else "lane"
+        fam = k.split("<")[1].split(">")[0].split(",")[0] if "decode_family" in k else "lane"  # (<FAM, FS>: the family)
         by.setdefault(fam, []).append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     return {f: sorted(v)[-1][1] for f, v in by.items()}
 
