@@ -165,9 +165,15 @@ __device__ __forceinline__ uint32_t range16(int32_t s, int32_t e) {
     if (e <= s) return 0u;
     return ((1u << e) - 1u) & ~((1u << s) - 1u);
 }
-// 7-bit groups of up to four LEB128 bytes (little-endian in x)
+// 7-bit groups of up to four LEB128 bytes (little-endian in x): the byte pairs of each 16-bit half joined
+// by one packed 16-bit shift (no bits cross the halves), then the two 14-bit halves -- five VALU with the
+// caller's mask folded into the first (four shifts and masks took eight)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pext7(uint32_t x) {
-    return (x & 0x7fu) | ((x >> 1) & 0x3f80u) | ((x >> 2) & 0x1fc000u) | ((x >> 3) & 0xfe00000u);
+    x &= 0x7f7f7f7fu;
+    const uint32_t y = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, x) >> (u16x2){1, 1});  // v_pk_lshrrev_b16
+    const uint32_t t = (x & 0x007f007fu) | (y & ~0x007f007fu);  // b0 | b1 << 7 at bit 0, b2 | b3 << 7 at bit 16
+    return (t & 0x3fffu) | ((t >> 2) & ~0x3fffu);
 }
 __device__ __forceinline__ uint32_t bytemask(int n) {  // low n bytes, clamped to [0,4]
     return n >= 4 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << (8 * n)) - 1u));
