@@ -157,6 +157,28 @@ def main():
             continue
         print("%-12s total %7.3f G  " % (NAMES.get(op, op), tot.sum() / 1e9) +
               " ".join("%d:%4.1f%%" % (k, 100.0 * tot[k] / tot.sum()) for k in range(8) if tot[k]))
+    if heads.size:
+        # split chunks: phase clocks of run_fastpfor / the varint decode in slots 2..7 of each chunk's row (phases
+        # 0..5, s_memtime clocks), (duration, start) in slots 0, 1 (100 MHz ticks).  The clock rate is calibrated
+        # on the whole streams (their phases cover their whole decode); a chunk's time outside its phases is its
+        # setup, look-back and carry.
+        whole = np.ones(len(s), dtype=bool)
+        whole[np.unique(plan.desc_streams[heads])] = False
+        clk = ph[whole].sum(axis=1)
+        ok = (d_t[whole] > 0) & (clk > 0)
+        ghz = (clk[ok].sum() / (d_t[whole][ok].sum() * TICK_US * 1e3)) if ok.any() else 0.0
+        print("split chunks by phase (shader clock %.2f GHz from the whole streams; 'rest' = wall time outside the phases: "
+              "setup, look-back, carry)" % ghz)
+        hop = ops[heads]
+        for op in sorted(set(hop.tolist())):
+            m = hop == op
+            tot = ph_launch[heads][m, 2:8].sum(axis=0)
+            wall = ph_launch[heads][m, 0].sum() * TICK_US
+            inph = tot.sum() / (ghz * 1e3) if ghz else 0.0
+            print("  %-12s chunks %5d  wall %9.1f us  p50 %6.1f us  " % (
+                NAMES.get(int(op), op), int(m.sum()), wall, np.percentile(ph_launch[heads][m, 0], 50) * TICK_US) +
+                " ".join("%d:%4.1f%%" % (k, 100.0 * tot[k] * 1e-3 / ghz / wall) for k in range(6) if tot[k] and ghz) +
+                "  rest:%4.1f%%" % (100.0 * max(wall - inph, 0.0) / wall if wall else 0.0))
     # duration vs size buckets
     print("duration by stream size (all ops):")
     b = s["byte_length"]
