@@ -239,3 +239,16 @@ def test_device_batch_api_surface(covt):
         assert callable(getattr(covt.DeviceBatch, m, None)), m
     for m in ("decode", "results"):
         assert callable(getattr(covt.DeviceSubset, m, None)), m
+
+
+def test_python_constants_mirror_header(covt):
+    """Every #define of include/covt.h that the Python module mirrors (same name without COVT_) has the same
+    value: launch modes and FastPFOR kernel flags, families, descriptor flags, scratch release flags, ..."""
+    hdr = open(os.path.join(ROOT, "include", "covt.h")).read()
+    defs = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"#define COVT_([A-Z0-9_]+)\s+(0x[0-9a-fA-F]+|\d+)u?\b", hdr)}
+    checked = [k for k in defs if isinstance(getattr(covt, k, None), int)]
+    for k in checked:
+        assert getattr(covt, k) == defs[k], k
+    for k in ("LAUNCH_AUTO", "LAUNCH_FUSED", "LAUNCH_FORKED", "LAUNCH_FPF_STREAM", "LAUNCH_FPF_CLASSIC",
+              "FAMILY_FASTPFOR", "FAMILY_SPLIT_FPF", "DESC_SPLIT", "RELEASE_PINNED", "INPUT_PADDING"):
+        assert k in checked, k
