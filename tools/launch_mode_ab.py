@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The config-5 decode launch in its three shapes (covt_decode_streams_device_grouped_mode): auto (the four
 family kernels on forked queues for this batch), fused (every family in one kernel) and forked; paired rounds
-in one process.  usage: python tools/launch_mode_ab.py [rounds] [launches]"""
+in one process.  --shard=N/k: shard k of the N-way LPT split of the batch (bench.py's strong scaling) instead.
+usage: python tools/launch_mode_ab.py [rounds] [launches] [--shard=N/k]"""
 import os
 import sys
 
@@ -14,10 +15,16 @@ import bench  # noqa: E402
 def main():
     import torch
 
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    per = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    rounds = int(args[0]) if len(args) > 0 else 5
+    per = int(args[1]) if len(args) > 1 else 10
     covt = bench.load_covt()
     picks = bench.sample_batch(bench.tile_library(), 10000, bench.SEED)
+    for a in sys.argv[1:]:
+        if a.startswith("--shard="):
+            n, k = (int(x) for x in a[8:].split("/"))
+            picks = [picks[i] for i in bench.lpt_shards([len(t) for _, t in picks], n)[k]]
+            print("shard %d/%d: %d tiles" % (k, n, len(picks)))
     plan = covt.Plan.from_tiles([t for _, t in picks])
     batch = covt.DeviceBatch(plan, "cuda")
 
